@@ -1,0 +1,301 @@
+#!/usr/bin/env python3
+"""bench.py -- rows/s + achieved HBM GB/s on the numbers_mt aggregation hot path
+(BASELINE.json metric), 1..8 GPUs of one node.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--query c3]
+  torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL)
+
+Workload (BASELINE.json configs[2], the north_star query):
+  SELECT sum(number)/count(number), max(number), min(number)
+  FROM system.numbers_mt(1e10 x N_gpus)
+Weak scaling: every GPU owns 1e10 rows = its share [8r/G, 8(r+1)/G) of the
+8 numbers_mt partitions, materialised in HBM before timing (the 8-GPU run is
+configs[4], numbers_mt(8e10)).  One step = the hot path over the resident
+column: per partition one fused scan kernel (sum/count/max/min in one read)
+-> partial states -> AggregateFinal merge, across GPUs one RCCL all-reduce of
+the 48-byte states over xGMI.  Rank 0 prints ONE JSON line.
+"""
+import argparse
+import ctypes as C
+import glob
+import json
+import os
+import platform
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (os.path.join(ROOT, "fuse-query_amd"), os.path.join(ROOT, "oracle")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from fq_amd import abi, ops  # noqa: E402
+from fq_amd.expr import chain, predicate  # noqa: E402
+from fq_amd.numbers import BLOCK_SIZE, generate_parts, shard, stream_rows  # noqa: E402
+
+METRIC = "rows/s + achieved HBM GB/s on 10B-row numbers_mt agg, 1/2/4/8 GPUs"
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+README_C3_ROWS_PER_S = 1e10 / 6.40  # reference README.md:62 (8 vCPU KVM), BASELINE.md section 1
+U64 = 2**64
+
+QUERIES = {
+    "c2": ("SELECT sum(number) FROM system.numbers_mt({N})", abi.AGG_SUM),
+    "c3": ("SELECT sum(number)/count(number), max(number), min(number) FROM system.numbers_mt({N})",
+           abi.AGG_SUM | abi.AGG_COUNT | abi.AGG_MAX | abi.AGG_MIN),
+    "c4": ("SELECT max(number+1) FROM system.numbers_mt({N}) WHERE (number%8)<3", abi.AGG_MAX | abi.AGG_COUNT),
+}
+
+
+def closed_form(query, n):
+    """Expected results for numbers 0..n-1 (n a multiple of 80,000: no dropped rows)."""
+    s = (n * (n - 1) // 2) % U64
+    if query == "c2":
+        return [s]
+    if query == "c3":
+        return [s // n, n - 1, 0]
+    top = n - 1
+    while top % 8 >= 3:
+        top -= 1
+    return [top + 1]
+
+
+def log(rank, *a):
+    if rank == 0:
+        print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def latest_pmc_traffic(kernel_substr):
+    """HBM bytes per launch from the newest committed rocprofv3 --pmc summary
+    (profiles/*pmc*.json, written by tools/pmc_summary.py with the gfx950
+    FETCH_SIZE x2 correction already applied); None when absent."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")))
+    for f in reversed(files):
+        try:
+            d = json.load(open(f))
+        except Exception:
+            continue
+        for k in d.get("kernels", []):
+            if kernel_substr in k.get("name", "") and k.get("hbm_bytes_per_launch"):
+                return k["hbm_bytes_per_launch"], k.get("rows_per_launch"), os.path.basename(f)
+    return None
+
+
+def cpu_baseline(sample_rows, threads):
+    """Restated reference CPU path (oracle/fq_oracle.c) on the host cores."""
+    import oracle_c
+    native = True
+    try:
+        oracle_c.build(native=True)
+    except Exception:
+        native = False
+    aggs = [(abi.AGG_SUM, None), (abi.AGG_COUNT, None), (abi.AGG_MAX, None), (abi.AGG_MIN, None)]
+    L = oracle_c.lib(native)
+    n = sample_rows
+    # warmup on a small sample, then one timed run
+    oracle_c.numbers_partial(80_000_000, aggs, threads=threads, native=native)
+    t0 = time.perf_counter()
+    rows, st, err = oracle_c.numbers_partial(n, aggs, threads=threads, native=native)
+    dt = time.perf_counter() - t0
+    assert not any(st), err
+    res = [oracle_c.merge_states(op, [r[a] for r in rows]) for a, (op, _) in enumerate(aggs)]
+    s, c, mx, mn = (r[2] for r in res)
+    assert [s // c, mx, mn] == closed_form("c3", n), "cpu baseline parity"
+    cpu = platform.processor() or platform.machine()
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    del L
+    return {
+        "value": n / dt, "unit": "rows/s", "cores": threads, "kind": "port",
+        "sample": "C3 query over numbers_mt(%d): 8 partitions, one thread per partition, "
+                  "10,000-row blocks regenerated per block, one pass per aggregator "
+                  "(oracle/fq_oracle.c, %s); %.2f s wall on %s (nproc=%d)"
+                  % (n, "-O3 -march=native" if native else "-O3 -march=x86-64-v2", dt, cpu,
+                     os.cpu_count() or 0),
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--query", default="c3", choices=sorted(QUERIES))
+    ap.add_argument("--rows-per-gpu", type=float, default=1e10)
+    ap.add_argument("--cpu-sample-rows", type=float, default=4e9)
+    ap.add_argument("--cpu-threads", type=int, default=8)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    ops.require_gpu()
+    torch.cuda.set_device(local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    rows_per_gpu = int(args.rows_per_gpu)
+    n_total = rows_per_gpu * world
+    sql, mask = QUERIES[args.query]
+    sql = sql.format(N=n_total)
+    parts = generate_parts(n_total)
+    mine = shard(parts, rank, world)
+
+    # ---- materialise my partitions in HBM (SourceTransform, untimed) ----
+    rows = [stream_rows(b, e) for _, b, e in mine]
+    total_rows = sum(rows)
+    # each partition 256-byte aligned inside one allocation
+    offs, o = [], 0
+    for r in rows:
+        offs.append(o)
+        o += ((r * 8 + 255) // 256) * 256
+    buf = torch.empty(max(o, 256), dtype=torch.uint8, device="cuda")
+    cols = []
+    for (_, b, _e), r, off in zip(mine, rows, offs):
+        col = ops.DeviceColumn(buf, r, abi.DT_UINT64, offset=off)
+        from fq_amd._lib import check, lib
+        check(lib.fq_fill_numbers_u64(C.c_void_p(col.ptr), b, r, ops._stream()))
+        cols.append(col)
+    torch.cuda.synchronize()
+    log(rank, "materialised %d partitions, %d rows (%.1f GB) on rank %d" % (len(cols), total_rows,
+                                                                            total_rows * 8 / 1e9, rank))
+
+    if args.query == "c4":
+        value, _ = chain(abi.DT_UINT64, [("+", 1)])
+        pred = predicate(abi.DT_UINT64, [("%", 8)], "<", 3)
+    else:
+        value, pred = None, None
+
+    ws = [ops.Workspace(ops.lib.fq_aggregate_workspace_bytes(c.len)) for c in cols]
+    slots = torch.empty((max(len(cols), 1), 48), dtype=torch.uint8, device="cuda")
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in cols]
+    xbuf = torch.zeros((world, 6), dtype=torch.int64, device="cuda")
+    kern_ms = [0.0]
+    kern_launches = [0]
+
+    def step(timed):
+        for i, c in enumerate(cols):
+            ev[i][0].record()
+            ops.aggregate_async(c, BLOCK_SIZE, pred, value, mask, ws[i], out=slots[i])
+            ev[i][1].record()
+        host = slots.cpu().numpy().tobytes()  # D2H + sync
+        if timed:
+            for s, e in ev:
+                kern_ms[0] += s.elapsed_time(e)
+            kern_launches[0] += len(cols)
+        states = [abi.fq_agg_state.from_buffer_copy(host[48 * i:48 * (i + 1)]) for i in range(len(cols))]
+        merged = ops.state_merge(states) if states else abi.fq_agg_state(0, 0, U64 - 1, 0, 0, 0, abi.DT_UINT64)
+        if world > 1:
+            # AggregateFinal across GPUs: one RCCL all-reduce (sum) of a
+            # [world, 6] int64 buffer in which every rank fills only its own
+            # row == an all-gather of the 48-byte states, exact for any bits.
+            xbuf.zero_()
+            raw = bytes(merged)
+            xbuf[rank] = torch.frombuffer(bytearray(raw), dtype=torch.int64).to("cuda")
+            dist.all_reduce(xbuf)
+            allb = xbuf.cpu().numpy().tobytes()
+            merged = ops.state_merge([abi.fq_agg_state.from_buffer_copy(allb[48 * r:48 * (r + 1)])
+                                      for r in range(world)])
+        if args.query == "c2":
+            return [merged.sum]
+        if args.query == "c3":
+            return [merged.sum // merged.count, merged.max, merged.min]
+        return [merged.max]
+
+    for _ in range(args.warmup):
+        res = step(False)
+    if args.warmup == 0:
+        res = step(False)
+    expect = closed_form(args.query, n_total)
+    if res != expect:
+        raise SystemExit("PARITY FAILURE: got %r expected %r" % (res, expect))
+    log(rank, "result", res, "== closed form")
+
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = step(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    assert res == expect
+
+    avg_launch_ms = kern_ms[0] / max(kern_launches[0], 1)
+    rows_per_launch = total_rows / max(len(cols), 1)
+    achieved = rows_per_launch * 8 / (avg_launch_ms * 1e-3) / 1e9  # algorithmic GB/s
+    value = n_total * args.steps / dt
+    out = None
+    if rank == 0:
+        traffic = None
+        pmc = latest_pmc_traffic("agg_flat_kernel")
+        if pmc and pmc[1]:
+            traffic = pmc[0] * rows_per_launch / pmc[1]  # scale to this launch size
+        out = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "rows/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": dt / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": value / README_C3_ROWS_PER_S if args.query == "c3" else None,
+            "vs_baseline_ref": "reference README.md:62 (6.40 s for 1e10 rows, 8 vCPU KVM)",
+            "dtype": "u64",
+            "data": "synthetic: system.numbers_mt iota column (u64), resident in HBM before timing",
+            "config": {
+                "workload": sql,
+                "query": args.query,
+                "rows_per_gpu": rows_per_gpu,
+                "rows_total": n_total,
+                "partitions_per_gpu": len(cols),
+                "block_rows": BLOCK_SIZE,
+                "parallelism": "dp%d (numbers_mt partitions sharded, RCCL all-reduce of states)" % world,
+            },
+            "achieved_hbm_gbps": achieved,
+            "kernel_ms_per_launch": avg_launch_ms,
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBPS,
+                "traffic": traffic,
+                "kernel": "agg_flat_kernel (fq_aggregate scan) + finalize, per partition launch",
+                "bytes_per_launch": rows_per_launch * 8,
+            },
+            "result": res,
+        }
+    if world > 1:
+        dist.barrier()
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            out["cpu_baseline"] = cpu_baseline(int(args.cpu_sample_rows), args.cpu_threads)
+        except Exception as e:  # report, never hide
+            out["cpu_baseline"] = {"error": repr(e)}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

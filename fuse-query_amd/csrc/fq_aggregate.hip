@@ -1,0 +1,593 @@
+// Fused AggregatePartial scan for gfx950.
+//
+// Replaces, per device block (one numbers_mt partition or one DataBlock):
+//   FilterTransform::expression_executor  (transform_filter.rs:38-55)   -> predicate
+//   AggregatorFunction::accumulate        (function_aggregator.rs:57-100)
+//     arg.eval  -> ArithmeticFunction chain (function_arithmetic.rs:64-72)
+//     data_array_aggregate_op sum/min/max (data_array_aggregate.rs:14-163)
+// with ONE read of the column from HBM: coalesced 16-byte loads (4 in flight
+// per lane), per-lane accumulators in registers, a wave64 butterfly reduce,
+// an LDS combine across the 4 waves of a workgroup, one Partial per
+// workgroup, and a single-workgroup finalize in a fixed order (so float sums
+// are reproducible run to run).  No MFMA: nothing here is a contraction.
+//
+// Block mode: when a predicate is fused with sum(), the reference's per-block
+// state machine errors if ANY 10,000-row block is empty after filtering
+// (arrow sum -> None, data_value_arithmetic.rs:10-27).  Block mode assigns
+// whole reference blocks to waves and reduces "any row passed" with one
+// ballot per block, so that flag is exact.
+#include <hip/hip_runtime.h>
+
+#include <string>
+
+#include "fq_common.h"
+#include "fq_device.h"
+
+namespace fqk {
+
+constexpr int kThreads = 256;       // 4 waves per workgroup
+constexpr int kMaxPartials = 4096;  // workgroups per launch upper bound
+
+template <typename V>
+struct Acc {
+    V sum, mx, mn;
+    uint64_t cnt;
+    uint32_t flags;
+    __device__ void init() {
+        sum = V(0);
+        mx = Lim<V>::lo();
+        mn = Lim<V>::hi();
+        cnt = 0;
+        flags = 0;
+    }
+};
+
+// Evaluate predicate and value expression for M elements, accumulate.
+// Returns the pass mask (bit j = element j passed and is live).
+template <typename TIn, typename V, int PRED, bool CHAIN, int M>
+__device__ __forceinline__ uint32_t process(const TIn (&x)[M], const int64_t (&idx)[M],
+                                            uint32_t live, const KPred &pred, const KProg &val,
+                                            uint32_t mask, Acc<V> &acc) {
+    uint32_t pass = live;
+    if constexpr (PRED == FQ_PRED_EXPR) {
+        uint64_t l[M], r[M];
+#pragma unroll
+        for (int j = 0; j < M; ++j) l[j] = to_bits<TIn>(x[j]);
+        run_prog<M, TIn>(pred.lhs, x, l, live, acc.flags);
+        if (pred.rhs_operand == FQ_OPERAND_COLUMN) {
+#pragma unroll
+            for (int j = 0; j < M; ++j)
+                r[j] = col_as<TIn>(pred.cmp_dtype, x[j], (live >> j) & 1u, acc.flags);
+        } else {
+#pragma unroll
+            for (int j = 0; j < M; ++j) r[j] = pred.rhs;
+        }
+        pass &= cmp_mask<M>(pred.cmp, pred.cmp_dtype, l, r);
+    } else if constexpr (PRED == FQ_PRED_BITMAP) {
+#pragma unroll
+        for (int j = 0; j < M; ++j) {
+            if ((live >> j) & 1u) {
+                const uint64_t w = pred.bitmap[idx[j] >> 6];
+                if (!((w >> (idx[j] & 63)) & 1ull)) pass &= ~(1u << j);
+            }
+        }
+    }
+    V v[M];
+    if constexpr (CHAIN) {
+        uint64_t a[M];
+#pragma unroll
+        for (int j = 0; j < M; ++j) a[j] = to_bits<TIn>(x[j]);
+        run_prog<M, TIn>(val, x, a, pass, acc.flags);
+#pragma unroll
+        for (int j = 0; j < M; ++j) v[j] = from_bits<V>(a[j]);
+    } else {
+#pragma unroll
+        for (int j = 0; j < M; ++j) v[j] = (V)x[j];
+    }
+    if (mask & FQ_AGG_SUM) {
+#pragma unroll
+        for (int j = 0; j < M; ++j) acc.sum = acc.sum + (((pass >> j) & 1u) ? v[j] : V(0));
+    }
+    if (mask & FQ_AGG_MAX) {
+#pragma unroll
+        for (int j = 0; j < M; ++j) acc.mx = ((pass >> j) & 1u) ? vmax(acc.mx, v[j]) : acc.mx;
+    }
+    if (mask & FQ_AGG_MIN) {
+#pragma unroll
+        for (int j = 0; j < M; ++j) acc.mn = ((pass >> j) & 1u) ? vmin(acc.mn, v[j]) : acc.mn;
+    }
+    acc.cnt += __builtin_popcount(pass);
+    return pass;
+}
+
+// wave butterfly + LDS combine; thread 0 of the workgroup returns the result
+template <typename V>
+__device__ __forceinline__ void reduce_and_store(Acc<V> &acc, Partial *out, int32_t dtype) {
+#pragma unroll
+    for (int off = kWave / 2; off > 0; off >>= 1) {
+        acc.sum = acc.sum + shfl_xor64(acc.sum, off);
+        acc.mx = vmax(acc.mx, shfl_xor64(acc.mx, off));
+        acc.mn = vmin(acc.mn, shfl_xor64(acc.mn, off));
+        acc.cnt += shfl_xor64(acc.cnt, off);
+        acc.flags |= (uint32_t)__shfl_xor((int)acc.flags, off, kWave);
+    }
+    __shared__ V s_sum[kThreads / kWave], s_mx[kThreads / kWave], s_mn[kThreads / kWave];
+    __shared__ uint64_t s_cnt[kThreads / kWave];
+    __shared__ uint32_t s_flags[kThreads / kWave];
+    const int wave = threadIdx.x / kWave;
+    if ((threadIdx.x & (kWave - 1)) == 0) {
+        s_sum[wave] = acc.sum;
+        s_mx[wave] = acc.mx;
+        s_mn[wave] = acc.mn;
+        s_cnt[wave] = acc.cnt;
+        s_flags[wave] = acc.flags;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        V sum = s_sum[0], mx = s_mx[0], mn = s_mn[0];
+        uint64_t cnt = s_cnt[0];
+        uint32_t flags = s_flags[0];
+#pragma unroll
+        for (int w = 1; w < kThreads / kWave; ++w) {
+            sum = sum + s_sum[w];
+            mx = vmax(mx, s_mx[w]);
+            mn = vmin(mn, s_mn[w]);
+            cnt += s_cnt[w];
+            flags |= s_flags[w];
+        }
+        Partial p;
+        p.sum = to_bits<V>(sum);
+        p.max = to_bits<V>(mx);
+        p.min = to_bits<V>(mn);
+        p.count = cnt;
+        p.blocks = 0;
+        p.flags = flags;
+        p.dtype = dtype;
+        *out = p;
+    }
+}
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// Flat streaming mode: grid-stride over 16-byte vectors, U vectors in flight
+// per lane.  `head` scalar elements precede the first 16-byte boundary.
+template <typename TIn, typename V, int PRED, bool CHAIN, int U>
+__global__ void __launch_bounds__(kThreads)
+    agg_flat_kernel(const TIn *__restrict__ col, int64_t n, int64_t head, KPred pred, KProg val,
+                    uint32_t mask, int32_t vdtype, Partial *__restrict__ parts) {
+    constexpr int VE = 16 / sizeof(TIn);
+    constexpr int E = VE * U;
+    static_assert(E <= 32, "pass mask is 32 bits");
+    Acc<V> acc;
+    acc.init();
+    const int64_t T = (int64_t)gridDim.x * kThreads;
+    const int64_t g = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+    const int64_t nvec = (n - head) / VE;
+    const u32x4 *__restrict__ vp = reinterpret_cast<const u32x4 *>(col + head);
+    constexpr uint32_t kFull = (E == 32) ? 0xffffffffu : ((1u << E) - 1u);
+
+    int64_t v = g;
+    for (; v + (int64_t)(U - 1) * T < nvec; v += (int64_t)U * T) {
+        u32x4 raw[U];
+#pragma unroll
+        for (int k = 0; k < U; ++k) raw[k] = __builtin_nontemporal_load(vp + v + (int64_t)k * T);
+        TIn x[E];
+        int64_t idx[E];
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            __builtin_memcpy(&x[k * VE], &raw[k], 16);
+#pragma unroll
+            for (int e = 0; e < VE; ++e) idx[k * VE + e] = head + (v + (int64_t)k * T) * VE + e;
+        }
+        process<TIn, V, PRED, CHAIN, E>(x, idx, kFull, pred, val, mask, acc);
+    }
+    for (; v < nvec; v += T) {
+        const u32x4 raw = __builtin_nontemporal_load(vp + v);
+        TIn x[VE];
+        int64_t idx[VE];
+        __builtin_memcpy(&x[0], &raw, 16);
+#pragma unroll
+        for (int e = 0; e < VE; ++e) idx[e] = head + v * VE + e;
+        process<TIn, V, PRED, CHAIN, VE>(x, idx, (1u << VE) - 1u, pred, val, mask, acc);
+    }
+    // scalar edges: [0, head) and [head + nvec*VE, n)
+    const int64_t tail0 = head + nvec * VE;
+    const int64_t nedge = head + (n - tail0);
+    for (int64_t t = g; t < nedge; t += T) {
+        const int64_t i = t < head ? t : tail0 + (t - head);
+        TIn x[1] = {col[i]};
+        int64_t idx[1] = {i};
+        process<TIn, V, PRED, CHAIN, 1>(x, idx, 1u, pred, val, mask, acc);
+    }
+    reduce_and_store<V>(acc, parts + blockIdx.x, vdtype);
+}
+
+// Block mode: one wave owns whole reference blocks of R rows; one ballot per
+// block tells whether any of its rows survived the predicate.
+template <typename TIn, typename V, int PRED, bool CHAIN, int U>
+__global__ void __launch_bounds__(kThreads)
+    agg_block_kernel(const TIn *__restrict__ col, int64_t n, int64_t R, KPred pred, KProg val,
+                     uint32_t mask, int32_t vdtype, Partial *__restrict__ parts) {
+    Acc<V> acc;
+    acc.init();
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t w = ((int64_t)blockIdx.x * kThreads + threadIdx.x) / kWave;
+    const int64_t W = ((int64_t)gridDim.x * kThreads) / kWave;
+    const int64_t nb = (n + R - 1) / R;
+    for (int64_t b = w; b < nb; b += W) {
+        const int64_t s = b * R;
+        const int64_t e = (s + R < n) ? s + R : n;
+        uint32_t any = 0;
+        for (int64_t i = s + lane; i < e; i += (int64_t)kWave * U) {
+            TIn x[U];
+            int64_t idx[U];
+            uint32_t live = 0;
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                idx[k] = i + (int64_t)k * kWave;
+                if (idx[k] < e) {
+                    x[k] = __builtin_nontemporal_load(col + idx[k]);
+                    live |= 1u << k;
+                } else {
+                    x[k] = TIn(0);
+                }
+            }
+            any |= process<TIn, V, PRED, CHAIN, U>(x, idx, live, pred, val, mask, acc);
+        }
+        if (__ballot(any != 0) == 0ull) acc.flags |= FQ_STATE_ANY_EMPTY;
+    }
+    reduce_and_store<V>(acc, parts + blockIdx.x, vdtype);
+}
+
+// Single workgroup, fixed order: thread t folds partials t, t+256, ... then a
+// butterfly; the result is deterministic for a given grid.
+template <typename V>
+__global__ void __launch_bounds__(kThreads)
+    agg_finalize_kernel(const Partial *__restrict__ parts, int nparts, uint64_t blocks,
+                        int32_t vdtype, int empty_if_zero, fq_agg_state *__restrict__ out) {
+    Acc<V> acc;
+    acc.init();
+    for (int i = threadIdx.x; i < nparts; i += kThreads) {
+        const Partial p = parts[i];
+        acc.sum = acc.sum + from_bits<V>(p.sum);
+        acc.mx = vmax(acc.mx, from_bits<V>(p.max));
+        acc.mn = vmin(acc.mn, from_bits<V>(p.min));
+        acc.cnt += p.count;
+        acc.flags |= p.flags;
+    }
+    __shared__ Partial s_out;
+    reduce_and_store<V>(acc, &s_out, vdtype);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        fq_agg_state r;
+        r.sum = s_out.sum;
+        r.max = s_out.max;
+        r.min = s_out.min;
+        r.count = s_out.count;
+        r.blocks = blocks;
+        r.flags = s_out.flags;
+        if (empty_if_zero && r.count == 0) r.flags |= FQ_STATE_ANY_EMPTY;
+        r.dtype = vdtype;
+        *out = r;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// host-side lowering and dispatch
+// ---------------------------------------------------------------------------
+
+static bool is_pow2(uint64_t v) { return v && !(v & (v - 1)); }
+
+// libdivide's u64 round-up magic (branchful form)
+static void u64_magic(uint64_t d, uint64_t &magic, uint32_t &shift, uint32_t &add) {
+    const uint32_t l = 63 - __builtin_clzll(d);
+    const unsigned __int128 num = (unsigned __int128)1 << (64 + l);
+    uint64_t proposed = (uint64_t)(num / d);
+    const uint64_t rem = (uint64_t)(num % d);
+    const uint64_t e = d - rem;
+    if (e < (1ull << l)) {
+        add = 0;
+    } else {
+        proposed += proposed;
+        const uint64_t twice_rem = rem + rem;
+        if (twice_rem >= d || twice_rem < rem) proposed += 1;
+        add = 1;
+    }
+    shift = l;
+    magic = proposed + 1;
+}
+
+static bool is_chain_dtype(int32_t dt) {
+    return dt == FQ_DT_UINT64 || dt == FQ_DT_INT64 || dt == FQ_DT_FLOAT64;
+}
+
+static fq_status push_cast(int32_t from, int32_t to, KProg &out) {
+    if (from == to) return FQ_OK;
+    if (out.n >= (int)(sizeof(out.s) / sizeof(out.s[0])))
+        return fqc::fail(FQ_E_UNSUPPORTED, "expression too long for the fused device path");
+    KStep &s = out.s[out.n++];
+    s = KStep{};
+    s.dtype = to;
+    if (from == FQ_DT_UINT64 && to == FQ_DT_INT64) s.code = K_CAST_U2I;
+    else if (from == FQ_DT_UINT64 && to == FQ_DT_FLOAT64) s.code = K_CAST_U2F;
+    else if (from == FQ_DT_INT64 && to == FQ_DT_FLOAT64) s.code = K_CAST_I2F;
+    else
+        return fqc::fail(FQ_E_UNSUPPORTED, std::string("fused cast ") + fqc::dtype_name(from) + " -> " +
+                                               fqc::dtype_name(to) + " is not supported on the device path");
+    return FQ_OK;
+}
+
+// fq_expr (semantic) -> KProg (lowered).  Returns the resulting dtype.
+fq_status lower_expr(const fq_expr &e, int32_t col_dtype, KProg &out, int32_t &res_dtype) {
+    out.n = 0;
+    int32_t acc = col_dtype;
+    if (e.n_steps < 0 || e.n_steps > FQ_MAX_STEPS)
+        return fqc::fail(FQ_E_INVALID, "fq_expr: n_steps out of range");
+    if (e.n_steps > 0 && !is_chain_dtype(col_dtype))
+        return fqc::fail(FQ_E_UNSUPPORTED, std::string("fused expressions over ") + fqc::dtype_name(col_dtype) +
+                                               " columns are not supported on the device path");
+    for (int i = 0; i < e.n_steps; ++i) {
+        const fq_step &st = e.steps[i];
+        if (!is_chain_dtype(st.dtype))
+            return fqc::fail(FQ_E_UNSUPPORTED, "fused step dtype must be UInt64, Int64 or Float64");
+        fq_status s = push_cast(acc, st.dtype, out);
+        if (s != FQ_OK) return s;
+        if (st.operand == FQ_OPERAND_COLUMN && col_dtype == FQ_DT_FLOAT64 && st.dtype != FQ_DT_FLOAT64)
+            return fqc::fail(FQ_E_INVALID, "fq_step: Float64 column operand in an integer step");
+        if (out.n >= (int)(sizeof(out.s) / sizeof(out.s[0])))
+            return fqc::fail(FQ_E_UNSUPPORTED, "expression too long for the fused device path");
+        KStep &k = out.s[out.n++];
+        k = KStep{};
+        k.operand = st.operand;
+        k.reversed = st.reversed;
+        k.dtype = st.dtype;
+        k.c = st.bits;
+        const bool konst = st.operand == FQ_OPERAND_CONST && !st.reversed;
+        if (st.dtype == FQ_DT_FLOAT64) {
+            switch (st.op) {
+                case FQ_OP_ADD: k.code = K_ADD_F; break;
+                case FQ_OP_SUB: k.code = K_SUB_F; break;
+                case FQ_OP_MUL: k.code = K_MUL_F; break;
+                case FQ_OP_DIV: k.code = K_DIV_F; break;
+                case FQ_OP_MOD: k.code = K_MOD_F; break;
+                default: return fqc::fail(FQ_E_INVALID, "fq_step: bad op");
+            }
+        } else {
+            const bool u = st.dtype == FQ_DT_UINT64;
+            switch (st.op) {
+                case FQ_OP_ADD: k.code = K_ADD_I; break;
+                case FQ_OP_SUB: k.code = K_SUB_I; break;
+                case FQ_OP_MUL: k.code = K_MUL_I; break;
+                case FQ_OP_DIV:
+                    if (u && konst && st.bits != 0) {
+                        if (is_pow2(st.bits)) {
+                            k.code = K_SHR_U;
+                            k.shift = (uint32_t)__builtin_ctzll(st.bits);
+                        } else {
+                            k.code = K_DIVM_U;
+                            u64_magic(st.bits, k.magic, k.shift, k.add);
+                        }
+                    } else {
+                        k.code = u ? K_DIV_U : K_DIV_S;
+                    }
+                    break;
+                case FQ_OP_MOD:
+                    if (u && konst && st.bits != 0) {
+                        if (is_pow2(st.bits)) {
+                            k.code = K_AND_U;
+                            k.magic = st.bits - 1;
+                        } else {
+                            k.code = K_MODM_U;
+                            u64_magic(st.bits, k.magic, k.shift, k.add);
+                        }
+                    } else {
+                        k.code = u ? K_MOD_U : K_MOD_S;
+                    }
+                    break;
+                default: return fqc::fail(FQ_E_INVALID, "fq_step: bad op");
+            }
+        }
+        acc = st.dtype;
+    }
+    if (e.n_steps > 0 && e.out_dtype != acc)
+        return fqc::fail(FQ_E_INVALID, "fq_expr: out_dtype does not match the last step");
+    res_dtype = acc;
+    out.out_dtype = acc;
+    return FQ_OK;
+}
+
+struct Launch {
+    const void *col;
+    int64_t n;
+    int64_t head;
+    int64_t block_rows;
+    bool block_mode;
+    KPred pred;
+    KProg val;
+    uint32_t mask;
+    int32_t vdtype;
+    Partial *parts;
+    int grid;
+    hipStream_t stream;
+};
+
+template <typename TIn, typename V, int PRED, bool CHAIN>
+static fq_status launch_scan(const Launch &L) {
+    // vectors in flight per lane: 64 B for 64-bit columns, 16 elements otherwise
+    constexpr int U = sizeof(TIn) >= 4 ? 4 : (sizeof(TIn) == 2 ? 2 : 1);
+    if (PRED != FQ_PRED_NONE && L.block_mode) {
+        hipLaunchKernelGGL((agg_block_kernel<TIn, V, PRED, CHAIN, 8>), dim3(L.grid), dim3(kThreads), 0,
+                           L.stream, (const TIn *)L.col, L.n, L.block_rows, L.pred, L.val, L.mask,
+                           L.vdtype, L.parts);
+    } else {
+        hipLaunchKernelGGL((agg_flat_kernel<TIn, V, PRED, CHAIN, U>), dim3(L.grid), dim3(kThreads), 0,
+                           L.stream, (const TIn *)L.col, L.n, L.head, L.pred, L.val, L.mask, L.vdtype,
+                           L.parts);
+    }
+    FQ_HIP_TRY(hipGetLastError());
+    return FQ_OK;
+}
+
+template <typename TIn, typename V, bool CHAIN>
+static fq_status dispatch_pred(const Launch &L) {
+    switch (L.pred.kind) {
+        case FQ_PRED_NONE: return launch_scan<TIn, V, FQ_PRED_NONE, CHAIN>(L);
+        case FQ_PRED_BITMAP: return launch_scan<TIn, V, FQ_PRED_BITMAP, CHAIN>(L);
+        case FQ_PRED_EXPR:
+            if constexpr (sizeof(TIn) == 8) return launch_scan<TIn, V, FQ_PRED_EXPR, CHAIN>(L);
+            return fqc::fail(FQ_E_UNSUPPORTED, "fused predicates need a 64-bit column");
+        default: return fqc::fail(FQ_E_INVALID, "fq_pred: bad kind");
+    }
+}
+
+template <typename V>
+static fq_status launch_finalize(const Launch &L, uint64_t blocks, int empty_if_zero, fq_agg_state *d_out) {
+    hipLaunchKernelGGL((agg_finalize_kernel<V>), dim3(1), dim3(kThreads), 0, L.stream, L.parts, L.grid,
+                       blocks, L.vdtype, empty_if_zero, d_out);
+    FQ_HIP_TRY(hipGetLastError());
+    return FQ_OK;
+}
+
+static fq_status dispatch(int32_t col_dt, const Launch &L, bool chain) {
+    const int32_t v = L.vdtype;
+    if (!chain) {
+        switch (col_dt) {
+            case FQ_DT_INT8: return dispatch_pred<int8_t, int8_t, false>(L);
+            case FQ_DT_INT16: return dispatch_pred<int16_t, int16_t, false>(L);
+            case FQ_DT_INT32: return dispatch_pred<int32_t, int32_t, false>(L);
+            case FQ_DT_INT64: return dispatch_pred<int64_t, int64_t, false>(L);
+            case FQ_DT_UINT8: return dispatch_pred<uint8_t, uint8_t, false>(L);
+            case FQ_DT_UINT16: return dispatch_pred<uint16_t, uint16_t, false>(L);
+            case FQ_DT_UINT32: return dispatch_pred<uint32_t, uint32_t, false>(L);
+            case FQ_DT_UINT64: return dispatch_pred<uint64_t, uint64_t, false>(L);
+            case FQ_DT_FLOAT32: return dispatch_pred<float, float, false>(L);
+            case FQ_DT_FLOAT64: return dispatch_pred<double, double, false>(L);
+            default: break;
+        }
+    } else if (col_dt == FQ_DT_UINT64) {
+        if (v == FQ_DT_UINT64) return dispatch_pred<uint64_t, uint64_t, true>(L);
+        if (v == FQ_DT_INT64) return dispatch_pred<uint64_t, int64_t, true>(L);
+        if (v == FQ_DT_FLOAT64) return dispatch_pred<uint64_t, double, true>(L);
+    } else if (col_dt == FQ_DT_INT64) {
+        if (v == FQ_DT_INT64) return dispatch_pred<int64_t, int64_t, true>(L);
+        if (v == FQ_DT_FLOAT64) return dispatch_pred<int64_t, double, true>(L);
+    } else if (col_dt == FQ_DT_FLOAT64) {
+        if (v == FQ_DT_FLOAT64) return dispatch_pred<double, double, true>(L);
+    }
+    return fqc::fail(FQ_E_UNSUPPORTED, std::string("aggregate over ") + fqc::dtype_name(col_dt) +
+                                           " column with " + fqc::dtype_name(v) +
+                                           " value is not supported on the device path");
+}
+
+static fq_status dispatch_finalize(const Launch &L, uint64_t blocks, int empty_if_zero, fq_agg_state *d_out) {
+    switch (L.vdtype) {
+        case FQ_DT_INT8: return launch_finalize<int8_t>(L, blocks, empty_if_zero, d_out);
+        case FQ_DT_INT16: return launch_finalize<int16_t>(L, blocks, empty_if_zero, d_out);
+        case FQ_DT_INT32: return launch_finalize<int32_t>(L, blocks, empty_if_zero, d_out);
+        case FQ_DT_INT64: return launch_finalize<int64_t>(L, blocks, empty_if_zero, d_out);
+        case FQ_DT_UINT8: return launch_finalize<uint8_t>(L, blocks, empty_if_zero, d_out);
+        case FQ_DT_UINT16: return launch_finalize<uint16_t>(L, blocks, empty_if_zero, d_out);
+        case FQ_DT_UINT32: return launch_finalize<uint32_t>(L, blocks, empty_if_zero, d_out);
+        case FQ_DT_UINT64: return launch_finalize<uint64_t>(L, blocks, empty_if_zero, d_out);
+        case FQ_DT_FLOAT32: return launch_finalize<float>(L, blocks, empty_if_zero, d_out);
+        case FQ_DT_FLOAT64: return launch_finalize<double>(L, blocks, empty_if_zero, d_out);
+        default: return fqc::fail(FQ_E_INVALID, "finalize: bad dtype");
+    }
+}
+
+}  // namespace fqk
+
+extern "C" {
+
+size_t fq_aggregate_workspace_bytes(int64_t len) {
+    (void)len;
+    return (size_t)fqk::kMaxPartials * sizeof(fqk::Partial);
+}
+
+fq_status fq_aggregate(const fq_col *col, int64_t block_rows, const fq_pred *pred, const fq_expr *value,
+                       uint32_t agg_mask, fq_agg_state *d_out, void *d_ws, size_t ws_bytes, void *stream) {
+    using namespace fqk;
+    if (!col || !d_out || !d_ws) return fqc::fail(FQ_E_INVALID, "fq_aggregate: NULL argument");
+    if (col->len < 0) return fqc::fail(FQ_E_INVALID, "fq_aggregate: negative length");
+    if (ws_bytes < fq_aggregate_workspace_bytes(col->len))
+        return fqc::fail(FQ_E_INVALID, "fq_aggregate: workspace too small");
+    const int esize = fqc::dtype_size(col->dtype);
+    if (!fqc::dtype_is_numeric(col->dtype))
+        return fqc::internal(std::string("Unsupported data_array_aggregate for data type: ") +
+                             fqc::dtype_name(col->dtype));
+    if (col->len > 0 && !col->data) return fqc::fail(FQ_E_INVALID, "fq_aggregate: NULL column data");
+    if (((uintptr_t)col->data) % esize)
+        return fqc::fail(FQ_E_INVALID, "fq_aggregate: column not aligned to its element size");
+    if (block_rows <= 0) block_rows = col->len > 0 ? col->len : 1;
+
+    Launch L{};
+    L.col = col->data;
+    L.n = col->len;
+    L.block_rows = block_rows;
+    L.mask = agg_mask;
+    L.stream = (hipStream_t)stream;
+    L.parts = (Partial *)d_ws;
+
+    // value expression
+    bool chain = value && value->n_steps > 0;
+    int32_t vdt = col->dtype;
+    if (chain) {
+        fq_status s = lower_expr(*value, col->dtype, L.val, vdt);
+        if (s != FQ_OK) return s;
+    }
+    L.vdtype = vdt;
+
+    // predicate
+    L.pred.kind = pred ? pred->kind : FQ_PRED_NONE;
+    if (L.pred.kind == FQ_PRED_EXPR) {
+        int32_t ldt = col->dtype;
+        fq_status s = lower_expr(pred->lhs, col->dtype, L.pred.lhs, ldt);
+        if (s != FQ_OK) return s;
+        if (!is_chain_dtype(pred->cmp_dtype))
+            return fqc::fail(FQ_E_UNSUPPORTED, "fused comparison type must be UInt64, Int64 or Float64");
+        s = push_cast(ldt, pred->cmp_dtype, L.pred.lhs);
+        if (s != FQ_OK) return s;
+        if (pred->rhs_operand == FQ_OPERAND_COLUMN && col->dtype == FQ_DT_FLOAT64 &&
+            pred->cmp_dtype != FQ_DT_FLOAT64)
+            return fqc::fail(FQ_E_INVALID, "fq_pred: Float64 column compared as integer");
+        L.pred.cmp = pred->cmp;
+        L.pred.cmp_dtype = pred->cmp_dtype;
+        L.pred.rhs_operand = pred->rhs_operand;
+        L.pred.rhs = pred->rhs_bits;
+    } else if (L.pred.kind == FQ_PRED_BITMAP) {
+        if (!pred->bitmap && col->len > 0) return fqc::fail(FQ_E_INVALID, "fq_pred: NULL bitmap");
+        L.pred.bitmap = pred->bitmap;
+    } else if (L.pred.kind != FQ_PRED_NONE) {
+        return fqc::fail(FQ_E_INVALID, "fq_pred: bad kind");
+    }
+
+    const uint64_t blocks = col->len == 0 ? 0 : (uint64_t)((col->len + block_rows - 1) / block_rows);
+    // Block mode only where the per-block emptiness matters (filtered sum over
+    // more than one reference block); otherwise stream flat.
+    L.block_mode = L.pred.kind != FQ_PRED_NONE && (agg_mask & FQ_AGG_SUM) && blocks > 1;
+    const int empty_if_zero = (L.pred.kind != FQ_PRED_NONE && blocks == 1) ? 1 : 0;
+
+    const int cus = fqc::device_cu_count();
+    const int max_grid = cus * 8 < kMaxPartials ? cus * 8 : kMaxPartials;
+    if (L.block_mode) {
+        const int64_t waves_needed = (int64_t)blocks;
+        int64_t grid = (waves_needed + (kThreads / kWave) - 1) / (kThreads / kWave);
+        L.grid = (int)(grid < max_grid ? (grid < 1 ? 1 : grid) : max_grid);
+        L.head = 0;
+    } else {
+        const int64_t vec_elems = 16 / esize;
+        const uintptr_t mis = ((uintptr_t)col->data) & 15u;
+        int64_t head = mis ? (int64_t)((16 - mis) / esize) : 0;
+        if (head > col->len) head = col->len;
+        L.head = head;
+        const int64_t nvec = (col->len - head) / vec_elems;
+        int64_t grid = (nvec + (int64_t)kThreads * 4 - 1) / ((int64_t)kThreads * 4);
+        if (grid < 1) grid = 1;
+        L.grid = (int)(grid < max_grid ? grid : max_grid);
+    }
+    fq_status s = dispatch(col->dtype, L, chain);
+    if (s != FQ_OK) return s;
+    return dispatch_finalize(L, blocks, empty_if_zero, d_out);
+}
+
+}  // extern "C"

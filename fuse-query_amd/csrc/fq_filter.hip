@@ -1,0 +1,175 @@
+// FilterTransform compaction on gfx950 (arrow filter_record_batch,
+// src/transforms/transform_filter.rs:51): keep the rows whose predicate bit
+// is set, preserving order.
+//
+// Three passes over tiles of 256 bitmap words (16,384 rows):
+//   count   one workgroup per tile, popcount of its 256 words -> counts[tile]
+//   scan    one workgroup, exclusive scan of the tile counts (+ total)
+//   scatter one workgroup per tile: LDS scan of its word popcounts, then each
+//           wave walks 64 words; lane l moves row 64w+l to
+//           base + word_offset + popcount(word & lanemask_lt(l)).
+// Reads and writes are contiguous per wave; the bitmap is read twice
+// (1/64 of a u64 column's bytes each time).
+#include <hip/hip_runtime.h>
+
+#include "fq_common.h"
+#include "fq_device.h"
+
+namespace fqk {
+
+constexpr int kTileWords = 256;
+constexpr int kScanThreads = 1024;
+
+__device__ __forceinline__ uint64_t word_at(const uint64_t *bm, int64_t w, int64_t nwords, int64_t n) {
+    if (w >= nwords) return 0;
+    uint64_t v = bm[w];
+    const int64_t rows = n - w * 64;
+    if (rows < 64) v &= (1ull << rows) - 1ull;  // ignore bits past len
+    return v;
+}
+
+__global__ void __launch_bounds__(kTileWords)
+    compact_count_kernel(const uint64_t *__restrict__ bm, int64_t n, uint64_t *__restrict__ counts) {
+    const int64_t nwords = (n + 63) / 64;
+    const int64_t w = (int64_t)blockIdx.x * kTileWords + threadIdx.x;
+    uint64_t c = __popcll(word_at(bm, w, nwords, n));
+#pragma unroll
+    for (int off = kWave / 2; off > 0; off >>= 1) c += shfl_xor64(c, off);
+    __shared__ uint64_t s[kTileWords / kWave];
+    if ((threadIdx.x & (kWave - 1)) == 0) s[threadIdx.x / kWave] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t t = 0;
+#pragma unroll
+        for (int i = 0; i < kTileWords / kWave; ++i) t += s[i];
+        counts[blockIdx.x] = t;
+    }
+}
+
+// exclusive scan of counts[0..ntiles) in place; counts[ntiles] = total
+__global__ void __launch_bounds__(kScanThreads) compact_scan_kernel(uint64_t *counts, int64_t ntiles) {
+    const int64_t per = (ntiles + kScanThreads - 1) / kScanThreads;
+    const int64_t b = threadIdx.x * per;
+    const int64_t e = (b + per < ntiles) ? b + per : ntiles;
+    uint64_t local = 0;
+    for (int64_t i = b; i < e; ++i) local += counts[i];
+    __shared__ uint64_t s[kScanThreads];
+    s[threadIdx.x] = local;
+    __syncthreads();
+    // Hillis-Steele inclusive scan over 1024 sums
+    for (int off = 1; off < kScanThreads; off <<= 1) {
+        const uint64_t v = threadIdx.x >= off ? s[threadIdx.x - off] : 0;
+        __syncthreads();
+        s[threadIdx.x] += v;
+        __syncthreads();
+    }
+    uint64_t run = s[threadIdx.x] - local;  // exclusive prefix of this chunk
+    for (int64_t i = b; i < e; ++i) {
+        const uint64_t c = counts[i];
+        counts[i] = run;
+        run += c;
+    }
+    if (threadIdx.x == kScanThreads - 1) counts[ntiles] = s[kScanThreads - 1];
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kTileWords)
+    compact_scatter_kernel(const T *__restrict__ in, const uint64_t *__restrict__ bm, int64_t n,
+                           const uint64_t *__restrict__ offsets, T *__restrict__ out) {
+    const int64_t nwords = (n + 63) / 64;
+    const int64_t w0 = (int64_t)blockIdx.x * kTileWords;
+    __shared__ uint64_t s_word[kTileWords];
+    __shared__ uint32_t s_off[kTileWords];
+    __shared__ uint32_t s_wsum[kTileWords / kWave];
+    const int t = threadIdx.x;
+    const int lane = t & (kWave - 1);
+    const int wave = t / kWave;
+    const uint64_t word = word_at(bm, w0 + t, nwords, n);
+    s_word[t] = word;
+    // wave-inclusive scan of popcounts
+    uint32_t c = (uint32_t)__popcll(word);
+    uint32_t incl = c;
+#pragma unroll
+    for (int off = 1; off < kWave; off <<= 1) {
+        const uint32_t v = (uint32_t)__shfl_up((int)incl, off, kWave);
+        if (lane >= off) incl += v;
+    }
+    if (lane == kWave - 1) s_wsum[wave] = incl;
+    __syncthreads();
+    uint32_t wave_base = 0;
+    for (int i = 0; i < wave; ++i) wave_base += s_wsum[i];
+    s_off[t] = wave_base + incl - c;
+    __syncthreads();
+    const uint64_t base = offsets[blockIdx.x];
+    const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    for (int j = 0; j < kWave; ++j) {
+        const int wi = wave * kWave + j;
+        const uint64_t wd = s_word[wi];
+        if (wd == 0) continue;  // wave-uniform
+        const int64_t row = (w0 + wi) * 64 + lane;
+        if ((wd >> lane) & 1ull) {
+            const uint64_t pos = base + s_off[wi] + (uint64_t)__popcll(wd & lt_mask);
+            out[pos] = in[row];
+        }
+    }
+}
+
+}  // namespace fqk
+
+extern "C" {
+
+size_t fq_filter_workspace_bytes(int64_t len) {
+    const int64_t nwords = (len + 63) / 64;
+    const int64_t ntiles = (nwords + fqk::kTileWords - 1) / fqk::kTileWords;
+    return (size_t)(ntiles + 1) * sizeof(uint64_t);
+}
+
+fq_status fq_filter_compact(const fq_col *in, const uint64_t *d_bitmap, void *d_out, int64_t *out_len,
+                            void *d_ws, size_t ws_bytes, void *stream) {
+    using namespace fqk;
+    if (!in || !out_len) return fqc::fail(FQ_E_INVALID, "fq_filter_compact: NULL argument");
+    const int64_t n = in->len;
+    *out_len = 0;
+    if (n == 0) return FQ_OK;
+    if (!in->data || !d_bitmap || !d_out || !d_ws)
+        return fqc::fail(FQ_E_INVALID, "fq_filter_compact: NULL buffer");
+    if (ws_bytes < fq_filter_workspace_bytes(n))
+        return fqc::fail(FQ_E_INVALID, "fq_filter_compact: workspace too small");
+    const int esz = in->dtype == FQ_DT_BOOLEAN ? 0 : fqc::dtype_size(in->dtype);
+    if (esz == 0) return fqc::fail(FQ_E_UNSUPPORTED, "fq_filter_compact: column type not supported");
+    hipStream_t st = (hipStream_t)stream;
+    const int64_t nwords = (n + 63) / 64;
+    const int64_t ntiles = (nwords + kTileWords - 1) / kTileWords;
+    uint64_t *counts = (uint64_t *)d_ws;
+    hipLaunchKernelGGL(compact_count_kernel, dim3((unsigned)ntiles), dim3(kTileWords), 0, st, d_bitmap, n,
+                       counts);
+    FQ_HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(compact_scan_kernel, dim3(1), dim3(kScanThreads), 0, st, counts, ntiles);
+    FQ_HIP_TRY(hipGetLastError());
+    switch (esz) {
+        case 1:
+            hipLaunchKernelGGL(compact_scatter_kernel<uint8_t>, dim3((unsigned)ntiles), dim3(kTileWords), 0, st,
+                               (const uint8_t *)in->data, d_bitmap, n, counts, (uint8_t *)d_out);
+            break;
+        case 2:
+            hipLaunchKernelGGL(compact_scatter_kernel<uint16_t>, dim3((unsigned)ntiles), dim3(kTileWords), 0, st,
+                               (const uint16_t *)in->data, d_bitmap, n, counts, (uint16_t *)d_out);
+            break;
+        case 4:
+            hipLaunchKernelGGL(compact_scatter_kernel<uint32_t>, dim3((unsigned)ntiles), dim3(kTileWords), 0, st,
+                               (const uint32_t *)in->data, d_bitmap, n, counts, (uint32_t *)d_out);
+            break;
+        default:
+            hipLaunchKernelGGL(compact_scatter_kernel<uint64_t>, dim3((unsigned)ntiles), dim3(kTileWords), 0, st,
+                               (const uint64_t *)in->data, d_bitmap, n, counts, (uint64_t *)d_out);
+            break;
+    }
+    FQ_HIP_TRY(hipGetLastError());
+    uint64_t total = 0;
+    FQ_HIP_TRY(hipMemcpyAsync(&total, counts + ntiles, sizeof(total), hipMemcpyDeviceToHost, st));
+    FQ_HIP_TRY(hipStreamSynchronize(st));
+    *out_len = (int64_t)total;
+    return FQ_OK;
+}
+
+}  // extern "C"

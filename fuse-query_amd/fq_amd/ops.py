@@ -1,0 +1,210 @@
+"""Tensor-level wrappers over the C ABI of include/fq_gpu.h.
+
+PyTorch only provides device memory and the current HIP stream here; every
+computation is one of the library's gfx950 kernels.  All functions raise
+FQError (status + the reference's error text) on failure, and raise
+immediately when no GPU is present -- there is no CPU fallback.
+"""
+import ctypes as C
+
+import numpy as np
+import torch
+
+from . import abi
+from ._lib import FQError, check, lib
+from .expr import from_bits, to_bits
+
+NP_DTYPES = {
+    abi.DT_INT8: np.int8, abi.DT_INT16: np.int16, abi.DT_INT32: np.int32,
+    abi.DT_INT64: np.int64, abi.DT_UINT8: np.uint8, abi.DT_UINT16: np.uint16,
+    abi.DT_UINT32: np.uint32, abi.DT_UINT64: np.uint64, abi.DT_FLOAT32: np.float32,
+    abi.DT_FLOAT64: np.float64,
+}
+DT_OF_NP = {np.dtype(v): k for k, v in NP_DTYPES.items()}
+ELEM_SIZE = {k: np.dtype(v).itemsize for k, v in NP_DTYPES.items()}
+
+
+def require_gpu():
+    if not torch.cuda.is_available():
+        raise FQError(abi.FQ_E_HIP, "fq_amd: no GPU visible (the device path has no CPU fallback)")
+
+
+def _stream(stream=None):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return C.c_void_p(s.cuda_stream)
+
+
+class DeviceColumn:
+    """An Arrow-layout column in HBM (values buffer, no nulls).  Boolean
+    columns are LSB-first bitmaps in uint64 words."""
+
+    def __init__(self, buf, length, dtype, offset=0):
+        self.buf = buf  # torch uint8 tensor owning the bytes
+        self.len = int(length)
+        self.dtype = dtype
+        self.offset = offset
+
+    @property
+    def ptr(self):
+        return self.buf.data_ptr() + self.offset
+
+    def col(self):
+        return abi.fq_col(C.c_void_p(self.ptr), self.len, self.dtype, 0)
+
+    def nbytes(self):
+        if self.dtype == abi.DT_BOOLEAN:
+            return ((self.len + 63) // 64) * 8
+        return self.len * ELEM_SIZE[self.dtype]
+
+    def to_numpy(self):
+        nb = self.nbytes()
+        host = self.buf[self.offset:self.offset + nb].cpu().numpy()
+        if self.dtype == abi.DT_BOOLEAN:
+            words = host.view(np.uint64)
+            bits = np.unpackbits(words.view(np.uint8), bitorder="little")
+            return bits[: self.len].astype(bool)
+        return host.view(NP_DTYPES[self.dtype]).copy()
+
+
+def empty_column(n, dtype, device=None):
+    require_gpu()
+    nb = ((n + 63) // 64) * 8 if dtype == abi.DT_BOOLEAN else n * ELEM_SIZE[dtype]
+    buf = torch.empty(max(nb, 16), dtype=torch.uint8, device=device or "cuda")
+    return DeviceColumn(buf, n, dtype)
+
+
+def from_numpy(arr, dtype=None):
+    require_gpu()
+    arr = np.ascontiguousarray(arr)
+    dt = dtype if dtype is not None else DT_OF_NP[arr.dtype]
+    raw = arr.view(np.uint8).reshape(-1) if arr.size else np.zeros(16, np.uint8)
+    buf = torch.from_numpy(raw.copy()).to("cuda")
+    return DeviceColumn(buf, arr.shape[0], dt)
+
+
+def numbers_column(begin, count, stream=None):
+    """SourceTransform of one numbers_mt range: [begin, begin+count)."""
+    c = empty_column(count, abi.DT_UINT64)
+    check(lib.fq_fill_numbers_u64(C.c_void_p(c.ptr), begin, count, _stream(stream)))
+    return c
+
+
+def splitmix_column(seed, first_index, count, stream=None):
+    c = empty_column(count, abi.DT_UINT64)
+    check(lib.fq_fill_splitmix64(C.c_void_p(c.ptr), seed, first_index, count, _stream(stream)))
+    return c
+
+
+class Workspace:
+    def __init__(self, nbytes):
+        require_gpu()
+        self.buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device="cuda")
+        self.nbytes = self.buf.numel()
+
+    @property
+    def ptr(self):
+        return C.c_void_p(self.buf.data_ptr())
+
+
+def aggregate_async(col, block_rows=0, pred=None, value=None, mask=0xF, ws=None, out=None,
+                    stream=None):
+    """Launch fq_aggregate; returns the device tensor holding the fq_agg_state."""
+    require_gpu()
+    ws = ws or Workspace(lib.fq_aggregate_workspace_bytes(col.len))
+    if out is None:
+        out = torch.empty(48, dtype=torch.uint8, device="cuda")
+    c = col.col()
+    check(lib.fq_aggregate(C.byref(c), block_rows, C.byref(pred) if pred is not None else None,
+                           C.byref(value) if value is not None else None, mask,
+                           C.c_void_p(out.data_ptr()), ws.ptr, ws.nbytes, _stream(stream)))
+    return out
+
+
+def state_from_device(t):
+    raw = t.cpu().numpy().tobytes()
+    return abi.fq_agg_state.from_buffer_copy(raw)
+
+
+def aggregate(col, block_rows=0, pred=None, value=None, mask=0xF, ws=None, stream=None):
+    """Fused AggregatePartial over one device block -> host fq_agg_state."""
+    t = aggregate_async(col, block_rows, pred, value, mask, ws, None, stream)
+    return state_from_device(t)
+
+
+def state_values(st):
+    """fq_agg_state -> dict(sum, max, min, count, blocks, flags) of Python values."""
+    dt = st.dtype
+    return {
+        "sum": from_bits(st.sum, dt), "max": from_bits(st.max, dt),
+        "min": from_bits(st.min, dt), "count": st.count, "blocks": st.blocks,
+        "flags": st.flags, "dtype": dt,
+    }
+
+
+def _side(x):
+    """DeviceColumn -> (fq_col, None); python scalar / (value, dtype) -> (None, fq_value)."""
+    if isinstance(x, DeviceColumn):
+        return x.col(), None
+    if isinstance(x, abi.fq_value):
+        return None, x
+    from .expr import literal
+    val, dt = literal(x)
+    if val is None:
+        return None, abi.fq_value(dt, 0, 0)
+    return None, abi.fq_value(dt, 1, to_bits(val, dt))
+
+
+def arith(op_sym, lhs, rhs, stream=None):
+    """ArithmeticFunction::eval on device columns / scalars -> DeviceColumn."""
+    require_gpu()
+    lc, ls = _side(lhs)
+    rc, rs = _side(rhs)
+    ldt = lc.dtype if lc is not None else ls.dtype
+    rdt = rc.dtype if rc is not None else rs.dtype
+    out_dt = C.c_int32(0)
+    check(lib.fq_arith_result_type(abi.OP_BY_SYM[op_sym], ldt, rdt, C.byref(out_dt)))
+    n = lc.len if lc is not None else (rc.len if rc is not None else 1)
+    out = empty_column(n, out_dt.value)
+    oc = out.col()
+    flag = torch.zeros(1, dtype=torch.int32, device="cuda")
+    check(lib.fq_arith(abi.OP_BY_SYM[op_sym], C.byref(lc) if lc is not None else None,
+                       C.byref(ls) if ls is not None else None, C.byref(rc) if rc is not None else None,
+                       C.byref(rs) if rs is not None else None, C.byref(oc),
+                       C.c_void_p(flag.data_ptr()), _stream(stream)))
+    return out
+
+
+def compare(cmp_sym, lhs, rhs, stream=None):
+    """ComparisonFunction::eval -> Boolean DeviceColumn (LSB-first bitmap)."""
+    require_gpu()
+    lc, ls = _side(lhs)
+    rc, rs = _side(rhs)
+    n = lc.len if lc is not None else (rc.len if rc is not None else 1)
+    out = empty_column(n, abi.DT_BOOLEAN)
+    flag = torch.zeros(1, dtype=torch.int32, device="cuda")
+    check(lib.fq_compare(abi.CMP_BY_SYM[cmp_sym], C.byref(lc) if lc is not None else None,
+                         C.byref(ls) if ls is not None else None,
+                         C.byref(rc) if rc is not None else None,
+                         C.byref(rs) if rs is not None else None, C.c_void_p(out.ptr), n,
+                         C.c_void_p(flag.data_ptr()), _stream(stream)))
+    return out
+
+
+def filter_compact(col, bitmap, stream=None):
+    """FilterTransform: keep rows whose bit is set, in order -> DeviceColumn."""
+    require_gpu()
+    out = empty_column(col.len, col.dtype)
+    ws = Workspace(lib.fq_filter_workspace_bytes(col.len))
+    n = C.c_int64(0)
+    c = col.col()
+    check(lib.fq_filter_compact(C.byref(c), C.c_void_p(bitmap.ptr), C.c_void_p(out.ptr), C.byref(n),
+                                ws.ptr, ws.nbytes, _stream(stream)))
+    out.len = n.value
+    return out
+
+
+def state_merge(states):
+    arr = (abi.fq_agg_state * len(states))(*states)
+    out = abi.fq_agg_state()
+    check(lib.fq_state_merge(arr, len(states), C.byref(out)))
+    return out

@@ -1,0 +1,230 @@
+/*
+ * fq_gpu.h -- C ABI of the MI355X (gfx950) kernels behind fuse-query's
+ * DataBlock expression + aggregation hot path.
+ *
+ * Every entry point replaces one call site of the reference's CPU path
+ * (dantengsky/fuse-query @ /root/reference, Rust + arrow 2.0 compute):
+ *
+ *   fq_fill_numbers_u64   NumbersStream::poll_next        src/datasources/system/numbers_stream.rs:65-83
+ *   fq_aggregate          AggregatorFunction::accumulate  src/functions/function_aggregator.rs:57-100
+ *                         (-> data_array_aggregate_op     src/datavalues/data_array_aggregate.rs:14-163,
+ *                             arrow::compute::sum/min/max src/datavalues/macros.rs:143-157)
+ *                         fused with the argument eval    src/functions/function_arithmetic.rs:64-72
+ *                         and the WHERE predicate         src/transforms/transform_filter.rs:38-55
+ *   fq_arith              data_array_arithmetic_op        src/datavalues/data_array_arithmetic.rs:14-55
+ *   fq_compare            data_array_comparison_op        src/datavalues/data_array_comparison.rs:14-94
+ *   fq_filter_compact     arrow filter_record_batch       src/transforms/transform_filter.rs:51
+ *   fq_state_merge        AggregatorFunction::merge_state src/functions/function_aggregator.rs:106-139
+ *
+ * Conventions:
+ *   - plain pointers and sizes only; device buffers are owned by the caller and
+ *     are never freed by the library;
+ *   - column values use the Arrow layout: a contiguous values buffer (16-byte
+ *     aligned for the vector path), no null bitmap; Boolean columns are
+ *     LSB-first bit-packed into little-endian uint64 words;
+ *   - `stream` is a hipStream_t passed as void* (NULL = default stream); every
+ *     call is asynchronous on that stream unless documented otherwise;
+ *   - errors are returned as fq_status and the message (the reference's
+ *     FuseQueryError display text where one exists, e.g.
+ *     "Internal Error: Divide by zero error") is kept in a thread-local buffer
+ *     readable with fq_last_error().
+ */
+#ifndef FQ_GPU_H
+#define FQ_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FQ_ABI_VERSION 1
+
+/* ---- status (src/error.rs:10-22 FuseQueryError{SQLParse,Plan,Internal}) ---- */
+typedef int32_t fq_status;
+#define FQ_OK 0
+#define FQ_E_INTERNAL 1       /* FuseQueryError::Internal                       */
+#define FQ_E_PLAN 2           /* FuseQueryError::Plan                           */
+#define FQ_E_DIVIDE_BY_ZERO 3 /* ArrowError::DivideByZero -> Internal (error.rs:24-28) */
+#define FQ_E_UNSUPPORTED 4    /* not supported on the device path (message says what) */
+#define FQ_E_HIP 5            /* HIP runtime error / no GPU                     */
+#define FQ_E_RCCL 6           /* RCCL error                                     */
+#define FQ_E_INVALID 7        /* bad argument (null pointer, misaligned buffer, ...) */
+
+/* ---- DataType (arrow::datatypes::DataType as used by src/datavalues/data_type.rs) ---- */
+#define FQ_DT_NULL 0
+#define FQ_DT_BOOLEAN 1
+#define FQ_DT_INT8 2
+#define FQ_DT_INT16 3
+#define FQ_DT_INT32 4
+#define FQ_DT_INT64 5
+#define FQ_DT_UINT8 6
+#define FQ_DT_UINT16 7
+#define FQ_DT_UINT32 8
+#define FQ_DT_UINT64 9
+#define FQ_DT_FLOAT32 10
+#define FQ_DT_FLOAT64 11
+#define FQ_DT_UTF8 12
+
+/* ---- operators (src/datavalues/data_value_operator.rs:5-81) ---- */
+#define FQ_OP_ADD 0
+#define FQ_OP_SUB 1
+#define FQ_OP_MUL 2
+#define FQ_OP_DIV 3
+#define FQ_OP_MOD 4 /* EXTENSION: '%' has no arm in function_factory.rs:17-39 */
+
+#define FQ_CMP_EQ 0
+#define FQ_CMP_LT 1
+#define FQ_CMP_LTEQ 2
+#define FQ_CMP_GT 3
+#define FQ_CMP_GTEQ 4
+
+/* aggregate op bit mask (DataValueAggregateOperator) */
+#define FQ_AGG_MIN 1u
+#define FQ_AGG_MAX 2u
+#define FQ_AGG_SUM 4u
+#define FQ_AGG_COUNT 8u
+
+/*
+ * A scalar DataValue (src/datavalues/data_value.rs:20-35), numeric/boolean
+ * subset.  dtype FQ_DT_NULL is DataValue::Null; is_some=0 is `X(None)`.
+ * bits: integers hold the value sign/zero-extended to 64 bits, floats hold
+ * the IEEE binary64 bits (Float32 values are widened exactly), booleans 0/1.
+ */
+typedef struct fq_value {
+    int32_t dtype;
+    int32_t is_some;
+    uint64_t bits;
+} fq_value;
+
+/* A device column: Arrow PrimitiveArray values buffer (or Boolean bitmap). */
+typedef struct fq_col {
+    void *data; /* device pointer */
+    int64_t len;
+    int32_t dtype;
+    int32_t reserved;
+} fq_col;
+
+/*
+ * Fusable expression: a chain of binary operators applied to one column x,
+ *   acc = x;  for each step: acc = acc OP operand   (or operand OP acc if reversed)
+ * where operand is a constant or x itself.  This is the shape that
+ * Function::eval produces for ArithmeticFunction trees whose every right (or
+ * left) child is a Constant/Field leaf (function_arithmetic.rs:64-72).
+ * Each step carries the coerced type of that step
+ * (numerical_coercion, data_type.rs:27-90); the library inserts the casts.
+ */
+#define FQ_MAX_STEPS 8
+#define FQ_OPERAND_CONST 0
+#define FQ_OPERAND_COLUMN 1
+typedef struct fq_step {
+    int32_t op;       /* FQ_OP_*                                  */
+    int32_t operand;  /* FQ_OPERAND_CONST / FQ_OPERAND_COLUMN     */
+    int32_t reversed; /* 1: operand OP acc (scalar-array form)    */
+    int32_t dtype;    /* UINT64 / INT64 / FLOAT64                 */
+    uint64_t bits;    /* constant in `dtype` (fq_value encoding)  */
+} fq_step;
+
+typedef struct fq_expr {
+    int32_t n_steps; /* 0 = identity (the column itself)            */
+    int32_t out_dtype; /* type of the result; == column type if n_steps==0 */
+    fq_step steps[FQ_MAX_STEPS];
+} fq_expr;
+
+/* WHERE predicate, fused into the aggregate scan (transform_filter.rs:38-55). */
+#define FQ_PRED_NONE 0
+#define FQ_PRED_EXPR 1   /* cmp(lhs(x), rhs) with rhs a constant or x            */
+#define FQ_PRED_BITMAP 2 /* precomputed Boolean column (from fq_compare)          */
+typedef struct fq_pred {
+    int32_t kind;
+    int32_t cmp;         /* FQ_CMP_*  (already flipped for scalar-array forms)   */
+    int32_t cmp_dtype;   /* equal_coercion type: UINT64 / INT64 / FLOAT64         */
+    int32_t rhs_operand; /* FQ_OPERAND_CONST / FQ_OPERAND_COLUMN                  */
+    uint64_t rhs_bits;   /* constant in cmp_dtype                                */
+    fq_expr lhs;         /* lhs.out_dtype must equal cmp_dtype                   */
+    const uint64_t *bitmap; /* device, kind == FQ_PRED_BITMAP                    */
+} fq_pred;
+
+/*
+ * Partial aggregate over one device block = a run of `blocks` reference
+ * blocks of `block_rows` rows (numbers_stream.rs:29 block_size = 10000; the
+ * last one may be shorter).  Values are in `dtype` (fq_value bit encoding).
+ * flags lets the host replay the reference's per-block state machine exactly:
+ *   FQ_STATE_ANY_EMPTY   some reference block had no row left after the
+ *                        predicate (arrow sum -> None -> the Sum state errors,
+ *                        data_value_arithmetic.rs:10-27)
+ *   FQ_STATE_DIV_ZERO    a row reaching an integer/float '/' or '%' had a zero
+ *                        divisor (ArrowError::DivideByZero)
+ *   FQ_STATE_CAST_NULL   a coercion cast overflowed (arrow cast -> null; nulls
+ *                        are not representable on the device path)
+ */
+#define FQ_STATE_ANY_EMPTY 1u
+#define FQ_STATE_DIV_ZERO 2u
+#define FQ_STATE_CAST_NULL 4u
+typedef struct fq_agg_state {
+    uint64_t sum;   /* wrapping sum (integers) / binary64 sum bits (floats)      */
+    uint64_t max;
+    uint64_t min;
+    uint64_t count;  /* rows that passed the predicate                           */
+    uint64_t blocks; /* reference blocks covered                                 */
+    uint32_t flags;
+    int32_t dtype; /* value dtype                                               */
+} fq_agg_state;
+
+/* ---- library ---- */
+int32_t fq_abi_version(void);
+const char *fq_last_error(void);
+fq_status fq_device_count(int32_t *out);
+
+/* ---- SourceTransform: system.numbers_mt (numbers_stream.rs:65-83) ----
+ * Writes d_out[i] = begin + i for i in [0, count).  One partition of
+ * numbers_mt is one contiguous range (see SURVEY.md finding 8).            */
+fq_status fq_fill_numbers_u64(uint64_t *d_out, uint64_t begin, uint64_t count, void *stream);
+/* Anti-closed-form control column: d_out[i] = splitmix64(seed, first_index + i). */
+fq_status fq_fill_splitmix64(uint64_t *d_out, uint64_t seed, uint64_t first_index,
+                             uint64_t count, void *stream);
+
+/* ---- AggregatePartial: fused predicate + argument expression + sum/max/min/count ----
+ * One pass over `col`; writes one fq_agg_state to device memory d_out.
+ * block_rows: reference block size of this device block (10000 for
+ * numbers_mt, or col->len for a single DataBlock).  Workspace is device
+ * memory of at least fq_aggregate_workspace_bytes(col->len) bytes.
+ * value may be NULL (identity).  pred may be NULL (no WHERE).                */
+size_t fq_aggregate_workspace_bytes(int64_t len);
+fq_status fq_aggregate(const fq_col *col, int64_t block_rows, const fq_pred *pred,
+                       const fq_expr *value, uint32_t agg_mask, fq_agg_state *d_out,
+                       void *d_ws, size_t ws_bytes, void *stream);
+
+/* ---- ArithmeticFunction::eval (data_array_arithmetic.rs:14-55) ----
+ * Exactly one of {lhs, lhs_scalar} and one of {rhs, rhs_scalar} is non-NULL.
+ * out->data must hold out->len elements of the coercion type returned by
+ * fq_arith_result_type.  d_flag: 4 bytes of device scratch; when non-NULL the
+ * call synchronises `stream` and reports FQ_E_DIVIDE_BY_ZERO / cast nulls.   */
+fq_status fq_arith_result_type(int32_t op, int32_t lhs_dtype, int32_t rhs_dtype, int32_t *out);
+fq_status fq_arith(int32_t op, const fq_col *lhs, const fq_value *lhs_scalar, const fq_col *rhs,
+                   const fq_value *rhs_scalar, fq_col *out, uint32_t *d_flag, void *stream);
+
+/* ---- ComparisonFunction::eval (data_array_comparison.rs:14-94) ----
+ * Writes an LSB-first bitmap of ceil(len/64) uint64 words (bits past len are 0).
+ * Scalar-array forms flip the operator as the reference does (:76-84).       */
+fq_status fq_compare(int32_t cmp, const fq_col *lhs, const fq_value *lhs_scalar,
+                     const fq_col *rhs, const fq_value *rhs_scalar, uint64_t *d_bitmap,
+                     int64_t len, uint32_t *d_flag, void *stream);
+
+/* ---- FilterTransform: order-preserving compaction (arrow filter_record_batch) ----
+ * Synchronises `stream`; *out_len receives the number of rows kept.          */
+size_t fq_filter_workspace_bytes(int64_t len);
+fq_status fq_filter_compact(const fq_col *in, const uint64_t *d_bitmap, void *d_out,
+                            int64_t *out_len, void *d_ws, size_t ws_bytes, void *stream);
+
+/* ---- AggregateFinal state merge (host, function_aggregator.rs:106-139) ----
+ * Merges `n` partial states in the given order into *out (wrapping sum,
+ * summed counts/blocks, max, min, OR-ed flags).  All dtypes must match.      */
+fq_status fq_state_merge(const fq_agg_state *states, int32_t n, fq_agg_state *out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FQ_GPU_H */

@@ -1,0 +1,518 @@
+/*
+ * fq_oracle.c -- TEST INFRASTRUCTURE ONLY (parity checker + CPU baseline).
+ * See fq_oracle.h for what it restates and why its structure is kept slow on
+ * purpose.  Every function cites the reference file:line it follows.
+ */
+#define _GNU_SOURCE
+#include "fq_oracle.h"
+
+#include <math.h>
+#include <pthread.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define BLOCK_SIZE 10000 /* numbers_stream.rs:29 */
+
+/* ------------------------------------------------------------------ */
+/* numbers_mt partitioning                                              */
+/* ------------------------------------------------------------------ */
+
+/* NumbersTable::generate_parts (numbers_table.rs:29-55) */
+int32_t fqo_num_partitions(uint64_t total) { return total / 8 == 0 ? 1 : 8; }
+
+void fqo_partition_range(uint64_t total, int32_t p, uint64_t *begin, uint64_t *end) {
+    const uint64_t workers = 8, chunk = total / workers;
+    if (chunk == 0) {
+        *begin = 0;
+        *end = total - 1; /* total == 0 wraps in release: unsupported, see DESIGN.md */
+        return;
+    }
+    *begin = (uint64_t)p * chunk;
+    *end = ((uint64_t)p + 1) * chunk - 1;
+    if (p == (int32_t)workers - 1) *end += total % workers;
+}
+
+/* NumbersStream::create (numbers_stream.rs:27-62): the partition's block list.
+ * Calls fn(begin, end_inclusive) for every block in order. */
+typedef int (*block_fn)(void *ctx, uint64_t b, uint64_t e);
+static int numbers_blocks(uint64_t begin, uint64_t end, block_fn fn, void *ctx) {
+    const uint64_t count = end - begin + 1;
+    const uint64_t nblocks = count / BLOCK_SIZE, remain = count % BLOCK_SIZE;
+    if (nblocks > 0) {
+        for (uint64_t i = 0; i < nblocks; ++i) {
+            const uint64_t bb = begin + BLOCK_SIZE * i;
+            uint64_t be = begin + BLOCK_SIZE * (i + 1) - 1;
+            if (i == nblocks - 1 && remain > 0) be = bb + remain; /* the quirk: rows dropped */
+            int rc = fn(ctx, bb, be);
+            if (rc) return rc;
+        }
+        return 0;
+    }
+    return fn(ctx, begin, end);
+}
+
+static int count_rows_fn(void *ctx, uint64_t b, uint64_t e) {
+    *(uint64_t *)ctx += e - b + 1;
+    return 0;
+}
+
+uint64_t fqo_partition_rows(uint64_t total, int32_t p) {
+    uint64_t b, e, rows = 0;
+    fqo_partition_range(total, p, &b, &e);
+    numbers_blocks(b, e, count_rows_fn, &rows);
+    return rows;
+}
+
+uint64_t fqo_splitmix64(uint64_t seed, uint64_t i) {
+    uint64_t z = seed + (i + 1) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+/* ------------------------------------------------------------------ */
+/* arrays (arrow PrimitiveArray restated as bits + dtype)               */
+/* ------------------------------------------------------------------ */
+typedef struct {
+    uint64_t *v;
+    int64_t n;
+    int32_t dtype;
+} arr_t;
+
+typedef struct {
+    int status; /* fq_status */
+    char msg[256];
+} err_t;
+
+static int set_err(err_t *e, int st, const char *m) {
+    if (!e->status) {
+        e->status = st;
+        snprintf(e->msg, sizeof(e->msg), "%s", m);
+    }
+    return st;
+}
+
+static double as_f(uint64_t b) {
+    double d;
+    memcpy(&d, &b, 8);
+    return d;
+}
+static uint64_t of_f(double d) {
+    uint64_t b;
+    memcpy(&b, &d, 8);
+    return b;
+}
+
+static arr_t arr_new(int64_t n, int32_t dt) {
+    arr_t a;
+    a.v = (uint64_t *)malloc((size_t)(n > 0 ? n : 1) * 8);
+    a.n = n;
+    a.dtype = dt;
+    return a;
+}
+static void arr_free(arr_t *a) {
+    free(a->v);
+    a->v = NULL;
+}
+
+/* arrow::compute::cast between the 64-bit types (num-traits NumCast); a value
+ * that does not fit becomes null in the reference.  Nulls are outside this
+ * restatement's scope: reported as FQ_E_UNSUPPORTED "cast produced nulls"
+ * (the device path reports the same; documented in DESIGN.md). */
+static int cast_arr(const arr_t *in, int32_t to, arr_t *out, err_t *err) {
+    *out = arr_new(in->n, to);
+    for (int64_t i = 0; i < in->n; ++i) {
+        const uint64_t x = in->v[i];
+        if (in->dtype == to) {
+            out->v[i] = x;
+        } else if (to == FQ_DT_FLOAT64) {
+            out->v[i] = of_f(in->dtype == FQ_DT_INT64 ? (double)(int64_t)x : (double)x);
+        } else if (in->dtype == FQ_DT_UINT64 && to == FQ_DT_INT64) {
+            if (x >> 63) return set_err(err, FQ_E_UNSUPPORTED, "cast produced nulls");
+            out->v[i] = x;
+        } else {
+            return set_err(err, FQ_E_UNSUPPORTED, "cast not covered by the oracle");
+        }
+    }
+    return 0;
+}
+
+/* DataValue::to_array(size): materialised constant broadcast (data_value.rs:77-111) */
+static arr_t broadcast(uint64_t bits, int32_t dt, int64_t n) {
+    arr_t a = arr_new(n, dt);
+    for (int64_t i = 0; i < n; ++i) a.v[i] = bits;
+    return a;
+}
+
+/* arrow add/subtract/multiply/divide (+ '%' extension) on same-typed arrays
+ * (data_array_arithmetic.rs:42-54).  Release build: integer wrap.  Divide
+ * checks every divisor first and fails with DivideByZero. */
+static int arith_arr(int32_t op, const arr_t *l, const arr_t *r, arr_t *out, err_t *err) {
+    const int32_t dt = l->dtype;
+    const int64_t n = l->n;
+    if (op == FQ_OP_DIV || op == FQ_OP_MOD) {
+        for (int64_t i = 0; i < n; ++i) {
+            const int zero = dt == FQ_DT_FLOAT64 ? as_f(r->v[i]) == 0.0 : r->v[i] == 0;
+            if (zero) return set_err(err, FQ_E_DIVIDE_BY_ZERO, "Internal Error: Divide by zero error");
+        }
+    }
+    *out = arr_new(n, dt);
+    for (int64_t i = 0; i < n; ++i) {
+        const uint64_t a = l->v[i], b = r->v[i];
+        uint64_t z = 0;
+        if (dt == FQ_DT_FLOAT64) {
+            const double fa = as_f(a), fb = as_f(b);
+            double fz = 0;
+            switch (op) {
+                case FQ_OP_ADD: fz = fa + fb; break;
+                case FQ_OP_SUB: fz = fa - fb; break;
+                case FQ_OP_MUL: fz = fa * fb; break;
+                case FQ_OP_DIV: fz = fa / fb; break;
+                default: fz = fmod(fa, fb); break;
+            }
+            z = of_f(fz);
+        } else if (dt == FQ_DT_INT64) {
+            const int64_t sa = (int64_t)a, sb = (int64_t)b;
+            switch (op) {
+                case FQ_OP_ADD: z = a + b; break;
+                case FQ_OP_SUB: z = a - b; break;
+                case FQ_OP_MUL: z = a * b; break;
+                case FQ_OP_DIV: z = sb == -1 ? (uint64_t)0 - a : (uint64_t)(sa / sb); break;
+                default: z = sb == -1 ? 0 : (uint64_t)(sa % sb); break;
+            }
+        } else {
+            switch (op) {
+                case FQ_OP_ADD: z = a + b; break;
+                case FQ_OP_SUB: z = a - b; break;
+                case FQ_OP_MUL: z = a * b; break;
+                case FQ_OP_DIV: z = a / b; break;
+                default: z = a % b; break;
+            }
+        }
+        out->v[i] = z;
+    }
+    return 0;
+}
+
+/* operand of a step: constant broadcast or the block's column cast to dtype */
+static int operand_arr(int32_t operand, uint64_t bits, int32_t dt, const arr_t *x, arr_t *out, err_t *err) {
+    if (operand == FQ_OPERAND_CONST) {
+        *out = broadcast(bits, dt, x->n);
+        return 0;
+    }
+    return cast_arr(x, dt, out, err);
+}
+
+/* Function::eval of an ArithmeticFunction chain (function_arithmetic.rs:64-72):
+ * each level evaluates its children to arrays, casts both to the coercion
+ * type (data_array_arithmetic.rs:34-40) and runs one arrow kernel. */
+static int eval_chain(const fq_expr *e, const arr_t *x, arr_t *out, err_t *err) {
+    arr_t acc = arr_new(x->n, x->dtype);
+    memcpy(acc.v, x->v, (size_t)x->n * 8);
+    for (int s = 0; s < e->n_steps; ++s) {
+        const fq_step *st = &e->steps[s];
+        arr_t accc, opnd, res;
+        if (cast_arr(&acc, st->dtype, &accc, err)) {
+            arr_free(&acc);
+            return err->status;
+        }
+        arr_free(&acc);
+        if (operand_arr(st->operand, st->bits, st->dtype, x, &opnd, err)) {
+            arr_free(&accc);
+            return err->status;
+        }
+        int rc = st->reversed ? arith_arr(st->op, &opnd, &accc, &res, err) : arith_arr(st->op, &accc, &opnd, &res, err);
+        arr_free(&accc);
+        arr_free(&opnd);
+        if (rc) return rc;
+        acc = res;
+    }
+    *out = acc;
+    return 0;
+}
+
+static int cmp1(int32_t cmp, int32_t dt, uint64_t a, uint64_t b) {
+    if (dt == FQ_DT_FLOAT64) {
+        const double x = as_f(a), y = as_f(b);
+        switch (cmp) {
+            case FQ_CMP_EQ: return x == y;
+            case FQ_CMP_LT: return x < y;
+            case FQ_CMP_LTEQ: return x <= y;
+            case FQ_CMP_GT: return x > y;
+            default: return x >= y;
+        }
+    }
+    if (dt == FQ_DT_INT64) {
+        const int64_t x = (int64_t)a, y = (int64_t)b;
+        switch (cmp) {
+            case FQ_CMP_EQ: return x == y;
+            case FQ_CMP_LT: return x < y;
+            case FQ_CMP_LTEQ: return x <= y;
+            case FQ_CMP_GT: return x > y;
+            default: return x >= y;
+        }
+    }
+    switch (cmp) {
+        case FQ_CMP_EQ: return a == b;
+        case FQ_CMP_LT: return a < b;
+        case FQ_CMP_LTEQ: return a <= b;
+        case FQ_CMP_GT: return a > b;
+        default: return a >= b;
+    }
+}
+
+/* FilterTransform::expression_executor (transform_filter.rs:38-55): evaluate
+ * the ComparisonFunction to a BooleanArray, then filter_record_batch. */
+static int filter_block(const fq_pred *p, const arr_t *x, arr_t *out, err_t *err) {
+    arr_t l, lc, r;
+    if (eval_chain(&p->lhs, x, &l, err)) return err->status;
+    if (cast_arr(&l, p->cmp_dtype, &lc, err)) {
+        arr_free(&l);
+        return err->status;
+    }
+    arr_free(&l);
+    if (operand_arr(p->rhs_operand, p->rhs_bits, p->cmp_dtype, x, &r, err)) {
+        arr_free(&lc);
+        return err->status;
+    }
+    unsigned char *mask = (unsigned char *)malloc((size_t)(x->n > 0 ? x->n : 1));
+    for (int64_t i = 0; i < x->n; ++i) mask[i] = (unsigned char)cmp1(p->cmp, p->cmp_dtype, lc.v[i], r.v[i]);
+    arr_free(&lc);
+    arr_free(&r);
+    int64_t k = 0;
+    for (int64_t i = 0; i < x->n; ++i) k += mask[i];
+    *out = arr_new(k, x->dtype);
+    k = 0;
+    for (int64_t i = 0; i < x->n; ++i)
+        if (mask[i]) out->v[k++] = x->v[i];
+    free(mask);
+    return 0;
+}
+
+/* ------------------------------------------------------------------ */
+/* DataValue state machine                                              */
+/* ------------------------------------------------------------------ */
+
+/* data_value_arithmetic_op(Add, state, delta) (data_value_arithmetic.rs:10-27):
+ * Null absorbs; otherwise both sides go through to_array(1), which fails on
+ * X(None) with "DataValue to array cannot be NONE NULL". */
+static int state_add(fqo_state *s, fqo_state d, err_t *err) {
+    if (s->kind == FQO_NULL) {
+        *s = d;
+        return 0;
+    }
+    if (d.kind == FQO_NULL) return 0;
+    if (s->kind == FQO_NONE || d.kind == FQO_NONE)
+        return set_err(err, FQ_E_INTERNAL, "Internal Error: DataValue to array cannot be NONE NULL");
+    if (s->dtype == FQ_DT_FLOAT64) s->bits = of_f(as_f(s->bits) + as_f(d.bits));
+    else s->bits = s->bits + d.bits; /* release-build wrap */
+    return 0;
+}
+
+/* data_value_aggregate_op(Min|Max, state, delta) (data_value_aggregate.rs:8-101 +
+ * typed_data_value_min_max, macros.rs:179-188): None-aware, uses Ord/f64::min. */
+static void state_minmax(fqo_state *s, fqo_state d, int is_max) {
+    if (s->kind == FQO_NULL) {
+        *s = d;
+        return;
+    }
+    if (d.kind == FQO_NULL || d.kind == FQO_NONE) return;
+    if (s->kind == FQO_NONE) {
+        *s = d;
+        return;
+    }
+    const uint64_t a = s->bits, b = d.bits;
+    int take_b;
+    if (s->dtype == FQ_DT_FLOAT64) {
+        const double x = as_f(a), y = as_f(b);
+        if (x != x) take_b = 1;       /* f64::max/min ignore NaN */
+        else if (y != y) take_b = 0;
+        else take_b = is_max ? y > x : y < x;
+    } else if (s->dtype == FQ_DT_INT64) {
+        take_b = is_max ? (int64_t)b > (int64_t)a : (int64_t)b < (int64_t)a;
+    } else {
+        take_b = is_max ? b > a : b < a;
+    }
+    if (take_b) s->bits = b;
+}
+
+/* data_array_aggregate_op (data_array_aggregate.rs:14-163) over one block. */
+static fqo_state block_agg(int32_t op, const arr_t *v) {
+    fqo_state r;
+    r.dtype = v->dtype;
+    r.bits = 0;
+    if (v->n == 0) { /* arrow returns None when null_count == len */
+        r.kind = FQO_NONE;
+        return r;
+    }
+    r.kind = FQO_SOME;
+    if (op == FQ_AGG_SUM) {
+        if (v->dtype == FQ_DT_FLOAT64) {
+            double s = 0;
+            for (int64_t i = 0; i < v->n; ++i) s += as_f(v->v[i]);
+            r.bits = of_f(s);
+        } else {
+            uint64_t s = 0;
+            for (int64_t i = 0; i < v->n; ++i) s += v->v[i];
+            r.bits = s;
+        }
+        return r;
+    }
+    /* min_max_helper: n = fold(m[0], |n, item| if cmp(n, item) {item} else {n}) */
+    uint64_t n = v->v[0];
+    for (int64_t i = 1; i < v->n; ++i) {
+        const uint64_t it = v->v[i];
+        int take;
+        if (v->dtype == FQ_DT_FLOAT64) take = op == FQ_AGG_MAX ? as_f(n) < as_f(it) : as_f(n) > as_f(it);
+        else if (v->dtype == FQ_DT_INT64) take = op == FQ_AGG_MAX ? (int64_t)n < (int64_t)it : (int64_t)n > (int64_t)it;
+        else take = op == FQ_AGG_MAX ? n < it : n > it;
+        if (take) n = it;
+    }
+    r.bits = n;
+    return r;
+}
+
+/* ------------------------------------------------------------------ */
+/* AggregatePartialTransform over one block stream                      */
+/* ------------------------------------------------------------------ */
+typedef struct {
+    int32_t src, col_dtype;
+    uint64_t seed;
+    const void *host_col; /* for fqo_column_partial */
+    const fq_pred *pred;
+    int32_t n_aggs;
+    const int32_t *agg_ops;
+    const fq_expr *agg_args;
+    fqo_state *states; /* [n_aggs] */
+    err_t err;
+} task_t;
+
+/* one block: materialise (numbers_stream.rs:76), filter, accumulate every func */
+static int process_block(task_t *t, const arr_t *blk) {
+    arr_t filtered;
+    const arr_t *x = blk;
+    if (t->pred && t->pred->kind == FQ_PRED_EXPR) {
+        if (filter_block(t->pred, blk, &filtered, &t->err)) return t->err.status;
+        x = &filtered;
+    }
+    for (int a = 0; a < t->n_aggs; ++a) {
+        arr_t val;
+        /* AggregatorFunction::accumulate: val = arg.eval(block) for every op */
+        if (eval_chain(&t->agg_args[a], x, &val, &t->err)) break;
+        const int32_t op = t->agg_ops[a];
+        if (op == FQ_AGG_COUNT) {
+            fqo_state d = {FQO_SOME, FQ_DT_UINT64, (uint64_t)x->n};
+            state_add(&t->states[a], d, &t->err);
+        } else if (op == FQ_AGG_SUM) {
+            state_add(&t->states[a], block_agg(op, &val), &t->err);
+        } else {
+            state_minmax(&t->states[a], block_agg(op, &val), op == FQ_AGG_MAX);
+        }
+        arr_free(&val);
+        if (t->err.status) break;
+    }
+    if (x == &filtered) arr_free(&filtered);
+    return t->err.status;
+}
+
+static int numbers_block_fn(void *ctx, uint64_t b, uint64_t e) {
+    task_t *t = (task_t *)ctx;
+    arr_t blk = arr_new((int64_t)(e - b + 1), FQ_DT_UINT64);
+    for (uint64_t i = b; i <= e; ++i)
+        blk.v[i - b] = t->src == FQO_SRC_SPLITMIX ? fqo_splitmix64(t->seed, i) : i;
+    int rc = process_block(t, &blk);
+    arr_free(&blk);
+    return rc;
+}
+
+typedef struct {
+    task_t task;
+    uint64_t total;
+    int32_t part;
+} part_job_t;
+
+static void *part_thread(void *arg) {
+    part_job_t *j = (part_job_t *)arg;
+    uint64_t b, e;
+    fqo_partition_range(j->total, j->part, &b, &e);
+    numbers_blocks(b, e, numbers_block_fn, &j->task);
+    return NULL;
+}
+
+static void init_states(fqo_state *s, int n) {
+    for (int i = 0; i < n; ++i) {
+        s[i].kind = FQO_NULL;
+        s[i].dtype = FQ_DT_NULL;
+        s[i].bits = 0;
+    }
+}
+
+int32_t fqo_numbers_partial(uint64_t total, int32_t src, uint64_t seed, int32_t p0, int32_t p1,
+                            const fq_pred *pred, int32_t n_aggs, const int32_t *agg_ops,
+                            const fq_expr *agg_args, int32_t n_threads, fqo_state *out_states,
+                            int32_t *part_status, char *errbuf, int32_t errlen) {
+    const int32_t np = p1 - p0;
+    if (np <= 0) return 0;
+    part_job_t *jobs = (part_job_t *)calloc((size_t)np, sizeof(part_job_t));
+    for (int32_t i = 0; i < np; ++i) {
+        jobs[i].total = total;
+        jobs[i].part = p0 + i;
+        jobs[i].task.src = src;
+        jobs[i].task.col_dtype = FQ_DT_UINT64;
+        jobs[i].task.seed = seed;
+        jobs[i].task.pred = pred;
+        jobs[i].task.n_aggs = n_aggs;
+        jobs[i].task.agg_ops = agg_ops;
+        jobs[i].task.agg_args = agg_args;
+        jobs[i].task.states = out_states + (size_t)i * n_aggs;
+        init_states(jobs[i].task.states, n_aggs);
+    }
+    if (n_threads <= 0 || n_threads > np) n_threads = np;
+    /* waves of n_threads threads, partition order (one tokio task per source) */
+    pthread_t *th = (pthread_t *)calloc((size_t)n_threads, sizeof(pthread_t));
+    for (int32_t w = 0; w < np; w += n_threads) {
+        const int32_t k = (np - w) < n_threads ? (np - w) : n_threads;
+        for (int32_t i = 0; i < k; ++i) pthread_create(&th[i], NULL, part_thread, &jobs[w + i]);
+        for (int32_t i = 0; i < k; ++i) pthread_join(th[i], NULL);
+    }
+    free(th);
+    int32_t rc = 0;
+    for (int32_t i = 0; i < np; ++i) {
+        part_status[i] = jobs[i].task.err.status;
+        if (jobs[i].task.err.status && !rc) {
+            rc = jobs[i].task.err.status;
+            if (errbuf && errlen > 0) snprintf(errbuf, (size_t)errlen, "%s", jobs[i].task.err.msg);
+        }
+    }
+    free(jobs);
+    return rc;
+}
+
+int32_t fqo_column_partial(const void *col, int32_t col_dtype, int64_t len, int64_t block_rows,
+                           const fq_pred *pred, int32_t n_aggs, const int32_t *agg_ops,
+                           const fq_expr *agg_args, fqo_state *out_states, char *errbuf,
+                           int32_t errlen) {
+    task_t t;
+    memset(&t, 0, sizeof(t));
+    t.col_dtype = col_dtype;
+    t.host_col = col;
+    t.pred = pred;
+    t.n_aggs = n_aggs;
+    t.agg_ops = agg_ops;
+    t.agg_args = agg_args;
+    t.states = out_states;
+    init_states(out_states, n_aggs);
+    if (block_rows <= 0) block_rows = len > 0 ? len : 1;
+    const uint64_t *c = (const uint64_t *)col;
+    for (int64_t s = 0; s < len; s += block_rows) {
+        const int64_t n = (s + block_rows < len) ? block_rows : len - s;
+        arr_t blk = arr_new(n, col_dtype);
+        memcpy(blk.v, c + s, (size_t)n * 8);
+        const int rc = process_block(&t, &blk);
+        arr_free(&blk);
+        if (rc) break;
+    }
+    if (t.err.status && errbuf && errlen > 0) snprintf(errbuf, (size_t)errlen, "%s", t.err.msg);
+    return t.err.status;
+}

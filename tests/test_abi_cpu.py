@@ -1,0 +1,99 @@
+"""CPU-only checks of the boundary: the C-ABI library loads, exports every
+symbol include/*.h declares, and its host-only entry points (state merge,
+coercion, error text) behave; no kernel is launched here."""
+import ctypes as C
+import os
+import re
+
+import pytest
+
+from fq_amd import abi
+from fq_amd._lib import GPU_SYMBOLS, LIB_PATH, lib
+from fq_amd.expr import CoercionError, chain, numerical_coercion, predicate
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols(header):
+    src = open(os.path.join(ROOT, "include", header)).read()
+    return sorted(set(re.findall(r"^\s*(?:[\w\s\*]+?)\b(fq_\w+)\s*\(", src, re.M)))
+
+
+@pytest.mark.parametrize("header", sorted(h for h in os.listdir(os.path.join(ROOT, "include"))
+                                          if h.endswith(".h")))
+def test_library_exports_every_declared_symbol(header):
+    syms = declared_symbols(header)
+    assert syms, header
+    missing = [s for s in syms if not hasattr(lib, s)]
+    assert not missing, missing
+
+
+def test_gpu_symbol_list_matches_header():
+    assert sorted(GPU_SYMBOLS) == declared_symbols("fq_gpu.h")
+
+
+def test_abi_version_and_struct_sizes():
+    assert lib.fq_abi_version() == abi.FQ_ABI_VERSION
+    assert C.sizeof(abi.fq_agg_state) == 48
+    assert C.sizeof(abi.fq_expr) == 8 + 24 * abi.MAX_STEPS
+    assert os.path.exists(LIB_PATH)
+
+
+def test_state_merge_host():
+    s1 = abi.fq_agg_state(10, 4, 1, 4, 1, 0, abi.DT_UINT64)
+    s2 = abi.fq_agg_state(2**64 - 5, 9, 3, 2, 2, 0, abi.DT_UINT64)
+    empty = abi.fq_agg_state(0, 0, 2**64 - 1, 0, 1, abi.STATE_ANY_EMPTY, abi.DT_UINT64)
+    arr = (abi.fq_agg_state * 3)(s1, empty, s2)
+    out = abi.fq_agg_state()
+    assert lib.fq_state_merge(arr, 3, C.byref(out)) == 0
+    assert out.sum == 5 and out.max == 9 and out.min == 1 and out.count == 6
+    assert out.blocks == 4 and out.flags == abi.STATE_ANY_EMPTY
+
+
+def test_state_merge_signed_and_type_mismatch():
+    a = abi.fq_agg_state((-3) & (2**64 - 1), 5, (-3) & (2**64 - 1), 2, 1, 0, abi.DT_INT64)
+    b = abi.fq_agg_state(7, 7, 2, 2, 1, 0, abi.DT_INT64)
+    out = abi.fq_agg_state()
+    assert lib.fq_state_merge((abi.fq_agg_state * 2)(a, b), 2, C.byref(out)) == 0
+    assert out.sum == 4 and out.max == 7 and out.min == (-3) & (2**64 - 1)
+    c = abi.fq_agg_state(1, 1, 1, 1, 1, 0, abi.DT_UINT64)
+    assert lib.fq_state_merge((abi.fq_agg_state * 2)(a, c), 2, C.byref(out)) == abi.FQ_E_INTERNAL
+    assert lib.fq_last_error().decode().startswith("Internal Error: Unsupported data_value_sum")
+
+
+def test_result_type_is_numerical_coercion():
+    out = C.c_int32()
+    cases = [(abi.DT_UINT64, abi.DT_UINT64, abi.DT_UINT64), (abi.DT_UINT64, abi.DT_FLOAT64, abi.DT_FLOAT64),
+             (abi.DT_INT64, abi.DT_INT8, abi.DT_INT64), (abi.DT_UINT64, abi.DT_INT8, abi.DT_INT8),
+             (abi.DT_UINT32, abi.DT_UINT64, abi.DT_UINT64), (abi.DT_FLOAT32, abi.DT_INT64, abi.DT_FLOAT32)]
+    for l, r, exp in cases:
+        assert lib.fq_arith_result_type(abi.OP_ADD, l, r, C.byref(out)) == 0
+        assert out.value == exp == numerical_coercion("+", l, r)
+    assert lib.fq_arith_result_type(abi.OP_ADD, abi.DT_UTF8, abi.DT_UTF8, C.byref(out)) == abi.FQ_E_INTERNAL
+    assert lib.fq_last_error().decode() == "Internal Error: Unsupported (Utf8) + (Utf8)"
+    with pytest.raises(CoercionError, match=r"Unsupported \(Utf8\) / \(Utf8\)"):
+        numerical_coercion("/", abi.DT_UTF8, abi.DT_UTF8)
+
+
+def test_expression_builder_types():
+    e, dt = chain(abi.DT_UINT64, [("+", 1)])
+    assert dt == abi.DT_UINT64 and e.n_steps == 1 and e.steps[0].bits == 1
+    e, dt = chain(abi.DT_UINT64, [("/", 2.0)])
+    assert dt == abi.DT_FLOAT64
+    p = predicate(abi.DT_UINT64, [("%", 8)], "<", 3)
+    assert p.cmp == abi.CMP_LT and p.cmp_dtype == abi.DT_UINT64 and p.rhs_bits == 3
+    p = predicate(abi.DT_UINT64, [], ">", 3, flipped=True)  # 3 > number  ==  number < 3
+    assert p.cmp == abi.CMP_LT
+
+
+def test_no_gpu_calls_fail_loudly_without_device():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible")
+    n = C.c_int32(-1)
+    st = lib.fq_device_count(C.byref(n))
+    assert st != 0 or n.value == 0
+    from fq_amd import ops
+    from fq_amd._lib import FQError
+    with pytest.raises(FQError):
+        ops.require_gpu()

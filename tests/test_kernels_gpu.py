@@ -1,0 +1,213 @@
+"""Parity of the gfx950 kernels (through the C ABI) against the C oracle and
+numpy, on seeded inputs at sizes the oracle finishes in seconds.
+
+Bit-exact for integer results; float sums within the tolerance written in
+each test (reduction order differs from arrow's lane-wise simd sum)."""
+import numpy as np
+import pytest
+
+from fq_amd import abi
+from fq_amd.expr import COL, chain, predicate, to_bits
+
+import oracle_c
+from replay import as_tuple, replay
+
+pytestmark = pytest.mark.gpu
+
+ops = None
+
+
+def setup_module():
+    global ops
+    from fq_amd import ops as _ops
+    _ops.require_gpu()
+    ops = _ops
+
+
+ALL = abi.AGG_SUM | abi.AGG_MAX | abi.AGG_MIN | abi.AGG_COUNT
+AGGS = [abi.AGG_SUM, abi.AGG_MAX, abi.AGG_MIN, abi.AGG_COUNT]
+
+
+def check_against_oracle(host, dtype, block_rows, pred=None, value=None, gpu_col=None):
+    """One device block vs the oracle's per-block loop over the same column."""
+    col = gpu_col if gpu_col is not None else ops.from_numpy(host, dtype)
+    aggs = [(op, value) for op in AGGS]
+    try:
+        exp = [as_tuple(s) for s in oracle_c.column_partial(host, dtype, block_rows, aggs, pred)]
+        exp_err = None
+    except oracle_c.OracleError as e:
+        exp, exp_err = None, e
+    st = ops.aggregate(col, block_rows, pred, value, ALL)
+    if exp_err is not None:
+        with pytest.raises(oracle_c.OracleError) as ei:
+            for op in AGGS:
+                replay(op, st)
+        assert str(ei.value) == str(exp_err)
+        return st
+    got = [replay(op, st) for op in AGGS]
+    assert got == exp, (got, exp, ops.state_values(st))
+    return st
+
+
+def test_fill_numbers_matches_numbers_stream():
+    for begin, n in [(0, 1), (5, 17), (1_250_000_000, 100_003), (2**40, 4097)]:
+        c = ops.numbers_column(begin, n)
+        assert np.array_equal(c.to_numpy(), np.arange(begin, begin + n, dtype=np.uint64))
+
+
+def test_fill_splitmix_matches_oracle():
+    c = ops.splitmix_column(0x5EED, 123, 1000)
+    L = oracle_c.lib()
+    exp = np.array([L.fqo_splitmix64(0x5EED, 123 + i) for i in range(1000)], dtype=np.uint64)
+    assert np.array_equal(c.to_numpy(), exp)
+
+
+@pytest.mark.parametrize("n", [0, 1, 2, 3, 7, 16, 63, 64, 65, 1000, 10000, 10001, 123457, 1 << 20])
+def test_identity_u64_all_aggs(n):
+    host = np.random.default_rng(n).integers(0, 2**64, size=n, dtype=np.uint64)
+    st = check_against_oracle(host, abi.DT_UINT64, 10000)
+    if n:
+        assert st.sum == int(host.sum(dtype=np.uint64))  # numpy wraps mod 2^64
+        assert st.max == int(host.max()) and st.min == int(host.min()) and st.count == n
+
+
+def test_misaligned_column_head_and_tail():
+    host = np.arange(1, 1 + 100_003, dtype=np.uint64) * np.uint64(7919)
+    base = ops.from_numpy(np.concatenate([np.zeros(1, np.uint64), host]))
+    col = ops.DeviceColumn(base.buf, host.shape[0], abi.DT_UINT64, offset=8)  # 8-byte aligned only
+    check_against_oracle(host, abi.DT_UINT64, 10000, gpu_col=col)
+
+
+@pytest.mark.parametrize("dt,npdt", [(abi.DT_INT64, np.int64), (abi.DT_INT32, np.int32),
+                                     (abi.DT_UINT8, np.uint8), (abi.DT_INT16, np.int16),
+                                     (abi.DT_UINT32, np.uint32)])
+def test_identity_small_and_signed_types(dt, npdt):
+    rng = np.random.default_rng(7)
+    info = np.iinfo(npdt)
+    host = rng.integers(info.min, info.max, size=50_001, dtype=npdt, endpoint=True)
+    st = ops.aggregate(ops.from_numpy(host, dt), 0, None, None, ALL)
+    v = ops.state_values(st)
+    # arrow sum on T wraps in T (simd add); compare modulo the width
+    mod = 1 << (8 * host.dtype.itemsize)
+    assert (v["sum"] - int(host.astype(object).sum())) % mod == 0
+    assert v["max"] == int(host.max()) and v["min"] == int(host.min()) and v["count"] == host.shape[0]
+
+
+def test_f64_sum_tolerance_minmax_exact():
+    rng = np.random.default_rng(11)
+    host = rng.standard_normal(1_000_003) * 1e3
+    st = ops.aggregate(ops.from_numpy(host), 0, None, None, ALL)
+    v = ops.state_values(st)
+    exp = float(np.sum(host.astype(np.float64)))
+    # tolerance: |err| <= 1e-12 * sum(|x|) (order-of-summation bound, n ~ 1e6)
+    assert abs(v["sum"] - exp) <= 1e-12 * float(np.abs(host).sum())
+    assert v["max"] == float(host.max()) and v["min"] == float(host.min())
+
+
+def test_numbers_plus_one_with_mod_predicate():
+    # C4 shape: max(number+1) WHERE (number%8)<3 over one numbers_mt partition
+    n = 250_000
+    host = np.arange(1_000_000, 1_000_000 + n, dtype=np.uint64)
+    value, _ = chain(abi.DT_UINT64, [("+", 1)])
+    pred = predicate(abi.DT_UINT64, [("%", 8)], "<", 3)
+    check_against_oracle(host, abi.DT_UINT64, 10000, pred=pred, value=value)
+
+
+@pytest.mark.parametrize("d", [1, 2, 3, 7, 8, 10, 1000, 1 << 33, (1 << 63) + 1, 2**64 - 1, 0x1234567890abcdef])
+def test_div_mod_by_constant_magic(d):
+    rng = np.random.default_rng(d & 0xffff)
+    host = rng.integers(0, 2**64, size=70_001, dtype=np.uint64)
+    host[:4] = [0, 1, d - 1 if d > 1 else 0, 2**64 - 1]
+    for sym, ref in (("/", host // np.uint64(d)), ("%", host % np.uint64(d))):
+        value, _ = chain(abi.DT_UINT64, [(sym, d)])
+        st = ops.aggregate(ops.from_numpy(host), 0, None, value, ALL)
+        assert st.flags == 0
+        assert st.sum == int(ref.sum(dtype=np.uint64)), sym
+        assert st.max == int(ref.max()) and st.min == int(ref.min()), sym
+
+
+def test_div_by_zero_constant_and_column():
+    host = np.arange(0, 20_000, dtype=np.uint64)
+    value, _ = chain(abi.DT_UINT64, [("/", 0)])
+    check_against_oracle(host, abi.DT_UINT64, 10000, value=value)  # error path
+    value2, _ = chain(abi.DT_UINT64, [("/", 7, True)])  # 7 / number: zero at row 0
+    check_against_oracle(host, abi.DT_UINT64, 10000, value=value2)
+    # zero divisor only in rows the predicate drops -> no error (eval on filtered block)
+    pred = predicate(abi.DT_UINT64, [], ">", 0)
+    check_against_oracle(host, abi.DT_UINT64, 10000, pred=pred, value=value2)
+
+
+def test_filtered_sum_empty_block_semantics():
+    host = np.arange(0, 50_000, dtype=np.uint64)
+    value, _ = chain(abi.DT_UINT64, [])
+    # only the first block has rows with number < 5 -> later blocks empty -> Sum errors
+    pred = predicate(abi.DT_UINT64, [], "<", 5)
+    st = check_against_oracle(host, abi.DT_UINT64, 10000, pred=pred)
+    assert st.flags & abi.STATE_ANY_EMPTY
+    # every block keeps rows -> fine
+    pred2 = predicate(abi.DT_UINT64, [("%", 10)], "=", 3)
+    check_against_oracle(host, abi.DT_UINT64, 10000, pred=pred2)
+    # single block, nothing passes -> Sum state None, Min/Max None
+    pred3 = predicate(abi.DT_UINT64, [], ">", 10**12)
+    check_against_oracle(host[:7000], abi.DT_UINT64, 10000, pred=pred3)
+
+
+def test_mixed_types_chain_f64_and_i64():
+    host = np.arange(0, 30_000, dtype=np.uint64)
+    v1, _ = chain(abi.DT_UINT64, [("*", 3), ("/", 2.0)])  # u64 * u64 -> / f64 -> Float64
+    st = ops.aggregate(ops.from_numpy(host), 10000, None, v1, ALL)
+    ref = host.astype(np.float64) * 3 / 2.0
+    v = ops.state_values(st)
+    assert v["dtype"] == abi.DT_FLOAT64
+    assert abs(v["sum"] - ref.sum()) <= 1e-12 * abs(ref).sum()
+    assert v["max"] == ref.max() and v["min"] == ref.min()
+    v2, _ = chain(abi.DT_UINT64, [("-", (5000, "Int64"))])  # UInt64 - Int64 -> Int64
+    check_against_oracle(host, abi.DT_UINT64, 10000, value=v2)
+
+
+def test_random_column_matches_oracle_loop():
+    seed, n = 0x5EED, 300_000
+    col = ops.splitmix_column(seed, 0, n)
+    host = col.to_numpy()
+    value, _ = chain(abi.DT_UINT64, [("%", 1000003), ("*", 13)])
+    pred = predicate(abi.DT_UINT64, [("%", 8)], "<", 3)
+    check_against_oracle(host, abi.DT_UINT64, 10000, pred=pred, value=value, gpu_col=col)
+
+
+def test_arith_compare_filter_elementwise():
+    rng = np.random.default_rng(3)
+    a = rng.integers(0, 2**64, size=10_007, dtype=np.uint64)
+    b = rng.integers(1, 2**20, size=10_007, dtype=np.uint64)
+    A, B = ops.from_numpy(a), ops.from_numpy(b)
+    assert np.array_equal(ops.arith("+", A, B).to_numpy(), a + b)
+    assert np.array_equal(ops.arith("-", A, B).to_numpy(), a - b)
+    assert np.array_equal(ops.arith("*", A, B).to_numpy(), a * b)
+    assert np.array_equal(ops.arith("/", A, B).to_numpy(), a // b)
+    assert np.array_equal(ops.arith("%", A, B).to_numpy(), a % b)
+    assert np.array_equal(ops.arith("-", 1, B).to_numpy(), np.uint64(1) - b)
+    m = ops.compare("<", B, 1000)
+    assert np.array_equal(m.to_numpy(), b < 1000)
+    m2 = ops.compare(">", 1000, B)  # scalar-array: flipped operator
+    assert np.array_equal(m2.to_numpy(), b < 1000)
+    kept = ops.filter_compact(A, m)
+    assert np.array_equal(kept.to_numpy(), a[b < 1000])
+
+
+def test_arith_div_zero_error_text():
+    A = ops.from_numpy(np.array([4, 3, 2, 1], np.uint64))
+    Z = ops.from_numpy(np.array([1, 0, 3, 4], np.uint64))
+    with pytest.raises(ops.FQError) as ei:
+        ops.arith("/", A, Z)
+    assert str(ei.value) == "Internal Error: Divide by zero error"
+    assert ei.value.status == abi.FQ_E_DIVIDE_BY_ZERO
+
+
+def test_filter_compaction_large_ragged():
+    n = 3 * 16384 + 77
+    rng = np.random.default_rng(9)
+    x = rng.integers(0, 2**64, size=n, dtype=np.uint64)
+    X = ops.from_numpy(x)
+    for thr in (0, 2**62, 2**63, 2**64 - 1):
+        m = ops.compare("<", X, (thr, "UInt64"))
+        kept = ops.filter_compact(X, m)
+        assert np.array_equal(kept.to_numpy(), x[x < np.uint64(thr)])
