@@ -30,6 +30,14 @@ class FQError(RuntimeError):
 
 
 def _load():
+    # torch ships its own libamdhip64.so (SONAME libamdhip64.so.7).  Load it
+    # first so libfq_amd.so binds to the SAME HIP runtime as the tensors we are
+    # handed; loading /opt/rocm's copy first gives the process two runtimes
+    # and the second one reports hipErrorNoDevice.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(LIB_PATH):
         raise ImportError("fq_amd: %s is missing; run `make -C fuse-query_amd` "
                           "(or __graft_entry__.build())" % LIB_PATH)
