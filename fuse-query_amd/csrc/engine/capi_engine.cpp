@@ -1,0 +1,309 @@
+// C ABI of the engine (include/fq_engine.h).
+#include <string.h>
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../fq_common.h"
+#include "core.h"
+#include "fq_engine.h"
+#include "pipeline.h"
+#include "planner.h"
+
+struct fq_result {
+    std::vector<std::string> names;
+    std::vector<int32_t> types;
+    std::vector<std::vector<fq::DataValue>> cols;
+    int64_t rows = 0;
+    mutable std::vector<std::string> text;  // fq_result_text storage
+};
+
+struct fq_engine {
+    std::unique_ptr<fq::Runtime> rt;
+    std::shared_ptr<fq::DataSource> ds;
+    size_t worker_threads = 8;
+    bool modulo = true;
+};
+
+namespace {
+
+template <typename F>
+fq_status guard(F &&f) {
+    try {
+        f();
+        return FQ_OK;
+    } catch (const fq::FQException &e) {
+        return fqc::fail(e.status, e.msg);
+    } catch (const std::exception &e) {
+        return fqc::internal(e.what());
+    } catch (...) {
+        return fqc::internal("unknown exception");
+    }
+}
+
+fq::QueryContextRef make_ctx(fq_engine *e, int rank, int world) {
+    auto c = std::make_shared<fq::QueryContext>();
+    c->worker_threads = e->worker_threads;
+    c->datasource = e->ds;
+    c->factory.modulo = e->modulo;
+    c->rt = e->rt.get();
+    c->rank = rank;
+    c->world = world;
+    return c;
+}
+
+void append_block(fq_result *r, const fq::DataBlock &b0, fq::ExecCtx &ctx) {
+    fq::DataBlock b = fq::materialize(b0, ctx);
+    if (r->names.empty()) {
+        for (const auto &f : b.schema->fields) {
+            r->names.push_back(f.name);
+            r->types.push_back(f.dtype);
+        }
+        r->cols.resize(b.columns.size());
+    }
+    int64_t n = 0;
+    for (size_t c = 0; c < b.columns.size() && c < r->cols.size(); ++c) {
+        std::vector<fq::DataValue> v = b.columns[c].to_host(ctx.stream());
+        if (b.columns[c].dtype == FQ_DT_NULL && v.empty()) v.assign((size_t)b.columns[c].len, fq::DataValue::null());
+        n = std::max<int64_t>(n, (int64_t)v.size());
+        r->cols[c].insert(r->cols[c].end(), v.begin(), v.end());
+    }
+    r->rows += n;
+}
+
+const fq::PlanNode *aggregate_node(const fq::QueryPlan &p) {
+    for (const auto &n : p.nodes)
+        if (n.kind == fq::PlanNode::kAggregate) return &n;
+    return nullptr;
+}
+
+}  // namespace
+
+extern "C" {
+
+fq_status fq_engine_create(int32_t device, fq_engine **out) {
+    if (!out) return fqc::fail(FQ_E_INVALID, "fq_engine_create: out is NULL");
+    *out = nullptr;
+    return guard([&] {
+        auto e = std::make_unique<fq_engine>();
+        e->rt = std::make_unique<fq::Runtime>(device);
+        e->ds = std::make_shared<fq::DataSource>();
+        *out = e.release();
+    });
+}
+
+void fq_engine_destroy(fq_engine *e) {
+    if (!e) return;
+    if (e->ds) e->ds->numbers()->unpin_all();
+    delete e;
+}
+
+fq_status fq_engine_set_option(fq_engine *e, int32_t option, int64_t value) {
+    if (!e) return fqc::fail(FQ_E_INVALID, "fq_engine_set_option: NULL engine");
+    return guard([&] {
+        switch (option) {
+            case FQ_OPT_WORKER_THREADS: e->worker_threads = (size_t)(value < 0 ? 0 : value); break;
+            case FQ_OPT_MODULO: e->modulo = value != 0; break;
+            case FQ_OPT_PROFILE: e->rt->profile = value != 0; break;
+            case FQ_OPT_STREAMS: e->rt->set_streams((int)value); break;
+            default: throw fq::FQException(FQ_E_INVALID, "fq_engine_set_option: unknown option");
+        }
+    });
+}
+
+fq_status fq_engine_materialize_numbers(fq_engine *e, uint64_t total, int32_t rank, int32_t world) {
+    if (!e) return fqc::fail(FQ_E_INVALID, "NULL engine");
+    if (world < 1 || rank < 0 || rank >= world) return fqc::fail(FQ_E_INVALID, "bad rank/world");
+    return guard([&] {
+        fq::ExecCtx ctx(e->rt.get());
+        auto parts = fq::NumbersTable::generate_parts(total);
+        const size_t np = parts.size();
+        const size_t lo = np * (size_t)rank / (size_t)world, hi = np * (size_t)(rank + 1) / (size_t)world;
+        for (size_t i = lo; i < hi; ++i) {
+            uint64_t t, b, en;
+            fq::NumbersTable::parse_part(parts[i].name, t, b, en);
+            if (en < b) throw fq::FQException(FQ_E_UNSUPPORTED, "numbers_mt(0) is not supported");
+            const uint64_t rows = fq::NumbersTable::stream_rows(b, en);
+            fq::Column c;
+            c.dtype = FQ_DT_UINT64;
+            c.len = (int64_t)rows;
+            c.dev = fq::DeviceBuffer::alloc_sync(rows * 8);
+            fq::check_fq(fq_fill_numbers_u64((uint64_t *)c.dptr(), b, rows, ctx.stream()));
+            ctx.sync();
+            e->ds->numbers()->pin(parts[i].name, c);
+        }
+    });
+}
+
+fq_status fq_engine_release_numbers(fq_engine *e) {
+    if (!e) return fqc::fail(FQ_E_INVALID, "NULL engine");
+    return guard([&] { e->ds->numbers()->unpin_all(); });
+}
+
+fq_status fq_engine_execute(fq_engine *e, const char *sql, fq_result **out) {
+    if (!e || !sql || !out) return fqc::fail(FQ_E_INVALID, "fq_engine_execute: NULL argument");
+    *out = nullptr;
+    return guard([&] {
+        fq::ExecCtx ctx(e->rt.get());
+        auto qctx = make_ctx(e, 0, 1);
+        fq::QueryPlan plan = fq::build_from_sql(sql, *qctx);
+        auto r = std::make_unique<fq_result>();
+        if (plan.explain) {  // ExplainExecutor (executor_explain.rs:38-59)
+            fq::Pipeline p = fq::build_pipeline(plan, qctx);
+            r->names = {"explain"};
+            r->types = {FQ_DT_UTF8};
+            r->cols.resize(1);
+            r->cols[0].push_back(fq::DataValue::string(plan.display()));
+            r->cols[0].push_back(fq::DataValue::string(p.display()));
+            r->rows = 2;
+        } else {
+            fq::Pipeline p = fq::build_pipeline(plan, qctx);
+            fq::StreamRef s = p.execute();
+            fq::DataBlock b;
+            while (s->next(b)) append_block(r.get(), b, ctx);
+            if (r->names.empty())
+                for (const auto &f : plan.nodes.back().schema->fields) {
+                    r->names.push_back(f.name);
+                    r->types.push_back(f.dtype);
+                    r->cols.emplace_back();
+                }
+        }
+        e->rt->stats.queries++;
+        *out = r.release();
+    });
+}
+
+fq_status fq_engine_explain(fq_engine *e, const char *sql, char *buf, size_t cap, size_t *len) {
+    if (!e || !sql) return fqc::fail(FQ_E_INVALID, "fq_engine_explain: NULL argument");
+    return guard([&] {
+        fq::ExecCtx ctx(e->rt.get());
+        auto qctx = make_ctx(e, 0, 1);
+        fq::QueryPlan plan = fq::build_from_sql(sql, *qctx);
+        fq::Pipeline p = fq::build_pipeline(plan, qctx);
+        const std::string s = plan.display() + "\n" + p.display();
+        if (len) *len = s.size();
+        if (buf && cap) {
+            const size_t n = std::min(cap - 1, s.size());
+            memcpy(buf, s.data(), n);
+            buf[n] = 0;
+        }
+    });
+}
+
+fq_status fq_engine_execute_partial(fq_engine *e, const char *sql, int32_t rank, int32_t world, void *buf,
+                                    size_t cap, size_t *len) {
+    if (!e || !sql || !len) return fqc::fail(FQ_E_INVALID, "fq_engine_execute_partial: NULL argument");
+    if (world < 1 || rank < 0 || rank >= world) return fqc::fail(FQ_E_INVALID, "bad rank/world");
+    return guard([&] {
+        fq::ExecCtx ctx(e->rt.get());
+        auto qctx = make_ctx(e, rank, world);
+        fq::QueryPlan plan = fq::build_from_sql(sql, *qctx);
+        if (plan.explain || !aggregate_node(plan))
+            throw fq::FQException(FQ_E_UNSUPPORTED, "distributed execution covers aggregate queries only");
+        fq::QueryPlan partial = plan;
+        while (!partial.nodes.empty() && partial.nodes.back().kind == fq::PlanNode::kLimit) partial.nodes.pop_back();
+        fq::Pipeline p = fq::build_pipeline(partial, qctx, /*emit_states=*/true);
+        fq::StreamRef s = p.execute();
+        fq::DataBlock b;
+        std::vector<std::vector<fq::DataValue>> per_func;
+        while (s->next(b)) {
+            const auto &rows = *b.columns.at(0).host;
+            for (const auto &v : rows) per_func.push_back(v.fields);
+        }
+        const std::vector<uint8_t> enc = fq::encode_states(per_func);
+        *len = enc.size();
+        if (!buf || cap < enc.size())
+            throw fq::FQException(FQ_E_INVALID, "fq_engine_execute_partial: buffer too small (need " +
+                                                    std::to_string(enc.size()) + " bytes)");
+        memcpy(buf, enc.data(), enc.size());
+        e->rt->stats.queries++;
+    });
+}
+
+fq_status fq_engine_execute_final(fq_engine *e, const char *sql, const void *states, size_t stride, int32_t world,
+                                  fq_result **out) {
+    if (!e || !sql || !states || !out || world < 1) return fqc::fail(FQ_E_INVALID, "fq_engine_execute_final: bad argument");
+    *out = nullptr;
+    return guard([&] {
+        fq::ExecCtx ctx(e->rt.get());
+        auto qctx = make_ctx(e, 0, 1);
+        fq::QueryPlan plan = fq::build_from_sql(sql, *qctx);
+        const fq::PlanNode *agg = aggregate_node(plan);
+        if (plan.explain || !agg) throw fq::FQException(FQ_E_UNSUPPORTED, "distributed execution covers aggregate queries only");
+        std::vector<fq::DataBlock> blocks;
+        for (int32_t r = 0; r < world; ++r) {
+            auto per_func = fq::decode_states((const uint8_t *)states + (size_t)r * stride, stride);
+            std::vector<fq::DataValue> rows;
+            for (auto &v : per_func) rows.push_back(fq::DataValue::make_struct(std::move(v)));
+            fq::DataBlock b;
+            b.schema = agg->schema;
+            b.columns.push_back(fq::Column::host_values(FQ_DT_NULL, std::move(rows)));
+            blocks.push_back(std::move(b));
+        }
+        fq::Pipeline p;
+        p.add_source(std::make_shared<fq::BlocksProcessor>(blocks));
+        p.add_simple_transform([&]() {
+            std::vector<fq::FunctionRef> fs;
+            for (const auto &x : agg->exprs) fs.push_back(x.to_function(qctx->factory));
+            return std::make_shared<fq::AggregateFinalTransform>(agg->schema, fs);
+        });
+        for (const auto &n : plan.nodes)
+            if (n.kind == fq::PlanNode::kLimit) {
+                const size_t lim = n.limit;
+                p.add_simple_transform([lim]() { return std::make_shared<fq::LimitTransform>(lim); });
+            }
+        auto r = std::make_unique<fq_result>();
+        fq::StreamRef s = p.execute();
+        fq::DataBlock b;
+        while (s->next(b)) append_block(r.get(), b, ctx);
+        *out = r.release();
+    });
+}
+
+fq_status fq_engine_get_stats(fq_engine *e, fq_engine_stats *out) {
+    if (!e || !out) return fqc::fail(FQ_E_INVALID, "NULL argument");
+    out->scan_launches = e->rt->stats.scan_launches.load();
+    out->scan_rows = e->rt->stats.scan_rows.load();
+    out->scan_bytes = e->rt->stats.scan_bytes.load();
+    out->scan_ms = (double)e->rt->stats.scan_ns.load() * 1e-6;
+    out->queries = e->rt->stats.queries.load();
+    return FQ_OK;
+}
+
+fq_status fq_engine_reset_stats(fq_engine *e) {
+    if (!e) return fqc::fail(FQ_E_INVALID, "NULL engine");
+    e->rt->stats.scan_launches = 0;
+    e->rt->stats.scan_rows = 0;
+    e->rt->stats.scan_bytes = 0;
+    e->rt->stats.scan_ns = 0;
+    e->rt->stats.queries = 0;
+    return FQ_OK;
+}
+
+int64_t fq_result_num_rows(const fq_result *r) { return r ? r->rows : 0; }
+int32_t fq_result_num_columns(const fq_result *r) { return r ? (int32_t)r->names.size() : 0; }
+const char *fq_result_column_name(const fq_result *r, int32_t col) {
+    if (!r || col < 0 || col >= (int32_t)r->names.size()) return nullptr;
+    return r->names[(size_t)col].c_str();
+}
+int32_t fq_result_column_type(const fq_result *r, int32_t col) {
+    if (!r || col < 0 || col >= (int32_t)r->types.size()) return -1;
+    return r->types[(size_t)col];
+}
+fq_status fq_result_value(const fq_result *r, int64_t row, int32_t col, fq_value *out) {
+    if (!r || !out || col < 0 || col >= (int32_t)r->cols.size() || row < 0 ||
+        row >= (int64_t)r->cols[(size_t)col].size())
+        return fqc::fail(FQ_E_INVALID, "fq_result_value: out of range");
+    *out = r->cols[(size_t)col][(size_t)row].to_abi();
+    return FQ_OK;
+}
+const char *fq_result_text(const fq_result *r, int64_t row, int32_t col) {
+    if (!r || col < 0 || col >= (int32_t)r->cols.size() || row < 0 || row >= (int64_t)r->cols[(size_t)col].size())
+        return nullptr;
+    r->text.push_back(r->cols[(size_t)col][(size_t)row].debug());
+    return r->text.back().c_str();
+}
+void fq_result_free(fq_result *r) { delete r; }
+
+}  // extern "C"

@@ -1,0 +1,501 @@
+// DataValue semantics, schema, device runtime and columns of the engine.
+#include "core.h"
+
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "../fq_common.h"
+
+namespace fq {
+
+// ---------------------------------------------------------------------------
+// errors / dtypes
+// ---------------------------------------------------------------------------
+void throw_internal(const std::string &m) { throw FQException(FQ_E_INTERNAL, "Internal Error: " + m); }
+void throw_plan(const std::string &m) { throw FQException(FQ_E_PLAN, "Error during plan: " + m); }
+void throw_status(fq_status st, const std::string &m) { throw FQException(st, m); }
+void check_fq(fq_status st) {
+    if (st != FQ_OK) throw FQException(st, fq_last_error());
+}
+void check_hip(hipError_t e, const char *what) {
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        throw FQException(FQ_E_HIP, std::string("HIP error ") + hipGetErrorName(e) + " (" +
+                                        hipGetErrorString(e) + ") in " + what);
+    }
+}
+
+const char *dtype_name(DataType dt) { return fqc::dtype_name(dt); }
+int dtype_size(DataType dt) { return fqc::dtype_size(dt); }
+bool dtype_is_numeric(DataType dt) { return fqc::dtype_is_numeric(dt); }
+bool dtype_is_float(DataType dt) { return fqc::dtype_is_float(dt); }
+bool dtype_is_signed(DataType dt) { return fqc::dtype_is_signed_int(dt); }
+
+// ---------------------------------------------------------------------------
+// DataValue
+// ---------------------------------------------------------------------------
+DataType DataValue::data_type() const {
+    switch (kind) {
+        case kNull: return FQ_DT_NULL;
+        case kStruct: throw_internal("not implemented: DataValue::Struct data_type");
+        default: return dtype;
+    }
+}
+
+static double bits_f64(uint64_t b) {
+    double d;
+    memcpy(&d, &b, 8);
+    return d;
+}
+static uint64_t f64_bits(double d) {
+    uint64_t b;
+    memcpy(&b, &d, 8);
+    return b;
+}
+
+// Shortest round-trip digits, then positional notation as Rust's Display.
+static std::string format_float(double d, bool is_f32) {
+    if (d != d) return "NaN";
+    if (isinf(d)) return d > 0 ? "inf" : "-inf";
+    if (d == 0) return signbit(d) ? "-0" : "0";
+    char buf[64];
+    int prec = 1;
+    for (; prec <= 17; ++prec) {
+        snprintf(buf, sizeof buf, "%.*e", prec - 1, d);
+        if (is_f32 ? (float)strtod(buf, nullptr) == (float)d : strtod(buf, nullptr) == d) break;
+    }
+    // buf = [-]D.DDDDe[+-]XX
+    std::string s(buf);
+    bool neg = s[0] == '-';
+    if (neg) s = s.substr(1);
+    const size_t epos = s.find('e');
+    std::string mant = s.substr(0, epos);
+    const int exp = atoi(s.c_str() + epos + 1);
+    std::string digits;
+    for (char c : mant)
+        if (c != '.') digits += c;
+    while (digits.size() > 1 && digits.back() == '0') digits.pop_back();
+    std::string out;
+    const int n = (int)digits.size();
+    if (exp < 0) {
+        out = "0." + std::string(-exp - 1, '0') + digits;
+    } else if (exp >= n - 1) {
+        out = digits + std::string(exp - (n - 1), '0');
+    } else {
+        out = digits.substr(0, exp + 1) + "." + digits.substr(exp + 1);
+    }
+    return neg ? "-" + out : out;
+}
+
+std::string format_f64(double d) { return format_float(d, false); }
+
+std::string DataValue::debug() const {
+    switch (kind) {
+        case kNull: return "Null";
+        case kNone: return "NULL";
+        case kStruct: {
+            std::string s = "[";
+            for (size_t i = 0; i < fields.size(); ++i) {
+                if (i) s += ", ";
+                s += fields[i].debug();
+            }
+            return s + "]";
+        }
+        default: break;
+    }
+    if (dtype == FQ_DT_UTF8) return str;
+    if (dtype == FQ_DT_BOOLEAN) return bits ? "true" : "false";
+    if (dtype == FQ_DT_FLOAT64) return format_float(bits_f64(bits), false);
+    if (dtype == FQ_DT_FLOAT32) return format_float(bits_f64(bits), true);
+    if (dtype_is_signed(dtype)) return std::to_string((long long)(int64_t)bits);
+    return std::to_string((unsigned long long)bits);
+}
+
+fq_value DataValue::to_abi() const {
+    fq_value v;
+    v.dtype = kind == kNull ? FQ_DT_NULL : dtype;
+    v.is_some = kind == kSome ? 1 : 0;
+    v.bits = kind == kSome ? bits : 0;
+    return v;
+}
+
+DataValue DataValue::from_abi(const fq_value &v) {
+    if (v.dtype == FQ_DT_NULL) return null();
+    return v.is_some ? some(v.dtype, v.bits) : none(v.dtype);
+}
+
+bool DataValue::operator==(const DataValue &o) const {
+    if (kind != o.kind) return false;
+    if (kind == kNull) return true;
+    if (kind == kStruct) return fields == o.fields;
+    if (dtype != o.dtype) return false;
+    if (kind == kNone) return true;
+    return dtype == FQ_DT_UTF8 ? str == o.str : bits == o.bits;
+}
+
+const char *agg_op_name(uint32_t agg) {
+    switch (agg) {
+        case FQ_AGG_MIN: return "min";
+        case FQ_AGG_MAX: return "max";
+        case FQ_AGG_SUM: return "sum";
+        default: return "count";
+    }
+}
+const char *agg_op_debug_name(uint32_t agg) {
+    switch (agg) {
+        case FQ_AGG_MIN: return "Min";
+        case FQ_AGG_MAX: return "Max";
+        case FQ_AGG_SUM: return "Sum";
+        default: return "Count";
+    }
+}
+
+// wrap an integer result into the width of dt (release-build arithmetic)
+static uint64_t wrap_int(uint64_t v, DataType dt) {
+    const int bits = 8 * dtype_size(dt);
+    if (bits >= 64) return v;
+    const uint64_t m = (1ull << bits) - 1;
+    v &= m;
+    if (dtype_is_signed(dt) && (v >> (bits - 1))) v |= ~m;
+    return v;
+}
+
+static void to_array_check(const DataValue &v) {
+    if (v.kind == DataValue::kNone) throw_internal("DataValue to array cannot be NONE NULL");
+    if (v.kind == DataValue::kStruct) throw_internal("DataValue to array cannot be NONE " + v.debug());
+}
+
+// data_value_arithmetic_op (data_value_arithmetic.rs:10-27): Null absorbs,
+// otherwise both scalars go through to_array(1) + data_array_arithmetic_op.
+DataValue data_value_arithmetic_op(int32_t op, const DataValue &l, const DataValue &r) {
+    if (l.kind == DataValue::kNull) return r;
+    if (r.kind == DataValue::kNull) return l;
+    to_array_check(l);
+    to_array_check(r);
+    int32_t ct = 0;
+    if (fqc::numerical_coercion(fqc::arith_op_str(op), l.dtype, r.dtype, &ct) != FQ_OK)
+        throw FQException(FQ_E_INTERNAL, fq_last_error());
+    uint64_t a = 0, b = 0;
+    if (!fqc::cast_scalar(l.bits, l.dtype, ct, &a) || !fqc::cast_scalar(r.bits, r.dtype, ct, &b))
+        return DataValue::none(ct);  // arrow cast -> null -> op -> null
+    if (dtype_is_float(ct)) {
+        double x = bits_f64(a), y = bits_f64(b), z = 0;
+        if ((op == FQ_OP_DIV || op == FQ_OP_MOD) && y == 0.0)
+            throw FQException(FQ_E_DIVIDE_BY_ZERO, "Internal Error: Divide by zero error");
+        if (ct == FQ_DT_FLOAT32) {
+            const float fx = (float)x, fy = (float)y;
+            float fz = op == FQ_OP_ADD ? fx + fy : op == FQ_OP_SUB ? fx - fy : op == FQ_OP_MUL ? fx * fy
+                       : op == FQ_OP_DIV ? fx / fy : fmodf(fx, fy);
+            z = fz;
+        } else {
+            z = op == FQ_OP_ADD ? x + y : op == FQ_OP_SUB ? x - y : op == FQ_OP_MUL ? x * y
+                : op == FQ_OP_DIV ? x / y : fmod(x, y);
+        }
+        return DataValue::some(ct, f64_bits(z));
+    }
+    uint64_t z = 0;
+    switch (op) {
+        case FQ_OP_ADD: z = a + b; break;
+        case FQ_OP_SUB: z = a - b; break;
+        case FQ_OP_MUL: z = a * b; break;
+        default:
+            if (b == 0) throw FQException(FQ_E_DIVIDE_BY_ZERO, "Internal Error: Divide by zero error");
+            if (dtype_is_signed(ct)) {
+                const int64_t sa = (int64_t)a, sb = (int64_t)b;
+                if (sb == -1) z = op == FQ_OP_DIV ? (uint64_t)0 - a : 0;  // overflow wraps (unpinned)
+                else z = (uint64_t)(op == FQ_OP_DIV ? sa / sb : sa % sb);
+            } else {
+                z = op == FQ_OP_DIV ? a / b : a % b;
+            }
+    }
+    return DataValue::some(ct, wrap_int(z, ct));
+}
+
+static bool lt_bits(DataType dt, uint64_t a, uint64_t b) {
+    if (dtype_is_float(dt)) return bits_f64(a) < bits_f64(b);
+    if (dtype_is_signed(dt)) return (int64_t)a < (int64_t)b;
+    return a < b;
+}
+
+// data_value_aggregate_op (data_value_aggregate.rs:8-101 + macros.rs:168-200)
+DataValue data_value_aggregate_op(uint32_t agg, const DataValue &l, const DataValue &r) {
+    if (l.kind == DataValue::kNull) return r;
+    if (r.kind == DataValue::kNull) return l;
+    auto unsupported = [&]() {
+        throw_internal(std::string("Unsupported data_value_") + agg_op_name(agg) + " for data type: left:" +
+                       dtype_name(l.kind == DataValue::kStruct ? FQ_DT_NULL : l.dtype) + ", right:" +
+                       dtype_name(r.kind == DataValue::kStruct ? FQ_DT_NULL : r.dtype));
+    };
+    if (l.kind == DataValue::kStruct || r.kind == DataValue::kStruct || l.dtype != r.dtype) unsupported();
+    const DataType dt = l.dtype;
+    if (dt == FQ_DT_UTF8) {
+        if (agg != FQ_AGG_MIN && agg != FQ_AGG_MAX) unsupported();
+        if (l.kind == DataValue::kNone) return r;
+        if (r.kind == DataValue::kNone) return l;
+        const bool take_r = agg == FQ_AGG_MAX ? r.str > l.str : r.str < l.str;
+        return take_r ? r : l;
+    }
+    if (!dtype_is_numeric(dt)) unsupported();
+    if (agg == FQ_AGG_COUNT) return DataValue::u64(1);
+    if (l.kind == DataValue::kNone && r.kind == DataValue::kNone) return DataValue::none(dt);
+    if (r.kind == DataValue::kNone) return l;
+    if (l.kind == DataValue::kNone) return r;
+    if (agg == FQ_AGG_SUM) {
+        if (dtype_is_float(dt)) {
+            double z = bits_f64(l.bits) + bits_f64(r.bits);
+            if (dt == FQ_DT_FLOAT32) z = (float)bits_f64(l.bits) + (float)bits_f64(r.bits);
+            return DataValue::some(dt, f64_bits(z));
+        }
+        return DataValue::some(dt, wrap_int(l.bits + r.bits, dt));
+    }
+    // f64::min / f64::max ignore NaN; Ord::min/max for integers
+    if (dtype_is_float(dt)) {
+        const double a = bits_f64(l.bits), b = bits_f64(r.bits);
+        if (a != a) return r;
+        if (b != b) return l;
+    }
+    const bool take_r = agg == FQ_AGG_MAX ? lt_bits(dt, l.bits, r.bits) : lt_bits(dt, r.bits, l.bits);
+    return take_r ? r : l;
+}
+
+// ---------------------------------------------------------------------------
+// schema
+// ---------------------------------------------------------------------------
+int DataSchema::index_of(const std::string &name) const {
+    for (size_t i = 0; i < fields.size(); ++i)
+        if (fields[i].name == name) return (int)i;
+    std::string valid = "[";
+    for (size_t i = 0; i < fields.size(); ++i) {
+        if (i) valid += ", ";
+        valid += "\"" + fields[i].name + "\"";
+    }
+    valid += "]";
+    throw_internal("Invalid argument error: Unable to get field named \"" + name + "\". Valid fields: " + valid);
+}
+
+const DataField &DataSchema::field_with_name(const std::string &name) const { return fields[index_of(name)]; }
+
+// ---------------------------------------------------------------------------
+// runtime
+// ---------------------------------------------------------------------------
+Runtime::Runtime(int device) : device_(device) {
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n <= device || device < 0)
+        throw FQException(FQ_E_HIP, "fq_engine: no HIP device " + std::to_string(device) +
+                                        " (the device path has no CPU fallback)");
+    check_hip(hipSetDevice(device), "hipSetDevice");
+    set_streams(1);
+}
+
+void Runtime::set_streams(int n) {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (n < 1) n = 1;
+    while ((int)shared_.size() < n) {
+        hipStream_t s;
+        check_hip(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreateWithFlags");
+        shared_.push_back(s);
+    }
+    // existing workers keep their queue; new ones pick round-robin among the first n
+    next_shared_ = 0;
+    active_streams_ = n;
+}
+
+WorkerRes *Runtime::acquire() {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (!free_.empty()) {
+        WorkerRes *w = free_.back();
+        free_.pop_back();
+        return w;
+    }
+    auto w = std::make_unique<WorkerRes>();
+    w->stream = shared_[next_shared_++ % (size_t)active_streams_];
+    w->ws_bytes = fq_aggregate_workspace_bytes(0);
+    check_hip(hipMalloc(&w->ws, w->ws_bytes), "hipMalloc(workspace)");
+    all_.push_back(std::move(w));
+    return all_.back().get();
+}
+
+void Runtime::release(WorkerRes *w) {
+    std::lock_guard<std::mutex> lk(mu_);
+    free_.push_back(w);
+}
+
+Runtime::~Runtime() {
+    (void)hipSetDevice(device_);
+    for (auto &s : shared_) (void)hipStreamSynchronize(s);
+    for (auto &w : all_) {
+        if (w->ws) (void)hipFree(w->ws);
+        for (auto ev : w->events) (void)hipEventDestroy(ev);
+    }
+    for (auto &s : shared_) (void)hipStreamDestroy(s);
+}
+
+DeviceBuffer::~DeviceBuffer() {
+    if (!ptr) return;
+    if (async) (void)hipFreeAsync(ptr, stream);
+    else (void)hipFree(ptr);
+}
+
+std::shared_ptr<DeviceBuffer> DeviceBuffer::alloc(size_t bytes, hipStream_t st) {
+    auto b = std::make_shared<DeviceBuffer>();
+    b->bytes = bytes < 256 ? 256 : bytes;
+    b->stream = st;
+    if (hipMallocAsync(&b->ptr, b->bytes, st) != hipSuccess) {
+        (void)hipGetLastError();
+        b->async = false;
+        check_hip(hipMalloc(&b->ptr, b->bytes), "hipMalloc");
+    }
+    return b;
+}
+
+std::shared_ptr<DeviceBuffer> DeviceBuffer::alloc_sync(size_t bytes) {
+    auto b = std::make_shared<DeviceBuffer>();
+    b->bytes = bytes < 256 ? 256 : bytes;
+    b->async = false;
+    check_hip(hipMalloc(&b->ptr, b->bytes), "hipMalloc(table)");
+    return b;
+}
+
+static thread_local ExecCtx *g_current = nullptr;
+
+ExecCtx::ExecCtx(Runtime *r) : rt(r), res(nullptr), prev_(g_current) {
+    check_hip(hipSetDevice(rt->device()), "hipSetDevice");
+    res = rt->acquire();
+    g_current = this;
+}
+
+ExecCtx::~ExecCtx() {
+    g_current = prev_;
+    rt->release(res);
+}
+
+ExecCtx &ExecCtx::current() {
+    if (!g_current) throw_internal("no device execution context on this thread");
+    return *g_current;
+}
+
+void ExecCtx::sync() { check_hip(hipStreamSynchronize(stream()), "hipStreamSynchronize"); }
+
+// ---------------------------------------------------------------------------
+// columns / blocks
+// ---------------------------------------------------------------------------
+static size_t col_bytes(DataType dt, int64_t len) {
+    if (dt == FQ_DT_BOOLEAN) return (size_t)((len + 63) / 64) * 8;
+    return (size_t)len * (size_t)dtype_size(dt);
+}
+
+fq_col Column::abi() const {
+    fq_col c;
+    c.data = dptr();
+    c.len = len;
+    c.dtype = dtype;
+    c.reserved = 0;
+    return c;
+}
+
+Column Column::device(DataType dt, int64_t len, hipStream_t st) {
+    Column c;
+    c.dtype = dt;
+    c.len = len;
+    c.dev = DeviceBuffer::alloc(col_bytes(dt, len), st);
+    return c;
+}
+
+Column Column::host_values(DataType dt, std::vector<DataValue> rows) {
+    Column c;
+    c.dtype = dt;
+    c.len = (int64_t)rows.size();
+    c.host = std::make_shared<std::vector<DataValue>>(std::move(rows));
+    return c;
+}
+
+Column Column::slice(int64_t start, int64_t n) const {
+    Column c = *this;
+    if (start < 0) start = 0;
+    if (start > len) start = len;
+    if (n > len - start) n = len - start;
+    c.len = n;
+    if (host) {
+        c.host = std::make_shared<std::vector<DataValue>>(host->begin() + start, host->begin() + start + n);
+    } else if (dev) {
+        if (dtype == FQ_DT_BOOLEAN) {
+            if (start % 64) throw_internal("bitmap slices must start on a 64-row boundary");
+            c.offset = offset + (size_t)(start / 64) * 8;
+        } else {
+            c.offset = offset + (size_t)start * dtype_size(dtype);
+        }
+    }
+    return c;
+}
+
+std::vector<DataValue> Column::to_host(hipStream_t st) const {
+    if (host) return *host;
+    std::vector<DataValue> out;
+    if (!dev || len == 0) {
+        if (dtype == FQ_DT_NULL) out.assign((size_t)len, DataValue::null());
+        return out;
+    }
+    const size_t nb = col_bytes(dtype, len);
+    std::vector<uint8_t> h(nb);
+    check_hip(hipMemcpyAsync(h.data(), dptr(), nb, hipMemcpyDeviceToHost, st), "hipMemcpyAsync(D2H)");
+    check_hip(hipStreamSynchronize(st), "hipStreamSynchronize");
+    out.reserve((size_t)len);
+    for (int64_t i = 0; i < len; ++i) {
+        uint64_t bits = 0;
+        switch (dtype) {
+            case FQ_DT_BOOLEAN: bits = (h[(size_t)i / 8] >> (i % 8)) & 1; break;
+            case FQ_DT_INT8: bits = (uint64_t)(int64_t)((int8_t *)h.data())[i]; break;
+            case FQ_DT_INT16: bits = (uint64_t)(int64_t)((int16_t *)h.data())[i]; break;
+            case FQ_DT_INT32: bits = (uint64_t)(int64_t)((int32_t *)h.data())[i]; break;
+            case FQ_DT_INT64: bits = (uint64_t)((int64_t *)h.data())[i]; break;
+            case FQ_DT_UINT8: bits = ((uint8_t *)h.data())[i]; break;
+            case FQ_DT_UINT16: bits = ((uint16_t *)h.data())[i]; break;
+            case FQ_DT_UINT32: bits = ((uint32_t *)h.data())[i]; break;
+            case FQ_DT_UINT64: bits = ((uint64_t *)h.data())[i]; break;
+            case FQ_DT_FLOAT32: bits = f64_bits((double)((float *)h.data())[i]); break;
+            case FQ_DT_FLOAT64: bits = ((uint64_t *)h.data())[i]; break;
+            default: throw_internal("to_host: unsupported column type");
+        }
+        out.push_back(DataValue::some(dtype, bits));
+    }
+    return out;
+}
+
+int64_t DataBlock::num_rows() const {
+    if (filter) throw_internal("num_rows() of a block with a pending filter");
+    return columns.empty() ? 0 : columns[0].len;
+}
+
+const Column &DataBlock::column_by_name(const std::string &name) const {
+    return columns[(size_t)schema->index_of(name)];
+}
+
+uint64_t DataBlock::sub_blocks() const {
+    const int64_t rows = columns.empty() ? 0 : columns[0].len;
+    if (rows == 0 || sub_block_rows <= 0) return 1;
+    return (uint64_t)((rows + sub_block_rows - 1) / sub_block_rows);
+}
+
+Column value_to_array(const DataValue &v, int64_t size, ExecCtx &ctx) {
+    if (v.kind == DataValue::kNull) {  // NullArray::new(size)
+        Column c;
+        c.dtype = FQ_DT_NULL;
+        c.len = size;
+        return c;
+    }
+    to_array_check(v);
+    if (v.dtype == FQ_DT_UTF8)
+        throw_status(FQ_E_UNSUPPORTED, "Utf8 columns are not supported on the device path");
+    Column c = Column::device(v.dtype, size, ctx.stream());
+    check_fq(fq_fill_value(c.dptr(), size, v.dtype, v.bits, ctx.stream()));
+    return c;
+}
+
+Column ColumnarValue::to_array(int64_t size, ExecCtx &ctx) const {
+    if (is_array) return array;
+    return value_to_array(scalar, size, ctx);
+}
+
+}  // namespace fq

@@ -1,0 +1,246 @@
+// C++ restatement of the reference's data layer for the device engine:
+//   FuseQueryError / FuseQueryResult        src/error.rs:10-28
+//   DataValue + scalar ops                  src/datavalues/data_value.rs:20-239,
+//                                           data_value_arithmetic.rs:10-27,
+//                                           data_value_aggregate.rs:8-101
+//   DataField / DataSchema                  src/datavalues/data_field.rs, data_schema.rs
+//   DataBlock (schema + columns)            src/datablocks/data_block.rs:10-62
+//   DataColumnarValue                       src/datavalues/data_columnar_value.rs:8-31
+// Columns live in HBM (Arrow layout) or, for small results and aggregate
+// states, on the host.  Errors are C++ exceptions carrying the reference's
+// display text; the C ABI turns them back into fq_status + fq_last_error().
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <atomic>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "fq_gpu.h"
+
+namespace fq {
+
+using DataType = int32_t;  // FQ_DT_*
+class AggFusion;
+
+// ---------------------------------------------------------------------------
+// errors
+// ---------------------------------------------------------------------------
+struct FQException : std::exception {
+    fq_status status;
+    std::string msg;
+    FQException(fq_status s, std::string m) : status(s), msg(std::move(m)) {}
+    const char *what() const noexcept override { return msg.c_str(); }
+};
+[[noreturn]] void throw_internal(const std::string &m);  // "Internal Error: " + m
+[[noreturn]] void throw_plan(const std::string &m);      // "Error during plan: " + m
+[[noreturn]] void throw_status(fq_status st, const std::string &m);
+void check_fq(fq_status st);  // rethrows fq_last_error() of a C-ABI call
+void check_hip(hipError_t e, const char *what);
+
+const char *dtype_name(DataType dt);
+int dtype_size(DataType dt);
+bool dtype_is_numeric(DataType dt);
+bool dtype_is_float(DataType dt);
+bool dtype_is_signed(DataType dt);
+
+// ---------------------------------------------------------------------------
+// DataValue
+// ---------------------------------------------------------------------------
+struct DataValue {
+    enum Kind : int32_t { kNull = 0, kNone = 1, kSome = 2, kStruct = 3 };
+    int32_t kind = kNull;
+    DataType dtype = FQ_DT_NULL;
+    uint64_t bits = 0;              // fq_value encoding
+    std::string str;                // Utf8 payload
+    std::vector<DataValue> fields;  // Struct payload
+
+    static DataValue null() { return DataValue(); }
+    static DataValue none(DataType dt) {
+        DataValue v;
+        v.kind = kNone;
+        v.dtype = dt;
+        return v;
+    }
+    static DataValue some(DataType dt, uint64_t b) {
+        DataValue v;
+        v.kind = kSome;
+        v.dtype = dt;
+        v.bits = b;
+        return v;
+    }
+    static DataValue u64(uint64_t x) { return some(FQ_DT_UINT64, x); }
+    static DataValue string(const std::string &s) {
+        DataValue v = some(FQ_DT_UTF8, 0);
+        v.str = s;
+        return v;
+    }
+    static DataValue make_struct(std::vector<DataValue> f) {
+        DataValue v;
+        v.kind = kStruct;
+        v.fields = std::move(f);
+        return v;
+    }
+    bool is_untyped_null() const { return kind == kNull; }
+    bool is_none() const { return kind == kNone; }  // DataValue::is_null (data_value.rs:40-56)
+    DataType data_type() const;                     // data_value.rs:58-75
+    std::string debug() const;                      // fmt::Debug (data_value.rs:220-239)
+    fq_value to_abi() const;
+    static DataValue from_abi(const fq_value &v);
+    bool operator==(const DataValue &o) const;
+};
+
+std::string format_f64(double d);  // Rust `{}` formatting of an f64
+
+DataValue data_value_arithmetic_op(int32_t op, const DataValue &l, const DataValue &r);
+DataValue data_value_aggregate_op(uint32_t agg, const DataValue &l, const DataValue &r);
+const char *agg_op_name(uint32_t agg);        // Display: "min", "max", "sum", "count"
+const char *agg_op_debug_name(uint32_t agg);  // Debug: "Min", "Max", "Sum", "Count"
+
+// ---------------------------------------------------------------------------
+// schema
+// ---------------------------------------------------------------------------
+struct DataField {
+    std::string name;
+    DataType dtype = FQ_DT_NULL;
+    bool nullable = false;
+};
+
+struct DataSchema {
+    std::vector<DataField> fields;
+    int index_of(const std::string &name) const;  // throws the arrow error text
+    const DataField &field_with_name(const std::string &name) const;
+};
+using SchemaRef = std::shared_ptr<const DataSchema>;
+
+// ---------------------------------------------------------------------------
+// device runtime: one per engine; a WorkerRes per executing pipe thread
+// ---------------------------------------------------------------------------
+struct EngineStats {
+    std::atomic<uint64_t> scan_launches{0}, scan_rows{0}, scan_bytes{0}, queries{0};
+    std::atomic<uint64_t> scan_ns{0};
+};
+
+struct WorkerRes {
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    void *ws = nullptr;  // fq_aggregate workspace
+    size_t ws_bytes = 0;
+    std::vector<hipEvent_t> events;  // profiling pairs
+};
+
+class Runtime {
+   public:
+    explicit Runtime(int device);
+    ~Runtime();
+    int device() const { return device_; }
+    WorkerRes *acquire();
+    void release(WorkerRes *w);
+    void set_streams(int n);
+    EngineStats stats;
+    std::atomic<bool> profile{false};
+
+   private:
+    int device_;
+    std::mutex mu_;
+    std::vector<std::unique_ptr<WorkerRes>> all_;
+    std::vector<WorkerRes *> free_;
+    std::vector<hipStream_t> shared_;  // FQ_OPT_STREAMS queues shared by the pipes
+    size_t next_shared_ = 0;
+    int active_streams_ = 1;
+};
+
+// Device memory released with hipFreeAsync on the stream that owns it.
+struct DeviceBuffer {
+    void *ptr = nullptr;
+    size_t bytes = 0;
+    hipStream_t stream = nullptr;
+    bool async = true;
+    DeviceBuffer() = default;
+    DeviceBuffer(const DeviceBuffer &) = delete;
+    DeviceBuffer &operator=(const DeviceBuffer &) = delete;
+    ~DeviceBuffer();
+    static std::shared_ptr<DeviceBuffer> alloc(size_t bytes, hipStream_t st);
+    static std::shared_ptr<DeviceBuffer> alloc_sync(size_t bytes);  // long-lived tables
+};
+
+// Execution context of the thread running a pipe (tokio task in the
+// reference, processor_merge.rs:45-63): its device queue and workspaces.
+class ExecCtx {
+   public:
+    ExecCtx(Runtime *rt);
+    ~ExecCtx();
+    ExecCtx(const ExecCtx &) = delete;
+    ExecCtx &operator=(const ExecCtx &) = delete;
+    static ExecCtx &current();  // throws when no context is bound on this thread
+    Runtime *rt;
+    WorkerRes *res;
+    AggFusion *fusion = nullptr;  // set while an AggregatePartial drains its input
+    hipStream_t stream() const { return res->stream; }
+    void sync();
+
+   private:
+    ExecCtx *prev_;
+};
+
+// ---------------------------------------------------------------------------
+// columns and blocks
+// ---------------------------------------------------------------------------
+struct Column {
+    DataType dtype = FQ_DT_NULL;
+    int64_t len = 0;
+    std::shared_ptr<DeviceBuffer> dev;  // device values (or Boolean bitmap words)
+    size_t offset = 0;                  // byte offset into dev
+    std::shared_ptr<std::vector<DataValue>> host;  // host rows (results, states)
+
+    bool on_device() const { return (bool)dev; }
+    void *dptr() const { return dev ? (char *)dev->ptr + offset : nullptr; }
+    fq_col abi() const;
+    static Column device(DataType dt, int64_t len, hipStream_t st);  // uninitialised
+    static Column host_values(DataType dt, std::vector<DataValue> rows);
+    Column slice(int64_t start, int64_t n) const;
+    std::vector<DataValue> to_host(hipStream_t st) const;  // synchronous copy
+};
+
+class Function;
+
+
+struct DataBlock {
+    SchemaRef schema;
+    std::vector<Column> columns;
+    // Reference block granularity this device block stands for: the rows are
+    // a run of ceil(n / sub_block_rows) blocks of sub_block_rows rows
+    // (NumbersStream 10,000-row blocks kept as one partition-sized device
+    // block).  0 = one block.
+    int64_t sub_block_rows = 0;
+    // FilterTransform output not yet compacted: rows where this predicate is
+    // true (the aggregate scan fuses it; other consumers call materialize()).
+    std::shared_ptr<Function> filter;
+
+    int64_t num_rows() const;  // columns[0].len (data_block.rs:46-48); needs no pending filter
+    int num_columns() const { return (int)columns.size(); }
+    const Column &column_by_name(const std::string &name) const;
+    uint64_t sub_blocks() const;  // reference blocks represented (>= 1 if rows > 0)
+};
+
+// Compact a block with a pending filter (fq_compare/eval + fq_filter_compact).
+DataBlock materialize(const DataBlock &b, ExecCtx &ctx);
+
+// DataColumnarValue
+struct ColumnarValue {
+    bool is_array = false;
+    Column array;
+    DataValue scalar;
+    DataType data_type() const { return is_array ? array.dtype : scalar.data_type(); }
+    Column to_array(int64_t size, ExecCtx &ctx) const;  // data_columnar_value.rs:24-30
+};
+
+// DataValue::to_array(size) on the device (fq_fill_value)
+Column value_to_array(const DataValue &v, int64_t size, ExecCtx &ctx);
+
+}  // namespace fq

@@ -1,0 +1,692 @@
+// Expression tree over device columns + the fused aggregate driver.
+#include "functions.h"
+
+#include <string.h>
+
+#include <algorithm>
+
+#include "../fq_common.h"
+
+namespace fq {
+
+static bool is_chain_dtype(DataType dt) {
+    return dt == FQ_DT_UINT64 || dt == FQ_DT_INT64 || dt == FQ_DT_FLOAT64;
+}
+
+std::string FusedChain::key() const {
+    std::string k = column + ":" + std::to_string(col_dtype) + ":" + std::to_string(out_dtype);
+    for (int i = 0; i < expr.n_steps; ++i) {
+        const fq_step &s = expr.steps[i];
+        k += "/" + std::to_string(s.op) + "," + std::to_string(s.operand) + "," + std::to_string(s.reversed) +
+             "," + std::to_string(s.dtype) + "," + std::to_string(s.bits);
+    }
+    return k;
+}
+
+std::string FusedPred::key() const {
+    FusedChain c;
+    c.column = column;
+    c.col_dtype = col_dtype;
+    c.expr = pred.lhs;
+    c.out_dtype = pred.lhs.out_dtype;
+    return c.key() + "?" + std::to_string(pred.cmp) + "," + std::to_string(pred.cmp_dtype) + "," +
+           std::to_string(pred.rhs_operand) + "," + std::to_string(pred.rhs_bits);
+}
+
+// ---------------------------------------------------------------------------
+// device element-wise ops (data_array_arithmetic_op / data_array_comparison_op)
+// ---------------------------------------------------------------------------
+static void side(const ColumnarValue &v, fq_col &c, fq_value &s, bool &is_col) {
+    is_col = v.is_array;
+    if (v.is_array) c = v.array.abi();
+    else s = v.scalar.to_abi();
+}
+
+static void none_check(const ColumnarValue &v) {
+    if (!v.is_array && v.scalar.kind == DataValue::kNone) throw_internal("DataValue to array cannot be NONE NULL");
+    if (!v.is_array && v.scalar.kind == DataValue::kStruct)
+        throw_internal("DataValue to array cannot be NONE " + v.scalar.debug());
+}
+
+static Column device_arith(int32_t op, const ColumnarValue &l, const ColumnarValue &r, ExecCtx &ctx) {
+    none_check(l);
+    none_check(r);
+    if (!l.is_array && !r.is_array) {
+        // both to_array(1): one-row result (data_array_arithmetic.rs:277-279)
+        int32_t ct = 0;
+        check_fq(fq_arith_result_type(op, l.scalar.data_type(), r.scalar.data_type(), &ct));
+        const DataValue v = data_value_arithmetic_op(op, l.scalar, r.scalar);
+        if (v.kind != DataValue::kSome)
+            throw_status(FQ_E_UNSUPPORTED, "cast produced nulls (nulls are not supported on the device path)");
+        return value_to_array(v, 1, ctx);
+    }
+    fq_col lc{}, rc{};
+    fq_value ls{}, rs{};
+    bool lcol, rcol;
+    side(l, lc, ls, lcol);
+    side(r, rc, rs, rcol);
+    int32_t ct = 0;
+    check_fq(fq_arith_result_type(op, lcol ? lc.dtype : ls.dtype, rcol ? rc.dtype : rs.dtype, &ct));
+    const int64_t n = lcol ? lc.len : rc.len;
+    Column out = Column::device(ct, n, ctx.stream());
+    fq_col oc = out.abi();
+    auto flag = DeviceBuffer::alloc(4, ctx.stream());
+    check_fq(fq_arith(op, lcol ? &lc : nullptr, lcol ? nullptr : &ls, rcol ? &rc : nullptr, rcol ? nullptr : &rs,
+                      &oc, (uint32_t *)flag->ptr, ctx.stream()));
+    return out;
+}
+
+static Column device_compare(int32_t cmp, const ColumnarValue &l, const ColumnarValue &r, ExecCtx &ctx) {
+    if (!l.is_array && !r.is_array)  // data_array_comparison.rs:90-95
+        throw_internal(std::string("Cannot do data_array ") + fqc::cmp_op_str(cmp) + ", left:" +
+                       dtype_name(l.data_type()) + ", right:" + dtype_name(r.data_type()));
+    none_check(l);
+    none_check(r);
+    fq_col lc{}, rc{};
+    fq_value ls{}, rs{};
+    bool lcol, rcol;
+    side(l, lc, ls, lcol);
+    side(r, rc, rs, rcol);
+    const int64_t n = lcol ? lc.len : rc.len;
+    Column out = Column::device(FQ_DT_BOOLEAN, n, ctx.stream());
+    auto flag = DeviceBuffer::alloc(4, ctx.stream());
+    check_fq(fq_compare(cmp, lcol ? &lc : nullptr, lcol ? nullptr : &ls, rcol ? &rc : nullptr,
+                        rcol ? nullptr : &rs, (uint64_t *)out.dptr(), n, (uint32_t *)flag->ptr, ctx.stream()));
+    return out;
+}
+
+// ---------------------------------------------------------------------------
+// FieldFunction
+// ---------------------------------------------------------------------------
+DataType FieldFunction::return_type(const DataSchema &s) const { return s.field_with_name(name_).dtype; }
+bool FieldFunction::nullable(const DataSchema &s) const { return s.field_with_name(name_).nullable; }
+
+ColumnarValue FieldFunction::eval(const DataBlock &b, ExecCtx &) {
+    ColumnarValue v;
+    v.is_array = true;
+    v.array = b.column_by_name(name_);
+    return v;
+}
+
+void FieldFunction::accumulate(const DataBlock &b, ExecCtx &ctx) {
+    try {
+        (void)b.column_by_name(name_);  // `saved = Some(column_by_name(..)?)`
+    } catch (const FQException &e) {
+        if (ctx.fusion) ctx.fusion->add_error(e);
+        else throw;
+    }
+}
+
+std::vector<DataValue> FieldFunction::accumulate_result() const {
+    throw_internal("Unsupported aggregate operation for function field");
+}
+void FieldFunction::merge_state(const std::vector<DataValue> &) {
+    throw_internal("Unsupported aggregate operation for function field");
+}
+DataValue FieldFunction::merge_result() const { throw_internal("Unsupported aggregate operation for function field"); }
+
+bool FieldFunction::to_chain(const DataSchema &s, FusedChain &c) const {
+    int idx;
+    try {
+        idx = s.index_of(name_);
+    } catch (const FQException &) {
+        return false;
+    }
+    const DataType dt = s.fields[(size_t)idx].dtype;
+    if (!dtype_is_numeric(dt)) return false;
+    c = FusedChain{};
+    c.column = name_;
+    c.col_dtype = dt;
+    c.expr.n_steps = 0;
+    c.expr.out_dtype = dt;
+    c.out_dtype = dt;
+    return true;
+}
+
+// ---------------------------------------------------------------------------
+// ConstantFunction
+// ---------------------------------------------------------------------------
+ColumnarValue ConstantFunction::eval(const DataBlock &, ExecCtx &) {
+    ColumnarValue v;
+    v.is_array = false;
+    v.scalar = value_;
+    return v;
+}
+
+// ---------------------------------------------------------------------------
+// ArithmeticFunction
+// ---------------------------------------------------------------------------
+std::string ArithmeticFunction::display() const {
+    return left_->display() + " " + fqc::arith_op_str(op_) + " " + right_->display();
+}
+
+DataType ArithmeticFunction::return_type(const DataSchema &s) const {
+    int32_t ct = 0;
+    check_fq(fq_arith_result_type(op_, left_->return_type(s), right_->return_type(s), &ct));
+    return ct;
+}
+
+ColumnarValue ArithmeticFunction::eval(const DataBlock &b, ExecCtx &ctx) {
+    ColumnarValue l = left_->eval(b, ctx);
+    ColumnarValue r = right_->eval(b, ctx);
+    ColumnarValue out;
+    out.is_array = true;
+    out.array = device_arith(op_, l, r, ctx);
+    return out;
+}
+
+std::vector<DataValue> ArithmeticFunction::accumulate_result() const {
+    std::vector<DataValue> a = left_->accumulate_result();
+    std::vector<DataValue> b = right_->accumulate_result();
+    a.insert(a.end(), b.begin(), b.end());
+    return a;
+}
+
+DataValue ArithmeticFunction::merge_result() const {
+    return data_value_arithmetic_op(op_, left_->merge_result(), right_->merge_result());
+}
+
+// Append one step `acc OP operand` (or `operand OP acc`) to a chain.
+static bool push_step(FusedChain &c, int32_t op, bool column_operand, const DataValue *k, bool reversed) {
+    if (c.expr.n_steps >= FQ_MAX_STEPS) return false;
+    if (!is_chain_dtype(c.col_dtype)) return false;
+    const DataType odt = column_operand ? c.col_dtype : k->dtype;
+    int32_t ct = 0;
+    const int32_t l = reversed ? odt : c.out_dtype, r = reversed ? c.out_dtype : odt;
+    if (fqc::numerical_coercion(fqc::arith_op_str(op), l, r, &ct) != FQ_OK) return false;
+    if (!is_chain_dtype(ct)) return false;
+    fq_step &st = c.expr.steps[c.expr.n_steps];
+    st.op = op;
+    st.operand = column_operand ? FQ_OPERAND_COLUMN : FQ_OPERAND_CONST;
+    st.reversed = reversed ? 1 : 0;
+    st.dtype = ct;
+    st.bits = 0;
+    if (!column_operand && !fqc::cast_scalar(k->bits, k->dtype, ct, &st.bits)) return false;
+    c.expr.n_steps++;
+    c.expr.out_dtype = ct;
+    c.out_dtype = ct;
+    return true;
+}
+
+static bool numeric_constant(const Function &f, const DataValue *&v) {
+    v = f.as_constant();
+    return v && v->kind == DataValue::kSome && dtype_is_numeric(v->dtype);
+}
+
+bool ArithmeticFunction::to_chain(const DataSchema &s, FusedChain &c) const {
+    const DataValue *k = nullptr;
+    const std::string *fld = nullptr;
+    FusedChain sub;
+    if (numeric_constant(*right_, k) && left_->to_chain(s, sub)) {
+        c = sub;
+        return push_step(c, op_, false, k, false);
+    }
+    if (numeric_constant(*left_, k) && right_->to_chain(s, sub)) {
+        c = sub;
+        return push_step(c, op_, false, k, true);
+    }
+    if ((fld = right_->as_field()) && left_->to_chain(s, sub) && *fld == sub.column) {
+        c = sub;
+        return push_step(c, op_, true, nullptr, false);
+    }
+    if ((fld = left_->as_field()) && right_->to_chain(s, sub) && *fld == sub.column) {
+        c = sub;
+        return push_step(c, op_, true, nullptr, true);
+    }
+    return false;
+}
+
+// ---------------------------------------------------------------------------
+// ComparisonFunction
+// ---------------------------------------------------------------------------
+std::string ComparisonFunction::display() const {
+    return left_->display() + " " + fqc::cmp_op_str(cmp_) + " " + right_->display();
+}
+
+ColumnarValue ComparisonFunction::eval(const DataBlock &b, ExecCtx &ctx) {
+    ColumnarValue l = left_->eval(b, ctx);
+    ColumnarValue r = right_->eval(b, ctx);
+    ColumnarValue out;
+    out.is_array = true;
+    out.array = device_compare(cmp_, l, r, ctx);
+    return out;
+}
+
+std::vector<DataValue> ComparisonFunction::accumulate_result() const {
+    throw_internal(std::string("Unsupported aggregate operation for function ") + fqc::cmp_op_str(cmp_));
+}
+void ComparisonFunction::merge_state(const std::vector<DataValue> &) {
+    throw_internal(std::string("Unsupported aggregate operation for function ") + fqc::cmp_op_str(cmp_));
+}
+DataValue ComparisonFunction::merge_result() const {
+    throw_internal(std::string("Unsupported aggregate operation for function ") + fqc::cmp_op_str(cmp_));
+}
+
+static int32_t flip(int32_t cmp) {
+    switch (cmp) {
+        case FQ_CMP_LT: return FQ_CMP_GT;
+        case FQ_CMP_LTEQ: return FQ_CMP_GTEQ;
+        case FQ_CMP_GT: return FQ_CMP_LT;
+        case FQ_CMP_GTEQ: return FQ_CMP_LTEQ;
+        default: return cmp;
+    }
+}
+
+static bool make_pred(const FusedChain &lhs, int32_t cmp, bool column_rhs, const DataValue *k, FusedPred &p) {
+    if (!is_chain_dtype(lhs.col_dtype)) return false;
+    const DataType rdt = column_rhs ? lhs.col_dtype : k->dtype;
+    int32_t ct = 0;
+    if (fqc::equal_coercion(fqc::cmp_op_str(cmp), lhs.out_dtype, rdt, &ct) != FQ_OK) return false;
+    if (!is_chain_dtype(ct)) return false;
+    p = FusedPred{};
+    p.column = lhs.column;
+    p.col_dtype = lhs.col_dtype;
+    p.pred.kind = FQ_PRED_EXPR;
+    p.pred.cmp = cmp;
+    p.pred.cmp_dtype = ct;
+    p.pred.rhs_operand = column_rhs ? FQ_OPERAND_COLUMN : FQ_OPERAND_CONST;
+    p.pred.lhs = lhs.expr;
+    if (!column_rhs && !fqc::cast_scalar(k->bits, k->dtype, ct, &p.pred.rhs_bits)) return false;
+    return true;
+}
+
+bool ComparisonFunction::to_pred(const DataSchema &s, FusedPred &p) const {
+    const DataValue *k = nullptr;
+    const std::string *fld = nullptr;
+    FusedChain c;
+    if (numeric_constant(*right_, k) && left_->to_chain(s, c)) return make_pred(c, cmp_, false, k, p);
+    // scalar-array form: the reference flips the operator (data_array_comparison.rs:76-84)
+    if (numeric_constant(*left_, k) && right_->to_chain(s, c)) return make_pred(c, flip(cmp_), false, k, p);
+    if ((fld = right_->as_field()) && left_->to_chain(s, c) && *fld == c.column) return make_pred(c, cmp_, true, nullptr, p);
+    if ((fld = left_->as_field()) && right_->to_chain(s, c) && *fld == c.column)
+        return make_pred(c, flip(cmp_), true, nullptr, p);
+    return false;
+}
+
+// ---------------------------------------------------------------------------
+// AggregatorFunction
+// ---------------------------------------------------------------------------
+std::string AggregatorFunction::display() const {
+    return std::string(agg_op_debug_name(op_)) + "(" + arg_->display() + ")";
+}
+
+DataType AggregatorFunction::return_type(const DataSchema &s) const {
+    return op_ == FQ_AGG_COUNT ? FQ_DT_UINT64 : arg_->return_type(s);
+}
+
+void AggregatorFunction::merge_state(const std::vector<DataValue> &states) {
+    if (depth_ >= states.size())
+        throw_internal("index out of bounds: the len is " + std::to_string(states.size()) + " but the index is " +
+                       std::to_string(depth_));
+    const DataValue &val = states[depth_];
+    if (op_ == FQ_AGG_COUNT || op_ == FQ_AGG_SUM) state_ = data_value_arithmetic_op(FQ_OP_ADD, state_, val);
+    else state_ = data_value_aggregate_op(op_, state_, val);
+}
+
+void AggregatorFunction::accumulate(const DataBlock &b, ExecCtx &ctx) {
+    if (ctx.fusion) {
+        ctx.fusion->add(this, b);
+        return;
+    }
+    accumulate_summary(summarize(b, ctx));
+}
+
+// One device block = `st.blocks` reference blocks.  For each block the
+// reference does (function_aggregator.rs:57-100):
+//   Count:   state = state + UInt64(rows)
+//   Min/Max: state = min/max(state, arrow min/max(block))   (None when empty)
+//   Sum:     state = state + arrow sum(block)               (None when empty;
+//            any later None / None state -> to_array error)
+void AggregatorFunction::accumulate_summary(const fq_agg_state &st) {
+    if (st.blocks == 0) return;
+    if (st.flags & FQ_STATE_DIV_ZERO) throw_status(FQ_E_DIVIDE_BY_ZERO, "Internal Error: Divide by zero error");
+    if (st.flags & FQ_STATE_CAST_NULL)
+        throw_status(FQ_E_UNSUPPORTED, "cast produced nulls (nulls are not supported on the device path)");
+    switch (op_) {
+        case FQ_AGG_COUNT:
+            state_ = data_value_arithmetic_op(FQ_OP_ADD, state_, DataValue::u64(st.count));
+            return;
+        case FQ_AGG_MIN:
+        case FQ_AGG_MAX: {
+            const DataValue d = st.count ? DataValue::some(st.dtype, op_ == FQ_AGG_MAX ? st.max : st.min)
+                                         : DataValue::none(st.dtype);
+            state_ = data_value_aggregate_op(op_, state_, d);
+            return;
+        }
+        default: {
+            if (st.blocks == 1) {
+                const DataValue d = st.count ? DataValue::some(st.dtype, st.sum) : DataValue::none(st.dtype);
+                state_ = data_value_arithmetic_op(FQ_OP_ADD, state_, d);
+                return;
+            }
+            if (st.flags & FQ_STATE_ANY_EMPTY) {
+                // some block's sum is None and there are >= 2 blocks: the add
+                // that meets it fails in to_array (data_value.rs:104-109)
+                throw_internal("DataValue to array cannot be NONE NULL");
+            }
+            state_ = data_value_arithmetic_op(FQ_OP_ADD, state_, DataValue::some(st.dtype, st.sum));
+            return;
+        }
+    }
+}
+
+static uint32_t scan_mask(uint32_t op) { return op | FQ_AGG_COUNT; }
+
+static fq_agg_state run_scan(const Column &col, int64_t block_rows, const fq_pred *pred, const fq_expr *value,
+                             uint32_t mask, ExecCtx &ctx) {
+    auto out = DeviceBuffer::alloc(sizeof(fq_agg_state), ctx.stream());
+    fq_col c = col.abi();
+    check_fq(fq_aggregate(&c, block_rows, pred, value, mask, (fq_agg_state *)out->ptr, ctx.res->ws, ctx.res->ws_bytes,
+                          ctx.stream()));
+    fq_agg_state st{};
+    check_hip(hipMemcpyAsync(&st, out->ptr, sizeof st, hipMemcpyDeviceToHost, ctx.stream()), "hipMemcpyAsync");
+    ctx.sync();
+    ctx.rt->stats.scan_launches++;
+    ctx.rt->stats.scan_rows += (uint64_t)col.len;
+    ctx.rt->stats.scan_bytes += (uint64_t)col.len * (uint64_t)dtype_size(col.dtype);
+    return st;
+}
+
+static DataBlock compact_block(const DataBlock &b, const Column &bitmap, ExecCtx &ctx);
+
+fq_agg_state AggregatorFunction::summarize(const DataBlock &b, ExecCtx &ctx) {
+    const DataSchema &s = *b.schema;
+    const uint64_t k = b.sub_blocks();
+    const int64_t rows = b.columns.empty() ? 0 : b.columns[0].len;
+    const int64_t R = b.sub_block_rows > 0 ? b.sub_block_rows : (rows > 0 ? rows : 1);
+    FusedChain fc;
+    FusedPred fp;
+    const bool chain = arg_->to_chain(s, fc);
+    const bool pred_ok = !b.filter || (b.filter->to_pred(s, fp) && chain && fp.column == fc.column);
+    if (chain && pred_ok) {
+        fq_agg_state st = run_scan(b.column_by_name(fc.column), R, b.filter ? &fp.pred : nullptr,
+                                   fc.expr.n_steps ? &fc.expr : nullptr, scan_mask(op_), ctx);
+        st.blocks = k;
+        return st;
+    }
+    // general path: materialise what the reference would evaluate
+    DataBlock fb = b;
+    fq_agg_state info{};
+    if (b.filter) {
+        DataBlock nb = b;
+        nb.filter = nullptr;
+        Column bm = eval_predicate(*b.filter, nb, ctx);
+        fq_pred bp{};
+        bp.kind = FQ_PRED_BITMAP;
+        bp.bitmap = (const uint64_t *)bm.dptr();
+        Column probe;
+        for (const Column &c : nb.columns)
+            if (c.on_device() && dtype_is_numeric(c.dtype)) {
+                probe = c;
+                break;
+            }
+        if (!probe.on_device()) throw_status(FQ_E_UNSUPPORTED, "filtered aggregate needs a numeric device column");
+        info = run_scan(probe, R, &bp, nullptr, FQ_AGG_SUM | FQ_AGG_COUNT, ctx);
+        fb = compact_block(nb, bm, ctx);
+    }
+    const ColumnarValue v = arg_->eval(fb, ctx);
+    const int64_t frows = fb.num_rows();
+    const DataType vdt = v.data_type();
+    fq_agg_state st{};
+    if (!dtype_is_numeric(vdt)) {
+        if (op_ != FQ_AGG_COUNT)  // data_array_aggregate.rs:155-160
+            throw_internal(std::string("Unsupported data_array_") + agg_op_name(op_) + " for data type: " +
+                           dtype_name(vdt));
+        if (!v.is_array) none_check(v);
+        st.count = (uint64_t)frows;
+        st.dtype = vdt;
+    } else {
+        const Column vc = v.to_array(frows, ctx);
+        st = run_scan(vc, vc.len > 0 ? vc.len : 1, nullptr, nullptr, scan_mask(op_), ctx);
+    }
+    st.blocks = k;
+    if (b.filter) st.flags |= info.flags & FQ_STATE_ANY_EMPTY;
+    return st;
+}
+
+// ---------------------------------------------------------------------------
+// factory (function_factory.rs:14-40)
+// ---------------------------------------------------------------------------
+FunctionRef function_factory(const std::string &name, std::vector<FunctionRef> args, const FactoryOptions &o) {
+    std::string n = name;
+    std::transform(n.begin(), n.end(), n.begin(), [](unsigned char c) { return (char)tolower(c); });
+    auto need = [&](size_t k) {
+        if (args.size() < k)
+            throw_internal("index out of bounds: the len is " + std::to_string(args.size()) + " but the index is " +
+                           std::to_string(k - 1));
+    };
+    int32_t op = -1, cmp = -1;
+    uint32_t agg = 0;
+    if (n == "+") op = FQ_OP_ADD;
+    else if (n == "-") op = FQ_OP_SUB;
+    else if (n == "*") op = FQ_OP_MUL;
+    else if (n == "/") op = FQ_OP_DIV;
+    else if (n == "%" && o.modulo) op = FQ_OP_MOD;
+    else if (n == "=") cmp = FQ_CMP_EQ;
+    else if (n == "<") cmp = FQ_CMP_LT;
+    else if (n == ">") cmp = FQ_CMP_GT;
+    else if (n == "<=") cmp = FQ_CMP_LTEQ;
+    else if (n == ">=") cmp = FQ_CMP_GTEQ;
+    else if (n == "count") agg = FQ_AGG_COUNT;
+    else if (n == "min") agg = FQ_AGG_MIN;
+    else if (n == "max") agg = FQ_AGG_MAX;
+    else if (n == "sum") agg = FQ_AGG_SUM;
+    else if (n == "and" || n == "or")
+        throw_status(FQ_E_UNSUPPORTED, "logic function '" + n + "' (function_logic.rs) is outside the device hot path");
+    else throw_internal("Unsupported Function: " + name);
+    if (op >= 0) {
+        need(2);
+        return std::make_shared<ArithmeticFunction>(op, args[0], args[1]);
+    }
+    if (cmp >= 0) {
+        need(2);
+        return std::make_shared<ComparisonFunction>(cmp, args[0], args[1]);
+    }
+    need(1);
+    return std::make_shared<AggregatorFunction>(agg, args[0]);
+}
+
+// ---------------------------------------------------------------------------
+// predicate evaluation + compaction (FilterTransform::expression_executor)
+// ---------------------------------------------------------------------------
+Column eval_predicate(Function &pred, const DataBlock &b, ExecCtx &ctx) {
+    const ColumnarValue v = pred.eval(b, ctx);
+    const int64_t rows = b.num_rows();
+    if (!v.is_array) {
+        if (v.scalar.kind == DataValue::kSome && v.scalar.dtype == FQ_DT_BOOLEAN) return value_to_array(v.scalar, rows, ctx);
+        throw_internal("cannot downcast to boolean array");
+    }
+    if (v.array.dtype != FQ_DT_BOOLEAN) throw_internal("cannot downcast to boolean array");
+    return v.array;
+}
+
+static DataBlock compact_block(const DataBlock &b, const Column &bitmap, ExecCtx &ctx) {
+    DataBlock out;
+    out.schema = b.schema;
+    out.sub_block_rows = 0;
+    const int64_t n = b.num_rows();
+    const size_t wsb = fq_filter_workspace_bytes(n);
+    auto ws = DeviceBuffer::alloc(wsb, ctx.stream());
+    std::vector<uint8_t> hbits;
+    for (const Column &c : b.columns) {
+        if (c.on_device() && c.dtype != FQ_DT_BOOLEAN) {
+            Column o = Column::device(c.dtype, n, ctx.stream());
+            fq_col ic = c.abi();
+            int64_t kept = 0;
+            check_fq(fq_filter_compact(&ic, (const uint64_t *)bitmap.dptr(), o.dptr(), &kept, ws->ptr, wsb, ctx.stream()));
+            o.len = kept;
+            out.columns.push_back(o);
+            continue;
+        }
+        // host / Boolean / Null columns: select on the host
+        if (hbits.empty()) {
+            std::vector<DataValue> bv = bitmap.to_host(ctx.stream());
+            hbits.resize(bv.size());
+            for (size_t i = 0; i < bv.size(); ++i) hbits[i] = (uint8_t)bv[i].bits;
+        }
+        std::vector<DataValue> rows = c.to_host(ctx.stream());
+        std::vector<DataValue> kept;
+        for (size_t i = 0; i < rows.size() && i < hbits.size(); ++i)
+            if (hbits[i]) kept.push_back(rows[i]);
+        if (c.dtype == FQ_DT_NULL) {
+            Column nc;
+            nc.dtype = FQ_DT_NULL;
+            int64_t cnt = 0;
+            for (auto h : hbits) cnt += h;
+            nc.len = cnt;
+            out.columns.push_back(nc);
+        } else {
+            out.columns.push_back(Column::host_values(c.dtype, std::move(kept)));
+        }
+    }
+    return out;
+}
+
+DataBlock materialize(const DataBlock &b, ExecCtx &ctx) {
+    if (!b.filter) return b;
+    DataBlock nb = b;
+    nb.filter = nullptr;
+    Column bm = eval_predicate(*b.filter, nb, ctx);
+    return compact_block(nb, bm, ctx);
+}
+
+// ---------------------------------------------------------------------------
+// AggFusion
+// ---------------------------------------------------------------------------
+static constexpr size_t kSlotChunk = 64;
+
+AggFusion::AggFusion(ExecCtx &ctx) : ctx_(ctx) {}
+
+AggFusion::~AggFusion() {
+    for (auto &p : events_) {
+        ctx_.res->events.push_back(p.first);
+        ctx_.res->events.push_back(p.second);
+    }
+}
+
+size_t AggFusion::alloc_slot() {
+    if (nslots_ == cap_) {
+        // grow: a new buffer holding every slot so far + a chunk, old contents
+        // copied on the stream (kernels already queued wrote to the old one)
+        const size_t ncap = cap_ + kSlotChunk;
+        auto nb = DeviceBuffer::alloc(ncap * sizeof(fq_agg_state), ctx_.stream());
+        if (slots_ && nslots_)
+            check_hip(hipMemcpyAsync(nb->ptr, slots_->ptr, nslots_ * sizeof(fq_agg_state), hipMemcpyDeviceToDevice,
+                                     ctx_.stream()),
+                      "hipMemcpyAsync(D2D)");
+        slots_ = nb;
+        cap_ = ncap;
+    }
+    return nslots_++;
+}
+
+void AggFusion::add_error(const FQException &e) {
+    Entry en;
+    en.has_error = true;
+    en.err = e;
+    log_.push_back(en);
+}
+
+void AggFusion::add(AggregatorFunction *agg, const DataBlock &b) {
+    const DataSchema &s = *b.schema;
+    FusedChain fc;
+    FusedPred fp;
+    bool ok = agg->arg().to_chain(s, fc);
+    if (ok && b.filter) ok = b.filter->to_pred(s, fp) && fp.column == fc.column;
+    if (!ok) {
+        Entry en;
+        en.agg = agg;
+        try {
+            en.st = agg->summarize(b, ctx_);
+        } catch (const FQException &e) {
+            en.has_error = true;
+            en.err = e;
+        }
+        log_.push_back(en);
+        return;
+    }
+    const std::string key = fc.key() + "|" + (b.filter ? fp.key() : std::string());
+    Group *g = nullptr;
+    for (auto &x : cur_)
+        if (x.key == key) g = &x;
+    if (!g) {
+        cur_.emplace_back();
+        g = &cur_.back();
+        g->key = key;
+        g->col = b.column_by_name(fc.column);
+        g->value = fc;
+        g->has_pred = (bool)b.filter;
+        if (g->has_pred) g->pred = fp.pred;
+        g->filter_keepalive = b.filter;
+        const int64_t rows = g->col.len;
+        g->block_rows = b.sub_block_rows > 0 ? b.sub_block_rows : (rows > 0 ? rows : 1);
+        g->blocks = b.sub_blocks();
+        g->slot = alloc_slot();
+    }
+    g->mask |= scan_mask(agg->op());
+    Entry en;
+    en.agg = agg;
+    en.slot = g->slot;
+    en.st.blocks = g->blocks;
+    log_.push_back(en);
+}
+
+void AggFusion::end_block() {
+    const bool prof = ctx_.rt->profile.load();
+    for (Group &g : cur_) {
+        fq_col c = g.col.abi();
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        if (prof) {
+            for (hipEvent_t *e : {&e0, &e1}) {
+                if (!ctx_.res->events.empty()) {
+                    *e = ctx_.res->events.back();
+                    ctx_.res->events.pop_back();
+                } else {
+                    check_hip(hipEventCreate(e), "hipEventCreate");
+                }
+            }
+            check_hip(hipEventRecord(e0, ctx_.stream()), "hipEventRecord");
+        }
+        fq_agg_state *dst = (fq_agg_state *)slots_->ptr + g.slot;
+        check_fq(fq_aggregate(&c, g.block_rows, g.has_pred ? &g.pred : nullptr,
+                              g.value.expr.n_steps ? &g.value.expr : nullptr, g.mask, dst, ctx_.res->ws,
+                              ctx_.res->ws_bytes, ctx_.stream()));
+        if (prof) {
+            check_hip(hipEventRecord(e1, ctx_.stream()), "hipEventRecord");
+            events_.push_back({e0, e1});
+        }
+        ctx_.rt->stats.scan_launches++;
+        ctx_.rt->stats.scan_rows += (uint64_t)g.col.len;
+        ctx_.rt->stats.scan_bytes += (uint64_t)g.col.len * (uint64_t)dtype_size(g.col.dtype);
+        keepalive_.push_back(g.col);
+    }
+    cur_.clear();
+}
+
+void AggFusion::finish() {
+    end_block();
+    std::vector<fq_agg_state> host(nslots_);
+    if (nslots_)
+        check_hip(hipMemcpyAsync(host.data(), slots_->ptr, nslots_ * sizeof(fq_agg_state), hipMemcpyDeviceToHost,
+                                 ctx_.stream()),
+                  "hipMemcpyAsync(D2H)");
+    ctx_.sync();
+    for (auto &p : events_) {
+        float ms = 0;
+        if (hipEventElapsedTime(&ms, p.first, p.second) == hipSuccess)
+            ctx_.rt->stats.scan_ns += (uint64_t)((double)ms * 1e6);
+    }
+    keepalive_.clear();
+    for (Entry &en : log_) {
+        if (en.has_error) throw en.err;
+        fq_agg_state st = en.st;
+        if (en.slot != (size_t)-1) {
+            const uint64_t blocks = en.st.blocks;
+            st = host[en.slot];
+            st.blocks = blocks;
+        }
+        en.agg->accumulate_summary(st);
+    }
+}
+
+}  // namespace fq

@@ -1,0 +1,276 @@
+// The reference's expression tree (src/functions/), restated over device
+// columns.  `Function` keeps the reference's method set exactly
+// (function.rs:28-131: return_type, nullable, eval, set_depth, accumulate,
+// accumulate_result, merge_state, merge_result) with its depth-indexed state
+// merging (plan_expression.rs:40-60, function_arithmetic.rs:48-52); two
+// extra hooks describe fusable shapes to the device scan (to_chain/to_pred).
+#pragma once
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "core.h"
+
+namespace fq {
+
+// An ArithmeticFunction tree expressed as fq_expr over one column.
+struct FusedChain {
+    std::string column;
+    DataType col_dtype = FQ_DT_NULL;
+    fq_expr expr{};
+    DataType out_dtype = FQ_DT_NULL;
+    std::string key() const;
+};
+
+// A ComparisonFunction expressed as fq_pred over one column.
+struct FusedPred {
+    std::string column;
+    DataType col_dtype = FQ_DT_NULL;
+    fq_pred pred{};
+    std::string key() const;
+};
+
+class Function;
+using FunctionRef = std::shared_ptr<Function>;
+
+class Function {
+   public:
+    virtual ~Function() = default;
+    virtual std::string display() const = 0;  // fmt::Debug of Function (function.rs:134-146)
+    virtual DataType return_type(const DataSchema &s) const = 0;
+    virtual bool nullable(const DataSchema &s) const = 0;
+    virtual ColumnarValue eval(const DataBlock &b, ExecCtx &ctx) = 0;
+    virtual void set_depth(size_t depth) = 0;
+    virtual void accumulate(const DataBlock &b, ExecCtx &ctx) = 0;
+    virtual std::vector<DataValue> accumulate_result() const = 0;
+    virtual void merge_state(const std::vector<DataValue> &states) = 0;
+    virtual DataValue merge_result() const = 0;
+    virtual FunctionRef clone() const = 0;
+
+    // fusion hooks (not in the reference: describe the shape, no semantics)
+    virtual bool to_chain(const DataSchema &, FusedChain &) const { return false; }
+    virtual bool to_pred(const DataSchema &, FusedPred &) const { return false; }
+    virtual const DataValue *as_constant() const { return nullptr; }
+    virtual const std::string *as_field() const { return nullptr; }
+};
+
+// FieldFunction (function_field.rs:13-73)
+class FieldFunction : public Function {
+   public:
+    explicit FieldFunction(std::string name) : name_(std::move(name)) {}
+    std::string display() const override { return name_; }
+    DataType return_type(const DataSchema &s) const override;
+    bool nullable(const DataSchema &s) const override;
+    ColumnarValue eval(const DataBlock &b, ExecCtx &ctx) override;
+    void set_depth(size_t d) override { depth_ = d; }
+    void accumulate(const DataBlock &b, ExecCtx &ctx) override;
+    std::vector<DataValue> accumulate_result() const override;
+    void merge_state(const std::vector<DataValue> &) override;
+    DataValue merge_result() const override;
+    FunctionRef clone() const override { return std::make_shared<FieldFunction>(*this); }
+    bool to_chain(const DataSchema &s, FusedChain &c) const override;
+    const std::string *as_field() const override { return &name_; }
+
+   private:
+    size_t depth_ = 0;
+    std::string name_;
+};
+
+// ConstantFunction (function_constant.rs:13-51)
+class ConstantFunction : public Function {
+   public:
+    explicit ConstantFunction(DataValue v) : value_(std::move(v)) {}
+    std::string display() const override { return value_.debug(); }
+    DataType return_type(const DataSchema &) const override { return value_.data_type(); }
+    bool nullable(const DataSchema &) const override { return value_.is_none(); }
+    ColumnarValue eval(const DataBlock &b, ExecCtx &ctx) override;
+    void set_depth(size_t) override {}
+    void accumulate(const DataBlock &, ExecCtx &) override {}
+    std::vector<DataValue> accumulate_result() const override { return {value_}; }
+    void merge_state(const std::vector<DataValue> &) override {}
+    DataValue merge_result() const override { return value_; }
+    FunctionRef clone() const override { return std::make_shared<ConstantFunction>(*this); }
+    const DataValue *as_constant() const override { return &value_; }
+
+   private:
+    DataValue value_;
+};
+
+// AliasFunction (function_alias.rs:13-59)
+class AliasFunction : public Function {
+   public:
+    AliasFunction(std::string alias, FunctionRef f) : alias_(std::move(alias)), func_(std::move(f)) {}
+    std::string display() const override { return alias_; }
+    DataType return_type(const DataSchema &s) const override { return func_->return_type(s); }
+    bool nullable(const DataSchema &s) const override { return func_->nullable(s); }
+    ColumnarValue eval(const DataBlock &b, ExecCtx &ctx) override { return func_->eval(b, ctx); }
+    void set_depth(size_t d) override { depth_ = d; }
+    void accumulate(const DataBlock &b, ExecCtx &ctx) override { func_->accumulate(b, ctx); }
+    std::vector<DataValue> accumulate_result() const override { return func_->accumulate_result(); }
+    void merge_state(const std::vector<DataValue> &s) override { func_->merge_state(s); }
+    DataValue merge_result() const override { return func_->merge_result(); }
+    FunctionRef clone() const override { return std::make_shared<AliasFunction>(alias_, func_->clone()); }
+    bool to_chain(const DataSchema &s, FusedChain &c) const override { return func_->to_chain(s, c); }
+    bool to_pred(const DataSchema &s, FusedPred &p) const override { return func_->to_pred(s, p); }
+
+   private:
+    size_t depth_ = 0;
+    std::string alias_;
+    FunctionRef func_;
+};
+
+// ArithmeticFunction (function_arithmetic.rs:16-89); op FQ_OP_MOD is the '%' extension
+class ArithmeticFunction : public Function {
+   public:
+    ArithmeticFunction(int32_t op, FunctionRef l, FunctionRef r) : op_(op), left_(std::move(l)), right_(std::move(r)) {}
+    std::string display() const override;
+    DataType return_type(const DataSchema &s) const override;
+    bool nullable(const DataSchema &) const override { return false; }
+    ColumnarValue eval(const DataBlock &b, ExecCtx &ctx) override;
+    void set_depth(size_t d) override {
+        left_->set_depth(d);
+        right_->set_depth(d + 1);
+        depth_ = d;
+    }
+    void accumulate(const DataBlock &b, ExecCtx &ctx) override {
+        left_->accumulate(b, ctx);
+        right_->accumulate(b, ctx);
+    }
+    std::vector<DataValue> accumulate_result() const override;
+    void merge_state(const std::vector<DataValue> &s) override {
+        left_->merge_state(s);
+        right_->merge_state(s);
+    }
+    DataValue merge_result() const override;
+    FunctionRef clone() const override {
+        auto f = std::make_shared<ArithmeticFunction>(op_, left_->clone(), right_->clone());
+        f->depth_ = depth_;
+        return f;
+    }
+    bool to_chain(const DataSchema &s, FusedChain &c) const override;
+
+   private:
+    size_t depth_ = 0;
+    int32_t op_;
+    FunctionRef left_, right_;
+};
+
+// ComparisonFunction (function_comparison.rs:17-86)
+class ComparisonFunction : public Function {
+   public:
+    ComparisonFunction(int32_t cmp, FunctionRef l, FunctionRef r) : cmp_(cmp), left_(std::move(l)), right_(std::move(r)) {}
+    std::string display() const override;
+    DataType return_type(const DataSchema &) const override { return FQ_DT_BOOLEAN; }
+    bool nullable(const DataSchema &) const override { return false; }
+    ColumnarValue eval(const DataBlock &b, ExecCtx &ctx) override;
+    void set_depth(size_t d) override { depth_ = d; }
+    void accumulate(const DataBlock &b, ExecCtx &ctx) override {
+        left_->accumulate(b, ctx);
+        right_->accumulate(b, ctx);
+    }
+    std::vector<DataValue> accumulate_result() const override;
+    void merge_state(const std::vector<DataValue> &) override;
+    DataValue merge_result() const override;
+    FunctionRef clone() const override {
+        auto f = std::make_shared<ComparisonFunction>(cmp_, left_->clone(), right_->clone());
+        f->depth_ = depth_;
+        return f;
+    }
+    bool to_pred(const DataSchema &s, FusedPred &p) const override;
+
+   private:
+    size_t depth_ = 0;
+    int32_t cmp_;
+    FunctionRef left_, right_;
+};
+
+// AggregatorFunction (function_aggregator.rs:17-144)
+class AggregatorFunction : public Function {
+   public:
+    AggregatorFunction(uint32_t op, FunctionRef arg) : op_(op), arg_(std::move(arg)) {}
+    std::string display() const override;
+    DataType return_type(const DataSchema &s) const override;
+    bool nullable(const DataSchema &) const override { return false; }
+    ColumnarValue eval(const DataBlock &b, ExecCtx &ctx) override { return arg_->eval(b, ctx); }
+    void set_depth(size_t d) override { depth_ = d; }
+    void accumulate(const DataBlock &b, ExecCtx &ctx) override;
+    std::vector<DataValue> accumulate_result() const override { return {state_}; }
+    void merge_state(const std::vector<DataValue> &states) override;
+    DataValue merge_result() const override { return state_; }
+    FunctionRef clone() const override {
+        auto f = std::make_shared<AggregatorFunction>(op_, arg_->clone());
+        f->depth_ = depth_;
+        f->state_ = state_;
+        return f;
+    }
+
+    uint32_t op() const { return op_; }
+    const Function &arg() const { return *arg_; }
+    // Replays the reference's per-block accumulate over a run of `st.blocks`
+    // reference blocks summarised by one device scan (see fq_agg_state).
+    void accumulate_summary(const fq_agg_state &st);
+    // Non-deferred evaluation of this aggregator over one block.
+    fq_agg_state summarize(const DataBlock &b, ExecCtx &ctx);
+
+   private:
+    size_t depth_ = 0;
+    uint32_t op_;
+    FunctionRef arg_;
+    DataValue state_;  // DataValue::Null initially (function_aggregator.rs:29)
+};
+
+// ScalarFunctionFactory::get (function_factory.rs:14-40)
+struct FactoryOptions {
+    bool modulo = true;  // '%' extension
+};
+FunctionRef function_factory(const std::string &name, std::vector<FunctionRef> args, const FactoryOptions &o);
+
+// Deferred, fused accumulate for AggregatePartialTransform: aggregators that
+// share an argument expression (and the block's pending predicate) are served
+// by ONE fq_aggregate scan per block; results are replayed into each
+// aggregator in the reference's (block, function) order at finish().
+class AggFusion {
+   public:
+    explicit AggFusion(ExecCtx &ctx);
+    ~AggFusion();
+    void add(AggregatorFunction *agg, const DataBlock &b);
+    void add_error(const FQException &e);  // a non-aggregator failure at this point
+    void end_block();                      // launch this block's scans
+    void finish();                         // sync + replay; throws the first error
+
+   private:
+    struct Group {
+        std::string key;
+        Column col;
+        FusedChain value;
+        bool has_pred = false;
+        fq_pred pred{};
+        std::shared_ptr<Function> filter_keepalive;
+        uint32_t mask = 0;
+        int64_t block_rows = 0;
+        uint64_t blocks = 0;
+        size_t slot = 0;
+    };
+    struct Entry {
+        AggregatorFunction *agg = nullptr;
+        size_t slot = (size_t)-1;  // device result slot, or
+        fq_agg_state st{};         // an immediate summary
+        bool has_error = false;
+        FQException err{0, ""};
+    };
+    ExecCtx &ctx_;
+    std::vector<Group> cur_;
+    std::vector<Entry> log_;
+    std::vector<Column> keepalive_;
+    std::shared_ptr<DeviceBuffer> slots_;
+    size_t nslots_ = 0, cap_ = 0;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> events_;
+    std::vector<uint64_t> event_bytes_;
+    size_t alloc_slot();
+};
+
+// evaluate a predicate over a block into a Boolean column (the non-fused path)
+Column eval_predicate(Function &pred, const DataBlock &b, ExecCtx &ctx);
+
+}  // namespace fq

@@ -1,0 +1,513 @@
+// Data sources, processors, streams and the pipeline.
+#include "pipeline.h"
+
+#include <string.h>
+
+#include <exception>
+
+namespace fq {
+
+// ---------------------------------------------------------------------------
+// system.numbers_mt
+// ---------------------------------------------------------------------------
+static constexpr uint64_t kBlockSize = 10000;  // numbers_stream.rs:29
+
+NumbersTable::NumbersTable() {
+    auto s = std::make_shared<DataSchema>();
+    s->fields.push_back(DataField{"number", FQ_DT_UINT64, false});  // numbers_table.rs:21-25
+    schema_ = s;
+}
+
+// NumbersTable::generate_parts (numbers_table.rs:29-55)
+std::vector<Partition> NumbersTable::generate_parts(uint64_t total) {
+    const uint64_t workers = 8, chunk = total / workers;
+    std::vector<Partition> parts;
+    auto name = [&](uint64_t a, uint64_t b) {
+        return std::to_string(total) + "-" + std::to_string(a) + "-" + std::to_string(b);
+    };
+    if (chunk == 0) {
+        parts.push_back(Partition{name(0, total - 1), 0});  // total - 1 wraps at 0 (release build)
+        return parts;
+    }
+    const uint64_t remain = total % workers;
+    for (uint64_t p = 0; p < workers; ++p) {
+        const uint64_t start = p * chunk;
+        uint64_t end = (p + 1) * chunk - 1;
+        if (p == workers - 1 && remain > 0) end += remain;
+        parts.push_back(Partition{name(start, end), 0});
+    }
+    return parts;
+}
+
+void NumbersTable::parse_part(const std::string &n, uint64_t &total, uint64_t &begin, uint64_t &end) {
+    const size_t a = n.find('-'), b = n.find('-', a == std::string::npos ? a : a + 1);
+    if (a == std::string::npos || b == std::string::npos) throw_internal("bad numbers_mt partition name: " + n);
+    total = std::stoull(n.substr(0, a));
+    begin = std::stoull(n.substr(a + 1, b - a - 1));
+    end = std::stoull(n.substr(b + 1));
+}
+
+// NumbersStream::create (numbers_stream.rs:27-62): the partition's blocks are
+// one contiguous run; the last block ends at block_begin + remain.
+uint64_t NumbersTable::stream_rows(uint64_t begin, uint64_t end) {
+    const uint64_t count = end - begin + 1;
+    const uint64_t nblocks = count / kBlockSize, remain = count % kBlockSize;
+    if (nblocks == 0 || remain == 0) return count;
+    return kBlockSize * (nblocks - 1) + remain + 1;
+}
+
+ReadDataSourcePlan NumbersTable::read_plan(const DataValue *arg) const {
+    uint64_t total = 10000;  // numbers_table.rs:69
+    if (arg && arg->kind == DataValue::kSome && (arg->dtype == FQ_DT_UINT64 || arg->dtype == FQ_DT_INT64))
+        total = arg->bits;
+    ReadDataSourcePlan p;
+    p.db = "system";
+    p.table = name();
+    p.table_type = "System";
+    p.schema = schema_;
+    p.partitions = generate_parts(total);
+    p.description = "(Read from system.numbers_mt table)";
+    return p;
+}
+
+void NumbersTable::pin(const std::string &part, Column col) {
+    std::lock_guard<std::mutex> lk(mu_);
+    resident_[part] = std::move(col);
+}
+void NumbersTable::unpin_all() {
+    std::lock_guard<std::mutex> lk(mu_);
+    resident_.clear();
+}
+bool NumbersTable::pinned(const std::string &part, Column &out) {
+    std::lock_guard<std::mutex> lk(mu_);
+    auto it = resident_.find(part);
+    if (it == resident_.end()) return false;
+    out = it->second;
+    return true;
+}
+
+// NumbersStream::poll_next (numbers_stream.rs:65-83): one device block per
+// partition (its 10,000-row blocks are kept as sub_block_rows).
+class NumbersStream : public BlockStream {
+   public:
+    NumbersStream(NumbersTable *t, SchemaRef s, std::vector<Partition> parts)
+        : t_(t), schema_(std::move(s)), parts_(std::move(parts)) {}
+    bool next(DataBlock &out) override {
+        if (i_ >= parts_.size()) return false;
+        const Partition &p = parts_[i_++];
+        uint64_t total, begin, end;
+        NumbersTable::parse_part(p.name, total, begin, end);
+        if (end - begin + 1 == 0 || end < begin)
+            throw_status(FQ_E_UNSUPPORTED, "numbers_mt partition " + p.name +
+                                               " materialises 2^64 rows in the reference (total - 1 wraps)");
+        const uint64_t rows = NumbersTable::stream_rows(begin, end);
+        Column col;
+        if (!t_->pinned(p.name, col) || (uint64_t)col.len != rows) {
+            ExecCtx &ctx = ExecCtx::current();
+            col = Column::device(FQ_DT_UINT64, (int64_t)rows, ctx.stream());
+            check_fq(fq_fill_numbers_u64((uint64_t *)col.dptr(), begin, rows, ctx.stream()));
+        }
+        out = DataBlock{};
+        out.schema = schema_;
+        out.columns.push_back(col);
+        out.sub_block_rows = (int64_t)kBlockSize;
+        return true;
+    }
+
+   private:
+    NumbersTable *t_;
+    SchemaRef schema_;
+    std::vector<Partition> parts_;
+    size_t i_ = 0;
+};
+
+StreamRef NumbersTable::read(const std::vector<Partition> &parts) {
+    return std::make_unique<NumbersStream>(this, schema_, parts);
+}
+
+DataSource::DataSource() : numbers_(std::make_shared<NumbersTable>()) {
+    dbs_["system"]["numbers_mt"] = numbers_;  // datasource.rs:22-33
+}
+
+TableRef DataSource::get_table(const std::string &db, const std::string &table) const {
+    auto d = dbs_.find(db);
+    if (d == dbs_.end()) throw_internal("Cannot find the database: " + db);
+    auto t = d->second.find(table);
+    if (t == d->second.end()) throw_internal("Cannot find the table: " + table);
+    return t->second;
+}
+
+// ---------------------------------------------------------------------------
+// processors
+// ---------------------------------------------------------------------------
+std::string IProcessor::format(FormatterSettings &s) const {
+    std::string out;
+    if (s.indent > 0) {
+        out += "\n";
+        for (size_t i = 0; i < s.indent; ++i) out += s.indent_char;
+    }
+    out += s.prefix + " " + name() + " \xc3\x97 " + std::to_string(s.ways) + " " +
+           (s.ways == 1 ? "processor" : "processors");
+    return out;
+}
+
+std::string MergeProcessor::format(FormatterSettings &s) const {
+    std::string out;
+    if (s.indent > 0) {
+        out += "\n";
+        for (size_t i = 0; i < s.indent; ++i) out += s.indent_char;
+    }
+    out += s.prefix + " Merge (" + s.prev_name + " \xc3\x97 " + std::to_string(s.prev_ways) + " " +
+           (s.prev_ways == 1 ? "processor" : "processors") + ") to (" + name() + " \xc3\x97 " +
+           std::to_string(s.ways) + ")";
+    return out;
+}
+
+// tokio mpsc::channel(partitions) + ChannelStream (stream_channel.rs:14-28)
+struct Channel {
+    std::mutex mu;
+    std::condition_variable cv_send, cv_recv;
+    struct Item {
+        bool is_err = false;
+        DataBlock block;
+        FQException err{0, ""};
+    };
+    std::deque<Item> q;
+    size_t cap = 1;
+    int live = 0;
+    bool closed = false;
+
+    bool send(Item it) {
+        std::unique_lock<std::mutex> lk(mu);
+        cv_send.wait(lk, [&] { return q.size() < cap || closed; });
+        if (closed) return false;
+        q.push_back(std::move(it));
+        cv_recv.notify_one();
+        return true;
+    }
+    void done() {
+        std::lock_guard<std::mutex> lk(mu);
+        --live;
+        cv_recv.notify_all();
+    }
+    bool recv(Item &it) {
+        std::unique_lock<std::mutex> lk(mu);
+        cv_recv.wait(lk, [&] { return !q.empty() || live == 0; });
+        if (q.empty()) return false;
+        it = std::move(q.front());
+        q.pop_front();
+        cv_send.notify_one();
+        return true;
+    }
+    void close() {
+        std::lock_guard<std::mutex> lk(mu);
+        closed = true;
+        cv_send.notify_all();
+    }
+};
+
+class ChannelStream : public BlockStream {
+   public:
+    std::shared_ptr<Channel> ch;
+    std::vector<std::thread> threads;
+    ~ChannelStream() override {
+        ch->close();
+        for (auto &t : threads)
+            if (t.joinable()) t.join();
+    }
+    bool next(DataBlock &out) override {
+        Channel::Item it;
+        if (!ch->recv(it)) return false;
+        if (it.is_err) throw it.err;
+        out = std::move(it.block);
+        return true;
+    }
+};
+
+// MergeProcessor::execute (processor_merge.rs:37-66): one host thread per
+// input pipe (the tokio::spawn), each with its own device context.
+StreamRef MergeProcessor::execute() {
+    if (list_.empty()) throw_internal("Merge processor cannot be zero");
+    if (list_.size() == 1) return list_[0]->execute();
+    Runtime *rt = ExecCtx::current().rt;
+    auto cs = std::make_unique<ChannelStream>();
+    cs->ch = std::make_shared<Channel>();
+    cs->ch->cap = list_.size();
+    cs->ch->live = (int)list_.size();
+    for (auto &input : list_) {
+        std::shared_ptr<Channel> ch = cs->ch;
+        ProcessorRef in = input;
+        cs->threads.emplace_back([in, ch, rt]() {
+            try {
+                ExecCtx ctx(rt);
+                StreamRef s = in->execute();
+                DataBlock b;
+                while (s->next(b)) {
+                    ctx.sync();  // device work of this block done before another thread reads it
+                    Channel::Item it;
+                    it.block = std::move(b);
+                    if (!ch->send(std::move(it))) break;
+                }
+            } catch (const FQException &e) {
+                Channel::Item it;
+                it.is_err = true;
+                it.err = e;
+                ch->send(std::move(it));
+            } catch (const std::exception &e) {
+                Channel::Item it;
+                it.is_err = true;
+                it.err = FQException(FQ_E_INTERNAL, std::string("Internal Error: ") + e.what());
+                ch->send(std::move(it));
+            }
+            ch->done();
+        });
+    }
+    return cs;
+}
+
+StreamRef SourceTransform::execute() {
+    TableRef t = ctx_->get_table(db_, table_);  // transform_source.rs:49-52
+    return t->read(parts_);
+}
+
+namespace {
+class MapStream : public BlockStream {
+   public:
+    MapStream(StreamRef in, std::function<DataBlock(DataBlock)> f) : in_(std::move(in)), f_(std::move(f)) {}
+    bool next(DataBlock &out) override {
+        DataBlock b;
+        if (!in_->next(b)) return false;
+        out = f_(std::move(b));
+        return true;
+    }
+
+   private:
+    StreamRef in_;
+    std::function<DataBlock(DataBlock)> f_;
+};
+
+struct FusionGuard {
+    ExecCtx &ctx;
+    AggFusion *prev;
+    FusionGuard(ExecCtx &c, AggFusion *f) : ctx(c), prev(c.fusion) { ctx.fusion = f; }
+    ~FusionGuard() { ctx.fusion = prev; }
+};
+}  // namespace
+
+// FilterTransform: the block keeps its columns and carries the predicate;
+// the aggregate scan fuses it, every other consumer compacts (materialize).
+StreamRef FilterTransform::execute() {
+    FunctionRef pred = func_->clone();
+    return std::make_unique<MapStream>(input_->execute(), [pred](DataBlock b) {
+        if (b.filter) b = materialize(b, ExecCtx::current());
+        b.filter = pred;
+        return b;
+    });
+}
+
+StreamRef ProjectionTransform::execute() {
+    SchemaRef schema = schema_;
+    std::vector<FunctionRef> funcs;
+    for (auto &f : funcs_) funcs.push_back(f->clone());
+    return std::make_unique<MapStream>(input_->execute(), [schema, funcs](DataBlock b) {
+        ExecCtx &ctx = ExecCtx::current();
+        b = materialize(b, ctx);
+        const int64_t rows = b.num_rows();
+        DataBlock out;
+        out.schema = schema;
+        for (auto &f : funcs) out.columns.push_back(f->eval(b, ctx).to_array(rows, ctx));
+        return out;
+    });
+}
+
+StreamRef AggregatePartialTransform::execute() {
+    std::vector<FunctionRef> funcs;
+    for (auto &f : funcs_) funcs.push_back(f->clone());
+    ExecCtx &ctx = ExecCtx::current();
+    StreamRef in = input_->execute();
+    {
+        AggFusion fusion(ctx);
+        FusionGuard guard(ctx, &fusion);
+        DataBlock b;
+        while (in->next(b)) {
+            for (auto &f : funcs) f->accumulate(b, ctx);
+            fusion.end_block();
+        }
+        fusion.finish();
+    }
+    std::vector<DataValue> rows;
+    for (auto &f : funcs) rows.push_back(DataValue::make_struct(f->accumulate_result()));
+    DataBlock out;
+    out.schema = schema_;
+    out.columns.push_back(Column::host_values(FQ_DT_NULL, std::move(rows)));
+    return std::make_unique<DataBlockStream>(std::vector<DataBlock>{out});
+}
+
+StreamRef AggregateFinalTransform::execute() {
+    std::vector<FunctionRef> funcs;
+    for (auto &f : funcs_) funcs.push_back(f->clone());
+    StreamRef in = input_->execute();
+    DataBlock b;
+    while (in->next(b)) {
+        if (b.columns.empty() || !b.columns[0].host) continue;
+        const std::vector<DataValue> &rows = *b.columns[0].host;
+        for (size_t i = 0; i < funcs.size() && i < rows.size(); ++i)
+            if (rows[i].kind == DataValue::kStruct) funcs[i]->merge_state(rows[i].fields);
+    }
+    DataBlock out;
+    out.schema = schema_;
+    if (emit_states_) {
+        std::vector<DataValue> rows;
+        for (auto &f : funcs) rows.push_back(DataValue::make_struct(f->accumulate_result()));
+        out.columns.push_back(Column::host_values(FQ_DT_NULL, std::move(rows)));
+    } else {
+        for (auto &f : funcs) {
+            const DataValue v = f->merge_result();
+            if (v.kind == DataValue::kNone) throw_internal("DataValue to array cannot be NONE NULL");
+            if (v.kind == DataValue::kStruct) throw_internal("DataValue to array cannot be NONE " + v.debug());
+            out.columns.push_back(Column::host_values(v.kind == DataValue::kNull ? FQ_DT_NULL : v.dtype, {v}));
+        }
+    }
+    return std::make_unique<DataBlockStream>(std::vector<DataBlock>{out});
+}
+
+// LimitStream (stream_limit.rs:13-60)
+namespace {
+class LimitStream : public BlockStream {
+   public:
+    LimitStream(StreamRef in, size_t limit) : in_(std::move(in)), limit_(limit) {}
+    bool next(DataBlock &out) override {
+        DataBlock b;
+        if (!in_->next(b)) return false;
+        if (current_ == limit_) return false;
+        ExecCtx &ctx = ExecCtx::current();
+        b = materialize(b, ctx);
+        const size_t rows = (size_t)b.num_rows();
+        if (current_ + rows < limit_) {
+            current_ += rows;
+            out = b;
+            return true;
+        }
+        const size_t keep = limit_ - current_;
+        current_ = limit_;
+        out = b;
+        for (auto &c : out.columns) c = c.slice(0, (int64_t)keep);
+        return true;
+    }
+
+   private:
+    StreamRef in_;
+    size_t limit_, current_ = 0;
+};
+}  // namespace
+
+StreamRef LimitTransform::execute() { return std::make_unique<LimitStream>(input_->execute(), limit_); }
+
+// ---------------------------------------------------------------------------
+// Pipeline
+// ---------------------------------------------------------------------------
+void Pipeline::add_source(ProcessorRef source) {
+    if (pipes_.empty()) pipes_.emplace_back();
+    pipes_[0].push_back(std::move(source));
+}
+
+void Pipeline::add_simple_transform(const std::function<ProcessorRef()> &f) {
+    if (pipes_.empty()) throw_internal("Can't add transform to an empty pipe list");
+    std::vector<ProcessorRef> items;
+    for (auto &x : pipes_.back()) {
+        ProcessorRef p = f();
+        p->connect_to(x);
+        items.push_back(p);
+    }
+    pipes_.push_back(std::move(items));
+}
+
+void Pipeline::merge_processor() {
+    if (pipes_.empty()) throw_internal("Can't merge processor when the last pipe is empty");
+    if (pipes_.back().size() > 1) {
+        auto p = std::make_shared<MergeProcessor>();
+        for (auto &x : pipes_.back()) p->connect_to(x);
+        pipes_.push_back({p});
+    }
+}
+
+StreamRef Pipeline::execute() {
+    if (pipes_.empty()) throw_internal("Pipeline is empty");
+    if (pipes_.back().size() > 1) merge_processor();
+    return pipes_.back()[0]->execute();
+}
+
+std::string Pipeline::display() const {
+    FormatterSettings s;
+    std::string out;
+    for (size_t k = pipes_.size(); k-- > 0;) {
+        const auto &cur = pipes_[k];
+        if (k > 0) {
+            s.prev_ways = pipes_[k - 1].size();
+            s.prev_name = pipes_[k - 1][0]->name();
+        }
+        s.ways = cur.size();
+        s.indent += 1;
+        out += cur[0]->format(s);
+    }
+    return out;
+}
+
+// ---------------------------------------------------------------------------
+// partial-state wire format (replaces the reference's serde_json Utf8 rows,
+// transform_aggregate_partial.rs:61-72): "FQS1", u32 n_funcs, then per func
+// u32 n_values, u32 0, n_values x {i32 kind, i32 dtype, u64 bits}.
+// ---------------------------------------------------------------------------
+std::vector<uint8_t> encode_states(const std::vector<std::vector<DataValue>> &per_func) {
+    std::vector<uint8_t> out(8);
+    memcpy(out.data(), "FQS1", 4);
+    const uint32_t nf = (uint32_t)per_func.size();
+    memcpy(out.data() + 4, &nf, 4);
+    for (const auto &vals : per_func) {
+        uint32_t hdr[2] = {(uint32_t)vals.size(), 0};
+        const size_t o = out.size();
+        out.resize(o + 8 + vals.size() * 16);
+        memcpy(out.data() + o, hdr, 8);
+        for (size_t i = 0; i < vals.size(); ++i) {
+            const DataValue &v = vals[i];
+            if (v.kind == DataValue::kStruct || (v.kind == DataValue::kSome && v.dtype == FQ_DT_UTF8))
+                throw_status(FQ_E_UNSUPPORTED, "partial state " + v.debug() + " has no fixed-size encoding");
+            const int32_t kd[2] = {v.kind, v.kind == DataValue::kNull ? FQ_DT_NULL : v.dtype};
+            memcpy(out.data() + o + 8 + i * 16, kd, 8);
+            memcpy(out.data() + o + 16 + i * 16, &v.bits, 8);
+        }
+    }
+    return out;
+}
+
+std::vector<std::vector<DataValue>> decode_states(const uint8_t *p, size_t n) {
+    if (n < 8 || memcmp(p, "FQS1", 4) != 0) throw_status(FQ_E_INVALID, "partial states: bad header");
+    uint32_t nf;
+    memcpy(&nf, p + 4, 4);
+    size_t o = 8;
+    std::vector<std::vector<DataValue>> out;
+    for (uint32_t f = 0; f < nf; ++f) {
+        if (o + 8 > n) throw_status(FQ_E_INVALID, "partial states: truncated");
+        uint32_t cnt;
+        memcpy(&cnt, p + o, 4);
+        o += 8;
+        if (o + (size_t)cnt * 16 > n) throw_status(FQ_E_INVALID, "partial states: truncated");
+        std::vector<DataValue> vals;
+        for (uint32_t i = 0; i < cnt; ++i) {
+            int32_t kd[2];
+            uint64_t bits;
+            memcpy(kd, p + o, 8);
+            memcpy(&bits, p + o + 8, 8);
+            o += 16;
+            DataValue v;
+            v.kind = kd[0];
+            v.dtype = kd[1];
+            v.bits = v.kind == DataValue::kSome ? bits : 0;
+            vals.push_back(v);
+        }
+        out.push_back(std::move(vals));
+    }
+    return out;
+}
+
+}  // namespace fq

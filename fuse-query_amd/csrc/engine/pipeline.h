@@ -1,0 +1,277 @@
+// Processors, streams and pipeline (src/processors/, src/transforms/,
+// src/datastreams/, src/datasources/) restated for device DataBlocks.
+//
+// One host thread per pipe replaces the reference's tokio task per pipe
+// (processor_merge.rs:45-63); each thread binds an ExecCtx (device queue +
+// scan workspace).  Blocks flow by pull (BlockStream::next) as in the
+// reference's Stream::poll_next; errors are exceptions forwarded through the
+// MergeProcessor channel like the reference forwards Err items.
+#pragma once
+
+#include <condition_variable>
+#include <deque>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "core.h"
+#include "functions.h"
+
+namespace fq {
+
+// ---------------------------------------------------------------------------
+// streams (SendableDataBlockStream, stream.rs:8-9)
+// ---------------------------------------------------------------------------
+class BlockStream {
+   public:
+    virtual ~BlockStream() = default;
+    virtual bool next(DataBlock &out) = 0;  // false = end of stream; throws on error
+};
+using StreamRef = std::unique_ptr<BlockStream>;
+
+// DataBlockStream (stream_datablock.rs:13-60)
+class DataBlockStream : public BlockStream {
+   public:
+    explicit DataBlockStream(std::vector<DataBlock> blocks) : blocks_(std::move(blocks)) {}
+    bool next(DataBlock &out) override {
+        if (i_ >= blocks_.size()) return false;
+        out = blocks_[i_++];
+        return true;
+    }
+
+   private:
+    std::vector<DataBlock> blocks_;
+    size_t i_ = 0;
+};
+
+// ---------------------------------------------------------------------------
+// data sources (src/datasources/)
+// ---------------------------------------------------------------------------
+struct Partition {  // partition.rs:5-11
+    std::string name;
+    uint64_t version = 0;
+};
+
+struct ReadDataSourcePlan {  // plan_read_datasource.rs
+    std::string db, table, table_type, description;
+    SchemaRef schema;
+    std::vector<Partition> partitions;
+};
+
+class ITable {  // table.rs:13-22
+   public:
+    virtual ~ITable() = default;
+    virtual std::string name() const = 0;
+    virtual SchemaRef schema() const = 0;
+    virtual ReadDataSourcePlan read_plan(const DataValue *table_arg) const = 0;
+    virtual StreamRef read(const std::vector<Partition> &parts) = 0;
+};
+using TableRef = std::shared_ptr<ITable>;
+
+// system.numbers_mt (numbers_table.rs:14-97, numbers_stream.rs:20-84) with
+// partitions optionally pinned in HBM.
+class NumbersTable : public ITable {
+   public:
+    NumbersTable();
+    std::string name() const override { return "numbers_mt"; }
+    SchemaRef schema() const override { return schema_; }
+    ReadDataSourcePlan read_plan(const DataValue *table_arg) const override;
+    StreamRef read(const std::vector<Partition> &parts) override;
+
+    static std::vector<Partition> generate_parts(uint64_t total);
+    static void parse_part(const std::string &name, uint64_t &total, uint64_t &begin, uint64_t &end);
+    static uint64_t stream_rows(uint64_t begin, uint64_t end);  // rows NumbersStream yields
+    void pin(const std::string &part, Column col);
+    void unpin_all();
+    bool pinned(const std::string &part, Column &out);
+
+   private:
+    SchemaRef schema_;
+    std::mutex mu_;
+    std::map<std::string, Column> resident_;
+};
+
+class DataSource {  // datasource.rs:11-62
+   public:
+    DataSource();
+    TableRef get_table(const std::string &db, const std::string &table) const;
+    std::shared_ptr<NumbersTable> numbers() const { return numbers_; }
+
+   private:
+    std::map<std::string, std::map<std::string, TableRef>> dbs_;
+    std::shared_ptr<NumbersTable> numbers_;
+};
+
+// FuseQueryContext (context.rs:10-37) + the engine's execution knobs
+struct QueryContext {
+    size_t worker_threads = 8;
+    std::string default_db = "default";
+    std::shared_ptr<DataSource> datasource;
+    FactoryOptions factory;
+    Runtime *rt = nullptr;
+    int rank = 0, world = 1;  // distributed partial: this rank's partition shard
+    TableRef get_table(const std::string &db, const std::string &table) const {
+        return datasource->get_table(db, table);
+    }
+};
+using QueryContextRef = std::shared_ptr<QueryContext>;
+
+// ---------------------------------------------------------------------------
+// processors (processor.rs:22-57)
+// ---------------------------------------------------------------------------
+struct FormatterSettings {
+    size_t ways = 0, indent = 0;
+    std::string indent_char = "  ", prefix = "\xe2\x94\x94\xe2\x94\x80";  // "└─"
+    size_t prev_ways = 0;
+    std::string prev_name;
+};
+
+class IProcessor {
+   public:
+    virtual ~IProcessor() = default;
+    virtual std::string name() const = 0;
+    virtual void connect_to(std::shared_ptr<IProcessor> input) = 0;
+    virtual StreamRef execute() = 0;
+    virtual std::string format(FormatterSettings &s) const;
+};
+using ProcessorRef = std::shared_ptr<IProcessor>;
+
+class EmptyProcessor : public IProcessor {  // processor_empty.rs:14-49
+   public:
+    std::string name() const override { return "EmptyProcessor"; }
+    void connect_to(ProcessorRef) override { throw_internal("Cannot call EmptyProcessor connect_to"); }
+    StreamRef execute() override { return std::make_unique<DataBlockStream>(std::vector<DataBlock>{}); }
+    std::string format(FormatterSettings &) const override { return ""; }
+};
+
+class MergeProcessor : public IProcessor {  // processor_merge.rs:16-94
+   public:
+    std::string name() const override { return "MergeProcessor"; }
+    void connect_to(ProcessorRef input) override { list_.push_back(std::move(input)); }
+    StreamRef execute() override;
+    std::string format(FormatterSettings &s) const override;
+
+   private:
+    std::vector<ProcessorRef> list_;
+};
+
+class SourceTransform : public IProcessor {  // transform_source.rs:14-53
+   public:
+    SourceTransform(QueryContextRef ctx, std::string db, std::string table, std::vector<Partition> parts)
+        : ctx_(std::move(ctx)), db_(std::move(db)), table_(std::move(table)), parts_(std::move(parts)) {}
+    std::string name() const override { return "SourceTransform"; }
+    void connect_to(ProcessorRef) override { throw_internal("Cannot call SourceTransform connect_to"); }
+    StreamRef execute() override;
+
+   private:
+    QueryContextRef ctx_;
+    std::string db_, table_;
+    std::vector<Partition> parts_;
+};
+
+class FilterTransform : public IProcessor {  // transform_filter.rs:17-77
+   public:
+    explicit FilterTransform(FunctionRef pred) : func_(std::move(pred)), input_(std::make_shared<EmptyProcessor>()) {}
+    std::string name() const override { return "FilterTransform"; }
+    void connect_to(ProcessorRef input) override { input_ = std::move(input); }
+    StreamRef execute() override;
+
+   private:
+    FunctionRef func_;
+    ProcessorRef input_;
+};
+
+class ProjectionTransform : public IProcessor {  // transform_projection.rs:16-78
+   public:
+    ProjectionTransform(SchemaRef schema, std::vector<FunctionRef> funcs)
+        : schema_(std::move(schema)), funcs_(std::move(funcs)), input_(std::make_shared<EmptyProcessor>()) {}
+    std::string name() const override { return "ProjectionTransform"; }
+    void connect_to(ProcessorRef input) override { input_ = std::move(input); }
+    StreamRef execute() override;
+
+   private:
+    SchemaRef schema_;
+    std::vector<FunctionRef> funcs_;
+    ProcessorRef input_;
+};
+
+class AggregatePartialTransform : public IProcessor {  // transform_aggregate_partial.rs:18-79
+   public:
+    AggregatePartialTransform(SchemaRef schema, std::vector<FunctionRef> funcs)
+        : schema_(std::move(schema)), funcs_(std::move(funcs)), input_(std::make_shared<EmptyProcessor>()) {}
+    std::string name() const override { return "AggregatePartialTransform"; }
+    void connect_to(ProcessorRef input) override { input_ = std::move(input); }
+    StreamRef execute() override;
+
+   private:
+    SchemaRef schema_;
+    std::vector<FunctionRef> funcs_;
+    ProcessorRef input_;
+};
+
+class AggregateFinalTransform : public IProcessor {  // transform_aggregate_final.rs:18-79
+   public:
+    // emit_states: output the merged accumulate_result() (for a cross-GPU
+    // exchange) instead of merge_result() values.
+    AggregateFinalTransform(SchemaRef schema, std::vector<FunctionRef> funcs, bool emit_states = false)
+        : schema_(std::move(schema)), funcs_(std::move(funcs)), input_(std::make_shared<EmptyProcessor>()),
+          emit_states_(emit_states) {}
+    std::string name() const override { return "AggregateFinalTransform"; }
+    void connect_to(ProcessorRef input) override { input_ = std::move(input); }
+    StreamRef execute() override;
+
+   private:
+    SchemaRef schema_;
+    std::vector<FunctionRef> funcs_;
+    ProcessorRef input_;
+    bool emit_states_;
+};
+
+class LimitTransform : public IProcessor {  // transform_limit.rs:12-43
+   public:
+    explicit LimitTransform(size_t n) : limit_(n), input_(std::make_shared<EmptyProcessor>()) {}
+    std::string name() const override { return "LimitTransform"; }
+    void connect_to(ProcessorRef input) override { input_ = std::move(input); }
+    StreamRef execute() override;
+
+   private:
+    size_t limit_;
+    ProcessorRef input_;
+};
+
+// A processor yielding prepared blocks (AggregateFinal input across GPUs).
+class BlocksProcessor : public IProcessor {
+   public:
+    explicit BlocksProcessor(std::vector<DataBlock> b) : blocks_(std::move(b)) {}
+    std::string name() const override { return "ExchangeSource"; }
+    void connect_to(ProcessorRef) override { throw_internal("Cannot call ExchangeSource connect_to"); }
+    StreamRef execute() override { return std::make_unique<DataBlockStream>(blocks_); }
+
+   private:
+    std::vector<DataBlock> blocks_;
+};
+
+// ---------------------------------------------------------------------------
+// Pipeline (pipeline.rs:15-135)
+// ---------------------------------------------------------------------------
+class Pipeline {
+   public:
+    size_t pipe_num() const { return pipes_.empty() ? 0 : pipes_.back().size(); }
+    void add_source(ProcessorRef source);
+    void add_simple_transform(const std::function<ProcessorRef()> &f);
+    void merge_processor();
+    StreamRef execute();
+    std::string display() const;
+
+   private:
+    std::vector<std::vector<ProcessorRef>> pipes_;
+};
+
+// serialised partial states (one 16-byte record per DataValue)
+std::vector<uint8_t> encode_states(const std::vector<std::vector<DataValue>> &per_func);
+std::vector<std::vector<DataValue>> decode_states(const uint8_t *p, size_t n);
+
+}  // namespace fq

@@ -7,6 +7,8 @@
 // back at HBM speed.  A splitmix64 column is the anti-closed-form control.
 #include <hip/hip_runtime.h>
 
+#include <string>
+
 #include "fq_common.h"
 #include "fq_device.h"
 
@@ -93,3 +95,57 @@ fq_status fq_fill_splitmix64(uint64_t *d_out, uint64_t seed, uint64_t first_inde
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------
+// DataValue::to_array(size): scalar broadcast (data_value.rs:77-111)
+// ---------------------------------------------------------------------------
+namespace fqk {
+
+template <typename T>
+__global__ void __launch_bounds__(256) fill_value_kernel(T *__restrict__ out, int64_t n, T v) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) out[i] = v;
+}
+
+template <typename T>
+static fq_status fill_value(void *out, int64_t n, T v, hipStream_t st) {
+    if (n <= 0) return FQ_OK;
+    const int max_grid = fqc::device_cu_count() * 8;
+    int64_t grid = (n + 255) / 256;
+    if (grid > max_grid) grid = max_grid;
+    hipLaunchKernelGGL((fill_value_kernel<T>), dim3((int)grid), dim3(256), 0, st, (T *)out, n, v);
+    FQ_HIP_TRY(hipGetLastError());
+    return FQ_OK;
+}
+
+}  // namespace fqk
+
+extern "C" fq_status fq_fill_value(void *d_out, int64_t n, int32_t dtype, uint64_t bits, void *stream) {
+    using namespace fqk;
+    hipStream_t st = (hipStream_t)stream;
+    if (n < 0) return fqc::fail(FQ_E_INVALID, "fq_fill_value: negative length");
+    if (n > 0 && !d_out) return fqc::fail(FQ_E_INVALID, "fq_fill_value: NULL output");
+    switch (dtype) {
+        case FQ_DT_BOOLEAN: {
+            const int64_t words = (n + 63) / 64;
+            fq_status s = fill_value<uint64_t>(d_out, words, bits ? ~0ull : 0ull, st);
+            if (s != FQ_OK || !bits || (n & 63) == 0) return s;
+            const uint64_t last = (1ull << (n & 63)) - 1;  // clear bits past n
+            return fill_value<uint64_t>((uint64_t *)d_out + words - 1, 1, last, st);
+        }
+        case FQ_DT_INT8:
+        case FQ_DT_UINT8: return fill_value<uint8_t>(d_out, n, (uint8_t)bits, st);
+        case FQ_DT_INT16:
+        case FQ_DT_UINT16: return fill_value<uint16_t>(d_out, n, (uint16_t)bits, st);
+        case FQ_DT_INT32:
+        case FQ_DT_UINT32: return fill_value<uint32_t>(d_out, n, (uint32_t)bits, st);
+        case FQ_DT_FLOAT32: {
+            const float f = (float)__builtin_bit_cast(double, bits);
+            return fill_value<uint32_t>(d_out, n, __builtin_bit_cast(uint32_t, f), st);
+        }
+        case FQ_DT_INT64:
+        case FQ_DT_UINT64:
+        case FQ_DT_FLOAT64: return fill_value<uint64_t>(d_out, n, bits, st);
+        default: return fqc::fail(FQ_E_UNSUPPORTED, std::string("fq_fill_value: ") + fqc::dtype_name(dtype));
+    }
+}

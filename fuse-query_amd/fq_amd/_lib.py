@@ -14,7 +14,7 @@ LIB_PATH = os.path.normpath(os.path.join(_HERE, "..", "lib", "libfq_amd.so"))
 
 # Exported symbols promised by include/fq_gpu.h (checked by the CPU tests)
 GPU_SYMBOLS = [
-    "fq_abi_version", "fq_last_error", "fq_device_count", "fq_fill_numbers_u64",
+    "fq_abi_version", "fq_last_error", "fq_device_count", "fq_fill_numbers_u64", "fq_fill_value",
     "fq_fill_splitmix64", "fq_aggregate_workspace_bytes", "fq_aggregate",
     "fq_arith_result_type", "fq_arith", "fq_compare", "fq_filter_workspace_bytes",
     "fq_filter_compact", "fq_state_merge",

@@ -1,0 +1,174 @@
+"""Python binding of include/fq_engine.h: run SQL through the C++ pipeline
+(Source -> Filter -> AggregatePartial x P -> Merge -> AggregateFinal, or
+Projection / Limit) on the gfx950 kernels.
+
+    with Engine() as e:
+        r = e.execute("SELECT sum(number)/count(number), max(number), min(number) "
+                      "FROM system.numbers_mt(10000000000)")
+        r.names  -> ['Sum(number) / Count(number)', 'Max(number)', 'Min(number)']
+        r.rows   -> [(1310651184, 9999999999, 0)]
+"""
+import ctypes as C
+
+from . import abi
+from ._lib import FQError, check, last_error, lib
+from .expr import from_bits
+
+P = C.POINTER
+
+OPT_WORKER_THREADS, OPT_MODULO, OPT_PROFILE, OPT_STREAMS = 1, 2, 3, 4
+
+ENGINE_SYMBOLS = [
+    "fq_engine_create", "fq_engine_destroy", "fq_engine_set_option", "fq_engine_materialize_numbers",
+    "fq_engine_release_numbers", "fq_engine_execute", "fq_engine_explain", "fq_engine_execute_partial",
+    "fq_engine_execute_final", "fq_engine_get_stats", "fq_engine_reset_stats", "fq_result_num_rows",
+    "fq_result_num_columns", "fq_result_column_name", "fq_result_column_type", "fq_result_value",
+    "fq_result_text", "fq_result_free",
+]
+
+
+class fq_engine_stats(C.Structure):
+    _fields_ = [("scan_launches", C.c_uint64), ("scan_rows", C.c_uint64), ("scan_bytes", C.c_uint64),
+                ("scan_ms", C.c_double), ("queries", C.c_uint64)]
+
+
+_protos = {
+    "fq_engine_create": (C.c_int32, [C.c_int32, P(C.c_void_p)]),
+    "fq_engine_destroy": (None, [C.c_void_p]),
+    "fq_engine_set_option": (C.c_int32, [C.c_void_p, C.c_int32, C.c_int64]),
+    "fq_engine_materialize_numbers": (C.c_int32, [C.c_void_p, C.c_uint64, C.c_int32, C.c_int32]),
+    "fq_engine_release_numbers": (C.c_int32, [C.c_void_p]),
+    "fq_engine_execute": (C.c_int32, [C.c_void_p, C.c_char_p, P(C.c_void_p)]),
+    "fq_engine_explain": (C.c_int32, [C.c_void_p, C.c_char_p, C.c_char_p, C.c_size_t, P(C.c_size_t)]),
+    "fq_engine_execute_partial": (C.c_int32, [C.c_void_p, C.c_char_p, C.c_int32, C.c_int32, C.c_void_p,
+                                              C.c_size_t, P(C.c_size_t)]),
+    "fq_engine_execute_final": (C.c_int32, [C.c_void_p, C.c_char_p, C.c_void_p, C.c_size_t, C.c_int32,
+                                            P(C.c_void_p)]),
+    "fq_engine_get_stats": (C.c_int32, [C.c_void_p, P(fq_engine_stats)]),
+    "fq_engine_reset_stats": (C.c_int32, [C.c_void_p]),
+    "fq_result_num_rows": (C.c_int64, [C.c_void_p]),
+    "fq_result_num_columns": (C.c_int32, [C.c_void_p]),
+    "fq_result_column_name": (C.c_char_p, [C.c_void_p, C.c_int32]),
+    "fq_result_column_type": (C.c_int32, [C.c_void_p, C.c_int32]),
+    "fq_result_value": (C.c_int32, [C.c_void_p, C.c_int64, C.c_int32, P(abi.fq_value)]),
+    "fq_result_text": (C.c_char_p, [C.c_void_p, C.c_int64, C.c_int32]),
+    "fq_result_free": (None, [C.c_void_p]),
+}
+for _n, (_r, _a) in _protos.items():
+    _f = getattr(lib, _n)
+    _f.restype = _r
+    _f.argtypes = _a
+
+
+class Result:
+    """A query result: column names/types as the reference names them and
+    rows of Python values (None for NULL)."""
+
+    def __init__(self, ptr):
+        try:
+            ncol = lib.fq_result_num_columns(ptr)
+            nrow = lib.fq_result_num_rows(ptr)
+            self.names = [lib.fq_result_column_name(ptr, c).decode() for c in range(ncol)]
+            self.types = [lib.fq_result_column_type(ptr, c) for c in range(ncol)]
+            cols = []
+            for c in range(ncol):
+                vals = []
+                for r in range(nrow):
+                    if self.types[c] == abi.DT_UTF8:
+                        t = lib.fq_result_text(ptr, r, c)
+                        vals.append(t.decode() if t is not None else None)
+                        continue
+                    v = abi.fq_value()
+                    if lib.fq_result_value(ptr, r, c, C.byref(v)) != 0:
+                        vals.append(None)
+                        continue
+                    vals.append(from_bits(v.bits, v.dtype) if v.is_some else None)
+                cols.append(vals)
+            self.columns = cols
+            self.rows = [tuple(col[r] for col in cols) for r in range(nrow)]
+        finally:
+            lib.fq_result_free(ptr)
+
+    def __repr__(self):
+        return "Result(names=%r, rows=%r)" % (self.names, self.rows[:10])
+
+
+class Engine:
+    def __init__(self, device=0, worker_threads=8, modulo=True, profile=False, streams=1):
+        h = C.c_void_p()
+        check(lib.fq_engine_create(device, C.byref(h)))
+        self.h = h
+        self.set_option(OPT_WORKER_THREADS, worker_threads)
+        self.set_option(OPT_MODULO, 1 if modulo else 0)
+        self.set_option(OPT_PROFILE, 1 if profile else 0)
+        self.set_option(OPT_STREAMS, streams)
+
+    def set_option(self, opt, value):
+        check(lib.fq_engine_set_option(self.h, opt, int(value)))
+
+    def close(self):
+        if self.h:
+            lib.fq_engine_destroy(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def materialize_numbers(self, total, rank=0, world=1):
+        check(lib.fq_engine_materialize_numbers(self.h, int(total), rank, world))
+
+    def release_numbers(self):
+        check(lib.fq_engine_release_numbers(self.h))
+
+    def execute(self, sql):
+        out = C.c_void_p()
+        check(lib.fq_engine_execute(self.h, sql.encode(), C.byref(out)))
+        return Result(out)
+
+    def explain(self, sql):
+        n = C.c_size_t(0)
+        check(lib.fq_engine_explain(self.h, sql.encode(), None, 0, C.byref(n)))
+        buf = C.create_string_buffer(n.value + 1)
+        check(lib.fq_engine_explain(self.h, sql.encode(), buf, n.value + 1, C.byref(n)))
+        return buf.value.decode()
+
+    def execute_partial(self, sql, rank, world):
+        """Serialised merged partial states of this rank's shard (bytes)."""
+        n = C.c_size_t(0)
+        cap = 4096
+        while True:
+            buf = C.create_string_buffer(cap)
+            st = lib.fq_engine_execute_partial(self.h, sql.encode(), rank, world, buf, cap, C.byref(n))
+            if st == abi.FQ_E_INVALID and n.value > cap:
+                cap = n.value
+                continue
+            check(st)
+            return buf.raw[: n.value]
+
+    def execute_final(self, sql, states, stride=None):
+        """AggregateFinal over per-rank serialised states (list of bytes, rank order)."""
+        stride = stride or max(len(s) for s in states)
+        blob = b"".join(s.ljust(stride, b"\0") for s in states)
+        out = C.c_void_p()
+        check(lib.fq_engine_execute_final(self.h, sql.encode(), blob, stride, len(states), C.byref(out)))
+        return Result(out)
+
+    def stats(self):
+        s = fq_engine_stats()
+        check(lib.fq_engine_get_stats(self.h, C.byref(s)))
+        return {k: getattr(s, k) for k, _ in fq_engine_stats._fields_}
+
+    def reset_stats(self):
+        check(lib.fq_engine_reset_stats(self.h))
+
+
+__all__ = ["Engine", "Result", "FQError", "last_error", "ENGINE_SYMBOLS"]

@@ -1,0 +1,100 @@
+/*
+ * fq_engine.h -- C ABI of the pipeline layer: the C++ restatement of the
+ * reference's query path (SQL -> plan -> PipelineBuilder -> IProcessor
+ * transforms) running its DataBlocks on the gfx950 kernels of fq_gpu.h.
+ *
+ *   fq_engine_execute        SelectExecutor::execute        src/executors/executor_select.rs:35-40
+ *                            (PipelineBuilder::build        src/processors/pipeline_builder.rs:26-106,
+ *                             Pipeline::execute             src/processors/pipeline.rs:129-134)
+ *   fq_engine_explain        ExplainExecutor::execute       src/executors/executor_explain.rs:38-59
+ *   fq_engine_execute_partial / fq_engine_execute_final
+ *                            the AggregatePartial -> Merge -> AggregateFinal split
+ *                            (transform_aggregate_partial.rs:50-78, transform_aggregate_final.rs:50-78)
+ *                            cut at the merge so ranks on different GPUs can exchange
+ *                            their partial states (one RCCL all-reduce) in between
+ *   fq_engine_materialize_numbers
+ *                            system.numbers_mt partitions pinned in HBM
+ *                            (NumbersTable::read, numbers_table.rs:94-96)
+ *
+ * Results are host copies: one fq_result per query, column names as the
+ * reference formats them (`format!("{:?}", func)`, plan_expression.rs:31-38),
+ * values as fq_value (see fq_gpu.h).
+ */
+#ifndef FQ_ENGINE_H
+#define FQ_ENGINE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "fq_gpu.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct fq_engine fq_engine;
+typedef struct fq_result fq_result;
+
+/* engine options */
+#define FQ_OPT_WORKER_THREADS 1 /* FuseQueryContext::worker_threads (context.rs:11); default 8 */
+#define FQ_OPT_MODULO 2         /* 1 (default): '%' extension on; 0: reference behaviour
+                                   ("Unsupported Function: %", function_factory.rs:34-37) */
+#define FQ_OPT_PROFILE 3        /* 1: time every fused scan launch with HIP events */
+#define FQ_OPT_STREAMS 4        /* device queues the pipes share (default 1: the scans are
+                                   HBM-bound, concurrency buys nothing and blurs timing) */
+
+typedef struct fq_engine_stats {
+    uint64_t scan_launches; /* fused aggregate scans launched                    */
+    uint64_t scan_rows;     /* rows those scans read                            */
+    uint64_t scan_bytes;    /* algorithmic bytes those scans read               */
+    double scan_ms;         /* summed event time of those launches (FQ_OPT_PROFILE) */
+    uint64_t queries;
+} fq_engine_stats;
+
+/* device: HIP device ordinal.  Fails with FQ_E_HIP when no GPU is present. */
+fq_status fq_engine_create(int32_t device, fq_engine **out);
+void fq_engine_destroy(fq_engine *e);
+fq_status fq_engine_set_option(fq_engine *e, int32_t option, int64_t value);
+
+/* Materialise (and keep resident) the numbers_mt(total) partitions that rank
+ * `rank` of `world` owns ([8r/G, 8(r+1)/G) of generate_parts).  Queries over
+ * numbers_mt(total) then read these instead of regenerating them.          */
+fq_status fq_engine_materialize_numbers(fq_engine *e, uint64_t total, int32_t rank, int32_t world);
+fq_status fq_engine_release_numbers(fq_engine *e);
+
+/* Run a SELECT through the whole pipeline on this engine's GPU. */
+fq_status fq_engine_execute(fq_engine *e, const char *sql, fq_result **out);
+
+/* EXPLAIN-style text: the plan and the pipeline (processor.rs:33-57 format). */
+fq_status fq_engine_explain(fq_engine *e, const char *sql, char *buf, size_t cap, size_t *len);
+
+/* Distributed aggregate: rank r runs Source -> Filter -> AggregatePartial for
+ * its partitions and merges them locally; the merged partial states are
+ * serialised into buf (fixed 16-byte DataValue records).  *len gets the size;
+ * when cap is too small the call fails with FQ_E_INVALID and *len holds the
+ * size needed.                                                              */
+fq_status fq_engine_execute_partial(fq_engine *e, const char *sql, int32_t rank, int32_t world,
+                                    void *buf, size_t cap, size_t *len);
+/* AggregateFinal over `world` serialised partial states laid out back to back
+ * with a stride of `stride` bytes (rank order). */
+fq_status fq_engine_execute_final(fq_engine *e, const char *sql, const void *states, size_t stride,
+                                  int32_t world, fq_result **out);
+
+fq_status fq_engine_get_stats(fq_engine *e, fq_engine_stats *out);
+fq_status fq_engine_reset_stats(fq_engine *e);
+
+/* results */
+int64_t fq_result_num_rows(const fq_result *r);
+int32_t fq_result_num_columns(const fq_result *r);
+const char *fq_result_column_name(const fq_result *r, int32_t col);
+int32_t fq_result_column_type(const fq_result *r, int32_t col);
+fq_status fq_result_value(const fq_result *r, int64_t row, int32_t col, fq_value *out);
+/* the value as text, DataValue's Display (NULL for None); valid until fq_result_free */
+const char *fq_result_text(const fq_result *r, int64_t row, int32_t col);
+void fq_result_free(fq_result *r);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FQ_ENGINE_H */

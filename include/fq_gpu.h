@@ -6,6 +6,7 @@
  * (dantengsky/fuse-query @ /root/reference, Rust + arrow 2.0 compute):
  *
  *   fq_fill_numbers_u64   NumbersStream::poll_next        src/datasources/system/numbers_stream.rs:65-83
+ *   fq_fill_value         DataValue::to_array             src/datavalues/data_value.rs:77-111
  *   fq_aggregate          AggregatorFunction::accumulate  src/functions/function_aggregator.rs:57-100
  *                         (-> data_array_aggregate_op     src/datavalues/data_array_aggregate.rs:14-163,
  *                             arrow::compute::sum/min/max src/datavalues/macros.rs:143-157)
@@ -184,6 +185,11 @@ fq_status fq_fill_numbers_u64(uint64_t *d_out, uint64_t begin, uint64_t count, v
 /* Anti-closed-form control column: d_out[i] = splitmix64(seed, first_index + i). */
 fq_status fq_fill_splitmix64(uint64_t *d_out, uint64_t seed, uint64_t first_index,
                              uint64_t count, void *stream);
+
+/* DataValue::to_array(size) (data_value.rs:77-111): broadcast one scalar.
+ * dtype is a numeric type (bits in fq_value encoding) or FQ_DT_BOOLEAN
+ * (writes ceil(n/64) bitmap words, bits past n cleared).                   */
+fq_status fq_fill_value(void *d_out, int64_t n, int32_t dtype, uint64_t bits, void *stream);
 
 /* ---- AggregatePartial: fused predicate + argument expression + sum/max/min/count ----
  * One pass over `col`; writes one fq_agg_state to device memory d_out.

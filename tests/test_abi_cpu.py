@@ -16,6 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def declared_symbols(header):
     src = open(os.path.join(ROOT, "include", header)).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)  # declarations only, not comments
     return sorted(set(re.findall(r"^\s*(?:[\w\s\*]+?)\b(fq_\w+)\s*\(", src, re.M)))
 
 

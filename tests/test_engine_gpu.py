@@ -1,0 +1,246 @@
+"""End-to-end parity of the C++ pipeline (SQL -> Source -> Filter ->
+AggregatePartial x 8 -> Merge -> AggregateFinal, Projection, Limit) on the
+GPU against the reference's own test expectations, the README results and
+the C oracle.  Integer results are bit-exact."""
+import pytest
+
+from fq_amd import abi
+from fq_amd.expr import chain, predicate
+
+import oracle_c
+
+pytestmark = pytest.mark.gpu
+
+Engine = None
+E = None
+
+
+def setup_module():
+    global Engine, E
+    from fq_amd import ops
+    ops.require_gpu()
+    from fq_amd.engine import Engine as _E
+    Engine = _E
+    E = Engine()
+
+
+def teardown_module():
+    if E is not None:
+        E.close()
+
+
+def q(sql):
+    return E.execute(sql)
+
+
+def oracle(total, aggs, pred=None):
+    """[(kind, dtype, value)] from the oracle's Source->Partial->Final."""
+    return [v for _, _, v in oracle_c.numbers_query(total, aggs, pred)]
+
+
+# ---- the reference's own pipeline tests ----------------------------------
+
+def test_transform_aggregate_sum_plus_2_is_122():
+    # src/transforms/transform_aggregate_test.rs:5-59 (sum(number)+2 over numbers_mt(16))
+    r = q("SELECT sum(number)+2 FROM system.numbers_mt(16)")
+    assert r.rows == [(122,)]
+    assert r.names == ["Sum(number) + 2"]
+    assert r.types == [abi.DT_UINT64]
+
+
+def test_transform_filter_number_eq_1():
+    # src/transforms/transform_filter_test.rs:5-44
+    r = q("SELECT number FROM system.numbers_mt(8) WHERE number = 1")
+    assert r.rows == [(1,)]
+
+
+def test_source_reads_all_rows():
+    # transform_source_test.rs: numbers_mt(16) -> 16 rows
+    r = q("SELECT number FROM system.numbers_mt(16)")
+    assert sorted(v for (v,) in r.rows) == list(range(16))
+
+
+def test_readme_projection_filter_limit():
+    # README.md:120-127 (alias push-down is the optimizer's job, out of scope:
+    # the WHERE spells the aliased expressions out)
+    r = q("select (number+1) as c1, number/2 as c2 from system.numbers_mt(10000000) "
+          "where ((number+1)+(number/2)+1) < 100 limit 3")
+    assert r.names == ["c1", "c2"]
+    assert r.rows == [(1, 0), (2, 0), (3, 1)]
+
+
+def test_explain_matches_reference_format():
+    txt = E.explain("select (number+1) as c1, number/2 as c2 from system.numbers_mt(10000000) "
+                    "where ((number+1)+(number/2)+1) < 100 limit 3")
+    plan, pipe = txt.split("\n", 4)[:4], txt
+    assert txt.startswith("└─ Limit: 3\n  └─ Projection: (number + 1) as c1, (number / 2) as c2\n"
+                          "    └─ Filter: ((((number + 1) + (number / 2)) + 1) < 100)\n"
+                          "      └─ ReadDataSource: scan parts [8](Read from system.numbers_mt table)")
+    assert ("\n  └─ LimitTransform × 1 processor\n    └─ Merge (LimitTransform × 8 processors) to "
+            "(MergeProcessor × 1)\n      └─ LimitTransform × 8 processors\n        └─ ProjectionTransform"
+            " × 8 processors\n          └─ FilterTransform × 8 processors\n            └─ SourceTransform"
+            " × 8 processors") in pipe
+
+
+def test_explain_aggregate_pipeline_shape():
+    # pipeline_builder_test.rs:25-31
+    txt = E.explain("SELECT sum(number) FROM system.numbers_mt(80000)")
+    assert ("└─ AggregateFinalTransform × 1 processor\n    └─ Merge (AggregatePartialTransform × 8 "
+            "processors) to (MergeProcessor × 1)\n      └─ AggregatePartialTransform × 8 processors\n"
+            "        └─ SourceTransform × 8 processors") in txt
+
+
+# ---- BASELINE configs at oracle-sized N ----------------------------------
+
+AGGS_C3 = [(abi.AGG_SUM, None), (abi.AGG_COUNT, None), (abi.AGG_MAX, None), (abi.AGG_MIN, None)]
+
+
+@pytest.mark.parametrize("n", [1, 7, 8, 9, 16, 10000, 79999, 80000, 100001, 1000000, 12345679])
+def test_c3_matches_oracle(n):
+    r = q("SELECT sum(number)/count(number), max(number), min(number), count(number), sum(number) "
+          "FROM system.numbers_mt(%d)" % n)
+    s, c, mx, mn = oracle(n, AGGS_C3)
+    assert r.rows == [(s // c, mx, mn, c, s)]
+
+
+def test_numbers_mt_row_quirk_counts():
+    # SURVEY finding 8: numbers_mt(100001) yields 20,009 rows, (1000000) 920,008
+    assert q("SELECT count(number) FROM system.numbers_mt(100001)").rows == [(20009,)]
+    assert q("SELECT count(number) FROM system.numbers_mt(1000000)").rows == [(920008,)]
+
+
+@pytest.mark.parametrize("n", [80000, 1000000, 7777777])
+def test_c4_matches_oracle(n):
+    r = q("SELECT max(number+1), count(number+1) FROM system.numbers_mt(%d) WHERE (number%%8)<3" % n)
+    value, _ = chain(abi.DT_UINT64, [("+", 1)])
+    pred = predicate(abi.DT_UINT64, [("%", 8)], "<", 3)
+    exp = oracle(n, [(abi.AGG_MAX, value), (abi.AGG_COUNT, value)], pred)
+    assert r.rows == [tuple(exp)]
+
+
+def test_c1_sum_1e8():
+    assert q("SELECT sum(number) FROM system.numbers_mt(100000000)").rows == [(4999999950000000,)]
+
+
+def test_c2_c3_c4_full_size_closed_forms():
+    # BASELINE.md section 3 expected results at N = 1e10 (80 GB resident)
+    n = 10_000_000_000
+    E.materialize_numbers(n)
+    try:
+        assert q("SELECT sum(number) FROM system.numbers_mt(%d)" % n).rows == [(13106511847580896768,)]
+        assert q("SELECT sum(number)/count(number), max(number), min(number) FROM system.numbers_mt(%d)"
+                 % n).rows == [(1310651184, 9999999999, 0)]
+        assert q("SELECT max(number+1), count(number) FROM system.numbers_mt(%d) WHERE (number%%8)<3"
+                 % n).rows == [(9999999995, 3750000000)]
+    finally:
+        E.release_numbers()
+
+
+# ---- expression shapes beyond the fused chain ------------------------------
+
+def test_non_chain_argument_uses_materialised_path():
+    # (number+1)*(number+2) is a tree, not a chain: eval kernels + identity scan
+    n = 50000
+    r = q("SELECT sum((number+1)*(number+2)), max((number+1)*(number+2)) FROM system.numbers_mt(%d)" % n)
+    exp_sum = sum((i + 1) * (i + 2) for i in range(n)) % 2**64
+    assert r.rows == [(exp_sum, n * (n + 1))]
+
+
+def test_filtered_non_chain_argument():
+    n = 40000
+    r = q("SELECT sum((number+1)*(number+2)), count(number) FROM system.numbers_mt(%d) "
+          "WHERE (number%%7) > 2" % n)
+    keep = [i for i in range(n) if i % 7 > 2]
+    assert r.rows == [(sum((i + 1) * (i + 2) for i in keep) % 2**64, len(keep))]
+
+
+def test_f64_expression_within_tolerance():
+    n = 1_000_000
+    r = q("SELECT sum(number/2.0), max(number*1.5) FROM system.numbers_mt(%d)" % n)
+    exp = sum(i / 2.0 for i in range(n))
+    (s, mx), = r.rows
+    # tolerance: relative 1e-12 (summation order differs from arrow's simd lanes)
+    assert abs(s - exp) <= 1e-12 * exp
+    assert mx == (n - 1) * 1.5
+
+
+def test_sum_over_count_is_integer_division():
+    # SURVEY finding 5 / function_aggregator_test.rs:118-140: UInt64 '/' truncates
+    assert q("SELECT sum(number)/count(number) FROM system.numbers_mt(10)").rows == [(4,)]
+
+
+# ---- error behaviour (texts as the reference formats them) ----------------
+
+def err(sql, eng=None):
+    from fq_amd import FQError
+    with pytest.raises(FQError) as ei:
+        (eng or E).execute(sql)
+    return str(ei.value)
+
+
+def test_error_modulo_disabled_is_reference_behaviour():
+    with Engine(modulo=False) as e2:
+        assert err("SELECT max(number+1) FROM system.numbers_mt(100) WHERE (number%8)<3", e2) == \
+            "Internal Error: Unsupported Function: %"
+
+
+def test_error_filtered_sum_with_empty_block():
+    # number < 5 leaves the second 10,000-row block of partition 0 empty:
+    # arrow sum -> None -> state add fails (data_value_arithmetic.rs)
+    assert err("SELECT sum(number) FROM system.numbers_mt(1000000) WHERE number < 5") == \
+        "Internal Error: DataValue to array cannot be NONE NULL"
+    # count/max survive empty blocks
+    assert q("SELECT count(number), max(number) FROM system.numbers_mt(1000000) WHERE number < 5").rows \
+        == [(5, 4)]
+
+
+def test_error_final_none_to_array():
+    # every partition single-block and empty -> Sum state None -> to_array(1) fails
+    assert err("SELECT sum(number) FROM system.numbers_mt(10) WHERE number > 100") == \
+        "Internal Error: DataValue to array cannot be NONE NULL"
+
+
+def test_error_divide_by_zero():
+    assert err("SELECT sum(number/0) FROM system.numbers_mt(100)") == "Internal Error: Divide by zero error"
+
+
+def test_error_unknown_function_and_table():
+    assert err("SELECT avg(number) FROM system.numbers_mt(100)") == "Internal Error: Unsupported Function: avg"
+    assert err("SELECT number FROM system.numbers(100)") == "Internal Error: Cannot find the table: numbers"
+    assert err("SELECT number FROM numbers_mt(100)") == "Internal Error: Cannot find the database: default"
+    assert err("SELECT sum(number), number FROM system.numbers_mt(10)") == \
+        "Error during plan: Projection references non-aggregate values"
+
+
+def test_error_aggregate_in_where():
+    assert err("SELECT number FROM system.numbers_mt(10) WHERE sum(number) > 1") == \
+        "Internal Error: Aggregate function sum([number]) is found in WHERE in query"
+
+
+# ---- distributed split on one device ---------------------------------------
+
+def test_partial_final_split_matches_single_pipeline():
+    sql = "SELECT sum(number)/count(number), max(number), min(number) FROM system.numbers_mt(1000000)"
+    world = 4
+    states = [E.execute_partial(sql, r, world) for r in range(world)]
+    assert E.execute_final(sql, states).rows == q(sql).rows
+
+
+def test_partial_states_none_error_survives_exchange():
+    # 8 single-block partitions, one per rank: rank 0 holds Some(10), the others
+    # None; only the cross-rank AggregateFinal merge meets Some + None
+    sql = "SELECT sum(number) FROM system.numbers_mt(80) WHERE number < 5"
+    states = [E.execute_partial(sql, r, 8) for r in range(8)]
+    from fq_amd import FQError
+    with pytest.raises(FQError) as ei:
+        E.execute_final(sql, states)
+    assert str(ei.value) == "Internal Error: DataValue to array cannot be NONE NULL"
+
+
+def test_engine_stats_count_fused_scans():
+    with Engine(profile=True) as e2:
+        e2.execute("SELECT sum(number)/count(number), max(number), min(number) FROM system.numbers_mt(800000)")
+        s = e2.stats()
+        assert s["scan_launches"] == 8  # one fused scan per partition for all 4 aggregators
+        assert s["scan_rows"] == 800000 and s["scan_bytes"] == 6400000
+        assert s["scan_ms"] > 0
