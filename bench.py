@@ -16,7 +16,6 @@ column: per partition one fused scan kernel (sum/count/max/min in one read)
 the 48-byte states over xGMI.  Rank 0 prints ONE JSON line.
 """
 import argparse
-import ctypes as C
 import glob
 import json
 import os
@@ -34,7 +33,8 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 from fq_amd import abi, ops  # noqa: E402
-from fq_amd.expr import chain, predicate  # noqa: E402
+from fq_amd import dist as fqd  # noqa: E402
+from fq_amd.engine import Engine  # noqa: E402
 from fq_amd.numbers import BLOCK_SIZE, generate_parts, shard, stream_rows  # noqa: E402
 
 METRIC = "rows/s + achieved HBM GB/s on 10B-row numbers_mt agg, 1/2/4/8 GPUs"
@@ -146,87 +146,38 @@ def main():
 
     rows_per_gpu = int(args.rows_per_gpu)
     n_total = rows_per_gpu * world
-    sql, mask = QUERIES[args.query]
+    sql, _mask = QUERIES[args.query]
     sql = sql.format(N=n_total)
-    parts = generate_parts(n_total)
-    mine = shard(parts, rank, world)
 
-    # ---- materialise my partitions in HBM (SourceTransform, untimed) ----
-    rows = [stream_rows(b, e) for _, b, e in mine]
-    total_rows = sum(rows)
-    # each partition 256-byte aligned inside one allocation
-    offs, o = [], 0
-    for r in rows:
-        offs.append(o)
-        o += ((r * 8 + 255) // 256) * 256
-    buf = torch.empty(max(o, 256), dtype=torch.uint8, device="cuda")
-    cols = []
-    for (_, b, _e), r, off in zip(mine, rows, offs):
-        col = ops.DeviceColumn(buf, r, abi.DT_UINT64, offset=off)
-        from fq_amd._lib import check, lib
-        check(lib.fq_fill_numbers_u64(C.c_void_p(col.ptr), b, r, ops._stream()))
-        cols.append(col)
+    # The engine: SQL -> Source x P -> [Filter] -> AggregatePartial x P -> Merge
+    # -> AggregateFinal on this GPU (one host thread per pipe, fused scans).
+    eng = Engine(device=local, profile=True)
+    mine = shard(generate_parts(n_total), rank, world)
+    total_rows = sum(stream_rows(b, e) for _, b, e in mine)
+    eng.materialize_numbers(n_total, rank, world)  # SourceTransform's column, resident in HBM
     torch.cuda.synchronize()
-    log(rank, "materialised %d partitions, %d rows (%.1f GB) on rank %d" % (len(cols), total_rows,
-                                                                            total_rows * 8 / 1e9, rank))
+    log(rank, "materialised %d partitions, %d rows (%.1f GB) on rank %d"
+        % (len(mine), total_rows, total_rows * 8 / 1e9, rank))
 
-    if args.query == "c4":
-        value, _ = chain(abi.DT_UINT64, [("+", 1)])
-        pred = predicate(abi.DT_UINT64, [("%", 8)], "<", 3)
-    else:
-        value, pred = None, None
+    def step():
+        if world == 1:
+            return list(eng.execute(sql).rows[0])
+        return list(fqd.execute(eng, sql).rows[0])
 
-    ws = [ops.Workspace(ops.lib.fq_aggregate_workspace_bytes(c.len)) for c in cols]
-    slots = torch.empty((max(len(cols), 1), 48), dtype=torch.uint8, device="cuda")
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in cols]
-    xbuf = torch.zeros((world, 6), dtype=torch.int64, device="cuda")
-    kern_ms = [0.0]
-    kern_launches = [0]
-
-    def step(timed):
-        for i, c in enumerate(cols):
-            ev[i][0].record()
-            ops.aggregate_async(c, BLOCK_SIZE, pred, value, mask, ws[i], out=slots[i])
-            ev[i][1].record()
-        host = slots.cpu().numpy().tobytes()  # D2H + sync
-        if timed:
-            for s, e in ev:
-                kern_ms[0] += s.elapsed_time(e)
-            kern_launches[0] += len(cols)
-        states = [abi.fq_agg_state.from_buffer_copy(host[48 * i:48 * (i + 1)]) for i in range(len(cols))]
-        merged = ops.state_merge(states) if states else abi.fq_agg_state(0, 0, U64 - 1, 0, 0, 0, abi.DT_UINT64)
-        if world > 1:
-            # AggregateFinal across GPUs: one RCCL all-reduce (sum) of a
-            # [world, 6] int64 buffer in which every rank fills only its own
-            # row == an all-gather of the 48-byte states, exact for any bits.
-            xbuf.zero_()
-            raw = bytes(merged)
-            xbuf[rank] = torch.frombuffer(bytearray(raw), dtype=torch.int64).to("cuda")
-            dist.all_reduce(xbuf)
-            allb = xbuf.cpu().numpy().tobytes()
-            merged = ops.state_merge([abi.fq_agg_state.from_buffer_copy(allb[48 * r:48 * (r + 1)])
-                                      for r in range(world)])
-        if args.query == "c2":
-            return [merged.sum]
-        if args.query == "c3":
-            return [merged.sum // merged.count, merged.max, merged.min]
-        return [merged.max]
-
-    for _ in range(args.warmup):
-        res = step(False)
-    if args.warmup == 0:
-        res = step(False)
+    for _ in range(max(args.warmup, 1)):
+        res = step()
     expect = closed_form(args.query, n_total)
     if res != expect:
         raise SystemExit("PARITY FAILURE: got %r expected %r" % (res, expect))
     log(rank, "result", res, "== closed form")
 
+    eng.reset_stats()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        res = step(True)
+        res = step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -237,16 +188,19 @@ def main():
         dt = float(t.item())
     assert res == expect
 
-    avg_launch_ms = kern_ms[0] / max(kern_launches[0], 1)
-    rows_per_launch = total_rows / max(len(cols), 1)
-    achieved = rows_per_launch * 8 / (avg_launch_ms * 1e-3) / 1e9  # algorithmic GB/s
+    st = eng.stats()
+    launches = max(st["scan_launches"], 1)
+    avg_launch_ms = st["scan_ms"] / launches
+    bytes_per_launch = st["scan_bytes"] / launches
+    rows_per_launch = st["scan_rows"] / launches
+    achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9  # algorithmic GB/s of the fused scan
     value = n_total * args.steps / dt
     out = None
     if rank == 0:
         traffic = None
         pmc = latest_pmc_traffic("agg_flat_kernel")
         if pmc and pmc[1]:
-            traffic = pmc[0] * rows_per_launch / pmc[1]  # scale to this launch size
+            traffic = pmc[0] * rows_per_launch / pmc[1]  # HBM bytes per launch, scaled to this launch size
         out = {
             "metric": METRIC,
             "value": value,
@@ -266,12 +220,16 @@ def main():
                 "query": args.query,
                 "rows_per_gpu": rows_per_gpu,
                 "rows_total": n_total,
-                "partitions_per_gpu": len(cols),
+                "partitions_per_gpu": len(mine),
                 "block_rows": BLOCK_SIZE,
+                "path": "fq_engine_execute: SQL -> PipelineBuilder -> Source x P -> AggregatePartial x P "
+                        "(fused gfx950 scan) -> Merge -> AggregateFinal"
+                        + ("" if world == 1 else " ; cross-GPU: one RCCL all-reduce of partial states"),
                 "parallelism": "dp%d (numbers_mt partitions sharded, RCCL all-reduce of states)" % world,
             },
             "achieved_hbm_gbps": achieved,
             "kernel_ms_per_launch": avg_launch_ms,
+            "scan_launches_per_step": st["scan_launches"] / args.steps,
             "roofline": {
                 "bound": "hbm",
                 "achieved": achieved,
@@ -279,8 +237,8 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBPS,
                 "traffic": traffic,
-                "kernel": "agg_flat_kernel (fq_aggregate scan) + finalize, per partition launch",
-                "bytes_per_launch": rows_per_launch * 8,
+                "kernel": "fq_aggregate fused scan (agg_flat_kernel + finalize), one launch per partition",
+                "bytes_per_launch": bytes_per_launch,
             },
             "result": res,
         }
@@ -293,6 +251,7 @@ def main():
             out["cpu_baseline"] = {"error": repr(e)}
     if rank == 0:
         print(json.dumps(out), flush=True)
+    eng.close()
     if world > 1:
         dist.destroy_process_group()
 

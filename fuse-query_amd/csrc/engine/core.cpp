@@ -280,6 +280,7 @@ const DataField &DataSchema::field_with_name(const std::string &name) const { re
 // runtime
 // ---------------------------------------------------------------------------
 Runtime::Runtime(int device) : device_(device) {
+    if (device == kHostOnly) return;  // planning / AggregateFinal merges only
     int n = 0;
     hipError_t e = hipGetDeviceCount(&n);
     if (e != hipSuccess || n <= device || device < 0)
@@ -291,6 +292,7 @@ Runtime::Runtime(int device) : device_(device) {
 
 void Runtime::set_streams(int n) {
     std::lock_guard<std::mutex> lk(mu_);
+    if (device_ == kHostOnly) return;
     if (n < 1) n = 1;
     while ((int)shared_.size() < n) {
         hipStream_t s;
@@ -310,6 +312,10 @@ WorkerRes *Runtime::acquire() {
         return w;
     }
     auto w = std::make_unique<WorkerRes>();
+    if (device_ == kHostOnly) {
+        all_.push_back(std::move(w));
+        return all_.back().get();
+    }
     w->stream = shared_[next_shared_++ % (size_t)active_streams_];
     w->ws_bytes = fq_aggregate_workspace_bytes(0);
     check_hip(hipMalloc(&w->ws, w->ws_bytes), "hipMalloc(workspace)");
@@ -323,6 +329,7 @@ void Runtime::release(WorkerRes *w) {
 }
 
 Runtime::~Runtime() {
+    if (device_ == kHostOnly) return;
     (void)hipSetDevice(device_);
     for (auto &s : shared_) (void)hipStreamSynchronize(s);
     for (auto &w : all_) {
@@ -332,13 +339,23 @@ Runtime::~Runtime() {
     for (auto &s : shared_) (void)hipStreamDestroy(s);
 }
 
+static thread_local ExecCtx *g_current = nullptr;
+
 DeviceBuffer::~DeviceBuffer() {
     if (!ptr) return;
     if (async) (void)hipFreeAsync(ptr, stream);
     else (void)hipFree(ptr);
 }
 
+static void require_device() {
+    ExecCtx *c = ExecCtx::current_or_null();
+    if (c && !c->rt->has_device())
+        throw FQException(FQ_E_HIP, "fq_engine: this engine has no device (created with device -1); "
+                                    "the hot path has no CPU fallback");
+}
+
 std::shared_ptr<DeviceBuffer> DeviceBuffer::alloc(size_t bytes, hipStream_t st) {
+    require_device();
     auto b = std::make_shared<DeviceBuffer>();
     b->bytes = bytes < 256 ? 256 : bytes;
     b->stream = st;
@@ -351,6 +368,7 @@ std::shared_ptr<DeviceBuffer> DeviceBuffer::alloc(size_t bytes, hipStream_t st) 
 }
 
 std::shared_ptr<DeviceBuffer> DeviceBuffer::alloc_sync(size_t bytes) {
+    require_device();
     auto b = std::make_shared<DeviceBuffer>();
     b->bytes = bytes < 256 ? 256 : bytes;
     b->async = false;
@@ -358,10 +376,8 @@ std::shared_ptr<DeviceBuffer> DeviceBuffer::alloc_sync(size_t bytes) {
     return b;
 }
 
-static thread_local ExecCtx *g_current = nullptr;
-
 ExecCtx::ExecCtx(Runtime *r) : rt(r), res(nullptr), prev_(g_current) {
-    check_hip(hipSetDevice(rt->device()), "hipSetDevice");
+    if (rt->has_device()) check_hip(hipSetDevice(rt->device()), "hipSetDevice");
     res = rt->acquire();
     g_current = this;
 }
@@ -371,12 +387,16 @@ ExecCtx::~ExecCtx() {
     rt->release(res);
 }
 
+ExecCtx *ExecCtx::current_or_null() { return g_current; }
+
 ExecCtx &ExecCtx::current() {
     if (!g_current) throw_internal("no device execution context on this thread");
     return *g_current;
 }
 
-void ExecCtx::sync() { check_hip(hipStreamSynchronize(stream()), "hipStreamSynchronize"); }
+void ExecCtx::sync() {
+    if (rt->has_device()) check_hip(hipStreamSynchronize(stream()), "hipStreamSynchronize");
+}
 
 // ---------------------------------------------------------------------------
 // columns / blocks

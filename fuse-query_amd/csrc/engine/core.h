@@ -136,7 +136,9 @@ struct WorkerRes {
 
 class Runtime {
    public:
+    static constexpr int kHostOnly = -1;  // no GPU: planning and AggregateFinal merges only
     explicit Runtime(int device);
+    bool has_device() const { return device_ != kHostOnly; }
     ~Runtime();
     int device() const { return device_; }
     WorkerRes *acquire();
@@ -178,6 +180,7 @@ class ExecCtx {
     ExecCtx(const ExecCtx &) = delete;
     ExecCtx &operator=(const ExecCtx &) = delete;
     static ExecCtx &current();  // throws when no context is bound on this thread
+    static ExecCtx *current_or_null();
     Runtime *rt;
     WorkerRes *res;
     AggFusion *fusion = nullptr;  // set while an AggregatePartial drains its input

@@ -51,7 +51,11 @@ typedef struct fq_engine_stats {
     uint64_t queries;
 } fq_engine_stats;
 
-/* device: HIP device ordinal.  Fails with FQ_E_HIP when no GPU is present. */
+/* device: HIP device ordinal.  Fails with FQ_E_HIP when no GPU is present.
+ * device = -1 creates a host-only engine: SQL planning, EXPLAIN and
+ * fq_engine_execute_final (the AggregateFinal merge of exchanged states,
+ * which the reference also runs on the host) work; anything that touches a
+ * column fails with FQ_E_HIP -- there is no CPU fallback for the hot path. */
 fq_status fq_engine_create(int32_t device, fq_engine **out);
 void fq_engine_destroy(fq_engine *e);
 fq_status fq_engine_set_option(fq_engine *e, int32_t option, int64_t value);

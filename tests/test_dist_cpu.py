@@ -1,0 +1,76 @@
+"""CPU, world_size 2 (and 3) over gloo: the multi-GPU path minus the GPU.
+Each rank owns its numbers_mt shard [8r/G, 8(r+1)/G) (fq_amd.numbers.shard),
+ships its merged partial states through fq_amd.dist.allgather_states (the
+same single all-reduce bench.py runs over RCCL), and every rank's
+AggregateFinal merge must equal the single-process oracle result.  The
+per-rank partial states come from the oracle: without a GPU the scan cannot
+run, and there is no CPU fallback to run it with."""
+import os
+import socket
+import sys
+
+import pytest
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+SQL = ("SELECT sum(number)/count(number), max(number), min(number), count(number) "
+       "FROM system.numbers_mt(%d)")
+
+
+def worker(rank, world, port, n, out_q):
+    for p in (os.path.join(ROOT, "fuse-query_amd"), os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")):
+        sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+
+    import fq_ref as R
+    from fq_amd import dist as fqd
+    from fq_amd.engine import Engine
+    from fq_amd.numbers import generate_parts, shard
+    from test_engine_cpu import encode_states
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        num = R.E_field("number")
+        exprs = [R.E_bin("/", R.E_fn("sum", num), R.E_fn("count", num)), R.E_fn("max", num),
+                 R.E_fn("min", num), R.E_fn("count", num)]
+        mine = [(b, e) for _, b, e in shard(generate_parts(n), rank, world)]
+        local = encode_states(R.aggregate_partial_states(n, exprs, mine))
+        everyone = fqd.allgather_states(local)
+        with Engine(device=-1) as eng:
+            rows = eng.execute_final(SQL % n, everyone).rows
+        out_q.put((rank, rows, [len(s) for s in everyone]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n", [(2, 1000000), (2, 7), (3, 123457)])
+def test_sharded_exchange_and_final_merge(world, n):
+    import fq_ref as R
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=worker, args=(r, world, port, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    num = R.E_field("number")
+    exp = [tuple(v.value for v in R.aggregate_query(n, [
+        R.E_bin("/", R.E_fn("sum", num), R.E_fn("count", num)), R.E_fn("max", num), R.E_fn("min", num),
+        R.E_fn("count", num)]))]
+    for rank, rows, lens in results:
+        assert rows == exp, (rank, rows, exp)

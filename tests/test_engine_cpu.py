@@ -1,0 +1,136 @@
+"""CPU: the engine's host-side layers without a GPU (device = -1): SQL
+planning, EXPLAIN text, plan-time error texts, and the AggregateFinal merge of
+exchanged partial states.  Anything that would touch a column must fail
+loudly -- there is no CPU fallback for the hot path."""
+import struct
+
+import pytest
+
+import fq_ref as R
+from fq_amd import FQError, abi
+from fq_amd.engine import Engine
+from fq_amd.expr import to_bits
+from fq_amd.numbers import generate_parts, shard
+
+README_SQL = ("select (number+1) as c1, number/2 as c2 from system.numbers_mt(10000000) "
+              "where ((number+1)+(number/2)+1) < 100 limit 3")
+
+
+@pytest.fixture(scope="module")
+def eng():
+    e = Engine(device=-1)
+    yield e
+    e.close()
+
+
+def encode_states(per_func):
+    """The engine's partial-state wire format (pipeline.cpp encode_states)."""
+    out = b"FQS1" + struct.pack("<I", len(per_func))
+    for vals in per_func:
+        out += struct.pack("<II", len(vals), 0)
+        for v in vals:
+            kind = 0 if v.type == "Null" else (1 if v.value is None else 2)
+            dt = abi.DT_BY_NAME[v.type] if kind else 0
+            out += struct.pack("<iiQ", kind, dt, to_bits(v.value, dt) if kind == 2 else 0)
+    return out
+
+
+def test_explain_plan_and_pipeline_text(eng):
+    # README.md:98-113 (plan + pipeline display)
+    txt = eng.explain(README_SQL)
+    assert txt == (
+        "└─ Limit: 3\n  └─ Projection: (number + 1) as c1, (number / 2) as c2\n"
+        "    └─ Filter: ((((number + 1) + (number / 2)) + 1) < 100)\n"
+        "      └─ ReadDataSource: scan parts [8](Read from system.numbers_mt table)\n"
+        "\n  └─ LimitTransform × 1 processor\n    └─ Merge (LimitTransform × 8 processors) to (MergeProcessor × 1)"
+        "\n      └─ LimitTransform × 8 processors\n        └─ ProjectionTransform × 8 processors"
+        "\n          └─ FilterTransform × 8 processors\n            └─ SourceTransform × 8 processors")
+
+
+def test_explain_worker_threads_chunking():
+    # pipeline_builder.rs:75-84: workers < partitions -> chunks of parts/workers per source
+    with Engine(device=-1, worker_threads=2) as e:
+        txt = e.explain("SELECT sum(number) FROM system.numbers_mt(1000)")
+    assert "AggregatePartialTransform × 2 processors" in txt and "SourceTransform × 2 processors" in txt
+
+
+def test_small_n_single_partition(eng):
+    assert "scan parts [1]" in eng.explain("SELECT sum(number) FROM system.numbers_mt(7)")
+
+
+@pytest.mark.parametrize("sql,msg", [
+    ("SELECT max(number) FROM system.numbers_mt(10) WHERE number %% 8 < 3", None),
+    ("SELECT avg(number) FROM system.numbers_mt(10)", "Internal Error: Unsupported Function: avg"),
+    ("SELECT number FROM system.nope(10)", "Internal Error: Cannot find the table: nope"),
+    ("SELECT number FROM nope.numbers_mt(10)", "Internal Error: Cannot find the database: nope"),
+    ("SELECT number FROM numbers_mt(10)", "Internal Error: Cannot find the database: default"),
+    ("SELECT sum(number), number FROM system.numbers_mt(10)",
+     "Error during plan: Projection references non-aggregate values"),
+    ("SELECT sum(number) FROM system.numbers_mt(10) HAVING sum(number) > 1",
+     "Internal Error: HAVING is not implemented yet"),
+    ("SELECT number FROM system.numbers_mt(10) LIMIT 1.5",
+     "Error during plan: Unexpected expression for LIMIT clause"),
+    ("SELECT sum(number) + 'a' FROM system.numbers_mt(10)", "Internal Error: Unsupported (UInt64) + (Utf8)"),
+    ("SELECT nope FROM system.numbers_mt(10)",
+     'Internal Error: Invalid argument error: Unable to get field named "nope". Valid fields: ["number"]'),
+])
+def test_plan_time_errors(eng, sql, msg):
+    sql = sql.replace("%%", "%")
+    if msg is None:
+        eng.explain(sql)  # '%' is accepted (extension on by default)
+        return
+    with pytest.raises(FQError) as ei:
+        eng.explain(sql)
+    assert str(ei.value) == msg
+
+
+def test_modulo_off_matches_reference_error():
+    with Engine(device=-1, modulo=False) as e:
+        with pytest.raises(FQError) as ei:
+            e.explain("SELECT max(number+1) FROM system.numbers_mt(100) WHERE (number%8)<3")
+    assert str(ei.value) == "Internal Error: Unsupported Function: %"
+
+
+def test_host_only_engine_has_no_cpu_fallback(eng):
+    with pytest.raises(FQError) as ei:
+        eng.execute("SELECT sum(number) FROM system.numbers_mt(10)")
+    assert ei.value.status == abi.FQ_E_HIP
+
+
+def test_result_column_names_follow_function_debug(eng):
+    n = R.E_field("number")
+    exprs = [R.E_bin("/", R.E_fn("sum", n), R.E_fn("count", n)), R.E_fn("max", n), R.E_fn("min", n)]
+    states = [encode_states(R.aggregate_partial_states(80, exprs, [(b, e) for _, b, e in generate_parts(80)]))]
+    r = eng.execute_final("SELECT sum(number)/count(number), max(number), min(number) "
+                          "FROM system.numbers_mt(80)", states)
+    assert r.names == ["Sum(number) / Count(number)", "Max(number)", "Min(number)"]
+    assert r.rows == [(39, 79, 0)]
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+@pytest.mark.parametrize("n", [7, 80000, 1000000, 123457])
+def test_final_merge_of_sharded_partials_matches_oracle(eng, world, n):
+    num = R.E_field("number")
+    exprs = [R.E_bin("/", R.E_fn("sum", num), R.E_fn("count", num)), R.E_fn("max", num), R.E_fn("min", num),
+             R.E_bin("+", R.E_fn("sum", R.E_bin("*", num, R.E_const(3))), R.E_const(1))]
+    sql = ("SELECT sum(number)/count(number), max(number), min(number), sum(number*3)+1 "
+           "FROM system.numbers_mt(%d)" % n)
+    parts = generate_parts(n)
+    states = [encode_states(R.aggregate_partial_states(n, exprs, [(b, e) for _, b, e in shard(parts, r, world)]))
+              for r in range(world)]
+    got = eng.execute_final(sql, states).rows
+    exp = [tuple(v.value for v in R.aggregate_query(n, exprs))]
+    assert got == exp
+
+
+def test_final_merge_none_error(eng):
+    # one rank Some(10), the others None: only the cross-rank merge fails
+    num = R.E_field("number")
+    where = R.E_bin("<", num, R.E_const(5))
+    parts = generate_parts(80)
+    states = [encode_states(R.aggregate_partial_states(80, [R.E_fn("sum", num)], [(b, e) for _, b, e in
+                                                                                    shard(parts, r, 8)], where))
+              for r in range(8)]
+    with pytest.raises(FQError) as ei:
+        eng.execute_final("SELECT sum(number) FROM system.numbers_mt(80) WHERE number < 5", states)
+    assert str(ei.value) == "Internal Error: DataValue to array cannot be NONE NULL"
