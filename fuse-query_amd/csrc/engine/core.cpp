@@ -298,6 +298,7 @@ void Runtime::set_streams(int n) {
         hipStream_t s;
         check_hip(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreateWithFlags");
         shared_.push_back(s);
+        shared_mu_.push_back(std::make_unique<std::mutex>());
     }
     // existing workers keep their queue; new ones pick round-robin among the first n
     next_shared_ = 0;
@@ -316,7 +317,9 @@ WorkerRes *Runtime::acquire() {
         all_.push_back(std::move(w));
         return all_.back().get();
     }
-    w->stream = shared_[next_shared_++ % (size_t)active_streams_];
+    const size_t q = next_shared_++ % (size_t)active_streams_;
+    w->stream = shared_[q];
+    w->launch_mu = shared_mu_[q].get();
     w->ws_bytes = fq_aggregate_workspace_bytes(0);
     check_hip(hipMalloc(&w->ws, w->ws_bytes), "hipMalloc(workspace)");
     all_.push_back(std::move(w));
@@ -335,8 +338,55 @@ Runtime::~Runtime() {
     for (auto &w : all_) {
         if (w->ws) (void)hipFree(w->ws);
         for (auto ev : w->events) (void)hipEventDestroy(ev);
+        for (auto *c : w->slot_chunks) (void)hipHostFree(c);
     }
     for (auto &s : shared_) (void)hipStreamDestroy(s);
+}
+
+hipEvent_t WorkerRes::take_event() {
+    if (!events.empty()) {
+        hipEvent_t e = events.back();
+        events.pop_back();
+        return e;
+    }
+    hipEvent_t e;
+    check_hip(hipEventCreate(&e), "hipEventCreate");
+    return e;
+}
+
+// ---------------------------------------------------------------------------
+// thread pool
+// ---------------------------------------------------------------------------
+void ThreadPool::submit(std::function<void()> task) {
+    std::unique_lock<std::mutex> lk(mu_);
+    queue_.push_back(std::move(task));
+    if (idle_ < queue_.size()) threads_.emplace_back([this] { run(); });  // never wait for a thread
+    else cv_.notify_one();
+}
+
+void ThreadPool::run() {
+    std::unique_lock<std::mutex> lk(mu_);
+    for (;;) {
+        ++idle_;
+        cv_.wait(lk, [&] { return stop_ || !queue_.empty(); });
+        --idle_;
+        if (queue_.empty()) return;  // stop_
+        std::function<void()> t = std::move(queue_.front());
+        queue_.pop_front();
+        lk.unlock();
+        t();
+        lk.lock();
+    }
+}
+
+ThreadPool::~ThreadPool() {
+    {
+        std::lock_guard<std::mutex> lk(mu_);
+        stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto &t : threads_)
+        if (t.joinable()) t.join();
 }
 
 static thread_local ExecCtx *g_current = nullptr;

@@ -15,6 +15,9 @@
 #include <stdint.h>
 
 #include <atomic>
+#include <condition_variable>
+#include <deque>
+#include <thread>
 #include <functional>
 #include <memory>
 #include <mutex>
@@ -128,10 +131,34 @@ struct EngineStats {
 
 struct WorkerRes {
     hipStream_t stream = nullptr;
-    bool own_stream = false;
-    void *ws = nullptr;  // fq_aggregate workspace
+    std::mutex *launch_mu = nullptr;  // serialises multi-call enqueues on a shared queue
+    void *ws = nullptr;               // fq_aggregate workspace
     size_t ws_bytes = 0;
-    std::vector<hipEvent_t> events;  // profiling pairs
+    std::vector<hipEvent_t> events;   // reusable events (timing pairs, completion)
+    // Pinned, device-visible result slots: the scan's finalize kernel writes
+    // its fq_agg_state straight to host memory, so no copy is queued behind
+    // the next partition's scan.  Chunks of kSlotChunk, reused across queries.
+    static constexpr size_t kSlotChunk = 64;
+    std::vector<fq_agg_state *> slot_chunks;
+    hipEvent_t take_event();
+    void give_event(hipEvent_t e) { events.push_back(e); }
+};
+
+// Persistent host threads for the pipes (the reference spawns tokio tasks per
+// query, processor_merge.rs:49); a submitted task never waits for a thread.
+class ThreadPool {
+   public:
+    ~ThreadPool();
+    void submit(std::function<void()> task);
+
+   private:
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::vector<std::thread> threads_;
+    std::deque<std::function<void()>> queue_;
+    size_t idle_ = 0;
+    bool stop_ = false;
+    void run();
 };
 
 class Runtime {
@@ -146,6 +173,7 @@ class Runtime {
     void set_streams(int n);
     EngineStats stats;
     std::atomic<bool> profile{false};
+    ThreadPool pool;
 
    private:
     int device_;
@@ -153,6 +181,7 @@ class Runtime {
     std::vector<std::unique_ptr<WorkerRes>> all_;
     std::vector<WorkerRes *> free_;
     std::vector<hipStream_t> shared_;  // FQ_OPT_STREAMS queues shared by the pipes
+    std::vector<std::unique_ptr<std::mutex>> shared_mu_;
     size_t next_shared_ = 0;
     int active_streams_ = 1;
 };

@@ -553,31 +553,49 @@ DataBlock materialize(const DataBlock &b, ExecCtx &ctx) {
 // ---------------------------------------------------------------------------
 // AggFusion
 // ---------------------------------------------------------------------------
-static constexpr size_t kSlotChunk = 64;
-
 AggFusion::AggFusion(ExecCtx &ctx) : ctx_(ctx) {}
 
 AggFusion::~AggFusion() {
+    // an exception left scans in flight: they write into this worker's pinned
+    // slots, which the next query reuses -- let them land first
+    if (launched_ && !finished_) {
+        try {
+            wait_launched();
+        } catch (...) {
+        }
+    }
     for (auto &p : events_) {
-        ctx_.res->events.push_back(p.first);
-        ctx_.res->events.push_back(p.second);
+        ctx_.res->give_event(p.first);
+        ctx_.res->give_event(p.second);
     }
 }
 
+fq_agg_state *AggFusion::slot_host(size_t k) const {
+    return ctx_.res->slot_chunks[k / WorkerRes::kSlotChunk] + k % WorkerRes::kSlotChunk;
+}
+
 size_t AggFusion::alloc_slot() {
-    if (nslots_ == cap_) {
-        // grow: a new buffer holding every slot so far + a chunk, old contents
-        // copied on the stream (kernels already queued wrote to the old one)
-        const size_t ncap = cap_ + kSlotChunk;
-        auto nb = DeviceBuffer::alloc(ncap * sizeof(fq_agg_state), ctx_.stream());
-        if (slots_ && nslots_)
-            check_hip(hipMemcpyAsync(nb->ptr, slots_->ptr, nslots_ * sizeof(fq_agg_state), hipMemcpyDeviceToDevice,
-                                     ctx_.stream()),
-                      "hipMemcpyAsync(D2D)");
-        slots_ = nb;
-        cap_ = ncap;
+    const size_t k = nslots_++;
+    auto &chunks = ctx_.res->slot_chunks;
+    while (chunks.size() * WorkerRes::kSlotChunk <= k) {
+        void *p = nullptr;
+        check_hip(hipHostMalloc(&p, WorkerRes::kSlotChunk * sizeof(fq_agg_state),
+                                hipHostMallocMapped | hipHostMallocCoherent),
+                  "hipHostMalloc(result slots)");
+        chunks.push_back((fq_agg_state *)p);
     }
-    return nslots_++;
+    return k;
+}
+
+void AggFusion::wait_launched() {
+    hipEvent_t done = ctx_.res->take_event();
+    {
+        std::lock_guard<std::mutex> lk(*ctx_.res->launch_mu);
+        check_hip(hipEventRecord(done, ctx_.stream()), "hipEventRecord");
+    }
+    hipError_t e = hipEventSynchronize(done);
+    ctx_.res->give_event(done);
+    check_hip(e, "hipEventSynchronize");
 }
 
 void AggFusion::add_error(const FQException &e) {
@@ -635,26 +653,25 @@ void AggFusion::end_block() {
     const bool prof = ctx_.rt->profile.load();
     for (Group &g : cur_) {
         fq_col c = g.col.abi();
+        void *dst = nullptr;
+        check_hip(hipHostGetDevicePointer(&dst, slot_host(g.slot), 0), "hipHostGetDevicePointer");
         hipEvent_t e0 = nullptr, e1 = nullptr;
         if (prof) {
-            for (hipEvent_t *e : {&e0, &e1}) {
-                if (!ctx_.res->events.empty()) {
-                    *e = ctx_.res->events.back();
-                    ctx_.res->events.pop_back();
-                } else {
-                    check_hip(hipEventCreate(e), "hipEventCreate");
-                }
-            }
-            check_hip(hipEventRecord(e0, ctx_.stream()), "hipEventRecord");
+            e0 = ctx_.res->take_event();
+            e1 = ctx_.res->take_event();
         }
-        fq_agg_state *dst = (fq_agg_state *)slots_->ptr + g.slot;
-        check_fq(fq_aggregate(&c, g.block_rows, g.has_pred ? &g.pred : nullptr,
-                              g.value.expr.n_steps ? &g.value.expr : nullptr, g.mask, dst, ctx_.res->ws,
-                              ctx_.res->ws_bytes, ctx_.stream()));
-        if (prof) {
-            check_hip(hipEventRecord(e1, ctx_.stream()), "hipEventRecord");
-            events_.push_back({e0, e1});
+        {
+            // events and the scan's two kernels enqueue back to back even when
+            // other pipes share this queue, so the event pair brackets this scan
+            std::lock_guard<std::mutex> lk(*ctx_.res->launch_mu);
+            if (prof) check_hip(hipEventRecord(e0, ctx_.stream()), "hipEventRecord");
+            check_fq(fq_aggregate(&c, g.block_rows, g.has_pred ? &g.pred : nullptr,
+                                  g.value.expr.n_steps ? &g.value.expr : nullptr, g.mask, (fq_agg_state *)dst,
+                                  ctx_.res->ws, ctx_.res->ws_bytes, ctx_.stream()));
+            if (prof) check_hip(hipEventRecord(e1, ctx_.stream()), "hipEventRecord");
         }
+        launched_ = true;
+        if (prof) events_.push_back({e0, e1});
         ctx_.rt->stats.scan_launches++;
         ctx_.rt->stats.scan_rows += (uint64_t)g.col.len;
         ctx_.rt->stats.scan_bytes += (uint64_t)g.col.len * (uint64_t)dtype_size(g.col.dtype);
@@ -665,12 +682,8 @@ void AggFusion::end_block() {
 
 void AggFusion::finish() {
     end_block();
-    std::vector<fq_agg_state> host(nslots_);
-    if (nslots_)
-        check_hip(hipMemcpyAsync(host.data(), slots_->ptr, nslots_ * sizeof(fq_agg_state), hipMemcpyDeviceToHost,
-                                 ctx_.stream()),
-                  "hipMemcpyAsync(D2H)");
-    ctx_.sync();
+    if (launched_) wait_launched();  // only this pipe's scans, not the whole queue
+    finished_ = true;
     for (auto &p : events_) {
         float ms = 0;
         if (hipEventElapsedTime(&ms, p.first, p.second) == hipSuccess)
@@ -682,7 +695,7 @@ void AggFusion::finish() {
         fq_agg_state st = en.st;
         if (en.slot != (size_t)-1) {
             const uint64_t blocks = en.st.blocks;
-            st = host[en.slot];
+            memcpy(&st, slot_host(en.slot), sizeof st);
             st.blocks = blocks;
         }
         en.agg->accumulate_summary(st);

@@ -263,11 +263,12 @@ class AggFusion {
     std::vector<Group> cur_;
     std::vector<Entry> log_;
     std::vector<Column> keepalive_;
-    std::shared_ptr<DeviceBuffer> slots_;
-    size_t nslots_ = 0, cap_ = 0;
+    size_t nslots_ = 0;
+    bool launched_ = false, finished_ = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> events_;
-    std::vector<uint64_t> event_bytes_;
     size_t alloc_slot();
+    fq_agg_state *slot_host(size_t k) const;
+    void wait_launched();
 };
 
 // evaluate a predicate over a block into a Boolean column (the non-fused path)

@@ -204,16 +204,18 @@ struct Channel {
         closed = true;
         cv_send.notify_all();
     }
+    void wait_all_done() {
+        std::unique_lock<std::mutex> lk(mu);
+        cv_recv.wait(lk, [&] { return live == 0; });
+    }
 };
 
 class ChannelStream : public BlockStream {
    public:
     std::shared_ptr<Channel> ch;
-    std::vector<std::thread> threads;
     ~ChannelStream() override {
         ch->close();
-        for (auto &t : threads)
-            if (t.joinable()) t.join();
+        ch->wait_all_done();  // every pipe task has released its device context
     }
     bool next(DataBlock &out) override {
         Channel::Item it;
@@ -237,7 +239,7 @@ StreamRef MergeProcessor::execute() {
     for (auto &input : list_) {
         std::shared_ptr<Channel> ch = cs->ch;
         ProcessorRef in = input;
-        cs->threads.emplace_back([in, ch, rt]() {
+        rt->pool.submit([in, ch, rt]() {
             try {
                 ExecCtx ctx(rt);
                 StreamRef s = in->execute();
