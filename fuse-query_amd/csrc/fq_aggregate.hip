@@ -166,22 +166,29 @@ __global__ void __launch_bounds__(kThreads)
     const u32x4 *__restrict__ vp = reinterpret_cast<const u32x4 *>(col + head);
     constexpr uint32_t kFull = (E == 32) ? 0xffffffffu : ((1u << E) - 1u);
 
-    int64_t v = g;
-    for (; v + (int64_t)(U - 1) * T < nvec; v += (int64_t)U * T) {
+    // Tile-contiguous streaming: a workgroup reads one contiguous tile of
+    // U * 256 vectors (16 KB for u64 at U=4) per iteration, non-temporal,
+    // and strides over tiles by the grid.  Measured on MI355X against the
+    // vector-granular grid stride: 7.2 vs 6.2 TB/s (tools/tune_scan.py,
+    // profiles/r01_tune_*.json); few workgroups per CU (see launch) helps too.
+    constexpr int64_t TV = (int64_t)U * kThreads;
+    const int64_t ntiles = nvec / TV;
+    for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const int64_t base = t * TV + threadIdx.x;
         u32x4 raw[U];
 #pragma unroll
-        for (int k = 0; k < U; ++k) raw[k] = __builtin_nontemporal_load(vp + v + (int64_t)k * T);
+        for (int k = 0; k < U; ++k) raw[k] = __builtin_nontemporal_load(vp + base + (int64_t)k * kThreads);
         TIn x[E];
         int64_t idx[E];
 #pragma unroll
         for (int k = 0; k < U; ++k) {
             __builtin_memcpy(&x[k * VE], &raw[k], 16);
 #pragma unroll
-            for (int e = 0; e < VE; ++e) idx[k * VE + e] = head + (v + (int64_t)k * T) * VE + e;
+            for (int e = 0; e < VE; ++e) idx[k * VE + e] = head + (base + (int64_t)k * kThreads) * VE + e;
         }
         process<TIn, V, PRED, CHAIN, E>(x, idx, kFull, pred, val, mask, acc);
     }
-    for (; v < nvec; v += T) {
+    for (int64_t v = ntiles * TV + g; v < nvec; v += T) {
         const u32x4 raw = __builtin_nontemporal_load(vp + v);
         TIn x[VE];
         int64_t idx[VE];
@@ -277,6 +284,16 @@ __global__ void __launch_bounds__(kThreads)
 // ---------------------------------------------------------------------------
 
 static bool is_pow2(uint64_t v) { return v && !(v & (v - 1)); }
+
+// Workgroups per CU for the flat scan; FQ_SCAN_WG_PER_CU overrides (tuning).
+static int scan_wg_per_cu() {
+    static const int v = [] {
+        const char *e = getenv("FQ_SCAN_WG_PER_CU");
+        const int x = e ? atoi(e) : 0;
+        return (x >= 1 && x <= 16) ? x : 2;
+    }();
+    return v;
+}
 
 // libdivide's u64 round-up magic (branchful form)
 static void u64_magic(uint64_t d, uint64_t &magic, uint32_t &shift, uint32_t &add) {
@@ -581,9 +598,12 @@ fq_status fq_aggregate(const fq_col *col, int64_t block_rows, const fq_pred *pre
         if (head > col->len) head = col->len;
         L.head = head;
         const int64_t nvec = (col->len - head) / vec_elems;
-        int64_t grid = (nvec + (int64_t)kThreads * 4 - 1) / ((int64_t)kThreads * 4);
+        const int64_t tile = (int64_t)kThreads * (esize >= 4 ? 4 : (esize == 2 ? 2 : 1));
+        int64_t grid = (nvec + tile - 1) / tile;
         if (grid < 1) grid = 1;
-        L.grid = (int)(grid < max_grid ? grid : max_grid);
+        // 2 workgroups (8 waves) per CU streamed fastest (tools/tune_scan.py)
+        const int64_t flat_max = (int64_t)cus * scan_wg_per_cu();
+        L.grid = (int)(grid < flat_max ? grid : flat_max);
     }
     fq_status s = dispatch(col->dtype, L, chain);
     if (s != FQ_OK) return s;
