@@ -22,11 +22,9 @@
 
 #include "fq_common.h"
 #include "fq_device.h"
+#include "fq_scan.h"
 
 namespace fqk {
-
-constexpr int kThreads = 256;       // 4 waves per workgroup
-constexpr int kMaxPartials = 4096;  // workgroups per launch upper bound
 
 template <typename V>
 struct Acc {
@@ -413,21 +411,6 @@ fq_status lower_expr(const fq_expr &e, int32_t col_dtype, KProg &out, int32_t &r
     return FQ_OK;
 }
 
-struct Launch {
-    const void *col;
-    int64_t n;
-    int64_t head;
-    int64_t block_rows;
-    bool block_mode;
-    KPred pred;
-    KProg val;
-    uint32_t mask;
-    int32_t vdtype;
-    Partial *parts;
-    int grid;
-    hipStream_t stream;
-};
-
 template <typename TIn, typename V, int PRED, bool CHAIN>
 static fq_status launch_scan(const Launch &L) {
     // vectors in flight per lane: 64 B for 64-bit columns, 16 elements otherwise
@@ -521,32 +504,34 @@ size_t fq_aggregate_workspace_bytes(int64_t len) {
     return (size_t)fqk::kMaxPartials * sizeof(fqk::Partial);
 }
 
-fq_status fq_aggregate(const fq_col *col, int64_t block_rows, const fq_pred *pred, const fq_expr *value,
-                       uint32_t agg_mask, fq_agg_state *d_out, void *d_ws, size_t ws_bytes, void *stream) {
-    using namespace fqk;
-    if (!col || !d_out || !d_ws) return fqc::fail(FQ_E_INVALID, "fq_aggregate: NULL argument");
+}  // extern "C"
+
+namespace fqk {
+
+// Validates the arguments and prepares the launch shared by fq_aggregate and
+// fq_jit_prepare (lowered programs, flat/block mode, grid).
+static fq_status plan_scan(const fq_col *col, int64_t block_rows, const fq_pred *pred, const fq_expr *value,
+                           uint32_t agg_mask, bool need_data, Launch &L, bool &chain, uint64_t &blocks,
+                           int &empty_if_zero) {
+    if (!col) return fqc::fail(FQ_E_INVALID, "fq_aggregate: NULL argument");
     if (col->len < 0) return fqc::fail(FQ_E_INVALID, "fq_aggregate: negative length");
-    if (ws_bytes < fq_aggregate_workspace_bytes(col->len))
-        return fqc::fail(FQ_E_INVALID, "fq_aggregate: workspace too small");
     const int esize = fqc::dtype_size(col->dtype);
     if (!fqc::dtype_is_numeric(col->dtype))
         return fqc::internal(std::string("Unsupported data_array_aggregate for data type: ") +
                              fqc::dtype_name(col->dtype));
-    if (col->len > 0 && !col->data) return fqc::fail(FQ_E_INVALID, "fq_aggregate: NULL column data");
+    if (need_data && col->len > 0 && !col->data) return fqc::fail(FQ_E_INVALID, "fq_aggregate: NULL column data");
     if (((uintptr_t)col->data) % esize)
         return fqc::fail(FQ_E_INVALID, "fq_aggregate: column not aligned to its element size");
     if (block_rows <= 0) block_rows = col->len > 0 ? col->len : 1;
 
-    Launch L{};
+    L = Launch{};
     L.col = col->data;
     L.n = col->len;
     L.block_rows = block_rows;
     L.mask = agg_mask;
-    L.stream = (hipStream_t)stream;
-    L.parts = (Partial *)d_ws;
 
     // value expression
-    bool chain = value && value->n_steps > 0;
+    chain = value && value->n_steps > 0;
     int32_t vdt = col->dtype;
     if (chain) {
         fq_status s = lower_expr(*value, col->dtype, L.val, vdt);
@@ -572,17 +557,17 @@ fq_status fq_aggregate(const fq_col *col, int64_t block_rows, const fq_pred *pre
         L.pred.rhs_operand = pred->rhs_operand;
         L.pred.rhs = pred->rhs_bits;
     } else if (L.pred.kind == FQ_PRED_BITMAP) {
-        if (!pred->bitmap && col->len > 0) return fqc::fail(FQ_E_INVALID, "fq_pred: NULL bitmap");
+        if (need_data && !pred->bitmap && col->len > 0) return fqc::fail(FQ_E_INVALID, "fq_pred: NULL bitmap");
         L.pred.bitmap = pred->bitmap;
     } else if (L.pred.kind != FQ_PRED_NONE) {
         return fqc::fail(FQ_E_INVALID, "fq_pred: bad kind");
     }
 
-    const uint64_t blocks = col->len == 0 ? 0 : (uint64_t)((col->len + block_rows - 1) / block_rows);
+    blocks = col->len == 0 ? 0 : (uint64_t)((col->len + block_rows - 1) / block_rows);
     // Block mode only where the per-block emptiness matters (filtered sum over
     // more than one reference block); otherwise stream flat.
     L.block_mode = L.pred.kind != FQ_PRED_NONE && (agg_mask & FQ_AGG_SUM) && blocks > 1;
-    const int empty_if_zero = (L.pred.kind != FQ_PRED_NONE && blocks == 1) ? 1 : 0;
+    empty_if_zero = (L.pred.kind != FQ_PRED_NONE && blocks == 1) ? 1 : 0;
 
     const int cus = fqc::device_cu_count();
     const int max_grid = cus * 8 < kMaxPartials ? cus * 8 : kMaxPartials;
@@ -605,9 +590,52 @@ fq_status fq_aggregate(const fq_col *col, int64_t block_rows, const fq_pred *pre
         const int64_t flat_max = (int64_t)cus * scan_wg_per_cu();
         L.grid = (int)(grid < flat_max ? grid : flat_max);
     }
-    fq_status s = dispatch(col->dtype, L, chain);
+    return FQ_OK;
+}
+
+}  // namespace fqk
+
+extern "C" {
+
+fq_status fq_aggregate(const fq_col *col, int64_t block_rows, const fq_pred *pred, const fq_expr *value,
+                       uint32_t agg_mask, fq_agg_state *d_out, void *d_ws, size_t ws_bytes, void *stream) {
+    using namespace fqk;
+    if (!col || !d_out || !d_ws) return fqc::fail(FQ_E_INVALID, "fq_aggregate: NULL argument");
+    if (ws_bytes < fq_aggregate_workspace_bytes(col->len))
+        return fqc::fail(FQ_E_INVALID, "fq_aggregate: workspace too small");
+    Launch L;
+    bool chain = false;
+    uint64_t blocks = 0;
+    int empty_if_zero = 0;
+    fq_status s = plan_scan(col, block_rows, pred, value, agg_mask, true, L, chain, blocks, empty_if_zero);
     if (s != FQ_OK) return s;
+    L.stream = (hipStream_t)stream;
+    L.parts = (Partial *)d_ws;
+    bool jitted = false;
+    s = jit_scan(col->dtype, chain, L, &jitted);
+    if (s != FQ_OK) return s;
+    if (!jitted) {
+        if (chain || L.pred.kind != FQ_PRED_NONE) jit_count_interp();
+        s = dispatch(col->dtype, L, chain);
+        if (s != FQ_OK) return s;
+    }
     return dispatch_finalize(L, blocks, empty_if_zero, d_out);
+}
+
+fq_status fq_jit_prepare(const fq_col *col, int64_t block_rows, const fq_pred *pred, const fq_expr *value,
+                         uint32_t agg_mask, int32_t *specialised) {
+    using namespace fqk;
+    if (specialised) *specialised = 0;
+    Launch L;
+    bool chain = false;
+    uint64_t blocks = 0;
+    int empty_if_zero = 0;
+    fq_status s = plan_scan(col, block_rows, pred, value, agg_mask, false, L, chain, blocks, empty_if_zero);
+    if (s != FQ_OK) return s;
+    bool ok = false;
+    s = jit_prepare(col->dtype, chain, L, &ok);
+    if (s == FQ_OK && specialised) *specialised = ok ? 1 : 0;
+    return s;
 }
 
 }  // extern "C"

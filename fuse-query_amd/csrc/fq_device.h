@@ -155,6 +155,11 @@ __device__ __forceinline__ uint64_t divm_u64(uint64_t x, uint64_t magic, uint32_
     return q >> shift;
 }
 
+// Rare, long operations are out-of-line calls so that the unrolled program
+// interpreter stays small enough for the instruction cache (a 64-bit divide
+// or fmod unrolled over E elements is thousands of instructions).
+__device__ __noinline__ inline uint64_t slow_divmod(int32_t code, uint64_t a, uint64_t b);
+
 // ---------------------------------------------------------------------------
 // The expression program, run over E elements per lane.  Every switch is on a
 // wave-uniform kernel argument, so each branch is a scalar jump; the element
@@ -217,29 +222,12 @@ __device__ __forceinline__ void run_prog(const KProg &p, const TIn (&x)[E], uint
                 break;
             case K_DIV_U:
             case K_MOD_U:
-#pragma unroll
-                for (int j = 0; j < E; ++j) {
-                    if (b[j] == 0) {
-                        if ((live >> j) & 1u) flags |= FQ_STATE_DIV_ZERO;
-                        a[j] = 0;
-                    } else {
-                        a[j] = code == K_DIV_U ? a[j] / b[j] : a[j] % b[j];
-                    }
-                }
-                break;
             case K_DIV_S:
             case K_MOD_S:
 #pragma unroll
                 for (int j = 0; j < E; ++j) {
-                    const int64_t sa = (int64_t)a[j], sb = (int64_t)b[j];
-                    if (sb == 0) {
-                        if ((live >> j) & 1u) flags |= FQ_STATE_DIV_ZERO;
-                        a[j] = 0;
-                    } else if (sb == -1) {  // i64::MIN / -1 wraps (unpinned in the reference)
-                        a[j] = code == K_DIV_S ? (uint64_t)0 - a[j] : 0;
-                    } else {
-                        a[j] = (uint64_t)(code == K_DIV_S ? sa / sb : sa % sb);
-                    }
+                    if (b[j] == 0 && ((live >> j) & 1u)) flags |= FQ_STATE_DIV_ZERO;
+                    a[j] = slow_divmod(code, a[j], b[j]);
                 }
                 break;
             case K_SHR_U:
@@ -260,31 +248,56 @@ __device__ __forceinline__ void run_prog(const KProg &p, const TIn (&x)[E], uint
                     a[j] = a[j] - divm_u64(a[j], st.magic, st.shift, st.add) * st.c;
                 break;
             case K_ADD_F:
+#pragma unroll
+                for (int j = 0; j < E; ++j)
+                    a[j] = __builtin_bit_cast(uint64_t, __builtin_bit_cast(double, a[j]) + __builtin_bit_cast(double, b[j]));
+                break;
             case K_SUB_F:
+#pragma unroll
+                for (int j = 0; j < E; ++j)
+                    a[j] = __builtin_bit_cast(uint64_t, __builtin_bit_cast(double, a[j]) - __builtin_bit_cast(double, b[j]));
+                break;
             case K_MUL_F:
+#pragma unroll
+                for (int j = 0; j < E; ++j)
+                    a[j] = __builtin_bit_cast(uint64_t, __builtin_bit_cast(double, a[j]) * __builtin_bit_cast(double, b[j]));
+                break;
             case K_DIV_F:
             case K_MOD_F:
 #pragma unroll
                 for (int j = 0; j < E; ++j) {
-                    const double fa = __builtin_bit_cast(double, a[j]);
-                    const double fb = __builtin_bit_cast(double, b[j]);
-                    double r;
-                    if (code == K_ADD_F) {
-                        r = fa + fb;
-                    } else if (code == K_SUB_F) {
-                        r = fa - fb;
-                    } else if (code == K_MUL_F) {
-                        r = fa * fb;
-                    } else {
-                        if (fb == 0.0 && ((live >> j) & 1u)) flags |= FQ_STATE_DIV_ZERO;
-                        r = code == K_DIV_F ? fa / fb : fmod(fa, fb);
-                    }
-                    a[j] = __builtin_bit_cast(uint64_t, r);
+                    if (__builtin_bit_cast(double, b[j]) == 0.0 && ((live >> j) & 1u)) flags |= FQ_STATE_DIV_ZERO;
+                    a[j] = slow_divmod(code, a[j], b[j]);
                 }
                 break;
             default:
                 break;
         }
+    }
+}
+
+// a OP b for the generic divide/modulo codes; a zero divisor yields 0 (the
+// caller raises DIV_ZERO for live rows).  i64::MIN / -1 wraps (unpinned in
+// the reference).
+__device__ __noinline__ inline uint64_t slow_divmod(int32_t code, uint64_t a, uint64_t b) {
+    switch (code) {
+        case K_DIV_U:
+            return b ? a / b : 0;
+        case K_MOD_U:
+            return b ? a % b : 0;
+        case K_DIV_S:
+        case K_MOD_S: {
+            const int64_t sa = (int64_t)a, sb = (int64_t)b;
+            if (sb == 0) return 0;
+            if (sb == -1) return code == K_DIV_S ? (uint64_t)0 - a : 0;
+            return (uint64_t)(code == K_DIV_S ? sa / sb : sa % sb);
+        }
+        case K_DIV_F:
+            return __builtin_bit_cast(uint64_t, __builtin_bit_cast(double, a) / __builtin_bit_cast(double, b));
+        case K_MOD_F:
+            return __builtin_bit_cast(uint64_t, fmod(__builtin_bit_cast(double, a), __builtin_bit_cast(double, b)));
+        default:
+            return a;
     }
 }
 

@@ -1,0 +1,598 @@
+// hipRTC specialisation of the fused AggregatePartial scan.
+//
+// The precompiled scan kernels (fq_aggregate.hip) interpret the lowered
+// expression program step by step: every step is a wave-uniform switch, which
+// is cheap per step but leaves the compiler a kernel of thousands of
+// instructions with copies at every join, 160+ VGPRs and three waves per SIMD.
+// For a filtered/computed scan (BASELINE C4, `max(number+1) WHERE
+// (number%8)<3`) that is compute-bound at ~60 % of HBM bandwidth.
+//
+// Here the same program is emitted as straight-line HIP source -- one inline
+// function for the predicate, one for the argument expression -- around the
+// same tile-contiguous streaming loop, compiled once per expression SHAPE
+// (step ops, operand kinds, dtypes, libdivide "add" marker, aggregate mask)
+// with hipRTC for the device's own gfx target, and cached for the process.
+// Constants (literals, divide magics, shifts) stay kernel arguments, so
+// `WHERE number % 8 < 3` and `WHERE number % 8 < 5` share one kernel.
+//
+// Semantics are the interpreter's, element for element (flag raising for
+// live rows only, the same per-lane accumulation order, the same partial
+// layout), so a specialised scan and an interpreted one return identical
+// fq_agg_state bits for the same grid; tests/test_kernels_gpu.py checks both
+// against the oracle.
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <hip/hiprtc.h>
+
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "fq_common.h"
+#include "fq_device.h"
+#include "fq_scan.h"
+
+namespace fqk {
+namespace {
+
+// ---------------------------------------------------------------------------
+// hipRTC, loaded on first use (libfq_amd.so does not link it, so the library
+// still loads where hipRTC is absent).  If torch already loaded its bundled
+// copy, dlopen by SONAME returns that one.
+// ---------------------------------------------------------------------------
+struct Rtc {
+    decltype(&hiprtcCreateProgram) create = nullptr;
+    decltype(&hiprtcCompileProgram) compile = nullptr;
+    decltype(&hiprtcGetProgramLogSize) log_size = nullptr;
+    decltype(&hiprtcGetProgramLog) log = nullptr;
+    decltype(&hiprtcGetCodeSize) code_size = nullptr;
+    decltype(&hiprtcGetCode) code = nullptr;
+    decltype(&hiprtcDestroyProgram) destroy = nullptr;
+    bool ok = false;
+};
+
+const Rtc &rtc() {
+    static const Rtc r = [] {
+        Rtc x;
+        void *h = dlopen("libhiprtc.so.7", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) h = dlopen("libhiprtc.so", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) return x;
+        x.create = (decltype(x.create))dlsym(h, "hiprtcCreateProgram");
+        x.compile = (decltype(x.compile))dlsym(h, "hiprtcCompileProgram");
+        x.log_size = (decltype(x.log_size))dlsym(h, "hiprtcGetProgramLogSize");
+        x.log = (decltype(x.log))dlsym(h, "hiprtcGetProgramLog");
+        x.code_size = (decltype(x.code_size))dlsym(h, "hiprtcGetCodeSize");
+        x.code = (decltype(x.code))dlsym(h, "hiprtcGetCode");
+        x.destroy = (decltype(x.destroy))dlsym(h, "hiprtcDestroyProgram");
+        x.ok = x.create && x.compile && x.log_size && x.log && x.code_size && x.code && x.destroy;
+        return x;
+    }();
+    return r;
+}
+
+// ---------------------------------------------------------------------------
+// policy + statistics
+// ---------------------------------------------------------------------------
+std::atomic<int32_t> g_mode{-1};
+std::atomic<int64_t> g_min_rows{-1};
+std::atomic<int64_t> g_compiled{0}, g_jit_launches{0}, g_interp_launches{0};
+std::atomic<int64_t> g_compile_us{0};
+std::atomic<int32_t> g_available{-1};
+
+int32_t jit_mode() {
+    int32_t m = g_mode.load(std::memory_order_relaxed);
+    if (m < 0) {
+        const char *e = getenv("FQ_JIT");
+        m = e ? atoi(e) : FQ_JIT_AUTO;
+        if (m < FQ_JIT_OFF || m > FQ_JIT_ALWAYS) m = FQ_JIT_AUTO;
+        int32_t expect = -1;
+        g_mode.compare_exchange_strong(expect, m);
+        m = g_mode.load();
+    }
+    return m;
+}
+
+int64_t jit_min_rows() {
+    int64_t r = g_min_rows.load(std::memory_order_relaxed);
+    if (r < 0) {
+        const char *e = getenv("FQ_JIT_MIN_ROWS");
+        r = e ? atoll(e) : (int64_t)1 << 22;
+        if (r < 0) r = (int64_t)1 << 22;
+        int64_t expect = -1;
+        g_min_rows.compare_exchange_strong(expect, r);
+        r = g_min_rows.load();
+    }
+    return r;
+}
+
+// ---------------------------------------------------------------------------
+// source generation
+// ---------------------------------------------------------------------------
+const char *ctype(int32_t dt) {
+    switch (dt) {
+        case FQ_DT_INT64: return "long long";
+        case FQ_DT_UINT64: return "unsigned long long";
+        case FQ_DT_FLOAT64: return "double";
+        default: return nullptr;
+    }
+}
+
+// column element x (type tin) -> 64-bit value encoding
+std::string x_bits(int32_t tin) {
+    if (tin == FQ_DT_FLOAT64) return "__builtin_bit_cast(u64, x)";
+    return "(u64)x";
+}
+
+struct Gen {
+    std::string key;          // shape key (cache)
+    std::vector<uint64_t> k;  // kernel-argument constants, in emission order
+    int konst(uint64_t v) {
+        k.push_back(v);
+        return (int)k.size() - 1;
+    }
+    std::string K(uint64_t v) { return "c.k[" + std::to_string(konst(v)) + "]"; }
+};
+
+// col_as(dtype, x, live): the column as the operand of a step in `dt`
+std::string col_as(Gen &g, std::string &body, int32_t tin, int32_t dt) {
+    if (dt == FQ_DT_FLOAT64) return "__builtin_bit_cast(u64, (double)x)";
+    if (tin == FQ_DT_UINT64 && dt == FQ_DT_INT64)
+        body += "    flags |= (u32)((x >> 63) & (u64)live) * " + std::to_string(FQ_STATE_CAST_NULL) + "u;\n";
+    (void)g;
+    return x_bits(tin);
+}
+
+// Straight-line code for one lowered program acting on `a`.
+void emit_prog(Gen &g, std::string &body, const KProg &p, int32_t tin) {
+    g.key += "P" + std::to_string(p.n) + ":";
+    for (int i = 0; i < p.n; ++i) {
+        const KStep &st = p.s[i];
+        g.key += std::to_string(st.code) + "," + std::to_string(st.operand) + "," + std::to_string(st.reversed) +
+                 "," + std::to_string(st.dtype) + "," + std::to_string(st.add) + ";";
+        const std::string DZ = std::to_string(FQ_STATE_DIV_ZERO) + "u";
+        switch (st.code) {
+            case K_NOP: continue;
+            case K_CAST_U2I:
+                body += "    flags |= (u32)((a >> 63) & (u64)live) * " + std::to_string(FQ_STATE_CAST_NULL) + "u;\n";
+                continue;
+            case K_CAST_U2F: body += "    a = __builtin_bit_cast(u64, (double)a);\n"; continue;
+            case K_CAST_I2F: body += "    a = __builtin_bit_cast(u64, (double)(long long)a);\n"; continue;
+            case K_SHR_U: body += "    a = a >> (u32)" + g.K(st.shift) + ";\n"; continue;
+            case K_AND_U: body += "    a = a & " + g.K(st.magic) + ";\n"; continue;
+            case K_DIVM_U:
+            case K_MODM_U: {
+                const std::string M = g.K(st.magic), S = g.K(st.shift);
+                body += "    { u64 q = __umul64hi(a, " + M + ");\n";
+                if (st.add) body += "      q = (((a - q) >> 1) + q) >> (u32)" + S + ";\n";
+                else body += "      q = q >> (u32)" + S + ";\n";
+                if (st.code == K_DIVM_U) body += "      a = q; }\n";
+                else body += "      a = a - q * " + g.K(st.c) + "; }\n";
+                continue;
+            }
+            default: break;
+        }
+        // binary step with an operand b
+        std::string b;
+        if (st.operand == FQ_OPERAND_COLUMN) b = col_as(g, body, tin, st.dtype);
+        else b = g.K(st.c);
+        body += "    { const u64 b = " + b + ";\n";
+        body += st.reversed ? "      const u64 L = b, R = a;\n" : "      const u64 L = a, R = b;\n";
+        switch (st.code) {
+            case K_ADD_I: body += "      a = L + R; }\n"; break;
+            case K_SUB_I: body += "      a = L - R; }\n"; break;
+            case K_MUL_I: body += "      a = L * R; }\n"; break;
+            case K_DIV_U:
+                body += "      flags |= (R == 0 && live) ? " + DZ + " : 0u;\n      a = R ? L / R : 0; }\n";
+                break;
+            case K_MOD_U:
+                body += "      flags |= (R == 0 && live) ? " + DZ + " : 0u;\n      a = R ? L % R : 0; }\n";
+                break;
+            case K_DIV_S:
+            case K_MOD_S: {
+                const bool div = st.code == K_DIV_S;
+                body += "      flags |= (R == 0 && live) ? " + DZ + " : 0u;\n";
+                body += "      const long long sl = (long long)L, sr = (long long)R;\n";
+                body += std::string("      a = sr == 0 ? 0 : (sr == -1 ? ") + (div ? "(u64)0 - L" : "(u64)0") +
+                        " : (u64)(sl " + (div ? "/" : "%") + " sr)); }\n";
+                break;
+            }
+            case K_ADD_F:
+            case K_SUB_F:
+            case K_MUL_F:
+            case K_DIV_F:
+            case K_MOD_F: {
+                body += "      const double fl = __builtin_bit_cast(double, L), fr = __builtin_bit_cast(double, R);\n";
+                const char *e = st.code == K_ADD_F   ? "fl + fr"
+                                : st.code == K_SUB_F ? "fl - fr"
+                                : st.code == K_MUL_F ? "fl * fr"
+                                : st.code == K_DIV_F ? "fl / fr"
+                                                     : "fmod(fl, fr)";
+                if (st.code == K_DIV_F || st.code == K_MOD_F)
+                    body += "      flags |= (fr == 0.0 && live) ? " + DZ + " : 0u;\n";
+                body += std::string("      a = __builtin_bit_cast(u64, ") + e + "); }\n";
+                break;
+            }
+            default: body += "      (void)L; (void)R; }\n"; break;
+        }
+    }
+}
+
+const char *cmp_op(int32_t cmp) {
+    switch (cmp) {
+        case FQ_CMP_EQ: return "==";
+        case FQ_CMP_LT: return "<";
+        case FQ_CMP_LTEQ: return "<=";
+        case FQ_CMP_GT: return ">";
+        case FQ_CMP_GTEQ: return ">=";
+        default: return nullptr;
+    }
+}
+
+const char *kCommon = R"(
+typedef unsigned long long u64;
+typedef unsigned int u32;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+struct Partial { u64 sum, max, min, count, blocks; u32 flags; int dtype; };
+template <typename T> __device__ __forceinline__ T shfl64(T v, int m) {
+    const u64 b = __builtin_bit_cast(u64, v);
+    const u32 lo = __shfl_xor((u32)(b & 0xffffffffu), m, 64);
+    const u32 hi = __shfl_xor((u32)(b >> 32), m, 64);
+    return __builtin_bit_cast(T, ((u64)hi << 32) | lo);
+}
+template <typename T> __device__ __forceinline__ T vmax(T a, T b) { return b > a ? b : a; }
+template <typename T> __device__ __forceinline__ T vmin(T a, T b) { return b < a ? b : a; }
+)";
+
+// Full kernel source for one shape.  Returns false if the shape is outside
+// what the generator handles (the caller then interprets).
+bool gen_source(const Launch &L, int32_t tin, bool chain, Gen &g, std::string &src) {
+    const char *TIn = ctype(tin);
+    const char *V = ctype(L.vdtype);
+    if (!TIn || !V) return false;
+    const int32_t pk = L.pred.kind;
+    g.key = "T" + std::to_string(tin) + "V" + std::to_string(L.vdtype) + "M" + std::to_string(L.mask) + "K" +
+            std::to_string(pk) + (L.block_mode ? "B" : "F");
+
+    std::string pred_body, val_body;
+    if (pk == FQ_PRED_EXPR) {
+        const char *op = cmp_op(L.pred.cmp);
+        if (!op) return false;
+        g.key += "c" + std::to_string(L.pred.cmp) + "d" + std::to_string(L.pred.cmp_dtype) + "r" +
+                 std::to_string(L.pred.rhs_operand);
+        pred_body += "    u64 a = " + x_bits(tin) + ";\n";
+        emit_prog(g, pred_body, L.pred.lhs, tin);
+        std::string r;
+        if (L.pred.rhs_operand == FQ_OPERAND_COLUMN) r = col_as(g, pred_body, tin, L.pred.cmp_dtype);
+        else r = g.K(L.pred.rhs);
+        pred_body += "    const u64 r = " + r + ";\n";
+        if (L.pred.cmp_dtype == FQ_DT_UINT64) pred_body += std::string("    return a ") + op + " r;\n";
+        else if (L.pred.cmp_dtype == FQ_DT_INT64)
+            pred_body += std::string("    return (long long)a ") + op + " (long long)r;\n";
+        else if (L.pred.cmp_dtype == FQ_DT_FLOAT64)
+            pred_body += std::string("    return __builtin_bit_cast(double, a) ") + op +
+                         " __builtin_bit_cast(double, r);\n";
+        else
+            return false;
+    }
+    g.key += "|";
+    if (chain) {
+        val_body += "    u64 a = " + x_bits(tin) + ";\n";
+        emit_prog(g, val_body, L.val, tin);
+        if (L.vdtype == FQ_DT_FLOAT64) val_body += "    return __builtin_bit_cast(double, a);\n";
+        else val_body += "    return (V)a;\n";
+    } else {
+        g.key += "id";
+        val_body += "    return (V)x;\n";
+    }
+
+    const int nk = g.k.empty() ? 1 : (int)g.k.size();
+    src = kCommon;
+    src += "typedef " + std::string(TIn) + " TIn;\ntypedef " + V + " V;\n";
+    src += "struct Consts { u64 k[" + std::to_string(nk) + "]; };\n";
+    src += "__device__ __forceinline__ bool fq_pred(TIn x, const Consts &c, u32 &flags, u32 live) {\n";
+    src += pk == FQ_PRED_EXPR ? pred_body : "    return true;\n";
+    src += "}\n";
+    src += "__device__ __forceinline__ V fq_val(TIn x, const Consts &c, u32 &flags, u32 live) {\n" + val_body + "}\n";
+    const uint32_t m = L.mask;
+    src += "struct Acc { V sum, mx, mn; u64 cnt; u32 flags; };\n";
+    src += "__device__ __forceinline__ u32 fq_acc(Acc &acc, TIn x, long long idx, u32 live, const Consts &c,\n"
+           "                                      const u64 *__restrict__ bitmap) {\n"
+           "    u32 pass = live;\n";
+    if (pk == FQ_PRED_EXPR) src += "    pass &= fq_pred(x, c, acc.flags, live) ? 1u : 0u;\n";
+    else if (pk == FQ_PRED_BITMAP)
+        src += "    if (live) pass &= (u32)((bitmap[idx >> 6] >> (idx & 63)) & 1ull);\n";
+    src += "    (void)idx; (void)bitmap;\n    const V v = fq_val(x, c, acc.flags, pass);\n";
+    if (m & FQ_AGG_SUM) src += "    acc.sum = acc.sum + (pass ? v : V(0));\n";
+    if (m & FQ_AGG_MAX) src += "    acc.mx = pass ? vmax(acc.mx, v) : acc.mx;\n";
+    if (m & FQ_AGG_MIN) src += "    acc.mn = pass ? vmin(acc.mn, v) : acc.mn;\n";
+    src += "    acc.cnt += pass;\n    return pass;\n}\n";
+
+    // limits of V for the accumulator init (Lim<V> in fq_device.h)
+    std::string lo, hi;
+    if (L.vdtype == FQ_DT_UINT64) lo = "0ull", hi = "~0ull";
+    else if (L.vdtype == FQ_DT_INT64) lo = "(-9223372036854775807ll - 1)", hi = "9223372036854775807ll";
+    else lo = "-__builtin_huge_val()", hi = "__builtin_huge_val()";
+
+    src += "extern \"C\" __global__ void __launch_bounds__(256)\n"
+           "fq_jit_scan(const TIn *__restrict__ col, long long n, long long head, long long R,\n"
+           "            const u64 *__restrict__ bitmap, Consts c, Partial *__restrict__ parts) {\n"
+           "    Acc acc;\n    acc.sum = V(0); acc.mx = " + lo + "; acc.mn = " + hi + "; acc.cnt = 0; acc.flags = 0;\n";
+    if (!L.block_mode) {
+        // flat tile-contiguous streaming (agg_flat_kernel, U = 4 16-byte vectors per lane)
+        src += R"(
+    (void)R;
+    const long long T = (long long)gridDim.x * 256;
+    const long long g = (long long)blockIdx.x * 256 + threadIdx.x;
+    const long long nvec = (n - head) / 2;
+    const u32x4 *__restrict__ vp = (const u32x4 *)(col + head);
+    const long long TV = 4 * 256;
+    const long long ntiles = nvec / TV;
+    for (long long t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const long long base = t * TV + threadIdx.x;
+        u32x4 raw[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) raw[k] = __builtin_nontemporal_load(vp + base + (long long)k * 256);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            TIn x[2];
+            __builtin_memcpy(&x[0], &raw[k], 16);
+            const long long i0 = head + (base + (long long)k * 256) * 2;
+            fq_acc(acc, x[0], i0, 1u, c, bitmap);
+            fq_acc(acc, x[1], i0 + 1, 1u, c, bitmap);
+        }
+    }
+    for (long long v = ntiles * TV + g; v < nvec; v += T) {
+        const u32x4 raw = __builtin_nontemporal_load(vp + v);
+        TIn x[2];
+        __builtin_memcpy(&x[0], &raw, 16);
+        fq_acc(acc, x[0], head + v * 2, 1u, c, bitmap);
+        fq_acc(acc, x[1], head + v * 2 + 1, 1u, c, bitmap);
+    }
+    const long long tail0 = head + nvec * 2;
+    const long long nedge = head + (n - tail0);
+    for (long long t = g; t < nedge; t += T) {
+        const long long i = t < head ? t : tail0 + (t - head);
+        fq_acc(acc, col[i], i, 1u, c, bitmap);
+    }
+)";
+    } else {
+        // block mode (agg_block_kernel, 8 elements per lane in flight)
+        src += R"(
+    (void)head;
+    const int lane = threadIdx.x & 63;
+    const long long w = ((long long)blockIdx.x * 256 + threadIdx.x) / 64;
+    const long long W = ((long long)gridDim.x * 256) / 64;
+    const long long nb = (n + R - 1) / R;
+    for (long long b = w; b < nb; b += W) {
+        const long long s = b * R;
+        const long long e = (s + R < n) ? s + R : n;
+        u32 any = 0;
+        for (long long i = s + lane; i < e; i += 64 * 8) {
+            TIn x[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const long long ik = i + (long long)k * 64;
+                x[k] = ik < e ? __builtin_nontemporal_load(col + ik) : TIn(0);
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const long long ik = i + (long long)k * 64;
+                any |= fq_acc(acc, x[k], ik, ik < e ? 1u : 0u, c, bitmap);
+            }
+        }
+        if (__ballot(any != 0) == 0ull) acc.flags |= )" + std::to_string(FQ_STATE_ANY_EMPTY) + R"(u;
+    }
+)";
+    }
+    // reduce_and_store (fq_aggregate.hip)
+    src += R"(
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        acc.sum = acc.sum + shfl64(acc.sum, off);
+        acc.mx = vmax(acc.mx, shfl64(acc.mx, off));
+        acc.mn = vmin(acc.mn, shfl64(acc.mn, off));
+        acc.cnt += shfl64(acc.cnt, off);
+        acc.flags |= (u32)__shfl_xor((int)acc.flags, off, 64);
+    }
+    __shared__ V s_sum[4], s_mx[4], s_mn[4];
+    __shared__ u64 s_cnt[4];
+    __shared__ u32 s_flags[4];
+    const int wave = threadIdx.x / 64;
+    if ((threadIdx.x & 63) == 0) {
+        s_sum[wave] = acc.sum; s_mx[wave] = acc.mx; s_mn[wave] = acc.mn;
+        s_cnt[wave] = acc.cnt; s_flags[wave] = acc.flags;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        V sum = s_sum[0], mx = s_mx[0], mn = s_mn[0];
+        u64 cnt = s_cnt[0];
+        u32 flags = s_flags[0];
+#pragma unroll
+        for (int w = 1; w < 4; ++w) {
+            sum = sum + s_sum[w]; mx = vmax(mx, s_mx[w]); mn = vmin(mn, s_mn[w]);
+            cnt += s_cnt[w]; flags |= s_flags[w];
+        }
+        Partial p;
+        p.sum = __builtin_bit_cast(u64, sum); p.max = __builtin_bit_cast(u64, mx); p.min = __builtin_bit_cast(u64, mn);
+        p.count = cnt; p.blocks = 0; p.flags = flags; p.dtype = )" + std::to_string(L.vdtype) + R"(;
+        parts[blockIdx.x] = p;
+    }
+}
+)";
+    return true;
+}
+
+// ---------------------------------------------------------------------------
+// compile + cache
+// ---------------------------------------------------------------------------
+struct Compiled {
+    hipModule_t mod = nullptr;
+    hipFunction_t fn = nullptr;
+};
+
+std::mutex g_mu;
+std::unordered_map<std::string, Compiled> g_cache;
+
+std::string device_arch(int dev) {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return "gfx950";
+    return prop.gcnArchName;
+}
+
+// dev < 0: no device here -- compile for gfx950 to validate the source only.
+fq_status compile(const std::string &src, int dev, Compiled &out) {
+    const Rtc &r = rtc();
+    const auto t0 = std::chrono::steady_clock::now();
+    hiprtcProgram prog;
+    if (r.create(&prog, src.c_str(), "fq_jit_scan.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS)
+        return fqc::fail(FQ_E_INTERNAL, "hipRTC: cannot create program");
+    const std::string arch = "--offload-arch=" + (dev >= 0 ? device_arch(dev) : std::string("gfx950"));
+    const char *opts[] = {arch.c_str(), "-O3", "-std=c++17"};
+    const hiprtcResult cr = r.compile(prog, 3, opts);
+    if (cr != HIPRTC_SUCCESS) {
+        size_t n = 0;
+        r.log_size(prog, &n);
+        std::string log(n + 1, '\0');
+        r.log(prog, &log[0]);
+        r.destroy(&prog);
+        return fqc::fail(FQ_E_INTERNAL, "hipRTC compile of the fused scan failed: " + log + "\n--- source ---\n" + src);
+    }
+    size_t n = 0;
+    r.code_size(prog, &n);
+    std::vector<char> code(n);
+    r.code(prog, code.data());
+    r.destroy(&prog);
+    if (dev >= 0) {
+        FQ_HIP_TRY(hipModuleLoadData(&out.mod, code.data()));
+        FQ_HIP_TRY(hipModuleGetFunction(&out.fn, out.mod, "fq_jit_scan"));
+    }
+    const auto t1 = std::chrono::steady_clock::now();
+    g_compile_us += (int64_t)std::chrono::duration_cast<std::chrono::microseconds>(t1 - t0).count();
+    g_compiled += 1;
+    if (const char *d = getenv("FQ_JIT_DUMP")) {
+        const std::string p = std::string(d) + "/fq_jit_" + std::to_string(g_compiled.load()) + ".hip";
+        if (FILE *f = fopen(p.c_str(), "w")) {
+            fwrite(src.data(), 1, src.size(), f);
+            fclose(f);
+        }
+    }
+    return FQ_OK;
+}
+
+}  // namespace
+
+void jit_count_interp() { g_interp_launches += 1; }
+
+namespace {
+
+bool eligible(int32_t col_dtype, bool chain, const Launch &L) {
+    if (!chain && L.pred.kind == FQ_PRED_NONE) return false;  // identity scans are already specialised
+    return fqc::dtype_size(col_dtype) == 8;                      // expressions are 64-bit; narrow columns interpret
+}
+
+bool load_rtc(int32_t mode, fq_status *err) {
+    const Rtc &r = rtc();
+    g_available.store(r.ok ? 1 : 0);
+    *err = FQ_OK;
+    if (!r.ok && mode == FQ_JIT_ALWAYS)
+        *err = fqc::fail(FQ_E_UNSUPPORTED, "FQ_JIT_ALWAYS: hipRTC (libhiprtc.so.7) could not be loaded");
+    return r.ok;
+}
+
+// Looks up / compiles the kernel for L's shape.  *fn stays null when there is
+// no device (source validated only) or the generator declines the shape.
+fq_status get_kernel(int32_t col_dtype, bool chain, const Launch &L, Gen &g, hipFunction_t *fn) {
+    *fn = nullptr;
+    std::string src;
+    if (!gen_source(L, col_dtype, chain, g, src)) return FQ_OK;
+    int ndev = 0, dev = -1;
+    if (hipGetDeviceCount(&ndev) == hipSuccess && ndev > 0) {
+        FQ_HIP_TRY(hipGetDevice(&dev));
+    } else {
+        (void)hipGetLastError();
+    }
+    const std::string key = std::to_string(dev) + "/" + g.key;
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto it = g_cache.find(key);
+    if (it == g_cache.end()) {
+        Compiled c;
+        fq_status s = compile(src, dev, c);
+        if (s != FQ_OK) return s;
+        if (dev < 0) return FQ_OK;
+        it = g_cache.emplace(key, c).first;
+    }
+    *fn = it->second.fn;
+    return FQ_OK;
+}
+
+}  // namespace
+
+fq_status jit_prepare(int32_t col_dtype, bool chain, const Launch &L, bool *ready) {
+    *ready = false;
+    const int32_t mode = jit_mode();
+    if (mode == FQ_JIT_OFF || !eligible(col_dtype, chain, L)) return FQ_OK;
+    fq_status err;
+    if (!load_rtc(mode, &err)) return err;
+    Gen g;
+    hipFunction_t fn;
+    fq_status s = get_kernel(col_dtype, chain, L, g, &fn);
+    if (s != FQ_OK) return s;
+    *ready = !g.key.empty();
+    return FQ_OK;
+}
+
+fq_status jit_scan(int32_t col_dtype, bool chain, const Launch &L, bool *used) {
+    *used = false;
+    const int32_t mode = jit_mode();
+    if (mode == FQ_JIT_OFF || !eligible(col_dtype, chain, L)) return FQ_OK;
+    if (mode == FQ_JIT_AUTO && L.n < jit_min_rows()) return FQ_OK;
+    fq_status err;
+    if (!load_rtc(mode, &err)) return err;
+    Gen g;
+    hipFunction_t fn;
+    fq_status s = get_kernel(col_dtype, chain, L, g, &fn);
+    if (s != FQ_OK) return s;
+    if (!fn) return FQ_OK;
+    std::vector<uint64_t> k = g.k;
+    if (k.empty()) k.push_back(0);
+    const void *col = L.col;
+    long long n = L.n, head = L.head, R = L.block_rows;
+    const uint64_t *bitmap = L.pred.bitmap;
+    Partial *parts = L.parts;
+    void *args[] = {&col, &n, &head, &R, &bitmap, k.data(), &parts};
+    FQ_HIP_TRY(hipModuleLaunchKernel(fn, (unsigned)L.grid, 1, 1, kThreads, 1, 1, 0, L.stream, args, nullptr));
+    g_jit_launches += 1;
+    *used = true;
+    return FQ_OK;
+}
+
+}  // namespace fqk
+
+extern "C" {
+
+fq_status fq_jit_config(int32_t mode, int64_t min_rows) {
+    if (mode < FQ_JIT_OFF || mode > FQ_JIT_ALWAYS) return fqc::fail(FQ_E_INVALID, "fq_jit_config: bad mode");
+    if (min_rows < 0) return fqc::fail(FQ_E_INVALID, "fq_jit_config: negative min_rows");
+    fqk::g_mode.store(mode);
+    fqk::g_min_rows.store(min_rows);
+    return FQ_OK;
+}
+
+fq_status fq_jit_get_stats(fq_jit_stats *out) {
+    if (!out) return fqc::fail(FQ_E_INVALID, "fq_jit_get_stats: NULL argument");
+    out->kernels_compiled = fqk::g_compiled.load();
+    out->jit_launches = fqk::g_jit_launches.load();
+    out->interp_launches = fqk::g_interp_launches.load();
+    out->compile_ms = fqk::g_compile_us.load() / 1000.0;
+    out->available = fqk::g_available.load();
+    out->mode = fqk::jit_mode();
+    out->min_rows = fqk::jit_min_rows();
+    return FQ_OK;
+}
+
+}  // extern "C"

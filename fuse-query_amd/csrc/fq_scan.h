@@ -1,0 +1,40 @@
+// One fused-scan launch as prepared by fq_aggregate (fq_aggregate.hip) and
+// consumed by either the precompiled program-interpreting kernels or a
+// hipRTC-specialised kernel (fq_jit.hip).  Internal; not part of the ABI.
+#pragma once
+
+#include "fq_device.h"
+
+namespace fqk {
+
+constexpr int kThreads = 256;       // 4 waves per workgroup
+constexpr int kMaxPartials = 4096;  // workgroups per launch upper bound
+
+struct Launch {
+    const void *col;
+    int64_t n;
+    int64_t head;  // flat mode: scalar elements before the first 16-byte boundary
+    int64_t block_rows;
+    bool block_mode;
+    KPred pred;
+    KProg val;
+    uint32_t mask;
+    int32_t vdtype;
+    Partial *parts;
+    int grid;
+    hipStream_t stream;
+};
+
+// Launches the scan of `L` from a specialised kernel when the JIT policy
+// (fq_jit_config) selects it; *used tells the caller whether it did.
+fq_status jit_scan(int32_t col_dtype, bool chain, const Launch &L, bool *used);
+
+// Compiles (and caches) the specialised kernel for L's shape ahead of the
+// first scan; *ready = the shape is specialisable.  Without a device the
+// source is compiled for gfx950 only to validate it.
+fq_status jit_prepare(int32_t col_dtype, bool chain, const Launch &L, bool *ready);
+
+// Counts a fused (non-identity) scan that ran on the interpreting kernel.
+void jit_count_interp();
+
+}  // namespace fqk

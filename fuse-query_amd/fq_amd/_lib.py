@@ -17,7 +17,7 @@ GPU_SYMBOLS = [
     "fq_abi_version", "fq_last_error", "fq_device_count", "fq_fill_numbers_u64", "fq_fill_value",
     "fq_fill_splitmix64", "fq_aggregate_workspace_bytes", "fq_aggregate",
     "fq_arith_result_type", "fq_arith", "fq_compare", "fq_filter_workspace_bytes",
-    "fq_filter_compact", "fq_state_merge",
+    "fq_filter_compact", "fq_state_merge", "fq_jit_config", "fq_jit_get_stats", "fq_jit_prepare",
 ]
 
 
@@ -66,6 +66,10 @@ _protos = {
     "fq_filter_workspace_bytes": (C.c_size_t, [C.c_int64]),
     "fq_filter_compact": (C.c_int32, [P(abi.fq_col), vp, vp, P(C.c_int64), vp, C.c_size_t, vp]),
     "fq_state_merge": (C.c_int32, [P(abi.fq_agg_state), C.c_int32, P(abi.fq_agg_state)]),
+    "fq_jit_config": (C.c_int32, [C.c_int32, C.c_int64]),
+    "fq_jit_get_stats": (C.c_int32, [P(abi.fq_jit_stats)]),
+    "fq_jit_prepare": (C.c_int32, [P(abi.fq_col), C.c_int64, P(abi.fq_pred), P(abi.fq_expr), C.c_uint32,
+                                   P(C.c_int32)]),
 }
 for _name, (_res, _args) in _protos.items():
     _f = getattr(lib, _name)

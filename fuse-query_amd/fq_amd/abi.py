@@ -80,5 +80,13 @@ class fq_agg_state(C.Structure):
                 ("dtype", C.c_int32)]
 
 
+class fq_jit_stats(C.Structure):
+    _fields_ = [("kernels_compiled", C.c_int64), ("jit_launches", C.c_int64),
+                ("interp_launches", C.c_int64), ("compile_ms", C.c_double),
+                ("available", C.c_int32), ("mode", C.c_int32), ("min_rows", C.c_int64)]
+
+
+JIT_OFF, JIT_AUTO, JIT_ALWAYS = 0, 1, 2
+
 assert C.sizeof(fq_agg_state) == 48
 assert C.sizeof(fq_step) == 24

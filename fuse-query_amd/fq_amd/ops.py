@@ -208,3 +208,26 @@ def state_merge(states):
     out = abi.fq_agg_state()
     check(lib.fq_state_merge(arr, len(states), C.byref(out)))
     return out
+
+
+# ---- expression specialisation (include/fq_gpu.h fq_jit_*) ----
+def jit_config(mode, min_rows=1 << 22):
+    """Process-wide JIT policy: abi.JIT_OFF / JIT_AUTO / JIT_ALWAYS."""
+    check(lib.fq_jit_config(mode, int(min_rows)))
+
+
+def jit_stats():
+    st = abi.fq_jit_stats()
+    check(lib.fq_jit_get_stats(C.byref(st)))
+    return {f: getattr(st, f) for f, _ in abi.fq_jit_stats._fields_}
+
+
+def jit_prepare(dtype, pred=None, value=None, mask=abi.AGG_SUM, block_rows=0, length=1 << 30):
+    """Compile the specialised scan for this shape ahead of time (works
+    without a GPU: the source is then only compiled for gfx950).  Returns
+    True if the shape has a specialised kernel."""
+    c = abi.fq_col(None, int(length), dtype, 0)
+    out = C.c_int32(0)
+    check(lib.fq_jit_prepare(C.byref(c), int(block_rows), C.byref(pred) if pred is not None else None,
+                             C.byref(value) if value is not None else None, mask, C.byref(out)))
+    return bool(out.value)

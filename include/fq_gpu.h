@@ -229,6 +229,41 @@ fq_status fq_filter_compact(const fq_col *in, const uint64_t *d_bitmap, void *d_
  * summed counts/blocks, max, min, OR-ed flags).  All dtypes must match.      */
 fq_status fq_state_merge(const fq_agg_state *states, int32_t n, fq_agg_state *out);
 
+/* ---- Expression specialisation for fq_aggregate (no reference counterpart:
+ * the reference evaluates each Function node per block, function.rs:17-132).
+ * A fused predicate/argument expression is compiled once per expression
+ * SHAPE (ops, operand kinds, dtypes; constants stay kernel arguments) with
+ * hipRTC into a straight-line gfx950 scan kernel and cached for the process.
+ * Shapes below `min_rows` rows, or with the JIT off, run the precompiled
+ * program-interpreting kernel (same results, bit for bit).
+ *   mode FQ_JIT_OFF    always interpret
+ *   mode FQ_JIT_AUTO   specialise when col->len >= min_rows (default 2^22;
+ *                      silently interprets if hipRTC cannot be loaded)
+ *   mode FQ_JIT_ALWAYS specialise every fused expression; fails with
+ *                      FQ_E_UNSUPPORTED if hipRTC cannot be loaded
+ * Initial values come from $FQ_JIT (0/1/2) and $FQ_JIT_MIN_ROWS.           */
+#define FQ_JIT_OFF 0
+#define FQ_JIT_AUTO 1
+#define FQ_JIT_ALWAYS 2
+typedef struct fq_jit_stats {
+    int64_t kernels_compiled; /* distinct shapes compiled in this process        */
+    int64_t jit_launches;     /* fq_aggregate scans run by a specialised kernel  */
+    int64_t interp_launches;  /* fused scans run by the interpreting kernel      */
+    double compile_ms;        /* total hipRTC compile + module load time         */
+    int32_t available;        /* 1 if hipRTC loaded, 0 if not, -1 not tried yet  */
+    int32_t mode;
+    int64_t min_rows;
+} fq_jit_stats;
+fq_status fq_jit_config(int32_t mode, int64_t min_rows);
+fq_status fq_jit_get_stats(fq_jit_stats *out);
+/* Compiles (and caches) the specialised kernel fq_aggregate would use for
+ * this call shape, so the first scan does not pay the compile; col->data may
+ * be NULL.  *specialised = 1 if the shape has a specialised kernel (mode not
+ * OFF, a fused 64-bit expression).  Without a GPU the generated source is
+ * compiled for gfx950 only to validate it.                                  */
+fq_status fq_jit_prepare(const fq_col *col, int64_t block_rows, const fq_pred *pred,
+                         const fq_expr *value, uint32_t agg_mask, int32_t *specialised);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,93 @@
+"""The hipRTC expression specialiser (fuse-query_amd/csrc/fq_jit.hip) on CPU:
+every step/compare/predicate shape it can emit is generated and compiled for
+gfx950 through fq_jit_prepare (no GPU needed -- the code object is built but
+not loaded).  GPU parity of the compiled kernels against the oracle is in
+tests/test_kernels_gpu.py, which runs every case interpreted and specialised."""
+import ctypes as C
+
+import pytest
+
+from fq_amd import abi, ops
+from fq_amd.expr import COL, chain, predicate
+
+ALL = abi.AGG_SUM | abi.AGG_MAX | abi.AGG_MIN | abi.AGG_COUNT
+U64, I64, F64 = abi.DT_UINT64, abi.DT_INT64, abi.DT_FLOAT64
+
+
+@pytest.fixture(autouse=True, scope="module")
+def _rtc_available():
+    ops.jit_config(abi.JIT_AUTO, 1 << 22)
+    if not ops.jit_prepare(U64, value=chain(U64, [("+", 1)])[0]):
+        pytest.skip("hipRTC not loadable here")
+    if ops.jit_stats()["available"] != 1:
+        pytest.skip("hipRTC not loadable here")
+
+
+VALUE_SHAPES = [
+    (U64, [("+", 1)]), (U64, [("-", 1)]), (U64, [("*", 3)]),
+    (U64, [("/", 8)]), (U64, [("/", 7)]), (U64, [("/", 3)]), (U64, [("%", 8)]), (U64, [("%", 10)]),
+    (U64, [("/", 0)]), (U64, [("%", 0)]), (U64, [("/", 7, True)]), (U64, [("%", COL)]),
+    (U64, [("-", (5000, "Int64"))]), (U64, [("*", 3), ("/", 2.0)]), (U64, [("%", 2.5)]),
+    (U64, [("+", COL), ("*", COL), ("-", 1, True)]),
+    (I64, [("/", (-3, "Int64"))]), (I64, [("%", (7, "Int64"))]), (I64, [("+", 0.5)]),
+    (F64, [("*", 2.0), ("+", COL)]), (F64, [("/", 0.0)]), (F64, [("%", 3.0)]),
+]
+
+
+@pytest.mark.parametrize("dt,steps", VALUE_SHAPES, ids=[str(s) for _, s in VALUE_SHAPES])
+def test_value_shapes_compile(dt, steps):
+    value, _ = chain(dt, steps)
+    assert ops.jit_prepare(dt, value=value, mask=ALL)
+
+
+PRED_SHAPES = [
+    (U64, [("%", 8)], "<", 3), (U64, [], ">", 0), (U64, [], "=", COL), (U64, [("+", 1)], ">=", COL),
+    (U64, [], "<=", -1), (U64, [("-", 10)], ">", 0.5), (I64, [], "<", (-5, "Int64")),
+    (F64, [("*", 2.0)], ">=", 1.5), (F64, [], "=", COL),
+]
+
+
+@pytest.mark.parametrize("dt,lhs,cmp,rhs", PRED_SHAPES, ids=[str(p) for p in PRED_SHAPES])
+def test_predicate_shapes_compile_flat_and_block(dt, lhs, cmp, rhs):
+    pred = predicate(dt, lhs, cmp, rhs)
+    value, _ = chain(dt, [("+", 1)])
+    # flat (no sum) and block mode (sum with >1 reference block)
+    assert ops.jit_prepare(dt, pred=pred, value=value, mask=abi.AGG_MAX | abi.AGG_COUNT, block_rows=10000)
+    assert ops.jit_prepare(dt, pred=pred, mask=ALL, block_rows=10000)
+
+
+def test_bitmap_predicate_compiles():
+    p = abi.fq_pred()
+    p.kind = abi.PRED_BITMAP
+    assert ops.jit_prepare(U64, pred=p, mask=ALL, block_rows=10000)
+    assert ops.jit_prepare(F64, pred=p, mask=abi.AGG_MIN)
+
+
+def test_unspecialised_shapes():
+    # identity scans use the precompiled kernels; narrow columns interpret
+    assert not ops.jit_prepare(U64, mask=ALL)
+    p = abi.fq_pred()
+    p.kind = abi.PRED_BITMAP
+    assert not ops.jit_prepare(abi.DT_INT32, pred=p, mask=ALL)
+    ops.jit_config(abi.JIT_OFF)
+    try:
+        assert not ops.jit_prepare(U64, value=chain(U64, [("+", 1)])[0])
+    finally:
+        ops.jit_config(abi.JIT_AUTO, 1 << 22)
+
+
+def test_config_roundtrip():
+    st0 = ops.jit_stats()
+    assert st0["mode"] == abi.JIT_AUTO and st0["min_rows"] == 1 << 22
+    with pytest.raises(ops.FQError):
+        ops.jit_config(7)
+
+
+def test_errors():
+    from fq_amd._lib import lib
+    assert lib.fq_jit_get_stats(None) == abi.FQ_E_INVALID
+    assert lib.fq_jit_config(0, -1) != 0
+    assert lib.fq_jit_prepare(None, 0, None, None, 0, None) != 0
+    c = abi.fq_col(None, 10, abi.DT_UTF8, 0)
+    out = C.c_int32(0)
+    assert lib.fq_jit_prepare(C.byref(c), 0, None, None, 0, C.byref(out)) != 0

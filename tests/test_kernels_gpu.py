@@ -28,6 +28,18 @@ ALL = abi.AGG_SUM | abi.AGG_MAX | abi.AGG_MIN | abi.AGG_COUNT
 AGGS = [abi.AGG_SUM, abi.AGG_MAX, abi.AGG_MIN, abi.AGG_COUNT]
 
 
+@pytest.fixture(autouse=True, params=["interp", "jit"])
+def jit_mode(request):
+    """Every case runs twice: on the precompiled program-interpreting scan and
+    on the hipRTC-specialised scan (fq_jit.hip) for the same shape."""
+    if request.param == "jit":
+        ops.jit_config(abi.JIT_ALWAYS, 0)
+    else:
+        ops.jit_config(abi.JIT_OFF)
+    yield request.param
+    ops.jit_config(abi.JIT_AUTO, 1 << 22)
+
+
 def check_against_oracle(host, dtype, block_rows, pred=None, value=None, gpu_col=None):
     """One device block vs the oracle's per-block loop over the same column."""
     col = gpu_col if gpu_col is not None else ops.from_numpy(host, dtype)
@@ -211,3 +223,35 @@ def test_filter_compaction_large_ragged():
         m = ops.compare("<", X, (thr, "UInt64"))
         kept = ops.filter_compact(X, m)
         assert np.array_equal(kept.to_numpy(), x[x < np.uint64(thr)])
+
+
+@pytest.mark.parametrize("shape", ["c4", "chain_f64", "div_col", "block_sum", "bitmap"])
+def test_specialised_scan_bit_identical_to_interpreter(shape, jit_mode):
+    """Same grid, same per-lane order: the fq_agg_state bytes must match."""
+    if jit_mode != "jit":
+        pytest.skip("compares both modes itself")
+    n = 3_000_017
+    col = ops.splitmix_column(0xC4, 0, n)
+    br, pred, value, mask = 0, None, None, ALL
+    if shape == "c4":
+        value, _ = chain(abi.DT_UINT64, [("+", 1)])
+        pred = predicate(abi.DT_UINT64, [("%", 8)], "<", 3)
+        mask = abi.AGG_MAX | abi.AGG_COUNT
+    elif shape == "chain_f64":
+        value, _ = chain(abi.DT_UINT64, [("%", 1000), ("*", 0.5), ("+", COL)])
+    elif shape == "div_col":
+        value, _ = chain(abi.DT_UINT64, [("%", 977), ("/", COL, True)])
+    elif shape == "block_sum":
+        pred = predicate(abi.DT_UINT64, [("%", 10)], "=", 3)
+        br = 10000
+    else:
+        bm = ops.compare("<", col, 2**63)
+        pred = abi.fq_pred()
+        pred.kind = abi.PRED_BITMAP
+        pred.bitmap = bm.ptr
+    before = ops.jit_stats()["jit_launches"]
+    got = bytes(ops.aggregate(col, br, pred, value, mask))
+    assert ops.jit_stats()["jit_launches"] == before + 1
+    ops.jit_config(abi.JIT_OFF)
+    exp = bytes(ops.aggregate(col, br, pred, value, mask))
+    assert got == exp
