@@ -84,26 +84,37 @@ def latest_pmc_traffic(kernel_substr):
     return None
 
 
-def cpu_baseline(sample_rows, threads):
-    """Restated reference CPU path (oracle/fq_oracle.c) on the host cores."""
+def cpu_baseline(sample_rows, threads, query="c3"):
+    """Restated reference CPU path (oracle/fq_oracle.c) on the host cores,
+    over the same query as the GPU line."""
     import oracle_c
+    from fq_amd.expr import chain, predicate
     native = True
     try:
         oracle_c.build(native=True)
     except Exception:
         native = False
-    aggs = [(abi.AGG_SUM, None), (abi.AGG_COUNT, None), (abi.AGG_MAX, None), (abi.AGG_MIN, None)]
+    pred = None
+    if query == "c2":
+        aggs = [(abi.AGG_SUM, None)]
+    elif query == "c3":
+        aggs = [(abi.AGG_SUM, None), (abi.AGG_COUNT, None), (abi.AGG_MAX, None), (abi.AGG_MIN, None)]
+    else:
+        aggs = [(abi.AGG_MAX, chain(abi.DT_UINT64, [("+", 1)])[0])]
+        pred = predicate(abi.DT_UINT64, [("%", 8)], "<", 3)
     L = oracle_c.lib(native)
     n = sample_rows
     # warmup on a small sample, then one timed run
-    oracle_c.numbers_partial(80_000_000, aggs, threads=threads, native=native)
+    oracle_c.numbers_partial(80_000_000, aggs, pred=pred, threads=threads, native=native)
     t0 = time.perf_counter()
-    rows, st, err = oracle_c.numbers_partial(n, aggs, threads=threads, native=native)
+    rows, st, err = oracle_c.numbers_partial(n, aggs, pred=pred, threads=threads, native=native)
     dt = time.perf_counter() - t0
     assert not any(st), err
-    res = [oracle_c.merge_states(op, [r[a] for r in rows]) for a, (op, _) in enumerate(aggs)]
-    s, c, mx, mn = (r[2] for r in res)
-    assert [s // c, mx, mn] == closed_form("c3", n), "cpu baseline parity"
+    res = [oracle_c.merge_states(op, [r[a] for r in rows])[2] for a, (op, _) in enumerate(aggs)]
+    if query == "c3":
+        s, c, mx, mn = res
+        res = [s // c, mx, mn]
+    assert res == closed_form(query, n), "cpu baseline parity"
     cpu = platform.processor() or platform.machine()
     try:
         for line in open("/proc/cpuinfo"):
@@ -115,10 +126,10 @@ def cpu_baseline(sample_rows, threads):
     del L
     return {
         "value": n / dt, "unit": "rows/s", "cores": threads, "kind": "port",
-        "sample": "C3 query over numbers_mt(%d): 8 partitions, one thread per partition, "
-                  "10,000-row blocks regenerated per block, one pass per aggregator "
+        "sample": "%s query over numbers_mt(%d): 8 partitions, one thread per partition, "
+                  "10,000-row blocks regenerated per block, one pass per aggregator%s "
                   "(oracle/fq_oracle.c, %s); %.2f s wall on %s (nproc=%d)"
-                  % (n, "-O3 -march=native" if native else "-O3 -march=x86-64-v2", dt, cpu,
+                  % (query.upper(), n, ", constant broadcast + filter compaction per block" if pred else "", "-O3 -march=native" if native else "-O3 -march=x86-64-v2", dt, cpu,
                      os.cpu_count() or 0),
     }
 
@@ -171,6 +182,7 @@ def main():
         raise SystemExit("PARITY FAILURE: got %r expected %r" % (res, expect))
     log(rank, "result", res, "== closed form")
 
+    jit0 = ops.jit_stats()
     eng.reset_stats()
     torch.cuda.synchronize()
     if world > 1:
@@ -189,6 +201,9 @@ def main():
     assert res == expect
 
     st = eng.stats()
+    jit1 = ops.jit_stats()
+    jitted = jit1["jit_launches"] - jit0["jit_launches"]
+    kernel = "fq_jit_scan" if jitted else "agg_flat_kernel"
     launches = max(st["scan_launches"], 1)
     avg_launch_ms = st["scan_ms"] / launches
     bytes_per_launch = st["scan_bytes"] / launches
@@ -198,7 +213,7 @@ def main():
     out = None
     if rank == 0:
         traffic = None
-        pmc = latest_pmc_traffic("agg_flat_kernel")
+        pmc = latest_pmc_traffic(kernel)
         if pmc and pmc[1]:
             traffic = pmc[0] * rows_per_launch / pmc[1]  # HBM bytes per launch, scaled to this launch size
         out = {
@@ -237,16 +252,19 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBPS,
                 "traffic": traffic,
-                "kernel": "fq_aggregate fused scan (agg_flat_kernel + finalize), one launch per partition",
+                "kernel": "fq_aggregate fused scan (%s + finalize), one launch per partition%s"
+                          % (kernel, " (hipRTC-specialised for this expression shape)" if jitted else ""),
                 "bytes_per_launch": bytes_per_launch,
             },
             "result": res,
+            "jit": {"specialised_launches": jitted, "kernels_compiled": jit1["kernels_compiled"],
+                    "compile_ms": jit1["compile_ms"], "mode": jit1["mode"]},
         }
     if world > 1:
         dist.barrier()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
-            out["cpu_baseline"] = cpu_baseline(int(args.cpu_sample_rows), args.cpu_threads)
+            out["cpu_baseline"] = cpu_baseline(int(args.cpu_sample_rows), args.cpu_threads, args.query)
         except Exception as e:  # report, never hide
             out["cpu_baseline"] = {"error": repr(e)}
     if rank == 0:

@@ -659,6 +659,13 @@ void AggFusion::end_block() {
         if (prof) {
             e0 = ctx_.res->take_event();
             e1 = ctx_.res->take_event();
+            // compile a specialised scan (first use of this expression shape)
+            // outside the timed event pair
+            fq_jit_stats js;
+            if (fq_jit_get_stats(&js) == FQ_OK &&
+                (js.mode == FQ_JIT_ALWAYS || (js.mode == FQ_JIT_AUTO && c.len >= js.min_rows)))
+                check_fq(fq_jit_prepare(&c, g.block_rows, g.has_pred ? &g.pred : nullptr,
+                                        g.value.expr.n_steps ? &g.value.expr : nullptr, g.mask, nullptr));
         }
         {
             // events and the scan's two kernels enqueue back to back even when

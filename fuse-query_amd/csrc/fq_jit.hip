@@ -128,15 +128,66 @@ std::string x_bits(int32_t tin) {
     return "(u64)x";
 }
 
-struct Gen {
-    std::string key;          // shape key (cache)
-    std::vector<uint64_t> k;  // kernel-argument constants, in emission order
-    int konst(uint64_t v) {
-        k.push_back(v);
-        return (int)k.size() - 1;
-    }
-    std::string K(uint64_t v) { return "c.k[" + std::to_string(konst(v)) + "]"; }
+// Constants of step i of the predicate ("p") or argument ("v") program are
+// kernel arguments c.p[i] / c.v[i] (fields c, m = magic, s = shift), packed
+// straight from the lowered KProg (pack_consts); the predicate's constant
+// right-hand side is c.rhs.
+constexpr int kSteps = (int)(sizeof(KProg{}.s) / sizeof(KStep));
+struct HostStep {
+    uint64_t c, m, s;
 };
+struct HostConsts {
+    uint64_t rhs;
+    HostStep p[kSteps], v[kSteps];
+};
+
+struct Gen {
+    const char *prefix = "v";
+    int step = 0;
+    std::string K(const char *field) const {
+        return std::string("c.") + prefix + "[" + std::to_string(step) + "]." + field;
+    }
+};
+
+void pack_consts(const Launch &L, HostConsts &hc) {
+    hc.rhs = L.pred.rhs;
+    for (int i = 0; i < kSteps; ++i) {
+        hc.p[i] = HostStep{L.pred.lhs.s[i].c, L.pred.lhs.s[i].magic, L.pred.lhs.s[i].shift};
+        hc.v[i] = HostStep{L.val.s[i].c, L.val.s[i].magic, L.val.s[i].shift};
+    }
+}
+
+// Binary shape key: everything the generated source depends on.
+std::string shape_key(const Launch &L, int32_t tin, bool chain, int dev) {
+    std::string k;
+    k.reserve(256);
+    auto put = [&k](int32_t v) { k.append(reinterpret_cast<const char *>(&v), sizeof v); };
+    put(dev);
+    put(tin);
+    put(L.vdtype);
+    put((int32_t)L.mask);
+    put(L.pred.kind);
+    put(L.block_mode ? 1 : 0);
+    put(chain ? 1 : 0);
+    auto prog = [&put](const KProg &p) {
+        put(p.n);
+        for (int i = 0; i < p.n; ++i) {
+            put(p.s[i].code);
+            put(p.s[i].operand);
+            put(p.s[i].reversed);
+            put(p.s[i].dtype);
+            put((int32_t)p.s[i].add);
+        }
+    };
+    if (L.pred.kind == FQ_PRED_EXPR) {
+        put(L.pred.cmp);
+        put(L.pred.cmp_dtype);
+        put(L.pred.rhs_operand);
+        prog(L.pred.lhs);
+    }
+    if (chain) prog(L.val);
+    return k;
+}
 
 // col_as(dtype, x, live): the column as the operand of a step in `dt`
 std::string col_as(Gen &g, std::string &body, int32_t tin, int32_t dt) {
@@ -148,12 +199,11 @@ std::string col_as(Gen &g, std::string &body, int32_t tin, int32_t dt) {
 }
 
 // Straight-line code for one lowered program acting on `a`.
-void emit_prog(Gen &g, std::string &body, const KProg &p, int32_t tin) {
-    g.key += "P" + std::to_string(p.n) + ":";
+void emit_prog(Gen &g, std::string &body, const KProg &p, int32_t tin, const char *prefix) {
+    g.prefix = prefix;
     for (int i = 0; i < p.n; ++i) {
         const KStep &st = p.s[i];
-        g.key += std::to_string(st.code) + "," + std::to_string(st.operand) + "," + std::to_string(st.reversed) +
-                 "," + std::to_string(st.dtype) + "," + std::to_string(st.add) + ";";
+        g.step = i;
         const std::string DZ = std::to_string(FQ_STATE_DIV_ZERO) + "u";
         switch (st.code) {
             case K_NOP: continue;
@@ -162,16 +212,16 @@ void emit_prog(Gen &g, std::string &body, const KProg &p, int32_t tin) {
                 continue;
             case K_CAST_U2F: body += "    a = __builtin_bit_cast(u64, (double)a);\n"; continue;
             case K_CAST_I2F: body += "    a = __builtin_bit_cast(u64, (double)(long long)a);\n"; continue;
-            case K_SHR_U: body += "    a = a >> (u32)" + g.K(st.shift) + ";\n"; continue;
-            case K_AND_U: body += "    a = a & " + g.K(st.magic) + ";\n"; continue;
+            case K_SHR_U: body += "    a = a >> (u32)" + g.K("s") + ";\n"; continue;
+            case K_AND_U: body += "    a = a & " + g.K("m") + ";\n"; continue;
             case K_DIVM_U:
             case K_MODM_U: {
-                const std::string M = g.K(st.magic), S = g.K(st.shift);
+                const std::string M = g.K("m"), S = g.K("s");
                 body += "    { u64 q = __umul64hi(a, " + M + ");\n";
                 if (st.add) body += "      q = (((a - q) >> 1) + q) >> (u32)" + S + ";\n";
                 else body += "      q = q >> (u32)" + S + ";\n";
                 if (st.code == K_DIVM_U) body += "      a = q; }\n";
-                else body += "      a = a - q * " + g.K(st.c) + "; }\n";
+                else body += "      a = a - q * " + g.K("c") + "; }\n";
                 continue;
             }
             default: break;
@@ -179,7 +229,7 @@ void emit_prog(Gen &g, std::string &body, const KProg &p, int32_t tin) {
         // binary step with an operand b
         std::string b;
         if (st.operand == FQ_OPERAND_COLUMN) b = col_as(g, body, tin, st.dtype);
-        else b = g.K(st.c);
+        else b = g.K("c");
         body += "    { const u64 b = " + b + ";\n";
         body += st.reversed ? "      const u64 L = b, R = a;\n" : "      const u64 L = a, R = b;\n";
         switch (st.code) {
@@ -255,20 +305,16 @@ bool gen_source(const Launch &L, int32_t tin, bool chain, Gen &g, std::string &s
     const char *V = ctype(L.vdtype);
     if (!TIn || !V) return false;
     const int32_t pk = L.pred.kind;
-    g.key = "T" + std::to_string(tin) + "V" + std::to_string(L.vdtype) + "M" + std::to_string(L.mask) + "K" +
-            std::to_string(pk) + (L.block_mode ? "B" : "F");
 
     std::string pred_body, val_body;
     if (pk == FQ_PRED_EXPR) {
         const char *op = cmp_op(L.pred.cmp);
         if (!op) return false;
-        g.key += "c" + std::to_string(L.pred.cmp) + "d" + std::to_string(L.pred.cmp_dtype) + "r" +
-                 std::to_string(L.pred.rhs_operand);
         pred_body += "    u64 a = " + x_bits(tin) + ";\n";
-        emit_prog(g, pred_body, L.pred.lhs, tin);
+        emit_prog(g, pred_body, L.pred.lhs, tin, "p");
         std::string r;
         if (L.pred.rhs_operand == FQ_OPERAND_COLUMN) r = col_as(g, pred_body, tin, L.pred.cmp_dtype);
-        else r = g.K(L.pred.rhs);
+        else r = "c.rhs";
         pred_body += "    const u64 r = " + r + ";\n";
         if (L.pred.cmp_dtype == FQ_DT_UINT64) pred_body += std::string("    return a ") + op + " r;\n";
         else if (L.pred.cmp_dtype == FQ_DT_INT64)
@@ -279,21 +325,19 @@ bool gen_source(const Launch &L, int32_t tin, bool chain, Gen &g, std::string &s
         else
             return false;
     }
-    g.key += "|";
     if (chain) {
         val_body += "    u64 a = " + x_bits(tin) + ";\n";
-        emit_prog(g, val_body, L.val, tin);
+        emit_prog(g, val_body, L.val, tin, "v");
         if (L.vdtype == FQ_DT_FLOAT64) val_body += "    return __builtin_bit_cast(double, a);\n";
         else val_body += "    return (V)a;\n";
     } else {
-        g.key += "id";
         val_body += "    return (V)x;\n";
     }
 
-    const int nk = g.k.empty() ? 1 : (int)g.k.size();
     src = kCommon;
     src += "typedef " + std::string(TIn) + " TIn;\ntypedef " + V + " V;\n";
-    src += "struct Consts { u64 k[" + std::to_string(nk) + "]; };\n";
+    src += "struct Step { u64 c, m, s; };\nstruct Consts { u64 rhs; Step p[" + std::to_string(kSteps) +
+           "], v[" + std::to_string(kSteps) + "]; };\n";
     src += "__device__ __forceinline__ bool fq_pred(TIn x, const Consts &c, u32 &flags, u32 live) {\n";
     src += pk == FQ_PRED_EXPR ? pred_body : "    return true;\n";
     src += "}\n";
@@ -433,6 +477,7 @@ bool gen_source(const Launch &L, int32_t tin, bool chain, Gen &g, std::string &s
 struct Compiled {
     hipModule_t mod = nullptr;
     hipFunction_t fn = nullptr;
+    bool ok = false;  // the generator handles this shape
 };
 
 std::mutex g_mu;
@@ -505,28 +550,36 @@ bool load_rtc(int32_t mode, fq_status *err) {
 }
 
 // Looks up / compiles the kernel for L's shape.  *fn stays null when there is
-// no device (source validated only) or the generator declines the shape.
-fq_status get_kernel(int32_t col_dtype, bool chain, const Launch &L, Gen &g, hipFunction_t *fn) {
+// no device (source validated only) or the generator declines the shape
+// (*ok = false).  The hit path is one binary key and one hash lookup.
+fq_status get_kernel(int32_t col_dtype, bool chain, const Launch &L, hipFunction_t *fn, bool *ok) {
     *fn = nullptr;
-    std::string src;
-    if (!gen_source(L, col_dtype, chain, g, src)) return FQ_OK;
-    int ndev = 0, dev = -1;
-    if (hipGetDeviceCount(&ndev) == hipSuccess && ndev > 0) {
-        FQ_HIP_TRY(hipGetDevice(&dev));
-    } else {
+    *ok = false;
+    int dev = -1;
+    if (hipGetDevice(&dev) != hipSuccess) {
         (void)hipGetLastError();
+        dev = -1;
     }
-    const std::string key = std::to_string(dev) + "/" + g.key;
+    const std::string key = shape_key(L, col_dtype, chain, dev);
     std::lock_guard<std::mutex> lk(g_mu);
     auto it = g_cache.find(key);
     if (it == g_cache.end()) {
+        Gen g;
+        std::string src;
         Compiled c;
-        fq_status s = compile(src, dev, c);
-        if (s != FQ_OK) return s;
-        if (dev < 0) return FQ_OK;
+        if (gen_source(L, col_dtype, chain, g, src)) {
+            fq_status s = compile(src, dev, c);
+            if (s != FQ_OK) return s;
+            c.ok = true;
+        }
+        if (dev < 0) {  // nothing loaded; do not cache
+            *ok = c.ok;
+            return FQ_OK;
+        }
         it = g_cache.emplace(key, c).first;
     }
     *fn = it->second.fn;
+    *ok = it->second.ok;
     return FQ_OK;
 }
 
@@ -538,12 +591,8 @@ fq_status jit_prepare(int32_t col_dtype, bool chain, const Launch &L, bool *read
     if (mode == FQ_JIT_OFF || !eligible(col_dtype, chain, L)) return FQ_OK;
     fq_status err;
     if (!load_rtc(mode, &err)) return err;
-    Gen g;
     hipFunction_t fn;
-    fq_status s = get_kernel(col_dtype, chain, L, g, &fn);
-    if (s != FQ_OK) return s;
-    *ready = !g.key.empty();
-    return FQ_OK;
+    return get_kernel(col_dtype, chain, L, &fn, ready);
 }
 
 fq_status jit_scan(int32_t col_dtype, bool chain, const Launch &L, bool *used) {
@@ -553,18 +602,18 @@ fq_status jit_scan(int32_t col_dtype, bool chain, const Launch &L, bool *used) {
     if (mode == FQ_JIT_AUTO && L.n < jit_min_rows()) return FQ_OK;
     fq_status err;
     if (!load_rtc(mode, &err)) return err;
-    Gen g;
     hipFunction_t fn;
-    fq_status s = get_kernel(col_dtype, chain, L, g, &fn);
+    bool ok;
+    fq_status s = get_kernel(col_dtype, chain, L, &fn, &ok);
     if (s != FQ_OK) return s;
     if (!fn) return FQ_OK;
-    std::vector<uint64_t> k = g.k;
-    if (k.empty()) k.push_back(0);
+    HostConsts hc;
+    pack_consts(L, hc);
     const void *col = L.col;
     long long n = L.n, head = L.head, R = L.block_rows;
     const uint64_t *bitmap = L.pred.bitmap;
     Partial *parts = L.parts;
-    void *args[] = {&col, &n, &head, &R, &bitmap, k.data(), &parts};
+    void *args[] = {&col, &n, &head, &R, &bitmap, &hc, &parts};
     FQ_HIP_TRY(hipModuleLaunchKernel(fn, (unsigned)L.grid, 1, 1, kThreads, 1, 1, 0, L.stream, args, nullptr));
     g_jit_launches += 1;
     *used = true;
