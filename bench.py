@@ -47,6 +47,9 @@ QUERIES = {
     "c3": ("SELECT sum(number)/count(number), max(number), min(number) FROM system.numbers_mt({N})",
            abi.AGG_SUM | abi.AGG_COUNT | abi.AGG_MAX | abi.AGG_MIN),
     "c4": ("SELECT max(number+1) FROM system.numbers_mt({N}) WHERE (number%8)<3", abi.AGG_MAX | abi.AGG_COUNT),
+    # not a BASELINE config: filtered SUM, which needs the per-block emptiness
+    # of the reference's state machine (block-mode scan)
+    "c4s": ("SELECT sum(number+1) FROM system.numbers_mt({N}) WHERE (number%8)<3", abi.AGG_SUM),
 }
 
 
@@ -57,6 +60,12 @@ def closed_form(query, n):
         return [s]
     if query == "c3":
         return [s // n, n - 1, 0]
+    if query == "c4s":
+        tot = 0
+        for r in range(3):
+            k = (n - r + 7) // 8 if n > r else 0
+            tot += 8 * k * (k - 1) // 2 + (r + 1) * k
+        return [tot % U64]
     top = n - 1
     while top % 8 >= 3:
         top -= 1
@@ -68,11 +77,14 @@ def log(rank, *a):
         print("[bench]", *a, file=sys.stderr, flush=True)
 
 
-def latest_pmc_traffic(kernel_substr):
+def latest_pmc_traffic(kernel_substr, query):
     """HBM bytes per launch from the newest committed rocprofv3 --pmc summary
-    (profiles/*pmc*.json, written by tools/pmc_summary.py with the gfx950
-    FETCH_SIZE x2 correction already applied); None when absent."""
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")))
+    of this query (profiles/*pmc_<query>[_.]*.json, written by
+    tools/pmc_summary.py with the gfx950 FETCH_SIZE x2 correction already
+    applied); None when absent."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_%s.json" % query)) +
+                   glob.glob(os.path.join(ROOT, "profiles", "*pmc_%s_*.json" % query)),
+                   key=os.path.basename)
     for f in reversed(files):
         try:
             d = json.load(open(f))
@@ -100,7 +112,7 @@ def cpu_baseline(sample_rows, threads, query="c3"):
     elif query == "c3":
         aggs = [(abi.AGG_SUM, None), (abi.AGG_COUNT, None), (abi.AGG_MAX, None), (abi.AGG_MIN, None)]
     else:
-        aggs = [(abi.AGG_MAX, chain(abi.DT_UINT64, [("+", 1)])[0])]
+        aggs = [(abi.AGG_MAX if query == "c4" else abi.AGG_SUM, chain(abi.DT_UINT64, [("+", 1)])[0])]
         pred = predicate(abi.DT_UINT64, [("%", 8)], "<", 3)
     L = oracle_c.lib(native)
     n = sample_rows
@@ -213,7 +225,7 @@ def main():
     out = None
     if rank == 0:
         traffic = None
-        pmc = latest_pmc_traffic(kernel)
+        pmc = latest_pmc_traffic(kernel, args.query)
         if pmc and pmc[1]:
             traffic = pmc[0] * rows_per_launch / pmc[1]  # HBM bytes per launch, scaled to this launch size
         out = {
