@@ -156,16 +156,23 @@ def main():
     ap.add_argument("--cpu-sample-rows", type=float, default=4e9)
     ap.add_argument("--cpu-threads", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
+                    help="nccl = RCCL over xGMI (default); gloo rehearses N ranks on fewer GPUs")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     ops.require_gpu()
+    if args.dist_backend == "gloo":
+        local = local % torch.cuda.device_count()  # rehearsal: ranks may share a GPU
     torch.cuda.set_device(local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
 
     rows_per_gpu = int(args.rows_per_gpu)
     n_total = rows_per_gpu * world
@@ -207,7 +214,7 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda" if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     assert res == expect
@@ -252,7 +259,8 @@ def main():
                 "path": "fq_engine_execute: SQL -> PipelineBuilder -> Source x P -> AggregatePartial x P "
                         "(fused gfx950 scan) -> Merge -> AggregateFinal"
                         + ("" if world == 1 else " ; cross-GPU: one RCCL all-reduce of partial states"),
-                "parallelism": "dp%d (numbers_mt partitions sharded, RCCL all-reduce of states)" % world,
+                "parallelism": "dp%d (numbers_mt partitions sharded, %s all-reduce of states)"
+                               % (world, "RCCL" if args.dist_backend == "nccl" else "gloo rehearsal"),
             },
             "achieved_hbm_gbps": achieved,
             "kernel_ms_per_launch": avg_launch_ms,
