@@ -146,6 +146,8 @@ fq_status fq_engine_execute(fq_engine *e, const char *sql, fq_result **out) {
     *out = nullptr;
     return guard([&] {
         fq::ExecCtx ctx(e->rt.get());
+        const int64_t t0 = fq::now_ns();
+        e->rt->stats.query_t0 = t0;
         auto qctx = make_ctx(e, 0, 1);
         fq::QueryPlan plan = fq::build_from_sql(sql, *qctx);
         auto r = std::make_unique<fq_result>();
@@ -159,9 +161,12 @@ fq_status fq_engine_execute(fq_engine *e, const char *sql, fq_result **out) {
             r->rows = 2;
         } else {
             fq::Pipeline p = fq::build_pipeline(plan, qctx);
+            const int64_t t1 = fq::now_ns();
+            e->rt->stats.plan_ns += (uint64_t)(t1 - t0);
             fq::StreamRef s = p.execute();
             fq::DataBlock b;
             while (s->next(b)) append_block(r.get(), b, ctx);
+            e->rt->stats.exec_ns += (uint64_t)(fq::now_ns() - t1);
             if (r->names.empty())
                 for (const auto &f : plan.nodes.back().schema->fields) {
                     r->names.push_back(f.name);
@@ -268,6 +273,9 @@ fq_status fq_engine_get_stats(fq_engine *e, fq_engine_stats *out) {
     out->scan_bytes = e->rt->stats.scan_bytes.load();
     out->scan_ms = (double)e->rt->stats.scan_ns.load() * 1e-6;
     out->queries = e->rt->stats.queries.load();
+    out->plan_ms = (double)e->rt->stats.plan_ns.load() * 1e-6;
+    out->exec_ms = (double)e->rt->stats.exec_ns.load() * 1e-6;
+    out->first_launch_ms = (double)e->rt->stats.first_launch_ns.load() * 1e-6;
     return FQ_OK;
 }
 
@@ -278,6 +286,9 @@ fq_status fq_engine_reset_stats(fq_engine *e) {
     e->rt->stats.scan_bytes = 0;
     e->rt->stats.scan_ns = 0;
     e->rt->stats.queries = 0;
+    e->rt->stats.plan_ns = 0;
+    e->rt->stats.exec_ns = 0;
+    e->rt->stats.first_launch_ns = 0;
     return FQ_OK;
 }
 

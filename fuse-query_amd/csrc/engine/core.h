@@ -15,6 +15,7 @@
 #include <stdint.h>
 
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <deque>
 #include <thread>
@@ -27,6 +28,13 @@
 #include "fq_gpu.h"
 
 namespace fq {
+
+// steady-clock nanoseconds (host phase timers in RuntimeStats)
+inline int64_t now_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+
 
 using DataType = int32_t;  // FQ_DT_*
 class AggFusion;
@@ -127,6 +135,10 @@ using SchemaRef = std::shared_ptr<const DataSchema>;
 struct EngineStats {
     std::atomic<uint64_t> scan_launches{0}, scan_rows{0}, scan_bytes{0}, queries{0};
     std::atomic<uint64_t> scan_ns{0};
+    std::atomic<uint64_t> plan_ns{0}, exec_ns{0}, first_launch_ns{0};
+    // query start (steady_clock ns) while a query runs; the first scan launch
+    // of the query adds (launch - start) to first_launch_ns and clears it
+    std::atomic<int64_t> query_t0{0};
 };
 
 struct WorkerRes {

@@ -678,6 +678,8 @@ void AggFusion::end_block() {
             if (prof) check_hip(hipEventRecord(e1, ctx_.stream()), "hipEventRecord");
         }
         launched_ = true;
+        if (const int64_t q0 = ctx_.rt->stats.query_t0.exchange(0))
+            ctx_.rt->stats.first_launch_ns += (uint64_t)(now_ns() - q0);
         if (prof) events_.push_back({e0, e1});
         ctx_.rt->stats.scan_launches++;
         ctx_.rt->stats.scan_rows += (uint64_t)g.col.len;

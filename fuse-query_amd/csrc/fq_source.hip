@@ -38,7 +38,7 @@ __global__ void __launch_bounds__(256)
             v.x = i0;
             v.y = i0 + 1;
         }
-        __builtin_nontemporal_store(v, vp + p);
+        vp[p] = v;
     }
 }
 
@@ -55,7 +55,9 @@ static fq_status fill(uint64_t *d_out, uint64_t begin, uint64_t seed, uint64_t c
     if (count == 0) return FQ_OK;
     if (!d_out) return fqc::fail(FQ_E_INVALID, "fill: NULL output");
     if ((uintptr_t)d_out & 7u) return fqc::fail(FQ_E_INVALID, "fill: output not 8-byte aligned");
-    const int max_grid = fqc::device_cu_count() * 8;
+    // one workgroup per CU streams writes fastest (tools/tune_scan.py --write,
+    // profiles/r01_tune_write_10gb.json: 6.0 TB/s vs 4.8 at 8 per CU)
+    const int max_grid = fqc::device_cu_count();
     uint64_t head = ((uintptr_t)d_out & 15u) ? 1 : 0;
     if (head > count) head = count;
     if (head) {

@@ -162,3 +162,96 @@ extern "C" fq_status fq_tune_scan_u64(const uint64_t *col, int64_t n, int32_t va
 #undef FQ_T
     return fqc::fail(FQ_E_INVALID, "fq_tune_scan_u64: unknown variant");
 }
+
+namespace fqk {
+
+// ---------------------------------------------------------------------------
+// Write-side variants: out[i] = base + i (fill) and out[i] = in[i] + 1 (a
+// read+write stream, the shape of fq_arith), for tools/tune_scan.py --write.
+// ---------------------------------------------------------------------------
+template <int NT>
+__device__ __forceinline__ void st16(u32x4_t *p, u32x4_t v) {
+    if constexpr (NT == 1) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
+__device__ __forceinline__ u32x4_t iota2(uint64_t i0) {
+    u32x4_t v;
+    v.x = (uint32_t)i0;
+    v.y = (uint32_t)(i0 >> 32);
+    v.z = (uint32_t)(i0 + 1);
+    v.w = (uint32_t)((i0 + 1) >> 32);
+    return v;
+}
+
+__device__ __forceinline__ u32x4_t add1(u32x4_t r) {
+    uint64_t a = ((uint64_t)r.y << 32) | r.x, b = ((uint64_t)r.w << 32) | r.z;
+    a += 1;
+    b += 1;
+    u32x4_t v;
+    v.x = (uint32_t)a;
+    v.y = (uint32_t)(a >> 32);
+    v.z = (uint32_t)b;
+    v.w = (uint32_t)(b >> 32);
+    return v;
+}
+
+// KIND 0 fill, 1 add; MAP 0 grid-stride by vector, 2 tile-contiguous
+template <int KIND, int U, int NT, int MAP>
+__global__ void tune_write_kernel(const uint64_t *__restrict__ in, uint64_t *__restrict__ out, int64_t n) {
+    const u32x4_t *ip = reinterpret_cast<const u32x4_t *>(in);
+    u32x4_t *op = reinterpret_cast<u32x4_t *>(out);
+    const int64_t nvec = n / 2;
+    const int64_t B = blockDim.x;
+    if constexpr (MAP == 0) {
+        const int64_t T = (int64_t)gridDim.x * B;
+        for (int64_t v = (int64_t)blockIdx.x * B + threadIdx.x; v < nvec; v += T) {
+            if constexpr (KIND == 0) st16<NT>(op + v, iota2(2 * (uint64_t)v));
+            else st16<NT>(op + v, add1(ld16<NT>(ip + v)));
+        }
+    } else {
+        const int64_t tile = (int64_t)U * B;
+        const int64_t ntiles = nvec / tile;
+        for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+            const int64_t base = t * tile + threadIdx.x;
+            if constexpr (KIND == 0) {
+#pragma unroll
+                for (int k = 0; k < U; ++k) {
+                    const int64_t v = base + (int64_t)k * B;
+                    st16<NT>(op + v, iota2(2 * (uint64_t)v));
+                }
+            } else {
+                u32x4_t r[U];
+#pragma unroll
+                for (int k = 0; k < U; ++k) r[k] = ld16<NT>(ip + base + (int64_t)k * B);
+#pragma unroll
+                for (int k = 0; k < U; ++k) st16<NT>(op + base + (int64_t)k * B, add1(r[k]));
+            }
+        }
+        for (int64_t v = ntiles * tile + (int64_t)blockIdx.x * B + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * B) {
+            if constexpr (KIND == 0) st16<NT>(op + v, iota2(2 * (uint64_t)v));
+            else st16<NT>(op + v, add1(ld16<NT>(ip + v)));
+        }
+    }
+}
+
+}  // namespace fqk
+
+// variant = KIND*1000 + U*100 + NT*10 + MAP
+extern "C" fq_status fq_tune_write_u64(const uint64_t *in, uint64_t *out, int64_t n, int32_t variant, int32_t grid,
+                                       int32_t block, void *stream) {
+    using namespace fqk;
+    hipStream_t st = (hipStream_t)stream;
+    const int KIND = variant / 1000, U = (variant / 100) % 10, NT = (variant / 10) % 10, MAP = variant % 10;
+#define FQ_W(kd, u, nt, m)                                                                                  \
+    if (KIND == kd && U == u && NT == nt && MAP == m) {                                                     \
+        hipLaunchKernelGGL((tune_write_kernel<kd, u, nt, m>), dim3(grid), dim3(block), 0, st, in, out, n); \
+        FQ_HIP_TRY(hipGetLastError());                                                                      \
+        return FQ_OK;                                                                                       \
+    }
+#define FQ_WU(kd, u) FQ_W(kd, u, 0, 0) FQ_W(kd, u, 1, 0) FQ_W(kd, u, 0, 2) FQ_W(kd, u, 1, 2)
+    FQ_WU(0, 1) FQ_WU(0, 2) FQ_WU(0, 4) FQ_WU(0, 8) FQ_WU(1, 1) FQ_WU(1, 2) FQ_WU(1, 4) FQ_WU(1, 8)
+#undef FQ_WU
+#undef FQ_W
+    return fqc::fail(FQ_E_INVALID, "fq_tune_write_u64: unknown variant");
+}

@@ -255,3 +255,78 @@ def test_specialised_scan_bit_identical_to_interpreter(shape, jit_mode):
     ops.jit_config(abi.JIT_OFF)
     exp = bytes(ops.aggregate(col, br, pred, value, mask))
     assert got == exp
+
+
+def _trunc_divmod(a, b):
+    q = (np.abs(a) // np.abs(b)) * (np.sign(a) * np.sign(b))
+    return q, a - q * b
+
+
+@pytest.mark.parametrize("n", [4096 * 3, 4096 * 3 + 1, 512 * 7 + 63, 200_003])
+@pytest.mark.parametrize("dt", [abi.DT_UINT64, abi.DT_INT64, abi.DT_FLOAT64])
+def test_elementwise_vector_fast_paths(n, dt, jit_mode):
+    """64-bit same-type operands take the 16-byte vector kernels for whole
+    tiles and the generic kernels for the rest; both must agree with numpy
+    (arrow semantics: wrapping ints, truncating integer division)."""
+    if jit_mode != "interp":
+        pytest.skip("no expression program involved")
+    rng = np.random.default_rng(n + dt)
+    if dt == abi.DT_UINT64:
+        a = rng.integers(0, 2**64, size=n, dtype=np.uint64)
+        b = rng.integers(1, 2**40, size=n, dtype=np.uint64)
+        k = (12345, "UInt64")
+    elif dt == abi.DT_INT64:
+        a = rng.integers(-2**62, 2**62, size=n, dtype=np.int64)
+        b = rng.integers(-2**30, 2**30, size=n, dtype=np.int64)
+        b[b == 0] = 7
+        k = (-977, "Int64")
+    else:
+        a = rng.standard_normal(n) * 1e6
+        b = rng.standard_normal(n)
+        a[::97] = np.nan
+        k = 0.75
+    A, B = ops.from_numpy(a, dt), ops.from_numpy(b, dt)
+    kv = np.array([k[0] if isinstance(k, tuple) else k], dtype=a.dtype)[0]
+    with np.errstate(all="ignore"):
+        for sym in "+-*/%":
+            for lhs, rhs, x, y in ((A, B, a, b), (A, k, a, kv), (k, B, kv, b)):
+                got = ops.arith(sym, lhs, rhs).to_numpy()
+                if sym == "+":
+                    exp = x + y
+                elif sym == "-":
+                    exp = x - y
+                elif sym == "*":
+                    exp = x * y
+                elif dt == abi.DT_FLOAT64:
+                    exp = x / y if sym == "/" else np.fmod(x, y)
+                elif dt == abi.DT_UINT64:
+                    exp = x // y if sym == "/" else x % y
+                else:
+                    q, r = _trunc_divmod(np.asarray(x, np.int64), np.asarray(y, np.int64))
+                    exp = q if sym == "/" else r
+                exp = np.broadcast_to(exp, (n,))
+                if dt == abi.DT_FLOAT64:
+                    assert np.array_equal(got, exp, equal_nan=True), sym
+                else:
+                    assert np.array_equal(got, exp), sym
+        for sym, f in (("=", np.equal), ("<", np.less), ("<=", np.less_equal), (">", np.greater),
+                       (">=", np.greater_equal)):
+            assert np.array_equal(ops.compare(sym, A, B).to_numpy(), f(a, b)), sym
+            assert np.array_equal(ops.compare(sym, A, k).to_numpy(), f(a, kv)), sym
+    # misaligned slices (8-byte offset) fall back to the generic kernels
+    As = ops.DeviceColumn(A.buf, n - 1, dt, offset=8)
+    Bs = ops.DeviceColumn(B.buf, n - 1, dt, offset=8)
+    with np.errstate(all="ignore"):
+        assert np.array_equal(ops.arith("+", As, Bs).to_numpy(), (a[1:] + b[1:]), equal_nan=dt == abi.DT_FLOAT64)
+    assert np.array_equal(ops.compare("<", As, Bs).to_numpy(), a[1:] < b[1:])
+
+
+def test_elementwise_fast_path_div_zero_in_tile_and_tail():
+    n = 4096 * 2 + 100
+    a = np.arange(n, dtype=np.uint64)
+    for zero_at in (5, 4096 + 17, n - 3):  # inside a vector tile / in the generic tail
+        b = np.ones(n, np.uint64)
+        b[zero_at] = 0
+        with pytest.raises(ops.FQError) as ei:
+            ops.arith("%", ops.from_numpy(a), ops.from_numpy(b))
+        assert str(ei.value) == "Internal Error: Divide by zero error"
