@@ -6,7 +6,7 @@
 //   count   one workgroup per tile, popcount of its 256 words -> counts[tile]
 //   scan    one workgroup, exclusive scan of the tile counts (+ total)
 //   scatter one workgroup per tile: LDS scan of its word popcounts, then each
-//           wave walks 64 words; lane l moves row 64w+l to
+//           wave walks 64 words, 8 at a time; lane l moves row 64w+l to
 //           base + word_offset + popcount(word & lanemask_lt(l)).
 // Reads and writes are contiguous per wave; the bitmap is read twice
 // (1/64 of a u64 column's bytes each time).
@@ -102,14 +102,26 @@ __global__ void __launch_bounds__(kTileWords)
     __syncthreads();
     const uint64_t base = offsets[blockIdx.x];
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    for (int j = 0; j < kWave; ++j) {
-        const int wi = wave * kWave + j;
-        const uint64_t wd = s_word[wi];
-        if (wd == 0) continue;  // wave-uniform
-        const int64_t row = (w0 + wi) * 64 + lane;
-        if ((wd >> lane) & 1ull) {
-            const uint64_t pos = base + s_off[wi] + (uint64_t)__popcll(wd & lt_mask);
-            out[pos] = in[row];
+    // 8 words per step: all loads of the step are issued before the first
+    // store (8 rows per lane in flight); empty words are skipped (uniform).
+    constexpr int kStep = 8;
+    for (int j = 0; j < kWave; j += kStep) {
+        T x[kStep];
+        uint64_t wd[kStep];
+#pragma unroll
+        for (int k = 0; k < kStep; ++k) {
+            const int wi = wave * kWave + j + k;
+            wd[k] = s_word[wi];
+            const int64_t row = (w0 + wi) * 64 + lane;
+            x[k] = ((wd[k] >> lane) & 1ull) ? __builtin_nontemporal_load(in + row) : T(0);
+        }
+#pragma unroll
+        for (int k = 0; k < kStep; ++k) {
+            const int wi = wave * kWave + j + k;
+            if ((wd[k] >> lane) & 1ull) {
+                const uint64_t pos = base + s_off[wi] + (uint64_t)__popcll(wd[k] & lt_mask);
+                out[pos] = x[k];
+            }
         }
     }
 }
