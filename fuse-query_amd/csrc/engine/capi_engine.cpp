@@ -302,6 +302,27 @@ int32_t fq_result_column_type(const fq_result *r, int32_t col) {
     if (!r || col < 0 || col >= (int32_t)r->types.size()) return -1;
     return r->types[(size_t)col];
 }
+fq_status fq_result_mysql_type(const fq_result *r, int32_t col, int32_t *out) {
+    if (!r || !out || col < 0 || col >= (int32_t)r->types.size())
+        return fqc::fail(FQ_E_INVALID, "fq_result_mysql_type: out of range");
+    // MySQLStream::execute (servers/mysql/mysql_stream.rs:30-62)
+    switch (r->types[(size_t)col]) {
+        case FQ_DT_INT8:
+        case FQ_DT_INT16:
+        case FQ_DT_INT32:
+        case FQ_DT_INT64:
+        case FQ_DT_UINT8:
+        case FQ_DT_UINT16:
+        case FQ_DT_UINT32:
+        case FQ_DT_UINT64: *out = FQ_MYSQL_TYPE_LONG; return FQ_OK;
+        case FQ_DT_FLOAT32:
+        case FQ_DT_FLOAT64: *out = FQ_MYSQL_TYPE_FLOAT; return FQ_OK;
+        case FQ_DT_UTF8: *out = FQ_MYSQL_TYPE_VARCHAR; return FQ_OK;
+        default:
+            return fqc::internal(std::string("Unsupported column type:") + fqc::dtype_name(r->types[(size_t)col]));
+    }
+}
+
 fq_status fq_result_value(const fq_result *r, int64_t row, int32_t col, fq_value *out) {
     if (!r || !out || col < 0 || col >= (int32_t)r->cols.size() || row < 0 ||
         row >= (int64_t)r->cols[(size_t)col].size())

@@ -411,6 +411,34 @@ fq_status lower_expr(const fq_expr &e, int32_t col_dtype, KProg &out, int32_t &r
     return FQ_OK;
 }
 
+// fq_pred (semantic) -> KPred (lowered): predicate program cast to the
+// comparison type.
+fq_status lower_pred(const fq_pred *pred, int32_t col_dtype, int64_t len, bool need_data, KPred &out) {
+    out = KPred{};
+    out.kind = pred ? pred->kind : FQ_PRED_NONE;
+    if (out.kind == FQ_PRED_EXPR) {
+        int32_t ldt = col_dtype;
+        fq_status s = lower_expr(pred->lhs, col_dtype, out.lhs, ldt);
+        if (s != FQ_OK) return s;
+        if (!is_chain_dtype(pred->cmp_dtype))
+            return fqc::fail(FQ_E_UNSUPPORTED, "fused comparison type must be UInt64, Int64 or Float64");
+        s = push_cast(ldt, pred->cmp_dtype, out.lhs);
+        if (s != FQ_OK) return s;
+        if (pred->rhs_operand == FQ_OPERAND_COLUMN && col_dtype == FQ_DT_FLOAT64 && pred->cmp_dtype != FQ_DT_FLOAT64)
+            return fqc::fail(FQ_E_INVALID, "fq_pred: Float64 column compared as integer");
+        out.cmp = pred->cmp;
+        out.cmp_dtype = pred->cmp_dtype;
+        out.rhs_operand = pred->rhs_operand;
+        out.rhs = pred->rhs_bits;
+    } else if (out.kind == FQ_PRED_BITMAP) {
+        if (need_data && !pred->bitmap && len > 0) return fqc::fail(FQ_E_INVALID, "fq_pred: NULL bitmap");
+        out.bitmap = pred->bitmap;
+    } else if (out.kind != FQ_PRED_NONE) {
+        return fqc::fail(FQ_E_INVALID, "fq_pred: bad kind");
+    }
+    return FQ_OK;
+}
+
 template <typename TIn, typename V, int PRED, bool CHAIN>
 static fq_status launch_scan(const Launch &L) {
     // vectors in flight per lane: 64 B for 64-bit columns, 16 elements otherwise
@@ -540,28 +568,8 @@ static fq_status plan_scan(const fq_col *col, int64_t block_rows, const fq_pred 
     L.vdtype = vdt;
 
     // predicate
-    L.pred.kind = pred ? pred->kind : FQ_PRED_NONE;
-    if (L.pred.kind == FQ_PRED_EXPR) {
-        int32_t ldt = col->dtype;
-        fq_status s = lower_expr(pred->lhs, col->dtype, L.pred.lhs, ldt);
-        if (s != FQ_OK) return s;
-        if (!is_chain_dtype(pred->cmp_dtype))
-            return fqc::fail(FQ_E_UNSUPPORTED, "fused comparison type must be UInt64, Int64 or Float64");
-        s = push_cast(ldt, pred->cmp_dtype, L.pred.lhs);
-        if (s != FQ_OK) return s;
-        if (pred->rhs_operand == FQ_OPERAND_COLUMN && col->dtype == FQ_DT_FLOAT64 &&
-            pred->cmp_dtype != FQ_DT_FLOAT64)
-            return fqc::fail(FQ_E_INVALID, "fq_pred: Float64 column compared as integer");
-        L.pred.cmp = pred->cmp;
-        L.pred.cmp_dtype = pred->cmp_dtype;
-        L.pred.rhs_operand = pred->rhs_operand;
-        L.pred.rhs = pred->rhs_bits;
-    } else if (L.pred.kind == FQ_PRED_BITMAP) {
-        if (need_data && !pred->bitmap && col->len > 0) return fqc::fail(FQ_E_INVALID, "fq_pred: NULL bitmap");
-        L.pred.bitmap = pred->bitmap;
-    } else if (L.pred.kind != FQ_PRED_NONE) {
-        return fqc::fail(FQ_E_INVALID, "fq_pred: bad kind");
-    }
+    fq_status ps = lower_pred(pred, col->dtype, col->len, need_data, L.pred);
+    if (ps != FQ_OK) return ps;
 
     blocks = col->len == 0 ? 0 : (uint64_t)((col->len + block_rows - 1) / block_rows);
     // Block mode only where the per-block emptiness matters (filtered sum over

@@ -1,0 +1,294 @@
+// GROUP BY hash aggregation (include/fq_gpu.h fq_group_*).
+//
+// No reference counterpart: fuse-query plans group_expr (plan_parser.rs:
+// 284-308, plan_aggregate.rs:12) but PipelineBuilder (pipeline_builder.rs:
+// 50-66) builds AggregatePartial/Final from aggr_expr only.  The semantics
+// here are the ungrouped path's (fq_aggregate) applied per key.
+//
+// Table layout in the caller's device memory (all 64-bit words):
+//   [0, 64)                     header: u32 flags (state flags | 256 = full),
+//                               u32 sentinel-used, u64 scratch counter
+//   keys[capacity + 1]          0xFFFF...FF = empty; slot `capacity` holds the
+//                               key 0xFFFF...FF itself when it occurs
+//   states[a][capacity + 1]     per aggregate a, initialised to the identity
+//                               of its kind (0, +max, lowest) so atomics need
+//                               no occupancy check
+// The accumulate kernel is generated per shape with hipRTC (fq_jit.hip
+// gen_groupby_source); init / count / extract are precompiled here.
+#include <hip/hip_runtime.h>
+
+#include <string>
+
+#include "fq_common.h"
+#include "fq_device.h"
+#include "fq_scan.h"
+
+namespace fqk {
+
+constexpr uint64_t kEmpty = ~0ull;
+constexpr uint32_t kFull = 256u;
+constexpr size_t kHdrBytes = 64;
+
+struct TableView {
+    uint32_t *hdr;
+    uint64_t *counter;
+    uint64_t *keys;
+    uint64_t *states[FQ_MAX_GROUP_AGGS];
+    int64_t cap;
+};
+
+static uint64_t identity_bits(int32_t kind, int32_t dt) {
+    if (kind == FQ_AGG_COUNT || kind == FQ_AGG_SUM) return 0;
+    if (dt == FQ_DT_UINT64) return kind == FQ_AGG_MAX ? 0ull : ~0ull;
+    if (dt == FQ_DT_INT64) return kind == FQ_AGG_MAX ? 0x8000000000000000ull : 0x7fffffffffffffffull;
+    return kind == FQ_AGG_MAX ? 0xfff0000000000000ull : 0x7ff0000000000000ull;  // -inf / +inf
+}
+
+static fq_status view(const fq_group_table *t, TableView &v) {
+    if (!t || !t->d_mem) return fqc::fail(FQ_E_INVALID, "fq_group_table: NULL table");
+    if (t->capacity < 64 || (t->capacity & (t->capacity - 1)))
+        return fqc::fail(FQ_E_INVALID, "fq_group_table: capacity must be a power of two >= 64");
+    if (t->n_aggs < 1 || t->n_aggs > FQ_MAX_GROUP_AGGS)
+        return fqc::fail(FQ_E_INVALID, "fq_group_table: n_aggs out of range");
+    if (t->key_dtype != FQ_DT_UINT64 && t->key_dtype != FQ_DT_INT64)
+        return fqc::fail(FQ_E_UNSUPPORTED, "GROUP BY keys must be UInt64 or Int64");
+    for (int a = 0; a < t->n_aggs; ++a) {
+        const int32_t k = t->kinds[a], d = t->dtypes[a];
+        if (k != FQ_AGG_COUNT && k != FQ_AGG_SUM && k != FQ_AGG_MIN && k != FQ_AGG_MAX)
+            return fqc::fail(FQ_E_INVALID, "fq_group_table: bad aggregate kind");
+        if (k == FQ_AGG_COUNT ? d != FQ_DT_UINT64 : (d != FQ_DT_UINT64 && d != FQ_DT_INT64 && d != FQ_DT_FLOAT64))
+            return fqc::fail(FQ_E_UNSUPPORTED, "GROUP BY states must be 64-bit (Count: UInt64)");
+    }
+    char *m = (char *)t->d_mem;
+    v.hdr = (uint32_t *)m;
+    v.counter = (uint64_t *)(m + 8);
+    v.keys = (uint64_t *)(m + kHdrBytes);
+    v.cap = t->capacity;
+    for (int a = 0; a < FQ_MAX_GROUP_AGGS; ++a)
+        v.states[a] = a < t->n_aggs ? v.keys + (size_t)(a + 1) * (size_t)(t->capacity + 1) : nullptr;
+    return FQ_OK;
+}
+
+struct InitArgs {
+    uint64_t *keys;
+    uint64_t *states[FQ_MAX_GROUP_AGGS];
+    uint64_t ident[FQ_MAX_GROUP_AGGS];
+    int32_t n_aggs;
+    int64_t slots;
+};
+
+__global__ void __launch_bounds__(256) group_init_kernel(InitArgs a) {
+    const int64_t T = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.slots; i += T) {
+        a.keys[i] = kEmpty;
+        for (int s = 0; s < a.n_aggs; ++s) a.states[s][i] = a.ident[s];
+    }
+}
+
+// counts occupied slots into *counter (wave-aggregated atomics)
+__global__ void __launch_bounds__(256)
+    group_count_kernel(const uint64_t *__restrict__ keys, int64_t cap, const uint32_t *hdr, uint64_t *counter) {
+    const int64_t T = (int64_t)gridDim.x * blockDim.x;
+    uint64_t c = 0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cap; i += T) c += keys[i] != kEmpty;
+    if (blockIdx.x == 0 && threadIdx.x == 0 && hdr[1]) c += 1;
+#pragma unroll
+    for (int off = kWave / 2; off > 0; off >>= 1) c += shfl_xor64(c, off);
+    if ((threadIdx.x & (kWave - 1)) == 0 && c) atomicAdd((unsigned long long *)counter, (unsigned long long)c);
+}
+
+struct ExtractArgs {
+    const uint64_t *keys;
+    const uint64_t *states[FQ_MAX_GROUP_AGGS];
+    uint64_t *out_keys;
+    uint64_t *out_states[FQ_MAX_GROUP_AGGS];
+    int32_t n_aggs;
+    int64_t cap;
+    int64_t out_cap;
+    const uint32_t *hdr;
+    uint64_t *counter;
+};
+
+__global__ void __launch_bounds__(256) group_extract_kernel(ExtractArgs a) {
+    const int64_t T = (int64_t)gridDim.x * blockDim.x;
+    const int lane = threadIdx.x & (kWave - 1);
+    // slot `cap` is the sentinel key's slot: scanned iff it was used
+    const int64_t slots = a.cap + 1;
+    for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < slots; base += T) {
+        const int64_t i = base + threadIdx.x;
+        bool occ = false;
+        if (i < a.cap) occ = a.keys[i] != kEmpty;
+        else if (i == a.cap) occ = a.hdr[1] != 0;
+        const uint64_t m = __ballot(occ);
+        if (m == 0) continue;
+        uint64_t first = 0;
+        if (lane == 0) first = atomicAdd((unsigned long long *)a.counter, (unsigned long long)__popcll(m));
+        first = __shfl((unsigned long long)first, 0, kWave);
+        if (!occ) continue;
+        const uint64_t pos = first + (uint64_t)__popcll(m & ((1ull << lane) - 1ull));
+        if ((int64_t)pos >= a.out_cap) continue;
+        a.out_keys[pos] = i < a.cap ? a.keys[i] : kEmpty;
+        for (int s = 0; s < a.n_aggs; ++s) a.out_states[s][pos] = a.states[s][i];
+    }
+}
+
+static int small_grid(int64_t work) {
+    const int64_t cap = (int64_t)fqc::device_cu_count() * 4;
+    int64_t g = (work + 255) / 256;
+    if (g < 1) g = 1;
+    return (int)(g < cap ? g : cap);
+}
+
+static fq_status read_header(const TableView &v, uint32_t &flags, uint64_t &count, hipStream_t st) {
+    uint64_t h[2] = {0, 0};
+    FQ_HIP_TRY(hipMemcpyAsync(h, v.hdr, 16, hipMemcpyDeviceToHost, st));
+    FQ_HIP_TRY(hipStreamSynchronize(st));
+    flags = (uint32_t)(h[0] & 0xffffffffu);
+    count = h[1];
+    if (flags & kFull) return fqc::fail(FQ_E_TABLE_FULL, "GROUP BY hash table is full");
+    if (flags & FQ_STATE_DIV_ZERO) return fqc::fail(FQ_E_DIVIDE_BY_ZERO, "Internal Error: Divide by zero error");
+    if (flags & FQ_STATE_CAST_NULL)
+        return fqc::fail(FQ_E_UNSUPPORTED, "cast produced nulls (nulls are not supported on the device path)");
+    return FQ_OK;
+}
+
+}  // namespace fqk
+
+extern "C" {
+
+size_t fq_group_table_bytes(int64_t capacity, int32_t n_aggs) {
+    if (capacity < 0 || n_aggs < 0) return 0;
+    return fqk::kHdrBytes + (size_t)(capacity + 1) * 8u * (size_t)(1 + n_aggs);
+}
+
+fq_status fq_group_table_init(const fq_group_table *t, void *stream) {
+    using namespace fqk;
+    TableView v;
+    fq_status s = view(t, v);
+    if (s != FQ_OK) return s;
+    hipStream_t st = (hipStream_t)stream;
+    FQ_HIP_TRY(hipMemsetAsync(v.hdr, 0, kHdrBytes, st));
+    InitArgs a{};
+    a.keys = v.keys;
+    a.n_aggs = t->n_aggs;
+    a.slots = t->capacity + 1;
+    for (int i = 0; i < t->n_aggs; ++i) {
+        a.states[i] = v.states[i];
+        a.ident[i] = identity_bits(t->kinds[i], t->dtypes[i]);
+    }
+    hipLaunchKernelGGL(group_init_kernel, dim3(small_grid(a.slots)), dim3(256), 0, st, a);
+    FQ_HIP_TRY(hipGetLastError());
+    return FQ_OK;
+}
+
+fq_status fq_group_aggregate(const fq_group_table *t, const fq_col *col, const fq_pred *pred,
+                             const fq_expr *key_expr, const fq_expr *values, void *stream) {
+    using namespace fqk;
+    TableView v;
+    fq_status s = view(t, v);
+    if (s != FQ_OK) return s;
+    if (!col) return fqc::fail(FQ_E_INVALID, "fq_group_aggregate: NULL column");
+    if (col->len < 0) return fqc::fail(FQ_E_INVALID, "fq_group_aggregate: negative length");
+    if (col->len > 0 && !col->data) return fqc::fail(FQ_E_INVALID, "fq_group_aggregate: NULL column data");
+    if (fqc::dtype_size(col->dtype) != 8 || !fqc::dtype_is_numeric(col->dtype))
+        return fqc::fail(FQ_E_UNSUPPORTED, "GROUP BY needs a 64-bit column on the device path");
+    if ((uintptr_t)col->data & 7u) return fqc::fail(FQ_E_INVALID, "fq_group_aggregate: misaligned column");
+    GroupLaunch G{};
+    G.col = col->data;
+    G.n = col->len;
+    s = lower_pred(pred, col->dtype, col->len, true, G.pred);
+    if (s != FQ_OK) return s;
+    int32_t kdt = col->dtype;
+    if (key_expr && key_expr->n_steps > 0) {
+        s = lower_expr(*key_expr, col->dtype, G.key, kdt);
+        if (s != FQ_OK) return s;
+    }
+    if (kdt != t->key_dtype)
+        return fqc::fail(FQ_E_INVALID, std::string("fq_group_aggregate: key expression is ") + fqc::dtype_name(kdt) +
+                                           ", table key is " + fqc::dtype_name(t->key_dtype));
+    G.key_dtype = kdt;
+    G.n_aggs = t->n_aggs;
+    for (int a = 0; a < t->n_aggs; ++a) {
+        G.kinds[a] = t->kinds[a];
+        G.dtypes[a] = t->dtypes[a];
+        if (t->kinds[a] == FQ_AGG_COUNT) continue;
+        int32_t vdt = col->dtype;
+        if (values && values[a].n_steps > 0) {
+            s = lower_expr(values[a], col->dtype, G.vals[a], vdt);
+            if (s != FQ_OK) return s;
+            G.chain[a] = true;
+        }
+        if (vdt != t->dtypes[a])
+            return fqc::fail(FQ_E_INVALID, "fq_group_aggregate: argument dtype does not match the table state");
+    }
+    for (int a = 0; a < FQ_MAX_GROUP_AGGS; ++a) G.states[a] = v.states[a];
+    G.keys = v.keys;
+    G.hdr = v.hdr;
+    G.capacity = t->capacity;
+    G.stream = (hipStream_t)stream;
+    const uintptr_t mis = ((uintptr_t)col->data) & 15u;
+    G.head = mis ? 1 : 0;
+    if (G.head > G.n) G.head = G.n;
+    const int64_t nvec = (G.n - G.head) / 2;
+    int64_t grid = (nvec + 1023) / 1024;
+    if (grid < 1) grid = 1;
+    const int64_t cap = (int64_t)fqc::device_cu_count() * 2;  // 64 KB LDS per workgroup: 2 per CU
+    G.grid = (int)(grid < cap ? grid : cap);
+    return jit_groupby(col->dtype, G);
+}
+
+fq_status fq_group_table_count(const fq_group_table *t, int64_t *groups, void *stream) {
+    using namespace fqk;
+    if (!groups) return fqc::fail(FQ_E_INVALID, "fq_group_table_count: NULL argument");
+    *groups = 0;
+    TableView v;
+    fq_status s = view(t, v);
+    if (s != FQ_OK) return s;
+    hipStream_t st = (hipStream_t)stream;
+    FQ_HIP_TRY(hipMemsetAsync(v.counter, 0, 8, st));
+    hipLaunchKernelGGL(group_count_kernel, dim3(small_grid(v.cap)), dim3(256), 0, st, v.keys, v.cap, v.hdr,
+                       v.counter);
+    FQ_HIP_TRY(hipGetLastError());
+    uint32_t flags;
+    uint64_t c;
+    s = read_header(v, flags, c, st);
+    if (s != FQ_OK) return s;
+    *groups = (int64_t)c;
+    return FQ_OK;
+}
+
+fq_status fq_group_table_extract(const fq_group_table *t, uint64_t *d_keys, uint64_t *const *d_states, int64_t cap,
+                                 int64_t *groups, void *stream) {
+    using namespace fqk;
+    if (!groups || !d_keys || !d_states) return fqc::fail(FQ_E_INVALID, "fq_group_table_extract: NULL argument");
+    *groups = 0;
+    TableView v;
+    fq_status s = view(t, v);
+    if (s != FQ_OK) return s;
+    hipStream_t st = (hipStream_t)stream;
+    ExtractArgs a{};
+    a.keys = v.keys;
+    a.out_keys = d_keys;
+    a.n_aggs = t->n_aggs;
+    for (int i = 0; i < t->n_aggs; ++i) {
+        if (!d_states[i]) return fqc::fail(FQ_E_INVALID, "fq_group_table_extract: NULL state output");
+        a.states[i] = v.states[i];
+        a.out_states[i] = d_states[i];
+    }
+    a.cap = v.cap;
+    a.out_cap = cap;
+    a.hdr = v.hdr;
+    a.counter = v.counter;
+    FQ_HIP_TRY(hipMemsetAsync(v.counter, 0, 8, st));
+    hipLaunchKernelGGL(group_extract_kernel, dim3(small_grid(v.cap + 1)), dim3(256), 0, st, a);
+    FQ_HIP_TRY(hipGetLastError());
+    uint32_t flags;
+    uint64_t c;
+    s = read_header(v, flags, c, st);
+    if (s != FQ_OK) return s;
+    if ((int64_t)c > cap) return fqc::fail(FQ_E_INVALID, "fq_group_table_extract: output arrays too small");
+    *groups = (int64_t)c;
+    return FQ_OK;
+}
+
+}  // extern "C"

@@ -298,6 +298,40 @@ template <typename T> __device__ __forceinline__ T vmax(T a, T b) { return b > a
 template <typename T> __device__ __forceinline__ T vmin(T a, T b) { return b < a ? b : a; }
 )";
 
+// Body of `bool fq_pred(TIn x, ...)`: the lowered predicate program on x,
+// then the comparison in cmp_dtype.
+bool emit_pred_body(Gen &g, const KPred &pr, int32_t tin, std::string &body) {
+    const char *op = cmp_op(pr.cmp);
+    if (!op) return false;
+    body += "    u64 a = " + x_bits(tin) + ";\n";
+    emit_prog(g, body, pr.lhs, tin, "p");
+    std::string r;
+    if (pr.rhs_operand == FQ_OPERAND_COLUMN) r = col_as(g, body, tin, pr.cmp_dtype);
+    else r = "c.rhs";
+    body += "    const u64 r = " + r + ";\n";
+    if (pr.cmp_dtype == FQ_DT_UINT64) body += std::string("    return a ") + op + " r;\n";
+    else if (pr.cmp_dtype == FQ_DT_INT64) body += std::string("    return (long long)a ") + op + " (long long)r;\n";
+    else if (pr.cmp_dtype == FQ_DT_FLOAT64)
+        body += std::string("    return __builtin_bit_cast(double, a) ") + op + " __builtin_bit_cast(double, r);\n";
+    else
+        return false;
+    return true;
+}
+
+// Body of `V fq_val(TIn x, ...)`: the lowered argument program (identity
+// when prog is null) returning a value of type `vname` (dtype vdt).
+void emit_value_body(Gen &g, const KProg *prog, int32_t tin, int32_t vdt, const char *prefix, const char *vname,
+                     std::string &body) {
+    if (!prog) {
+        body += std::string("    return (") + vname + ")x;\n";
+        return;
+    }
+    body += "    u64 a = " + x_bits(tin) + ";\n";
+    emit_prog(g, body, *prog, tin, prefix);
+    if (vdt == FQ_DT_FLOAT64) body += "    return __builtin_bit_cast(double, a);\n";
+    else body += std::string("    return (") + vname + ")a;\n";
+}
+
 // Full kernel source for one shape.  Returns false if the shape is outside
 // what the generator handles (the caller then interprets).
 bool gen_source(const Launch &L, int32_t tin, bool chain, Gen &g, std::string &src) {
@@ -307,32 +341,8 @@ bool gen_source(const Launch &L, int32_t tin, bool chain, Gen &g, std::string &s
     const int32_t pk = L.pred.kind;
 
     std::string pred_body, val_body;
-    if (pk == FQ_PRED_EXPR) {
-        const char *op = cmp_op(L.pred.cmp);
-        if (!op) return false;
-        pred_body += "    u64 a = " + x_bits(tin) + ";\n";
-        emit_prog(g, pred_body, L.pred.lhs, tin, "p");
-        std::string r;
-        if (L.pred.rhs_operand == FQ_OPERAND_COLUMN) r = col_as(g, pred_body, tin, L.pred.cmp_dtype);
-        else r = "c.rhs";
-        pred_body += "    const u64 r = " + r + ";\n";
-        if (L.pred.cmp_dtype == FQ_DT_UINT64) pred_body += std::string("    return a ") + op + " r;\n";
-        else if (L.pred.cmp_dtype == FQ_DT_INT64)
-            pred_body += std::string("    return (long long)a ") + op + " (long long)r;\n";
-        else if (L.pred.cmp_dtype == FQ_DT_FLOAT64)
-            pred_body += std::string("    return __builtin_bit_cast(double, a) ") + op +
-                         " __builtin_bit_cast(double, r);\n";
-        else
-            return false;
-    }
-    if (chain) {
-        val_body += "    u64 a = " + x_bits(tin) + ";\n";
-        emit_prog(g, val_body, L.val, tin, "v");
-        if (L.vdtype == FQ_DT_FLOAT64) val_body += "    return __builtin_bit_cast(double, a);\n";
-        else val_body += "    return (V)a;\n";
-    } else {
-        val_body += "    return (V)x;\n";
-    }
+    if (pk == FQ_PRED_EXPR && !emit_pred_body(g, L.pred, tin, pred_body)) return false;
+    emit_value_body(g, chain ? &L.val : nullptr, tin, L.vdtype, "v", "V", val_body);
 
     src = kCommon;
     src += "typedef " + std::string(TIn) + " TIn;\ntypedef " + V + " V;\n";
@@ -471,6 +481,288 @@ bool gen_source(const Launch &L, int32_t tin, bool chain, Gen &g, std::string &s
     return true;
 }
 
+
+// ---------------------------------------------------------------------------
+// GROUP BY (fq_group_aggregate).  Same streaming loop as the scan; each
+// passing row computes its key and arguments, updates a workgroup-private
+// LDS hash table (ds_cmpst_b64 to claim a slot, LDS atomics for the states)
+// and, when its key finds no LDS slot within kLdsProbe probes, the HBM table
+// directly.  At the end each workgroup flushes its LDS groups into the HBM
+// table (one global insert + one atomic per state per group).  HBM keys go
+// EMPTY -> key once, so a relaxed (possibly stale) read followed by a CAS is
+// enough to find or claim a slot across XCDs.
+// ---------------------------------------------------------------------------
+
+int lds_slots(int n_aggs) {
+    int s = 4096;
+    while ((int64_t)s * 8 * (1 + n_aggs) > 65536) s >>= 1;
+    return s;
+}
+
+struct HostGroupConsts {
+    uint64_t rhs;
+    HostStep p[kSteps], k[kSteps], v[FQ_MAX_GROUP_AGGS][kSteps];
+};
+
+void pack_group_consts(const GroupLaunch &G, HostGroupConsts &hc) {
+    hc.rhs = G.pred.rhs;
+    for (int i = 0; i < kSteps; ++i) {
+        hc.p[i] = HostStep{G.pred.lhs.s[i].c, G.pred.lhs.s[i].magic, G.pred.lhs.s[i].shift};
+        hc.k[i] = HostStep{G.key.s[i].c, G.key.s[i].magic, G.key.s[i].shift};
+        for (int a = 0; a < FQ_MAX_GROUP_AGGS; ++a)
+            hc.v[a][i] = HostStep{G.vals[a].s[i].c, G.vals[a].s[i].magic, G.vals[a].s[i].shift};
+    }
+}
+
+std::string group_shape_key(const GroupLaunch &G, int32_t tin, int dev) {
+    std::string k = "G";
+    auto put = [&k](int32_t v) { k.append(reinterpret_cast<const char *>(&v), sizeof v); };
+    auto prog = [&put](const KProg &p) {
+        put(p.n);
+        for (int i = 0; i < p.n; ++i) {
+            put(p.s[i].code);
+            put(p.s[i].operand);
+            put(p.s[i].reversed);
+            put(p.s[i].dtype);
+            put((int32_t)p.s[i].add);
+        }
+    };
+    put(dev);
+    put(tin);
+    put(G.key_dtype);
+    put(G.pred.kind);
+    if (G.pred.kind == FQ_PRED_EXPR) {
+        put(G.pred.cmp);
+        put(G.pred.cmp_dtype);
+        put(G.pred.rhs_operand);
+        prog(G.pred.lhs);
+    }
+    prog(G.key);
+    put(G.n_aggs);
+    for (int a = 0; a < G.n_aggs; ++a) {
+        put(G.kinds[a]);
+        put(G.dtypes[a]);
+        put(G.chain[a] ? 1 : 0);
+        if (G.chain[a]) prog(G.vals[a]);
+    }
+    return k;
+}
+
+// state update snippets: `P` = pointer expression, `v` = value of type Vi
+std::string state_update(int32_t kind, int32_t dt, const std::string &P, const std::string &v) {
+    const char *T = dt == FQ_DT_INT64 ? "long long" : (dt == FQ_DT_FLOAT64 ? "double" : "unsigned long long");
+    switch (kind) {
+        case FQ_AGG_COUNT: return "atomicAdd((unsigned long long *)(" + P + "), 1ull);";
+        case FQ_AGG_SUM:
+            if (dt == FQ_DT_FLOAT64) return "atomicAdd((double *)(" + P + "), " + v + ");";
+            return "atomicAdd((unsigned long long *)(" + P + "), (unsigned long long)(" + v + "));";
+        case FQ_AGG_MAX:
+            if (dt == FQ_DT_FLOAT64) return "amax_f64((u64 *)(" + P + "), " + v + ");";
+            return std::string("atomicMax((") + T + " *)(" + P + "), (" + T + ")(" + v + "));";
+        default:
+            if (dt == FQ_DT_FLOAT64) return "amin_f64((u64 *)(" + P + "), " + v + ");";
+            return std::string("atomicMin((") + T + " *)(" + P + "), (" + T + ")(" + v + "));";
+    }
+}
+
+bool gen_groupby_source(const GroupLaunch &G, int32_t tin, Gen &g, std::string &src) {
+    const char *TIn = ctype(tin);
+    if (!TIn || (G.key_dtype != FQ_DT_UINT64 && G.key_dtype != FQ_DT_INT64)) return false;
+    if (G.n_aggs < 1 || G.n_aggs > FQ_MAX_GROUP_AGGS) return false;
+    const int NA = G.n_aggs;
+    const int S = lds_slots(NA);
+    src = kCommon;
+    src += "typedef " + std::string(TIn) + " TIn;\n";
+    src += "struct Step { u64 c, m, s; };\nstruct Consts { u64 rhs; Step p[" + std::to_string(kSteps) + "], k[" +
+           std::to_string(kSteps) + "], v[" + std::to_string(FQ_MAX_GROUP_AGGS) + "][" + std::to_string(kSteps) +
+           "]; };\n";
+    src += "struct Tab { u64 *keys; u64 *st[" + std::to_string(FQ_MAX_GROUP_AGGS) + "]; u32 *hdr; long long mask; };\n";
+    src += "#define EMPTY 0xffffffffffffffffull\n#define NA " + std::to_string(NA) + "\n#define S " +
+           std::to_string(S) + "\n";
+    src += R"(
+__device__ __forceinline__ u64 mix(u64 z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+__device__ __forceinline__ void amax_f64(u64 *p, double v) {
+    u64 old = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    while (v > __builtin_bit_cast(double, old)) {
+        const u64 prev = atomicCAS((unsigned long long *)p, old, __builtin_bit_cast(u64, v));
+        if (prev == old) return;
+        old = prev;
+    }
+}
+__device__ __forceinline__ void amin_f64(u64 *p, double v) {
+    u64 old = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    while (v < __builtin_bit_cast(double, old)) {
+        const u64 prev = atomicCAS((unsigned long long *)p, old, __builtin_bit_cast(u64, v));
+        if (prev == old) return;
+        old = prev;
+    }
+}
+// slot of key k in the HBM table (claiming an empty one), -1 if full
+__device__ long long ginsert(const Tab &t, u64 k) {
+    if (k == EMPTY) {
+        atomicOr(&t.hdr[1], 1u);
+        return t.mask + 1;
+    }
+    long long h = (long long)(mix(k) & (u64)t.mask);
+    for (long long p = 0; p <= t.mask; ++p) {
+        const u64 cur = __hip_atomic_load(&t.keys[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (cur == k) return h;
+        if (cur == EMPTY) {
+            const u64 old = atomicCAS((unsigned long long *)&t.keys[h], EMPTY, k);
+            if (old == EMPTY || old == k) return h;
+        }
+        h = (h + 1) & t.mask;
+    }
+    atomicOr(&t.hdr[0], 256u);
+    return -1;
+}
+)";
+    // predicate, key and value functions
+    std::string body;
+    if (G.pred.kind == FQ_PRED_EXPR) {
+        if (!emit_pred_body(g, G.pred, tin, body)) return false;
+    } else {
+        body = "    return true;\n";
+    }
+    src += "__device__ __forceinline__ bool fq_pred(TIn x, const Consts &c, u32 &flags, u32 live) {\n" + body + "}\n";
+    body.clear();
+    emit_value_body(g, G.key.n ? &G.key : nullptr, tin, G.key_dtype, "k", "u64", body);
+    src += "__device__ __forceinline__ u64 fq_key(TIn x, const Consts &c, u32 &flags, u32 live) {\n" + body + "}\n";
+    for (int a = 0; a < NA; ++a) {
+        if (G.kinds[a] == FQ_AGG_COUNT) continue;
+        const char *V = ctype(G.dtypes[a]);
+        if (!V) return false;
+        body.clear();
+        emit_value_body(g, G.chain[a] ? &G.vals[a] : nullptr, tin, G.dtypes[a],
+                        ("v[" + std::to_string(a) + "]").c_str(), V, body);
+        src += std::string("__device__ __forceinline__ ") + V + " fq_val" + std::to_string(a) +
+               "(TIn x, const Consts &c, u32 &flags, u32 live) {\n" + body + "}\n";
+    }
+    // identity of each state (fq_groupby.hip initialises the HBM table the same way)
+    auto identity = [](int32_t kind, int32_t dt) -> std::string {
+        if (kind == FQ_AGG_COUNT || kind == FQ_AGG_SUM) return "0ull";
+        if (dt == FQ_DT_UINT64) return kind == FQ_AGG_MAX ? "0ull" : "0xffffffffffffffffull";
+        if (dt == FQ_DT_INT64) return kind == FQ_AGG_MAX ? "0x8000000000000000ull" : "0x7fffffffffffffffull";
+        return kind == FQ_AGG_MAX ? "0xfff0000000000000ull" : "0x7ff0000000000000ull";  // -inf / +inf
+    };
+    // per-row update
+    std::string row = "__device__ __forceinline__ void fq_row(TIn x, long long idx, const Consts &c, const Tab &t,\n"
+                      "    const u64 *__restrict__ bitmap, u64 *s_keys, u64 (*s_st)[S], u32 &flags, int *s_bypass) {\n";
+    if (G.pred.kind == FQ_PRED_EXPR) row += "    if (!fq_pred(x, c, flags, 1u)) return;\n";
+    else if (G.pred.kind == FQ_PRED_BITMAP) row += "    if (!((bitmap[idx >> 6] >> (idx & 63)) & 1ull)) return;\n";
+    row += "    (void)idx; (void)bitmap;\n    const u64 k = fq_key(x, c, flags, 1u);\n";
+    for (int a = 0; a < NA; ++a)
+        if (G.kinds[a] != FQ_AGG_COUNT)
+            row += std::string("    const ") + ctype(G.dtypes[a]) + " v" + std::to_string(a) + " = fq_val" +
+                   std::to_string(a) + "(x, c, flags, 1u);\n";
+    row += R"(    int slot = -1;
+    if (k != EMPTY && !*s_bypass) {
+        int h = (int)(mix(k) & (u64)(S - 1));
+#pragma unroll 1
+        for (int p = 0; p < 16; ++p) {
+            const u64 cur = s_keys[h];
+            if (cur == k) { slot = h; break; }
+            if (cur == EMPTY) {
+                const u64 old = atomicCAS((unsigned long long *)&s_keys[h], EMPTY, k);
+                if (old == EMPTY || old == k) { slot = h; break; }
+            }
+            h = (h + 1) & (S - 1);
+        }
+        // a full neighbourhood means the LDS table is saturated (high
+        // cardinality): stop probing it for the rest of this workgroup
+        if (slot < 0) *s_bypass = 1;
+    }
+    if (slot >= 0) {
+)";
+    for (int a = 0; a < NA; ++a)
+        row += "        " + state_update(G.kinds[a], G.dtypes[a], "&s_st[" + std::to_string(a) + "][slot]",
+                                         "v" + std::to_string(a)) + "\n";
+    row += "    } else {\n        const long long gs = ginsert(t, k);\n        if (gs >= 0) {\n";
+    for (int a = 0; a < NA; ++a)
+        row += "            " + state_update(G.kinds[a], G.dtypes[a], "&t.st[" + std::to_string(a) + "][gs]",
+                                             "v" + std::to_string(a)) + "\n";
+    row += "        }\n    }\n}\n";
+    src += row;
+
+    // kernel
+    src += R"(
+extern "C" __global__ void __launch_bounds__(256)
+fq_jit_groupby(const TIn *__restrict__ col, long long n, long long head, const u64 *__restrict__ bitmap,
+               Consts c, Tab t) {
+    __shared__ u64 s_keys[S];
+    __shared__ u64 s_st[NA][S];
+    __shared__ int s_bypass;
+    if (threadIdx.x == 0) s_bypass = 0;
+    for (int i = threadIdx.x; i < S; i += 256) {
+        s_keys[i] = EMPTY;
+)";
+    for (int a = 0; a < NA; ++a)
+        src += "        s_st[" + std::to_string(a) + "][i] = " + identity(G.kinds[a], G.dtypes[a]) + ";\n";
+    src += R"(    }
+    __syncthreads();
+    u32 flags = 0;
+    const long long T = (long long)gridDim.x * 256;
+    const long long g = (long long)blockIdx.x * 256 + threadIdx.x;
+    const long long nvec = (n - head) / 2;
+    const u32x4 *__restrict__ vp = (const u32x4 *)(col + head);
+    const long long TV = 4 * 256;
+    const long long ntiles = nvec / TV;
+    for (long long tt = blockIdx.x; tt < ntiles; tt += gridDim.x) {
+        const long long base = tt * TV + threadIdx.x;
+        u32x4 raw[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) raw[k] = __builtin_nontemporal_load(vp + base + (long long)k * 256);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            TIn x[2];
+            __builtin_memcpy(&x[0], &raw[k], 16);
+            const long long i0 = head + (base + (long long)k * 256) * 2;
+            fq_row(x[0], i0, c, t, bitmap, s_keys, s_st, flags, &s_bypass);
+            fq_row(x[1], i0 + 1, c, t, bitmap, s_keys, s_st, flags, &s_bypass);
+        }
+    }
+    for (long long v = ntiles * TV + g; v < nvec; v += T) {
+        const u32x4 raw = __builtin_nontemporal_load(vp + v);
+        TIn x[2];
+        __builtin_memcpy(&x[0], &raw, 16);
+        fq_row(x[0], head + v * 2, c, t, bitmap, s_keys, s_st, flags, &s_bypass);
+        fq_row(x[1], head + v * 2 + 1, c, t, bitmap, s_keys, s_st, flags, &s_bypass);
+    }
+    const long long tail0 = head + nvec * 2;
+    const long long nedge = head + (n - tail0);
+    for (long long e = g; e < nedge; e += T) {
+        const long long i = e < head ? e : tail0 + (e - head);
+        fq_row(col[i], i, c, t, bitmap, s_keys, s_st, flags, &s_bypass);
+    }
+    if (flags) atomicOr(&t.hdr[0], flags);
+    __syncthreads();
+    // flush this workgroup's groups into the HBM table
+    for (int i = threadIdx.x; i < S; i += 256) {
+        const u64 k = s_keys[i];
+        if (k == EMPTY) continue;
+        const long long gs = ginsert(t, k);
+        if (gs < 0) continue;
+)";
+    for (int a = 0; a < NA; ++a) {
+        const std::string sa = "s_st[" + std::to_string(a) + "][i]";
+        std::string v;
+        if (G.kinds[a] == FQ_AGG_COUNT) {
+            src += "        atomicAdd((unsigned long long *)&t.st[" + std::to_string(a) + "][gs], (unsigned long long)" + sa +
+                   ");\n";
+            continue;
+        }
+        if (G.dtypes[a] == FQ_DT_FLOAT64) v = "__builtin_bit_cast(double, " + sa + ")";
+        else v = "(" + std::string(ctype(G.dtypes[a])) + ")" + sa;
+        src += "        " + state_update(G.kinds[a], G.dtypes[a], "&t.st[" + std::to_string(a) + "][gs]", v) + "\n";
+    }
+    src += "    }\n}\n";
+    return true;
+}
+
 // ---------------------------------------------------------------------------
 // compile + cache
 // ---------------------------------------------------------------------------
@@ -490,7 +782,7 @@ std::string device_arch(int dev) {
 }
 
 // dev < 0: no device here -- compile for gfx950 to validate the source only.
-fq_status compile(const std::string &src, int dev, Compiled &out) {
+fq_status compile(const std::string &src, int dev, Compiled &out, const char *fn_name = "fq_jit_scan") {
     const Rtc &r = rtc();
     const auto t0 = std::chrono::steady_clock::now();
     hiprtcProgram prog;
@@ -514,7 +806,7 @@ fq_status compile(const std::string &src, int dev, Compiled &out) {
     r.destroy(&prog);
     if (dev >= 0) {
         FQ_HIP_TRY(hipModuleLoadData(&out.mod, code.data()));
-        FQ_HIP_TRY(hipModuleGetFunction(&out.fn, out.mod, "fq_jit_scan"));
+        FQ_HIP_TRY(hipModuleGetFunction(&out.fn, out.mod, fn_name));
     }
     const auto t1 = std::chrono::steady_clock::now();
     g_compile_us += (int64_t)std::chrono::duration_cast<std::chrono::microseconds>(t1 - t0).count();
@@ -617,6 +909,56 @@ fq_status jit_scan(int32_t col_dtype, bool chain, const Launch &L, bool *used) {
     FQ_HIP_TRY(hipModuleLaunchKernel(fn, (unsigned)L.grid, 1, 1, kThreads, 1, 1, 0, L.stream, args, nullptr));
     g_jit_launches += 1;
     *used = true;
+    return FQ_OK;
+}
+
+
+fq_status jit_groupby(int32_t col_dtype, const GroupLaunch &G) {
+    fq_status err;
+    if (!load_rtc(FQ_JIT_ALWAYS, &err)) return err;
+    int dev = -1;
+    if (hipGetDevice(&dev) != hipSuccess) {
+        (void)hipGetLastError();
+        dev = -1;
+    }
+    const std::string key = group_shape_key(G, col_dtype, dev);
+    hipFunction_t fn = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        auto it = g_cache.find(key);
+        if (it == g_cache.end()) {
+            Gen g;
+            std::string src;
+            Compiled c;
+            if (!gen_groupby_source(G, col_dtype, g, src))
+                return fqc::fail(FQ_E_UNSUPPORTED, "GROUP BY: key/aggregate types outside the device path");
+            fq_status s = compile(src, dev, c, "fq_jit_groupby");
+            if (s != FQ_OK) return s;
+            c.ok = true;
+            if (dev < 0) return FQ_OK;  // validated only
+            it = g_cache.emplace(key, c).first;
+        }
+        fn = it->second.fn;
+    }
+    if (!G.col || G.n == 0) return FQ_OK;
+    HostGroupConsts hc;
+    pack_group_consts(G, hc);
+    struct {
+        uint64_t *keys;
+        uint64_t *st[FQ_MAX_GROUP_AGGS];
+        uint32_t *hdr;
+        long long mask;
+    } tab;
+    tab.keys = G.keys;
+    for (int a = 0; a < FQ_MAX_GROUP_AGGS; ++a) tab.st[a] = G.states[a];
+    tab.hdr = G.hdr;
+    tab.mask = (long long)G.capacity - 1;
+    const void *col = G.col;
+    long long n = G.n, head = G.head;
+    const uint64_t *bitmap = G.pred.bitmap;
+    void *args[] = {&col, &n, &head, &bitmap, &hc, &tab};
+    FQ_HIP_TRY(hipModuleLaunchKernel(fn, (unsigned)G.grid, 1, 1, kThreads, 1, 1, 0, G.stream, args, nullptr));
+    g_jit_launches += 1;
     return FQ_OK;
 }
 

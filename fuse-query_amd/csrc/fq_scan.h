@@ -25,6 +25,11 @@ struct Launch {
     hipStream_t stream;
 };
 
+// Host lowering (fq_aggregate.hip): fq_expr -> KProg (res_dtype = result
+// type) and fq_pred -> KPred.
+fq_status lower_expr(const fq_expr &e, int32_t col_dtype, KProg &out, int32_t &res_dtype);
+fq_status lower_pred(const fq_pred *pred, int32_t col_dtype, int64_t len, bool need_data, KPred &out);
+
 // Launches the scan of `L` from a specialised kernel when the JIT policy
 // (fq_jit_config) selects it; *used tells the caller whether it did.
 fq_status jit_scan(int32_t col_dtype, bool chain, const Launch &L, bool *used);
@@ -33,6 +38,30 @@ fq_status jit_scan(int32_t col_dtype, bool chain, const Launch &L, bool *used);
 // first scan; *ready = the shape is specialisable.  Without a device the
 // source is compiled for gfx950 only to validate it.
 fq_status jit_prepare(int32_t col_dtype, bool chain, const Launch &L, bool *ready);
+
+// One fq_group_aggregate launch (fq_groupby.hip -> fq_jit.hip).
+struct GroupLaunch {
+    const void *col;
+    int64_t n;
+    int64_t head;
+    KPred pred;
+    KProg key;  // key expression (lowered); n == 0 = the column itself
+    int32_t key_dtype;
+    int32_t n_aggs;
+    int32_t kinds[FQ_MAX_GROUP_AGGS];
+    int32_t dtypes[FQ_MAX_GROUP_AGGS];
+    bool chain[FQ_MAX_GROUP_AGGS];
+    KProg vals[FQ_MAX_GROUP_AGGS];
+    uint64_t *keys;  // capacity + 1 slots
+    uint64_t *states[FQ_MAX_GROUP_AGGS];
+    uint32_t *hdr;
+    int64_t capacity;
+    int grid;
+    hipStream_t stream;
+};
+
+// Launches the hipRTC-specialised group-by kernel for G.
+fq_status jit_groupby(int32_t col_dtype, const GroupLaunch &G);
 
 // Counts a fused (non-identity) scan that ran on the interpreting kernel.
 void jit_count_interp();

@@ -18,6 +18,8 @@ GPU_SYMBOLS = [
     "fq_fill_splitmix64", "fq_aggregate_workspace_bytes", "fq_aggregate",
     "fq_arith_result_type", "fq_arith", "fq_compare", "fq_filter_workspace_bytes",
     "fq_filter_compact", "fq_state_merge", "fq_jit_config", "fq_jit_get_stats", "fq_jit_prepare",
+    "fq_group_table_bytes", "fq_group_table_init", "fq_group_aggregate", "fq_group_table_count",
+    "fq_group_table_extract",
 ]
 
 
@@ -70,6 +72,13 @@ _protos = {
     "fq_jit_get_stats": (C.c_int32, [P(abi.fq_jit_stats)]),
     "fq_jit_prepare": (C.c_int32, [P(abi.fq_col), C.c_int64, P(abi.fq_pred), P(abi.fq_expr), C.c_uint32,
                                    P(C.c_int32)]),
+    "fq_group_table_bytes": (C.c_size_t, [C.c_int64, C.c_int32]),
+    "fq_group_table_init": (C.c_int32, [P(abi.fq_group_table), vp]),
+    "fq_group_aggregate": (C.c_int32, [P(abi.fq_group_table), P(abi.fq_col), P(abi.fq_pred), P(abi.fq_expr),
+                                       P(abi.fq_expr), vp]),
+    "fq_group_table_count": (C.c_int32, [P(abi.fq_group_table), P(C.c_int64), vp]),
+    "fq_group_table_extract": (C.c_int32, [P(abi.fq_group_table), vp, P(C.c_void_p), C.c_int64, P(C.c_int64),
+                                           vp]),
 }
 for _name, (_res, _args) in _protos.items():
     _f = getattr(lib, _name)

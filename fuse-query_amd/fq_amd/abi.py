@@ -88,5 +88,14 @@ class fq_jit_stats(C.Structure):
 
 JIT_OFF, JIT_AUTO, JIT_ALWAYS = 0, 1, 2
 
+MAX_GROUP_AGGS = 8
+FQ_E_TABLE_FULL = 8
+
+
+class fq_group_table(C.Structure):
+    _fields_ = [("d_mem", C.c_void_p), ("capacity", C.c_int64), ("key_dtype", C.c_int32),
+                ("n_aggs", C.c_int32), ("kinds", C.c_int32 * MAX_GROUP_AGGS),
+                ("dtypes", C.c_int32 * MAX_GROUP_AGGS)]
+
 assert C.sizeof(fq_agg_state) == 48
 assert C.sizeof(fq_step) == 24

@@ -23,13 +23,14 @@ ENGINE_SYMBOLS = [
     "fq_engine_release_numbers", "fq_engine_execute", "fq_engine_explain", "fq_engine_execute_partial",
     "fq_engine_execute_final", "fq_engine_get_stats", "fq_engine_reset_stats", "fq_result_num_rows",
     "fq_result_num_columns", "fq_result_column_name", "fq_result_column_type", "fq_result_value",
-    "fq_result_text", "fq_result_free",
+    "fq_result_text", "fq_result_free", "fq_result_mysql_type",
 ]
 
 
 class fq_engine_stats(C.Structure):
     _fields_ = [("scan_launches", C.c_uint64), ("scan_rows", C.c_uint64), ("scan_bytes", C.c_uint64),
-                ("scan_ms", C.c_double), ("queries", C.c_uint64)]
+                ("scan_ms", C.c_double), ("queries", C.c_uint64), ("plan_ms", C.c_double),
+                ("exec_ms", C.c_double), ("first_launch_ms", C.c_double)]
 
 
 _protos = {
@@ -53,6 +54,7 @@ _protos = {
     "fq_result_value": (C.c_int32, [C.c_void_p, C.c_int64, C.c_int32, P(abi.fq_value)]),
     "fq_result_text": (C.c_char_p, [C.c_void_p, C.c_int64, C.c_int32]),
     "fq_result_free": (None, [C.c_void_p]),
+    "fq_result_mysql_type": (C.c_int32, [C.c_void_p, C.c_int32, P(C.c_int32)]),
 }
 for _n, (_r, _a) in _protos.items():
     _f = getattr(lib, _n)
@@ -86,6 +88,17 @@ class Result:
                 cols.append(vals)
             self.columns = cols
             self.rows = [tuple(col[r] for col in cols) for r in range(nrow)]
+            # what the reference's MySQL writer sends (mysql_stream.rs:21-84):
+            # column types, or the error it raises, and the text of every value
+            self.mysql_types, self.mysql_error = [], None
+            for c in range(ncol):
+                t = C.c_int32(0)
+                if lib.fq_result_mysql_type(ptr, c, C.byref(t)) != 0:
+                    self.mysql_error = last_error()
+                    break
+                self.mysql_types.append(t.value)
+            self.text_rows = [tuple((lambda t: t.decode() if t is not None else None)(lib.fq_result_text(ptr, r, c))
+                                    for c in range(ncol)) for r in range(nrow)]
         finally:
             lib.fq_result_free(ptr)
 

@@ -231,3 +231,73 @@ def jit_prepare(dtype, pred=None, value=None, mask=abi.AGG_SUM, block_rows=0, le
     check(lib.fq_jit_prepare(C.byref(c), int(block_rows), C.byref(pred) if pred is not None else None,
                              C.byref(value) if value is not None else None, mask, C.byref(out)))
     return bool(out.value)
+
+
+# ---- GROUP BY hash aggregation (include/fq_gpu.h fq_group_*) ----
+class GroupTable:
+    """A device hash table of groups: key -> one 64-bit state per aggregate.
+    aggs: [(abi.AGG_*, state dtype)]; Count's state dtype is UInt64."""
+
+    def __init__(self, capacity, aggs, key_dtype=abi.DT_UINT64, stream=None):
+        require_gpu()
+        cap = 64
+        while cap < capacity:
+            cap *= 2
+        self.desc = abi.fq_group_table()
+        self.desc.capacity = cap
+        self.desc.key_dtype = key_dtype
+        self.desc.n_aggs = len(aggs)
+        for i, (k, dt) in enumerate(aggs):
+            self.desc.kinds[i] = k
+            self.desc.dtypes[i] = dt
+        self.buf = torch.empty(lib.fq_group_table_bytes(cap, len(aggs)), dtype=torch.uint8, device="cuda")
+        self.desc.d_mem = self.buf.data_ptr()
+        self.aggs = list(aggs)
+        check(lib.fq_group_table_init(C.byref(self.desc), _stream(stream)))
+
+    def aggregate(self, col, pred=None, key=None, values=None, stream=None):
+        c = col.col()
+        vals = (abi.fq_expr * abi.MAX_GROUP_AGGS)()
+        for i, v in enumerate(values or []):
+            if v is not None:
+                vals[i] = v
+        check(lib.fq_group_aggregate(C.byref(self.desc), C.byref(c), C.byref(pred) if pred is not None else None,
+                                     C.byref(key) if key is not None else None, vals, _stream(stream)))
+
+    def count(self, stream=None):
+        n = C.c_int64(0)
+        check(lib.fq_group_table_count(C.byref(self.desc), C.byref(n), _stream(stream)))
+        return n.value
+
+    def extract(self, stream=None):
+        """-> (keys uint64[g], [states uint64[g] per aggregate]) in slot order."""
+        g = self.count(stream)
+        n = max(g, 1)
+        keys = torch.empty(n, dtype=torch.int64, device="cuda")
+        sts = [torch.empty(n, dtype=torch.int64, device="cuda") for _ in self.aggs]
+        ptrs = (C.c_void_p * len(sts))(*[t.data_ptr() for t in sts])
+        out = C.c_int64(0)
+        check(lib.fq_group_table_extract(C.byref(self.desc), C.c_void_p(keys.data_ptr()), ptrs, n, C.byref(out),
+                                         _stream(stream)))
+        k = keys[: out.value].cpu().numpy().view(np.uint64)
+        return k, [t[: out.value].cpu().numpy().view(np.uint64) for t in sts]
+
+
+def group_compile_check(col_dtype, aggs, key=None, values=None, pred=None, key_dtype=abi.DT_UINT64):
+    """Generate + compile the group-by kernel for a shape (no GPU needed: a
+    zero-length call compiles the source for gfx950 without loading it)."""
+    d = abi.fq_group_table()
+    d.d_mem = 0x1000  # never dereferenced for a zero-length column
+    d.capacity = 64
+    d.key_dtype = key_dtype
+    d.n_aggs = len(aggs)
+    for i, (k, dt) in enumerate(aggs):
+        d.kinds[i] = k
+        d.dtypes[i] = dt
+    c = abi.fq_col(None, 0, col_dtype, 0)
+    vals = (abi.fq_expr * abi.MAX_GROUP_AGGS)()
+    for i, v in enumerate(values or []):
+        if v is not None:
+            vals[i] = v
+    check(lib.fq_group_aggregate(C.byref(d), C.byref(c), C.byref(pred) if pred is not None else None,
+                                 C.byref(key) if key is not None else None, vals, None))

@@ -49,6 +49,9 @@ typedef struct fq_engine_stats {
     uint64_t scan_bytes;    /* algorithmic bytes those scans read               */
     double scan_ms;         /* summed event time of those launches (FQ_OPT_PROFILE) */
     uint64_t queries;
+    double plan_ms;         /* host: SQL parse + plan + PipelineBuilder, summed   */
+    double exec_ms;         /* host: pipeline execution until the result block    */
+    double first_launch_ms; /* host: query start -> first scan enqueued, summed   */
 } fq_engine_stats;
 
 /* device: HIP device ordinal.  Fails with FQ_E_HIP when no GPU is present.
@@ -95,6 +98,16 @@ int32_t fq_result_column_type(const fq_result *r, int32_t col);
 fq_status fq_result_value(const fq_result *r, int64_t row, int32_t col, fq_value *out);
 /* the value as text, DataValue's Display (NULL for None); valid until fq_result_free */
 const char *fq_result_text(const fq_result *r, int64_t row, int32_t col);
+/* MySQL column type the reference's result writer declares for a column
+ * (MySQLStream::execute, src/servers/mysql/mysql_stream.rs:30-62): integer
+ * types -> MYSQL_TYPE_LONG, Float32/64 -> MYSQL_TYPE_FLOAT, Utf8 ->
+ * MYSQL_TYPE_VARCHAR; anything else fails with "Internal Error: Unsupported
+ * column type:<DataType>".  Row values are fq_result_text (arrow
+ * array_value_to_string), column names fq_result_column_name.              */
+#define FQ_MYSQL_TYPE_LONG 3
+#define FQ_MYSQL_TYPE_FLOAT 4
+#define FQ_MYSQL_TYPE_VARCHAR 15
+fq_status fq_result_mysql_type(const fq_result *r, int32_t col, int32_t *out);
 void fq_result_free(fq_result *r);
 
 #ifdef __cplusplus

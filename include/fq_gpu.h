@@ -264,6 +264,55 @@ fq_status fq_jit_get_stats(fq_jit_stats *out);
 fq_status fq_jit_prepare(const fq_col *col, int64_t block_rows, const fq_pred *pred,
                          const fq_expr *value, uint32_t agg_mask, int32_t *specialised);
 
+/* ---- GROUP BY hash aggregation (NO reference counterpart:
+ * plan_parser.rs:284-308 plans group_expr but pipeline_builder.rs:50-66 builds
+ * AggregatePartial/Final from aggr_expr only, so the reference has no grouped
+ * semantics to match.  Here a group is a distinct value of an integer key
+ * expression over the column; each aggregate is count/sum/min/max of an
+ * argument expression over the rows of the group that pass the predicate,
+ * with the same value semantics as fq_aggregate (wrapping integer sums, f64
+ * IEEE sums in unspecified order).
+ *
+ * The table is caller-owned device memory of fq_group_table_bytes(capacity,
+ * n_aggs) bytes described by an fq_group_table; capacity is a power of two.
+ * One extra slot holds the key 0xFFFFFFFFFFFFFFFF (the empty marker).
+ * fq_group_aggregate streams a column once: every workgroup pre-aggregates
+ * in an LDS hash table and flushes its groups into the HBM table with
+ * atomics; keys that do not fit in LDS go to HBM directly.  The kernel is
+ * specialised per expression shape with hipRTC (see fq_jit_config); there is
+ * no interpreting fallback, so it fails with FQ_E_UNSUPPORTED if hipRTC
+ * cannot be loaded.  A table that runs out of slots is reported by
+ * fq_group_table_count (FQ_E_TABLE_FULL): re-run into a larger table.       */
+#define FQ_MAX_GROUP_AGGS 8
+#define FQ_E_TABLE_FULL 8
+typedef struct fq_group_table {
+    void *d_mem;       /* fq_group_table_bytes(capacity, n_aggs) bytes, device */
+    int64_t capacity;  /* slots, a power of two >= 64                          */
+    int32_t key_dtype; /* FQ_DT_UINT64 or FQ_DT_INT64                          */
+    int32_t n_aggs;    /* 1..FQ_MAX_GROUP_AGGS                                 */
+    int32_t kinds[FQ_MAX_GROUP_AGGS];  /* FQ_AGG_COUNT / SUM / MIN / MAX        */
+    int32_t dtypes[FQ_MAX_GROUP_AGGS]; /* state dtype: COUNT UInt64, else the
+                                          argument's dtype (64-bit types)      */
+} fq_group_table;
+size_t fq_group_table_bytes(int64_t capacity, int32_t n_aggs);
+/* Empties the table (async on stream). */
+fq_status fq_group_table_init(const fq_group_table *t, void *stream);
+/* Accumulates one device block: key = key_expr(x) (fq_expr over col, integer
+ * result of dtype t->key_dtype), aggregate i over values[i](x), rows kept by
+ * pred (may be NULL).  Asynchronous. */
+fq_status fq_group_aggregate(const fq_group_table *t, const fq_col *col, const fq_pred *pred,
+                             const fq_expr *key_expr, const fq_expr *values, void *stream);
+/* Number of groups (synchronises stream); FQ_E_TABLE_FULL if any insert
+ * found no free slot, FQ_E_DIVIDE_BY_ZERO / FQ_E_UNSUPPORTED for the flags
+ * fq_aggregate reports. */
+fq_status fq_group_table_count(const fq_group_table *t, int64_t *groups, void *stream);
+/* Compacts the occupied slots into d_keys[0..groups) and, per aggregate i,
+ * d_states[i][0..groups) (64-bit state bits; slot order, unsorted);
+ * *groups = the number written (synchronises stream).  cap = room in the
+ * output arrays. */
+fq_status fq_group_table_extract(const fq_group_table *t, uint64_t *d_keys, uint64_t *const *d_states,
+                                 int64_t cap, int64_t *groups, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

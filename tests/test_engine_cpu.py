@@ -105,6 +105,19 @@ def test_result_column_names_follow_function_debug(eng):
                           "FROM system.numbers_mt(80)", states)
     assert r.names == ["Sum(number) / Count(number)", "Max(number)", "Min(number)"]
     assert r.rows == [(39, 79, 0)]
+    # the reference's MySQL writer: UInt64 -> MYSQL_TYPE_LONG (mysql_stream.rs:32-45),
+    # values through arrow array_value_to_string
+    assert r.mysql_types == [3, 3, 3] and r.mysql_error is None
+    assert r.text_rows == [("39", "79", "0")]
+
+
+def test_result_mysql_float_type_and_text(eng):
+    n = R.E_field("number")
+    exprs = [R.E_fn("sum", R.E_bin("/", n, R.E_const(2.0))), R.E_fn("max", R.E_bin("*", n, R.E_const(1.5)))]
+    states = [encode_states(R.aggregate_partial_states(80, exprs, [(b, e) for _, b, e in generate_parts(80)]))]
+    r = eng.execute_final("SELECT sum(number/2.0), max(number*1.5) FROM system.numbers_mt(80)", states)
+    assert r.mysql_types == [4, 4]  # Float64 -> MYSQL_TYPE_FLOAT
+    assert r.text_rows == [("1580", "118.5")]  # Rust f64 Display
 
 
 @pytest.mark.parametrize("world", [1, 2, 3, 8])

@@ -244,3 +244,11 @@ def test_engine_stats_count_fused_scans():
         assert s["scan_launches"] == 8  # one fused scan per partition for all 4 aggregators
         assert s["scan_rows"] == 800000 and s["scan_bytes"] == 6400000
         assert s["scan_ms"] > 0
+
+
+def test_mysql_writer_types_and_boolean_error():
+    # mysql_stream.rs:30-62: Boolean has no MySQL column arm -> Internal error
+    r = q("SELECT number = 1 FROM system.numbers_mt(8)")
+    assert r.mysql_error == "Internal Error: Unsupported column type:Boolean"
+    r = q("select (number+1) as c1, number/2 as c2 from system.numbers_mt(10000000) where number+1=4 limit 10")
+    assert r.mysql_types == [3, 3] and r.text_rows == [("4", "1")]

@@ -1,0 +1,202 @@
+"""GROUP BY hash aggregation kernels (include/fq_gpu.h fq_group_*) against a
+numpy group-by on the same seeded columns.
+
+The reference has no GROUP BY execution (plan_parser.rs:284-308 plans it,
+pipeline_builder.rs:50-66 ignores group_expr), so there is nothing of the
+reference to pin these results to: they are checked against numpy with the
+ungrouped path's value semantics (wrapping u64/i64 sums, IEEE f64, f64 sums
+within a written tolerance because atomics add in no fixed order)."""
+import numpy as np
+import pytest
+
+from fq_amd import abi
+from fq_amd.expr import COL, chain, predicate
+
+pytestmark = pytest.mark.gpu
+
+ops = None
+U, I, F = abi.DT_UINT64, abi.DT_INT64, abi.DT_FLOAT64
+
+
+def setup_module():
+    global ops
+    from fq_amd import ops as _ops
+    _ops.require_gpu()
+    ops = _ops
+
+
+def np_groupby(keys, vals_list, kinds):
+    """-> {key: [state per aggregate]} with the device's state semantics."""
+    order = np.argsort(keys, kind="stable")
+    k = keys[order]
+    uniq, start = np.unique(k, return_index=True)
+    out = {}
+    bounds = list(start) + [len(k)]
+    for gi, key in enumerate(uniq):
+        sl = order[bounds[gi]:bounds[gi + 1]]
+        st = []
+        for kind, vals in zip(kinds, vals_list):
+            if kind == abi.AGG_COUNT:
+                st.append(len(sl))
+                continue
+            v = vals[sl]
+            if kind == abi.AGG_SUM:
+                st.append(v.sum(dtype=v.dtype) if v.dtype != np.float64 else float(np.sum(v)))
+            elif kind == abi.AGG_MAX:
+                st.append(v.max())
+            else:
+                st.append(v.min())
+        out[int(key)] = st
+    return out
+
+
+def decode(states, dts):
+    res = []
+    for s, dt in zip(states, dts):
+        if dt == F:
+            res.append(s.view(np.float64))
+        elif dt == I:
+            res.append(s.view(np.int64))
+        else:
+            res.append(s)
+    return res
+
+
+def run(col, aggs, key=None, values=None, pred=None, key_dtype=U, capacity=1 << 12):
+    t = ops.GroupTable(capacity, aggs, key_dtype)
+    t.aggregate(col, pred, key, values)
+    keys, states = t.extract()
+    if key_dtype == I:
+        keys = keys.view(np.int64)
+    st = decode(states, [dt for _, dt in aggs])
+    return {int(k): [st[a][i] for a in range(len(aggs))] for i, k in enumerate(keys)}
+
+
+def compare(got, exp, kinds, dts, fsum_bound=None):
+    assert set(got) == set(exp), (len(got), len(exp))
+    for k, e in exp.items():
+        g = got[k]
+        for a, (kind, dt) in enumerate(zip(kinds, dts)):
+            if dt == F and kind == abi.AGG_SUM:
+                assert abs(g[a] - e[a]) <= fsum_bound[k], (k, a, g[a], e[a])
+            elif dt == F:
+                assert g[a] == e[a] or (np.isnan(g[a]) and np.isnan(e[a])), (k, a, g[a], e[a])
+            else:
+                assert int(g[a]) == int(e[a]), (k, a, g[a], e[a])
+
+
+def test_low_cardinality_mod_key_all_aggregates():
+    n = 3_000_017
+    col = ops.splitmix_column(0x6B, 0, n)
+    x = col.to_numpy()
+    key, _ = chain(U, [("%", 1000)])
+    vf, _ = chain(U, [("*", 1.5)])
+    aggs = [(abi.AGG_COUNT, U), (abi.AGG_SUM, U), (abi.AGG_MAX, U), (abi.AGG_MIN, U), (abi.AGG_SUM, F),
+            (abi.AGG_MAX, F)]
+    got = run(col, aggs, key=key, values=[None, None, None, None, vf, vf])
+    xf = x.astype(np.float64) * 1.5
+    exp = np_groupby(x % np.uint64(1000), [None, x, x, x, xf, xf], [k for k, _ in aggs])
+    # f64 sum tolerance: 1e-12 * sum(|v|) of the group (atomic add order is unspecified)
+    k = x % np.uint64(1000)
+    bound = {int(g): 1e-12 * float(np.abs(xf[k == g]).sum()) for g in np.unique(k)}
+    compare(got, exp, [k for k, _ in aggs], [d for _, d in aggs], bound)
+
+
+def test_filtered_group_by_c4_shape():
+    # SELECT number%10, max(number+1), count(number) ... WHERE (number%8)<3 GROUP BY number%10
+    n = 2_000_000
+    col = ops.numbers_column(0, n)
+    x = np.arange(n, dtype=np.uint64)
+    key, _ = chain(U, [("%", 10)])
+    v, _ = chain(U, [("+", 1)])
+    pred = predicate(U, [("%", 8)], "<", 3)
+    aggs = [(abi.AGG_MAX, U), (abi.AGG_COUNT, U)]
+    got = run(col, aggs, key=key, values=[v, None], pred=pred)
+    m = (x % np.uint64(8)) < 3
+    exp = np_groupby((x % np.uint64(10))[m], [(x + np.uint64(1))[m], None], [abi.AGG_MAX, abi.AGG_COUNT])
+    compare(got, exp, [abi.AGG_MAX, abi.AGG_COUNT], [U, U])
+
+
+def test_high_cardinality_bypasses_lds():
+    n = 1_000_003
+    col = ops.splitmix_column(0x77, 5, n)
+    x = col.to_numpy()
+    aggs = [(abi.AGG_COUNT, U), (abi.AGG_SUM, U)]
+    got = run(col, aggs, capacity=1 << 21)
+    uniq, cnt = np.unique(x, return_counts=True)
+    assert len(got) == len(uniq)
+    for kk, c in zip(uniq[:1000], cnt[:1000]):
+        assert got[int(kk)] == [c, kk * np.uint64(c)]
+
+
+def test_signed_keys_and_states():
+    n = 500_000
+    col = ops.numbers_column(0, n)
+    x = np.arange(n, dtype=np.int64)
+    key, kdt = chain(U, [("-", (250_000, "Int64")), ("/", (1000, "Int64"))])  # Int64, negative keys
+    assert kdt == I
+    v, _ = chain(U, [("-", (300_000, "Int64"))])
+    aggs = [(abi.AGG_MIN, I), (abi.AGG_MAX, I), (abi.AGG_SUM, I)]
+    got = run(col, aggs, key=key, values=[v, v, v], key_dtype=I)
+    kk = np.trunc((x - 250_000) / 1000).astype(np.int64)  # truncating division
+    vv = x - 300_000
+    exp = np_groupby(kk, [vv, vv, vv], [abi.AGG_MIN, abi.AGG_MAX, abi.AGG_SUM])
+    compare(got, exp, [abi.AGG_MIN, abi.AGG_MAX, abi.AGG_SUM], [I, I, I])
+
+
+def test_empty_marker_key_gets_its_own_slot():
+    col = ops.numbers_column(0, 10_000)
+    key, _ = chain(U, [("*", 0), ("-", 1)])  # every key = 2^64-1 (the table's empty marker)
+    got = run(col, [(abi.AGG_COUNT, U), (abi.AGG_MAX, U)], key=key)
+    assert got == {2**64 - 1: [10_000, 9_999]}
+    key2, _ = chain(U, [("%", 2), ("-", 1)])  # keys 2^64-1 and 0
+    got = run(col, [(abi.AGG_COUNT, U)], key=key2)
+    assert got == {2**64 - 1: [5000], 0: [5000]}
+
+
+def test_bitmap_predicate_and_no_rows():
+    n = 100_000
+    col = ops.splitmix_column(1, 0, n)
+    x = col.to_numpy()
+    bm = ops.compare("<", col, 2**62)
+    p = abi.fq_pred()
+    p.kind = abi.PRED_BITMAP
+    p.bitmap = bm.ptr
+    key, _ = chain(U, [("%", 7)])
+    got = run(col, [(abi.AGG_COUNT, U)], key=key, pred=p)
+    m = x < np.uint64(2**62)
+    exp = np_groupby((x % np.uint64(7))[m], [None], [abi.AGG_COUNT])
+    compare(got, exp, [abi.AGG_COUNT], [U])
+    none = predicate(U, [], ">", 2**64 - 1)
+    assert run(col, [(abi.AGG_COUNT, U)], key=key, pred=none) == {}
+
+
+def test_table_full_and_div_zero_are_reported():
+    col = ops.numbers_column(0, 100_000)
+    t = ops.GroupTable(64, [(abi.AGG_COUNT, U)])
+    t.aggregate(col)  # 100k distinct keys into 64 slots
+    with pytest.raises(ops.FQError) as ei:
+        t.count()
+    assert ei.value.status == abi.FQ_E_TABLE_FULL
+    key, _ = chain(U, [("%", 2), ("/", 7, True)])  # 7 / (number % 2): zero on even rows
+    t2 = ops.GroupTable(64, [(abi.AGG_COUNT, U)])
+    t2.aggregate(col, key=key)
+    with pytest.raises(ops.FQError) as ei:
+        t2.count()
+    assert str(ei.value) == "Internal Error: Divide by zero error"
+
+
+def test_accumulates_across_blocks():
+    # two device blocks into one table == one block over both
+    a = ops.numbers_column(0, 600_000)
+    b = ops.numbers_column(600_000, 400_001)
+    key, _ = chain(U, [("%", 97)])
+    aggs = [(abi.AGG_SUM, U), (abi.AGG_COUNT, U), (abi.AGG_MIN, U)]
+    t = ops.GroupTable(256, aggs)
+    t.aggregate(a, key=key)
+    t.aggregate(b, key=key)
+    keys, sts = t.extract()
+    got = {int(k): [int(s[i]) for s in sts] for i, k in enumerate(keys)}
+    x = np.arange(1_000_001, dtype=np.uint64)
+    exp = np_groupby(x % np.uint64(97), [x, None, x], [abi.AGG_SUM, abi.AGG_COUNT, abi.AGG_MIN])
+    compare(got, exp, [abi.AGG_SUM, abi.AGG_COUNT, abi.AGG_MIN], [U, U, U])

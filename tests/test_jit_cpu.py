@@ -91,3 +91,29 @@ def test_errors():
     c = abi.fq_col(None, 10, abi.DT_UTF8, 0)
     out = C.c_int32(0)
     assert lib.fq_jit_prepare(C.byref(c), 0, None, None, 0, C.byref(out)) != 0
+
+
+GROUP_SHAPES = [
+    ("mod_key_all", U64, [("%", 1000)], [(abi.AGG_COUNT, U64, None), (abi.AGG_SUM, U64, None),
+                                         (abi.AGG_MAX, U64, [("+", 1)]), (abi.AGG_MIN, F64, [("*", 1.5)]),
+                                         (abi.AGG_SUM, F64, [("/", 3.0)]), (abi.AGG_MAX, F64, [("*", 0.5)])], U64),
+    ("signed", U64, [("-", (5, "Int64"))], [(abi.AGG_MIN, I64, [("-", (7, "Int64"))]),
+                                           (abi.AGG_MAX, I64, [("-", (7, "Int64"))]),
+                                           (abi.AGG_SUM, I64, [("-", (7, "Int64"))])], I64),
+    ("identity_key", U64, [], [(abi.AGG_COUNT, U64, None)], U64),
+    ("eight_aggs", U64, [("/", 7)], [(abi.AGG_COUNT, U64, None)] * 8, U64),
+    ("f64_column", F64, None, [(abi.AGG_SUM, F64, None)], None),
+]
+
+
+@pytest.mark.parametrize("name,dt,key_steps,aggs,kdt", GROUP_SHAPES, ids=[g[0] for g in GROUP_SHAPES])
+def test_groupby_shapes_compile(name, dt, key_steps, aggs, kdt):
+    key = chain(dt, key_steps)[0] if key_steps else None
+    values = [chain(dt, st)[0] if st else None for _, _, st in aggs]
+    spec = [(k, d) for k, d, _ in aggs]
+    if kdt is None:  # a Float64 key is outside the device path
+        with pytest.raises(ops.FQError):
+            ops.group_compile_check(dt, spec, key=key, values=values, key_dtype=F64)
+        return
+    pred = predicate(dt, [("%", 8)], "<", 3) if dt == U64 else None
+    ops.group_compile_check(dt, spec, key=key, values=values, pred=pred, key_dtype=kdt)

@@ -142,6 +142,42 @@ def main():
     rec("aggregate C4 shape (interpreted)", "C4 with FQ_JIT_OFF", ms, 8 * n)
     ops.jit_config(abi.JIT_AUTO, 1 << 22)
 
+    # GROUP BY (fq_group_aggregate): LDS pre-aggregation, low and high cardinality
+    key, _ = chain(abi.DT_UINT64, [("%", 1000)])
+    aggs3 = [(abi.AGG_COUNT, abi.DT_UINT64), (abi.AGG_SUM, abi.DT_UINT64), (abi.AGG_MAX, abi.DT_UINT64)]
+    gt = ops.GroupTable(1 << 12, aggs3)
+
+    def group_low():
+        check(lib.fq_group_table_init(C.byref(gt.desc), st))
+        gt.aggregate(a, key=key)
+
+    ms = timed(group_low, args.reps)
+    rec("group by number%1000: count,sum,max", "no reference (plan_parser.rs:284-308)", ms, 8 * n,
+        "includes the table init")
+    assert gt.count() == 1000
+    key8, _ = chain(abi.DT_UINT64, [("%", 8)])
+    pred = predicate(abi.DT_UINT64, [("%", 8)], "<", 3)
+    v1, _ = chain(abi.DT_UINT64, [("+", 1)])
+    gt8 = ops.GroupTable(64, [(abi.AGG_MAX, abi.DT_UINT64), (abi.AGG_COUNT, abi.DT_UINT64)])
+
+    def group_c4():
+        check(lib.fq_group_table_init(C.byref(gt8.desc), st))
+        gt8.aggregate(a, pred=pred, key=key8, values=[v1, None])
+
+    ms = timed(group_c4, args.reps)
+    rec("group by number%8 WHERE %8<3: max(+1),count", "C4 shape grouped", ms, 8 * n, "includes the table init")
+    hn = min(n, 1 << 27)
+    hc = ops.DeviceColumn(b.buf, hn, abi.DT_UINT64)
+    gth = ops.GroupTable(1 << 28, [(abi.AGG_COUNT, abi.DT_UINT64)])
+
+    def group_high():
+        check(lib.fq_group_table_init(C.byref(gth.desc), st))
+        gth.aggregate(hc)
+
+    ms = timed(group_high, max(3, args.reps // 3))
+    rec("group by x (distinct, %d rows): count" % hn, "high cardinality: HBM table, 2^28 slots", ms, 8 * hn,
+        "includes the table init (4 GB)")
+
     print(json.dumps({"rows": n, "peak_gbps": PEAK, "device": torch.cuda.get_device_name(0),
                       "kernels": res}, indent=1))
 
