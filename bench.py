@@ -277,6 +277,8 @@ def main():
                 "bytes_per_launch": bytes_per_launch,
             },
             "result": res,
+            "host_ms_per_step": {"plan": st["plan_ms"] / args.steps, "first_launch": st["first_launch_ms"] / args.steps,
+                                 "exec": st["exec_ms"] / args.steps},
             "jit": {"specialised_launches": jitted, "kernels_compiled": jit1["kernels_compiled"],
                     "compile_ms": jit1["compile_ms"], "mode": jit1["mode"]},
         }

@@ -160,13 +160,25 @@ fq_status fq_engine_execute(fq_engine *e, const char *sql, fq_result **out) {
             r->cols[0].push_back(fq::DataValue::string(p.display()));
             r->rows = 2;
         } else {
-            fq::Pipeline p = fq::build_pipeline(plan, qctx);
-            const int64_t t1 = fq::now_ns();
-            e->rt->stats.plan_ns += (uint64_t)(t1 - t0);
-            fq::StreamRef s = p.execute();
-            fq::DataBlock b;
-            while (s->next(b)) append_block(r.get(), b, ctx);
-            e->rt->stats.exec_ns += (uint64_t)(fq::now_ns() - t1);
+            for (int attempt = 0;; ++attempt) {
+                fq::Pipeline p = fq::build_pipeline(plan, qctx);
+                const int64_t t1 = fq::now_ns();
+                e->rt->stats.plan_ns += (uint64_t)(t1 - t0);
+                try {
+                    fq::StreamRef s = p.execute();
+                    fq::DataBlock b;
+                    while (s->next(b)) append_block(r.get(), b, ctx);
+                } catch (const fq::FQException &ex) {
+                    // a GROUP BY table ran out of slots: re-run with 16x the slots
+                    const int64_t cap = e->rt->group_capacity.load();
+                    if (ex.status != FQ_E_TABLE_FULL || attempt >= 4 || cap >= ((int64_t)1 << 30)) throw;
+                    e->rt->group_capacity.store(cap * 16);
+                    r = std::make_unique<fq_result>();
+                    continue;
+                }
+                e->rt->stats.exec_ns += (uint64_t)(fq::now_ns() - t1);
+                break;
+            }
             if (r->names.empty())
                 for (const auto &f : plan.nodes.back().schema->fields) {
                     r->names.push_back(f.name);
@@ -208,13 +220,24 @@ fq_status fq_engine_execute_partial(fq_engine *e, const char *sql, int32_t rank,
             throw fq::FQException(FQ_E_UNSUPPORTED, "distributed execution covers aggregate queries only");
         fq::QueryPlan partial = plan;
         while (!partial.nodes.empty() && partial.nodes.back().kind == fq::PlanNode::kLimit) partial.nodes.pop_back();
-        fq::Pipeline p = fq::build_pipeline(partial, qctx, /*emit_states=*/true);
-        fq::StreamRef s = p.execute();
-        fq::DataBlock b;
         std::vector<std::vector<fq::DataValue>> per_func;
-        while (s->next(b)) {
-            const auto &rows = *b.columns.at(0).host;
-            for (const auto &v : rows) per_func.push_back(v.fields);
+        for (int attempt = 0;; ++attempt) {
+            per_func.clear();
+            try {
+                fq::Pipeline p = fq::build_pipeline(partial, qctx, /*emit_states=*/true);
+                fq::StreamRef s = p.execute();
+                fq::DataBlock b;
+                while (s->next(b)) {
+                    const auto &rows = *b.columns.at(0).host;
+                    for (const auto &v : rows) per_func.push_back(v.fields);
+                }
+            } catch (const fq::FQException &ex) {  // GROUP BY table full: 16x the slots
+                const int64_t cap = e->rt->group_capacity.load();
+                if (ex.status != FQ_E_TABLE_FULL || attempt >= 4 || cap >= ((int64_t)1 << 30)) throw;
+                e->rt->group_capacity.store(cap * 16);
+                continue;
+            }
+            break;
         }
         const std::vector<uint8_t> enc = fq::encode_states(per_func);
         *len = enc.size();
@@ -248,9 +271,12 @@ fq_status fq_engine_execute_final(fq_engine *e, const char *sql, const void *sta
         }
         fq::Pipeline p;
         p.add_source(std::make_shared<fq::BlocksProcessor>(blocks));
-        p.add_simple_transform([&]() {
+        p.add_simple_transform([&]() -> fq::ProcessorRef {
             std::vector<fq::FunctionRef> fs;
             for (const auto &x : agg->exprs) fs.push_back(x.to_function(qctx->factory));
+            if (!agg->groups.empty())  // merge exchanged groups by key on the host
+                return std::make_shared<fq::GroupByFinalTransform>(agg->schema, fs,
+                                                                   std::make_shared<fq::GroupByShared>(), false);
             return std::make_shared<fq::AggregateFinalTransform>(agg->schema, fs);
         });
         for (const auto &n : plan.nodes)

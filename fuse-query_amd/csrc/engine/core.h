@@ -185,6 +185,9 @@ class Runtime {
     void set_streams(int n);
     EngineStats stats;
     std::atomic<bool> profile{false};
+    // GROUP BY table slots for the next query (grows x16 when a query fills
+    // its table; the query is then re-run)
+    std::atomic<int64_t> group_capacity{4096};
     ThreadPool pool;
 
    private:

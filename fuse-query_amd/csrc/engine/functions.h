@@ -32,6 +32,7 @@ struct FusedPred {
 };
 
 class Function;
+class AggregatorFunction;
 using FunctionRef = std::shared_ptr<Function>;
 
 class Function {
@@ -53,6 +54,9 @@ class Function {
     virtual bool to_pred(const DataSchema &, FusedPred &) const { return false; }
     virtual const DataValue *as_constant() const { return nullptr; }
     virtual const std::string *as_field() const { return nullptr; }
+    // the AggregatorFunction leaves of this tree, left to right (GROUP BY
+    // evaluates the tree per group from device states)
+    virtual void collect_aggregators(std::vector<AggregatorFunction *> &) {}
 };
 
 // FieldFunction (function_field.rs:13-73)
@@ -113,6 +117,7 @@ class AliasFunction : public Function {
     FunctionRef clone() const override { return std::make_shared<AliasFunction>(alias_, func_->clone()); }
     bool to_chain(const DataSchema &s, FusedChain &c) const override { return func_->to_chain(s, c); }
     bool to_pred(const DataSchema &s, FusedPred &p) const override { return func_->to_pred(s, p); }
+    void collect_aggregators(std::vector<AggregatorFunction *> &v) override { func_->collect_aggregators(v); }
 
    private:
     size_t depth_ = 0;
@@ -149,6 +154,10 @@ class ArithmeticFunction : public Function {
         return f;
     }
     bool to_chain(const DataSchema &s, FusedChain &c) const override;
+    void collect_aggregators(std::vector<AggregatorFunction *> &v) override {
+        left_->collect_aggregators(v);
+        right_->collect_aggregators(v);
+    }
 
    private:
     size_t depth_ = 0;
@@ -178,6 +187,10 @@ class ComparisonFunction : public Function {
         return f;
     }
     bool to_pred(const DataSchema &s, FusedPred &p) const override;
+    void collect_aggregators(std::vector<AggregatorFunction *> &v) override {
+        left_->collect_aggregators(v);
+        right_->collect_aggregators(v);
+    }
 
    private:
     size_t depth_ = 0;
@@ -207,6 +220,9 @@ class AggregatorFunction : public Function {
 
     uint32_t op() const { return op_; }
     const Function &arg() const { return *arg_; }
+    void collect_aggregators(std::vector<AggregatorFunction *> &v) override { v.push_back(this); }
+    // GROUP BY: this group's state, as accumulate would have left it
+    void set_state(const DataValue &v) { state_ = v; }
     // Replays the reference's per-block accumulate over a run of `st.blocks`
     // reference blocks summarised by one device scan (see fq_agg_state).
     void accumulate_summary(const fq_agg_state &st);

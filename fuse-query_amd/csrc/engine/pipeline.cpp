@@ -4,6 +4,7 @@
 #include <string.h>
 
 #include <exception>
+#include <map>
 
 namespace fq {
 
@@ -369,6 +370,237 @@ StreamRef AggregateFinalTransform::execute() {
             if (v.kind == DataValue::kStruct) throw_internal("DataValue to array cannot be NONE " + v.debug());
             out.columns.push_back(Column::host_values(v.kind == DataValue::kNull ? FQ_DT_NULL : v.dtype, {v}));
         }
+    }
+    return std::make_unique<DataBlockStream>(std::vector<DataBlock>{out});
+}
+
+// ---------------------------------------------------------------------------
+// GROUP BY
+// ---------------------------------------------------------------------------
+namespace {
+
+std::vector<AggregatorFunction *> leaves_of(const std::vector<FunctionRef> &funcs) {
+    std::vector<AggregatorFunction *> v;
+    for (auto &f : funcs) f->collect_aggregators(v);
+    return v;
+}
+
+// one leaf's state from its 64-bit device word
+DataValue leaf_value(uint32_t op, DataType dt, uint64_t bits) {
+    return DataValue::some(op == FQ_AGG_COUNT ? FQ_DT_UINT64 : dt, bits);
+}
+
+// the atomics' fold, on host values of one leaf (exchange merge)
+DataValue fold_leaf(uint32_t op, const DataValue &a, const DataValue &b) {
+    if (a.kind != DataValue::kSome) return b;
+    if (b.kind != DataValue::kSome) return a;
+    const DataType dt = a.dtype;
+    if (op == FQ_AGG_COUNT || op == FQ_AGG_SUM) {
+        if (dt == FQ_DT_FLOAT64) {
+            const double r = __builtin_bit_cast(double, a.bits) + __builtin_bit_cast(double, b.bits);
+            return DataValue::some(dt, __builtin_bit_cast(uint64_t, r));
+        }
+        return DataValue::some(dt, a.bits + b.bits);
+    }
+    bool b_better;
+    if (dt == FQ_DT_FLOAT64) {
+        const double x = __builtin_bit_cast(double, a.bits), y = __builtin_bit_cast(double, b.bits);
+        b_better = op == FQ_AGG_MAX ? y > x : y < x;
+    } else if (dt == FQ_DT_INT64) {
+        const int64_t x = (int64_t)a.bits, y = (int64_t)b.bits;
+        b_better = op == FQ_AGG_MAX ? y > x : y < x;
+    } else {
+        b_better = op == FQ_AGG_MAX ? b.bits > a.bits : b.bits < a.bits;
+    }
+    return b_better ? b : a;
+}
+
+}  // namespace
+
+StreamRef GroupByPartialTransform::execute() {
+    ExecCtx &ctx = ExecCtx::current();
+    std::vector<FunctionRef> funcs;
+    for (auto &f : funcs_) funcs.push_back(f->clone());
+    const std::vector<AggregatorFunction *> leaves = leaves_of(funcs);
+    if (leaves.size() > FQ_MAX_GROUP_AGGS)
+        throw_status(FQ_E_UNSUPPORTED, "GROUP BY supports at most " + std::to_string(FQ_MAX_GROUP_AGGS) +
+                                           " aggregate functions on the device path");
+    StreamRef in = input_->execute();
+    DataBlock b;
+    bool launched = false;
+    while (in->next(b)) {
+        const DataSchema &s = *b.schema;
+        FusedChain kc;
+        if (!key_->to_chain(s, kc))
+            throw_status(FQ_E_UNSUPPORTED, "GROUP BY key " + key_->display() +
+                                               " must be an arithmetic expression over one column on the device path");
+        if (kc.out_dtype != FQ_DT_UINT64 && kc.out_dtype != FQ_DT_INT64)
+            throw_status(FQ_E_UNSUPPORTED, std::string("GROUP BY key must be UInt64 or Int64, not ") +
+                                               dtype_name(kc.out_dtype));
+        std::vector<FusedChain> args(leaves.size());
+        for (size_t i = 0; i < leaves.size(); ++i) {
+            if (leaves[i]->op() == FQ_AGG_COUNT) {
+                args[i].column = kc.column;
+                args[i].out_dtype = FQ_DT_UINT64;
+                continue;
+            }
+            if (!leaves[i]->arg().to_chain(s, args[i]) || args[i].column != kc.column)
+                throw_status(FQ_E_UNSUPPORTED, "GROUP BY aggregate " + leaves[i]->display() +
+                                                   " must be over the key's column on the device path");
+            const DataType dt = args[i].out_dtype;
+            if (dt != FQ_DT_UINT64 && dt != FQ_DT_INT64 && dt != FQ_DT_FLOAT64)
+                throw_status(FQ_E_UNSUPPORTED, std::string("GROUP BY state type ") + dtype_name(dt) +
+                                                   " is not supported on the device path");
+        }
+        // the pending filter: fused when it is a predicate over the same column
+        FusedPred fp;
+        bool has_pred = false;
+        if (b.filter) {
+            if (b.filter->to_pred(s, fp) && fp.column == kc.column) has_pred = true;
+            else b = materialize(b, ctx);
+        }
+        const Column &col = b.column_by_name(kc.column);
+        if (col.len == 0) continue;
+        fq_col c = col.abi();
+        {
+            std::lock_guard<std::mutex> lk(shared_->mu);
+            if (!shared_->ready) {
+                fq_group_table &d = shared_->desc;
+                d = fq_group_table{};
+                d.capacity = ctx.rt->group_capacity.load();
+                d.key_dtype = kc.out_dtype;
+                d.n_aggs = (int32_t)leaves.size();
+                shared_->leaf_ops.clear();
+                for (size_t i = 0; i < leaves.size(); ++i) {
+                    d.kinds[i] = (int32_t)leaves[i]->op();
+                    d.dtypes[i] = args[i].out_dtype;
+                    shared_->leaf_ops.push_back(leaves[i]->op());
+                }
+                if (leaves.empty()) {  // keys only (SELECT k ... GROUP BY k)
+                    d.n_aggs = 1;
+                    d.kinds[0] = FQ_AGG_COUNT;
+                    d.dtypes[0] = FQ_DT_UINT64;
+                    shared_->dummy_count = true;
+                }
+                shared_->mem = DeviceBuffer::alloc(fq_group_table_bytes(d.capacity, d.n_aggs), ctx.stream());
+                d.d_mem = shared_->mem->ptr;
+                {
+                    std::lock_guard<std::mutex> lk2(*ctx.res->launch_mu);
+                    check_fq(fq_group_table_init(&d, ctx.stream()));
+                }
+                ctx.sync();  // other pipes may use other queues
+                shared_->ready = true;
+            }
+        }
+        fq_expr vals[FQ_MAX_GROUP_AGGS];
+        for (size_t i = 0; i < leaves.size(); ++i) vals[i] = args[i].expr;
+        {
+            std::lock_guard<std::mutex> lk(*ctx.res->launch_mu);
+            check_fq(fq_group_aggregate(&shared_->desc, &c, has_pred ? &fp.pred : nullptr,
+                                        kc.expr.n_steps ? &kc.expr : nullptr, vals, ctx.stream()));
+        }
+        launched = true;
+        ctx.rt->stats.scan_launches++;
+        ctx.rt->stats.scan_rows += (uint64_t)c.len;
+        ctx.rt->stats.scan_bytes += (uint64_t)c.len * 8u;
+        if (const int64_t q0 = ctx.rt->stats.query_t0.exchange(0))
+            ctx.rt->stats.first_launch_ns += (uint64_t)(now_ns() - q0);
+    }
+    if (launched) ctx.sync();  // the final transform reads the table from another pipe
+    return std::make_unique<DataBlockStream>(std::vector<DataBlock>{});
+}
+
+StreamRef GroupByFinalTransform::execute() {
+    ExecCtx &ctx = ExecCtx::current();
+    std::vector<FunctionRef> funcs;
+    for (auto &f : funcs_) funcs.push_back(f->clone());
+    const std::vector<AggregatorFunction *> leaves = leaves_of(funcs);
+    StreamRef in = input_->execute();
+    // groups: key -> leaf states; exchanged partial rows arrive as Struct
+    // rows [key, leaf states...] (fq_engine_execute_final)
+    std::map<std::pair<int, uint64_t>, std::vector<DataValue>> host_groups;  // ordered by key
+    DataType kdt = FQ_DT_NULL;
+    auto order_key = [&kdt](uint64_t k) {
+        // (sign bucket, bits) orders Int64 keys numerically and UInt64 keys as unsigned
+        if (kdt == FQ_DT_INT64) return std::make_pair((int64_t)k < 0 ? 0 : 1, k);
+        return std::make_pair(1, k);
+    };
+    DataBlock b;
+    std::vector<std::vector<DataValue>> exchanged;
+    while (in->next(b)) {
+        if (b.columns.empty() || !b.columns[0].host) continue;
+        for (const auto &row : *b.columns[0].host)
+            if (row.kind == DataValue::kStruct && !row.fields.empty()) exchanged.push_back(row.fields);
+    }
+    if (shared_->ready) {
+        const fq_group_table &d = shared_->desc;
+        kdt = d.key_dtype;
+        int64_t groups = 0;
+        check_fq(fq_group_table_count(&d, &groups, ctx.stream()));
+        const int64_t n = groups > 0 ? groups : 1;
+        auto keys = DeviceBuffer::alloc((size_t)n * 8, ctx.stream());
+        std::vector<std::shared_ptr<DeviceBuffer>> st;
+        uint64_t *ptrs[FQ_MAX_GROUP_AGGS] = {};
+        for (int a = 0; a < d.n_aggs; ++a) {
+            st.push_back(DeviceBuffer::alloc((size_t)n * 8, ctx.stream()));
+            ptrs[a] = (uint64_t *)st.back()->ptr;
+        }
+        int64_t got = 0;
+        check_fq(fq_group_table_extract(&d, (uint64_t *)keys->ptr, ptrs, n, &got, ctx.stream()));
+        std::vector<uint64_t> hk((size_t)got);
+        std::vector<std::vector<uint64_t>> hs((size_t)d.n_aggs, std::vector<uint64_t>((size_t)got));
+        if (got > 0) {
+            check_hip(hipMemcpyAsync(hk.data(), keys->ptr, (size_t)got * 8, hipMemcpyDeviceToHost, ctx.stream()),
+                      "hipMemcpyAsync");
+            for (int a = 0; a < d.n_aggs; ++a)
+                check_hip(hipMemcpyAsync(hs[(size_t)a].data(), st[(size_t)a]->ptr, (size_t)got * 8,
+                                         hipMemcpyDeviceToHost, ctx.stream()),
+                          "hipMemcpyAsync");
+            ctx.sync();
+        }
+        for (int64_t g = 0; g < got; ++g) {
+            std::vector<DataValue> row;
+            row.push_back(DataValue::some(kdt, hk[(size_t)g]));
+            for (size_t a = 0; a < leaves.size(); ++a)
+                row.push_back(leaf_value(leaves[a]->op(), (DataType)d.dtypes[a], hs[a][(size_t)g]));
+            exchanged.push_back(std::move(row));
+        }
+    }
+    for (auto &row : exchanged) {
+        if (row.size() != 1 + leaves.size()) throw_status(FQ_E_INVALID, "GROUP BY: malformed partial state row");
+        if (kdt == FQ_DT_NULL) kdt = row[0].dtype;
+        auto ok = order_key(row[0].bits);
+        auto it = host_groups.find(ok);
+        if (it == host_groups.end()) {
+            host_groups.emplace(ok, std::move(row));
+            continue;
+        }
+        for (size_t a = 0; a < leaves.size(); ++a) it->second[a + 1] = fold_leaf(leaves[a]->op(), it->second[a + 1], row[a + 1]);
+    }
+    DataBlock out;
+    out.schema = schema_;
+    if (emit_states_) {
+        std::vector<DataValue> rows;
+        for (auto &kv : host_groups) rows.push_back(DataValue::make_struct(kv.second));
+        out.columns.push_back(Column::host_values(FQ_DT_NULL, std::move(rows)));
+        return std::make_unique<DataBlockStream>(std::vector<DataBlock>{out});
+    }
+    // key column, then each aggregate expression evaluated from its leaves
+    std::vector<std::vector<DataValue>> cols(1 + funcs.size());
+    for (auto &kv : host_groups) {
+        const std::vector<DataValue> &row = kv.second;
+        cols[0].push_back(row[0]);
+        for (size_t a = 0; a < leaves.size(); ++a) leaves[a]->set_state(row[a + 1]);
+        for (size_t f = 0; f < funcs.size(); ++f) {
+            const DataValue v = funcs[f]->merge_result();
+            if (v.kind == DataValue::kNone) throw_internal("DataValue to array cannot be NONE NULL");
+            cols[f + 1].push_back(v);
+        }
+    }
+    for (size_t c = 0; c < cols.size(); ++c) {
+        DataType dt = c < schema_->fields.size() ? schema_->fields[c].dtype : FQ_DT_NULL;
+        if (!cols[c].empty() && cols[c][0].kind == DataValue::kSome) dt = cols[c][0].dtype;
+        out.columns.push_back(Column::host_values(dt, std::move(cols[c])));
     }
     return std::make_unique<DataBlockStream>(std::vector<DataBlock>{out});
 }

@@ -230,6 +230,57 @@ class AggregateFinalTransform : public IProcessor {  // transform_aggregate_fina
     bool emit_states_;
 };
 
+// GROUP BY.  The reference plans group_expr but has no
+// transform for it (pipeline_builder.rs:50-66 builds AggregatePartial/Final
+// from aggr_expr only).  Here every pipe streams its blocks into ONE device
+// hash table per query (fq_group_aggregate: key = the group expression's
+// fused chain, one state per AggregatorFunction leaf of the aggregate
+// expressions), and the final transform extracts the groups, sorts them by
+// key and evaluates each aggregate expression per group from its leaves'
+// states (merge_result over the Function tree).
+struct GroupByShared {
+    std::mutex mu;
+    bool ready = false;
+    fq_group_table desc{};
+    std::shared_ptr<DeviceBuffer> mem;
+    std::vector<uint32_t> leaf_ops;  // per table aggregate
+    bool dummy_count = false;        // no aggregate: a Count keeps the table valid
+};
+
+class GroupByPartialTransform : public IProcessor {
+   public:
+    GroupByPartialTransform(FunctionRef key, std::vector<FunctionRef> funcs, std::shared_ptr<GroupByShared> shared)
+        : key_(std::move(key)), funcs_(std::move(funcs)), shared_(std::move(shared)),
+          input_(std::make_shared<EmptyProcessor>()) {}
+    std::string name() const override { return "GroupByPartialTransform"; }
+    void connect_to(ProcessorRef input) override { input_ = std::move(input); }
+    StreamRef execute() override;
+
+   private:
+    FunctionRef key_;
+    std::vector<FunctionRef> funcs_;
+    std::shared_ptr<GroupByShared> shared_;
+    ProcessorRef input_;
+};
+
+class GroupByFinalTransform : public IProcessor {
+   public:
+    GroupByFinalTransform(SchemaRef schema, std::vector<FunctionRef> funcs, std::shared_ptr<GroupByShared> shared,
+                          bool emit_states)
+        : schema_(std::move(schema)), funcs_(std::move(funcs)), shared_(std::move(shared)),
+          input_(std::make_shared<EmptyProcessor>()), emit_states_(emit_states) {}
+    std::string name() const override { return "GroupByFinalTransform"; }
+    void connect_to(ProcessorRef input) override { input_ = std::move(input); }
+    StreamRef execute() override;
+
+   private:
+    SchemaRef schema_;
+    std::vector<FunctionRef> funcs_;
+    std::shared_ptr<GroupByShared> shared_;
+    ProcessorRef input_;
+    bool emit_states_;
+};
+
 class LimitTransform : public IProcessor {  // transform_limit.rs:12-43
    public:
     explicit LimitTransform(size_t n) : limit_(n), input_(std::make_shared<EmptyProcessor>()) {}

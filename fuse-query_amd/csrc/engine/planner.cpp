@@ -202,6 +202,7 @@ struct SelectAst {
     bool has_where = false;
     ExpressionPlan where;
     bool has_group = false, has_having = false;
+    std::vector<ExpressionPlan> group;
     bool has_limit = false;
     ExpressionPlan limit;
 };
@@ -248,7 +249,7 @@ class Parser {
             ++p_;
             a.has_group = true;
             for (;;) {
-                (void)expr(0);
+                a.group.push_back(expr(0));
                 if (!sym(",")) break;
             }
         }
@@ -485,17 +486,21 @@ QueryPlan build_from_sql(const std::string &sql, const QueryContext &ctx) {
     std::vector<ExpressionPlan> aggr;
     for (const auto &e : a.items)
         if (e.is_aggregate()) aggr.push_back(e);
-    if (a.has_group)
-        throw_status(FQ_E_UNSUPPORTED, "GROUP BY is outside the device hot path (no transform implements it in the reference)");
     PlanNode pn;
-    pn.exprs = aggr.empty() ? items : aggr;
-    if (!aggr.empty()) {
-        if (aggr.size() != a.items.size()) throw_plan("Projection references non-aggregate values");
+    pn.exprs = aggr.empty() && !a.has_group ? items : aggr;
+    if (!aggr.empty() || a.has_group) {
+        // PlanParser::aggregate (plan_parser.rs:284-308): group + aggregate
+        // expressions must account for the whole projection
+        if (a.group.size() + aggr.size() != items.size()) throw_plan("Projection references non-aggregate values");
         pn.kind = PlanNode::kAggregate;
+        pn.groups = a.group;
     } else {
         pn.kind = PlanNode::kProjection;
     }
-    pn.schema = fields_schema(pn.exprs, *input, ctx.factory);
+    // PlanBuilder::aggregate (plan_builder.rs:63-83): schema = group ++ aggr
+    std::vector<ExpressionPlan> out_exprs = pn.groups;
+    out_exprs.insert(out_exprs.end(), pn.exprs.begin(), pn.exprs.end());
+    pn.schema = fields_schema(out_exprs, *input, ctx.factory);
     qp.nodes.push_back(pn);
     // limit
     if (a.has_limit) {
@@ -528,6 +533,12 @@ std::string QueryPlan::display() const {
                 for (size_t i = 0; i < n.exprs.size(); ++i) {
                     if (i) out += ", ";
                     out += n.exprs[i].debug();
+                }
+                // plan_display.rs:43-49 writes the group list straight after
+                // the aggregate list (no separator between the two)
+                for (size_t i = 0; i < n.groups.size(); ++i) {
+                    if (i) out += ", ";
+                    out += n.groups[i].debug();
                 }
                 break;
             }
@@ -568,6 +579,25 @@ Pipeline build_pipeline(const QueryPlan &plan, const QueryContextRef &ctx, bool 
                 break;
             }
             case PlanNode::kAggregate: {
+                if (!n.groups.empty()) {  // GROUP BY (no reference transform; fq_group_*)
+                    if (n.groups.size() != 1)
+                        throw_status(FQ_E_UNSUPPORTED, "GROUP BY supports one key expression on the device path");
+                    auto shared = std::make_shared<GroupByShared>();
+                    auto funcs = [&]() {
+                        std::vector<FunctionRef> fs;
+                        for (const auto &e : n.exprs) fs.push_back(e.to_function(ctx->factory));
+                        return fs;
+                    };
+                    const ExpressionPlan key = n.groups[0];
+                    p.add_simple_transform([&, shared, key]() {
+                        return std::make_shared<GroupByPartialTransform>(key.to_function(ctx->factory), funcs(), shared);
+                    });
+                    p.merge_processor();
+                    p.add_simple_transform([&, shared]() {
+                        return std::make_shared<GroupByFinalTransform>(n.schema, funcs(), shared, emit_states);
+                    });
+                    break;
+                }
                 auto funcs = [&]() {
                     std::vector<FunctionRef> fs;
                     for (const auto &e : n.exprs) fs.push_back(e.to_function(ctx->factory));

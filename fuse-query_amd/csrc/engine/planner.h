@@ -4,7 +4,7 @@
 //   PlanBuilder                                src/planners/plan_builder.rs
 //   PipelineBuilder::build                     src/processors/pipeline_builder.rs:26-106
 // Grammar: [EXPLAIN] SELECT item[, ...] FROM [db.]table[(args)] [WHERE expr]
-//          [LIMIT n]; operators + - * / % = < <= > >= with sqlparser 0.6
+//          [GROUP BY expr] [LIMIT n]; operators + - * / % = < <= > >= with sqlparser 0.6
 //          precedence, function calls, parentheses, AS aliases.
 #pragma once
 
@@ -36,6 +36,7 @@ struct PlanNode {
     ReadDataSourcePlan read;
     ExpressionPlan predicate;
     std::vector<ExpressionPlan> exprs;  // projection / aggr exprs
+    std::vector<ExpressionPlan> groups;  // GROUP BY exprs (kAggregate)
     SchemaRef schema;
     size_t limit = 0;
 };

@@ -10,9 +10,11 @@
 //                               u32 sentinel-used, u64 scratch counter
 //   keys[capacity + 1]          0xFFFF...FF = empty; slot `capacity` holds the
 //                               key 0xFFFF...FF itself when it occurs
-//   states[a][capacity + 1]     per aggregate a, initialised to the identity
-//                               of its kind (0, +max, lowest) so atomics need
-//                               no occupancy check
+//   states[a][r][capacity + 1]  per aggregate a and replica r < R (see
+//                               group_replicas: workgroup b updates replica
+//                               b % R), initialised to the identity of its
+//                               kind (0, +max, lowest) so atomics need no
+//                               occupancy check; extract folds the replicas
 // The accumulate kernel is generated per shape with hipRTC (fq_jit.hip
 // gen_groupby_source); init / count / extract are precompiled here.
 #include <hip/hip_runtime.h>
@@ -33,8 +35,9 @@ struct TableView {
     uint32_t *hdr;
     uint64_t *counter;
     uint64_t *keys;
-    uint64_t *states[FQ_MAX_GROUP_AGGS];
+    uint64_t *states[FQ_MAX_GROUP_AGGS];  // replica 0; replica r at + r * (cap + 1)
     int64_t cap;
+    int replicas;
 };
 
 static uint64_t identity_bits(int32_t kind, int32_t dt) {
@@ -64,8 +67,9 @@ static fq_status view(const fq_group_table *t, TableView &v) {
     v.counter = (uint64_t *)(m + 8);
     v.keys = (uint64_t *)(m + kHdrBytes);
     v.cap = t->capacity;
+    v.replicas = group_replicas(t->capacity);
     for (int a = 0; a < FQ_MAX_GROUP_AGGS; ++a)
-        v.states[a] = a < t->n_aggs ? v.keys + (size_t)(a + 1) * (size_t)(t->capacity + 1) : nullptr;
+        v.states[a] = a < t->n_aggs ? v.keys + (size_t)(1 + a * v.replicas) * (size_t)(t->capacity + 1) : nullptr;
     return FQ_OK;
 }
 
@@ -74,15 +78,36 @@ struct InitArgs {
     uint64_t *states[FQ_MAX_GROUP_AGGS];
     uint64_t ident[FQ_MAX_GROUP_AGGS];
     int32_t n_aggs;
-    int64_t slots;
+    int64_t slots;     // capacity + 1
+    int32_t replicas;
 };
 
 __global__ void __launch_bounds__(256) group_init_kernel(InitArgs a) {
     const int64_t T = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.slots; i += T) {
-        a.keys[i] = kEmpty;
+    const int64_t all = a.slots * a.replicas;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < all; i += T) {
+        if (i < a.slots) a.keys[i] = kEmpty;
         for (int s = 0; s < a.n_aggs; ++s) a.states[s][i] = a.ident[s];
     }
+}
+
+// fold of two states of one aggregate (the atomics' operation)
+__device__ __forceinline__ uint64_t fold(int32_t kind, int32_t dt, uint64_t x, uint64_t y) {
+    if (kind == FQ_AGG_COUNT) return x + y;
+    if (dt == FQ_DT_FLOAT64) {
+        const double a = __builtin_bit_cast(double, x), b = __builtin_bit_cast(double, y);
+        if (kind == FQ_AGG_SUM) return __builtin_bit_cast(uint64_t, a + b);
+        if (kind == FQ_AGG_MAX) return b > a ? y : x;
+        return b < a ? y : x;
+    }
+    if (kind == FQ_AGG_SUM) return x + y;
+    if (dt == FQ_DT_INT64) {
+        const int64_t a = (int64_t)x, b = (int64_t)y;
+        if (kind == FQ_AGG_MAX) return b > a ? y : x;
+        return b < a ? y : x;
+    }
+    if (kind == FQ_AGG_MAX) return y > x ? y : x;
+    return y < x ? y : x;
 }
 
 // counts occupied slots into *counter (wave-aggregated atomics)
@@ -103,6 +128,9 @@ struct ExtractArgs {
     uint64_t *out_keys;
     uint64_t *out_states[FQ_MAX_GROUP_AGGS];
     int32_t n_aggs;
+    int32_t kinds[FQ_MAX_GROUP_AGGS];
+    int32_t dtypes[FQ_MAX_GROUP_AGGS];
+    int32_t replicas;
     int64_t cap;
     int64_t out_cap;
     const uint32_t *hdr;
@@ -128,7 +156,12 @@ __global__ void __launch_bounds__(256) group_extract_kernel(ExtractArgs a) {
         const uint64_t pos = first + (uint64_t)__popcll(m & ((1ull << lane) - 1ull));
         if ((int64_t)pos >= a.out_cap) continue;
         a.out_keys[pos] = i < a.cap ? a.keys[i] : kEmpty;
-        for (int s = 0; s < a.n_aggs; ++s) a.out_states[s][pos] = a.states[s][i];
+        for (int s = 0; s < a.n_aggs; ++s) {
+            uint64_t v = a.states[s][i];
+            for (int r = 1; r < a.replicas; ++r)
+                v = fold(a.kinds[s], a.dtypes[s], v, a.states[s][(int64_t)r * slots + i]);
+            a.out_states[s][pos] = v;
+        }
     }
 }
 
@@ -158,7 +191,7 @@ extern "C" {
 
 size_t fq_group_table_bytes(int64_t capacity, int32_t n_aggs) {
     if (capacity < 0 || n_aggs < 0) return 0;
-    return fqk::kHdrBytes + (size_t)(capacity + 1) * 8u * (size_t)(1 + n_aggs);
+    return fqk::kHdrBytes + (size_t)(capacity + 1) * 8u * (size_t)(1 + n_aggs * fqk::group_replicas(capacity));
 }
 
 fq_status fq_group_table_init(const fq_group_table *t, void *stream) {
@@ -172,11 +205,12 @@ fq_status fq_group_table_init(const fq_group_table *t, void *stream) {
     a.keys = v.keys;
     a.n_aggs = t->n_aggs;
     a.slots = t->capacity + 1;
+    a.replicas = v.replicas;
     for (int i = 0; i < t->n_aggs; ++i) {
         a.states[i] = v.states[i];
         a.ident[i] = identity_bits(t->kinds[i], t->dtypes[i]);
     }
-    hipLaunchKernelGGL(group_init_kernel, dim3(small_grid(a.slots)), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(group_init_kernel, dim3(small_grid(a.slots * a.replicas)), dim3(256), 0, st, a);
     FQ_HIP_TRY(hipGetLastError());
     return FQ_OK;
 }
@@ -274,7 +308,10 @@ fq_status fq_group_table_extract(const fq_group_table *t, uint64_t *d_keys, uint
         if (!d_states[i]) return fqc::fail(FQ_E_INVALID, "fq_group_table_extract: NULL state output");
         a.states[i] = v.states[i];
         a.out_states[i] = d_states[i];
+        a.kinds[i] = t->kinds[i];
+        a.dtypes[i] = t->dtypes[i];
     }
+    a.replicas = v.replicas;
     a.cap = v.cap;
     a.out_cap = cap;
     a.hdr = v.hdr;

@@ -576,7 +576,8 @@ bool gen_groupby_source(const GroupLaunch &G, int32_t tin, Gen &g, std::string &
     src += "struct Step { u64 c, m, s; };\nstruct Consts { u64 rhs; Step p[" + std::to_string(kSteps) + "], k[" +
            std::to_string(kSteps) + "], v[" + std::to_string(FQ_MAX_GROUP_AGGS) + "][" + std::to_string(kSteps) +
            "]; };\n";
-    src += "struct Tab { u64 *keys; u64 *st[" + std::to_string(FQ_MAX_GROUP_AGGS) + "]; u32 *hdr; long long mask; };\n";
+    src += "struct Tab { u64 *keys; u64 *st[" + std::to_string(FQ_MAX_GROUP_AGGS) +
+           "]; u32 *hdr; long long mask; int rmask; };\n";
     src += "#define EMPTY 0xffffffffffffffffull\n#define NA " + std::to_string(NA) + "\n#define S " +
            std::to_string(S) + "\n";
     src += R"(
@@ -668,13 +669,17 @@ __device__ long long ginsert(const Tab &t, u64 k) {
             if (cur == k) { slot = h; break; }
             if (cur == EMPTY) {
                 const u64 old = atomicCAS((unsigned long long *)&s_keys[h], EMPTY, k);
-                if (old == EMPTY || old == k) { slot = h; break; }
+                if (old == EMPTY) {
+                    // a saturated LDS table (high cardinality) stops being
+                    // probed for the rest of this workgroup
+                    if (atomicAdd(s_bypass + 1, 1) + 1 >= S * 3 / 4) *s_bypass = 1;
+                    slot = h;
+                    break;
+                }
+                if (old == k) { slot = h; break; }
             }
             h = (h + 1) & (S - 1);
         }
-        // a full neighbourhood means the LDS table is saturated (high
-        // cardinality): stop probing it for the rest of this workgroup
-        if (slot < 0) *s_bypass = 1;
     }
     if (slot >= 0) {
 )";
@@ -695,8 +700,8 @@ fq_jit_groupby(const TIn *__restrict__ col, long long n, long long head, const u
                Consts c, Tab t) {
     __shared__ u64 s_keys[S];
     __shared__ u64 s_st[NA][S];
-    __shared__ int s_bypass;
-    if (threadIdx.x == 0) s_bypass = 0;
+    __shared__ int s_bypass[2];  // [0] bypass flag, [1] slots claimed
+    if (threadIdx.x < 2) s_bypass[threadIdx.x] = 0;
     for (int i = threadIdx.x; i < S; i += 256) {
         s_keys[i] = EMPTY;
 )";
@@ -704,6 +709,10 @@ fq_jit_groupby(const TIn *__restrict__ col, long long n, long long head, const u
         src += "        s_st[" + std::to_string(a) + "][i] = " + identity(G.kinds[a], G.dtypes[a]) + ";\n";
     src += R"(    }
     __syncthreads();
+    // this workgroup's replica of the HBM states
+    Tab tr = t;
+    const long long roff = (long long)(blockIdx.x & t.rmask) * (t.mask + 2);
+    for (int a = 0; a < NA; ++a) tr.st[a] += roff;
     u32 flags = 0;
     const long long T = (long long)gridDim.x * 256;
     const long long g = (long long)blockIdx.x * 256 + threadIdx.x;
@@ -721,22 +730,22 @@ fq_jit_groupby(const TIn *__restrict__ col, long long n, long long head, const u
             TIn x[2];
             __builtin_memcpy(&x[0], &raw[k], 16);
             const long long i0 = head + (base + (long long)k * 256) * 2;
-            fq_row(x[0], i0, c, t, bitmap, s_keys, s_st, flags, &s_bypass);
-            fq_row(x[1], i0 + 1, c, t, bitmap, s_keys, s_st, flags, &s_bypass);
+            fq_row(x[0], i0, c, tr, bitmap, s_keys, s_st, flags, s_bypass);
+            fq_row(x[1], i0 + 1, c, tr, bitmap, s_keys, s_st, flags, s_bypass);
         }
     }
     for (long long v = ntiles * TV + g; v < nvec; v += T) {
         const u32x4 raw = __builtin_nontemporal_load(vp + v);
         TIn x[2];
         __builtin_memcpy(&x[0], &raw, 16);
-        fq_row(x[0], head + v * 2, c, t, bitmap, s_keys, s_st, flags, &s_bypass);
-        fq_row(x[1], head + v * 2 + 1, c, t, bitmap, s_keys, s_st, flags, &s_bypass);
+        fq_row(x[0], head + v * 2, c, tr, bitmap, s_keys, s_st, flags, s_bypass);
+        fq_row(x[1], head + v * 2 + 1, c, tr, bitmap, s_keys, s_st, flags, s_bypass);
     }
     const long long tail0 = head + nvec * 2;
     const long long nedge = head + (n - tail0);
     for (long long e = g; e < nedge; e += T) {
         const long long i = e < head ? e : tail0 + (e - head);
-        fq_row(col[i], i, c, t, bitmap, s_keys, s_st, flags, &s_bypass);
+        fq_row(col[i], i, c, tr, bitmap, s_keys, s_st, flags, s_bypass);
     }
     if (flags) atomicOr(&t.hdr[0], flags);
     __syncthreads();
@@ -744,20 +753,20 @@ fq_jit_groupby(const TIn *__restrict__ col, long long n, long long head, const u
     for (int i = threadIdx.x; i < S; i += 256) {
         const u64 k = s_keys[i];
         if (k == EMPTY) continue;
-        const long long gs = ginsert(t, k);
+        const long long gs = ginsert(tr, k);
         if (gs < 0) continue;
 )";
     for (int a = 0; a < NA; ++a) {
         const std::string sa = "s_st[" + std::to_string(a) + "][i]";
         std::string v;
         if (G.kinds[a] == FQ_AGG_COUNT) {
-            src += "        atomicAdd((unsigned long long *)&t.st[" + std::to_string(a) + "][gs], (unsigned long long)" + sa +
+            src += "        atomicAdd((unsigned long long *)&tr.st[" + std::to_string(a) + "][gs], (unsigned long long)" + sa +
                    ");\n";
             continue;
         }
         if (G.dtypes[a] == FQ_DT_FLOAT64) v = "__builtin_bit_cast(double, " + sa + ")";
         else v = "(" + std::string(ctype(G.dtypes[a])) + ")" + sa;
-        src += "        " + state_update(G.kinds[a], G.dtypes[a], "&t.st[" + std::to_string(a) + "][gs]", v) + "\n";
+        src += "        " + state_update(G.kinds[a], G.dtypes[a], "&tr.st[" + std::to_string(a) + "][gs]", v) + "\n";
     }
     src += "    }\n}\n";
     return true;
@@ -948,11 +957,13 @@ fq_status jit_groupby(int32_t col_dtype, const GroupLaunch &G) {
         uint64_t *st[FQ_MAX_GROUP_AGGS];
         uint32_t *hdr;
         long long mask;
+        int rmask;
     } tab;
     tab.keys = G.keys;
     for (int a = 0; a < FQ_MAX_GROUP_AGGS; ++a) tab.st[a] = G.states[a];
     tab.hdr = G.hdr;
     tab.mask = (long long)G.capacity - 1;
+    tab.rmask = group_replicas(G.capacity) - 1;
     const void *col = G.col;
     long long n = G.n, head = G.head;
     const uint64_t *bitmap = G.pred.bitmap;

@@ -39,6 +39,16 @@ fq_status jit_scan(int32_t col_dtype, bool chain, const Launch &L, bool *used);
 // source is compiled for gfx950 only to validate it.
 fq_status jit_prepare(int32_t col_dtype, bool chain, const Launch &L, bool *ready);
 
+// State replicas of a group table of `cap` slots: workgroup b updates replica
+// b % R, so workgroups rarely contend for one group's state words (the
+// extract folds the replicas).  R * cap <= 2^22 words per aggregate (32 MB),
+// at most 256 replicas; tables of 2^22 slots and more get one.
+inline int group_replicas(int64_t cap) {
+    int r = 1;
+    while (r < 256 && cap * (int64_t)r * 2 <= ((int64_t)1 << 22)) r *= 2;
+    return r;
+}
+
 // One fq_group_aggregate launch (fq_groupby.hip -> fq_jit.hip).
 struct GroupLaunch {
     const void *col;

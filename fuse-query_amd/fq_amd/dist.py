@@ -19,13 +19,18 @@ STATE_CAP = 4096  # bytes per rank; a query's states are 8 + 16 per value + 8 pe
 
 
 def allgather_states(states, group=None, device=None, cap=STATE_CAP):
-    """bytes of this rank -> [bytes of rank 0, ..., rank world-1] (one all-reduce)."""
+    """bytes of this rank -> [bytes of rank 0, ..., rank world-1] (one all-reduce;
+    payloads above `cap` -- GROUP BY states grow with the number of groups --
+    first agree on the largest length with a second, 8-byte-per-rank one)."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
-    if len(states) > cap:
-        raise ValueError("partial states (%d bytes) exceed the exchange cap %d" % (len(states), cap))
     if device is None:
         device = "cuda" if dist.get_backend(group) == "nccl" else "cpu"
+    if len(states) > cap or cap != STATE_CAP:
+        lens = torch.zeros(world, dtype=torch.int64, device=device)
+        lens[rank] = len(states)
+        dist.all_reduce(lens, op=dist.ReduceOp.SUM, group=group)
+        cap = max(cap, (int(lens.max().item()) + 7) // 8 * 8)
     buf = torch.zeros((world, cap // 8), dtype=torch.int64, device=device)
     row = torch.frombuffer(bytearray(states.ljust(cap, b"\0")), dtype=torch.int64)
     buf[rank].copy_(row)

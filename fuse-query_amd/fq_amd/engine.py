@@ -157,7 +157,7 @@ class Engine:
     def execute_partial(self, sql, rank, world):
         """Serialised merged partial states of this rank's shard (bytes)."""
         n = C.c_size_t(0)
-        cap = 4096
+        cap = 1 << 20
         while True:
             buf = C.create_string_buffer(cap)
             st = lib.fq_engine_execute_partial(self.h, sql.encode(), rank, world, buf, cap, C.byref(n))

@@ -826,3 +826,40 @@ def aggregate_partial_states(total, exprs, parts, where=None, modulo=True):
         for m, f in zip(merged, funcs):
             m.merge_state(f.accumulate_result())
     return [m.accumulate_result() for m in merged]
+
+
+def group_by_query(total, key_expr, exprs, where=None, modulo=True):
+    """GROUP BY -- NOT a restatement: the reference plans group_expr
+    (plan_parser.rs:284-308) but PipelineBuilder ignores it
+    (pipeline_builder.rs:50-66), so there is no reference behaviour to
+    follow.  This is the semantics the device path implements, stated with
+    the reference's own Function machinery: rows are filtered, grouped by the
+    value of key_expr, every AggregatorFunction accumulates each block's rows
+    of its group (function_aggregator.rs:57-100) and the aggregate
+    expressions are merge_result()-ed per group.  Parity unpinned.
+    Returns [(key, value...)] sorted by key."""
+    key_fn = to_function(key_expr, modulo=modulo)
+    pred = to_function(where, modulo=modulo) if where is not None else None
+    groups = {}
+    for b in numbers_stream(total):
+        if pred is not None:
+            b = filter_block(pred, b)
+        if b.num_rows() == 0:
+            continue
+        kv = key_fn.eval(b)
+        karr = kv if isinstance(kv, Arr) else to_array(kv, b.num_rows())
+        keys = np.asarray(karr.values)
+        for k in np.unique(keys):
+            sub = b.take(list(keys == k))
+            fs = groups.get(int(k))
+            if fs is None:
+                fs = groups[int(k)] = [to_function(e, modulo=modulo) for e in exprs]
+            for f in fs:
+                f.accumulate(sub)
+    out = []
+    for k in sorted(groups):
+        row = [k]
+        for f in groups[k]:
+            row.append(f.merge_result().value)
+        out.append(tuple(row))
+    return out

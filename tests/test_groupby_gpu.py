@@ -200,3 +200,67 @@ def test_accumulates_across_blocks():
     x = np.arange(1_000_001, dtype=np.uint64)
     exp = np_groupby(x % np.uint64(97), [x, None, x], [abi.AGG_SUM, abi.AGG_COUNT, abi.AGG_MIN])
     compare(got, exp, [abi.AGG_SUM, abi.AGG_COUNT, abi.AGG_MIN], [U, U, U])
+
+
+# ---- GROUP BY through the SQL pipeline (GroupByPartial x P -> Merge -> Final) ----
+import fq_ref as R  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from fq_amd.engine import Engine
+    e = Engine()
+    yield e
+    e.close()
+
+
+N = R.E_field("number")
+
+
+def _c(v):
+    return R.E_const(v)
+
+
+@pytest.mark.parametrize("total", [100_000, 1_000_000, 4_000_000])
+def test_sql_group_by_matches_oracle(eng, total):
+    sql = ("SELECT number%%3, count(number), sum(number)/count(number), max(number+1), min(number) "
+           "FROM system.numbers_mt(%d) WHERE (number%%8)<3 GROUP BY number%%3" % total)
+    r = eng.execute(sql)
+    exp = R.group_by_query(total, R.E_bin("%", N, _c(3)),
+                           [R.E_fn("count", N), R.E_bin("/", R.E_fn("sum", N), R.E_fn("count", N)),
+                            R.E_fn("max", R.E_bin("+", N, _c(1))), R.E_fn("min", N)],
+                           where=R.E_bin("<", R.E_bin("%", N, _c(8)), _c(3)))
+    assert r.rows == exp
+    assert r.names == ["number % 3", "Count(number)", "Sum(number) / Count(number)", "Max(number + 1)",
+                       "Min(number)"]
+
+
+def test_sql_group_by_f64_and_keys_only(eng):
+    r = eng.execute("SELECT number%5, sum(number*1.5) FROM system.numbers_mt(80000) GROUP BY number%5")
+    exp = R.group_by_query(80000, R.E_bin("%", N, _c(5)), [R.E_fn("sum", R.E_bin("*", N, _c(1.5)))])
+    assert [k for k, _ in r.rows] == [k for k, _ in exp]
+    for (k, got), (_, e) in zip(r.rows, exp):
+        assert abs(got - e) <= 1e-12 * abs(e)  # f64 sum: atomic add order unspecified
+    r = eng.execute("SELECT number%7 FROM system.numbers_mt(1000) GROUP BY number%7")
+    assert r.rows == [(k,) for k in range(7)]
+
+
+def test_sql_group_by_grows_a_full_table(eng):
+    # 100k distinct keys: 4096 slots -> TABLE_FULL -> re-run with 16x, twice
+    r = eng.execute("SELECT number, count(number) FROM system.numbers_mt(160000) GROUP BY number")
+    assert len(r.rows) == 160000 and r.rows[0] == (0, 1) and r.rows[-1] == (159999, 1)
+
+
+def test_sql_group_by_limit_and_explain(eng):
+    r = eng.execute("SELECT number%10, count(number) FROM system.numbers_mt(80000) GROUP BY number%10 LIMIT 3")
+    assert r.rows == [(0, 8000), (1, 8000), (2, 8000)]
+    txt = eng.explain("SELECT number%10, sum(number) FROM system.numbers_mt(80000) GROUP BY number%10")
+    # plan_display.rs:43-49 prints the group list right after the aggregates
+    assert "Aggregate: sum([number])(number % 10)" in txt or "Aggregate: sum([number])" in txt
+
+
+def test_sql_group_by_errors(eng):
+    from fq_amd import FQError  # noqa: F401
+    with pytest.raises(Exception) as ei:
+        eng.execute("SELECT number, number+1, sum(number) FROM system.numbers_mt(10) GROUP BY number%3")
+    assert "Projection references non-aggregate values" in str(ei.value)

@@ -1,0 +1,25 @@
+import sys, os, ctypes as C, statistics
+sys.path.insert(0, "fuse-query_amd")
+import torch
+from fq_amd import abi, ops
+from fq_amd._lib import check, lib
+from fq_amd.expr import chain
+U = abi.DT_UINT64
+n = int(float(sys.argv[1])) if len(sys.argv) > 1 else 1_250_000_000
+a = ops.numbers_column(0, n)
+st = ops._stream()
+def timed(fn, reps=5):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn(); torch.cuda.synchronize(); ts = []
+    for _ in range(reps):
+        e0.record(); fn(); e1.record(); e1.synchronize(); ts.append(e0.elapsed_time(e1))
+    return statistics.median(ts)
+for mod in (8, 64, 1000, 4096, 100000):
+    for naggs in (1, 3):
+        key, _ = chain(U, [("%", mod)])
+        aggs = [(abi.AGG_COUNT, U), (abi.AGG_SUM, U), (abi.AGG_MAX, U)][:naggs]
+        gt = ops.GroupTable(max(64, 4 * mod), aggs)
+        def f():
+            check(lib.fq_group_table_init(C.byref(gt.desc), st)); gt.aggregate(a, key=key)
+        ms = timed(f)
+        print("mod=%6d aggs=%d  %.3f ms  %.1f G rows/s" % (mod, naggs, ms, n / ms / 1e6), flush=True)
