@@ -252,7 +252,9 @@ class GroupByPartialTransform : public IProcessor {
     GroupByPartialTransform(FunctionRef key, std::vector<FunctionRef> funcs, std::shared_ptr<GroupByShared> shared)
         : key_(std::move(key)), funcs_(std::move(funcs)), shared_(std::move(shared)),
           input_(std::make_shared<EmptyProcessor>()) {}
-    std::string name() const override { return "GroupByPartialTransform"; }
+    // the reference builds AggregatePartial/Final for a grouped plan too
+    // (pipeline_builder.rs:50-66), so EXPLAIN shows the same processors
+    std::string name() const override { return "AggregatePartialTransform"; }
     void connect_to(ProcessorRef input) override { input_ = std::move(input); }
     StreamRef execute() override;
 
@@ -269,7 +271,7 @@ class GroupByFinalTransform : public IProcessor {
                           bool emit_states)
         : schema_(std::move(schema)), funcs_(std::move(funcs)), shared_(std::move(shared)),
           input_(std::make_shared<EmptyProcessor>()), emit_states_(emit_states) {}
-    std::string name() const override { return "GroupByFinalTransform"; }
+    std::string name() const override { return "AggregateFinalTransform"; }
     void connect_to(ProcessorRef input) override { input_ = std::move(input); }
     StreamRef execute() override;
 

@@ -863,3 +863,46 @@ def group_by_query(total, key_expr, exprs, where=None, modulo=True):
             row.append(f.merge_result().value)
         out.append(tuple(row))
     return out
+
+
+def _agg_leaves(f, out):
+    if isinstance(f, Agg):
+        out.append(f)
+    for attr in ("left", "right", "func"):
+        g = getattr(f, attr, None)
+        if isinstance(g, Fn):
+            _agg_leaves(g, out)
+    return out
+
+
+def group_by_partial_states(total, key_expr, exprs, parts, where=None, modulo=True):
+    """What one rank ships for a GROUP BY over its partitions `parts`: per
+    group [key Value, state of every aggregate leaf (left to right)], sorted
+    by key (the engine's exchange rows; see group_by_query)."""
+    key_fn = to_function(key_expr, modulo=modulo)
+    pred = to_function(where, modulo=modulo) if where is not None else None
+    groups = {}
+    ktype = None
+    for b in numbers_stream(total, parts):
+        if pred is not None:
+            b = filter_block(pred, b)
+        if b.num_rows() == 0:
+            continue
+        kv = key_fn.eval(b)
+        karr = kv if isinstance(kv, Arr) else to_array(kv, b.num_rows())
+        ktype = karr.type
+        keys = np.asarray(karr.values)
+        for k in np.unique(keys):
+            sub = b.take(list(keys == k))
+            fs = groups.get(int(k))
+            if fs is None:
+                fs = groups[int(k)] = [to_function(e, modulo=modulo) for e in exprs]
+            for f in fs:
+                f.accumulate(sub)
+    rows = []
+    for k in sorted(groups):
+        leaves = []
+        for f in groups[k]:
+            _agg_leaves(f, leaves)
+        rows.append([Value(ktype, k)] + [a.state for a in leaves])
+    return rows

@@ -74,3 +74,55 @@ def test_sharded_exchange_and_final_merge(world, n):
         R.E_fn("count", num)]))]
     for rank, rows, lens in results:
         assert rows == exp, (rank, rows, exp)
+
+
+GB_SQL = "SELECT number%%97, count(number), sum(number), min(number+3) FROM system.numbers_mt(%d) GROUP BY number%%97"
+
+
+def gb_worker(rank, world, port, n, out_q):
+    for p in (os.path.join(ROOT, "fuse-query_amd"), os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")):
+        sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+
+    import fq_ref as R
+    from fq_amd import dist as fqd
+    from fq_amd.engine import Engine
+    from fq_amd.numbers import generate_parts, shard
+    from test_engine_cpu import encode_states
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        num = R.E_field("number")
+        key = R.E_bin("%", num, R.E_const(97))
+        exprs = [R.E_fn("count", num), R.E_fn("sum", num), R.E_fn("min", R.E_bin("+", num, R.E_const(3)))]
+        mine = [(b, e) for _, b, e in shard(generate_parts(n), rank, world)]
+        local = encode_states(R.group_by_partial_states(n, key, exprs, mine))
+        everyone = fqd.allgather_states(local)  # > 4096 bytes: length agreed first
+        with Engine(device=-1) as eng:
+            rows = eng.execute_final(GB_SQL % n, everyone).rows
+        out_q.put((rank, rows, len(local)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_group_by_exchange_and_final_merge():
+    import fq_ref as R
+    world, n = 2, 400000
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=gb_worker, args=(r, world, port, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    num = R.E_field("number")
+    exp = R.group_by_query(n, R.E_bin("%", num, R.E_const(97)),
+                           [R.E_fn("count", num), R.E_fn("sum", num), R.E_fn("min", R.E_bin("+", num, R.E_const(3)))])
+    for rank, rows, nbytes in results:
+        assert nbytes > 4096
+        assert rows == exp, rank

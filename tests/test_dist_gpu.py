@@ -1,0 +1,80 @@
+"""The multi-rank path ON THE GPU: 2 processes share cuda:0 (one box has one
+GPU), each runs its numbers_mt shard through fq_engine_execute_partial (the
+fused scans / GROUP BY kernels), the states go through
+fq_amd.dist.allgather_states over gloo (bench.py uses the same call over
+RCCL), and every rank's final merge must equal the single-process oracle."""
+import os
+import socket
+import sys
+
+import pytest
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+SQLS = [
+    "SELECT sum(number)/count(number), max(number), min(number) FROM system.numbers_mt(%d)",
+    "SELECT max(number+1), count(number) FROM system.numbers_mt(%d) WHERE (number%%8)<3",
+    "SELECT number%%10, count(number), sum(number)/count(number), max(number+1) "
+    "FROM system.numbers_mt(%d) WHERE (number%%8)<3 GROUP BY number%%10",
+]
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def worker(rank, world, port, n, out_q):
+    for p in (os.path.join(ROOT, "fuse-query_amd"), os.path.join(ROOT, "oracle")):
+        sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+
+    from fq_amd import dist as fqd
+    from fq_amd.engine import Engine
+
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        with Engine(device=0) as eng:
+            out = [fqd.execute(eng, sql % n).rows for sql in SQLS]
+        out_q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_ranks_on_the_gpu_match_the_oracle():
+    import fq_ref as R
+    world, n = 2, 4_000_000
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=worker, args=(r, world, port, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    num = R.E_field("number")
+    c = R.E_const
+    exp3 = [tuple(v.value for v in R.aggregate_query(n, [
+        R.E_bin("/", R.E_fn("sum", num), R.E_fn("count", num)), R.E_fn("max", num), R.E_fn("min", num)]))]
+    where = R.E_bin("<", R.E_bin("%", num, c(8)), c(3))
+    exp4 = [tuple(v.value for v in R.aggregate_query(n, [R.E_fn("max", R.E_bin("+", num, c(1))),
+                                                         R.E_fn("count", num)], where=where))]
+    expg = R.group_by_query(n, R.E_bin("%", num, c(10)),
+                            [R.E_fn("count", num), R.E_bin("/", R.E_fn("sum", num), R.E_fn("count", num)),
+                             R.E_fn("max", R.E_bin("+", num, c(1)))], where=where)
+    for rank, out in results:
+        assert out[0] == exp3, rank
+        assert out[1] == exp4, rank
+        assert out[2] == expg, rank

@@ -147,3 +147,44 @@ def test_final_merge_none_error(eng):
     with pytest.raises(FQError) as ei:
         eng.execute_final("SELECT sum(number) FROM system.numbers_mt(80) WHERE number < 5", states)
     assert str(ei.value) == "Internal Error: DataValue to array cannot be NONE NULL"
+
+
+# ---- GROUP BY: planning and the cross-rank merge (host-only engine) ----
+GB_SQL = ("SELECT number%%10, count(number), sum(number)/count(number), max(number+1) "
+          "FROM system.numbers_mt(%d) WHERE (number%%8)<3 GROUP BY number%%10")
+
+
+def _gb_exprs():
+    n = R.E_field("number")
+    key = R.E_bin("%", n, R.E_const(10))
+    exprs = [R.E_fn("count", n), R.E_bin("/", R.E_fn("sum", n), R.E_fn("count", n)),
+             R.E_fn("max", R.E_bin("+", n, R.E_const(1)))]
+    where = R.E_bin("<", R.E_bin("%", n, R.E_const(8)), R.E_const(3))
+    return key, exprs, where
+
+
+def test_group_by_explain_keeps_reference_display(eng):
+    txt = eng.explain("SELECT number%10, sum(number) FROM system.numbers_mt(80000) GROUP BY number%10")
+    # plan_display.rs:37-50: aggregate list, then the group list with no separator
+    assert txt.splitlines()[0] == "└─ Aggregate: sum([number])(number % 10)"
+    assert "AggregatePartialTransform × 8 processors" in txt and "AggregateFinalTransform × 1 processor" in txt
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+@pytest.mark.parametrize("total", [80000, 123457])
+def test_group_by_final_merge_of_sharded_partials(eng, world, total):
+    key, exprs, where = _gb_exprs()
+    parts = [(b, e) for _, b, e in generate_parts(total)]
+    states = []
+    for r in range(world):
+        mine = parts[len(parts) * r // world: len(parts) * (r + 1) // world]
+        states.append(encode_states(R.group_by_partial_states(total, key, exprs, mine, where)))
+    res = eng.execute_final(GB_SQL % total, states)
+    assert res.rows == R.group_by_query(total, key, exprs, where)
+    assert res.names == ["number % 10", "Count(number)", "Sum(number) / Count(number)", "Max(number + 1)"]
+
+
+def test_group_by_plan_errors(eng):
+    with pytest.raises(FQError) as ei:
+        eng.explain("SELECT number, number+1, sum(number) FROM system.numbers_mt(10) GROUP BY number%3")
+    assert str(ei.value) == "Error during plan: Projection references non-aggregate values"
