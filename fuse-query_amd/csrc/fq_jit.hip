@@ -579,12 +579,17 @@ bool gen_groupby_source(const GroupLaunch &G, int32_t tin, Gen &g, std::string &
     src += "struct Tab { u64 *keys; u64 *st[" + std::to_string(FQ_MAX_GROUP_AGGS) +
            "]; u32 *hdr; long long mask; int rmask; };\n";
     src += "#define EMPTY 0xffffffffffffffffull\n#define NA " + std::to_string(NA) + "\n#define S " +
-           std::to_string(S) + "\n";
+           std::to_string(S) + "\n#define LOG2S " + std::to_string(__builtin_ctz((unsigned)S)) + "\n";
     src += R"(
 __device__ __forceinline__ u64 mix(u64 z) {
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
     return z ^ (z >> 31);
+}
+// LDS slot hash: one 32-bit multiply (Fibonacci hashing of the folded key),
+// top bits kept; the HBM table keeps the full 64-bit mixer
+__device__ __forceinline__ u32 lds_hash(u64 k) {
+    return (((u32)k ^ (u32)(k >> 32)) * 0x9E3779B1u) >> (32 - LOG2S);
 }
 __device__ __forceinline__ void amax_f64(u64 *p, double v) {
     u64 old = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -661,17 +666,22 @@ __device__ long long ginsert(const Tab &t, u64 k) {
             row += std::string("    const ") + ctype(G.dtypes[a]) + " v" + std::to_string(a) + " = fq_val" +
                    std::to_string(a) + "(x, c, flags, 1u);\n";
     row += R"(    int slot = -1;
-    if (k != EMPTY && !*s_bypass) {
-        int h = (int)(mix(k) & (u64)(S - 1));
+    if (k != EMPTY) {
+        // Once the LDS table is 3/4 full (more groups than it holds) it stops
+        // taking new keys: resident keys still aggregate in LDS, the others
+        // go to HBM after a short probe (an empty slot proves absence: there
+        // are no deletions).
+        const bool full = *s_bypass != 0;
+        const int maxp = full ? 4 : 16;
+        int h = (int)(lds_hash(k) & (u32)(S - 1));
 #pragma unroll 1
-        for (int p = 0; p < 16; ++p) {
+        for (int p = 0; p < maxp; ++p) {
             const u64 cur = s_keys[h];
             if (cur == k) { slot = h; break; }
             if (cur == EMPTY) {
+                if (full) break;
                 const u64 old = atomicCAS((unsigned long long *)&s_keys[h], EMPTY, k);
                 if (old == EMPTY) {
-                    // a saturated LDS table (high cardinality) stops being
-                    // probed for the rest of this workgroup
                     if (atomicAdd(s_bypass + 1, 1) + 1 >= S * 3 / 4) *s_bypass = 1;
                     slot = h;
                     break;
