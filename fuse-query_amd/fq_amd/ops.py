@@ -11,7 +11,7 @@ import numpy as np
 import torch
 
 from . import abi
-from ._lib import FQError, check, lib
+from ._lib import FQError, check, last_error, lib  # noqa: F401
 from .expr import from_bits, to_bits
 
 NP_DTYPES = {
