@@ -1,3 +1,5 @@
+"""GROUP BY throughput vs number of groups and aggregates over one numbers_mt
+partition (python tools/groupby_sweep.py [rows]); prints one line per shape."""
 import sys, os, ctypes as C, statistics
 sys.path.insert(0, "fuse-query_amd")
 import torch
