@@ -50,6 +50,9 @@ QUERIES = {
     # not a BASELINE config: filtered SUM, which needs the per-block emptiness
     # of the reference's state machine (block-mode scan)
     "c4s": ("SELECT sum(number+1) FROM system.numbers_mt({N}) WHERE (number%8)<3", abi.AGG_SUM),
+    # not a BASELINE config: GROUP BY (no reference transform)
+    "g1": ("SELECT number%1000, count(number), sum(number), max(number) FROM system.numbers_mt({N}) "
+           "GROUP BY number%1000", 0),
 }
 
 
@@ -60,6 +63,9 @@ def closed_form(query, n):
         return [s]
     if query == "c3":
         return [s // n, n - 1, 0]
+    if query == "g1":
+        per = n // 1000  # n is a multiple of 80,000
+        return [(k, per, (k * per + 1000 * per * (per - 1) // 2) % U64, k + 1000 * (per - 1)) for k in range(1000)]
     if query == "c4s":
         tot = 0
         for r in range(3):
@@ -99,6 +105,8 @@ def latest_pmc_traffic(kernel_substr, query):
 def cpu_baseline(sample_rows, threads, query="c3"):
     """Restated reference CPU path (oracle/fq_oracle.c) on the host cores,
     over the same query as the GPU line."""
+    if query == "g1":
+        raise RuntimeError("no CPU restatement of GROUP BY: the reference has no GROUP BY transform")
     import oracle_c
     from fq_amd.expr import chain, predicate
     native = True
@@ -190,9 +198,8 @@ def main():
         % (len(mine), total_rows, total_rows * 8 / 1e9, rank))
 
     def step():
-        if world == 1:
-            return list(eng.execute(sql).rows[0])
-        return list(fqd.execute(eng, sql).rows[0])
+        r = eng.execute(sql) if world == 1 else fqd.execute(eng, sql)
+        return r.rows if args.query == "g1" else list(r.rows[0])
 
     for _ in range(max(args.warmup, 1)):
         res = step()
@@ -222,7 +229,7 @@ def main():
     st = eng.stats()
     jit1 = ops.jit_stats()
     jitted = jit1["jit_launches"] - jit0["jit_launches"]
-    kernel = "fq_jit_scan" if jitted else "agg_flat_kernel"
+    kernel = "fq_jit_groupby" if args.query == "g1" else ("fq_jit_scan" if jitted else "agg_flat_kernel")
     launches = max(st["scan_launches"], 1)
     avg_launch_ms = st["scan_ms"] / launches
     bytes_per_launch = st["scan_bytes"] / launches
@@ -272,11 +279,13 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBPS,
                 "traffic": traffic,
-                "kernel": "fq_aggregate fused scan (%s + finalize), one launch per partition%s"
-                          % (kernel, " (hipRTC-specialised for this expression shape)" if jitted else ""),
+                "kernel": ("fq_group_aggregate (fq_jit_groupby, hipRTC-specialised), one launch per partition"
+                           if args.query == "g1" else
+                           "fq_aggregate fused scan (%s + finalize), one launch per partition%s"
+                           % (kernel, " (hipRTC-specialised for this expression shape)" if jitted else "")),
                 "bytes_per_launch": bytes_per_launch,
             },
-            "result": res,
+            "result": res if args.query != "g1" else {"groups": len(res), "first": res[0], "last": res[-1]},
             "host_ms_per_step": {"plan": st["plan_ms"] / args.steps, "first_launch": st["first_launch_ms"] / args.steps,
                                  "exec": st["exec_ms"] / args.steps},
             "jit": {"specialised_launches": jitted, "kernels_compiled": jit1["kernels_compiled"],

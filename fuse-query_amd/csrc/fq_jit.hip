@@ -587,7 +587,9 @@ __device__ __forceinline__ u64 mix(u64 z) {
     return z ^ (z >> 31);
 }
 // LDS slot hash: one 32-bit multiply (Fibonacci hashing of the folded key),
-// top bits kept; the HBM table keeps the full 64-bit mixer
+// top bits kept; the HBM table keeps the full 64-bit mixer.  (An XOR-fold
+// that keeps consecutive keys in consecutive slots measured no faster: a
+// lane holds rows 2l and 2l+1, so a wave's keys are strided anyway.)
 __device__ __forceinline__ u32 lds_hash(u64 k) {
     return (((u32)k ^ (u32)(k >> 32)) * 0x9E3779B1u) >> (32 - LOG2S);
 }
@@ -655,16 +657,27 @@ __device__ long long ginsert(const Tab &t, u64 k) {
         if (dt == FQ_DT_INT64) return kind == FQ_AGG_MAX ? "0x8000000000000000ull" : "0x7fffffffffffffffull";
         return kind == FQ_AGG_MAX ? "0xfff0000000000000ull" : "0x7ff0000000000000ull";  // -inf / +inf
     };
-    // per-row update
-    std::string row = "__device__ __forceinline__ void fq_row(TIn x, long long idx, const Consts &c, const Tab &t,\n"
-                      "    const u64 *__restrict__ bitmap, u64 *s_keys, u64 (*s_st)[S], u32 &flags, int *s_bypass) {\n";
-    if (G.pred.kind == FQ_PRED_EXPR) row += "    if (!fq_pred(x, c, flags, 1u)) return;\n";
-    else if (G.pred.kind == FQ_PRED_BITMAP) row += "    if (!((bitmap[idx >> 6] >> (idx & 63)) & 1ull)) return;\n";
-    row += "    (void)idx; (void)bitmap;\n    const u64 k = fq_key(x, c, flags, 1u);\n";
+    // per-row work in two halves so a tile's 8 rows issue their first LDS
+    // probe reads together (independent loads, one latency): fq_prep
+    // evaluates predicate, key and arguments; fq_commit finds/claims the
+    // slot and applies the states.
+    std::string row = "struct Row { u64 k; int h; u32 pass;";
+    for (int a = 0; a < NA; ++a)
+        if (G.kinds[a] != FQ_AGG_COUNT) row += std::string(" ") + ctype(G.dtypes[a]) + " v" + std::to_string(a) + ";";
+    row += " };\n";
+    row += "__device__ __forceinline__ void fq_prep(TIn x, long long idx, const Consts &c,\n"
+           "    const u64 *__restrict__ bitmap, u32 &flags, Row &r) {\n    r.pass = 1u;\n";
+    if (G.pred.kind == FQ_PRED_EXPR) row += "    r.pass = fq_pred(x, c, flags, 1u) ? 1u : 0u;\n";
+    else if (G.pred.kind == FQ_PRED_BITMAP) row += "    r.pass = (u32)((bitmap[idx >> 6] >> (idx & 63)) & 1ull);\n";
+    row += "    (void)idx; (void)bitmap;\n    r.k = fq_key(x, c, flags, r.pass);\n";
     for (int a = 0; a < NA; ++a)
         if (G.kinds[a] != FQ_AGG_COUNT)
-            row += std::string("    const ") + ctype(G.dtypes[a]) + " v" + std::to_string(a) + " = fq_val" +
-                   std::to_string(a) + "(x, c, flags, 1u);\n";
+            row += "    r.v" + std::to_string(a) + " = fq_val" + std::to_string(a) + "(x, c, flags, r.pass);\n";
+    row += "    r.h = (int)(lds_hash(r.k) & (u32)(S - 1));\n}\n";
+    row += "__device__ __forceinline__ u64 fq_first(const Row &r, const u64 *s_keys) {\n"
+           "    return (r.pass && r.k != EMPTY) ? s_keys[r.h] : EMPTY;\n}\n";
+    row += "__device__ __forceinline__ void fq_commit(const Row &r, u64 cur0, const Tab &t, u64 *s_keys,\n"
+           "    u64 (*s_st)[S], int *s_bypass) {\n    if (!r.pass) return;\n    const u64 k = r.k;\n";
     row += R"(    int slot = -1;
     if (k != EMPTY) {
         // Once the LDS table is 3/4 full (more groups than it holds) it stops
@@ -673,10 +686,10 @@ __device__ long long ginsert(const Tab &t, u64 k) {
         // are no deletions).
         const bool full = *s_bypass != 0;
         const int maxp = full ? 4 : 16;
-        int h = (int)(lds_hash(k) & (u32)(S - 1));
+        int h = r.h;
 #pragma unroll 1
         for (int p = 0; p < maxp; ++p) {
-            const u64 cur = s_keys[h];
+            const u64 cur = p == 0 ? cur0 : s_keys[h];
             if (cur == k) { slot = h; break; }
             if (cur == EMPTY) {
                 if (full) break;
@@ -695,12 +708,16 @@ __device__ long long ginsert(const Tab &t, u64 k) {
 )";
     for (int a = 0; a < NA; ++a)
         row += "        " + state_update(G.kinds[a], G.dtypes[a], "&s_st[" + std::to_string(a) + "][slot]",
-                                         "v" + std::to_string(a)) + "\n";
+                                         "r.v" + std::to_string(a)) + "\n";
     row += "    } else {\n        const long long gs = ginsert(t, k);\n        if (gs >= 0) {\n";
     for (int a = 0; a < NA; ++a)
         row += "            " + state_update(G.kinds[a], G.dtypes[a], "&t.st[" + std::to_string(a) + "][gs]",
-                                             "v" + std::to_string(a)) + "\n";
+                                             "r.v" + std::to_string(a)) + "\n";
     row += "        }\n    }\n}\n";
+    row += "__device__ __forceinline__ void fq_row(TIn x, long long idx, const Consts &c, const Tab &t,\n"
+           "    const u64 *__restrict__ bitmap, u64 *s_keys, u64 (*s_st)[S], u32 &flags, int *s_bypass) {\n"
+           "    Row r;\n    fq_prep(x, idx, c, bitmap, flags, r);\n"
+           "    fq_commit(r, fq_first(r, s_keys), t, s_keys, s_st, s_bypass);\n}\n";
     src += row;
 
     // kernel
@@ -730,19 +747,39 @@ fq_jit_groupby(const TIn *__restrict__ col, long long n, long long head, const u
     const u32x4 *__restrict__ vp = (const u32x4 *)(col + head);
     const long long TV = 4 * 256;
     const long long ntiles = nvec / TV;
+    // software pipelined: the next tile's loads are in flight while this
+    // tile's rows go through the LDS table (2 waves per SIMD cannot hide the
+    // HBM latency otherwise)
+    u32x4 nxt[4];
+    if ((long long)blockIdx.x < ntiles) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            nxt[k] = __builtin_nontemporal_load(vp + (long long)blockIdx.x * TV + threadIdx.x + (long long)k * 256);
+    }
     for (long long tt = blockIdx.x; tt < ntiles; tt += gridDim.x) {
         const long long base = tt * TV + threadIdx.x;
         u32x4 raw[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) raw[k] = __builtin_nontemporal_load(vp + base + (long long)k * 256);
+        for (int k = 0; k < 4; ++k) raw[k] = nxt[k];
+        const long long tn = tt + gridDim.x;
+        if (tn < ntiles) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) nxt[k] = __builtin_nontemporal_load(vp + tn * TV + threadIdx.x + (long long)k * 256);
+        }
+        Row r[8];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             TIn x[2];
             __builtin_memcpy(&x[0], &raw[k], 16);
             const long long i0 = head + (base + (long long)k * 256) * 2;
-            fq_row(x[0], i0, c, tr, bitmap, s_keys, s_st, flags, s_bypass);
-            fq_row(x[1], i0 + 1, c, tr, bitmap, s_keys, s_st, flags, s_bypass);
+            fq_prep(x[0], i0, c, bitmap, flags, r[2 * k]);
+            fq_prep(x[1], i0 + 1, c, bitmap, flags, r[2 * k + 1]);
         }
+        u64 cur[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) cur[j] = fq_first(r[j], s_keys);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) fq_commit(r[j], cur[j], tr, s_keys, s_st, s_bypass);
     }
     for (long long v = ntiles * TV + g; v < nvec; v += T) {
         const u32x4 raw = __builtin_nontemporal_load(vp + v);

@@ -1,7 +1,7 @@
 """GROUP BY throughput vs number of groups and aggregates over one numbers_mt
-partition (python tools/groupby_sweep.py [rows]); prints one line per shape."""
+partition (python tools/groupby_sweep.py [rows] [mods] [naggs]); one line per shape."""
 import sys, os, ctypes as C, statistics
-sys.path.insert(0, "fuse-query_amd")
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "fuse-query_amd"))
 import torch
 from fq_amd import abi, ops
 from fq_amd._lib import check, lib
@@ -16,8 +16,10 @@ def timed(fn, reps=5):
     for _ in range(reps):
         e0.record(); fn(); e1.record(); e1.synchronize(); ts.append(e0.elapsed_time(e1))
     return statistics.median(ts)
-for mod in (8, 64, 1000, 4096, 100000):
-    for naggs in (1, 3):
+MODS = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else [8, 64, 1000, 4096, 100000]
+NAGGS = [int(x) for x in sys.argv[3].split(",")] if len(sys.argv) > 3 else [1, 3]
+for mod in MODS:
+    for naggs in NAGGS:
         key, _ = chain(U, [("%", mod)])
         aggs = [(abi.AGG_COUNT, U), (abi.AGG_SUM, U), (abi.AGG_MAX, U)][:naggs]
         gt = ops.GroupTable(max(64, 4 * mod), aggs)
