@@ -386,11 +386,23 @@ bool gen_source(const Launch &L, int32_t tin, bool chain, Gen &g, std::string &s
     const u32x4 *__restrict__ vp = (const u32x4 *)(col + head);
     const long long TV = 4 * 256;
     const long long ntiles = nvec / TV;
+    // next tile's loads in flight while this tile is evaluated
+    u32x4 nxt[4];
+    if ((long long)blockIdx.x < ntiles) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            nxt[k] = __builtin_nontemporal_load(vp + (long long)blockIdx.x * TV + threadIdx.x + (long long)k * 256);
+    }
     for (long long t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const long long base = t * TV + threadIdx.x;
         u32x4 raw[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) raw[k] = __builtin_nontemporal_load(vp + base + (long long)k * 256);
+        for (int k = 0; k < 4; ++k) raw[k] = nxt[k];
+        const long long tn = t + gridDim.x;
+        if (tn < ntiles) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) nxt[k] = __builtin_nontemporal_load(vp + tn * TV + threadIdx.x + (long long)k * 256);
+        }
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             TIn x[2];
