@@ -1,7 +1,7 @@
 // Tuning variants of the C3 scan (identity u64, sum/max/min/count, no
 // predicate) for tools/tune_scan.py.  Not used by the product path: the
 // winning configuration is folded into agg_flat_kernel (fq_aggregate.hip).
-// Exported as fq_tune_scan_u64 (internal; not declared in include/).
+// Built into lib/libfq_tune.so (make tune), not into the product library.
 #include <hip/hip_runtime.h>
 
 #include "fq_common.h"

@@ -11,6 +11,7 @@ import itertools
 import json
 import os
 import statistics
+import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -20,8 +21,13 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from fq_amd import ops  # noqa: E402
-from fq_amd._lib import check, lib  # noqa: E402
+from fq_amd._lib import check  # noqa: E402
 
+# the sweep kernels live in their own library (make -C fuse-query_amd tune)
+_TUNE = os.path.join(ROOT, "fuse-query_amd", "lib", "libfq_tune.so")
+if not os.path.exists(_TUNE):
+    subprocess.run(["make", "-C", os.path.join(ROOT, "fuse-query_amd"), "tune"], check=True)
+lib = C.CDLL(_TUNE)
 lib.fq_tune_scan_u64.restype = C.c_int32
 lib.fq_tune_scan_u64.argtypes = [C.c_void_p, C.c_int64, C.c_int32, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p]
 lib.fq_tune_write_u64.restype = C.c_int32
