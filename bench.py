@@ -39,7 +39,11 @@ from fq_amd.numbers import BLOCK_SIZE, generate_parts, shard, stream_rows  # noq
 
 METRIC = "rows/s + achieved HBM GB/s on 10B-row numbers_mt agg, 1/2/4/8 GPUs"
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-README_C3_ROWS_PER_S = 1e10 / 6.40  # reference README.md:62 (8 vCPU KVM), BASELINE.md section 1
+# reference README.md:57 / :62 (8 vCPU KVM), BASELINE.md section 1: the only
+# published numbers for these exact queries (sum; sum/count, max, min)
+README_ROWS_PER_S = {"c2": 1e10 / 1.77, "c3": 1e10 / 6.40}
+README_REF = {"c2": "reference README.md:57 (1.77 s for 1e10 rows, 8 vCPU KVM)",
+              "c3": "reference README.md:62 (6.40 s for 1e10 rows, 8 vCPU KVM)"}
 U64 = 2**64
 
 QUERIES = {
@@ -252,8 +256,8 @@ def main():
             "ms_per_step": dt / args.steps * 1e3,
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": value / README_C3_ROWS_PER_S if args.query == "c3" else None,
-            "vs_baseline_ref": "reference README.md:62 (6.40 s for 1e10 rows, 8 vCPU KVM)",
+            "vs_baseline": value / README_ROWS_PER_S[args.query] if args.query in README_ROWS_PER_S else None,
+            "vs_baseline_ref": README_REF.get(args.query, "no published reference number for this query"),
             "dtype": "u64",
             "data": "synthetic: system.numbers_mt iota column (u64), resident in HBM before timing",
             "config": {

@@ -252,3 +252,19 @@ def test_mysql_writer_types_and_boolean_error():
     assert r.mysql_error == "Internal Error: Unsupported column type:Boolean"
     r = q("select (number+1) as c1, number/2 as c2 from system.numbers_mt(10000000) where number+1=4 limit 10")
     assert r.mysql_types == [3, 3] and r.text_rows == [("4", "1")]
+
+
+def test_f64_division_within_one_ulp():
+    # north_star: f64 division within 1 ULP of the reference CPU path.  The
+    # device divides in IEEE binary64 exactly as the CPU does, so the
+    # distance is 0 ULP; max/min of a quotient involve no summation order.
+    import numpy as np
+    n = 10_000_000
+    r = q("SELECT max(number/3.0), min((number+1)/7.0), max(number/0.1) FROM system.numbers_mt(%d)" % n)
+    x = np.arange(0, n, dtype=np.uint64).astype(np.float64)  # 1.25M-row partitions: no dropped rows
+    exp = [np.max(x / 3.0), np.min((x + 1) / 7.0), np.max(x / 0.1)]
+    for got, e in zip(r.rows[0], exp):
+        ulp = abs(np.float64(got).view(np.int64) - np.float64(e).view(np.int64))
+        assert ulp <= 1, (got, e, ulp)
+        assert ulp == 0
+
