@@ -97,10 +97,33 @@ class Result:
                     self.mysql_error = last_error()
                     break
                 self.mysql_types.append(t.value)
-            self.text_rows = [tuple((lambda t: t.decode() if t is not None else None)(lib.fq_result_text(ptr, r, c))
-                                    for c in range(ncol)) for r in range(nrow)]
+            # the text form is built on first use (the handle stays open until then)
+            self._ptr, ptr = ptr, None
+            self._text = None
         finally:
-            lib.fq_result_free(ptr)
+            if ptr is not None:
+                lib.fq_result_free(ptr)
+
+    @property
+    def text_rows(self):
+        """Every value as arrow's array_value_to_string (fq_result_text)."""
+        if self._text is None:
+            ncol, nrow = len(self.names), len(self.rows)
+            self._text = [tuple((lambda t: t.decode() if t is not None else None)(lib.fq_result_text(self._ptr, r, c))
+                                for c in range(ncol)) for r in range(nrow)]
+            self._free()
+        return self._text
+
+    def _free(self):
+        if getattr(self, "_ptr", None) is not None:
+            lib.fq_result_free(self._ptr)
+            self._ptr = None
+
+    def __del__(self):
+        try:
+            self._free()
+        except Exception:  # interpreter shutdown
+            pass
 
     def __repr__(self):
         return "Result(names=%r, rows=%r)" % (self.names, self.rows[:10])
