@@ -359,4 +359,16 @@ __device__ __forceinline__ T shfl_xor64(T v, int m) {
     }
 }
 
+// 64-bit value of lane `src` / of lane (lane - d) (2 x 32-bit moves)
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
+    const uint32_t lo = __shfl((unsigned)(v & 0xffffffffu), src, kWave);
+    const uint32_t hi = __shfl((unsigned)(v >> 32), src, kWave);
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t shfl_up64(uint64_t v, int d) {
+    const uint32_t lo = __shfl_up((unsigned)(v & 0xffffffffu), d, kWave);
+    const uint32_t hi = __shfl_up((unsigned)(v >> 32), d, kWave);
+    return ((uint64_t)hi << 32) | lo;
+}
+
 }  // namespace fqk

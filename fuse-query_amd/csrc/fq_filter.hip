@@ -46,30 +46,52 @@ __global__ void __launch_bounds__(kTileWords)
     }
 }
 
-// exclusive scan of counts[0..ntiles) in place; counts[ntiles] = total
+// exclusive scan of counts[0..ntiles) in place; counts[ntiles] = total.
+// One workgroup of 16 waves; each wave owns a contiguous segment and walks it
+// 64 entries at a time (coalesced loads, wave scan by shuffles), twice: once
+// for its total, once to write prefixes after the 16 totals are scanned.
+__device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v, int lane) {
+#pragma unroll
+    for (int off = 1; off < kWave; off <<= 1) {
+        const uint64_t u = shfl_up64(v, off);
+        if (lane >= off) v += u;
+    }
+    return v;
+}
+
 __global__ void __launch_bounds__(kScanThreads) compact_scan_kernel(uint64_t *counts, int64_t ntiles) {
-    const int64_t per = (ntiles + kScanThreads - 1) / kScanThreads;
-    const int64_t b = threadIdx.x * per;
-    const int64_t e = (b + per < ntiles) ? b + per : ntiles;
-    uint64_t local = 0;
-    for (int64_t i = b; i < e; ++i) local += counts[i];
-    __shared__ uint64_t s[kScanThreads];
-    s[threadIdx.x] = local;
+    constexpr int W = kScanThreads / kWave;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wave = threadIdx.x / kWave;
+    const int64_t seg = (ntiles + W - 1) / W;
+    const int64_t b = (int64_t)wave * seg;
+    const int64_t e = (b + seg < ntiles) ? b + seg : ntiles;
+    uint64_t sum = 0;
+    for (int64_t i = b + lane; i < e; i += kWave) sum += counts[i];
+#pragma unroll
+    for (int off = kWave / 2; off > 0; off >>= 1) sum += shfl_xor64(sum, off);
+    __shared__ uint64_t s_tot[W + 1];
+    if (lane == 0) s_tot[wave] = sum;
     __syncthreads();
-    // Hillis-Steele inclusive scan over 1024 sums
-    for (int off = 1; off < kScanThreads; off <<= 1) {
-        const uint64_t v = threadIdx.x >= off ? s[threadIdx.x - off] : 0;
-        __syncthreads();
-        s[threadIdx.x] += v;
-        __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t run = 0;
+        for (int w = 0; w < W; ++w) {
+            const uint64_t t = s_tot[w];
+            s_tot[w] = run;
+            run += t;
+        }
+        s_tot[W] = run;
     }
-    uint64_t run = s[threadIdx.x] - local;  // exclusive prefix of this chunk
-    for (int64_t i = b; i < e; ++i) {
-        const uint64_t c = counts[i];
-        counts[i] = run;
-        run += c;
+    __syncthreads();
+    uint64_t run = s_tot[wave];
+    for (int64_t i0 = b; i0 < e; i0 += kWave) {
+        const int64_t i = i0 + lane;
+        const uint64_t v = i < e ? counts[i] : 0;
+        const uint64_t incl = wave_incl_scan(v, lane);
+        if (i < e) counts[i] = run + incl - v;
+        run += shfl64(incl, kWave - 1);
     }
-    if (threadIdx.x == kScanThreads - 1) counts[ntiles] = s[kScanThreads - 1];
+    if (threadIdx.x == 0) counts[ntiles] = s_tot[W];
 }
 
 template <typename T>
@@ -126,6 +148,76 @@ __global__ void __launch_bounds__(kTileWords)
     }
 }
 
+// 8-byte columns, 16-byte aligned: lane l of a wave loads rows 2l and 2l+1
+// of a 128-row word pair with one 16-byte load (lanes 0..31: the pair's first
+// word, 32..63: its second), 4 pairs in flight per step; positions come from
+// the same LDS word offsets.
+typedef unsigned long long u64x2_t __attribute__((ext_vector_type(2)));
+
+template <typename T>
+__global__ void __launch_bounds__(kTileWords)
+    compact_scatter_vec_kernel(const T *__restrict__ in, const uint64_t *__restrict__ bm, int64_t n,
+                               const uint64_t *__restrict__ offsets, T *__restrict__ out) {
+    static_assert(sizeof(T) == 8, "8-byte rows");
+    const int64_t nwords = (n + 63) / 64;
+    const int64_t w0 = (int64_t)blockIdx.x * kTileWords;
+    __shared__ uint64_t s_word[kTileWords];
+    __shared__ uint32_t s_off[kTileWords];
+    __shared__ uint32_t s_wsum[kTileWords / kWave];
+    const int t = threadIdx.x;
+    const int lane = t & (kWave - 1);
+    const int wave = t / kWave;
+    const uint64_t word = word_at(bm, w0 + t, nwords, n);
+    s_word[t] = word;
+    uint32_t c = (uint32_t)__popcll(word);
+    uint32_t incl = c;
+#pragma unroll
+    for (int off = 1; off < kWave; off <<= 1) {
+        const uint32_t v = (uint32_t)__shfl_up((int)incl, off, kWave);
+        if (lane >= off) incl += v;
+    }
+    if (lane == kWave - 1) s_wsum[wave] = incl;
+    __syncthreads();
+    uint32_t wave_base = 0;
+    for (int i = 0; i < wave; ++i) wave_base += s_wsum[i];
+    s_off[t] = wave_base + incl - c;
+    __syncthreads();
+    const uint64_t base = offsets[blockIdx.x];
+    const int half = lane >> 5;        // which word of the pair
+    const int bl = (lane & 31) * 2;    // bit of this lane's first row in that word
+    const uint64_t m_lt = bl == 0 ? 0ull : (~0ull >> (64 - bl));
+    const u64x2_t *__restrict__ vin = reinterpret_cast<const u64x2_t *>(in);
+    constexpr int kPairs = 4;
+    for (int j = 0; j < kWave; j += 2 * kPairs) {
+        u64x2_t x[kPairs];
+        uint64_t wd[kPairs];
+#pragma unroll
+        for (int k = 0; k < kPairs; ++k) {
+            const int wi = wave * kWave + j + 2 * k + half;
+            wd[k] = s_word[wi];
+            const int64_t row = (w0 + wave * kWave + j + 2 * k) * 64 + 2 * lane;
+            const uint64_t bits = (wd[k] >> bl) & 3ull;
+            x[k] = u64x2_t{0, 0};
+            if (bits) {
+                if (row + 1 < n) {
+                    x[k] = __builtin_nontemporal_load(vin + (row >> 1));
+                } else {
+                    x[k].x = (unsigned long long)__builtin_bit_cast(uint64_t, in[row]);
+                }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kPairs; ++k) {
+            const int wi = wave * kWave + j + 2 * k + half;
+            const uint64_t bits = (wd[k] >> bl) & 3ull;
+            if (!bits) continue;
+            uint64_t pos = base + s_off[wi] + (uint64_t)__popcll(wd[k] & m_lt);
+            if (bits & 1ull) out[pos++] = __builtin_bit_cast(T, (uint64_t)x[k].x);
+            if (bits & 2ull) out[pos] = __builtin_bit_cast(T, (uint64_t)x[k].y);
+        }
+    }
+}
+
 }  // namespace fqk
 
 extern "C" {
@@ -172,8 +264,12 @@ fq_status fq_filter_compact(const fq_col *in, const uint64_t *d_bitmap, void *d_
                                (const uint32_t *)in->data, d_bitmap, n, counts, (uint32_t *)d_out);
             break;
         default:
-            hipLaunchKernelGGL(compact_scatter_kernel<uint64_t>, dim3((unsigned)ntiles), dim3(kTileWords), 0, st,
-                               (const uint64_t *)in->data, d_bitmap, n, counts, (uint64_t *)d_out);
+            if (((uintptr_t)in->data & 15u) == 0)
+                hipLaunchKernelGGL(compact_scatter_vec_kernel<uint64_t>, dim3((unsigned)ntiles), dim3(kTileWords), 0,
+                                   st, (const uint64_t *)in->data, d_bitmap, n, counts, (uint64_t *)d_out);
+            else
+                hipLaunchKernelGGL(compact_scatter_kernel<uint64_t>, dim3((unsigned)ntiles), dim3(kTileWords), 0,
+                                   st, (const uint64_t *)in->data, d_bitmap, n, counts, (uint64_t *)d_out);
             break;
     }
     FQ_HIP_TRY(hipGetLastError());

@@ -330,3 +330,27 @@ def test_elementwise_fast_path_div_zero_in_tile_and_tail():
         with pytest.raises(ops.FQError) as ei:
             ops.arith("%", ops.from_numpy(a), ops.from_numpy(b))
         assert str(ei.value) == "Internal Error: Divide by zero error"
+
+
+@pytest.mark.parametrize("n", [1, 63, 64, 127, 128, 129, 16384 * 3 + 1, 16384 * 5 + 128, 1_000_003])
+def test_filter_compaction_vector_path_edges(n, jit_mode):
+    """16-byte-aligned 8-byte columns take the pairwise vector scatter; odd
+    lengths end on a row whose pair partner is past the column."""
+    if jit_mode != "interp":
+        pytest.skip("no expression program involved")
+    rng = np.random.default_rng(n)
+    for dt, npdt in ((abi.DT_UINT64, np.uint64), (abi.DT_FLOAT64, np.float64), (abi.DT_INT64, np.int64)):
+        x = rng.integers(0, 2**40, size=n).astype(npdt)
+        X = ops.from_numpy(x, dt)
+        for thr in (0.0, 0.3, 0.97, 1.0):
+            keep = rng.random(n) < thr
+            keep[-1] = True  # the last row (odd lengths: no pair partner)
+            m = ops.from_numpy(keep.astype(np.uint64), abi.DT_UINT64)
+            bm = ops.compare("=", m, 1)
+            got = ops.filter_compact(X, bm).to_numpy()
+            assert np.array_equal(got, x[keep]), (dt, thr)
+    # misaligned (8-byte offset) input keeps the scalar scatter
+    X = ops.from_numpy(np.arange(n + 1, dtype=np.uint64))
+    Xs = ops.DeviceColumn(X.buf, n, abi.DT_UINT64, offset=8)
+    bm = ops.compare("<", Xs, 2**63)
+    assert np.array_equal(ops.filter_compact(Xs, bm).to_numpy(), np.arange(1, n + 1, dtype=np.uint64))
