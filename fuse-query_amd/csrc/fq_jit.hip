@@ -427,17 +427,46 @@ bool gen_source(const Launch &L, int32_t tin, bool chain, Gen &g, std::string &s
     }
 )";
     } else {
-        // block mode (agg_block_kernel, 8 elements per lane in flight)
+        // block mode (agg_block_kernel): one wave per reference block; with a
+        // 16-byte-aligned column and an even block size every block starts
+        // on a 16-byte boundary and is read with 16-byte loads (4 per lane in
+        // flight), else with 8-byte loads (8 per lane)
         src += R"(
     (void)head;
     const int lane = threadIdx.x & 63;
     const long long w = ((long long)blockIdx.x * 256 + threadIdx.x) / 64;
     const long long W = ((long long)gridDim.x * 256) / 64;
     const long long nb = (n + R - 1) / R;
+    const bool vec = ((((unsigned long long)col) & 15ull) == 0ull) && ((R & 1) == 0);
     for (long long b = w; b < nb; b += W) {
         const long long s = b * R;
         const long long e = (s + R < n) ? s + R : n;
         u32 any = 0;
+        if (vec) {
+            const long long nv = (e - s) >> 1;
+            const u32x4 *__restrict__ bp = (const u32x4 *)(col + s);
+            for (long long v = lane; v < nv; v += 64 * 4) {
+                u32x4 raw[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const long long vk = v + (long long)k * 64;
+                    if (vk < nv) raw[k] = __builtin_nontemporal_load(bp + vk);
+                    else raw[k] = u32x4{0u, 0u, 0u, 0u};
+                }
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const long long vk = v + (long long)k * 64;
+                    const u32 li = vk < nv ? 1u : 0u;
+                    TIn x[2];
+                    __builtin_memcpy(&x[0], &raw[k], 16);
+                    any |= fq_acc(acc, x[0], s + 2 * vk, li, c, bitmap);
+                    any |= fq_acc(acc, x[1], s + 2 * vk + 1, li, c, bitmap);
+                }
+            }
+            if (((e - s) & 1) && lane == 0) any |= fq_acc(acc, col[e - 1], e - 1, 1u, c, bitmap);
+            if (__ballot(any != 0) == 0ull) acc.flags |= )" + std::to_string(FQ_STATE_ANY_EMPTY) + R"(u;
+            continue;
+        }
         for (long long i = s + lane; i < e; i += 64 * 8) {
             TIn x[8];
 #pragma unroll

@@ -354,3 +354,19 @@ def test_filter_compaction_vector_path_edges(n, jit_mode):
     Xs = ops.DeviceColumn(X.buf, n, abi.DT_UINT64, offset=8)
     bm = ops.compare("<", Xs, 2**63)
     assert np.array_equal(ops.filter_compact(Xs, bm).to_numpy(), np.arange(1, n + 1, dtype=np.uint64))
+
+
+@pytest.mark.parametrize("block_rows,n,offset", [(10000, 100_001, 0), (9999, 99_990, 0), (10000, 60_000, 1),
+                                                  (2, 1001, 0), (64, 6401, 0)])
+def test_block_mode_vector_and_scalar_paths(block_rows, n, offset):
+    """Filtered sum (block mode): even block sizes on an aligned column take
+    16-byte loads, odd ones / misaligned columns 8-byte loads; every block's
+    emptiness must match the reference's per-block state machine."""
+    host = np.arange(5, 5 + n + offset, dtype=np.uint64)
+    X = ops.from_numpy(host)
+    col = ops.DeviceColumn(X.buf, n, abi.DT_UINT64, offset=8 * offset) if offset else X
+    h = host[offset:]
+    value, _ = chain(abi.DT_UINT64, [("+", 1)])
+    for pred in (predicate(abi.DT_UINT64, [("%", 8)], "<", 3),     # every block keeps rows
+                 predicate(abi.DT_UINT64, [], "<", 5 + block_rows)):  # only the first block does
+        check_against_oracle(h, abi.DT_UINT64, block_rows, pred=pred, value=value, gpu_col=col)
