@@ -691,7 +691,12 @@ void AggFusion::end_block() {
 
 void AggFusion::finish() {
     end_block();
-    if (launched_) wait_launched();  // only this pipe's scans, not the whole queue
+    // only this pipe's scans, not the whole queue: with profiling the last
+    // scan's closing timing event already marks that point (no extra marker)
+    if (launched_) {
+        if (!events_.empty()) check_hip(hipEventSynchronize(events_.back().second), "hipEventSynchronize");
+        else wait_launched();
+    }
     finished_ = true;
     for (auto &p : events_) {
         float ms = 0;
