@@ -445,6 +445,45 @@ fq_agg_state AggregatorFunction::summarize(const DataBlock &b, ExecCtx &ctx) {
 }
 
 // ---------------------------------------------------------------------------
+// LogicFunction (function_logic.rs:47-94, data_array_logic.rs:10-31)
+// ---------------------------------------------------------------------------
+static const char *logic_op_str(int32_t op) { return op == FQ_LOGIC_AND ? "and" : "or"; }
+
+std::string LogicFunction::display() const {
+    return left_->display() + " " + logic_op_str(op_) + " " + right_->display();
+}
+
+ColumnarValue LogicFunction::eval(const DataBlock &b, ExecCtx &ctx) {
+    ColumnarValue l = left_->eval(b, ctx);
+    ColumnarValue r = right_->eval(b, ctx);
+    if (!l.is_array || !r.is_array)
+        throw_internal(std::string("Cannot do data_array ") + logic_op_str(op_) + ", left:" +
+                       dtype_name(l.data_type()) + ", right:" + dtype_name(r.data_type()));
+    for (const ColumnarValue *v : {&l, &r})  // downcast_array! (macros.rs:5-16)
+        if (v->array.dtype != FQ_DT_BOOLEAN)
+            throw_internal(std::string("Cannot downcast_array from datatype:") + dtype_name(v->array.dtype) +
+                           " item to:BooleanArray");
+    if (l.array.len != r.array.len) throw_internal("Cannot perform bitwise operation on arrays of different length");
+    Column out = Column::device(FQ_DT_BOOLEAN, l.array.len, ctx.stream());
+    check_fq(fq_logic(op_, (const uint64_t *)l.array.dptr(), (const uint64_t *)r.array.dptr(), (uint64_t *)out.dptr(),
+                      l.array.len, ctx.stream()));
+    ColumnarValue v;
+    v.is_array = true;
+    v.array = out;
+    return v;
+}
+
+std::vector<DataValue> LogicFunction::accumulate_result() const {
+    throw_internal(std::string("Unsupported aggregate operation for function ") + logic_op_str(op_));
+}
+void LogicFunction::merge_state(const std::vector<DataValue> &) {
+    throw_internal(std::string("Unsupported aggregate operation for function ") + logic_op_str(op_));
+}
+DataValue LogicFunction::merge_result() const {
+    throw_internal(std::string("Unsupported aggregate operation for function ") + logic_op_str(op_));
+}
+
+// ---------------------------------------------------------------------------
 // factory (function_factory.rs:14-40)
 // ---------------------------------------------------------------------------
 FunctionRef function_factory(const std::string &name, std::vector<FunctionRef> args, const FactoryOptions &o) {
@@ -471,9 +510,10 @@ FunctionRef function_factory(const std::string &name, std::vector<FunctionRef> a
     else if (n == "min") agg = FQ_AGG_MIN;
     else if (n == "max") agg = FQ_AGG_MAX;
     else if (n == "sum") agg = FQ_AGG_SUM;
-    else if (n == "and" || n == "or")
-        throw_status(FQ_E_UNSUPPORTED, "logic function '" + n + "' (function_logic.rs) is outside the device hot path");
-    else throw_internal("Unsupported Function: " + name);
+    else if (n == "and" || n == "or") {
+        need(2);
+        return std::make_shared<LogicFunction>(n == "and" ? FQ_LOGIC_AND : FQ_LOGIC_OR, args[0], args[1]);
+    } else throw_internal("Unsupported Function: " + name);
     if (op >= 0) {
         need(2);
         return std::make_shared<ArithmeticFunction>(op, args[0], args[1]);

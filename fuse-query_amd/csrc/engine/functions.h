@@ -198,6 +198,38 @@ class ComparisonFunction : public Function {
     FunctionRef left_, right_;
 };
 
+// LogicFunction (function_logic.rs:17-94): and/or of two Boolean arrays
+class LogicFunction : public Function {
+   public:
+    LogicFunction(int32_t op, FunctionRef l, FunctionRef r) : op_(op), left_(std::move(l)), right_(std::move(r)) {}
+    std::string display() const override;
+    DataType return_type(const DataSchema &) const override { return FQ_DT_BOOLEAN; }
+    bool nullable(const DataSchema &) const override { return false; }
+    ColumnarValue eval(const DataBlock &b, ExecCtx &ctx) override;
+    void set_depth(size_t d) override { depth_ = d; }
+    void accumulate(const DataBlock &b, ExecCtx &ctx) override {
+        left_->accumulate(b, ctx);
+        right_->accumulate(b, ctx);
+    }
+    std::vector<DataValue> accumulate_result() const override;
+    void merge_state(const std::vector<DataValue> &) override;
+    DataValue merge_result() const override;
+    FunctionRef clone() const override {
+        auto f = std::make_shared<LogicFunction>(op_, left_->clone(), right_->clone());
+        f->depth_ = depth_;
+        return f;
+    }
+    void collect_aggregators(std::vector<AggregatorFunction *> &v) override {
+        left_->collect_aggregators(v);
+        right_->collect_aggregators(v);
+    }
+
+   private:
+    size_t depth_ = 0;
+    int32_t op_;  // FQ_LOGIC_AND / FQ_LOGIC_OR
+    FunctionRef left_, right_;
+};
+
 // AggregatorFunction (function_aggregator.rs:17-144)
 class AggregatorFunction : public Function {
    public:

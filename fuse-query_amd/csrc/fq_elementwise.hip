@@ -552,3 +552,69 @@ fq_status fq_compare(int32_t cmp, const fq_col *lhs, const fq_value *lhs_scalar,
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------
+// LogicFunction: word-wise and/or of two bitmaps (16-byte loads/stores)
+// ---------------------------------------------------------------------------
+namespace fqk {
+
+template <int OP>
+__global__ void __launch_bounds__(256)
+    logic_kernel(const uint64_t *__restrict__ l, const uint64_t *__restrict__ r, uint64_t *__restrict__ out,
+                 int64_t nwords, int64_t len) {
+    const int64_t T = (int64_t)gridDim.x * blockDim.x;
+    const int64_t npairs = nwords / 2;
+    typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+    const u64x2 *lv = reinterpret_cast<const u64x2 *>(l), *rv = reinterpret_cast<const u64x2 *>(r);
+    u64x2 *ov = reinterpret_cast<u64x2 *>(out);
+    const bool vec = ((((uintptr_t)l) | ((uintptr_t)r) | ((uintptr_t)out)) & 15u) == 0;
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    int64_t done = 0;
+    if (vec) {
+        for (int64_t p = g; p < npairs; p += T) {
+            const u64x2 a = __builtin_nontemporal_load(lv + p), b = __builtin_nontemporal_load(rv + p);
+            ov[p] = OP == FQ_LOGIC_AND ? (a & b) : (a | b);
+        }
+        done = npairs * 2;
+    }
+    for (int64_t w = done + g; w < nwords; w += T) {
+        uint64_t v = OP == FQ_LOGIC_AND ? (l[w] & r[w]) : (l[w] | r[w]);
+        if (w == nwords - 1 && (len & 63)) v &= (1ull << (len & 63)) - 1ull;
+        out[w] = v;
+    }
+    // (an even word count puts the last word in the vector part: the host
+    // clears its tail bits with logic_tail_kernel)
+}
+
+__global__ void logic_tail_kernel(uint64_t *out, int64_t nwords, int64_t len) {
+    out[nwords - 1] &= (1ull << (len & 63)) - 1ull;
+}
+
+}  // namespace fqk
+
+extern "C" fq_status fq_logic(int32_t op, const uint64_t *d_lhs, const uint64_t *d_rhs, uint64_t *d_out, int64_t len,
+                              void *stream) {
+    using namespace fqk;
+    if (op != FQ_LOGIC_AND && op != FQ_LOGIC_OR) return fqc::fail(FQ_E_INVALID, "fq_logic: bad op");
+    if (len < 0) return fqc::fail(FQ_E_INVALID, "fq_logic: negative length");
+    if (len == 0) return FQ_OK;
+    if (!d_lhs || !d_rhs || !d_out) return fqc::fail(FQ_E_INVALID, "fq_logic: NULL bitmap");
+    hipStream_t st = (hipStream_t)stream;
+    const int64_t nwords = (len + 63) / 64;
+    const int64_t cap = (int64_t)fqc::device_cu_count() * 2;
+    int64_t grid = (nwords / 2 + 255) / 256;
+    if (grid < 1) grid = 1;
+    if (grid > cap) grid = cap;
+    if (op == FQ_LOGIC_AND)
+        hipLaunchKernelGGL((logic_kernel<FQ_LOGIC_AND>), dim3((int)grid), dim3(256), 0, st, d_lhs, d_rhs, d_out, nwords, len);
+    else
+        hipLaunchKernelGGL((logic_kernel<FQ_LOGIC_OR>), dim3((int)grid), dim3(256), 0, st, d_lhs, d_rhs, d_out, nwords, len);
+    FQ_HIP_TRY(hipGetLastError());
+    const bool vec = ((((uintptr_t)d_lhs) | ((uintptr_t)d_rhs) | ((uintptr_t)d_out)) & 15u) == 0;
+    if (vec && (len & 63) && (nwords & 1) == 0) {  // last word written by the vector loop
+        hipLaunchKernelGGL(logic_tail_kernel, dim3(1), dim3(1), 0, st, d_out, nwords, len);
+        FQ_HIP_TRY(hipGetLastError());
+    }
+    return FQ_OK;
+}
+

@@ -190,6 +190,15 @@ def compare(cmp_sym, lhs, rhs, stream=None):
     return out
 
 
+def logic(op, lhs, rhs, stream=None):
+    """LogicFunction::eval: 'and' / 'or' of two Boolean DeviceColumns."""
+    require_gpu()
+    out = empty_column(lhs.len, abi.DT_BOOLEAN)
+    check(lib.fq_logic(0 if op == "and" else 1, C.c_void_p(lhs.ptr), C.c_void_p(rhs.ptr), C.c_void_p(out.ptr),
+                       lhs.len, _stream(stream)))
+    return out
+
+
 def filter_compact(col, bitmap, stream=None):
     """FilterTransform: keep rows whose bit is set, in order -> DeviceColumn."""
     require_gpu()

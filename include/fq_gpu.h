@@ -15,6 +15,7 @@
  *   fq_arith              data_array_arithmetic_op        src/datavalues/data_array_arithmetic.rs:14-55
  *   fq_compare            data_array_comparison_op        src/datavalues/data_array_comparison.rs:14-94
  *   fq_filter_compact     arrow filter_record_batch       src/transforms/transform_filter.rs:51
+ *   fq_logic              data_array_logic_op             src/datavalues/data_array_logic.rs:10-31
  *   fq_state_merge        AggregatorFunction::merge_state src/functions/function_aggregator.rs:106-139
  *
  * Conventions:
@@ -217,6 +218,18 @@ fq_status fq_arith(int32_t op, const fq_col *lhs, const fq_value *lhs_scalar, co
 fq_status fq_compare(int32_t cmp, const fq_col *lhs, const fq_value *lhs_scalar,
                      const fq_col *rhs, const fq_value *rhs_scalar, uint64_t *d_bitmap,
                      int64_t len, uint32_t *d_flag, void *stream);
+
+/* ---- LogicFunction::eval (function_logic.rs:47-53 -> data_array_logic.rs:10-31) ----
+ * out = lhs AND/OR rhs over two Boolean bitmaps of `len` rows (ceil(len/64)
+ * words each; bits past len are cleared in the output).  Both sides must be
+ * Boolean ARRAYS: the reference errors on a scalar side ("Cannot do
+ * data_array and, left:..., right:...") and on a non-Boolean array
+ * ("Cannot downcast_array from datatype:<T> item to:BooleanArray"); those
+ * checks are the caller's (engine/functions.cpp LogicFunction).          */
+#define FQ_LOGIC_AND 0
+#define FQ_LOGIC_OR 1
+fq_status fq_logic(int32_t op, const uint64_t *d_lhs, const uint64_t *d_rhs, uint64_t *d_out, int64_t len,
+                   void *stream);
 
 /* ---- FilterTransform: order-preserving compaction (arrow filter_record_batch) ----
  * Synchronises `stream`; *out_len receives the number of rows kept.          */

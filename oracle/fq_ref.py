@@ -327,6 +327,21 @@ def data_array_comparison_op(op, left, right):
     raise internal("Cannot do data_array %s, left:%s, right:%s" % (op, left.type, right.type))
 
 
+def data_array_logic_op(op, left, right):
+    """data_array_logic.rs:10-31: and/or of two Boolean ARRAYS (arrow
+    compute::and / or via array_boolean_op!, macros.rs:212-218)."""
+    if not (isinstance(left, Arr) and isinstance(right, Arr)):
+        raise internal("Cannot do data_array %s, left:%s, right:%s" % (op, left.type, right.type))
+    for a in (left, right):
+        if a.type != "Boolean":  # downcast_array! (macros.rs:5-16)
+            raise internal("Cannot downcast_array from datatype:%s item to:BooleanArray" % a.type)
+    if len(left) != len(right):
+        raise internal("Cannot perform bitwise operation on arrays of different length")
+    lv, rv = left.values, right.values
+    out = [(bool(a) and bool(b)) if op == "and" else (bool(a) or bool(b)) for a, b in zip(lv, rv)]
+    return Arr("Boolean", out)
+
+
 def _bcast(one, n):
     if one.type in NP:
         return Arr(one.type, np.repeat(one.values, n), None if one.valid is None else np.repeat(one.valid, n))
@@ -582,6 +597,35 @@ class Compare(Fn):
         return c
 
 
+class Logic(Fn):
+    """LogicFunction (function_logic.rs:17-94)."""
+    def __init__(self, op, left, right):
+        self.op, self.left, self.right = op, left, right
+
+    def display(self):
+        return "%s %s %s" % (self.left.display(), self.op, self.right.display())
+
+    def return_type(self, s):
+        return "Boolean"
+
+    def eval(self, b):
+        return data_array_logic_op(self.op, self.left.eval(b), self.right.eval(b))
+
+    def accumulate(self, b):
+        self.left.accumulate(b)
+        self.right.accumulate(b)
+
+    def _err(self, *a):
+        raise internal("Unsupported aggregate operation for function %s" % self.op)
+
+    accumulate_result = merge_state = merge_result = _err
+
+    def clone(self):
+        c = Logic(self.op, self.left.clone(), self.right.clone())
+        c.depth = self.depth
+        return c
+
+
 class Agg(Fn):
     def __init__(self, op, arg):
         self.op, self.arg = op, arg
@@ -637,6 +681,8 @@ def factory(name, args, modulo=True):
         return Arith(n, args[0], args[1])
     if n in CMP:
         return Compare(n, args[0], args[1])
+    if n in ("and", "or"):
+        return Logic(n, args[0], args[1])
     if n in AGG_DEBUG:
         return Agg(n, args[0])
     raise internal("Unsupported Function: %s" % name)

@@ -8,6 +8,7 @@ operator, expected outputs / error texts) from its Rust test sources:
   src/datavalues/data_array_aggregate_test.rs    min/max/sum over one array
   src/datavalues/data_value_aggregate_test.rs    scalar state merges
   src/datavalues/data_value_arithmetic_test.rs   scalar add
+  src/datavalues/data_array_logic_test.rs        and / or over Boolean arrays
 
 Only literal values are read (the XArray::from(vec![...]) and
 DataValue::X(Some(..)) literals of each table row); nothing is executed.
@@ -142,7 +143,7 @@ def field(body, name):
 
 
 OPS = {"Add": "+", "Sub": "-", "Mul": "*", "Div": "/", "Eq": "=", "Lt": "<", "LtEq": "<=", "Gt": ">",
-       "GtEq": ">=", "Min": "min", "Max": "max", "Sum": "sum", "Count": "count"}
+       "GtEq": ">=", "Min": "min", "Max": "max", "Sum": "sum", "Count": "count", "And": "and", "Or": "or"}
 
 
 def tests_in(path, struct):
@@ -192,6 +193,7 @@ def main():
         "array_aggregate": tests_in("src/datavalues/data_array_aggregate_test.rs", "ArrayTest"),
         "value_aggregate": tests_in("src/datavalues/data_value_aggregate_test.rs", "ScalarTest"),
         "value_arithmetic": tests_in("src/datavalues/data_value_arithmetic_test.rs", "ScalarTest"),
+        "array_logic": tests_in("src/datavalues/data_array_logic_test.rs", "ArrayTest"),
     }
     for k, v in data.items():
         if isinstance(v, list):

@@ -188,3 +188,8 @@ def test_group_by_plan_errors(eng):
     with pytest.raises(FQError) as ei:
         eng.explain("SELECT number, number+1, sum(number) FROM system.numbers_mt(10) GROUP BY number%3")
     assert str(ei.value) == "Error during plan: Projection references non-aggregate values"
+
+
+def test_explain_logic_predicate(eng):
+    txt = eng.explain("SELECT sum(number) FROM system.numbers_mt(80000) WHERE number > 1 AND number < 5")
+    assert "Filter: ((number > 1) AND (number < 5))" in txt

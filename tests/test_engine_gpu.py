@@ -268,3 +268,38 @@ def test_f64_division_within_one_ulp():
         assert ulp <= 1, (got, e, ulp)
         assert ulp == 0
 
+
+
+@pytest.mark.parametrize("where", [
+    ("number > 100 AND number % 7 = 3", "and"),
+    ("number < 1000 OR number % 97 = 0", "or"),
+    ("(number % 8 < 3 AND number > 10) OR number = 5", "nested"),
+])
+def test_logic_in_where_matches_oracle(where):
+    # LogicFunction (function_logic.rs) over device bitmaps; the aggregate
+    # consumes the combined bitmap as its predicate
+    import fq_ref as R
+    n = 1_000_000
+    sql_where, kind = where
+    r = q("SELECT count(number), sum(number), max(number), min(number) FROM system.numbers_mt(%d) WHERE %s"
+          % (n, sql_where))
+    N = R.E_field("number")
+    c = R.E_const
+    if kind == "and":
+        w = R.E_bin("and", R.E_bin(">", N, c(100)), R.E_bin("=", R.E_bin("%", N, c(7)), c(3)))
+    elif kind == "or":
+        w = R.E_bin("or", R.E_bin("<", N, c(1000)), R.E_bin("=", R.E_bin("%", N, c(97)), c(0)))
+    else:
+        w = R.E_bin("or", R.E_bin("and", R.E_bin("<", R.E_bin("%", N, c(8)), c(3)), R.E_bin(">", N, c(10))),
+                    R.E_bin("=", N, c(5)))
+    exp = R.aggregate_query(n, [R.E_fn("count", N), R.E_fn("sum", N), R.E_fn("max", N), R.E_fn("min", N)], where=w)
+    assert r.rows == [tuple(v.value for v in exp)]
+
+
+def test_logic_projection_and_errors():
+    r = q("SELECT number FROM system.numbers_mt(100) WHERE number > 3 AND number < 7")
+    assert sorted(r.rows) == [(4,), (5,), (6,)]
+    assert err("SELECT count(number) FROM system.numbers_mt(100) WHERE number > 3 AND number") == \
+        "Internal Error: Cannot downcast_array from datatype:UInt64 item to:BooleanArray"
+    assert err("SELECT count(number) FROM system.numbers_mt(100) WHERE number > 3 AND 1") == \
+        "Internal Error: Cannot do data_array and, left:Boolean, right:UInt64"

@@ -130,3 +130,25 @@ def test_golden_aggregate_on_gpu(t):
 
 def to_bits_of(st, op):
     return {abi.AGG_SUM: st.sum, abi.AGG_MAX: st.max, abi.AGG_MIN: st.min}[op]
+
+
+@pytest.mark.parametrize("t", GOLDEN["array_logic"], ids=ids(GOLDEN["array_logic"]))
+def test_golden_logic_on_gpu(t):
+    for i, (l, r) in enumerate(t["args"]):
+        L = ops.compare("=", ops.from_numpy(np.array(l["values"], np.uint64)), 1)
+        Rr = ops.compare("=", ops.from_numpy(np.array(r["values"], np.uint64)), 1)
+        got = ops.logic(t["op"], L, Rr)
+        assert same(got, t["expect"][i]), (i, got.to_numpy())
+
+
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 128, 129, 1000, 100_003])
+def test_logic_lengths(n):
+    rng = np.random.default_rng(n)
+    a, b = rng.random(n) < 0.5, rng.random(n) < 0.5
+    A = ops.compare("=", ops.from_numpy(a.astype(np.uint64)), 1)
+    B = ops.compare("=", ops.from_numpy(b.astype(np.uint64)), 1)
+    assert np.array_equal(ops.logic("and", A, B).to_numpy(), a & b)
+    assert np.array_equal(ops.logic("or", A, B).to_numpy(), a | b)
+    words = ops.logic("or", A, B).buf[: ((n + 63) // 64) * 8].cpu().numpy().view(np.uint64)
+    if n % 64:
+        assert int(words[-1]) >> (n % 64) == 0  # bits past len cleared

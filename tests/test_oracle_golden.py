@@ -110,10 +110,28 @@ def test_golden_value_ops(t):
             assert str(e) == t["error"][i]
 
 
+@pytest.mark.parametrize("t", GOLDEN["array_logic"], ids=ids(GOLDEN["array_logic"]))
+def test_golden_array_logic(t):
+    for i, (l, r) in enumerate(t["args"]):
+        got = R.data_array_logic_op(t["op"], lit(l), lit(r))
+        assert same_array(got, t["expect"][i]), (i, got.to_list())
+
+
+def test_function_logic_display_and_eval():
+    # function_logic_test.rs:28-80
+    b = R.Block({"a": R.Arr("Boolean", [True, True, True, False]), "b": R.Arr("Boolean", [True, False, True, True])})
+    f = R.to_function(R.E_bin("and", R.E_field("a"), R.E_field("b")))
+    assert f.display() == "a and b" and f.eval(b).to_list() == [True, False, True, False]
+    f = R.to_function(R.E_bin("or", R.E_field("a"), R.E_field("b")))
+    assert f.display() == "a or b" and f.eval(b).to_list() == [True, True, True, True]
+    with pytest.raises(R.RefError, match="Unsupported aggregate operation for function and"):
+        R.to_function(R.E_bin("and", R.E_field("a"), R.E_field("b"))).accumulate_result()
+
+
 def test_golden_fixture_covers_all_tables():
     n = {k: len(v) for k, v in GOLDEN.items() if isinstance(v, list)}
     assert n == {"array_arithmetic": 12, "array_comparison": 17, "array_aggregate": 3,
-                 "value_aggregate": 3, "value_arithmetic": 1}
+                 "value_aggregate": 3, "value_arithmetic": 1, "array_logic": 2}
 
 
 # ---- function_aggregator_test.rs:5-192 (partial/merge protocol) -----------
