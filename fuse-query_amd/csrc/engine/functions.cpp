@@ -24,13 +24,23 @@ std::string FusedChain::key() const {
 }
 
 std::string FusedPred::key() const {
-    FusedChain c;
-    c.column = column;
-    c.col_dtype = col_dtype;
-    c.expr = pred.lhs;
-    c.out_dtype = pred.lhs.out_dtype;
-    return c.key() + "?" + std::to_string(pred.cmp) + "," + std::to_string(pred.cmp_dtype) + "," +
-           std::to_string(pred.rhs_operand) + "," + std::to_string(pred.rhs_bits);
+    auto leaf = [this](const fq_expr &lhs, int32_t cmp, int32_t cdt, int32_t ro, uint64_t rb) {
+        FusedChain c;
+        c.column = column;
+        c.col_dtype = col_dtype;
+        c.expr = lhs;
+        c.out_dtype = lhs.out_dtype;
+        return c.key() + "?" + std::to_string(cmp) + "," + std::to_string(cdt) + "," + std::to_string(ro) + "," +
+               std::to_string(rb);
+    };
+    if (pred.kind != FQ_PRED_TREE) return leaf(pred.lhs, pred.cmp, pred.cmp_dtype, pred.rhs_operand, pred.rhs_bits);
+    std::string k = "T";
+    for (int i = 0; i < tree.n_prog; ++i) k += std::to_string(tree.prog[i]) + ",";
+    for (int i = 0; i < tree.n_leaves; ++i) {
+        const fq_pred_leaf &l = tree.leaves[i];
+        k += "[" + leaf(l.lhs, l.cmp, l.cmp_dtype, l.rhs_operand, l.rhs_bits) + "]";
+    }
+    return k;
 }
 
 // ---------------------------------------------------------------------------
@@ -399,7 +409,7 @@ fq_agg_state AggregatorFunction::summarize(const DataBlock &b, ExecCtx &ctx) {
     const bool chain = arg_->to_chain(s, fc);
     const bool pred_ok = !b.filter || (b.filter->to_pred(s, fp) && chain && fp.column == fc.column);
     if (chain && pred_ok) {
-        fq_agg_state st = run_scan(b.column_by_name(fc.column), R, b.filter ? &fp.pred : nullptr,
+        fq_agg_state st = run_scan(b.column_by_name(fc.column), R, b.filter ? fp.get() : nullptr,
                                    fc.expr.n_steps ? &fc.expr : nullptr, scan_mask(op_), ctx);
         st.blocks = k;
         return st;
@@ -481,6 +491,48 @@ void LogicFunction::merge_state(const std::vector<DataValue> &) {
 }
 DataValue LogicFunction::merge_result() const {
     throw_internal(std::string("Unsupported aggregate operation for function ") + logic_op_str(op_));
+}
+
+// An and/or tree of fusable comparisons over one column -> FQ_PRED_TREE
+// (postfix program over at most FQ_MAX_PRED_LEAVES leaves).
+static bool flatten_logic(const Function &f, const DataSchema &s, FusedPred &out, std::vector<FusedPred> &leaves,
+                          std::vector<int32_t> &prog) {
+    if (const auto *lf = dynamic_cast<const LogicFunction *>(&f)) {
+        if (!flatten_logic(lf->left(), s, out, leaves, prog) || !flatten_logic(lf->right(), s, out, leaves, prog))
+            return false;
+        prog.push_back(lf->op() == FQ_LOGIC_AND ? FQ_PRED_AND : FQ_PRED_OR);
+        return true;
+    }
+    FusedPred p;
+    if (!f.to_pred(s, p) || p.pred.kind != FQ_PRED_EXPR) return false;
+    if (leaves.size() >= FQ_MAX_PRED_LEAVES) return false;
+    if (!leaves.empty() && p.column != leaves[0].column) return false;
+    prog.push_back((int32_t)leaves.size());
+    leaves.push_back(p);
+    return true;
+}
+
+bool LogicFunction::to_pred(const DataSchema &s, FusedPred &p) const {
+    std::vector<FusedPred> leaves;
+    std::vector<int32_t> prog;
+    if (!flatten_logic(*this, s, p, leaves, prog) || leaves.empty()) return false;
+    p = FusedPred{};
+    p.column = leaves[0].column;
+    p.col_dtype = leaves[0].col_dtype;
+    p.pred.kind = FQ_PRED_TREE;
+    p.tree.n_leaves = (int32_t)leaves.size();
+    p.tree.n_prog = (int32_t)prog.size();
+    for (size_t i = 0; i < prog.size(); ++i) p.tree.prog[i] = prog[i];
+    for (size_t i = 0; i < leaves.size(); ++i) {
+        const fq_pred &q = leaves[i].pred;
+        fq_pred_leaf &l = p.tree.leaves[i];
+        l.cmp = q.cmp;
+        l.cmp_dtype = q.cmp_dtype;
+        l.rhs_operand = q.rhs_operand;
+        l.rhs_bits = q.rhs_bits;
+        l.lhs = q.lhs;
+    }
+    return true;
 }
 
 // ---------------------------------------------------------------------------
@@ -674,7 +726,7 @@ void AggFusion::add(AggregatorFunction *agg, const DataBlock &b) {
         g->col = b.column_by_name(fc.column);
         g->value = fc;
         g->has_pred = (bool)b.filter;
-        if (g->has_pred) g->pred = fp.pred;
+        if (g->has_pred) g->pred = fp;
         g->filter_keepalive = b.filter;
         const int64_t rows = g->col.len;
         g->block_rows = b.sub_block_rows > 0 ? b.sub_block_rows : (rows > 0 ? rows : 1);
@@ -704,7 +756,7 @@ void AggFusion::end_block() {
             fq_jit_stats js;
             if (fq_jit_get_stats(&js) == FQ_OK &&
                 (js.mode == FQ_JIT_ALWAYS || (js.mode == FQ_JIT_AUTO && c.len >= js.min_rows)))
-                check_fq(fq_jit_prepare(&c, g.block_rows, g.has_pred ? &g.pred : nullptr,
+                check_fq(fq_jit_prepare(&c, g.block_rows, g.has_pred ? g.pred.get() : nullptr,
                                         g.value.expr.n_steps ? &g.value.expr : nullptr, g.mask, nullptr));
         }
         {
@@ -712,7 +764,7 @@ void AggFusion::end_block() {
             // other pipes share this queue, so the event pair brackets this scan
             std::lock_guard<std::mutex> lk(*ctx_.res->launch_mu);
             if (prof) check_hip(hipEventRecord(e0, ctx_.stream()), "hipEventRecord");
-            check_fq(fq_aggregate(&c, g.block_rows, g.has_pred ? &g.pred : nullptr,
+            check_fq(fq_aggregate(&c, g.block_rows, g.has_pred ? g.pred.get() : nullptr,
                                   g.value.expr.n_steps ? &g.value.expr : nullptr, g.mask, (fq_agg_state *)dst,
                                   ctx_.res->ws, ctx_.res->ws_bytes, ctx_.stream()));
             if (prof) check_hip(hipEventRecord(e1, ctx_.stream()), "hipEventRecord");

@@ -23,12 +23,19 @@ struct FusedChain {
     std::string key() const;
 };
 
-// A ComparisonFunction expressed as fq_pred over one column.
+// A ComparisonFunction (or an and/or tree of them, FQ_PRED_TREE) expressed
+// as fq_pred over one column.
 struct FusedPred {
     std::string column;
     DataType col_dtype = FQ_DT_NULL;
     fq_pred pred{};
+    fq_pred_tree tree{};  // kind == FQ_PRED_TREE
     std::string key() const;
+    // the fq_pred to hand to the ABI (points pred.tree at this object's tree)
+    const fq_pred *get() {
+        pred.tree = pred.kind == FQ_PRED_TREE ? &tree : nullptr;
+        return &pred;
+    }
 };
 
 class Function;
@@ -223,6 +230,10 @@ class LogicFunction : public Function {
         left_->collect_aggregators(v);
         right_->collect_aggregators(v);
     }
+    bool to_pred(const DataSchema &s, FusedPred &p) const override;
+    int32_t op() const { return op_; }
+    const Function &left() const { return *left_; }
+    const Function &right() const { return *right_; }
 
    private:
     size_t depth_ = 0;
@@ -293,7 +304,7 @@ class AggFusion {
         Column col;
         FusedChain value;
         bool has_pred = false;
-        fq_pred pred{};
+        FusedPred pred;
         std::shared_ptr<Function> filter_keepalive;
         uint32_t mask = 0;
         int64_t block_rows = 0;

@@ -504,13 +504,13 @@ StreamRef GroupByPartialTransform::execute() {
             fq_group_table probe = shared_->desc;
             fq_col empty = c;
             empty.len = 0;
-            check_fq(fq_group_aggregate(&probe, &empty, has_pred ? &fp.pred : nullptr,
+            check_fq(fq_group_aggregate(&probe, &empty, has_pred ? fp.get() : nullptr,
                                         kc.expr.n_steps ? &kc.expr : nullptr, vals, ctx.stream()));
         }
         {
             std::lock_guard<std::mutex> lk(*ctx.res->launch_mu);
             if (prof) check_hip(hipEventRecord(e0, ctx.stream()), "hipEventRecord");
-            check_fq(fq_group_aggregate(&shared_->desc, &c, has_pred ? &fp.pred : nullptr,
+            check_fq(fq_group_aggregate(&shared_->desc, &c, has_pred ? fp.get() : nullptr,
                                         kc.expr.n_steps ? &kc.expr : nullptr, vals, ctx.stream()));
             if (prof) check_hip(hipEventRecord(e1, ctx.stream()), "hipEventRecord");
         }

@@ -69,6 +69,35 @@ __device__ __forceinline__ uint32_t process(const TIn (&x)[M], const int64_t (&i
                 if (!((w >> (idx[j] & 63)) & 1ull)) pass &= ~(1u << j);
             }
         }
+    } else if constexpr (PRED == FQ_PRED_TREE) {
+        // every leaf over every live row (arrow and/or evaluate both sides),
+        // then the tree through its truth table
+        uint32_t m[FQ_MAX_PRED_LEAVES] = {};
+#pragma unroll
+        for (int li = 0; li < FQ_MAX_PRED_LEAVES; ++li) {
+            if (li >= pred.n_leaves) break;
+            const KLeaf &lf = pred.leaves[li];
+            uint64_t l[M], r[M];
+#pragma unroll
+            for (int j = 0; j < M; ++j) l[j] = to_bits<TIn>(x[j]);
+            run_prog<M, TIn>(lf.lhs, x, l, live, acc.flags);
+            if (lf.rhs_operand == FQ_OPERAND_COLUMN) {
+#pragma unroll
+                for (int j = 0; j < M; ++j) r[j] = col_as<TIn>(lf.cmp_dtype, x[j], (live >> j) & 1u, acc.flags);
+            } else {
+#pragma unroll
+                for (int j = 0; j < M; ++j) r[j] = lf.rhs;
+            }
+            m[li] = cmp_mask<M>(lf.cmp, lf.cmp_dtype, l, r);
+        }
+        uint32_t t = 0;
+#pragma unroll
+        for (int j = 0; j < M; ++j) {
+            const uint32_t idxbits = ((m[0] >> j) & 1u) | (((m[1] >> j) & 1u) << 1) | (((m[2] >> j) & 1u) << 2) |
+                                     (((m[3] >> j) & 1u) << 3);
+            t |= ((pred.truth >> idxbits) & 1u) << j;
+        }
+        pass &= t;
     }
     V v[M];
     if constexpr (CHAIN) {
@@ -433,6 +462,56 @@ fq_status lower_pred(const fq_pred *pred, int32_t col_dtype, int64_t len, bool n
     } else if (out.kind == FQ_PRED_BITMAP) {
         if (need_data && !pred->bitmap && len > 0) return fqc::fail(FQ_E_INVALID, "fq_pred: NULL bitmap");
         out.bitmap = pred->bitmap;
+    } else if (out.kind == FQ_PRED_TREE) {
+        const fq_pred_tree *t = pred->tree;
+        if (!t) return fqc::fail(FQ_E_INVALID, "fq_pred: NULL tree");
+        if (t->n_leaves < 1 || t->n_leaves > FQ_MAX_PRED_LEAVES || t->n_prog < 1 ||
+            t->n_prog > 2 * FQ_MAX_PRED_LEAVES)
+            return fqc::fail(FQ_E_INVALID, "fq_pred_tree: leaf / program count out of range");
+        if (fqc::dtype_size(col_dtype) != 8)
+            return fqc::fail(FQ_E_UNSUPPORTED, "fused predicates need a 64-bit column");
+        out.n_leaves = t->n_leaves;
+        out.n_prog = t->n_prog;
+        for (int i = 0; i < t->n_leaves; ++i) {
+            const fq_pred_leaf &lf = t->leaves[i];
+            KLeaf &k = out.leaves[i];
+            int32_t ldt = col_dtype;
+            fq_status s = lower_expr(lf.lhs, col_dtype, k.lhs, ldt);
+            if (s != FQ_OK) return s;
+            if (!is_chain_dtype(lf.cmp_dtype))
+                return fqc::fail(FQ_E_UNSUPPORTED, "fused comparison type must be UInt64, Int64 or Float64");
+            s = push_cast(ldt, lf.cmp_dtype, k.lhs);
+            if (s != FQ_OK) return s;
+            if (lf.cmp < FQ_CMP_EQ || lf.cmp > FQ_CMP_GTEQ) return fqc::fail(FQ_E_INVALID, "fq_pred_leaf: bad cmp");
+            if (lf.rhs_operand == FQ_OPERAND_COLUMN && col_dtype == FQ_DT_FLOAT64 && lf.cmp_dtype != FQ_DT_FLOAT64)
+                return fqc::fail(FQ_E_INVALID, "fq_pred: Float64 column compared as integer");
+            k.cmp = lf.cmp;
+            k.cmp_dtype = lf.cmp_dtype;
+            k.rhs_operand = lf.rhs_operand;
+            k.rhs = lf.rhs_bits;
+        }
+        // validate the postfix program and tabulate it over the 2^n leaf outcomes
+        uint32_t truth = 0;
+        for (uint32_t combo = 0; combo < (1u << FQ_MAX_PRED_LEAVES); ++combo) {
+            bool st[2 * FQ_MAX_PRED_LEAVES];
+            int sp = 0;
+            for (int i = 0; i < t->n_prog; ++i) {
+                const int32_t tok = t->prog[i];
+                out.prog[i] = tok;
+                if (tok >= 0 && tok < t->n_leaves) {
+                    st[sp++] = (combo >> tok) & 1u;
+                } else if (tok == FQ_PRED_AND || tok == FQ_PRED_OR) {
+                    if (sp < 2) return fqc::fail(FQ_E_INVALID, "fq_pred_tree: malformed program");
+                    const bool b = st[--sp], a = st[--sp];
+                    st[sp++] = tok == FQ_PRED_AND ? (a && b) : (a || b);
+                } else {
+                    return fqc::fail(FQ_E_INVALID, "fq_pred_tree: bad program token");
+                }
+            }
+            if (sp != 1) return fqc::fail(FQ_E_INVALID, "fq_pred_tree: malformed program");
+            if (st[0]) truth |= 1u << combo;
+        }
+        out.truth = truth;
     } else if (out.kind != FQ_PRED_NONE) {
         return fqc::fail(FQ_E_INVALID, "fq_pred: bad kind");
     }
@@ -463,6 +542,9 @@ static fq_status dispatch_pred(const Launch &L) {
         case FQ_PRED_BITMAP: return launch_scan<TIn, V, FQ_PRED_BITMAP, CHAIN>(L);
         case FQ_PRED_EXPR:
             if constexpr (sizeof(TIn) == 8) return launch_scan<TIn, V, FQ_PRED_EXPR, CHAIN>(L);
+            return fqc::fail(FQ_E_UNSUPPORTED, "fused predicates need a 64-bit column");
+        case FQ_PRED_TREE:
+            if constexpr (sizeof(TIn) == 8) return launch_scan<TIn, V, FQ_PRED_TREE, CHAIN>(L);
             return fqc::fail(FQ_E_UNSUPPORTED, "fused predicates need a 64-bit column");
         default: return fqc::fail(FQ_E_INVALID, "fq_pred: bad kind");
     }

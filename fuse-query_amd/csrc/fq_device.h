@@ -58,6 +58,16 @@ struct KProg {
     KStep s[FQ_MAX_STEPS + 4];  // room for inserted casts
 };
 
+// one comparison of an and/or predicate tree (FQ_PRED_TREE)
+struct KLeaf {
+    int32_t cmp;
+    int32_t cmp_dtype;
+    int32_t rhs_operand;
+    int32_t pad;
+    uint64_t rhs;
+    KProg lhs;
+};
+
 struct KPred {
     int32_t kind;
     int32_t cmp;
@@ -66,6 +76,14 @@ struct KPred {
     uint64_t rhs;
     const uint64_t *bitmap;
     KProg lhs;
+    // FQ_PRED_TREE: the leaves and the tree as a truth table over the leaf
+    // results (bit i of `truth` = value for leaf bits i); `prog` is the
+    // postfix form the hipRTC generator turns into a boolean expression
+    int32_t n_leaves;
+    uint32_t truth;
+    int32_t n_prog;
+    int32_t prog[2 * FQ_MAX_PRED_LEAVES];
+    KLeaf leaves[FQ_MAX_PRED_LEAVES];
 };
 
 // Per-workgroup partial; same field order as fq_agg_state.

@@ -139,7 +139,18 @@ struct HostStep {
 struct HostConsts {
     uint64_t rhs;
     HostStep p[kSteps], v[kSteps];
+    uint64_t rl[FQ_MAX_PRED_LEAVES];  // FQ_PRED_TREE leaves
+    HostStep pl[FQ_MAX_PRED_LEAVES][kSteps];
 };
+
+template <typename HC>
+void pack_tree_consts(const KPred &pr, HC &hc) {
+    for (int l = 0; l < FQ_MAX_PRED_LEAVES; ++l) {
+        hc.rl[l] = pr.leaves[l].rhs;
+        for (int i = 0; i < kSteps; ++i)
+            hc.pl[l][i] = HostStep{pr.leaves[l].lhs.s[i].c, pr.leaves[l].lhs.s[i].magic, pr.leaves[l].lhs.s[i].shift};
+    }
+}
 
 struct Gen {
     const char *prefix = "v";
@@ -155,6 +166,39 @@ void pack_consts(const Launch &L, HostConsts &hc) {
         hc.p[i] = HostStep{L.pred.lhs.s[i].c, L.pred.lhs.s[i].magic, L.pred.lhs.s[i].shift};
         hc.v[i] = HostStep{L.val.s[i].c, L.val.s[i].magic, L.val.s[i].shift};
     }
+    pack_tree_consts(L.pred, hc);
+}
+
+// the predicate's part of a shape key
+void put_pred_key(const KPred &pr, std::string &k) {
+    auto put = [&k](int32_t v) { k.append(reinterpret_cast<const char *>(&v), sizeof v); };
+    auto prog = [&put](const KProg &p) {
+        put(p.n);
+        for (int i = 0; i < p.n; ++i) {
+            put(p.s[i].code);
+            put(p.s[i].operand);
+            put(p.s[i].reversed);
+            put(p.s[i].dtype);
+            put((int32_t)p.s[i].add);
+        }
+    };
+    put(pr.kind);
+    if (pr.kind == FQ_PRED_EXPR) {
+        put(pr.cmp);
+        put(pr.cmp_dtype);
+        put(pr.rhs_operand);
+        prog(pr.lhs);
+    } else if (pr.kind == FQ_PRED_TREE) {
+        put(pr.n_leaves);
+        put(pr.n_prog);
+        for (int i = 0; i < pr.n_prog; ++i) put(pr.prog[i]);
+        for (int l = 0; l < pr.n_leaves; ++l) {
+            put(pr.leaves[l].cmp);
+            put(pr.leaves[l].cmp_dtype);
+            put(pr.leaves[l].rhs_operand);
+            prog(pr.leaves[l].lhs);
+        }
+    }
 }
 
 // Binary shape key: everything the generated source depends on.
@@ -166,7 +210,7 @@ std::string shape_key(const Launch &L, int32_t tin, bool chain, int dev) {
     put(tin);
     put(L.vdtype);
     put((int32_t)L.mask);
-    put(L.pred.kind);
+    put_pred_key(L.pred, k);
     put(L.block_mode ? 1 : 0);
     put(chain ? 1 : 0);
     auto prog = [&put](const KProg &p) {
@@ -179,12 +223,6 @@ std::string shape_key(const Launch &L, int32_t tin, bool chain, int dev) {
             put((int32_t)p.s[i].add);
         }
     };
-    if (L.pred.kind == FQ_PRED_EXPR) {
-        put(L.pred.cmp);
-        put(L.pred.cmp_dtype);
-        put(L.pred.rhs_operand);
-        prog(L.pred.lhs);
-    }
     if (chain) prog(L.val);
     return k;
 }
@@ -300,7 +338,57 @@ template <typename T> __device__ __forceinline__ T vmin(T a, T b) { return b < a
 
 // Body of `bool fq_pred(TIn x, ...)`: the lowered predicate program on x,
 // then the comparison in cmp_dtype.
+bool emit_leaf(Gen &g, int32_t cmp, int32_t cmp_dtype, int32_t rhs_operand, const KProg &lhs, const std::string &rhs,
+               const char *prefix, int32_t tin, std::string &body, const std::string &result) {
+    const char *op = cmp_op(cmp);
+    if (!op) return false;
+    body += "    {\n    u64 a = " + x_bits(tin) + ";\n";
+    emit_prog(g, body, lhs, tin, prefix);
+    std::string r;
+    if (rhs_operand == FQ_OPERAND_COLUMN) r = col_as(g, body, tin, cmp_dtype);
+    else r = rhs;
+    body += "    const u64 r = " + r + ";\n";
+    if (cmp_dtype == FQ_DT_UINT64) body += "    " + result + " = a " + op + " r;\n";
+    else if (cmp_dtype == FQ_DT_INT64) body += "    " + result + " = (long long)a " + op + " (long long)r;\n";
+    else if (cmp_dtype == FQ_DT_FLOAT64)
+        body += "    " + result + " = __builtin_bit_cast(double, a) " + op + " __builtin_bit_cast(double, r);\n";
+    else
+        return false;
+    body += "    }\n";
+    return true;
+}
+
 bool emit_pred_body(Gen &g, const KPred &pr, int32_t tin, std::string &body) {
+    if (pr.kind == FQ_PRED_TREE) {
+        // every leaf evaluated (no short circuit: arrow and/or evaluate both
+        // sides, so either side's errors raise), then the postfix program
+        std::vector<std::string> names;
+        for (int l = 0; l < pr.n_leaves; ++l) {
+            const std::string b = "b" + std::to_string(l);
+            body += "    bool " + b + ";\n";
+            const std::string prefix = "pl[" + std::to_string(l) + "]";
+            if (!emit_leaf(g, pr.leaves[l].cmp, pr.leaves[l].cmp_dtype, pr.leaves[l].rhs_operand, pr.leaves[l].lhs,
+                           "c.rl[" + std::to_string(l) + "]", prefix.c_str(), tin, body, b))
+                return false;
+        }
+        std::vector<std::string> st;
+        for (int i = 0; i < pr.n_prog; ++i) {
+            const int32_t t = pr.prog[i];
+            if (t >= 0 && t < pr.n_leaves) {
+                st.push_back("b" + std::to_string(t));
+            } else {
+                if (st.size() < 2) return false;
+                const std::string r = st.back();
+                st.pop_back();
+                const std::string l = st.back();
+                st.pop_back();
+                st.push_back("(" + l + (t == FQ_PRED_AND ? " & " : " | ") + r + ")");
+            }
+        }
+        if (st.size() != 1) return false;
+        body += "    return " + st[0] + ";\n";
+        return true;
+    }
     const char *op = cmp_op(pr.cmp);
     if (!op) return false;
     body += "    u64 a = " + x_bits(tin) + ";\n";
@@ -341,15 +429,17 @@ bool gen_source(const Launch &L, int32_t tin, bool chain, Gen &g, std::string &s
     const int32_t pk = L.pred.kind;
 
     std::string pred_body, val_body;
-    if (pk == FQ_PRED_EXPR && !emit_pred_body(g, L.pred, tin, pred_body)) return false;
+    const bool expr_pred = pk == FQ_PRED_EXPR || pk == FQ_PRED_TREE;
+    if (expr_pred && !emit_pred_body(g, L.pred, tin, pred_body)) return false;
     emit_value_body(g, chain ? &L.val : nullptr, tin, L.vdtype, "v", "V", val_body);
 
     src = kCommon;
     src += "typedef " + std::string(TIn) + " TIn;\ntypedef " + V + " V;\n";
     src += "struct Step { u64 c, m, s; };\nstruct Consts { u64 rhs; Step p[" + std::to_string(kSteps) +
-           "], v[" + std::to_string(kSteps) + "]; };\n";
+           "], v[" + std::to_string(kSteps) + "]; u64 rl[" + std::to_string(FQ_MAX_PRED_LEAVES) + "]; Step pl[" +
+           std::to_string(FQ_MAX_PRED_LEAVES) + "][" + std::to_string(kSteps) + "]; };\n";
     src += "__device__ __forceinline__ bool fq_pred(TIn x, const Consts &c, u32 &flags, u32 live) {\n";
-    src += pk == FQ_PRED_EXPR ? pred_body : "    return true;\n";
+    src += expr_pred ? pred_body : "    return true;\n";
     src += "}\n";
     src += "__device__ __forceinline__ V fq_val(TIn x, const Consts &c, u32 &flags, u32 live) {\n" + val_body + "}\n";
     const uint32_t m = L.mask;
@@ -357,7 +447,7 @@ bool gen_source(const Launch &L, int32_t tin, bool chain, Gen &g, std::string &s
     src += "__device__ __forceinline__ u32 fq_acc(Acc &acc, TIn x, long long idx, u32 live, const Consts &c,\n"
            "                                      const u64 *__restrict__ bitmap) {\n"
            "    u32 pass = live;\n";
-    if (pk == FQ_PRED_EXPR) src += "    pass &= fq_pred(x, c, acc.flags, live) ? 1u : 0u;\n";
+    if (expr_pred) src += "    pass &= fq_pred(x, c, acc.flags, live) ? 1u : 0u;\n";
     else if (pk == FQ_PRED_BITMAP)
         src += "    if (live) pass &= (u32)((bitmap[idx >> 6] >> (idx & 63)) & 1ull);\n";
     src += "    (void)idx; (void)bitmap;\n    const V v = fq_val(x, c, acc.flags, pass);\n";
@@ -543,6 +633,8 @@ int lds_slots(int n_aggs) {
 struct HostGroupConsts {
     uint64_t rhs;
     HostStep p[kSteps], k[kSteps], v[FQ_MAX_GROUP_AGGS][kSteps];
+    uint64_t rl[FQ_MAX_PRED_LEAVES];
+    HostStep pl[FQ_MAX_PRED_LEAVES][kSteps];
 };
 
 void pack_group_consts(const GroupLaunch &G, HostGroupConsts &hc) {
@@ -553,6 +645,7 @@ void pack_group_consts(const GroupLaunch &G, HostGroupConsts &hc) {
         for (int a = 0; a < FQ_MAX_GROUP_AGGS; ++a)
             hc.v[a][i] = HostStep{G.vals[a].s[i].c, G.vals[a].s[i].magic, G.vals[a].s[i].shift};
     }
+    pack_tree_consts(G.pred, hc);
 }
 
 std::string group_shape_key(const GroupLaunch &G, int32_t tin, int dev) {
@@ -571,13 +664,7 @@ std::string group_shape_key(const GroupLaunch &G, int32_t tin, int dev) {
     put(dev);
     put(tin);
     put(G.key_dtype);
-    put(G.pred.kind);
-    if (G.pred.kind == FQ_PRED_EXPR) {
-        put(G.pred.cmp);
-        put(G.pred.cmp_dtype);
-        put(G.pred.rhs_operand);
-        prog(G.pred.lhs);
-    }
+    put_pred_key(G.pred, k);
     prog(G.key);
     put(G.n_aggs);
     for (int a = 0; a < G.n_aggs; ++a) {
@@ -616,7 +703,8 @@ bool gen_groupby_source(const GroupLaunch &G, int32_t tin, Gen &g, std::string &
     src += "typedef " + std::string(TIn) + " TIn;\n";
     src += "struct Step { u64 c, m, s; };\nstruct Consts { u64 rhs; Step p[" + std::to_string(kSteps) + "], k[" +
            std::to_string(kSteps) + "], v[" + std::to_string(FQ_MAX_GROUP_AGGS) + "][" + std::to_string(kSteps) +
-           "]; };\n";
+           "]; u64 rl[" + std::to_string(FQ_MAX_PRED_LEAVES) + "]; Step pl[" + std::to_string(FQ_MAX_PRED_LEAVES) +
+           "][" + std::to_string(kSteps) + "]; };\n";
     src += "struct Tab { u64 *keys; u64 *st[" + std::to_string(FQ_MAX_GROUP_AGGS) +
            "]; u32 *hdr; long long mask; int rmask; };\n";
     src += "#define EMPTY 0xffffffffffffffffull\n#define NA " + std::to_string(NA) + "\n#define S " +
@@ -672,7 +760,7 @@ __device__ long long ginsert(const Tab &t, u64 k) {
 )";
     // predicate, key and value functions
     std::string body;
-    if (G.pred.kind == FQ_PRED_EXPR) {
+    if (G.pred.kind == FQ_PRED_EXPR || G.pred.kind == FQ_PRED_TREE) {
         if (!emit_pred_body(g, G.pred, tin, body)) return false;
     } else {
         body = "    return true;\n";
@@ -708,7 +796,8 @@ __device__ long long ginsert(const Tab &t, u64 k) {
     row += " };\n";
     row += "__device__ __forceinline__ void fq_prep(TIn x, long long idx, const Consts &c,\n"
            "    const u64 *__restrict__ bitmap, u32 &flags, Row &r) {\n    r.pass = 1u;\n";
-    if (G.pred.kind == FQ_PRED_EXPR) row += "    r.pass = fq_pred(x, c, flags, 1u) ? 1u : 0u;\n";
+    if (G.pred.kind == FQ_PRED_EXPR || G.pred.kind == FQ_PRED_TREE)
+        row += "    r.pass = fq_pred(x, c, flags, 1u) ? 1u : 0u;\n";
     else if (G.pred.kind == FQ_PRED_BITMAP) row += "    r.pass = (u32)((bitmap[idx >> 6] >> (idx & 63)) & 1ull);\n";
     row += "    (void)idx; (void)bitmap;\n    r.k = fq_key(x, c, flags, r.pass);\n";
     for (int a = 0; a < NA; ++a)

@@ -6,7 +6,7 @@ both speak the same struct layout.
 """
 import ctypes as C
 
-FQ_ABI_VERSION = 1
+FQ_ABI_VERSION = 2
 
 # status (src/error.rs:10-22)
 FQ_OK = 0
@@ -68,10 +68,25 @@ class fq_expr(C.Structure):
                 ("steps", fq_step * MAX_STEPS)]
 
 
+MAX_PRED_LEAVES = 4
+PRED_TREE = 3
+PRED_AND, PRED_OR = 100, 101
+
+
+class fq_pred_leaf(C.Structure):
+    _fields_ = [("cmp", C.c_int32), ("cmp_dtype", C.c_int32), ("rhs_operand", C.c_int32),
+                ("reserved", C.c_int32), ("rhs_bits", C.c_uint64), ("lhs", fq_expr)]
+
+
+class fq_pred_tree(C.Structure):
+    _fields_ = [("n_leaves", C.c_int32), ("n_prog", C.c_int32), ("prog", C.c_int32 * (2 * MAX_PRED_LEAVES)),
+                ("leaves", fq_pred_leaf * MAX_PRED_LEAVES)]
+
+
 class fq_pred(C.Structure):
     _fields_ = [("kind", C.c_int32), ("cmp", C.c_int32), ("cmp_dtype", C.c_int32),
                 ("rhs_operand", C.c_int32), ("rhs_bits", C.c_uint64), ("lhs", fq_expr),
-                ("bitmap", C.c_void_p)]
+                ("bitmap", C.c_void_p), ("tree", C.POINTER(fq_pred_tree))]
 
 
 class fq_agg_state(C.Structure):

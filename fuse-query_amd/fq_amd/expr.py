@@ -8,6 +8,7 @@ follow equal_coercion (:92-98).  Constants are typed like the SQL planner
 types literals (src/planners/plan_parser.rs:216-229): int >= 0 -> UInt64,
 int < 0 -> Int64, float -> Float64; or pass (value, "Int8") explicitly.
 """
+import ctypes as C
 import struct
 
 from . import abi
@@ -129,3 +130,25 @@ def predicate(col_dtype, lhs_steps, cmp_sym, rhs, flipped=False):
     if p.rhs_operand == abi.OPERAND_CONST:
         p.rhs_bits = to_bits(val, cdt)
     return p
+
+
+def pred_tree(col_dtype, leaves, prog):
+    """and/or predicate tree (FQ_PRED_TREE): leaves = [(lhs_steps, cmp_sym,
+    rhs)], prog = postfix tokens: leaf indices and "and" / "or"."""
+    t = abi.fq_pred_tree()
+    if not 1 <= len(leaves) <= abi.MAX_PRED_LEAVES:
+        raise ValueError("1..%d leaves" % abi.MAX_PRED_LEAVES)
+    t.n_leaves = len(leaves)
+    for i, (steps, cmp_sym, rhs) in enumerate(leaves):
+        p = predicate(col_dtype, steps, cmp_sym, rhs)
+        lf = t.leaves[i]
+        lf.cmp, lf.cmp_dtype, lf.rhs_operand, lf.rhs_bits, lf.lhs = p.cmp, p.cmp_dtype, p.rhs_operand, p.rhs_bits, p.lhs
+    toks = [(abi.PRED_AND if x == "and" else abi.PRED_OR) if isinstance(x, str) else int(x) for x in prog]
+    t.n_prog = len(toks)
+    for i, x in enumerate(toks):
+        t.prog[i] = x
+    pr = abi.fq_pred()
+    pr.kind = abi.PRED_TREE
+    pr.tree = C.pointer(t)
+    pr._tree = t  # keep the tree alive with the predicate
+    return pr

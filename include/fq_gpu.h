@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define FQ_ABI_VERSION 1
+#define FQ_ABI_VERSION 2
 
 /* ---- status (src/error.rs:10-22 FuseQueryError{SQLParse,Plan,Internal}) ---- */
 typedef int32_t fq_status;
@@ -138,6 +138,30 @@ typedef struct fq_expr {
 #define FQ_PRED_NONE 0
 #define FQ_PRED_EXPR 1   /* cmp(lhs(x), rhs) with rhs a constant or x            */
 #define FQ_PRED_BITMAP 2 /* precomputed Boolean column (from fq_compare)          */
+#define FQ_PRED_TREE 3   /* and/or of up to FQ_MAX_PRED_LEAVES comparisons        */
+
+/* One comparison leaf of an and/or predicate tree: cmp(lhs(x), rhs). */
+typedef struct fq_pred_leaf {
+    int32_t cmp, cmp_dtype, rhs_operand, reserved;
+    uint64_t rhs_bits;
+    fq_expr lhs;
+} fq_pred_leaf;
+
+/* LogicFunction trees (function_logic.rs) over comparisons of one column, as
+ * a postfix program: prog[i] < FQ_MAX_PRED_LEAVES pushes leaf prog[i],
+ * FQ_PRED_AND / FQ_PRED_OR pop two and push their and/or.  Both sides are
+ * always evaluated (arrow and/or work on whole arrays), so an error in
+ * either raises.                                                          */
+#define FQ_MAX_PRED_LEAVES 4
+#define FQ_PRED_AND 100
+#define FQ_PRED_OR 101
+typedef struct fq_pred_tree {
+    int32_t n_leaves;
+    int32_t n_prog;
+    int32_t prog[2 * FQ_MAX_PRED_LEAVES];
+    fq_pred_leaf leaves[FQ_MAX_PRED_LEAVES];
+} fq_pred_tree;
+
 typedef struct fq_pred {
     int32_t kind;
     int32_t cmp;         /* FQ_CMP_*  (already flipped for scalar-array forms)   */
@@ -146,6 +170,7 @@ typedef struct fq_pred {
     uint64_t rhs_bits;   /* constant in cmp_dtype                                */
     fq_expr lhs;         /* lhs.out_dtype must equal cmp_dtype                   */
     const uint64_t *bitmap; /* device, kind == FQ_PRED_BITMAP                    */
+    const fq_pred_tree *tree; /* host, kind == FQ_PRED_TREE (read during the call) */
 } fq_pred;
 
 /*

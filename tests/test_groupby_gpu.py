@@ -264,3 +264,12 @@ def test_sql_group_by_errors(eng):
     with pytest.raises(Exception) as ei:
         eng.execute("SELECT number, number+1, sum(number) FROM system.numbers_mt(10) GROUP BY number%3")
     assert "Projection references non-aggregate values" in str(ei.value)
+
+
+def test_sql_group_by_with_logic_predicate(eng):
+    total = 1_000_000
+    r = eng.execute("SELECT number%%4, count(number), max(number) FROM system.numbers_mt(%d) "
+                    "WHERE number%%8 < 3 AND number > 100 GROUP BY number%%4" % total)
+    w = R.E_bin("and", R.E_bin("<", R.E_bin("%", N, _c(8)), _c(3)), R.E_bin(">", N, _c(100)))
+    exp = R.group_by_query(total, R.E_bin("%", N, _c(4)), [R.E_fn("count", N), R.E_fn("max", N)], where=w)
+    assert r.rows == exp

@@ -117,3 +117,18 @@ def test_groupby_shapes_compile(name, dt, key_steps, aggs, kdt):
         return
     pred = predicate(dt, [("%", 8)], "<", 3) if dt == U64 else None
     ops.group_compile_check(dt, spec, key=key, values=values, pred=pred, key_dtype=kdt)
+
+
+def test_predicate_tree_shapes_compile():
+    from fq_amd.expr import pred_tree
+    t = pred_tree(U64, [([("%", 8)], "<", 3), ([], ">", 1000), ([("%", 97)], "=", 0)], [0, 1, "and", 2, "or"])
+    value, _ = chain(U64, [("+", 1)])
+    assert ops.jit_prepare(U64, pred=t, value=value, mask=abi.AGG_MAX | abi.AGG_COUNT)
+    assert ops.jit_prepare(U64, pred=t, value=value, mask=ALL, block_rows=10000)  # block mode
+    tf = pred_tree(F64, [([("*", 2.0)], ">=", 1.5), ([], "<", COL)], [0, 1, "or"])
+    assert ops.jit_prepare(F64, pred=tf, mask=ALL)
+    ops.group_compile_check(U64, [(abi.AGG_COUNT, U64)], key=chain(U64, [("%", 10)])[0], pred=t)
+    bad = pred_tree(U64, [([], ">", 1), ([], "<", 5)], [0, 1, "and"])
+    bad._tree.prog[2] = 0  # no operator: two values left on the stack
+    with pytest.raises(ops.FQError):
+        ops.jit_prepare(U64, pred=bad, mask=ALL)

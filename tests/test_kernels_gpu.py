@@ -370,3 +370,44 @@ def test_block_mode_vector_and_scalar_paths(block_rows, n, offset):
     for pred in (predicate(abi.DT_UINT64, [("%", 8)], "<", 3),     # every block keeps rows
                  predicate(abi.DT_UINT64, [], "<", 5 + block_rows)):  # only the first block does
         check_against_oracle(h, abi.DT_UINT64, block_rows, pred=pred, value=value, gpu_col=col)
+
+
+TREES = [
+    ("and", [([("%", 8)], "<", 3), ([], ">", 1000)], [0, 1, "and"]),
+    ("or", [([], "<", 5000), ([("%", 97)], "=", 0)], [0, 1, "or"]),
+    ("nested", [([("%", 8)], "<", 3), ([], ">", 10), ([], "=", 5), ([("/", 3)], ">=", 2)],
+     [0, 1, "and", 2, "or", 3, "and"]),
+]
+
+
+@pytest.mark.parametrize("name,leaves,prog", TREES, ids=[t[0] for t in TREES])
+def test_predicate_tree_scan_matches_numpy(name, leaves, prog, jit_mode):
+    """FQ_PRED_TREE (LogicFunction over comparisons) in the fused scan,
+    interpreted (truth table) and specialised (boolean expression)."""
+    from fq_amd.expr import pred_tree
+    n = 1_000_003
+    x = np.arange(3, 3 + n, dtype=np.uint64)
+    col = ops.from_numpy(x)
+    pred = pred_tree(abi.DT_UINT64, leaves, prog)
+    value, _ = chain(abi.DT_UINT64, [("+", 1)])
+    masks = []
+    for steps, cmp, rhs in leaves:
+        v = x.copy()
+        for sym, k in steps:
+            v = v % np.uint64(k) if sym == "%" else v // np.uint64(k)
+        masks.append({"<": v < rhs, ">": v > rhs, "=": v == rhs, ">=": v >= rhs}[cmp])
+    st = []
+    for t in prog:
+        if isinstance(t, str):
+            b, a = st.pop(), st.pop()
+            st.append(a & b if t == "and" else a | b)
+        else:
+            st.append(masks[t])
+    m = st[0]
+    y = (x + np.uint64(1))[m]
+    s = ops.aggregate(col, 0, pred, value, ALL)  # one block
+    assert s.count == int(m.sum())
+    assert s.sum == int(y.sum(dtype=np.uint64)) and s.max == int(y.max()) and s.min == int(y.min())
+    # many reference blocks: flat for max/count, block mode for sum
+    s2 = ops.aggregate(col, 10000, pred, value, abi.AGG_MAX | abi.AGG_COUNT)
+    assert s2.count == int(m.sum()) and s2.max == int(y.max())

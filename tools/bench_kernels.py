@@ -131,6 +131,10 @@ def main():
     rec("aggregate C4 shape (specialised)", "C4: max(number+1) WHERE (number%8)<3", ms, 8 * n)
     ms = timed(lambda: agg(a, pred=p, value=v, mask=abi.AGG_SUM), args.reps)
     rec("aggregate filtered sum (block mode)", "sum(number+1) WHERE (number%8)<3", ms, 8 * n)
+    from fq_amd.expr import pred_tree
+    tp = pred_tree(abi.DT_UINT64, [([("%", 8)], "<", 3), ([], ">", 1000)], [0, 1, "and"])
+    ms = timed(lambda: agg(a, pred=tp, value=v, mask=abi.AGG_MAX | abi.AGG_COUNT), args.reps)
+    rec("aggregate AND-tree predicate", "max(number+1) WHERE number%8<3 AND number>1000", ms, 8 * n)
     vf, _ = chain(abi.DT_UINT64, [("*", 1.5), ("+", 0.25)])
     ms = timed(lambda: agg(a, value=vf), args.reps)
     rec("aggregate f64 chain", "sum/max/min(number*1.5+0.25)", ms, 8 * n)
