@@ -205,7 +205,7 @@ class ComparisonFunction : public Function {
     FunctionRef left_, right_;
 };
 
-// LogicFunction (function_logic.rs:17-94): and/or of two Boolean arrays
+// LogicFunction (function_logic.rs:17-87): and/or of two Boolean arrays
 class LogicFunction : public Function {
    public:
     LogicFunction(int32_t op, FunctionRef l, FunctionRef r) : op_(op), left_(std::move(l)), right_(std::move(r)) {}

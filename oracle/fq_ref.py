@@ -598,7 +598,7 @@ class Compare(Fn):
 
 
 class Logic(Fn):
-    """LogicFunction (function_logic.rs:17-94)."""
+    """LogicFunction (function_logic.rs:17-87)."""
     def __init__(self, op, left, right):
         self.op, self.left, self.right = op, left, right
 
