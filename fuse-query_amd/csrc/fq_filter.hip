@@ -2,14 +2,18 @@
 // src/transforms/transform_filter.rs:51): keep the rows whose predicate bit
 // is set, preserving order.
 //
-// Three passes over tiles of 256 bitmap words (16,384 rows):
-//   count   one workgroup per tile, popcount of its 256 words -> counts[tile]
-//   scan    one workgroup, exclusive scan of the tile counts (+ total)
-//   scatter one workgroup per tile: LDS scan of its word popcounts, then each
-//           wave walks 64 words, 8 at a time; lane l moves row 64w+l to
-//           base + word_offset + popcount(word & lanemask_lt(l)).
-// Reads and writes are contiguous per wave; the bitmap is read twice
-// (1/64 of a u64 column's bytes each time).
+// Three passes over tiles of 256 bitmap words (16,384 rows), in groups of 16:
+//   count   one workgroup per group: popcounts of its tiles -> each tile's
+//           exclusive prefix inside the group, and the group's total
+//   scan    one workgroup: exclusive scan of the group totals
+//   scatter one workgroup per tile, LDS scan of its word popcounts, then:
+//           8-byte aligned columns: two 8,192-row rounds, each loading row
+//           pairs with 16-byte loads, dropping kept rows into an LDS stage
+//           at their output offset and writing the round's contiguous output
+//           range with aligned 16-byte stores;
+//           other widths: each wave walks 64 words, 8 at a time; lane l
+//           moves row 64w+l to base + word_offset + popcount(word & lt(l)).
+// The bitmap is read twice (1/64 of a u64 column's bytes each time).
 #include <hip/hip_runtime.h>
 
 #include "fq_common.h"
@@ -18,7 +22,6 @@
 namespace fqk {
 
 constexpr int kTileWords = 256;
-constexpr int kScanThreads = 1024;
 
 __device__ __forceinline__ uint64_t word_at(const uint64_t *bm, int64_t w, int64_t nwords, int64_t n) {
     if (w >= nwords) return 0;
@@ -28,76 +31,115 @@ __device__ __forceinline__ uint64_t word_at(const uint64_t *bm, int64_t w, int64
     return v;
 }
 
+// count: workgroup g covers the kGroupTiles tiles of group g (wave w: tiles
+// 4w..4w+3 of the group, all 16 word loads of a lane in flight together);
+// writes each tile's exclusive prefix within the group -> intra[tile] and
+// the group's total -> gpre[g].
+constexpr int kGroupTiles = 16;
+constexpr int kWaveTiles = kGroupTiles / (kTileWords / kWave);
+
 __global__ void __launch_bounds__(kTileWords)
-    compact_count_kernel(const uint64_t *__restrict__ bm, int64_t n, uint64_t *__restrict__ counts) {
+    compact_count_kernel(const uint64_t *__restrict__ bm, int64_t n, int64_t ntiles, uint64_t *__restrict__ intra,
+                         uint64_t *__restrict__ gpre) {
     const int64_t nwords = (n + 63) / 64;
-    const int64_t w = (int64_t)blockIdx.x * kTileWords + threadIdx.x;
-    uint64_t c = __popcll(word_at(bm, w, nwords, n));
-#pragma unroll
-    for (int off = kWave / 2; off > 0; off >>= 1) c += shfl_xor64(c, off);
-    __shared__ uint64_t s[kTileWords / kWave];
-    if ((threadIdx.x & (kWave - 1)) == 0) s[threadIdx.x / kWave] = c;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint64_t t = 0;
-#pragma unroll
-        for (int i = 0; i < kTileWords / kWave; ++i) t += s[i];
-        counts[blockIdx.x] = t;
-    }
-}
-
-// exclusive scan of counts[0..ntiles) in place; counts[ntiles] = total.
-// One workgroup of 16 waves; each wave owns a contiguous segment and walks it
-// 64 entries at a time (coalesced loads, wave scan by shuffles), twice: once
-// for its total, once to write prefixes after the 16 totals are scanned.
-__device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v, int lane) {
-#pragma unroll
-    for (int off = 1; off < kWave; off <<= 1) {
-        const uint64_t u = shfl_up64(v, off);
-        if (lane >= off) v += u;
-    }
-    return v;
-}
-
-__global__ void __launch_bounds__(kScanThreads) compact_scan_kernel(uint64_t *counts, int64_t ntiles) {
-    constexpr int W = kScanThreads / kWave;
     const int lane = threadIdx.x & (kWave - 1);
     const int wave = threadIdx.x / kWave;
-    const int64_t seg = (ntiles + W - 1) / W;
-    const int64_t b = (int64_t)wave * seg;
-    const int64_t e = (b + seg < ntiles) ? b + seg : ntiles;
-    uint64_t sum = 0;
-    for (int64_t i = b + lane; i < e; i += kWave) sum += counts[i];
+    const int64_t t0 = (int64_t)blockIdx.x * kGroupTiles + wave * kWaveTiles;
+    uint64_t wd[kWaveTiles][kTileWords / kWave];
 #pragma unroll
-    for (int off = kWave / 2; off > 0; off >>= 1) sum += shfl_xor64(sum, off);
-    __shared__ uint64_t s_tot[W + 1];
-    if (lane == 0) s_tot[wave] = sum;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint64_t run = 0;
-        for (int w = 0; w < W; ++w) {
-            const uint64_t t = s_tot[w];
-            s_tot[w] = run;
-            run += t;
+    for (int k = 0; k < kWaveTiles; ++k)
+#pragma unroll
+        for (int j = 0; j < kTileWords / kWave; ++j)
+            wd[k][j] = bm[min((t0 + k) * kTileWords + j * kWave + lane, nwords - 1)];  // all in flight
+#pragma unroll
+    for (int k = 0; k < kWaveTiles; ++k)
+#pragma unroll
+        for (int j = 0; j < kTileWords / kWave; ++j) {
+            const int64_t w = (t0 + k) * kTileWords + j * kWave + lane;
+            const int64_t rows = n - w * 64;
+            if (rows <= 0) wd[k][j] = 0;
+            else if (rows < 64) wd[k][j] &= (1ull << rows) - 1ull;  // ignore bits past len
         }
-        s_tot[W] = run;
+    __shared__ uint64_t s_c[kGroupTiles];
+#pragma unroll
+    for (int k = 0; k < kWaveTiles; ++k) {
+        uint64_t c = 0;
+#pragma unroll
+        for (int j = 0; j < kTileWords / kWave; ++j) c += __popcll(wd[k][j]);
+#pragma unroll
+        for (int off = kWave / 2; off > 0; off >>= 1) c += shfl_xor64(c, off);
+        if (lane == 0) s_c[wave * kWaveTiles + k] = c;
     }
     __syncthreads();
-    uint64_t run = s_tot[wave];
-    for (int64_t i0 = b; i0 < e; i0 += kWave) {
-        const int64_t i = i0 + lane;
-        const uint64_t v = i < e ? counts[i] : 0;
-        const uint64_t incl = wave_incl_scan(v, lane);
-        if (i < e) counts[i] = run + incl - v;
-        run += shfl64(incl, kWave - 1);
+    const int t = threadIdx.x;
+    if (t < kGroupTiles) {
+        uint64_t pre = 0;
+        for (int i = 0; i < t; ++i) pre += s_c[i];
+        const int64_t tile = (int64_t)blockIdx.x * kGroupTiles + t;
+        if (tile < ntiles) intra[tile] = pre;
+        if (t == kGroupTiles - 1) gpre[blockIdx.x] = pre + s_c[t];
     }
-    if (threadIdx.x == 0) counts[ntiles] = s_tot[W];
+}
+
+// exclusive scan of gpre[0..m) in place, gpre[m] = total.  One workgroup;
+// the array is taken 16,384 entries per round, 16 consecutive entries per
+// thread loaded together (indices clamped, values masked), so a round costs
+// one memory round trip.
+constexpr int kScanThreads = 1024;
+constexpr int kScanPer = 16;
+
+__global__ void __launch_bounds__(kScanThreads) compact_scan_kernel(uint64_t *gpre, int64_t m) {
+    constexpr int W = kScanThreads / kWave;
+    const int t = threadIdx.x;
+    const int lane = t & (kWave - 1);
+    const int wave = t / kWave;
+    __shared__ uint64_t s_w[W];
+    uint64_t run = 0;  // uniform: total of the earlier rounds
+    for (int64_t r0 = 0; r0 < m; r0 += (int64_t)kScanThreads * kScanPer) {
+        const int64_t i0 = r0 + (int64_t)t * kScanPer;
+        uint64_t v[kScanPer];
+#pragma unroll
+        for (int k = 0; k < kScanPer; ++k) v[k] = gpre[i0 + k < m ? i0 + k : m - 1];
+        uint64_t tot = 0;
+#pragma unroll
+        for (int k = 0; k < kScanPer; ++k) {
+            if (i0 + k >= m) v[k] = 0;
+            tot += v[k];
+        }
+        uint64_t incl = tot;
+#pragma unroll
+        for (int off = 1; off < kWave; off <<= 1) {
+            const uint64_t u = shfl_up64(incl, off);
+            if (lane >= off) incl += u;
+        }
+        if (lane == kWave - 1) s_w[wave] = incl;
+        __syncthreads();
+        uint64_t wbase = 0, rtot = 0;
+        for (int w = 0; w < W; ++w) {
+            const uint64_t x = s_w[w];
+            if (w < wave) wbase += x;
+            rtot += x;
+        }
+        uint64_t p = run + wbase + incl - tot;
+#pragma unroll
+        for (int k = 0; k < kScanPer; ++k) {
+            if (i0 + k < m) gpre[i0 + k] = p;
+            p += v[k];
+        }
+        run += rtot;
+        __syncthreads();  // s_w reused by the next round
+    }
+    if (t == 0) gpre[m] = run;
+}
+
+__device__ __forceinline__ uint64_t tile_base(const uint64_t *intra, const uint64_t *gpre, int64_t tile) {
+    return gpre[tile / kGroupTiles] + intra[tile];
 }
 
 template <typename T>
 __global__ void __launch_bounds__(kTileWords)
     compact_scatter_kernel(const T *__restrict__ in, const uint64_t *__restrict__ bm, int64_t n,
-                           const uint64_t *__restrict__ offsets, T *__restrict__ out) {
+                           const uint64_t *__restrict__ intra, const uint64_t *__restrict__ gpre, T *__restrict__ out) {
     const int64_t nwords = (n + 63) / 64;
     const int64_t w0 = (int64_t)blockIdx.x * kTileWords;
     __shared__ uint64_t s_word[kTileWords];
@@ -122,7 +164,7 @@ __global__ void __launch_bounds__(kTileWords)
     for (int i = 0; i < wave; ++i) wave_base += s_wsum[i];
     s_off[t] = wave_base + incl - c;
     __syncthreads();
-    const uint64_t base = offsets[blockIdx.x];
+    const uint64_t base = tile_base(intra, gpre, blockIdx.x);
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     // 8 words per step: all loads of the step are issued before the first
     // store (8 rows per lane in flight); empty words are skipped (uniform).
@@ -157,7 +199,7 @@ typedef unsigned long long u64x2_t __attribute__((ext_vector_type(2)));
 template <typename T>
 __global__ void __launch_bounds__(kTileWords)
     compact_scatter_vec_kernel(const T *__restrict__ in, const uint64_t *__restrict__ bm, int64_t n,
-                               const uint64_t *__restrict__ offsets, T *__restrict__ out) {
+                               const uint64_t *__restrict__ intra, const uint64_t *__restrict__ gpre, T *__restrict__ out) {
     static_assert(sizeof(T) == 8, "8-byte rows");
     const int64_t nwords = (n + 63) / 64;
     const int64_t w0 = (int64_t)blockIdx.x * kTileWords;
@@ -182,7 +224,7 @@ __global__ void __launch_bounds__(kTileWords)
     for (int i = 0; i < wave; ++i) wave_base += s_wsum[i];
     s_off[t] = wave_base + incl - c;
     __syncthreads();
-    const uint64_t base = offsets[blockIdx.x];
+    const uint64_t base = tile_base(intra, gpre, blockIdx.x);
     const int half = lane >> 5;        // which word of the pair
     const int bl = (lane & 31) * 2;    // bit of this lane's first row in that word
     const uint64_t m_lt = bl == 0 ? 0ull : (~0ull >> (64 - bl));
@@ -218,6 +260,98 @@ __global__ void __launch_bounds__(kTileWords)
     }
 }
 
+// 8-byte columns, input and output 16-byte aligned: the tile is compacted in
+// two 8,192-row rounds through LDS (64 KB stage, 2 workgroups per CU).  Each thread loads 8 row pairs with
+// 16-byte loads (consecutive threads, consecutive pairs), drops the kept rows
+// into a 32 KB LDS stage at their offset within the round, and the
+// workgroup then writes the round's contiguous output range as aligned
+// 16-byte stores (8-byte stores only at its two ends).
+constexpr int kRoundWords = 128;
+constexpr int kRoundPairs = kRoundWords * 32;
+
+template <typename T>
+__global__ void __launch_bounds__(kTileWords)
+    compact_scatter_lds_kernel(const T *__restrict__ in, const uint64_t *__restrict__ bm, int64_t n,
+                               const uint64_t *__restrict__ intra, const uint64_t *__restrict__ gpre, T *__restrict__ out) {
+    static_assert(sizeof(T) == 8, "8-byte rows");
+    const int64_t nwords = (n + 63) / 64;
+    const int64_t tile = blockIdx.x;
+    const int64_t w0 = tile * kTileWords;
+    __shared__ uint64_t s_word[kTileWords];
+    __shared__ uint32_t s_off[kTileWords + 1];
+    __shared__ uint32_t s_wsum[kTileWords / kWave];
+    __shared__ uint64_t s_stage[kRoundPairs * 2];
+    const int t = threadIdx.x;
+    const int lane = t & (kWave - 1);
+    const int wave = t / kWave;
+    const uint64_t word = word_at(bm, w0 + t, nwords, n);
+    s_word[t] = word;
+    uint32_t c = (uint32_t)__popcll(word);
+    uint32_t incl = c;
+#pragma unroll
+    for (int off = 1; off < kWave; off <<= 1) {
+        const uint32_t v = (uint32_t)__shfl_up((int)incl, off, kWave);
+        if (lane >= off) incl += v;
+    }
+    if (lane == kWave - 1) s_wsum[wave] = incl;
+    __syncthreads();
+    uint32_t wave_base = 0;
+    for (int i = 0; i < wave; ++i) wave_base += s_wsum[i];
+    s_off[t] = wave_base + incl - c;
+    if (t == kTileWords - 1) s_off[kTileWords] = wave_base + incl;
+    __syncthreads();
+    const uint64_t base = tile_base(intra, gpre, tile);
+    const u64x2_t *__restrict__ vin = reinterpret_cast<const u64x2_t *>(in);
+    u64x2_t *__restrict__ vout = reinterpret_cast<u64x2_t *>(out);
+    constexpr int kPer = kRoundPairs / kTileWords;
+    for (int rw = 0; rw < kTileWords; rw += kRoundWords) {
+        const uint32_t rb = s_off[rw], re = s_off[rw + kRoundWords];
+        if (rb == re) continue;  // nothing kept in this round (uniform)
+        const int64_t row_r = (w0 + rw) * 64;
+        u64x2_t x[kPer];
+#pragma unroll
+        for (int i = 0; i < kPer; ++i) {
+            const int v = t + kTileWords * i;
+            const int64_t row = row_r + 2 * v;
+            const uint64_t bits = (s_word[rw + (v >> 5)] >> ((2 * v) & 63)) & 3ull;
+            x[i] = u64x2_t{0, 0};
+            if (bits) {
+                if (row + 1 < n) {
+                    x[i] = __builtin_nontemporal_load(vin + (row >> 1));
+                } else if (row < n) {
+                    x[i].x = (unsigned long long)__builtin_bit_cast(uint64_t, in[row]);
+                }
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < kPer; ++i) {
+            const int v = t + kTileWords * i;
+            const int wi = rw + (v >> 5);
+            const int bl = (2 * v) & 63;
+            const uint64_t wd = s_word[wi];
+            const uint64_t bits = (wd >> bl) & 3ull;
+            if (!bits) continue;
+            const uint64_t m_lt = bl == 0 ? 0ull : (~0ull >> (64 - bl));
+            uint32_t pos = s_off[wi] - rb + (uint32_t)__popcll(wd & m_lt);
+            if (bits & 1ull) s_stage[pos++] = (uint64_t)x[i].x;
+            if (bits & 2ull) s_stage[pos] = (uint64_t)x[i].y;
+        }
+        __syncthreads();
+        const uint64_t g0 = base + rb, g1 = base + re;
+        for (uint64_t p = (g0 >> 1) + t; p < ((g1 + 1) >> 1); p += kTileWords) {
+            const uint64_t e0 = 2 * p, e1 = e0 + 1;
+            if (e0 >= g0 && e1 < g1) {
+                vout[p] = u64x2_t{s_stage[e0 - g0], s_stage[e1 - g0]};
+            } else if (e0 >= g0) {
+                out[e0] = __builtin_bit_cast(T, s_stage[e0 - g0]);
+            } else {
+                out[e1] = __builtin_bit_cast(T, s_stage[e1 - g0]);
+            }
+        }
+        __syncthreads();
+    }
+}
+
 }  // namespace fqk
 
 extern "C" {
@@ -225,7 +359,8 @@ extern "C" {
 size_t fq_filter_workspace_bytes(int64_t len) {
     const int64_t nwords = (len + 63) / 64;
     const int64_t ntiles = (nwords + fqk::kTileWords - 1) / fqk::kTileWords;
-    return (size_t)(ntiles + 1) * sizeof(uint64_t);
+    const int64_t ngroups = (ntiles + fqk::kGroupTiles - 1) / fqk::kGroupTiles;
+    return (size_t)(ntiles + ngroups + 1) * sizeof(uint64_t);
 }
 
 fq_status fq_filter_compact(const fq_col *in, const uint64_t *d_bitmap, void *d_out, int64_t *out_len,
@@ -244,37 +379,42 @@ fq_status fq_filter_compact(const fq_col *in, const uint64_t *d_bitmap, void *d_
     hipStream_t st = (hipStream_t)stream;
     const int64_t nwords = (n + 63) / 64;
     const int64_t ntiles = (nwords + kTileWords - 1) / kTileWords;
-    uint64_t *counts = (uint64_t *)d_ws;
-    hipLaunchKernelGGL(compact_count_kernel, dim3((unsigned)ntiles), dim3(kTileWords), 0, st, d_bitmap, n,
-                       counts);
+    const int64_t ngroups = (ntiles + kGroupTiles - 1) / kGroupTiles;
+    uint64_t *intra = (uint64_t *)d_ws;
+    uint64_t *gpre = intra + ntiles;
+    hipLaunchKernelGGL(compact_count_kernel, dim3((unsigned)ngroups), dim3(kTileWords), 0, st, d_bitmap, n, ntiles,
+                       intra, gpre);
     FQ_HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(compact_scan_kernel, dim3(1), dim3(kScanThreads), 0, st, counts, ntiles);
+    hipLaunchKernelGGL(compact_scan_kernel, dim3(1), dim3(kScanThreads), 0, st, gpre, ngroups);
     FQ_HIP_TRY(hipGetLastError());
     switch (esz) {
         case 1:
             hipLaunchKernelGGL(compact_scatter_kernel<uint8_t>, dim3((unsigned)ntiles), dim3(kTileWords), 0, st,
-                               (const uint8_t *)in->data, d_bitmap, n, counts, (uint8_t *)d_out);
+                               (const uint8_t *)in->data, d_bitmap, n, intra, gpre, (uint8_t *)d_out);
             break;
         case 2:
             hipLaunchKernelGGL(compact_scatter_kernel<uint16_t>, dim3((unsigned)ntiles), dim3(kTileWords), 0, st,
-                               (const uint16_t *)in->data, d_bitmap, n, counts, (uint16_t *)d_out);
+                               (const uint16_t *)in->data, d_bitmap, n, intra, gpre, (uint16_t *)d_out);
             break;
         case 4:
             hipLaunchKernelGGL(compact_scatter_kernel<uint32_t>, dim3((unsigned)ntiles), dim3(kTileWords), 0, st,
-                               (const uint32_t *)in->data, d_bitmap, n, counts, (uint32_t *)d_out);
+                               (const uint32_t *)in->data, d_bitmap, n, intra, gpre, (uint32_t *)d_out);
             break;
         default:
-            if (((uintptr_t)in->data & 15u) == 0)
+            if (((uintptr_t)in->data & 15u) == 0 && ((uintptr_t)d_out & 15u) == 0)
+                hipLaunchKernelGGL(compact_scatter_lds_kernel<uint64_t>, dim3((unsigned)ntiles), dim3(kTileWords), 0,
+                                   st, (const uint64_t *)in->data, d_bitmap, n, intra, gpre, (uint64_t *)d_out);
+            else if (((uintptr_t)in->data & 15u) == 0)
                 hipLaunchKernelGGL(compact_scatter_vec_kernel<uint64_t>, dim3((unsigned)ntiles), dim3(kTileWords), 0,
-                                   st, (const uint64_t *)in->data, d_bitmap, n, counts, (uint64_t *)d_out);
+                                   st, (const uint64_t *)in->data, d_bitmap, n, intra, gpre, (uint64_t *)d_out);
             else
                 hipLaunchKernelGGL(compact_scatter_kernel<uint64_t>, dim3((unsigned)ntiles), dim3(kTileWords), 0,
-                                   st, (const uint64_t *)in->data, d_bitmap, n, counts, (uint64_t *)d_out);
+                                   st, (const uint64_t *)in->data, d_bitmap, n, intra, gpre, (uint64_t *)d_out);
             break;
     }
     FQ_HIP_TRY(hipGetLastError());
     uint64_t total = 0;
-    FQ_HIP_TRY(hipMemcpyAsync(&total, counts + ntiles, sizeof(total), hipMemcpyDeviceToHost, st));
+    FQ_HIP_TRY(hipMemcpyAsync(&total, gpre + ngroups, sizeof(total), hipMemcpyDeviceToHost, st));
     FQ_HIP_TRY(hipStreamSynchronize(st));
     *out_len = (int64_t)total;
     return FQ_OK;

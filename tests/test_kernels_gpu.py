@@ -3,6 +3,8 @@ numpy, on seeded inputs at sizes the oracle finishes in seconds.
 
 Bit-exact for integer results; float sums within the tolerance written in
 each test (reduction order differs from arrow's lane-wise simd sum)."""
+import ctypes as C
+
 import numpy as np
 import pytest
 
@@ -332,6 +334,19 @@ def test_elementwise_fast_path_div_zero_in_tile_and_tail():
         assert str(ei.value) == "Internal Error: Divide by zero error"
 
 
+def test_filter_compaction_many_tiles(jit_mode):
+    """> 16 x 512 tiles: every wave of the tile-count scan walks several
+    512-entry chunks, the last one ragged."""
+    if jit_mode != "interp":
+        pytest.skip("no expression program involved")
+    n = 16384 * 9001 + 77
+    X = ops.splitmix_column(0xF1, 0, n)
+    x = X.to_numpy()
+    thr = np.uint64(5 * 2**61)
+    kept = ops.filter_compact(X, ops.compare("<", X, (int(thr), "UInt64")))
+    assert np.array_equal(kept.to_numpy(), x[x < thr])
+
+
 @pytest.mark.parametrize("n", [1, 63, 64, 127, 128, 129, 16384 * 3 + 1, 16384 * 5 + 128, 1_000_003])
 def test_filter_compaction_vector_path_edges(n, jit_mode):
     """16-byte-aligned 8-byte columns take the pairwise vector scatter; odd
@@ -349,6 +364,20 @@ def test_filter_compaction_vector_path_edges(n, jit_mode):
             bm = ops.compare("=", m, 1)
             got = ops.filter_compact(X, bm).to_numpy()
             assert np.array_equal(got, x[keep]), (dt, thr)
+    # 8-byte-offset output: aligned input takes the pairwise register scatter
+    x = rng.integers(0, 2**40, size=n).astype(np.uint64)
+    keep = rng.random(n) < 0.4
+    keep[-1] = True
+    X = ops.from_numpy(x)
+    bm = ops.compare("=", ops.from_numpy(keep.astype(np.uint64)), 1)
+    out = ops.empty_column(n + 1, abi.DT_UINT64)
+    ws = ops.Workspace(ops.lib.fq_filter_workspace_bytes(n))
+    kept = C.c_int64(0)
+    ops.check(ops.lib.fq_filter_compact(C.byref(X.col()), C.c_void_p(bm.ptr), C.c_void_p(out.ptr + 8),
+                                        C.byref(kept), ws.ptr, ws.nbytes, None))
+    assert kept.value == int(keep.sum())
+    got = out.buf[8: 8 + 8 * kept.value].cpu().numpy().view(np.uint64)
+    assert np.array_equal(got, x[keep])
     # misaligned (8-byte offset) input keeps the scalar scatter
     X = ops.from_numpy(np.arange(n + 1, dtype=np.uint64))
     Xs = ops.DeviceColumn(X.buf, n, abi.DT_UINT64, offset=8)
