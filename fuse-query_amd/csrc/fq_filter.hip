@@ -341,7 +341,7 @@ __global__ void __launch_bounds__(kTileWords)
         for (uint64_t p = (g0 >> 1) + t; p < ((g1 + 1) >> 1); p += kTileWords) {
             const uint64_t e0 = 2 * p, e1 = e0 + 1;
             if (e0 >= g0 && e1 < g1) {
-                vout[p] = u64x2_t{s_stage[e0 - g0], s_stage[e1 - g0]};
+                __builtin_nontemporal_store(u64x2_t{s_stage[e0 - g0], s_stage[e1 - g0]}, vout + p);
             } else if (e0 >= g0) {
                 out[e0] = __builtin_bit_cast(T, s_stage[e0 - g0]);
             } else {
