@@ -356,6 +356,14 @@ fq_status fq_result_value(const fq_result *r, int64_t row, int32_t col, fq_value
     *out = r->cols[(size_t)col][(size_t)row].to_abi();
     return FQ_OK;
 }
+fq_status fq_result_values(const fq_result *r, int32_t col, fq_value *out, int64_t n) {
+    if (!r || (!out && n > 0) || col < 0 || col >= (int32_t)r->cols.size() || n < 0 ||
+        n > (int64_t)r->cols[(size_t)col].size())
+        return fqc::fail(FQ_E_INVALID, "fq_result_values: out of range");
+    const auto &c = r->cols[(size_t)col];
+    for (int64_t i = 0; i < n; ++i) out[i] = c[(size_t)i].to_abi();
+    return FQ_OK;
+}
 const char *fq_result_text(const fq_result *r, int64_t row, int32_t col) {
     if (!r || col < 0 || col >= (int32_t)r->cols.size() || row < 0 || row >= (int64_t)r->cols[(size_t)col].size())
         return nullptr;

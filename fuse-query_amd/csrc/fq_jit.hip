@@ -624,9 +624,9 @@ bool gen_source(const Launch &L, int32_t tin, bool chain, Gen &g, std::string &s
 // enough to find or claim a slot across XCDs.
 // ---------------------------------------------------------------------------
 
-int lds_slots(int n_aggs) {
-    int s = 4096;
-    while ((int64_t)s * 8 * (1 + n_aggs) > 65536) s >>= 1;
+int lds_slots(int n_aggs, int budget) {
+    int s = 16384;
+    while (s > 64 && (int64_t)s * 8 * (1 + n_aggs) > budget) s >>= 1;
     return s;
 }
 
@@ -666,6 +666,9 @@ std::string group_shape_key(const GroupLaunch &G, int32_t tin, int dev) {
     put(G.key_dtype);
     put_pred_key(G.pred, k);
     prog(G.key);
+    put(G.lds_bytes);
+    put(G.threads);
+    put(G.rowmap);
     put(G.n_aggs);
     for (int a = 0; a < G.n_aggs; ++a) {
         put(G.kinds[a]);
@@ -698,7 +701,7 @@ bool gen_groupby_source(const GroupLaunch &G, int32_t tin, Gen &g, std::string &
     if (!TIn || (G.key_dtype != FQ_DT_UINT64 && G.key_dtype != FQ_DT_INT64)) return false;
     if (G.n_aggs < 1 || G.n_aggs > FQ_MAX_GROUP_AGGS) return false;
     const int NA = G.n_aggs;
-    const int S = lds_slots(NA);
+    const int S = lds_slots(NA, G.lds_bytes);
     src = kCommon;
     src += "typedef " + std::string(TIn) + " TIn;\n";
     src += "struct Step { u64 c, m, s; };\nstruct Consts { u64 rhs; Step p[" + std::to_string(kSteps) + "], k[" +
@@ -707,6 +710,7 @@ bool gen_groupby_source(const GroupLaunch &G, int32_t tin, Gen &g, std::string &
            "][" + std::to_string(kSteps) + "]; };\n";
     src += "struct Tab { u64 *keys; u64 *st[" + std::to_string(FQ_MAX_GROUP_AGGS) +
            "]; u32 *hdr; long long mask; int rmask; };\n";
+    src += "#define BT " + std::to_string(G.threads) + "\n#define ROWMAP " + std::to_string(G.rowmap) + "\n";
     src += "#define EMPTY 0xffffffffffffffffull\n#define NA " + std::to_string(NA) + "\n#define S " +
            std::to_string(S) + "\n#define LOG2S " + std::to_string(__builtin_ctz((unsigned)S)) + "\n";
     src += R"(
@@ -852,14 +856,14 @@ __device__ long long ginsert(const Tab &t, u64 k) {
 
     // kernel
     src += R"(
-extern "C" __global__ void __launch_bounds__(256)
+extern "C" __global__ void __launch_bounds__(BT)
 fq_jit_groupby(const TIn *__restrict__ col, long long n, long long head, const u64 *__restrict__ bitmap,
                Consts c, Tab t) {
     __shared__ u64 s_keys[S];
     __shared__ u64 s_st[NA][S];
     __shared__ int s_bypass[2];  // [0] bypass flag, [1] slots claimed
     if (threadIdx.x < 2) s_bypass[threadIdx.x] = 0;
-    for (int i = threadIdx.x; i < S; i += 256) {
+    for (int i = threadIdx.x; i < S; i += BT) {
         s_keys[i] = EMPTY;
 )";
     for (int a = 0; a < NA; ++a)
@@ -871,11 +875,42 @@ fq_jit_groupby(const TIn *__restrict__ col, long long n, long long head, const u
     const long long roff = (long long)(blockIdx.x & t.rmask) * (t.mask + 2);
     for (int a = 0; a < NA; ++a) tr.st[a] += roff;
     u32 flags = 0;
-    const long long T = (long long)gridDim.x * 256;
-    const long long g = (long long)blockIdx.x * 256 + threadIdx.x;
+    const long long T = (long long)gridDim.x * BT;
+    const long long g = (long long)blockIdx.x * BT + threadIdx.x;
     const long long nvec = (n - head) / 2;
     const u32x4 *__restrict__ vp = (const u32x4 *)(col + head);
-    const long long TV = 4 * 256;
+#if ROWMAP == 1
+    // lane-consecutive rows (8-byte loads): the 64 keys of one LDS access are
+    // 64 consecutive rows, so small sequential keys hit distinct banks
+    const TIn *__restrict__ cp = col + head;
+    const long long TV = 4 * BT;  // vectors (pairs) per tile, as below
+    const long long ntiles = nvec / TV;
+    TIn nxt[8];
+    if ((long long)blockIdx.x < ntiles) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            nxt[k] = __builtin_nontemporal_load(cp + (long long)blockIdx.x * TV * 2 + threadIdx.x + (long long)k * BT);
+    }
+    for (long long tt = blockIdx.x; tt < ntiles; tt += gridDim.x) {
+        TIn raw[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) raw[k] = nxt[k];
+        const long long tn = tt + gridDim.x;
+        if (tn < ntiles) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) nxt[k] = __builtin_nontemporal_load(cp + tn * TV * 2 + threadIdx.x + (long long)k * BT);
+        }
+        Row r[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) fq_prep(raw[k], head + tt * TV * 2 + threadIdx.x + (long long)k * BT, c, bitmap, flags, r[k]);
+        u64 cur[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) cur[j] = fq_first(r[j], s_keys);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) fq_commit(r[j], cur[j], tr, s_keys, s_st, s_bypass);
+    }
+#else
+    const long long TV = 4 * BT;
     const long long ntiles = nvec / TV;
     // software pipelined: the next tile's loads are in flight while this
     // tile's rows go through the LDS table (2 waves per SIMD cannot hide the
@@ -884,7 +919,7 @@ fq_jit_groupby(const TIn *__restrict__ col, long long n, long long head, const u
     if ((long long)blockIdx.x < ntiles) {
 #pragma unroll
         for (int k = 0; k < 4; ++k)
-            nxt[k] = __builtin_nontemporal_load(vp + (long long)blockIdx.x * TV + threadIdx.x + (long long)k * 256);
+            nxt[k] = __builtin_nontemporal_load(vp + (long long)blockIdx.x * TV + threadIdx.x + (long long)k * BT);
     }
     for (long long tt = blockIdx.x; tt < ntiles; tt += gridDim.x) {
         const long long base = tt * TV + threadIdx.x;
@@ -894,14 +929,14 @@ fq_jit_groupby(const TIn *__restrict__ col, long long n, long long head, const u
         const long long tn = tt + gridDim.x;
         if (tn < ntiles) {
 #pragma unroll
-            for (int k = 0; k < 4; ++k) nxt[k] = __builtin_nontemporal_load(vp + tn * TV + threadIdx.x + (long long)k * 256);
+            for (int k = 0; k < 4; ++k) nxt[k] = __builtin_nontemporal_load(vp + tn * TV + threadIdx.x + (long long)k * BT);
         }
         Row r[8];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             TIn x[2];
             __builtin_memcpy(&x[0], &raw[k], 16);
-            const long long i0 = head + (base + (long long)k * 256) * 2;
+            const long long i0 = head + (base + (long long)k * BT) * 2;
             fq_prep(x[0], i0, c, bitmap, flags, r[2 * k]);
             fq_prep(x[1], i0 + 1, c, bitmap, flags, r[2 * k + 1]);
         }
@@ -911,6 +946,7 @@ fq_jit_groupby(const TIn *__restrict__ col, long long n, long long head, const u
 #pragma unroll
         for (int j = 0; j < 8; ++j) fq_commit(r[j], cur[j], tr, s_keys, s_st, s_bypass);
     }
+#endif
     for (long long v = ntiles * TV + g; v < nvec; v += T) {
         const u32x4 raw = __builtin_nontemporal_load(vp + v);
         TIn x[2];
@@ -927,7 +963,7 @@ fq_jit_groupby(const TIn *__restrict__ col, long long n, long long head, const u
     if (flags) atomicOr(&t.hdr[0], flags);
     __syncthreads();
     // flush this workgroup's groups into the HBM table
-    for (int i = threadIdx.x; i < S; i += 256) {
+    for (int i = threadIdx.x; i < S; i += BT) {
         const u64 k = s_keys[i];
         if (k == EMPTY) continue;
         const long long gs = ginsert(tr, k);
@@ -1145,7 +1181,7 @@ fq_status jit_groupby(int32_t col_dtype, const GroupLaunch &G) {
     long long n = G.n, head = G.head;
     const uint64_t *bitmap = G.pred.bitmap;
     void *args[] = {&col, &n, &head, &bitmap, &hc, &tab};
-    FQ_HIP_TRY(hipModuleLaunchKernel(fn, (unsigned)G.grid, 1, 1, kThreads, 1, 1, 0, G.stream, args, nullptr));
+    FQ_HIP_TRY(hipModuleLaunchKernel(fn, (unsigned)G.grid, 1, 1, (unsigned)G.threads, 1, 1, 0, G.stream, args, nullptr));
     g_jit_launches += 1;
     return FQ_OK;
 }

@@ -40,12 +40,13 @@ fq_status jit_scan(int32_t col_dtype, bool chain, const Launch &L, bool *used);
 fq_status jit_prepare(int32_t col_dtype, bool chain, const Launch &L, bool *ready);
 
 // State replicas of a group table of `cap` slots: workgroup b updates replica
-// b % R, so workgroups rarely contend for one group's state words (the
-// extract folds the replicas).  R * cap <= 2^22 words per aggregate (32 MB),
-// at most 256 replicas; tables of 2^22 slots and more get one.
+// b % R, so the 256 flushing workgroups (one per CU) contend at most 16-fold
+// for one group's state words (the extract folds the replicas).
+// R * cap <= 2^22 words per aggregate (32 MB), at most 16 replicas; tables
+// of 2^22 slots and more get one.
 inline int group_replicas(int64_t cap) {
     int r = 1;
-    while (r < 256 && cap * (int64_t)r * 2 <= ((int64_t)1 << 22)) r *= 2;
+    while (r < 16 && cap * (int64_t)r * 2 <= ((int64_t)1 << 22)) r *= 2;
     return r;
 }
 
@@ -66,6 +67,9 @@ struct GroupLaunch {
     uint64_t *states[FQ_MAX_GROUP_AGGS];
     uint32_t *hdr;
     int64_t capacity;
+    int lds_bytes;  // LDS hash table budget per workgroup (sets S and the occupancy)
+    int threads;    // workgroup size
+    int rowmap;     // 1: lane-consecutive rows (8-byte loads), 0: row pairs per lane (16-byte loads)
     int grid;
     hipStream_t stream;
 };

@@ -10,6 +10,8 @@ Projection / Limit) on the gfx950 kernels.
 """
 import ctypes as C
 
+import numpy as np
+
 from . import abi
 from ._lib import FQError, check, last_error, lib
 from .expr import from_bits
@@ -23,7 +25,7 @@ ENGINE_SYMBOLS = [
     "fq_engine_release_numbers", "fq_engine_execute", "fq_engine_explain", "fq_engine_execute_partial",
     "fq_engine_execute_final", "fq_engine_get_stats", "fq_engine_reset_stats", "fq_result_num_rows",
     "fq_result_num_columns", "fq_result_column_name", "fq_result_column_type", "fq_result_value",
-    "fq_result_text", "fq_result_free", "fq_result_mysql_type",
+    "fq_result_text", "fq_result_free", "fq_result_mysql_type", "fq_result_values",
 ]
 
 
@@ -53,6 +55,7 @@ _protos = {
     "fq_result_column_type": (C.c_int32, [C.c_void_p, C.c_int32]),
     "fq_result_value": (C.c_int32, [C.c_void_p, C.c_int64, C.c_int32, P(abi.fq_value)]),
     "fq_result_text": (C.c_char_p, [C.c_void_p, C.c_int64, C.c_int32]),
+    "fq_result_values": (C.c_int32, [C.c_void_p, C.c_int32, P(abi.fq_value), C.c_int64]),
     "fq_result_free": (None, [C.c_void_p]),
     "fq_result_mysql_type": (C.c_int32, [C.c_void_p, C.c_int32, P(C.c_int32)]),
 }
@@ -60,6 +63,30 @@ for _n, (_r, _a) in _protos.items():
     _f = getattr(lib, _n)
     _f.restype = _r
     _f.argtypes = _a
+
+
+_VALUE_NP = np.dtype([("dtype", "<i4"), ("is_some", "<i4"), ("bits", "<u8")])
+
+
+def _column_values(ptr, c, nrow):
+    """One column of a result as Python values (None for NULL), fetched in
+    one fq_result_values call and converted with numpy."""
+    if nrow == 0:
+        return []
+    arr = (abi.fq_value * nrow)()
+    check(lib.fq_result_values(ptr, c, arr, nrow))
+    a = np.frombuffer(arr, dtype=_VALUE_NP)
+    dts = np.unique(a["dtype"])
+    if len(dts) == 1 and bool(a["is_some"].all()):
+        dt, bits = int(dts[0]), a["bits"]
+        if dt in (abi.DT_FLOAT32, abi.DT_FLOAT64):
+            return bits.view(np.float64).tolist()
+        if dt in (abi.DT_INT8, abi.DT_INT16, abi.DT_INT32, abi.DT_INT64):
+            return bits.view(np.int64).tolist()
+        if dt == abi.DT_BOOLEAN:
+            return (bits != 0).tolist()
+        return bits.tolist()
+    return [from_bits(int(b), int(d)) if s else None for d, s, b in zip(a["dtype"], a["is_some"], a["bits"])]
 
 
 class Result:
@@ -74,18 +101,14 @@ class Result:
             self.types = [lib.fq_result_column_type(ptr, c) for c in range(ncol)]
             cols = []
             for c in range(ncol):
-                vals = []
-                for r in range(nrow):
-                    if self.types[c] == abi.DT_UTF8:
+                if self.types[c] == abi.DT_UTF8:
+                    vals = []
+                    for r in range(nrow):
                         t = lib.fq_result_text(ptr, r, c)
                         vals.append(t.decode() if t is not None else None)
-                        continue
-                    v = abi.fq_value()
-                    if lib.fq_result_value(ptr, r, c, C.byref(v)) != 0:
-                        vals.append(None)
-                        continue
-                    vals.append(from_bits(v.bits, v.dtype) if v.is_some else None)
-                cols.append(vals)
+                    cols.append(vals)
+                    continue
+                cols.append(_column_values(ptr, c, nrow))
             self.columns = cols
             self.rows = [tuple(col[r] for col in cols) for r in range(nrow)]
             # what the reference's MySQL writer sends (mysql_stream.rs:21-84):

@@ -96,6 +96,8 @@ int32_t fq_result_num_columns(const fq_result *r);
 const char *fq_result_column_name(const fq_result *r, int32_t col);
 int32_t fq_result_column_type(const fq_result *r, int32_t col);
 fq_status fq_result_value(const fq_result *r, int64_t row, int32_t col, fq_value *out);
+/* rows 0..n-1 of one column in one call (n <= fq_result_num_rows) */
+fq_status fq_result_values(const fq_result *r, int32_t col, fq_value *out, int64_t n);
 /* the value as text, DataValue's Display (NULL for None); valid until fq_result_free */
 const char *fq_result_text(const fq_result *r, int64_t row, int32_t col);
 /* MySQL column type the reference's result writer declares for a column
