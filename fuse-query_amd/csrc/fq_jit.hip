@@ -711,7 +711,7 @@ bool gen_groupby_source(const GroupLaunch &G, int32_t tin, Gen &g, std::string &
     src += "struct Tab { u64 *keys; u64 *st[" + std::to_string(FQ_MAX_GROUP_AGGS) +
            "]; u32 *hdr; long long mask; int rmask; };\n";
     src += "#define BT " + std::to_string(G.threads) + "\n#define ROWMAP " + std::to_string(G.rowmap) + "\n";
-    src += "#define EMPTY 0xffffffffffffffffull\n#define NA " + std::to_string(NA) + "\n#define S " +
+    src += "#define PMAX 16\n#define EMPTY 0xffffffffffffffffull\n#define NA " + std::to_string(NA) + "\n#define S " +
            std::to_string(S) + "\n#define LOG2S " + std::to_string(__builtin_ctz((unsigned)S)) + "\n";
     src += R"(
 __device__ __forceinline__ u64 mix(u64 z) {
@@ -723,6 +723,10 @@ __device__ __forceinline__ u64 mix(u64 z) {
 // top bits kept; the HBM table keeps the full 64-bit mixer.  (An XOR-fold
 // that keeps consecutive keys in consecutive slots measured no faster: a
 // lane holds rows 2l and 2l+1, so a wave's keys are strided anyway.)
+// key partition (independent of the LDS slot bits)
+__device__ __forceinline__ u32 part_of(u64 k, u32 P) {
+    return ((((u32)k ^ (u32)(k >> 32)) * 0x2545F491u) >> 26) & (P - 1);
+}
 __device__ __forceinline__ u32 lds_hash(u64 k) {
     return (((u32)k ^ (u32)(k >> 32)) * 0x9E3779B1u) >> (32 - LOG2S);
 }
@@ -754,6 +758,7 @@ __device__ long long ginsert(const Tab &t, u64 k) {
         if (cur == k) return h;
         if (cur == EMPTY) {
             const u64 old = atomicCAS((unsigned long long *)&t.keys[h], EMPTY, k);
+            if (old == EMPTY) atomicAdd(&t.hdr[4], 1u);  // groups claimed (sizes later launches' partitions)
             if (old == EMPTY || old == k) return h;
         }
         h = (h + 1) & t.mask;
@@ -849,8 +854,10 @@ __device__ long long ginsert(const Tab &t, u64 k) {
                                              "r.v" + std::to_string(a)) + "\n";
     row += "        }\n    }\n}\n";
     row += "__device__ __forceinline__ void fq_row(TIn x, long long idx, const Consts &c, const Tab &t,\n"
-           "    const u64 *__restrict__ bitmap, u64 *s_keys, u64 (*s_st)[S], u32 &flags, int *s_bypass) {\n"
+           "    const u64 *__restrict__ bitmap, u64 *s_keys, u64 (*s_st)[S], u32 &flags, int *s_bypass, u32 P,\n"
+           "    u32 part) {\n"
            "    Row r;\n    fq_prep(x, idx, c, bitmap, flags, r);\n"
+           "    if (P > 1 && part_of(r.k, P) != part) r.pass = 0;\n"
            "    fq_commit(r, fq_first(r, s_keys), t, s_keys, s_st, s_bypass);\n}\n";
     src += row;
 
@@ -874,9 +881,23 @@ fq_jit_groupby(const TIn *__restrict__ col, long long n, long long head, const u
     Tab tr = t;
     const long long roff = (long long)(blockIdx.x & t.rmask) * (t.mask + 2);
     for (int a = 0; a < NA; ++a) tr.st[a] += roff;
+    // Key partitions: when the HBM table already holds more groups (from
+    // earlier launches into it) than half an LDS table, workgroup b only
+    // aggregates the keys of partition b % P and walks the rows with the
+    // other (grid / P) - 1 workgroups of its partition: every row is read P
+    // times, but every group stays in LDS.
+    const u32 seen = __hip_atomic_load(&t.hdr[4], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // (only past the LDS saturation point, 3/4 of S; beyond PMAX partitions
+    // the rows are cheaper to send to the HBM table than to re-read)
+    u32 P = 1;
+    if (seen > (u32)(S * 3 / 4))
+        while (P <= PMAX && P * (u32)(S / 2) < seen) P <<= 1;
+    if (P > PMAX || gridDim.x % P) P = 1;
+    const u32 part = blockIdx.x & (P - 1);
+    const long long RG = gridDim.x / P, rb = blockIdx.x / P;
     u32 flags = 0;
-    const long long T = (long long)gridDim.x * BT;
-    const long long g = (long long)blockIdx.x * BT + threadIdx.x;
+    const long long T = RG * BT;
+    const long long g = rb * BT + threadIdx.x;
     const long long nvec = (n - head) / 2;
     const u32x4 *__restrict__ vp = (const u32x4 *)(col + head);
 #if ROWMAP == 1
@@ -886,23 +907,26 @@ fq_jit_groupby(const TIn *__restrict__ col, long long n, long long head, const u
     const long long TV = 4 * BT;  // vectors (pairs) per tile, as below
     const long long ntiles = nvec / TV;
     TIn nxt[8];
-    if ((long long)blockIdx.x < ntiles) {
+    if (rb < ntiles) {
 #pragma unroll
         for (int k = 0; k < 8; ++k)
-            nxt[k] = __builtin_nontemporal_load(cp + (long long)blockIdx.x * TV * 2 + threadIdx.x + (long long)k * BT);
+            nxt[k] = __builtin_nontemporal_load(cp + rb * TV * 2 + threadIdx.x + (long long)k * BT);
     }
-    for (long long tt = blockIdx.x; tt < ntiles; tt += gridDim.x) {
+    for (long long tt = rb; tt < ntiles; tt += RG) {
         TIn raw[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) raw[k] = nxt[k];
-        const long long tn = tt + gridDim.x;
+        const long long tn = tt + RG;
         if (tn < ntiles) {
 #pragma unroll
             for (int k = 0; k < 8; ++k) nxt[k] = __builtin_nontemporal_load(cp + tn * TV * 2 + threadIdx.x + (long long)k * BT);
         }
         Row r[8];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) fq_prep(raw[k], head + tt * TV * 2 + threadIdx.x + (long long)k * BT, c, bitmap, flags, r[k]);
+        for (int k = 0; k < 8; ++k) {
+            fq_prep(raw[k], head + tt * TV * 2 + threadIdx.x + (long long)k * BT, c, bitmap, flags, r[k]);
+            if (P > 1 && part_of(r[k].k, P) != part) r[k].pass = 0;
+        }
         u64 cur[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) cur[j] = fq_first(r[j], s_keys);
@@ -916,17 +940,17 @@ fq_jit_groupby(const TIn *__restrict__ col, long long n, long long head, const u
     // tile's rows go through the LDS table (2 waves per SIMD cannot hide the
     // HBM latency otherwise)
     u32x4 nxt[4];
-    if ((long long)blockIdx.x < ntiles) {
+    if (rb < ntiles) {
 #pragma unroll
         for (int k = 0; k < 4; ++k)
-            nxt[k] = __builtin_nontemporal_load(vp + (long long)blockIdx.x * TV + threadIdx.x + (long long)k * BT);
+            nxt[k] = __builtin_nontemporal_load(vp + rb * TV + threadIdx.x + (long long)k * BT);
     }
-    for (long long tt = blockIdx.x; tt < ntiles; tt += gridDim.x) {
+    for (long long tt = rb; tt < ntiles; tt += RG) {
         const long long base = tt * TV + threadIdx.x;
         u32x4 raw[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) raw[k] = nxt[k];
-        const long long tn = tt + gridDim.x;
+        const long long tn = tt + RG;
         if (tn < ntiles) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) nxt[k] = __builtin_nontemporal_load(vp + tn * TV + threadIdx.x + (long long)k * BT);
@@ -939,6 +963,8 @@ fq_jit_groupby(const TIn *__restrict__ col, long long n, long long head, const u
             const long long i0 = head + (base + (long long)k * BT) * 2;
             fq_prep(x[0], i0, c, bitmap, flags, r[2 * k]);
             fq_prep(x[1], i0 + 1, c, bitmap, flags, r[2 * k + 1]);
+            if (P > 1 && part_of(r[2 * k].k, P) != part) r[2 * k].pass = 0;
+            if (P > 1 && part_of(r[2 * k + 1].k, P) != part) r[2 * k + 1].pass = 0;
         }
         u64 cur[8];
 #pragma unroll
@@ -951,14 +977,14 @@ fq_jit_groupby(const TIn *__restrict__ col, long long n, long long head, const u
         const u32x4 raw = __builtin_nontemporal_load(vp + v);
         TIn x[2];
         __builtin_memcpy(&x[0], &raw, 16);
-        fq_row(x[0], head + v * 2, c, tr, bitmap, s_keys, s_st, flags, s_bypass);
-        fq_row(x[1], head + v * 2 + 1, c, tr, bitmap, s_keys, s_st, flags, s_bypass);
+        fq_row(x[0], head + v * 2, c, tr, bitmap, s_keys, s_st, flags, s_bypass, P, part);
+        fq_row(x[1], head + v * 2 + 1, c, tr, bitmap, s_keys, s_st, flags, s_bypass, P, part);
     }
     const long long tail0 = head + nvec * 2;
     const long long nedge = head + (n - tail0);
     for (long long e = g; e < nedge; e += T) {
         const long long i = e < head ? e : tail0 + (e - head);
-        fq_row(col[i], i, c, tr, bitmap, s_keys, s_st, flags, s_bypass);
+        fq_row(col[i], i, c, tr, bitmap, s_keys, s_st, flags, s_bypass, P, part);
     }
     if (flags) atomicOr(&t.hdr[0], flags);
     __syncthreads();

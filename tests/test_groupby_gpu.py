@@ -202,6 +202,30 @@ def test_accumulates_across_blocks():
     compare(got, exp, [abi.AGG_SUM, abi.AGG_COUNT, abi.AGG_MIN], [U, U, U])
 
 
+@pytest.mark.parametrize("mod,rows", [(20_000, 3_000_017), (300_000, 2_000_003), (5_000, 10_001)])
+def test_partitioned_launches_after_the_table_fills(mod, rows):
+    """Later launches into a table holding more groups than half an LDS table
+    split the keys into partitions (each workgroup aggregates one partition
+    and every row is read once per partition); the result must equal one
+    numpy group-by over all blocks.  The last case has too few rows for a
+    grid the partition count divides (falls back to one partition)."""
+    aggs = [(abi.AGG_COUNT, U), (abi.AGG_SUM, U), (abi.AGG_MAX, U), (abi.AGG_MIN, F)]
+    key, _ = chain(U, [("%", mod)])
+    vf, _ = chain(U, [("*", 0.5)])
+    t = ops.GroupTable(1 << 20, aggs)
+    xs = []
+    for i in range(3):
+        col = ops.splitmix_column(0x9A + i, 0, rows)
+        xs.append(col.to_numpy())
+        t.aggregate(col, None, key, [None, None, None, vf])
+    keys, states = t.extract()
+    st = decode(states, [dt for _, dt in aggs])
+    got = {int(k): [st[a][i] for a in range(len(aggs))] for i, k in enumerate(keys)}
+    x = np.concatenate(xs)
+    exp = np_groupby(x % np.uint64(mod), [None, x, x, x.astype(np.float64) * 0.5], [k for k, _ in aggs])
+    compare(got, exp, [k for k, _ in aggs], [d for _, d in aggs])
+
+
 # ---- GROUP BY through the SQL pipeline (GroupByPartial x P -> Merge -> Final) ----
 import fq_ref as R  # noqa: E402
 

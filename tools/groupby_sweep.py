@@ -1,5 +1,7 @@
 """GROUP BY throughput vs number of groups and aggregates over one numbers_mt
-partition (python tools/groupby_sweep.py [rows] [mods] [naggs]); one line per shape."""
+partition (python tools/groupby_sweep.py [rows] [mods] [naggs] [launches]); one line per shape.
+With launches L > 1 the column is aggregated L times into one table (as the
+engine does for the partitions of one query); the time is per launch."""
 import sys, os, ctypes as C, statistics
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "fuse-query_amd"))
 import torch
@@ -18,12 +20,29 @@ def timed(fn, reps=5):
     return statistics.median(ts)
 MODS = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else [8, 64, 1000, 4096, 100000]
 NAGGS = [int(x) for x in sys.argv[3].split(",")] if len(sys.argv) > 3 else [1, 3]
+L = int(sys.argv[4]) if len(sys.argv) > 4 else 1
 for mod in MODS:
     for naggs in NAGGS:
         key, _ = chain(U, [("%", mod)])
         aggs = [(abi.AGG_COUNT, U), (abi.AGG_SUM, U), (abi.AGG_MAX, U)][:naggs]
         gt = ops.GroupTable(max(64, 4 * mod), aggs)
-        def f():
-            check(lib.fq_group_table_init(C.byref(gt.desc), st)); gt.aggregate(a, key=key)
-        ms = timed(f)
-        print("mod=%6d aggs=%d  %.3f ms  %.1f G rows/s" % (mod, naggs, ms, n / ms / 1e6), flush=True)
+        if L == 1:
+            def f():
+                check(lib.fq_group_table_init(C.byref(gt.desc), st)); gt.aggregate(a, key=key)
+            ms = timed(f)
+            print("mod=%6d aggs=%d  %.3f ms  %.1f G rows/s" % (mod, naggs, ms, n / ms / 1e6), flush=True)
+            continue
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(L + 1)]
+        per = []
+        for rep in range(3):
+            check(lib.fq_group_table_init(C.byref(gt.desc), st))
+            ev[0].record()
+            for i in range(L):
+                gt.aggregate(a, key=key)
+                ev[i + 1].record()
+            ev[L].synchronize()
+            per.append([ev[i].elapsed_time(ev[i + 1]) for i in range(L)])
+        first = statistics.median(p[0] for p in per)
+        rest = statistics.median(statistics.mean(p[1:]) for p in per)
+        print("mod=%6d aggs=%d launches=%d  first %.3f ms, then %.3f ms/launch (%.1f G rows/s)"
+              % (mod, naggs, L, first, rest, n / rest / 1e6), flush=True)
