@@ -201,8 +201,13 @@ def main():
     log(rank, "materialised %d partitions, %d rows (%.1f GB) on rank %d"
         % (len(mine), total_rows, total_rows * 8 / 1e9, rank))
 
+    # cross-GPU exchange: the library's own RCCL communicator (torch.distributed
+    # only ships its unique id); the gloo rehearsal drives the same native
+    # protocol through a torch callback
+    comm = fqd.RcclComm(local) if world > 1 and args.dist_backend == "nccl" else None
+
     def step():
-        r = eng.execute(sql) if world == 1 else fqd.execute(eng, sql)
+        r = eng.execute(sql) if world == 1 else fqd.execute(eng, sql, comm)
         return r.rows if args.query == "g1" else list(r.rows[0])
 
     for _ in range(max(args.warmup, 1)):
@@ -269,7 +274,8 @@ def main():
                 "block_rows": BLOCK_SIZE,
                 "path": "fq_engine_execute: SQL -> PipelineBuilder -> Source x P -> AggregatePartial x P "
                         "(fused gfx950 scan) -> Merge -> AggregateFinal"
-                        + ("" if world == 1 else " ; cross-GPU: one RCCL all-reduce of partial states"),
+                        + ("" if world == 1 else " ; cross-GPU: fq_engine_execute_rccl, one ncclAllReduce of partial states"
+                            if comm is not None else " ; cross-GPU: fq_engine_execute_exchange over gloo"),
                 "parallelism": "dp%d (numbers_mt partitions sharded, %s all-reduce of states)"
                                % (world, "RCCL" if args.dist_backend == "nccl" else "gloo rehearsal"),
             },
@@ -304,6 +310,8 @@ def main():
             out["cpu_baseline"] = {"error": repr(e)}
     if rank == 0:
         print(json.dumps(out), flush=True)
+    if comm is not None:
+        comm.close()
     eng.close()
     if world > 1:
         dist.destroy_process_group()

@@ -1,49 +1,137 @@
 """Multi-GPU AggregateFinal: one process per GPU, numbers_mt partitions
-sharded [8r/G, 8(r+1)/G), and the partial states exchanged with a
-SINGLE all-reduce -- RCCL over xGMI on GPUs (torch.distributed backend
-"nccl"), gloo on CPU.
+sharded [8r/G, 8(r+1)/G), and the partial states exchanged by the
+native protocol of include/fq_comm.h -- ONE all-reduce (two for GROUP BY
+states above 4 KB) -- then AggregateFinal in rank order on every rank.
 
 The reference's only "exchange" is the in-process MergeProcessor channel of
 JSON states (processor_merge.rs:45-63, transform_aggregate_partial.rs:61-72).
-Here every rank serialises its merged partial states (fixed 16-byte
-DataValue records, a few hundred bytes), writes them into ITS OWN row of a
-zeroed [world, cap/8] int64 buffer, and one all-reduce(SUM) turns that into an
-all-gather: each element has exactly one non-zero contributor, so the sum is
-bit-exact for any payload.  The merge itself then runs in rank order on every
-rank (AggregateFinalTransform), so all ranks agree on the result.
+Here every rank writes its serialised states into ITS OWN row of a zeroed
+u64 buffer and a wrapping SUM all-reduce turns that into an all-gather (each
+word has exactly one non-zero contributor, so the result is bit-exact).
+
+Transports for the collective:
+  * RcclComm -- the library's own RCCL communicator (ncclCommInitRank, one
+    per GPU, xGMI): fq_engine_execute_rccl runs partial -> exchange -> final
+    without leaving C++.  torch.distributed only ships the 128-byte unique id.
+  * any torch.distributed group (gloo on CPU for the tests, or nccl) through
+    an fq_allreduce_fn callback into the same native protocol.
 """
+import ctypes as C
+
+import numpy as np
 import torch
 import torch.distributed as dist
 
-STATE_CAP = 4096  # bytes per rank; a query's states are 8 + 16 per value + 8 per function
+from . import abi
+from ._lib import check, lib
+from .engine import Result
+
+P = C.POINTER
+ALLREDUCE_FN = C.CFUNCTYPE(C.c_int32, P(C.c_uint64), C.c_int64, C.c_void_p)
+COMM_ID_BYTES = 128
+STATE_CAP = 4096  # FQ_EXCHANGE_CAP_BYTES
+
+COMM_SYMBOLS = [
+    "fq_exchange_states", "fq_engine_execute_exchange", "fq_comm_unique_id", "fq_comm_init", "fq_comm_info",
+    "fq_comm_destroy", "fq_state_allreduce", "fq_comm_allreduce_u64", "fq_engine_execute_rccl",
+]
+_protos = {
+    "fq_exchange_states": (C.c_int32, [C.c_void_p, C.c_size_t, C.c_int32, C.c_int32, ALLREDUCE_FN, C.c_void_p,
+                                       P(C.c_void_p), P(C.c_size_t)]),
+    "fq_engine_execute_exchange": (C.c_int32, [C.c_void_p, C.c_char_p, C.c_int32, C.c_int32, ALLREDUCE_FN,
+                                               C.c_void_p, P(C.c_void_p)]),
+    "fq_comm_unique_id": (C.c_int32, [C.c_void_p]),
+    "fq_comm_init": (C.c_int32, [C.c_int32, C.c_int32, C.c_int32, C.c_void_p, P(C.c_void_p)]),
+    "fq_comm_info": (C.c_int32, [C.c_void_p, P(C.c_int32), P(C.c_int32)]),
+    "fq_comm_destroy": (None, [C.c_void_p]),
+    "fq_state_allreduce": (C.c_int32, [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p]),
+    "fq_comm_allreduce_u64": (C.c_int32, [P(C.c_uint64), C.c_int64, C.c_void_p]),
+    "fq_engine_execute_rccl": (C.c_int32, [C.c_void_p, C.c_char_p, C.c_void_p, P(C.c_void_p)]),
+}
+for _n, (_r, _a) in _protos.items():
+    _f = getattr(lib, _n)
+    _f.restype = _r
+    _f.argtypes = _a
 
 
-def allgather_states(states, group=None, device=None, cap=STATE_CAP):
-    """bytes of this rank -> [bytes of rank 0, ..., rank world-1] (one all-reduce;
-    payloads above `cap` -- GROUP BY states grow with the number of groups --
-    first agree on the largest length with a second, 8-byte-per-rank one)."""
+def torch_allreduce_fn(group=None):
+    """An fq_allreduce_fn over a torch.distributed group (keep the returned
+    object alive while the library may call it)."""
+    on_gpu = dist.get_backend(group) == "nccl"
+
+    def cb(ptr, n, _user):
+        try:
+            words = np.ctypeslib.as_array(ptr, shape=(n,)).view(np.int64)
+            t = torch.from_numpy(words)
+            if on_gpu:
+                d = t.cuda()
+                dist.all_reduce(d, op=dist.ReduceOp.SUM, group=group)
+                t.copy_(d.cpu())
+            else:
+                dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)  # in place on the library's words
+            return abi.FQ_OK
+        except Exception:  # the library reports a generic exchange failure
+            return abi.FQ_E_RCCL
+
+    return ALLREDUCE_FN(cb)
+
+
+class RcclComm:
+    """The library's RCCL communicator over all ranks of the default
+    torch.distributed group (which only carries the unique id)."""
+
+    def __init__(self, device, group=None):
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        uid = C.create_string_buffer(COMM_ID_BYTES)
+        if self.rank == 0:
+            check(lib.fq_comm_unique_id(uid))
+        box = [uid.raw if self.rank == 0 else None]
+        dist.broadcast_object_list(box, src=0, group=group)
+        uid = C.create_string_buffer(box[0], COMM_ID_BYTES)
+        h = C.c_void_p()
+        check(lib.fq_comm_init(device, self.world, self.rank, uid, C.byref(h)))
+        self.h = h
+
+    def allreduce_(self, words):
+        """In-place wrapping u64 sum of a numpy uint64 array over all ranks."""
+        assert words.dtype == np.uint64 and words.flags.c_contiguous
+        check(lib.fq_comm_allreduce_u64(words.ctypes.data_as(P(C.c_uint64)), words.size, self.h))
+        return words
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib.fq_comm_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def allgather_states(states, group=None):
+    """bytes of this rank -> [bytes of rank 0, ..., rank world-1] (zero padded
+    to a common stride) through the native exchange over `group`."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
-    if device is None:
-        device = "cuda" if dist.get_backend(group) == "nccl" else "cpu"
-    if len(states) > cap or cap != STATE_CAP:
-        lens = torch.zeros(world, dtype=torch.int64, device=device)
-        lens[rank] = len(states)
-        dist.all_reduce(lens, op=dist.ReduceOp.SUM, group=group)
-        cap = max(cap, (int(lens.max().item()) + 7) // 8 * 8)
-    buf = torch.zeros((world, cap // 8), dtype=torch.int64, device=device)
-    row = torch.frombuffer(bytearray(states.ljust(cap, b"\0")), dtype=torch.int64)
-    buf[rank].copy_(row)
-    dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group)
-    host = buf.cpu().numpy()
-    return [host[r].tobytes() for r in range(world)]
+    fn = torch_allreduce_fn(group)
+    rows, stride = C.c_void_p(), C.c_size_t()
+    check(lib.fq_exchange_states(states, len(states), rank, world, fn, None, C.byref(rows), C.byref(stride)))
+    blob = C.string_at(rows, stride.value * world)
+    return [blob[r * stride.value:(r + 1) * stride.value] for r in range(world)]
 
 
-def execute(engine, sql, group=None):
-    """Run an aggregate query across all ranks of `group`: local partial on this
-    rank's shard -> one all-reduce -> AggregateFinal merge in rank order."""
-    world = dist.get_world_size(group)
-    rank = dist.get_rank(group)
-    local = engine.execute_partial(sql, rank, world)
-    everyone = allgather_states(local, group)
-    return engine.execute_final(sql, everyone)
+def execute(engine, sql, comm=None, group=None):
+    """Run an aggregate query across all ranks: local partial on this rank's
+    shard -> exchange -> AggregateFinal merge in rank order.  `comm` is an
+    RcclComm (native RCCL) or None (the torch.distributed `group`)."""
+    out = C.c_void_p()
+    if comm is not None:
+        check(lib.fq_engine_execute_rccl(engine.h, sql.encode(), comm.h, C.byref(out)))
+    else:
+        fn = torch_allreduce_fn(group)
+        check(lib.fq_engine_execute_exchange(engine.h, sql.encode(), dist.get_rank(group),
+                                             dist.get_world_size(group), fn, None, C.byref(out)))
+    return Result(out)

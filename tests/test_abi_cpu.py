@@ -17,6 +17,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def declared_symbols(header):
     src = open(os.path.join(ROOT, "include", header)).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)  # declarations only, not comments
+    src = re.sub(r"^\s*typedef[^;]*;", "", src, flags=re.M)  # function-pointer types are not exports
     return sorted(set(re.findall(r"^\s*(?:[\w\s\*]+?)\b(fq_\w+)\s*\(", src, re.M)))
 
 
@@ -31,6 +32,11 @@ def test_library_exports_every_declared_symbol(header):
 
 def test_gpu_symbol_list_matches_header():
     assert sorted(GPU_SYMBOLS) == declared_symbols("fq_gpu.h")
+
+
+def test_comm_symbol_list_matches_header():
+    from fq_amd.dist import COMM_SYMBOLS
+    assert sorted(COMM_SYMBOLS) == declared_symbols("fq_comm.h")
 
 
 def test_abi_version_and_struct_sizes():

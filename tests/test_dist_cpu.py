@@ -1,7 +1,7 @@
 """CPU, world_size 2 (and 3) over gloo: the multi-GPU path minus the GPU.
 Each rank owns its numbers_mt shard [8r/G, 8(r+1)/G) (fq_amd.numbers.shard),
 ships its merged partial states through fq_amd.dist.allgather_states (the
-same single all-reduce bench.py runs over RCCL), and every rank's
+native fq_exchange_states protocol bench.py runs over RCCL), and every rank's
 AggregateFinal merge must equal the single-process oracle result.  The
 per-rank partial states come from the oracle: without a GPU the scan cannot
 run, and there is no CPU fallback to run it with."""
@@ -126,3 +126,45 @@ def test_group_by_exchange_and_final_merge():
     for rank, rows, nbytes in results:
         assert nbytes > 4096
         assert rows == exp, rank
+
+
+def ragged_worker(rank, world, port, lens, out_q):
+    for p in (os.path.join(ROOT, "fuse-query_amd"),):
+        sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+
+    from fq_amd import dist as fqd
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        mine = bytes((rank * 31 + i) % 251 + 1 for i in range(lens[rank]))
+        rows = fqd.allgather_states(mine)
+        out_q.put((rank, rows))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("lens", [(5000, 40), (0, 0, 7), (4096, 4097, 1), (10, 20)])
+def test_exchange_protocol_ragged_lengths(lens):
+    """fq_exchange_states: every rank takes the same number of all-reduces
+    even when only SOME ranks' states exceed the 4 KB first round (a per-rank
+    decision would leave the others waiting in a collective)."""
+    world = len(lens)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=ragged_worker, args=(r, world, port, lens, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    stride = 4096 if max(lens) <= 4096 else (max(lens) + 7) // 8 * 8
+    for rank, rows in results:
+        assert len(rows) == world
+        for r, row in enumerate(rows):
+            exp = bytes((r * 31 + i) % 251 + 1 for i in range(lens[r]))
+            assert len(row) == stride and row[:lens[r]] == exp and not any(row[lens[r]:]), (rank, r)

@@ -1,8 +1,9 @@
 """The multi-rank path ON THE GPU: 2 processes share cuda:0 (one box has one
 GPU), each runs its numbers_mt shard through fq_engine_execute_partial (the
-fused scans / GROUP BY kernels), the states go through
-fq_amd.dist.allgather_states over gloo (bench.py uses the same call over
-RCCL), and every rank's final merge must equal the single-process oracle."""
+fused scans / GROUP BY kernels), the states go through the native exchange
+(fq_engine_execute_exchange) over gloo -- bench.py runs the same protocol over
+the library's RCCL communicator -- and every rank's final merge must equal the
+single-process oracle."""
 import os
 import socket
 import sys
@@ -78,3 +79,57 @@ def test_two_ranks_on_the_gpu_match_the_oracle():
         assert out[0] == exp3, rank
         assert out[1] == exp4, rank
         assert out[2] == expg, rank
+
+
+def rccl_worker(port, n, out_q):
+    for p in (os.path.join(ROOT, "fuse-query_amd"),):
+        sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import ctypes as C
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from fq_amd import dist as fqd
+    from fq_amd._lib import check, lib
+    from fq_amd.engine import Engine
+
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        comm = fqd.RcclComm(0)
+        r, w = C.c_int32(-1), C.c_int32(-1)
+        check(lib.fq_comm_info(comm.h, C.byref(r), C.byref(w)))
+        words = np.array([1, 2**64 - 1, 12345], dtype=np.uint64)
+        host = comm.allreduce_(words.copy()).tolist()
+        d = torch.arange(1000, dtype=torch.int64, device="cuda")
+        s = torch.cuda.current_stream()
+        check(lib.fq_state_allreduce(comm.h, C.c_void_p(d.data_ptr()), d.numel(), C.c_void_p(s.cuda_stream)))
+        torch.cuda.synchronize()
+        dev_ok = bool((d.cpu() == torch.arange(1000)).all())
+        with Engine(device=0) as eng:
+            out = [(fqd.execute(eng, sql % n, comm).rows, eng.execute(sql % n).rows) for sql in SQLS]
+        comm.close()
+        out_q.put(((r.value, w.value), host, dev_ok, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_native_rccl_comm_single_rank():
+    """The library's own RCCL communicator (fq_comm_init / fq_state_allreduce /
+    fq_engine_execute_rccl) at world 1 -- the box has one GPU and RCCL refuses
+    two ranks on one device; bench.py runs the same calls at 2..8 ranks."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=rccl_worker, args=(free_port(), 3_000_017, q))
+    p.start()
+    info, host, dev_ok, out = q.get(timeout=300)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    assert info == (0, 1)
+    assert host == [1, 2**64 - 1, 12345]
+    assert dev_ok
+    for dist_rows, local_rows in out:
+        assert dist_rows == local_rows
