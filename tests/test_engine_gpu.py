@@ -136,6 +136,37 @@ def test_c2_c3_c4_full_size_closed_forms():
         E.release_numbers()
 
 
+def _range_closed_forms(b, e):
+    """C3 + C4 results over the rows [b, e) of numbers_mt (no dropped rows)."""
+    s = ((b + e - 1) * (e - b) // 2) % 2**64
+    top = e - 1
+    while top % 8 >= 3:
+        top -= 1
+    kept = sum(max(0, (e - r + 7) // 8 - (b - r + 7) // 8) for r in range(3))
+    return s, e - b, e - 1, b, top + 1, kept
+
+
+@pytest.mark.parametrize("world,rank", [(2, 1), (4, 3), (8, 7)])
+def test_weak_scaling_shard_beyond_2_pow_32_rows(world, rank):
+    # bench.py at N GPUs: numbers_mt(1e10 * N), rank r owns partitions
+    # [8r/N, 8(r+1)/N) -- 2.5e9 / 5e9 / 1e10-row partitions (> 2^31 and 2^32
+    # rows per launch, values up to 8e10), which the 1-GPU run never reaches
+    n = 10_000_000_000 * world
+    per = n // 8
+    b, e = per * 8 * rank // world, per * 8 * (rank + 1) // world
+    E.materialize_numbers(n, rank, world)
+    try:
+        sql3 = "SELECT sum(number), count(number), max(number), min(number) FROM system.numbers_mt(%d)" % n
+        sql4 = "SELECT max(number+1), count(number) FROM system.numbers_mt(%d) WHERE (number%%8)<3" % n
+        s, c, mx, mn, m4, k4 = _range_closed_forms(b, e)
+        assert E.execute_final(sql3, [E.execute_partial(sql3, rank, world)]).rows == [(s, c, mx, mn)]
+        assert E.execute_final(sql4, [E.execute_partial(sql4, rank, world)]).rows == [(m4, k4)]
+        st = E.stats()
+        assert st["scan_rows"] > 0
+    finally:
+        E.release_numbers()
+
+
 # ---- expression shapes beyond the fused chain ------------------------------
 
 def test_non_chain_argument_uses_materialised_path():
