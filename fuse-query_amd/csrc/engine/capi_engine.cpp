@@ -2,7 +2,9 @@
 #include <string.h>
 
 #include <memory>
+#include <mutex>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../fq_common.h"
@@ -24,6 +26,11 @@ struct fq_engine {
     std::shared_ptr<fq::DataSource> ds;
     size_t worker_threads = 8;
     bool modulo = true;
+    // Plans of recently seen statements (the reference re-parses every query;
+    // a plan is a pure function of the text and the planner options, so a
+    // repeated statement skips the parser and PlanBuilder).
+    std::mutex plan_mu;
+    std::unordered_map<std::string, fq::QueryPlan> plans;
 };
 
 namespace {
@@ -51,6 +58,22 @@ fq::QueryContextRef make_ctx(fq_engine *e, int rank, int world) {
     c->rank = rank;
     c->world = world;
     return c;
+}
+
+fq::QueryPlan plan_for(fq_engine *e, const char *sql, const fq::QueryContext &qctx) {
+    std::string key(sql);
+    key += '\0';
+    key += std::to_string(qctx.factory.modulo) + "/" + std::to_string(qctx.worker_threads);
+    {
+        std::lock_guard<std::mutex> lk(e->plan_mu);
+        auto it = e->plans.find(key);
+        if (it != e->plans.end()) return it->second;
+    }
+    fq::QueryPlan plan = fq::build_from_sql(sql, qctx);  // errors are not cached
+    std::lock_guard<std::mutex> lk(e->plan_mu);
+    if (e->plans.size() >= 256) e->plans.clear();
+    e->plans.emplace(std::move(key), plan);
+    return plan;
 }
 
 void append_block(fq_result *r, const fq::DataBlock &b0, fq::ExecCtx &ctx) {
@@ -149,7 +172,7 @@ fq_status fq_engine_execute(fq_engine *e, const char *sql, fq_result **out) {
         const int64_t t0 = fq::now_ns();
         e->rt->stats.query_t0 = t0;
         auto qctx = make_ctx(e, 0, 1);
-        fq::QueryPlan plan = fq::build_from_sql(sql, *qctx);
+        fq::QueryPlan plan = plan_for(e, sql, *qctx);
         auto r = std::make_unique<fq_result>();
         if (plan.explain) {  // ExplainExecutor (executor_explain.rs:38-59)
             fq::Pipeline p = fq::build_pipeline(plan, qctx);
@@ -196,7 +219,7 @@ fq_status fq_engine_explain(fq_engine *e, const char *sql, char *buf, size_t cap
     return guard([&] {
         fq::ExecCtx ctx(e->rt.get());
         auto qctx = make_ctx(e, 0, 1);
-        fq::QueryPlan plan = fq::build_from_sql(sql, *qctx);
+        fq::QueryPlan plan = plan_for(e, sql, *qctx);
         fq::Pipeline p = fq::build_pipeline(plan, qctx);
         const std::string s = plan.display() + "\n" + p.display();
         if (len) *len = s.size();
@@ -215,7 +238,7 @@ fq_status fq_engine_execute_partial(fq_engine *e, const char *sql, int32_t rank,
     return guard([&] {
         fq::ExecCtx ctx(e->rt.get());
         auto qctx = make_ctx(e, rank, world);
-        fq::QueryPlan plan = fq::build_from_sql(sql, *qctx);
+        fq::QueryPlan plan = plan_for(e, sql, *qctx);
         if (plan.explain || !aggregate_node(plan))
             throw fq::FQException(FQ_E_UNSUPPORTED, "distributed execution covers aggregate queries only");
         fq::QueryPlan partial = plan;
@@ -256,7 +279,7 @@ fq_status fq_engine_execute_final(fq_engine *e, const char *sql, const void *sta
     return guard([&] {
         fq::ExecCtx ctx(e->rt.get());
         auto qctx = make_ctx(e, 0, 1);
-        fq::QueryPlan plan = fq::build_from_sql(sql, *qctx);
+        fq::QueryPlan plan = plan_for(e, sql, *qctx);
         const fq::PlanNode *agg = aggregate_node(plan);
         if (plan.explain || !agg) throw fq::FQException(FQ_E_UNSUPPORTED, "distributed execution covers aggregate queries only");
         std::vector<fq::DataBlock> blocks;

@@ -70,11 +70,13 @@ _VALUE_NP = np.dtype([("dtype", "<i4"), ("is_some", "<i4"), ("bits", "<u8")])
 
 def _column_values(ptr, c, nrow):
     """One column of a result as Python values (None for NULL), fetched in
-    one fq_result_values call and converted with numpy."""
+    one fq_result_values call (numpy conversion for long columns)."""
     if nrow == 0:
         return []
     arr = (abi.fq_value * nrow)()
     check(lib.fq_result_values(ptr, c, arr, nrow))
+    if nrow <= 64:  # aggregate results: a plain loop beats numpy's setup cost
+        return [from_bits(v.bits, v.dtype) if v.is_some else None for v in arr]
     a = np.frombuffer(arr, dtype=_VALUE_NP)
     dts = np.unique(a["dtype"])
     if len(dts) == 1 and bool(a["is_some"].all()):
@@ -111,21 +113,42 @@ class Result:
                 cols.append(_column_values(ptr, c, nrow))
             self.columns = cols
             self.rows = [tuple(col[r] for col in cols) for r in range(nrow)]
-            # what the reference's MySQL writer sends (mysql_stream.rs:21-84):
-            # column types, or the error it raises, and the text of every value
-            self.mysql_types, self.mysql_error = [], None
-            for c in range(ncol):
-                t = C.c_int32(0)
-                if lib.fq_result_mysql_type(ptr, c, C.byref(t)) != 0:
-                    self.mysql_error = last_error()
-                    break
-                self.mysql_types.append(t.value)
+            # what the reference's MySQL writer sends (mysql_stream.rs:21-84) is
+            # read on first use (mysql_types / mysql_error), like the text form
+            self._mysql = None
             # the text form is built on first use (the handle stays open until then)
             self._ptr, ptr = ptr, None
             self._text = None
         finally:
             if ptr is not None:
                 lib.fq_result_free(ptr)
+
+    def _mysql_info(self):
+        if self._mysql is None:
+            types, err = [], None
+            for c in range(len(self.names)):
+                t = C.c_int32(0)
+                if lib.fq_result_mysql_type(self._handle(), c, C.byref(t)) != 0:
+                    err = last_error()
+                    break
+                types.append(t.value)
+            self._mysql = (types, err)
+        return self._mysql
+
+    @property
+    def mysql_types(self):
+        """Column types the reference's MySQL writer declares (mysql_stream.rs:30-62)."""
+        return self._mysql_info()[0]
+
+    @property
+    def mysql_error(self):
+        """The error that writer raises for this result, or None."""
+        return self._mysql_info()[1]
+
+    def _handle(self):
+        if self._ptr is None:
+            raise RuntimeError("result handle already released")
+        return self._ptr
 
     @property
     def text_rows(self):
@@ -134,6 +157,7 @@ class Result:
             ncol, nrow = len(self.names), len(self.rows)
             self._text = [tuple((lambda t: t.decode() if t is not None else None)(lib.fq_result_text(self._ptr, r, c))
                                 for c in range(ncol)) for r in range(nrow)]
+            self._mysql_info()  # everything read from the handle before it goes
             self._free()
         return self._text
 
