@@ -70,6 +70,7 @@ fq::QueryPlan plan_for(fq_engine *e, const char *sql, const fq::QueryContext &qc
         if (it != e->plans.end()) return it->second;
     }
     fq::QueryPlan plan = fq::build_from_sql(sql, qctx);  // errors are not cached
+    fq::optimize(plan);  // mysql_handler.rs:58: every statement is optimised before execution
     std::lock_guard<std::mutex> lk(e->plan_mu);
     if (e->plans.size() >= 256) e->plans.clear();
     e->plans.emplace(std::move(key), plan);

@@ -516,6 +516,54 @@ QueryPlan build_from_sql(const std::string &sql, const QueryContext &ctx) {
     return qp;
 }
 
+// ---------------------------------------------------------------------------
+// Optimizer::create().optimize (optimizer.rs:20-32): the one optimizer the
+// reference registers, FilterPushDownOptimizer
+// (optimizer_filter_push_down.rs:18-81), run by the MySQL handler between
+// planning and execution (mysql_handler.rs:58).
+// ---------------------------------------------------------------------------
+namespace {
+
+// rewrite_alias_expr (optimizer_filter_push_down.rs:18-36): children first,
+// then a Field naming a projection output becomes that output's expression
+// (Alias stripped by projections_to_map, optimizer.rs:40-47).
+ExpressionPlan rewrite_alias_expr(const ExpressionPlan &e, const std::vector<std::pair<std::string, ExpressionPlan>> &proj) {
+    if (e.kind == ExpressionPlan::kField) {
+        // HashMap::insert keeps the last field of a repeated name
+        for (size_t i = proj.size(); i-- > 0;)
+            if (proj[i].first == e.name) return proj[i].second;
+        return e;
+    }
+    // expression_plan_children / rebuild_alias_from_exprs (optimizer.rs:59-70,
+    // optimizer_filter_push_down.rs:38-60); constants and `*` have no children
+    ExpressionPlan out = e;
+    for (auto &a : out.args) a = rewrite_alias_expr(a, proj);
+    return out;
+}
+
+}  // namespace
+
+void optimize(QueryPlan &plan) {
+    // projections_to_map (optimizer.rs:36-57): from the top of the plan down
+    // through Limit / Filter / Aggregate to the first Projection
+    std::vector<std::pair<std::string, ExpressionPlan>> proj;
+    for (size_t k = plan.nodes.size(); k-- > 0;) {
+        const PlanNode &n = plan.nodes[k];
+        if (n.kind == PlanNode::kProjection) {
+            for (size_t i = 0; i < n.schema->fields.size() && i < n.exprs.size(); ++i) {
+                const ExpressionPlan &x = n.exprs[i];
+                proj.emplace_back(n.schema->fields[i].name, x.kind == ExpressionPlan::kAlias ? x.args[0] : x);
+            }
+            break;
+        }
+        if (n.kind == PlanNode::kReadSource) break;
+    }
+    // every Filter's predicate is rewritten (node_to_plans / plans_to_node
+    // rebuild the same chain; only the predicate changes)
+    for (PlanNode &n : plan.nodes)
+        if (n.kind == PlanNode::kFilter) n.predicate = rewrite_alias_expr(n.predicate, proj);
+}
+
 std::string QueryPlan::display() const {
     std::string out;
     size_t indent = 0;

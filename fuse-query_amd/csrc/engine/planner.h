@@ -49,6 +49,10 @@ struct QueryPlan {
 
 QueryPlan build_from_sql(const std::string &sql, const QueryContext &ctx);
 
+// Optimizer::create().optimize: FilterPushDownOptimizer (aliases in WHERE
+// replaced by the projected expressions), optimizer_filter_push_down.rs
+void optimize(QueryPlan &plan);
+
 // PipelineBuilder::build; emit_states = distributed partial (see fq_engine.h)
 Pipeline build_pipeline(const QueryPlan &plan, const QueryContextRef &ctx, bool emit_states = false);
 

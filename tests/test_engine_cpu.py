@@ -47,6 +47,34 @@ def test_explain_plan_and_pipeline_text(eng):
         "\n          └─ FilterTransform × 8 processors\n            └─ SourceTransform × 8 processors")
 
 
+README_ALIAS_SQL = ("select (number+1) as c1, number/2 as c2 from system.numbers_mt(10000000) "
+                    "where (c1+c2+1) < 100 limit 3")  # README.md:96, verbatim
+
+
+def test_filter_push_down_optimizer(eng):
+    # optimizers/optimizer_filter_push_down_test.rs:19-32: aliases in WHERE are
+    # replaced by the projected expressions
+    txt = eng.explain("select (number+1) as c1, number as c2 from system.numbers_mt where (c1+c2+1)=1")
+    assert txt.startswith("└─ Projection: (number + 1) as c1, number as c2"
+                          "\n  └─ Filter: ((((number + 1) + number) + 1) = 1)"
+                          "\n    └─ ReadDataSource: scan parts [8](Read from system.numbers_mt table)\n")
+
+
+def test_readme_explain_with_aliases(eng):
+    # README.md:96-113: the optimised plan of the aliased statement is the one
+    # the README prints
+    assert eng.explain(README_ALIAS_SQL) == eng.explain(README_SQL)
+    assert eng.explain("explain " + README_ALIAS_SQL) == eng.explain(README_SQL)
+
+
+def test_filter_push_down_leaves_other_fields(eng):
+    # a Field that names no projection output stays; an aggregate plan's map
+    # is built below the Aggregate (optimizer.rs:48-50) and is empty here
+    assert "Filter: (number > 1)" in eng.explain(
+        "select number+1 as c1 from system.numbers_mt(100) where number > 1")
+    assert "Filter: (c1 > 1)" in eng.explain("select sum(number) as c1 from system.numbers_mt(100) where c1 > 1")
+
+
 def test_explain_worker_threads_chunking():
     # pipeline_builder.rs:75-84: workers < partitions -> chunks of parts/workers per source
     with Engine(device=-1, worker_threads=2) as e:

@@ -61,10 +61,17 @@ def test_source_reads_all_rows():
 
 
 def test_readme_projection_filter_limit():
-    # README.md:120-127 (alias push-down is the optimizer's job, out of scope:
-    # the WHERE spells the aliased expressions out)
+    # README.md:120-127 with the aliased expressions spelled out
     r = q("select (number+1) as c1, number/2 as c2 from system.numbers_mt(10000000) "
           "where ((number+1)+(number/2)+1) < 100 limit 3")
+    assert r.names == ["c1", "c2"]
+    assert r.rows == [(1, 0), (2, 0), (3, 1)]
+
+
+def test_readme_query_verbatim_with_aliases():
+    # README.md:116-127: the WHERE uses the projection's aliases; the
+    # FilterPushDownOptimizer (optimizer_filter_push_down.rs) rewrites them
+    r = q("select (number+1) as c1, number/2 as c2 from system.numbers_mt(10000000) where (c1+c2+1) < 100 limit 3")
     assert r.names == ["c1", "c2"]
     assert r.rows == [(1, 0), (2, 0), (3, 1)]
 
