@@ -41,9 +41,10 @@ METRIC = "rows/s + achieved HBM GB/s on 10B-row numbers_mt agg, 1/2/4/8 GPUs"
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # reference README.md:57 / :62 (8 vCPU KVM), BASELINE.md section 1: the only
 # published numbers for these exact queries (sum; sum/count, max, min)
-README_ROWS_PER_S = {"c2": 1e10 / 1.77, "c3": 1e10 / 6.40}
-README_REF = {"c2": "reference README.md:57 (1.77 s for 1e10 rows, 8 vCPU KVM)",
-              "c3": "reference README.md:62 (6.40 s for 1e10 rows, 8 vCPU KVM)"}
+README_SECONDS = {"c2": (1.77, 57), "max": (2.83, 58), "max1": (6.13, 59), "avg": (2.04, 61), "c3": (6.40, 62)}
+README_ROWS_PER_S = {q: 1e10 / t for q, (t, _) in README_SECONDS.items()}
+README_REF = {q: "reference README.md:%d (%.2f s for 1e10 rows, 8 vCPU KVM)" % (line, t)
+              for q, (t, line) in README_SECONDS.items()}
 U64 = 2**64
 
 QUERIES = {
@@ -51,6 +52,11 @@ QUERIES = {
     "c3": ("SELECT sum(number)/count(number), max(number), min(number) FROM system.numbers_mt({N})",
            abi.AGG_SUM | abi.AGG_COUNT | abi.AGG_MAX | abi.AGG_MIN),
     "c4": ("SELECT max(number+1) FROM system.numbers_mt({N}) WHERE (number%8)<3", abi.AGG_MAX | abi.AGG_COUNT),
+    # the README's other timed queries (README.md:58-61; count(number) aside:
+    # it needs no column read)
+    "max": ("SELECT max(number) FROM system.numbers_mt({N})", abi.AGG_MAX),
+    "max1": ("SELECT max(number+1) FROM system.numbers_mt({N})", abi.AGG_MAX),
+    "avg": ("SELECT sum(number) / count(number) FROM system.numbers_mt({N})", abi.AGG_SUM | abi.AGG_COUNT),
     # not a BASELINE config: filtered SUM, which needs the per-block emptiness
     # of the reference's state machine (block-mode scan)
     "c4s": ("SELECT sum(number+1) FROM system.numbers_mt({N}) WHERE (number%8)<3", abi.AGG_SUM),
@@ -67,6 +73,12 @@ def closed_form(query, n):
         return [s]
     if query == "c3":
         return [s // n, n - 1, 0]
+    if query == "max":
+        return [n - 1]
+    if query == "max1":
+        return [n]
+    if query == "avg":
+        return [s // n]
     if query == "g1":
         per = n // 1000  # n is a multiple of 80,000
         return [(k, per, (k * per + 1000 * per * (per - 1) // 2) % U64, k + 1000 * (per - 1)) for k in range(1000)]
@@ -123,6 +135,12 @@ def cpu_baseline(sample_rows, threads, query="c3"):
         aggs = [(abi.AGG_SUM, None)]
     elif query == "c3":
         aggs = [(abi.AGG_SUM, None), (abi.AGG_COUNT, None), (abi.AGG_MAX, None), (abi.AGG_MIN, None)]
+    elif query == "max":
+        aggs = [(abi.AGG_MAX, None)]
+    elif query == "max1":
+        aggs = [(abi.AGG_MAX, chain(abi.DT_UINT64, [("+", 1)])[0])]
+    elif query == "avg":
+        aggs = [(abi.AGG_SUM, None), (abi.AGG_COUNT, None)]
     else:
         aggs = [(abi.AGG_MAX if query == "c4" else abi.AGG_SUM, chain(abi.DT_UINT64, [("+", 1)])[0])]
         pred = predicate(abi.DT_UINT64, [("%", 8)], "<", 3)
@@ -138,6 +156,8 @@ def cpu_baseline(sample_rows, threads, query="c3"):
     if query == "c3":
         s, c, mx, mn = res
         res = [s // c, mx, mn]
+    elif query == "avg":
+        res = [res[0] // res[1]]
     assert res == closed_form(query, n), "cpu baseline parity"
     cpu = platform.processor() or platform.machine()
     try:
@@ -204,7 +224,19 @@ def main():
     # cross-GPU exchange: the library's own RCCL communicator (torch.distributed
     # only ships its unique id); the gloo rehearsal drives the same native
     # protocol through a torch callback
-    comm = fqd.RcclComm(local) if world > 1 and args.dist_backend == "nccl" else None
+    comm = None
+    if world > 1 and args.dist_backend == "nccl":
+        ok = 1
+        try:
+            comm = fqd.RcclComm(local)
+        except Exception as e:  # reported; the same protocol then runs over torch's RCCL group
+            log(rank, "native RCCL communicator unavailable on rank %d: %r" % (rank, e))
+            ok = 0
+        flag = torch.tensor([ok], dtype=torch.int32, device="cuda")
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        if not int(flag.item()) and comm is not None:  # every rank takes the same transport
+            comm.close()
+            comm = None
 
     def step():
         r = eng.execute(sql) if world == 1 else fqd.execute(eng, sql, comm)
@@ -275,7 +307,8 @@ def main():
                 "path": "fq_engine_execute: SQL -> PipelineBuilder -> Source x P -> AggregatePartial x P "
                         "(fused gfx950 scan) -> Merge -> AggregateFinal"
                         + ("" if world == 1 else " ; cross-GPU: fq_engine_execute_rccl, one ncclAllReduce of partial states"
-                            if comm is not None else " ; cross-GPU: fq_engine_execute_exchange over gloo"),
+                            if comm is not None else " ; cross-GPU: fq_engine_execute_exchange over torch.distributed (%s)"
+                            % args.dist_backend),
                 "parallelism": "dp%d (numbers_mt partitions sharded, %s all-reduce of states)"
                                % (world, "RCCL" if args.dist_backend == "nccl" else "gloo rehearsal"),
             },

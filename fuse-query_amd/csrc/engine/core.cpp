@@ -287,6 +287,16 @@ Runtime::Runtime(int device) : device_(device) {
         throw FQException(FQ_E_HIP, "fq_engine: no HIP device " + std::to_string(device) +
                                         " (the device path has no CPU fallback)");
     check_hip(hipSetDevice(device), "hipSetDevice");
+    // Stream-ordered allocations (columns, workspaces) come from the device's
+    // default pool; with its default release threshold of 0 every
+    // synchronisation hands the freed memory back to the driver and the next
+    // morsel maps it again.  Keep up to kPoolKeepBytes cached.
+    hipMemPool_t pool;
+    if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
+        uint64_t keep = kPoolKeepBytes;
+        (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+    }
+    (void)hipGetLastError();
     set_streams(1);
 }
 

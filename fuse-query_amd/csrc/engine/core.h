@@ -178,6 +178,7 @@ class Runtime {
     static constexpr int kHostOnly = -1;  // no GPU: planning and AggregateFinal merges only
     explicit Runtime(int device);
     bool has_device() const { return device_ != kHostOnly; }
+    static constexpr uint64_t kPoolKeepBytes = 8ull << 30;  // default mem pool release threshold
     ~Runtime();
     int device() const { return device_; }
     WorkerRes *acquire();

@@ -88,42 +88,66 @@ bool NumbersTable::pinned(const std::string &part, Column &out) {
 }
 
 // NumbersStream::poll_next (numbers_stream.rs:65-83): one device block per
-// partition (its 10,000-row blocks are kept as sub_block_rows).
+// partition (its 10,000-row blocks are kept as sub_block_rows), or -- for a
+// row pipeline -- the partition's rows as consecutive morsels of growing size
+// (the same rows in the same order; a LIMIT that is satisfied stops pulling
+// after the first few instead of after a whole partition).
 class NumbersStream : public BlockStream {
    public:
-    NumbersStream(NumbersTable *t, SchemaRef s, std::vector<Partition> parts)
-        : t_(t), schema_(std::move(s)), parts_(std::move(parts)) {}
+    NumbersStream(NumbersTable *t, SchemaRef s, std::vector<Partition> parts, bool morsels)
+        : t_(t), schema_(std::move(s)), parts_(std::move(parts)), morsels_(morsels) {}
     bool next(DataBlock &out) override {
-        if (i_ >= parts_.size()) return false;
-        const Partition &p = parts_[i_++];
-        uint64_t total, begin, end;
-        NumbersTable::parse_part(p.name, total, begin, end);
-        if (end - begin + 1 == 0 || end < begin)
-            throw_status(FQ_E_UNSUPPORTED, "numbers_mt partition " + p.name +
-                                               " materialises 2^64 rows in the reference (total - 1 wraps)");
-        const uint64_t rows = NumbersTable::stream_rows(begin, end);
-        Column col;
-        if (!t_->pinned(p.name, col) || (uint64_t)col.len != rows) {
-            ExecCtx &ctx = ExecCtx::current();
-            col = Column::device(FQ_DT_UINT64, (int64_t)rows, ctx.stream());
-            check_fq(fq_fill_numbers_u64((uint64_t *)col.dptr(), begin, rows, ctx.stream()));
+        if (off_ >= rows_) {  // next partition
+            if (i_ >= parts_.size()) return false;
+            const Partition &p = parts_[i_++];
+            uint64_t total, end;
+            NumbersTable::parse_part(p.name, total, begin_, end);
+            if (end - begin_ + 1 == 0 || end < begin_)
+                throw_status(FQ_E_UNSUPPORTED, "numbers_mt partition " + p.name +
+                                                   " materialises 2^64 rows in the reference (total - 1 wraps)");
+            rows_ = NumbersTable::stream_rows(begin_, end);
+            off_ = 0;
+            morsel_ = NumbersTable::kMorselFirst;
+            has_pinned_ = t_->pinned(p.name, pinned_) && (uint64_t)pinned_.len == rows_;
+            if (rows_ == 0) {  // an empty partition still yields its (empty) block
+                emit(Column::device(FQ_DT_UINT64, 0, ExecCtx::current().stream()), out);
+                return true;
+            }
         }
-        out = DataBlock{};
-        out.schema = schema_;
-        out.columns.push_back(col);
-        out.sub_block_rows = (int64_t)kBlockSize;
+        const uint64_t n = morsels_ ? std::min(morsel_, rows_ - off_) : rows_ - off_;
+        Column col;
+        if (has_pinned_) {
+            col = pinned_.slice((int64_t)off_, (int64_t)n);
+        } else {
+            ExecCtx &ctx = ExecCtx::current();
+            col = Column::device(FQ_DT_UINT64, (int64_t)n, ctx.stream());
+            check_fq(fq_fill_numbers_u64((uint64_t *)col.dptr(), begin_ + off_, n, ctx.stream()));
+        }
+        off_ += n;
+        morsel_ = std::min(morsel_ * 2, NumbersTable::kMorselMax);
+        emit(col, out);
         return true;
     }
 
    private:
+    void emit(const Column &col, DataBlock &out) {
+        out = DataBlock{};
+        out.schema = schema_;
+        out.columns.push_back(col);
+        out.sub_block_rows = (int64_t)kBlockSize;
+    }
     NumbersTable *t_;
     SchemaRef schema_;
     std::vector<Partition> parts_;
+    bool morsels_;
     size_t i_ = 0;
+    uint64_t begin_ = 0, rows_ = 0, off_ = 0, morsel_ = 0;
+    bool has_pinned_ = false;
+    Column pinned_;
 };
 
-StreamRef NumbersTable::read(const std::vector<Partition> &parts) {
-    return std::make_unique<NumbersStream>(this, schema_, parts);
+StreamRef NumbersTable::read(const std::vector<Partition> &parts, bool morsels) {
+    return std::make_unique<NumbersStream>(this, schema_, parts, morsels);
 }
 
 DataSource::DataSource() : numbers_(std::make_shared<NumbersTable>()) {
@@ -205,6 +229,10 @@ struct Channel {
         closed = true;
         cv_send.notify_all();
     }
+    bool is_closed() {
+        std::lock_guard<std::mutex> lk(mu);
+        return closed;
+    }
     void wait_all_done() {
         std::unique_lock<std::mutex> lk(mu);
         cv_recv.wait(lk, [&] { return live == 0; });
@@ -245,7 +273,9 @@ StreamRef MergeProcessor::execute() {
                 ExecCtx ctx(rt);
                 StreamRef s = in->execute();
                 DataBlock b;
-                while (s->next(b)) {
+                // the consumer gone (a satisfied LIMIT dropped the merged
+                // stream): stop pulling instead of scanning the rest
+                while (!ch->is_closed() && s->next(b)) {
                     ctx.sync();  // device work of this block done before another thread reads it
                     Channel::Item it;
                     it.block = std::move(b);
@@ -270,7 +300,7 @@ StreamRef MergeProcessor::execute() {
 
 StreamRef SourceTransform::execute() {
     TableRef t = ctx_->get_table(db_, table_);  // transform_source.rs:49-52
-    return t->read(parts_);
+    return t->read(parts_, morsels_);
 }
 
 namespace {

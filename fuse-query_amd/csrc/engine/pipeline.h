@@ -67,7 +67,10 @@ class ITable {  // table.rs:13-22
     virtual std::string name() const = 0;
     virtual SchemaRef schema() const = 0;
     virtual ReadDataSourcePlan read_plan(const DataValue *table_arg) const = 0;
-    virtual StreamRef read(const std::vector<Partition> &parts) = 0;
+    // morsels: the consumer is a row pipeline (Filter/Projection/Limit, no
+    // aggregate), so a partition may be yielded as several consecutive blocks
+    // and a satisfied LIMIT stops the scan early (stream_limit.rs:28-48)
+    virtual StreamRef read(const std::vector<Partition> &parts, bool morsels = false) = 0;
 };
 using TableRef = std::shared_ptr<ITable>;
 
@@ -79,7 +82,11 @@ class NumbersTable : public ITable {
     std::string name() const override { return "numbers_mt"; }
     SchemaRef schema() const override { return schema_; }
     ReadDataSourcePlan read_plan(const DataValue *table_arg) const override;
-    StreamRef read(const std::vector<Partition> &parts) override;
+    StreamRef read(const std::vector<Partition> &parts, bool morsels = false) override;
+    // morsel sizes: the first is kMorselFirst rows, each next one twice the
+    // last up to kMorselMax (multiples of the 10,000-row block)
+    static constexpr uint64_t kMorselFirst = 160000;
+    static constexpr uint64_t kMorselMax = 327680000;
 
     static std::vector<Partition> generate_parts(uint64_t total);
     static void parse_part(const std::string &name, uint64_t &total, uint64_t &begin, uint64_t &end);
@@ -160,8 +167,10 @@ class MergeProcessor : public IProcessor {  // processor_merge.rs:16-94
 
 class SourceTransform : public IProcessor {  // transform_source.rs:14-53
    public:
-    SourceTransform(QueryContextRef ctx, std::string db, std::string table, std::vector<Partition> parts)
-        : ctx_(std::move(ctx)), db_(std::move(db)), table_(std::move(table)), parts_(std::move(parts)) {}
+    SourceTransform(QueryContextRef ctx, std::string db, std::string table, std::vector<Partition> parts,
+                    bool morsels = false)
+        : ctx_(std::move(ctx)), db_(std::move(db)), table_(std::move(table)), parts_(std::move(parts)),
+          morsels_(morsels) {}
     std::string name() const override { return "SourceTransform"; }
     void connect_to(ProcessorRef) override { throw_internal("Cannot call SourceTransform connect_to"); }
     StreamRef execute() override;
@@ -170,6 +179,7 @@ class SourceTransform : public IProcessor {  // transform_source.rs:14-53
     QueryContextRef ctx_;
     std::string db_, table_;
     std::vector<Partition> parts_;
+    bool morsels_;
 };
 
 class FilterTransform : public IProcessor {  // transform_filter.rs:17-77

@@ -605,6 +605,10 @@ std::string QueryPlan::display() const {
 // PipelineBuilder::build (pipeline_builder.rs:26-106)
 Pipeline build_pipeline(const QueryPlan &plan, const QueryContextRef &ctx, bool emit_states) {
     Pipeline p;
+    // no aggregate above the source: the source may stream morsels
+    bool row_pipeline = true;
+    for (const PlanNode &n : plan.nodes)
+        if (n.kind == PlanNode::kAggregate) row_pipeline = false;
     for (const PlanNode &n : plan.nodes) {
         switch (n.kind) {
             case PlanNode::kLimit: {
@@ -677,7 +681,7 @@ Pipeline build_pipeline(const QueryPlan &plan, const QueryContextRef &ctx, bool 
                 workers = (workers == 0 || workers >= parts.size()) ? 1 : parts.size() / workers;
                 for (size_t i = 0; i < parts.size(); i += workers) {
                     std::vector<Partition> chunk(parts.begin() + i, parts.begin() + std::min(parts.size(), i + workers));
-                    p.add_source(std::make_shared<SourceTransform>(ctx, n.read.db, n.read.table, chunk));
+                    p.add_source(std::make_shared<SourceTransform>(ctx, n.read.db, n.read.table, chunk, row_pipeline));
                 }
                 if (parts.empty()) p.add_source(std::make_shared<BlocksProcessor>(std::vector<DataBlock>{}));
                 break;

@@ -341,3 +341,52 @@ def test_logic_projection_and_errors():
         "Internal Error: Cannot downcast_array from datatype:UInt64 item to:BooleanArray"
     assert err("SELECT count(number) FROM system.numbers_mt(100) WHERE number > 3 AND 1") == \
         "Internal Error: Cannot do data_array and, left:Boolean, right:UInt64"
+
+
+# ---- row pipelines stream morsels; a satisfied LIMIT stops early -----------
+
+def _stream_rows(total):
+    """Rows numbers_mt(total) yields, partition by partition (fq_ref restates
+    numbers_table.rs / numbers_stream.rs, quirk included)."""
+    import fq_ref as R
+    out = []
+    for b, e in R.generate_parts(total):
+        for bb, be in R.numbers_blocks(b, e):
+            out.extend(range(bb, be + 1))
+    return out
+
+
+@pytest.mark.parametrize("total", [8, 100001, 1_280_000, 25_600_001])
+def test_projection_morsels_cover_every_row_in_order(total):
+    # one partition = several morsels (160,000 rows, then doubling): the rows of
+    # each partition arrive complete and in order
+    import fq_ref as R
+    r = E.execute("SELECT number, number+1 FROM system.numbers_mt(%d) WHERE number %% 97 = 5" % total)
+    got = [a for a, _ in r.rows]
+    assert all(b == a + 1 for a, b in r.rows)
+    exp = [x for x in _stream_rows(total) if x % 97 == 5]
+    assert sorted(got) == exp
+    # within a partition the order is the stream's
+    for b, e in R.generate_parts(total):
+        part = [x for x in got if b <= x <= e]
+        assert part == sorted(part)
+
+
+def test_limit_over_ten_billion_rows_stops_early():
+    # README.md:116-127 at numbers_mt(1e10), nothing resident: the pipes stop
+    # after their first morsels (the reference's LimitStream stops pulling),
+    # instead of materialising 8 x 10 GB partitions
+    import time
+    e = Engine()
+    try:
+        t = time.perf_counter()
+        r = e.execute("select (number+1) as c1, number/2 as c2 from system.numbers_mt(10000000000) "
+                      "where (c1+c2+1) < 100 limit 3")
+        dt = time.perf_counter() - t
+        assert r.rows == [(1, 0), (2, 0), (3, 1)]
+        r = e.execute("SELECT number FROM system.numbers_mt(10000000000) LIMIT 5")
+        assert len(r.rows) == 5
+        assert all(v % 1250000000 < 160000 for (v,) in r.rows)  # first morsel of some partition
+        assert dt < 5.0, dt
+    finally:
+        e.close()
