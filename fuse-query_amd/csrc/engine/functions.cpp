@@ -581,7 +581,28 @@ FunctionRef function_factory(const std::string &name, std::vector<FunctionRef> a
 // ---------------------------------------------------------------------------
 // predicate evaluation + compaction (FilterTransform::expression_executor)
 // ---------------------------------------------------------------------------
+// A predicate over one 64-bit device column as ONE hipRTC kernel
+// (fq_predicate_bitmap) instead of a kernel per Function node; false when the
+// shape is not fusable or the JIT is off/unavailable (the caller evaluates
+// the Function tree).
+static bool fused_predicate_bitmap(Function &pred, const DataBlock &b, ExecCtx &ctx, Column &out) {
+    FusedPred fp;
+    if (!b.schema || !pred.to_pred(*b.schema, fp)) return false;
+    const Column &c = b.column_by_name(fp.column);
+    if (!c.on_device() || dtype_size(c.dtype) != 8) return false;
+    Column bm = Column::device(FQ_DT_BOOLEAN, c.len, ctx.stream());
+    auto flag = DeviceBuffer::alloc(sizeof(uint32_t), ctx.stream());
+    fq_col ic = c.abi();
+    const fq_status st = fq_predicate_bitmap(&ic, fp.get(), (uint64_t *)bm.dptr(), (uint32_t *)flag->ptr, ctx.stream());
+    if (st == FQ_E_UNSUPPORTED) return false;  // no hipRTC / JIT off / shape outside it: per node (same errors)
+    check_fq(st);
+    out = bm;
+    return true;
+}
+
 Column eval_predicate(Function &pred, const DataBlock &b, ExecCtx &ctx) {
+    Column fused;
+    if (fused_predicate_bitmap(pred, b, ctx, fused)) return fused;
     const ColumnarValue v = pred.eval(b, ctx);
     const int64_t rows = b.num_rows();
     if (!v.is_array) {
@@ -640,6 +661,69 @@ DataBlock materialize(const DataBlock &b, ExecCtx &ctx) {
     nb.filter = nullptr;
     Column bm = eval_predicate(*b.filter, nb, ctx);
     return compact_block(nb, bm, ctx);
+}
+
+// ProjectionTransform over a block with a pending filter (or none): when every
+// projected expression is a chain over the same 64-bit device column, one
+// fq_filter_project call compacts and evaluates them together (the predicate
+// fused too when it is over that column, else its bitmap is evaluated
+// first).  false: not fusable, the caller materialises + evaluates.
+bool project_fused(const DataBlock &b, const std::vector<FunctionRef> &funcs, const SchemaRef &schema, ExecCtx &ctx,
+                   DataBlock &out) {
+    if (funcs.empty() || funcs.size() > FQ_MAX_PROJECT || !b.schema || b.columns.empty()) return false;
+    std::vector<FusedChain> chains(funcs.size());
+    bool computes = false;
+    for (size_t j = 0; j < funcs.size(); ++j) {
+        if (!funcs[j]->to_chain(*b.schema, chains[j])) return false;
+        if (chains[j].column != chains[0].column || dtype_size(chains[j].out_dtype) != 8) return false;
+        computes |= chains[j].expr.n_steps > 0;
+    }
+    if (!b.filter && !computes) return false;  // plain column references: zero-copy in the unfused path
+    const Column &c = b.column_by_name(chains[0].column);
+    if (!c.on_device() || dtype_size(c.dtype) != 8 || c.dtype == FQ_DT_BOOLEAN) return false;
+    fq_jit_stats js{};
+    if (fq_jit_get_stats(&js) != FQ_OK || js.mode == FQ_JIT_OFF || js.available == 0) return false;
+    FusedPred fp;
+    fq_pred bp{};
+    const fq_pred *pred = nullptr;
+    Column bm;
+    if (b.filter) {
+        if (b.filter->to_pred(*b.schema, fp) && fp.column == chains[0].column) {
+            pred = fp.get();
+        } else {
+            DataBlock nb = b;
+            nb.filter = nullptr;
+            bm = eval_predicate(*b.filter, nb, ctx);
+            bp.kind = FQ_PRED_BITMAP;
+            bp.bitmap = (const uint64_t *)bm.dptr();
+            pred = &bp;
+        }
+    }
+    const int64_t n = c.len;
+    std::vector<Column> outs;
+    std::vector<void *> ptrs;
+    std::vector<fq_expr> exprs;
+    for (auto &fc : chains) {
+        outs.push_back(Column::device(fc.out_dtype, n, ctx.stream()));
+        ptrs.push_back(outs.back().dptr());
+        exprs.push_back(fc.expr);
+    }
+    const size_t wsb = fq_filter_project_workspace_bytes(n);
+    auto ws = DeviceBuffer::alloc(wsb, ctx.stream());
+    fq_col ic = c.abi();
+    int64_t kept = 0;
+    const fq_status st = fq_filter_project(&ic, pred, exprs.data(), (int32_t)exprs.size(), ptrs.data(), &kept, ws->ptr,
+                                           wsb, ctx.stream());
+    if (st == FQ_E_UNSUPPORTED) return false;  // the unfused path evaluates it (and raises what the reference does)
+    check_fq(st);
+    out = DataBlock{};
+    out.schema = schema;
+    out.sub_block_rows = 0;
+    for (auto &o : outs) {
+        o.len = kept;
+        out.columns.push_back(o);
+    }
+    return true;
 }
 
 // ---------------------------------------------------------------------------

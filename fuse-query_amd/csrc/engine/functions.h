@@ -330,7 +330,13 @@ class AggFusion {
     void wait_launched();
 };
 
-// evaluate a predicate over a block into a Boolean column (the non-fused path)
+// evaluate a predicate over a block into a Boolean column (one fused kernel
+// when the predicate is a chain over one 64-bit column, else per node)
 Column eval_predicate(Function &pred, const DataBlock &b, ExecCtx &ctx);
+
+// ProjectionTransform's expressions (and the block's pending filter) through
+// one fq_filter_project call; false when the shape is not fusable
+bool project_fused(const DataBlock &b, const std::vector<FunctionRef> &funcs, const SchemaRef &schema, ExecCtx &ctx,
+                   DataBlock &out);
 
 }  // namespace fq

@@ -344,9 +344,10 @@ StreamRef ProjectionTransform::execute() {
     for (auto &f : funcs_) funcs.push_back(f->clone());
     return std::make_unique<MapStream>(input_->execute(), [schema, funcs](DataBlock b) {
         ExecCtx &ctx = ExecCtx::current();
+        DataBlock out;
+        if (project_fused(b, funcs, schema, ctx, out)) return out;  // filter + expressions in one pass
         b = materialize(b, ctx);
         const int64_t rows = b.num_rows();
-        DataBlock out;
         out.schema = schema;
         for (auto &f : funcs) out.columns.push_back(f->eval(b, ctx).to_array(rows, ctx));
         return out;

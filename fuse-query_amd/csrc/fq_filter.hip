@@ -18,6 +18,7 @@
 
 #include "fq_common.h"
 #include "fq_device.h"
+#include "fq_scan.h"
 
 namespace fqk {
 
@@ -361,6 +362,144 @@ size_t fq_filter_workspace_bytes(int64_t len) {
     const int64_t ntiles = (nwords + fqk::kTileWords - 1) / fqk::kTileWords;
     const int64_t ngroups = (ntiles + fqk::kGroupTiles - 1) / fqk::kGroupTiles;
     return (size_t)(ntiles + ngroups + 1) * sizeof(uint64_t);
+}
+
+}  // extern "C"
+
+namespace fqk {
+namespace {
+
+// Workspace of fq_filter_project: [bitmap words][tile prefixes][group
+// prefixes + total][2 flag words: predicate, expressions].
+struct ProjWs {
+    uint64_t *bitmap, *intra, *gpre;
+    uint32_t *flags;
+    int64_t nwords, ntiles, ngroups;
+};
+
+ProjWs proj_ws(void *d_ws, int64_t n) {
+    ProjWs w;
+    w.nwords = (n + 63) / 64;
+    w.ntiles = (w.nwords + kTileWords - 1) / kTileWords;
+    w.ngroups = (w.ntiles + kGroupTiles - 1) / kGroupTiles;
+    w.bitmap = (uint64_t *)d_ws;
+    w.intra = w.bitmap + w.nwords;
+    w.gpre = w.intra + w.ntiles;
+    w.flags = (uint32_t *)(w.gpre + w.ngroups + 1);
+    return w;
+}
+
+fq_status flag_error(uint32_t f) {
+    if (f & FQ_STATE_DIV_ZERO) return fqc::fail(FQ_E_DIVIDE_BY_ZERO, "Internal Error: Divide by zero error");
+    if (f & FQ_STATE_CAST_NULL)
+        return fqc::fail(FQ_E_UNSUPPORTED, "cast produced nulls (nulls are not supported on the device path)");
+    return FQ_OK;
+}
+
+fq_status lower_projection(const fq_col *col, const fq_pred *pred, const fq_expr *values, int32_t n_out, void *const *d_out,
+                           void *stream, ProjLaunch &P) {
+    if (!col) return fqc::fail(FQ_E_INVALID, "fq_filter_project: NULL column");
+    if (col->len > 0 && !col->data) return fqc::fail(FQ_E_INVALID, "fq_filter_project: NULL column data");
+    if (fqc::dtype_size(col->dtype) != 8 || col->dtype == FQ_DT_BOOLEAN)
+        return fqc::fail(FQ_E_UNSUPPORTED, "fused projection needs a 64-bit numeric column");
+    if (n_out < 0 || n_out > FQ_MAX_PROJECT || (n_out > 0 && (!values || !d_out)))
+        return fqc::fail(FQ_E_INVALID, "fq_filter_project: bad output list");
+    P = ProjLaunch{};
+    P.col = col->data;
+    P.n = col->len;
+    P.stream = (hipStream_t)stream;
+    fq_status s = lower_pred(pred, col->dtype, col->len, true, P.pred);
+    if (s != FQ_OK) return s;
+    P.n_out = n_out;
+    for (int j = 0; j < n_out; ++j) {
+        if (!d_out[j] && col->len > 0) return fqc::fail(FQ_E_INVALID, "fq_filter_project: NULL output");
+        int32_t dt = col->dtype;
+        s = lower_expr(values[j], col->dtype, P.vals[j], dt);
+        if (s != FQ_OK) return s;
+        if (fqc::dtype_size(dt) != 8) return fqc::fail(FQ_E_UNSUPPORTED, "fused projection outputs are 64-bit");
+        P.chain[j] = values[j].n_steps > 0;
+        P.dtypes[j] = dt;
+        P.out[j] = d_out[j];
+    }
+    return FQ_OK;
+}
+
+}  // namespace
+}  // namespace fqk
+
+extern "C" {
+
+size_t fq_filter_project_workspace_bytes(int64_t len) {
+    const fqk::ProjWs w = fqk::proj_ws(nullptr, len < 0 ? 0 : len);
+    return (size_t)(w.nwords + w.ntiles + w.ngroups + 1 + 1) * sizeof(uint64_t);
+}
+
+fq_status fq_filter_project(const fq_col *col, const fq_pred *pred, const fq_expr *values, int32_t n_out,
+                            void *const *d_out, int64_t *out_len, void *d_ws, size_t ws_bytes, void *stream) {
+    using namespace fqk;
+    if (!out_len) return fqc::fail(FQ_E_INVALID, "fq_filter_project: NULL out_len");
+    *out_len = 0;
+    ProjLaunch P;
+    fq_status s = lower_projection(col, pred, values, n_out, d_out, stream, P);
+    if (s != FQ_OK) return s;
+    if (n_out < 1) return fqc::fail(FQ_E_INVALID, "fq_filter_project: no outputs");
+    if (!jit_project_available())
+        return fqc::fail(FQ_E_UNSUPPORTED, "fq_filter_project: hipRTC unavailable or the JIT is off");
+    if ((s = jit_project_prepare(col->dtype, P)) != FQ_OK) return s;
+    const int64_t n = col->len;
+    if (n == 0) return FQ_OK;
+    if (!d_ws || ws_bytes < fq_filter_project_workspace_bytes(n))
+        return fqc::fail(FQ_E_INVALID, "fq_filter_project: workspace too small");
+    const ProjWs w = proj_ws(d_ws, n);
+    hipStream_t st = P.stream;
+    FQ_HIP_TRY(hipMemsetAsync(w.flags, 0, 2 * sizeof(uint32_t), st));
+    uint64_t host[2] = {0, 0};  // kept rows, flag words
+    if (P.pred.kind == FQ_PRED_NONE) {
+        if ((s = jit_project_map(col->dtype, P, w.flags + 1)) != FQ_OK) return s;
+        FQ_HIP_TRY(hipMemcpyAsync(&host[1], w.flags, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+        host[0] = (uint64_t)n;
+    } else {
+        const uint64_t *bm = w.bitmap;
+        if (P.pred.kind == FQ_PRED_BITMAP) bm = P.pred.bitmap;
+        else if ((s = jit_project_bits(col->dtype, P, w.bitmap, w.flags)) != FQ_OK) return s;
+        hipLaunchKernelGGL(compact_count_kernel, dim3((unsigned)w.ngroups), dim3(kTileWords), 0, st, bm, n, w.ntiles,
+                           w.intra, w.gpre);
+        FQ_HIP_TRY(hipGetLastError());
+        hipLaunchKernelGGL(compact_scan_kernel, dim3(1), dim3(kScanThreads), 0, st, w.gpre, w.ngroups);
+        FQ_HIP_TRY(hipGetLastError());
+        if ((s = jit_project_scatter(col->dtype, P, bm, w.intra, w.gpre, w.ntiles, w.flags + 1)) != FQ_OK) return s;
+        // the total (gpre[ngroups]) and the flag words are adjacent
+        FQ_HIP_TRY(hipMemcpyAsync(host, w.gpre + w.ngroups, sizeof(host), hipMemcpyDeviceToHost, st));
+    }
+    FQ_HIP_TRY(hipStreamSynchronize(st));
+    const uint32_t pred_flags = (uint32_t)(host[1] & 0xffffffffu), val_flags = (uint32_t)(host[1] >> 32);
+    if ((s = flag_error(pred_flags)) != FQ_OK) return s;  // FilterTransform runs first
+    if ((s = flag_error(val_flags)) != FQ_OK) return s;
+    *out_len = (int64_t)host[0];
+    return FQ_OK;
+}
+
+fq_status fq_predicate_bitmap(const fq_col *col, const fq_pred *pred, uint64_t *d_bitmap, uint32_t *d_flag,
+                              void *stream) {
+    using namespace fqk;
+    ProjLaunch P;
+    fq_status s = lower_projection(col, pred, nullptr, 0, nullptr, stream, P);
+    if (s != FQ_OK) return s;
+    if (P.pred.kind != FQ_PRED_EXPR && P.pred.kind != FQ_PRED_TREE)
+        return fqc::fail(FQ_E_INVALID, "fq_predicate_bitmap: needs an FQ_PRED_EXPR or FQ_PRED_TREE predicate");
+    if (!jit_project_available())
+        return fqc::fail(FQ_E_UNSUPPORTED, "fq_predicate_bitmap: hipRTC unavailable or the JIT is off");
+    P.n_out = 1;  // the module's shape needs one output; the bits kernel writes none
+    P.dtypes[0] = col->dtype;
+    if ((s = jit_project_prepare(col->dtype, P)) != FQ_OK) return s;
+    if (col->len == 0) return FQ_OK;
+    if (!d_bitmap || !d_flag) return fqc::fail(FQ_E_INVALID, "fq_predicate_bitmap: NULL buffer");
+    FQ_HIP_TRY(hipMemsetAsync(d_flag, 0, sizeof(uint32_t), P.stream));
+    if ((s = jit_project_bits(col->dtype, P, d_bitmap, d_flag)) != FQ_OK) return s;
+    uint32_t h = 0;
+    FQ_HIP_TRY(hipMemcpyAsync(&h, d_flag, sizeof(h), hipMemcpyDeviceToHost, P.stream));
+    FQ_HIP_TRY(hipStreamSynchronize(P.stream));
+    return flag_error(h);
 }
 
 fq_status fq_filter_compact(const fq_col *in, const uint64_t *d_bitmap, void *d_out, int64_t *out_len,

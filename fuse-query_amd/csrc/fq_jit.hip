@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -1012,6 +1013,225 @@ fq_jit_groupby(const TIn *__restrict__ col, long long n, long long head, const u
 }
 
 // ---------------------------------------------------------------------------
+// FilterTransform -> ProjectionTransform over one column (fq_filter_project,
+// fq_predicate_bitmap).  One module per shape holds three kernels:
+//   fq_jit_pbits    predicate -> bitmap: each wave evaluates 8 consecutive
+//                   64-row words per step (lane l = row l of each word, 8-byte
+//                   loads, 8 in flight per lane), one ballot per word, lanes
+//                   0..7 store the 8 words;
+//   fq_jit_pscatter the compaction's scatter (fq_filter.hip's tiles of 256
+//                   words and their count/scan prefixes) with the projection
+//                   evaluated on the kept rows only, one store per output;
+//   fq_jit_pmap     no predicate: every row's outputs, 16-byte loads/stores.
+// ---------------------------------------------------------------------------
+struct HostProjConsts {
+    uint64_t rhs;
+    HostStep p[kSteps], v[FQ_MAX_PROJECT][kSteps];
+    uint64_t rl[FQ_MAX_PRED_LEAVES];
+    HostStep pl[FQ_MAX_PRED_LEAVES][kSteps];
+};
+
+void pack_proj_consts(const ProjLaunch &P, HostProjConsts &hc) {
+    hc.rhs = P.pred.rhs;
+    for (int i = 0; i < kSteps; ++i) {
+        hc.p[i] = HostStep{P.pred.lhs.s[i].c, P.pred.lhs.s[i].magic, P.pred.lhs.s[i].shift};
+        for (int j = 0; j < FQ_MAX_PROJECT; ++j) hc.v[j][i] = HostStep{P.vals[j].s[i].c, P.vals[j].s[i].magic, P.vals[j].s[i].shift};
+    }
+    pack_tree_consts(P.pred, hc);
+}
+
+std::string proj_shape_key(const ProjLaunch &P, int32_t tin, int dev) {
+    std::string k = "PROJ";
+    auto put = [&k](int32_t v) { k.append(reinterpret_cast<const char *>(&v), sizeof v); };
+    put(dev);
+    put(tin);
+    put_pred_key(P.pred, k);
+    put(P.n_out);
+    for (int j = 0; j < P.n_out; ++j) {
+        put(P.dtypes[j]);
+        put(P.chain[j] ? 1 : 0);
+        if (!P.chain[j]) continue;
+        put(P.vals[j].n);
+        for (int i = 0; i < P.vals[j].n; ++i) {
+            const KStep &st = P.vals[j].s[i];
+            put(st.code);
+            put(st.operand);
+            put(st.reversed);
+            put(st.dtype);
+            put((int32_t)st.add);
+        }
+    }
+    return k;
+}
+
+bool gen_project_source(const ProjLaunch &P, int32_t tin, Gen &g, std::string &src) {
+    const char *TIn = ctype(tin);
+    if (!TIn || P.n_out < 1 || P.n_out > FQ_MAX_PROJECT) return false;
+    const int32_t pk = P.pred.kind;
+    std::string pred_body;
+    const bool expr_pred = pk == FQ_PRED_EXPR || pk == FQ_PRED_TREE;
+    if (expr_pred && !emit_pred_body(g, P.pred, tin, pred_body)) return false;
+    src = kCommon;
+    src += "typedef " + std::string(TIn) + " TIn;\n";
+    src += "struct Step { u64 c, m, s; };\nstruct Consts { u64 rhs; Step p[" + std::to_string(kSteps) + "], v[" +
+           std::to_string(FQ_MAX_PROJECT) + "][" + std::to_string(kSteps) + "]; u64 rl[" +
+           std::to_string(FQ_MAX_PRED_LEAVES) + "]; Step pl[" + std::to_string(FQ_MAX_PRED_LEAVES) + "][" +
+           std::to_string(kSteps) + "]; };\n";
+    src += "struct Outs { void *p[" + std::to_string(FQ_MAX_PROJECT) + "]; };\n";
+    src += "typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));\n";
+    src += "__device__ __forceinline__ bool fq_pred(TIn x, const Consts &c, u32 &flags, u32 live) {\n";
+    src += expr_pred ? pred_body : "    (void)x; (void)c; (void)flags; (void)live;\n    return true;\n";
+    src += "}\n";
+    // every output: its value function and its 64-bit store
+    std::string put_all = "__device__ __forceinline__ void fq_put(TIn x, const Consts &c, u32 &flags, u32 live, const Outs &o,\n"
+                          "                                       long long pos) {\n";
+    std::string vals_pair = "__device__ __forceinline__ void fq_put2(TIn x0, TIn x1, const Consts &c, u32 &flags, const Outs &o,\n"
+                            "                                        long long pair) {\n";
+    for (int j = 0; j < P.n_out; ++j) {
+        const char *V = ctype(P.dtypes[j]);
+        if (!V) return false;
+        std::string body;
+        const std::string prefix = "v[" + std::to_string(j) + "]";
+        emit_value_body(g, P.chain[j] ? &P.vals[j] : nullptr, tin, P.dtypes[j], prefix.c_str(), V, body);
+        const std::string J = std::to_string(j);
+        src += std::string("__device__ __forceinline__ ") + V + " fq_val" + J + "(TIn x, const Consts &c, u32 &flags, u32 live) {\n" +
+               "    (void)live;\n" + body + "}\n";
+        put_all += std::string("    ((") + V + " *)o.p[" + J + "])[pos] = fq_val" + J + "(x, c, flags, live);\n";
+        vals_pair += std::string("    { const ") + V + " a = fq_val" + J + "(x0, c, flags, 1u), b = fq_val" + J +
+                     "(x1, c, flags, 1u);\n      __builtin_nontemporal_store(u64x2{__builtin_bit_cast(u64, a), "
+                     "__builtin_bit_cast(u64, b)}, ((u64x2 *)o.p[" + J + "]) + pair); }\n";
+    }
+    src += put_all + "}\n" + vals_pair + "}\n";
+    src += R"(
+__device__ __forceinline__ u32 wave_or(u32 f) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) f |= (u32)__shfl_xor((int)f, off, 64);
+    return f;
+}
+
+extern "C" __global__ void __launch_bounds__(256)
+fq_jit_pbits(const TIn *__restrict__ col, long long n, Consts c, u64 *__restrict__ bm, u32 *__restrict__ fl) {
+    const int lane = threadIdx.x & 63;
+    const long long wave = ((long long)blockIdx.x * 256 + threadIdx.x) >> 6;
+    const long long W = ((long long)gridDim.x * 256) >> 6;
+    const long long nwords = (n + 63) >> 6;
+    u32 flags = 0;
+    for (long long w0 = wave * 8; w0 < nwords; w0 += W * 8) {
+        TIn x[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const long long r = (w0 + k) * 64 + lane;
+            x[k] = r < n ? __builtin_nontemporal_load(col + r) : TIn(0);
+        }
+        u64 mine = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const long long r = (w0 + k) * 64 + lane;
+            const u32 live = r < n ? 1u : 0u;
+            const bool pass = fq_pred(x[k], c, flags, live) && live;
+            const u64 word = __ballot(pass);
+            if (lane == k) mine = word;
+        }
+        if (lane < 8 && w0 + lane < nwords) bm[w0 + lane] = mine;
+    }
+    flags = wave_or(flags);
+    if (lane == 0 && flags) atomicOr(fl, flags);
+}
+
+// tiles of 256 words (16,384 rows): fq_filter.hip's compact_count/scan give
+// each tile's output base (gpre[tile / 16] + intra[tile])
+extern "C" __global__ void __launch_bounds__(256)
+fq_jit_pscatter(const TIn *__restrict__ col, long long n, Consts c, const u64 *__restrict__ bm,
+                const u64 *__restrict__ intra, const u64 *__restrict__ gpre, Outs o, u32 *__restrict__ fl) {
+    const long long nwords = (n + 63) >> 6;
+    const long long w0 = (long long)blockIdx.x * 256;
+    __shared__ u64 s_word[256];
+    __shared__ u32 s_off[256];
+    __shared__ u32 s_wsum[4];
+    const int t = threadIdx.x;
+    const int lane = t & 63;
+    const int wave = t >> 6;
+    u64 word = 0;
+    if (w0 + t < nwords) {
+        word = bm[w0 + t];
+        const long long rows = n - (w0 + t) * 64;
+        if (rows < 64) word &= (1ull << rows) - 1ull;
+    }
+    s_word[t] = word;
+    const u32 cnt = (u32)__popcll(word);
+    u32 incl = cnt;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const u32 v = (u32)__shfl_up((int)incl, off, 64);
+        if (lane >= off) incl += v;
+    }
+    if (lane == 63) s_wsum[wave] = incl;
+    __syncthreads();
+    u32 wave_base = 0;
+    for (int i = 0; i < wave; ++i) wave_base += s_wsum[i];
+    s_off[t] = wave_base + incl - cnt;
+    __syncthreads();
+    const u64 base = gpre[blockIdx.x / 16] + intra[blockIdx.x];
+    const u64 lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    u32 flags = 0;
+    // each wave walks its 64 words, 8 at a time (8 rows per lane in flight)
+    for (int j = 0; j < 64; j += 8) {
+        TIn x[8];
+        u64 wd[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int wi = wave * 64 + j + k;
+            wd[k] = s_word[wi];
+            const long long row = (w0 + wi) * 64 + lane;
+            x[k] = ((wd[k] >> lane) & 1ull) ? __builtin_nontemporal_load(col + row) : TIn(0);
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int wi = wave * 64 + j + k;
+            if ((wd[k] >> lane) & 1ull)
+                fq_put(x[k], c, flags, 1u, o, (long long)(base + s_off[wi] + (u64)__popcll(wd[k] & lt)));
+        }
+    }
+    flags = wave_or(flags);
+    if (lane == 0 && flags) atomicOr(fl, flags);
+}
+
+// every row: 16-byte loads and stores of row pairs when the column and every
+// output are 16-byte aligned (aligned != 0), else 8-byte rows
+extern "C" __global__ void __launch_bounds__(256)
+fq_jit_pmap(const TIn *__restrict__ col, long long n, Consts c, Outs o, int aligned, u32 *__restrict__ fl) {
+    const long long g = (long long)blockIdx.x * 256 + threadIdx.x;
+    const long long T = (long long)gridDim.x * 256;
+    u32 flags = 0;
+    long long done = 0;
+    if (aligned) {
+        const long long npair = n >> 1;
+        const u64x2 *__restrict__ vp = (const u64x2 *)col;
+        for (long long p0 = g; p0 < npair; p0 += 4 * T) {
+            u64x2 raw[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const long long p = p0 + (long long)k * T;
+                raw[k] = p < npair ? __builtin_nontemporal_load(vp + p) : u64x2{0, 0};
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const long long p = p0 + (long long)k * T;
+                if (p < npair)
+                    fq_put2(__builtin_bit_cast(TIn, (u64)raw[k].x), __builtin_bit_cast(TIn, (u64)raw[k].y), c, flags, o, p);
+            }
+        }
+        done = npair * 2;
+    }
+    for (long long i = done + g; i < n; i += T) fq_put(col[i], c, flags, 1u, o, i);
+    flags = wave_or(flags);
+    if ((threadIdx.x & 63) == 0 && flags) atomicOr(fl, flags);
+}
+)";
+    return true;
+}
+
+// ---------------------------------------------------------------------------
 // compile + cache
 // ---------------------------------------------------------------------------
 struct Compiled {
@@ -1208,6 +1428,122 @@ fq_status jit_groupby(int32_t col_dtype, const GroupLaunch &G) {
     const uint64_t *bitmap = G.pred.bitmap;
     void *args[] = {&col, &n, &head, &bitmap, &hc, &tab};
     FQ_HIP_TRY(hipModuleLaunchKernel(fn, (unsigned)G.grid, 1, 1, (unsigned)G.threads, 1, 1, 0, G.stream, args, nullptr));
+    g_jit_launches += 1;
+    return FQ_OK;
+}
+
+namespace {
+
+struct ProjKernels {
+    hipFunction_t bits = nullptr, scatter = nullptr, map = nullptr;
+};
+std::unordered_map<std::string, ProjKernels> g_proj_cache;
+
+fq_status get_proj_kernels(int32_t col_dtype, const ProjLaunch &P, ProjKernels *out) {
+    fq_status err;
+    if (!load_rtc(FQ_JIT_ALWAYS, &err)) return err;
+    int dev = -1;
+    if (hipGetDevice(&dev) != hipSuccess) {
+        (void)hipGetLastError();
+        dev = -1;
+    }
+    const std::string key = proj_shape_key(P, col_dtype, dev);
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto it = g_proj_cache.find(key);
+    if (it == g_proj_cache.end()) {
+        Gen g;
+        std::string src;
+        Compiled c;
+        if (!gen_project_source(P, col_dtype, g, src))
+            return fqc::fail(FQ_E_UNSUPPORTED, "fused projection: column/expression types outside the device path");
+        fq_status s = compile(src, dev, c, "fq_jit_pscatter");
+        if (s != FQ_OK) return s;
+        ProjKernels k;
+        if (dev < 0) {  // validated only
+            *out = k;
+            return FQ_OK;
+        }
+        k.scatter = c.fn;
+        FQ_HIP_TRY(hipModuleGetFunction(&k.bits, c.mod, "fq_jit_pbits"));
+        FQ_HIP_TRY(hipModuleGetFunction(&k.map, c.mod, "fq_jit_pmap"));
+        it = g_proj_cache.emplace(key, k).first;
+    }
+    *out = it->second;
+    return FQ_OK;
+}
+
+int proj_grid(int64_t units, int per_wg) {
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipGetLastError();
+    const int64_t want = (units + per_wg - 1) / per_wg;
+    const int64_t cap = (int64_t)cus * 8;
+    return (int)std::max<int64_t>(1, std::min<int64_t>(want, cap));
+}
+
+}  // namespace
+
+bool jit_project_available() { return jit_mode() != FQ_JIT_OFF && rtc().ok; }
+
+fq_status jit_project_prepare(int32_t col_dtype, const ProjLaunch &P) {
+    ProjKernels k;
+    return get_proj_kernels(col_dtype, P, &k);
+}
+
+fq_status jit_project_bits(int32_t col_dtype, const ProjLaunch &P, uint64_t *d_bitmap, uint32_t *d_flag) {
+    ProjKernels k;
+    fq_status s = get_proj_kernels(col_dtype, P, &k);
+    if (s != FQ_OK || !k.bits || P.n == 0) return s;
+    HostProjConsts hc;
+    pack_proj_consts(P, hc);
+    const void *col = P.col;
+    long long n = P.n;
+    const int64_t nwords = (P.n + 63) / 64;
+    void *args[] = {&col, &n, &hc, &d_bitmap, &d_flag};
+    FQ_HIP_TRY(hipModuleLaunchKernel(k.bits, (unsigned)proj_grid(nwords, 4 * 8), 1, 1, kThreads, 1, 1, 0, P.stream,
+                                     args, nullptr));
+    g_jit_launches += 1;
+    return FQ_OK;
+}
+
+fq_status jit_project_scatter(int32_t col_dtype, const ProjLaunch &P, const uint64_t *d_bitmap, const uint64_t *intra,
+                              const uint64_t *gpre, int64_t ntiles, uint32_t *d_flag) {
+    ProjKernels k;
+    fq_status s = get_proj_kernels(col_dtype, P, &k);
+    if (s != FQ_OK || !k.scatter || P.n == 0) return s;
+    HostProjConsts hc;
+    pack_proj_consts(P, hc);
+    struct {
+        void *p[FQ_MAX_PROJECT];
+    } outs;
+    for (int j = 0; j < FQ_MAX_PROJECT; ++j) outs.p[j] = j < P.n_out ? P.out[j] : nullptr;
+    const void *col = P.col;
+    long long n = P.n;
+    void *args[] = {&col, &n, &hc, &d_bitmap, &intra, &gpre, &outs, &d_flag};
+    FQ_HIP_TRY(hipModuleLaunchKernel(k.scatter, (unsigned)ntiles, 1, 1, kThreads, 1, 1, 0, P.stream, args, nullptr));
+    g_jit_launches += 1;
+    return FQ_OK;
+}
+
+fq_status jit_project_map(int32_t col_dtype, const ProjLaunch &P, uint32_t *d_flag) {
+    ProjKernels k;
+    fq_status s = get_proj_kernels(col_dtype, P, &k);
+    if (s != FQ_OK || !k.map || P.n == 0) return s;
+    HostProjConsts hc;
+    pack_proj_consts(P, hc);
+    struct {
+        void *p[FQ_MAX_PROJECT];
+    } outs;
+    int aligned = ((uintptr_t)P.col & 15u) == 0;
+    for (int j = 0; j < FQ_MAX_PROJECT; ++j) {
+        outs.p[j] = j < P.n_out ? P.out[j] : nullptr;
+        if (j < P.n_out && ((uintptr_t)P.out[j] & 15u)) aligned = 0;
+    }
+    const void *col = P.col;
+    long long n = P.n;
+    void *args[] = {&col, &n, &hc, &outs, &aligned, &d_flag};
+    FQ_HIP_TRY(hipModuleLaunchKernel(k.map, (unsigned)proj_grid(n / 2, kThreads * 4), 1, 1, kThreads, 1, 1, 0, P.stream,
+                                     args, nullptr));
     g_jit_launches += 1;
     return FQ_OK;
 }

@@ -77,6 +77,34 @@ struct GroupLaunch {
 // Launches the hipRTC-specialised group-by kernel for G.
 fq_status jit_groupby(int32_t col_dtype, const GroupLaunch &G);
 
+// One fq_filter_project / fq_predicate_bitmap call (fq_filter.hip ->
+// fq_jit.hip): FilterTransform's predicate and ProjectionTransform's
+// expressions over one 64-bit column, hipRTC-specialised per shape.
+struct ProjLaunch {
+    const void *col;
+    int64_t n;
+    KPred pred;  // FQ_PRED_NONE / EXPR / TREE (a BITMAP predicate skips the bits kernel)
+    int32_t n_out;
+    KProg vals[FQ_MAX_PROJECT];
+    bool chain[FQ_MAX_PROJECT];
+    int32_t dtypes[FQ_MAX_PROJECT];
+    void *out[FQ_MAX_PROJECT];
+    hipStream_t stream;
+};
+
+// predicate -> LSB-first bitmap words; predicate errors OR-ed into *d_flag
+fq_status jit_project_bits(int32_t col_dtype, const ProjLaunch &P, uint64_t *d_bitmap, uint32_t *d_flag);
+// kept rows (bitmap + the compaction's tile prefixes) -> the n_out outputs
+fq_status jit_project_scatter(int32_t col_dtype, const ProjLaunch &P, const uint64_t *d_bitmap, const uint64_t *intra,
+                              const uint64_t *gpre, int64_t ntiles, uint32_t *d_flag);
+// no predicate: every row -> the n_out outputs
+fq_status jit_project_map(int32_t col_dtype, const ProjLaunch &P, uint32_t *d_flag);
+// hipRTC loadable and the policy not FQ_JIT_OFF
+bool jit_project_available();
+// compiles (and caches) P's module; without a device the source is compiled
+// for gfx950 only to validate it
+fq_status jit_project_prepare(int32_t col_dtype, const ProjLaunch &P);
+
 // Counts a fused (non-identity) scan that ran on the interpreting kernel.
 void jit_count_interp();
 

@@ -19,7 +19,8 @@ GPU_SYMBOLS = [
     "fq_arith_result_type", "fq_arith", "fq_compare", "fq_filter_workspace_bytes",
     "fq_filter_compact", "fq_state_merge", "fq_jit_config", "fq_jit_get_stats", "fq_jit_prepare",
     "fq_group_table_bytes", "fq_group_table_init", "fq_group_aggregate", "fq_group_table_count",
-    "fq_group_table_extract", "fq_logic",
+    "fq_group_table_extract", "fq_logic", "fq_filter_project_workspace_bytes", "fq_filter_project",
+    "fq_predicate_bitmap",
 ]
 
 
@@ -73,6 +74,10 @@ _protos = {
     "fq_jit_prepare": (C.c_int32, [P(abi.fq_col), C.c_int64, P(abi.fq_pred), P(abi.fq_expr), C.c_uint32,
                                    P(C.c_int32)]),
     "fq_logic": (C.c_int32, [C.c_int32, vp, vp, vp, C.c_int64, vp]),
+    "fq_filter_project_workspace_bytes": (C.c_size_t, [C.c_int64]),
+    "fq_filter_project": (C.c_int32, [P(abi.fq_col), P(abi.fq_pred), P(abi.fq_expr), C.c_int32, P(vp),
+                                      P(C.c_int64), vp, C.c_size_t, vp]),
+    "fq_predicate_bitmap": (C.c_int32, [P(abi.fq_col), P(abi.fq_pred), vp, vp, vp]),
     "fq_group_table_bytes": (C.c_size_t, [C.c_int64, C.c_int32]),
     "fq_group_table_init": (C.c_int32, [P(abi.fq_group_table), vp]),
     "fq_group_aggregate": (C.c_int32, [P(abi.fq_group_table), P(abi.fq_col), P(abi.fq_pred), P(abi.fq_expr),

@@ -212,6 +212,60 @@ def filter_compact(col, bitmap, stream=None):
     return out
 
 
+def filter_project(col, pred, values, stream=None):
+    """FilterTransform -> ProjectionTransform fused (fq_filter_project): the
+    kept rows of `col` (pred None = all) through each fq_expr of `values`
+    (None = the column itself) -> [DeviceColumn] in row order."""
+    require_gpu()
+    n_out = len(values)
+    exprs = (abi.fq_expr * n_out)()
+    outs = []
+    for j, v in enumerate(values):
+        if v is None:
+            v = abi.fq_expr()
+            v.n_steps = 0
+            v.out_dtype = col.dtype
+        exprs[j] = v
+        outs.append(empty_column(col.len, v.out_dtype))
+    ptrs = (C.c_void_p * max(n_out, 1))(*[o.ptr for o in outs])
+    ws = Workspace(lib.fq_filter_project_workspace_bytes(col.len))
+    n = C.c_int64(0)
+    c = col.col()
+    check(lib.fq_filter_project(C.byref(c), C.byref(pred) if pred is not None else None, exprs, n_out, ptrs,
+                                C.byref(n), ws.ptr, ws.nbytes, _stream(stream)))
+    for o in outs:
+        o.len = n.value
+    return outs
+
+
+def predicate_bitmap(col, pred, stream=None):
+    """FilterTransform's predicate as a Boolean column (fq_predicate_bitmap)."""
+    require_gpu()
+    out = empty_column(col.len, abi.DT_BOOLEAN)
+    flag = Workspace(4)
+    c = col.col()
+    check(lib.fq_predicate_bitmap(C.byref(c), C.byref(pred), C.c_void_p(out.ptr), flag.ptr, _stream(stream)))
+    return out
+
+
+def project_compile_check(col_dtype, pred=None, values=(None,)):
+    """Generate + compile the fused projection module for this shape without
+    running it (no GPU needed: gfx950 code object only).  Returns the
+    fq_status of fq_filter_project on a fake column (FQ_E_HIP when there is no
+    device after a successful compile)."""
+    exprs = (abi.fq_expr * len(values))()
+    for j, v in enumerate(values):
+        if v is None:
+            v = abi.fq_expr()
+            v.out_dtype = col_dtype
+        exprs[j] = v
+    fake = (C.c_void_p * len(values))(*([C.c_void_p(256)] * len(values)))
+    c = abi.fq_col(C.c_void_p(256), 1 << 20, col_dtype, 0)
+    n = C.c_int64(0)
+    return lib.fq_filter_project(C.byref(c), C.byref(pred) if pred is not None else None, exprs, len(values), fake,
+                                 C.byref(n), C.c_void_p(256), lib.fq_filter_project_workspace_bytes(1 << 20), None)
+
+
 def state_merge(states):
     arr = (abi.fq_agg_state * len(states))(*states)
     out = abi.fq_agg_state()

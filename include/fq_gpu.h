@@ -262,6 +262,30 @@ size_t fq_filter_workspace_bytes(int64_t len);
 fq_status fq_filter_compact(const fq_col *in, const uint64_t *d_bitmap, void *d_out,
                             int64_t *out_len, void *d_ws, size_t ws_bytes, void *stream);
 
+/* ---- FilterTransform -> ProjectionTransform fused over one column ----
+ * (transform_filter.rs:38-55 then transform_projection.rs:45-56 /
+ * stream_expression.rs:37-50, for a predicate and expressions over the same
+ * 64-bit column).  Keeps the rows of `col` where `pred` holds (NULL or
+ * FQ_PRED_NONE: every row; FQ_PRED_BITMAP: the given bitmap) in order and
+ * writes d_out[j][r] = values[j](kept row r) for j < n_out
+ * (values[j].n_steps == 0: the column itself; the element type is
+ * values[j].out_dtype, 8 bytes).  Errors follow the reference's order: a
+ * predicate error on any row first ("Internal Error: Divide by zero error",
+ * cast nulls), then an expression error on a kept row.  hipRTC-specialised
+ * per expression shape (FQ_E_UNSUPPORTED when hipRTC is unavailable or the
+ * JIT is off: the caller then runs fq_compare / fq_filter_compact /
+ * fq_arith).  Synchronises `stream`; *out_len = rows kept.                  */
+#define FQ_MAX_PROJECT 8
+size_t fq_filter_project_workspace_bytes(int64_t len);
+fq_status fq_filter_project(const fq_col *col, const fq_pred *pred, const fq_expr *values, int32_t n_out,
+                            void *const *d_out, int64_t *out_len, void *d_ws, size_t ws_bytes, void *stream);
+/* FilterTransform's predicate alone as a Boolean column: LSB-first bitmap of
+ * ceil(len/64) words, bits past len cleared (one kernel instead of one
+ * fq_arith per expression node plus fq_compare).  d_flag: 4 bytes of device
+ * scratch; the call synchronises `stream` and reports predicate errors.    */
+fq_status fq_predicate_bitmap(const fq_col *col, const fq_pred *pred, uint64_t *d_bitmap, uint32_t *d_flag,
+                              void *stream);
+
 /* ---- AggregateFinal state merge (host, function_aggregator.rs:106-139) ----
  * Merges `n` partial states in the given order into *out (wrapping sum,
  * summed counts/blocks, max, min, OR-ed flags).  All dtypes must match.      */

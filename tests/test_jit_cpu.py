@@ -132,3 +132,43 @@ def test_predicate_tree_shapes_compile():
     bad._tree.prog[2] = 0  # no operator: two values left on the stack
     with pytest.raises(ops.FQError):
         ops.jit_prepare(U64, pred=bad, mask=ALL)
+
+
+# ---- fused FilterTransform -> ProjectionTransform (fq_filter_project) ------
+
+PROJECT_SHAPES = [
+    (U64, None, [None]),
+    (U64, None, [chain(U64, [("+", 1)])[0], chain(U64, [("/", 2)])[0]]),
+    (U64, ("EXPR", [("+", 1)], "<", 100), [None, chain(U64, [("*", 3)])[0]]),
+    (U64, ("EXPR", [("%", 1000)], "=", 999), [chain(U64, [("/", 2.0)])[0]]),
+    (U64, ("TREE",), [chain(U64, [("+", 1)])[0], chain(U64, [("-", (5, "Int64"))])[0], None]),
+    (I64, ("EXPR", [], "<", (-5, "Int64")), [chain(I64, [("%", (7, "Int64"))])[0]]),
+    (F64, ("EXPR", [("*", 2.0)], ">=", 1.5), [None, chain(F64, [("+", COL)])[0]]),
+    (U64, None, [chain(U64, [("+", k)])[0] for k in range(8)]),
+]
+
+
+def _project_pred(dt, spec):
+    if spec is None:
+        return None
+    if spec[0] == "TREE":
+        from fq_amd.expr import pred_tree
+        return pred_tree(U64, [([("%", 8)], "<", 3), ([], ">", 1000)], [0, 1, "and"])
+    _, lhs, cmp, rhs = spec
+    return predicate(dt, lhs, cmp, rhs)
+
+
+@pytest.mark.parametrize("i", range(len(PROJECT_SHAPES)))
+def test_project_shapes_compile(i):
+    # the module (bits, scatter, map kernels) is generated and compiled for
+    # gfx950; with no device the call then stops at its first HIP call
+    dt, spec, values = PROJECT_SHAPES[i]
+    before = ops.jit_stats()["kernels_compiled"]
+    st = ops.project_compile_check(dt, _project_pred(dt, spec), values)
+    assert st == abi.FQ_E_HIP, (st, ops.lib.fq_last_error())
+    assert ops.jit_stats()["kernels_compiled"] == before + 1
+
+
+def test_project_rejects_bad_arguments():
+    assert ops.project_compile_check(abi.DT_UINT32, None, [None]) == abi.FQ_E_UNSUPPORTED
+    assert ops.project_compile_check(U64, None, [None] * 9) == abi.FQ_E_INVALID
