@@ -196,6 +196,13 @@ DataValue ArithmeticFunction::merge_result() const {
     return data_value_arithmetic_op(op_, left_->merge_result(), right_->merge_result());
 }
 
+// Expression trees run on the hipRTC kernels only: fuse them while the JIT is
+// on (FQ_JIT / fq_jit_config) and hipRTC has not been found missing.
+static bool tree_fusion_enabled() {
+    fq_jit_stats js{};
+    return fq_jit_get_stats(&js) == FQ_OK && js.mode != FQ_JIT_OFF && js.available != 0;
+}
+
 // Append one step `acc OP operand` (or `operand OP acc`) to a chain.
 static bool push_step(FusedChain &c, int32_t op, bool column_operand, const DataValue *k, bool reversed) {
     if (c.expr.n_steps >= FQ_MAX_STEPS) return false;
@@ -226,24 +233,50 @@ static bool numeric_constant(const Function &f, const DataValue *&v) {
 bool ArithmeticFunction::to_chain(const DataSchema &s, FusedChain &c) const {
     const DataValue *k = nullptr;
     const std::string *fld = nullptr;
-    FusedChain sub;
-    if (numeric_constant(*right_, k) && left_->to_chain(s, sub)) {
-        c = sub;
+    FusedChain l, r;  // each child lowered once
+    const bool lok = left_->to_chain(s, l), rok = right_->to_chain(s, r);
+    if (numeric_constant(*right_, k) && lok) {
+        c = l;
         return push_step(c, op_, false, k, false);
     }
-    if (numeric_constant(*left_, k) && right_->to_chain(s, sub)) {
-        c = sub;
+    if (numeric_constant(*left_, k) && rok) {
+        c = r;
         return push_step(c, op_, false, k, true);
     }
-    if ((fld = right_->as_field()) && left_->to_chain(s, sub) && *fld == sub.column) {
-        c = sub;
+    if ((fld = right_->as_field()) && lok && *fld == l.column) {
+        c = l;
         return push_step(c, op_, true, nullptr, false);
     }
-    if ((fld = left_->as_field()) && right_->to_chain(s, sub) && *fld == sub.column) {
-        c = sub;
+    if ((fld = left_->as_field()) && rok && *fld == r.column) {
+        c = r;
         return push_step(c, op_, true, nullptr, true);
     }
-    return false;
+    // both children are expressions over the same column: an expression tree
+    // (left subtree, FQ_OP_PUSH, right subtree, then this node with the
+    // popped left value as its operand) -- hipRTC kernels only
+    if (!lok || !rok || l.column != r.column || !tree_fusion_enabled()) return false;
+    if (l.expr.n_steps + r.expr.n_steps + 2 > FQ_MAX_STEPS) return false;
+    const int depth = std::max(l.depth, 1 + r.depth);
+    if (depth > FQ_MAX_STACK || !is_chain_dtype(l.col_dtype)) return false;
+    int32_t ct = 0;
+    if (fqc::numerical_coercion(fqc::arith_op_str(op_), l.out_dtype, r.out_dtype, &ct) != FQ_OK || !is_chain_dtype(ct))
+        return false;
+    c = l;
+    fq_step &push = c.expr.steps[c.expr.n_steps++];
+    push = fq_step{};
+    push.op = FQ_OP_PUSH;
+    push.dtype = l.col_dtype;
+    for (int i = 0; i < r.expr.n_steps; ++i) c.expr.steps[c.expr.n_steps++] = r.expr.steps[i];
+    fq_step &node = c.expr.steps[c.expr.n_steps++];
+    node = fq_step{};
+    node.op = op_;
+    node.operand = FQ_OPERAND_STACK;
+    node.reversed = 1;  // left OP right
+    node.dtype = ct;
+    c.expr.out_dtype = ct;
+    c.out_dtype = ct;
+    c.depth = depth;
+    return true;
 }
 
 // ---------------------------------------------------------------------------

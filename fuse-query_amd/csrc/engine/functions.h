@@ -20,6 +20,7 @@ struct FusedChain {
     DataType col_dtype = FQ_DT_NULL;
     fq_expr expr{};
     DataType out_dtype = FQ_DT_NULL;
+    int depth = 0;  // value-stack depth the expression tree needs (FQ_OP_PUSH)
     std::string key() const;
 };
 

@@ -370,10 +370,36 @@ fq_status lower_expr(const fq_expr &e, int32_t col_dtype, KProg &out, int32_t &r
     if (e.n_steps > 0 && !is_chain_dtype(col_dtype))
         return fqc::fail(FQ_E_UNSUPPORTED, std::string("fused expressions over ") + fqc::dtype_name(col_dtype) +
                                                " columns are not supported on the device path");
+    int32_t stack[FQ_MAX_STACK];
+    int depth = 0;
     for (int i = 0; i < e.n_steps; ++i) {
         const fq_step &st = e.steps[i];
+        if (st.op == FQ_OP_PUSH) {  // expression tree: acc onto the stack, restart from the column
+            if (depth >= FQ_MAX_STACK) return fqc::fail(FQ_E_UNSUPPORTED, "expression tree too deep for the fused device path");
+            if (!is_chain_dtype(col_dtype)) return fqc::fail(FQ_E_UNSUPPORTED, "fused expression trees need a 64-bit column");
+            if (out.n >= (int)(sizeof(out.s) / sizeof(out.s[0])))
+                return fqc::fail(FQ_E_UNSUPPORTED, "expression too long for the fused device path");
+            KStep &k = out.s[out.n++];
+            k = KStep{};
+            k.code = K_PUSH;
+            k.dtype = col_dtype;
+            stack[depth++] = acc;
+            acc = col_dtype;
+            continue;
+        }
         if (!is_chain_dtype(st.dtype))
             return fqc::fail(FQ_E_UNSUPPORTED, "fused step dtype must be UInt64, Int64 or Float64");
+        int32_t sdt = 0;
+        if (st.operand == FQ_OPERAND_STACK) {
+            if (depth == 0) return fqc::fail(FQ_E_INVALID, "fq_step: stack operand without a pushed value");
+            sdt = stack[--depth];
+            if (sdt != st.dtype && !(sdt == FQ_DT_UINT64 && st.dtype != FQ_DT_UINT64) &&
+                !(sdt == FQ_DT_INT64 && st.dtype == FQ_DT_FLOAT64))
+                return fqc::fail(FQ_E_UNSUPPORTED, std::string("fused cast ") + fqc::dtype_name(sdt) + " -> " +
+                                                       fqc::dtype_name(st.dtype) + " is not supported on the device path");
+        } else if (st.operand != FQ_OPERAND_CONST && st.operand != FQ_OPERAND_COLUMN) {
+            return fqc::fail(FQ_E_INVALID, "fq_step: bad operand kind");
+        }
         fq_status s = push_cast(acc, st.dtype, out);
         if (s != FQ_OK) return s;
         if (st.operand == FQ_OPERAND_COLUMN && col_dtype == FQ_DT_FLOAT64 && st.dtype != FQ_DT_FLOAT64)
@@ -385,6 +411,7 @@ fq_status lower_expr(const fq_expr &e, int32_t col_dtype, KProg &out, int32_t &r
         k.operand = st.operand;
         k.reversed = st.reversed;
         k.dtype = st.dtype;
+        k.sdtype = sdt;
         k.c = st.bits;
         const bool konst = st.operand == FQ_OPERAND_CONST && !st.reversed;
         if (st.dtype == FQ_DT_FLOAT64) {
@@ -433,6 +460,7 @@ fq_status lower_expr(const fq_expr &e, int32_t col_dtype, KProg &out, int32_t &r
         }
         acc = st.dtype;
     }
+    if (depth != 0) return fqc::fail(FQ_E_INVALID, "fq_expr: pushed values left on the stack");
     if (e.n_steps > 0 && e.out_dtype != acc)
         return fqc::fail(FQ_E_INVALID, "fq_expr: out_dtype does not match the last step");
     res_dtype = acc;
@@ -702,8 +730,12 @@ fq_status fq_aggregate(const fq_col *col, int64_t block_rows, const fq_pred *pre
     L.stream = (hipStream_t)stream;
     L.parts = (Partial *)d_ws;
     bool jitted = false;
-    s = jit_scan(col->dtype, chain, L, &jitted);
+    const bool tree = (chain && prog_has_tree(L.val)) || pred_has_tree(L.pred);
+    s = jit_scan(col->dtype, chain, L, &jitted, tree);
     if (s != FQ_OK) return s;
+    if (!jitted && tree)
+        return fqc::fail(FQ_E_UNSUPPORTED, "fused expression trees run on the hipRTC kernels only (FQ_JIT is off "
+                                           "or hipRTC is unavailable)");
     if (!jitted) {
         if (chain || L.pred.kind != FQ_PRED_NONE) jit_count_interp();
         s = dispatch(col->dtype, L, chain);

@@ -39,6 +39,7 @@ enum Code : int32_t {
     K_MUL_F,
     K_DIV_F,  // f64 '/', zero divisor -> DIV_ZERO (arrow 2.0 divide checks is_zero)
     K_MOD_F,
+    K_PUSH,  // expression trees: push acc, acc = the column (hipRTC kernels only)
 };
 
 struct KStep {
@@ -49,7 +50,9 @@ struct KStep {
     uint64_t c;        // constant bits
     uint64_t magic;    // K_DIVM_U / K_MODM_U
     uint32_t shift;
-    uint32_t add;  // libdivide "add" marker
+    uint32_t add;    // libdivide "add" marker
+    int32_t sdtype;  // FQ_OPERAND_STACK: dtype of the popped value (cast to `dtype`)
+    int32_t pad;
 };
 
 struct KProg {

@@ -156,6 +156,8 @@ void pack_tree_consts(const KPred &pr, HC &hc) {
 struct Gen {
     const char *prefix = "v";
     int step = 0;
+    int uid = 0;                    // names of pushed tree values (s0, s1, ...)
+    std::vector<std::string> stk;  // the value stack of FQ_OP_PUSH / FQ_OPERAND_STACK
     std::string K(const char *field) const {
         return std::string("c.") + prefix + "[" + std::to_string(step) + "]." + field;
     }
@@ -181,6 +183,7 @@ void put_pred_key(const KPred &pr, std::string &k) {
             put(p.s[i].reversed);
             put(p.s[i].dtype);
             put((int32_t)p.s[i].add);
+            put(p.s[i].sdtype);
         }
     };
     put(pr.kind);
@@ -222,6 +225,7 @@ std::string shape_key(const Launch &L, int32_t tin, bool chain, int dev) {
             put(p.s[i].reversed);
             put(p.s[i].dtype);
             put((int32_t)p.s[i].add);
+            put(p.s[i].sdtype);
         }
     };
     if (chain) prog(L.val);
@@ -251,6 +255,12 @@ void emit_prog(Gen &g, std::string &body, const KProg &p, int32_t tin, const cha
                 continue;
             case K_CAST_U2F: body += "    a = __builtin_bit_cast(u64, (double)a);\n"; continue;
             case K_CAST_I2F: body += "    a = __builtin_bit_cast(u64, (double)(long long)a);\n"; continue;
+            case K_PUSH: {  // expression tree: keep acc, restart from the column
+                const std::string v = "s" + std::to_string(g.uid++);
+                body += "    const u64 " + v + " = a;\n    a = " + x_bits(tin) + ";\n";
+                g.stk.push_back(v);
+                continue;
+            }
             case K_SHR_U: body += "    a = a >> (u32)" + g.K("s") + ";\n"; continue;
             case K_AND_U: body += "    a = a & " + g.K("m") + ";\n"; continue;
             case K_DIVM_U:
@@ -267,8 +277,20 @@ void emit_prog(Gen &g, std::string &body, const KProg &p, int32_t tin, const cha
         }
         // binary step with an operand b
         std::string b;
-        if (st.operand == FQ_OPERAND_COLUMN) b = col_as(g, body, tin, st.dtype);
-        else b = g.K("c");
+        if (st.operand == FQ_OPERAND_COLUMN) {
+            b = col_as(g, body, tin, st.dtype);
+        } else if (st.operand == FQ_OPERAND_STACK) {  // the left subtree's value, cast like acc
+            const std::string v = g.stk.empty() ? std::string("0ull") : g.stk.back();
+            if (!g.stk.empty()) g.stk.pop_back();
+            if (st.sdtype == st.dtype) b = v;
+            else if (st.sdtype == FQ_DT_UINT64 && st.dtype == FQ_DT_INT64) {
+                body += "    flags |= (u32)((" + v + " >> 63) & (u64)live) * " + std::to_string(FQ_STATE_CAST_NULL) + "u;\n";
+                b = v;
+            } else if (st.sdtype == FQ_DT_UINT64) b = "__builtin_bit_cast(u64, (double)" + v + ")";
+            else b = "__builtin_bit_cast(u64, (double)(long long)" + v + ")";
+        } else {
+            b = g.K("c");
+        }
         body += "    { const u64 b = " + b + ";\n";
         body += st.reversed ? "      const u64 L = b, R = a;\n" : "      const u64 L = a, R = b;\n";
         switch (st.code) {
@@ -660,6 +682,7 @@ std::string group_shape_key(const GroupLaunch &G, int32_t tin, int dev) {
             put(p.s[i].reversed);
             put(p.s[i].dtype);
             put((int32_t)p.s[i].add);
+            put(p.s[i].sdtype);
         }
     };
     put(dev);
@@ -1059,6 +1082,7 @@ std::string proj_shape_key(const ProjLaunch &P, int32_t tin, int dev) {
             put(st.reversed);
             put(st.dtype);
             put((int32_t)st.add);
+            put(st.sdtype);
         }
     }
     return k;
@@ -1355,11 +1379,11 @@ fq_status jit_prepare(int32_t col_dtype, bool chain, const Launch &L, bool *read
     return get_kernel(col_dtype, chain, L, &fn, ready);
 }
 
-fq_status jit_scan(int32_t col_dtype, bool chain, const Launch &L, bool *used) {
+fq_status jit_scan(int32_t col_dtype, bool chain, const Launch &L, bool *used, bool force) {
     *used = false;
     const int32_t mode = jit_mode();
     if (mode == FQ_JIT_OFF || !eligible(col_dtype, chain, L)) return FQ_OK;
-    if (mode == FQ_JIT_AUTO && L.n < jit_min_rows()) return FQ_OK;
+    if (mode == FQ_JIT_AUTO && L.n < jit_min_rows() && !force) return FQ_OK;
     fq_status err;
     if (!load_rtc(mode, &err)) return err;
     hipFunction_t fn;

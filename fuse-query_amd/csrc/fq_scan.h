@@ -31,8 +31,24 @@ fq_status lower_expr(const fq_expr &e, int32_t col_dtype, KProg &out, int32_t &r
 fq_status lower_pred(const fq_pred *pred, int32_t col_dtype, int64_t len, bool need_data, KPred &out);
 
 // Launches the scan of `L` from a specialised kernel when the JIT policy
-// (fq_jit_config) selects it; *used tells the caller whether it did.
-fq_status jit_scan(int32_t col_dtype, bool chain, const Launch &L, bool *used);
+// (fq_jit_config) selects it -- or, with `force` (expression trees, which the
+// interpreter does not run), whenever the JIT is not off; *used tells the
+// caller whether it did.
+fq_status jit_scan(int32_t col_dtype, bool chain, const Launch &L, bool *used, bool force = false);
+
+// expression trees (FQ_OP_PUSH / FQ_OPERAND_STACK) in a lowered program
+inline bool prog_has_tree(const KProg &p) {
+    for (int i = 0; i < p.n; ++i)
+        if (p.s[i].code == K_PUSH) return true;
+    return false;
+}
+inline bool pred_has_tree(const KPred &p) {
+    if (p.kind == FQ_PRED_EXPR) return prog_has_tree(p.lhs);
+    if (p.kind == FQ_PRED_TREE)
+        for (int l = 0; l < p.n_leaves; ++l)
+            if (prog_has_tree(p.leaves[l].lhs)) return true;
+    return false;
+}
 
 // Compiles (and caches) the specialised kernel for L's shape ahead of the
 // first scan; *ready = the shape is specialisable.  Without a device the

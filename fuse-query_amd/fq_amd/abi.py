@@ -32,6 +32,7 @@ DT_BY_NAME = {v: k for k, v in DT_NAMES.items()}
 
 # operators (src/datavalues/data_value_operator.rs)
 OP_ADD, OP_SUB, OP_MUL, OP_DIV, OP_MOD = 0, 1, 2, 3, 4
+OP_PUSH = 5  # expression trees: push acc, acc = the column
 OP_BY_SYM = {"+": OP_ADD, "-": OP_SUB, "*": OP_MUL, "/": OP_DIV, "%": OP_MOD}
 CMP_EQ, CMP_LT, CMP_LTEQ, CMP_GT, CMP_GTEQ = 0, 1, 2, 3, 4
 CMP_BY_SYM = {"=": CMP_EQ, "<": CMP_LT, "<=": CMP_LTEQ, ">": CMP_GT, ">=": CMP_GTEQ}
@@ -40,7 +41,8 @@ CMP_FLIP = {CMP_EQ: CMP_EQ, CMP_LT: CMP_GT, CMP_LTEQ: CMP_GTEQ, CMP_GT: CMP_LT, 
 AGG_MIN, AGG_MAX, AGG_SUM, AGG_COUNT = 1, 2, 4, 8
 AGG_BY_NAME = {"min": AGG_MIN, "max": AGG_MAX, "sum": AGG_SUM, "count": AGG_COUNT}
 
-OPERAND_CONST, OPERAND_COLUMN = 0, 1
+OPERAND_CONST, OPERAND_COLUMN, OPERAND_STACK = 0, 1, 2
+MAX_STACK = 2
 PRED_NONE, PRED_EXPR, PRED_BITMAP = 0, 1, 2
 MAX_STEPS = 8
 

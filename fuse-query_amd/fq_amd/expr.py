@@ -76,6 +76,8 @@ def literal(v):
 
 
 COL = "col"  # operand marker: the column itself
+STACK = "stack"  # operand marker: the value pushed by the matching ("push",) step
+PUSH = ("push",)  # step: push acc, restart from the column (expression trees)
 
 
 def chain(col_dtype, steps):
@@ -83,12 +85,22 @@ def chain(col_dtype, steps):
     Returns (fq_expr, out_dtype)."""
     e = abi.fq_expr()
     acc = col_dtype
+    stack = []
     if len(steps) > abi.MAX_STEPS:
         raise ValueError("too many steps")
     for i, st in enumerate(steps):
+        if st[0] == "push":  # tree: keep acc (the left subtree), restart from the column
+            s = e.steps[i]
+            s.op, s.operand, s.reversed, s.dtype, s.bits = abi.OP_PUSH, abi.OPERAND_CONST, 0, col_dtype, 0
+            stack.append(acc)
+            acc = col_dtype
+            continue
         sym, operand = st[0], st[1]
         rev = bool(st[2]) if len(st) > 2 else False
-        if operand is COL or operand == COL:
+        if operand is STACK or operand == STACK:
+            odt = stack.pop()
+            okind, obits = abi.OPERAND_STACK, 0
+        elif operand is COL or operand == COL:
             odt = col_dtype
             okind, obits = abi.OPERAND_COLUMN, 0
         else:

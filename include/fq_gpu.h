@@ -75,6 +75,7 @@ typedef int32_t fq_status;
 #define FQ_OP_MUL 2
 #define FQ_OP_DIV 3
 #define FQ_OP_MOD 4 /* EXTENSION: '%' has no arm in function_factory.rs:17-39 */
+#define FQ_OP_PUSH 5 /* fq_step only: push acc, acc = the column (see FQ_OPERAND_STACK) */
 
 #define FQ_CMP_EQ 0
 #define FQ_CMP_LT 1
@@ -120,6 +121,15 @@ typedef struct fq_col {
 #define FQ_MAX_STEPS 8
 #define FQ_OPERAND_CONST 0
 #define FQ_OPERAND_COLUMN 1
+/* Expression TREES over the one column (e.g. (x + 1) + (x / 2)) use a
+ * two-deep value stack: FQ_OP_PUSH pushes acc and restarts acc = x; a later
+ * step with operand FQ_OPERAND_STACK pops that value as its operand
+ * (reversed = 1: popped OP acc, the left subtree first, as the reference
+ * evaluates ArithmeticFunction's children, function_arithmetic.rs:64-72).
+ * The popped value is cast to the step's dtype like acc.  Trees run on the
+ * hipRTC-specialised kernels only (FQ_E_UNSUPPORTED with FQ_JIT_OFF).     */
+#define FQ_OPERAND_STACK 2
+#define FQ_MAX_STACK 2
 typedef struct fq_step {
     int32_t op;       /* FQ_OP_*                                  */
     int32_t operand;  /* FQ_OPERAND_CONST / FQ_OPERAND_COLUMN     */

@@ -207,25 +207,73 @@ static int operand_arr(int32_t operand, uint64_t bits, int32_t dt, const arr_t *
 /* Function::eval of an ArithmeticFunction chain (function_arithmetic.rs:64-72):
  * each level evaluates its children to arrays, casts both to the coercion
  * type (data_array_arithmetic.rs:34-40) and runs one arrow kernel. */
+/* Expression trees (FQ_OP_PUSH / FQ_OPERAND_STACK): a pushed array is the
+ * evaluated left child of a node whose right child is evaluated next; the
+ * node casts both to its coercion type (the left one first, as the
+ * reference evaluates left_->eval before right_->eval). */
 static int eval_chain(const fq_expr *e, const arr_t *x, arr_t *out, err_t *err) {
     arr_t acc = arr_new(x->n, x->dtype);
     memcpy(acc.v, x->v, (size_t)x->n * 8);
+    arr_t stack[FQ_MAX_STACK];
+    int depth = 0;
     for (int s = 0; s < e->n_steps; ++s) {
         const fq_step *st = &e->steps[s];
         arr_t accc, opnd, res;
+        if (st->op == FQ_OP_PUSH) {
+            if (depth >= FQ_MAX_STACK) {
+                arr_free(&acc);
+                while (depth > 0) arr_free(&stack[--depth]);
+                return set_err(err, FQ_E_UNSUPPORTED, "expression tree too deep");
+            }
+            stack[depth++] = acc;
+            acc = arr_new(x->n, x->dtype);
+            memcpy(acc.v, x->v, (size_t)x->n * 8);
+            continue;
+        }
+        if (st->operand == FQ_OPERAND_STACK) {
+            arr_t left = stack[--depth];
+            int rc = cast_arr(&left, st->dtype, &opnd, err);
+            arr_free(&left);
+            if (rc) {
+                arr_free(&acc);
+                while (depth > 0) arr_free(&stack[--depth]);
+                return err->status;
+            }
+            if (cast_arr(&acc, st->dtype, &accc, err)) {
+                arr_free(&acc);
+                arr_free(&opnd);
+                while (depth > 0) arr_free(&stack[--depth]);
+                return err->status;
+            }
+            arr_free(&acc);
+            rc = st->reversed ? arith_arr(st->op, &opnd, &accc, &res, err) : arith_arr(st->op, &accc, &opnd, &res, err);
+            arr_free(&accc);
+            arr_free(&opnd);
+            if (rc) {
+                while (depth > 0) arr_free(&stack[--depth]);
+                return rc;
+            }
+            acc = res;
+            continue;
+        }
         if (cast_arr(&acc, st->dtype, &accc, err)) {
             arr_free(&acc);
+            while (depth > 0) arr_free(&stack[--depth]);
             return err->status;
         }
         arr_free(&acc);
         if (operand_arr(st->operand, st->bits, st->dtype, x, &opnd, err)) {
             arr_free(&accc);
+            while (depth > 0) arr_free(&stack[--depth]);
             return err->status;
         }
         int rc = st->reversed ? arith_arr(st->op, &opnd, &accc, &res, err) : arith_arr(st->op, &accc, &opnd, &res, err);
         arr_free(&accc);
         arr_free(&opnd);
-        if (rc) return rc;
+        if (rc) {
+            while (depth > 0) arr_free(&stack[--depth]);
+            return rc;
+        }
         acc = res;
     }
     *out = acc;

@@ -172,3 +172,66 @@ def test_project_shapes_compile(i):
 def test_project_rejects_bad_arguments():
     assert ops.project_compile_check(abi.DT_UINT32, None, [None]) == abi.FQ_E_UNSUPPORTED
     assert ops.project_compile_check(U64, None, [None] * 9) == abi.FQ_E_INVALID
+
+
+# ---- expression trees (FQ_OP_PUSH / FQ_OPERAND_STACK) ----------------------
+from fq_amd.expr import PUSH, STACK  # noqa: E402
+
+TREE_SHAPES = [
+    (U64, [("+", 1), PUSH, ("/", 2), ("+", STACK, True)]),                       # (x+1)+(x/2)
+    (U64, [("+", 1), PUSH, ("+", 2), ("*", STACK, True), ("%", 1000003)]),       # ((x+1)*(x+2))%p
+    (U64, [("/", 3), PUSH, ("%", 7), ("*", 2), ("-", STACK, True)]),            # (x/3)-(x%7)*2
+    (U64, [("+", 1), PUSH, ("/", 2.0), ("+", STACK, True)]),                     # u64 + f64
+    (U64, [("+", 1), PUSH, ("+", 2), PUSH, ("%", 5), ("-", STACK, True), ("*", STACK, True)]),  # depth 2
+    (U64, [("-", (5, "Int64")), PUSH, ("*", 3), ("+", STACK, True)]),            # i64 + u64 -> i64
+    (I64, [("*", (3, "Int64")), PUSH, ("%", (7, "Int64")), ("/", STACK, True)]),
+    (F64, [("*", 2.0), PUSH, ("+", COL), ("/", STACK, True)]),
+]
+
+
+@pytest.mark.parametrize("dt,steps", TREE_SHAPES, ids=[str(s) for _, s in TREE_SHAPES])
+def test_tree_shapes_compile(dt, steps):
+    value, _ = chain(dt, steps)
+    assert ops.jit_prepare(dt, value=value, mask=ALL)
+    pred = predicate(dt, steps, "<", 100)
+    assert ops.jit_prepare(dt, pred=pred, mask=ALL, block_rows=10000)
+    assert ops.project_compile_check(dt, pred, [value, None]) == abi.FQ_E_HIP
+
+
+def test_tree_lowering_rejects_unbalanced_and_deep():
+    unbalanced, _ = chain(U64, [("+", 1), PUSH, ("+", 2)])
+    unbalanced.out_dtype = U64
+    with pytest.raises(ops.FQError):
+        ops.jit_prepare(U64, value=unbalanced, mask=ALL)
+    deep = chain(U64, [PUSH, PUSH, PUSH, ("+", STACK, True), ("+", STACK, True), ("+", STACK, True)])[0]
+    with pytest.raises(ops.FQError):
+        ops.jit_prepare(U64, value=deep, mask=ALL)
+
+
+@pytest.mark.parametrize("i", range(5))
+def test_oracle_tree_matches_numpy(i):
+    # the C oracle's tree evaluation (oracle/fq_oracle.c eval_chain) against a
+    # direct numpy/python evaluation of the same tree
+    import numpy as np
+    import oracle_c
+    host = np.arange(1, 20_001, dtype=np.uint64) * np.uint64(7919)
+    dt, steps = TREE_SHAPES[i]
+    value, vdt = chain(dt, steps)
+    st = oracle_c.column_partial(host, dt, 10000, [(abi.AGG_MAX, value), (abi.AGG_MIN, value)])
+    x = [int(v) for v in host]
+    M = 2**64
+
+    def ev(v):
+        if i == 0:
+            return (v + 1 + v // 2) % M
+        if i == 1:
+            return ((v + 1) * (v + 2) % M) % 1000003
+        if i == 2:
+            return (v // 3 - (v % 7) * 2) % M
+        if i == 3:
+            return float(v + 1) + v / 2.0
+        return ((v + 1) * ((v + 2) - v % 5)) % M
+    vals = [ev(v) for v in x]
+    from fq_amd.expr import from_bits
+    assert from_bits(st[0].bits, vdt) == max(vals)
+    assert from_bits(st[1].bits, vdt) == min(vals)
