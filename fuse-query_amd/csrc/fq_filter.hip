@@ -369,27 +369,27 @@ size_t fq_filter_workspace_bytes(int64_t len) {
 namespace fqk {
 namespace {
 
-// Workspace of fq_filter_project: [bitmap words][tile prefixes][group
-// prefixes + total][2 flag words: predicate, expressions].
+// Workspace of fq_filter_project: [total][flag words: predicate,
+// expressions][ticket, pad][one look-back status word per tile].
 struct ProjWs {
-    uint64_t *bitmap, *intra, *gpre;
-    uint32_t *flags;
-    int64_t nwords, ntiles, ngroups;
+    uint64_t *total;
+    uint32_t *flags, *ticket;
+    uint64_t *status;
+    int64_t ntiles;
 };
 
 ProjWs proj_ws(void *d_ws, int64_t n) {
     ProjWs w;
-    w.nwords = (n + 63) / 64;
-    w.ntiles = (w.nwords + kTileWords - 1) / kTileWords;
-    w.ngroups = (w.ntiles + kGroupTiles - 1) / kGroupTiles;
-    w.bitmap = (uint64_t *)d_ws;
-    w.intra = w.bitmap + w.nwords;
-    w.gpre = w.intra + w.ntiles;
-    w.flags = (uint32_t *)(w.gpre + w.ngroups + 1);
+    w.ntiles = (n + select_tile_rows() - 1) / select_tile_rows();
+    w.total = (uint64_t *)d_ws;
+    w.flags = (uint32_t *)(w.total + 1);
+    w.ticket = (uint32_t *)(w.total + 2);
+    w.status = w.total + 3;
     return w;
 }
 
 fq_status flag_error(uint32_t f) {
+    if (f & 0x80000000u) return fqc::fail(FQ_E_INTERNAL, "fused projection: the offset look-back did not complete");
     if (f & FQ_STATE_DIV_ZERO) return fqc::fail(FQ_E_DIVIDE_BY_ZERO, "Internal Error: Divide by zero error");
     if (f & FQ_STATE_CAST_NULL)
         return fqc::fail(FQ_E_UNSUPPORTED, "cast produced nulls (nulls are not supported on the device path)");
@@ -431,7 +431,7 @@ extern "C" {
 
 size_t fq_filter_project_workspace_bytes(int64_t len) {
     const fqk::ProjWs w = fqk::proj_ws(nullptr, len < 0 ? 0 : len);
-    return (size_t)(w.nwords + w.ntiles + w.ngroups + 1 + 1) * sizeof(uint64_t);
+    return (size_t)(3 + w.ntiles) * sizeof(uint64_t);
 }
 
 fq_status fq_filter_project(const fq_col *col, const fq_pred *pred, const fq_expr *values, int32_t n_out,
@@ -452,24 +452,18 @@ fq_status fq_filter_project(const fq_col *col, const fq_pred *pred, const fq_exp
         return fqc::fail(FQ_E_INVALID, "fq_filter_project: workspace too small");
     const ProjWs w = proj_ws(d_ws, n);
     hipStream_t st = P.stream;
-    FQ_HIP_TRY(hipMemsetAsync(w.flags, 0, 2 * sizeof(uint32_t), st));
     uint64_t host[2] = {0, 0};  // kept rows, flag words
     if (P.pred.kind == FQ_PRED_NONE) {
+        FQ_HIP_TRY(hipMemsetAsync(w.flags, 0, 2 * sizeof(uint32_t), st));
         if ((s = jit_project_map(col->dtype, P, w.flags + 1)) != FQ_OK) return s;
         FQ_HIP_TRY(hipMemcpyAsync(&host[1], w.flags, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
         host[0] = (uint64_t)n;
     } else {
-        const uint64_t *bm = w.bitmap;
-        if (P.pred.kind == FQ_PRED_BITMAP) bm = P.pred.bitmap;
-        else if ((s = jit_project_bits(col->dtype, P, w.bitmap, w.flags)) != FQ_OK) return s;
-        hipLaunchKernelGGL(compact_count_kernel, dim3((unsigned)w.ngroups), dim3(kTileWords), 0, st, bm, n, w.ntiles,
-                           w.intra, w.gpre);
-        FQ_HIP_TRY(hipGetLastError());
-        hipLaunchKernelGGL(compact_scan_kernel, dim3(1), dim3(kScanThreads), 0, st, w.gpre, w.ngroups);
-        FQ_HIP_TRY(hipGetLastError());
-        if ((s = jit_project_scatter(col->dtype, P, bm, w.intra, w.gpre, w.ntiles, w.flags + 1)) != FQ_OK) return s;
-        // the total (gpre[ngroups]) and the flag words are adjacent
-        FQ_HIP_TRY(hipMemcpyAsync(host, w.gpre + w.ngroups, sizeof(host), hipMemcpyDeviceToHost, st));
+        FQ_HIP_TRY(hipMemsetAsync(d_ws, 0, fq_filter_project_workspace_bytes(n), st));
+        if ((s = jit_project_select(col->dtype, P, P.pred.kind == FQ_PRED_BITMAP ? P.pred.bitmap : nullptr, w.status,
+                                    w.ticket, w.flags, w.total)) != FQ_OK)
+            return s;
+        FQ_HIP_TRY(hipMemcpyAsync(host, w.total, sizeof(host), hipMemcpyDeviceToHost, st));  // total + flag words
     }
     FQ_HIP_TRY(hipStreamSynchronize(st));
     const uint32_t pred_flags = (uint32_t)(host[1] & 0xffffffffu), val_flags = (uint32_t)(host[1] >> 32);

@@ -1042,9 +1042,9 @@ fq_jit_groupby(const TIn *__restrict__ col, long long n, long long head, const u
 //                   64-row words per step (lane l = row l of each word, 8-byte
 //                   loads, 8 in flight per lane), one ballot per word, lanes
 //                   0..7 store the 8 words;
-//   fq_jit_pscatter the compaction's scatter (fq_filter.hip's tiles of 256
-//                   words and their count/scan prefixes) with the projection
-//                   evaluated on the kept rows only, one store per output;
+//   fq_jit_pselect  one pass: predicate, decoupled look-back over tiles for
+//                   the output offsets, the projection evaluated on the kept
+//                   rows only, one store per output;
 //   fq_jit_pmap     no predicate: every row's outputs, 16-byte loads/stores.
 // ---------------------------------------------------------------------------
 struct HostProjConsts {
@@ -1064,7 +1064,7 @@ void pack_proj_consts(const ProjLaunch &P, HostProjConsts &hc) {
 }
 
 std::string proj_shape_key(const ProjLaunch &P, int32_t tin, int dev) {
-    std::string k = "PROJ";
+    std::string k = "PROJ" + std::to_string(select_tile_rows());
     auto put = [&k](int32_t v) { k.append(reinterpret_cast<const char *>(&v), sizeof v); };
     put(dev);
     put(tin);
@@ -1102,6 +1102,7 @@ bool gen_project_source(const ProjLaunch &P, int32_t tin, Gen &g, std::string &s
            std::to_string(FQ_MAX_PRED_LEAVES) + "]; Step pl[" + std::to_string(FQ_MAX_PRED_LEAVES) + "][" +
            std::to_string(kSteps) + "]; };\n";
     src += "struct Outs { void *p[" + std::to_string(FQ_MAX_PROJECT) + "]; };\n";
+    src += "#define PS_ROWS " + std::to_string(select_tile_rows() / 256) + "\n";
     src += "typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));\n";
     src += "__device__ __forceinline__ bool fq_pred(TIn x, const Consts &c, u32 &flags, u32 live) {\n";
     src += expr_pred ? pred_body : "    (void)x; (void)c; (void)flags; (void)live;\n    return true;\n";
@@ -1162,62 +1163,143 @@ fq_jit_pbits(const TIn *__restrict__ col, long long n, Consts c, u64 *__restrict
     if (lane == 0 && flags) atomicOr(fl, flags);
 }
 
-// tiles of 256 words (16,384 rows): fq_filter.hip's compact_count/scan give
-// each tile's output base (gpre[tile / 16] + intra[tile])
+// Single pass over the column (decoupled look-back): a workgroup takes the
+// next tile of 4,096 rows from a ticket counter (tiles are handed out in
+// order, so every tile it waits on belongs to a workgroup that is already
+// running), loads it (lane-consecutive 8-byte rows, 16 per lane in flight),
+// evaluates the predicate, publishes the tile's kept count (flag A), then
+// wave 0 walks back over the predecessors' status words, 64 per round trip,
+// until it meets an inclusive prefix (flag P), publishes its own (P) and
+// every wave writes its kept rows' outputs at base + rank.  Status
+// words are 64-bit agent-scope atomics: flag in the top 2 bits, count below.
+// The look-back is bounded: after ~2^20 polls the kernel flags an error
+// (fl[1] bit 31) and moves on, so a wave can never spin forever.
+#ifndef PS_ROWS
+#define PS_ROWS 16
+#endif
+#define PS_TILE (256 * PS_ROWS)
+#define PS_A (1ull << 62)
+#define PS_P (2ull << 62)
+#define PS_VAL(s) ((s) & ((1ull << 62) - 1ull))
+__device__ __forceinline__ u64 wave_sum64(u64 v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const u32 lo = __shfl_xor((u32)(v & 0xffffffffu), off, 64);
+        const u32 hi = __shfl_xor((u32)(v >> 32), off, 64);
+        v += ((u64)hi << 32) | lo;
+    }
+    return v;
+}
 extern "C" __global__ void __launch_bounds__(256)
-fq_jit_pscatter(const TIn *__restrict__ col, long long n, Consts c, const u64 *__restrict__ bm,
-                const u64 *__restrict__ intra, const u64 *__restrict__ gpre, Outs o, u32 *__restrict__ fl) {
-    const long long nwords = (n + 63) >> 6;
-    const long long w0 = (long long)blockIdx.x * 256;
-    __shared__ u64 s_word[256];
-    __shared__ u32 s_off[256];
-    __shared__ u32 s_wsum[4];
-    const int t = threadIdx.x;
-    const int lane = t & 63;
-    const int wave = t >> 6;
-    u64 word = 0;
-    if (w0 + t < nwords) {
-        word = bm[w0 + t];
-        const long long rows = n - (w0 + t) * 64;
-        if (rows < 64) word &= (1ull << rows) - 1ull;
-    }
-    s_word[t] = word;
-    const u32 cnt = (u32)__popcll(word);
-    u32 incl = cnt;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const u32 v = (u32)__shfl_up((int)incl, off, 64);
-        if (lane >= off) incl += v;
-    }
-    if (lane == 63) s_wsum[wave] = incl;
-    __syncthreads();
-    u32 wave_base = 0;
-    for (int i = 0; i < wave; ++i) wave_base += s_wsum[i];
-    s_off[t] = wave_base + incl - cnt;
-    __syncthreads();
-    const u64 base = gpre[blockIdx.x / 16] + intra[blockIdx.x];
+fq_jit_pselect(const TIn *__restrict__ col, long long n, Consts c, const u64 *__restrict__ bm, Outs o,
+               u64 *__restrict__ status, u32 *__restrict__ ticket, u32 *__restrict__ fl, u64 *__restrict__ total) {
+    __shared__ u32 s_next;
+    __shared__ u32 s_off[PS_ROWS * 4];
+    __shared__ u64 s_base, s_agg;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const u64 lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-    u32 flags = 0;
-    // each wave walks its 64 words, 8 at a time (8 rows per lane in flight)
-    for (int j = 0; j < 64; j += 8) {
-        TIn x[8];
-        u64 wd[8];
+    const long long ntiles = (n + PS_TILE - 1) / PS_TILE;
+    u32 pflags = 0, vflags = 0;
+    for (;;) {
+        // a ticket only when this workgroup can start the tile at once: a
+        // reserved tile that waits behind another one would stall every
+        // look-back that reaches it
+        if (tid == 0) s_next = atomicAdd(ticket, 1u);
+        __syncthreads();
+        const long long t = s_next;
+        if (t >= ntiles) break;
+        const long long r0 = t * PS_TILE;
+        TIn x[PS_ROWS];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const int wi = wave * 64 + j + k;
-            wd[k] = s_word[wi];
-            const long long row = (w0 + wi) * 64 + lane;
-            x[k] = ((wd[k] >> lane) & 1ull) ? __builtin_nontemporal_load(col + row) : TIn(0);
+        for (int k = 0; k < PS_ROWS; ++k) {
+            const long long row = r0 + k * 256 + tid;
+            x[k] = row < n ? __builtin_nontemporal_load(col + row) : TIn(0);
         }
+        u32 pass = 0, rank[PS_ROWS];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const int wi = wave * 64 + j + k;
-            if ((wd[k] >> lane) & 1ull)
-                fq_put(x[k], c, flags, 1u, o, (long long)(base + s_off[wi] + (u64)__popcll(wd[k] & lt)));
+        for (int k = 0; k < PS_ROWS; ++k) {
+            const long long row = r0 + k * 256 + tid;
+            const u32 live = row < n ? 1u : 0u;
+)" + std::string(P.pred.kind == FQ_PRED_BITMAP
+                     ? "            const bool p = live && ((bm[row >> 6] >> (row & 63)) & 1ull);\n            (void)c;\n"
+                     : "            const bool p = fq_pred(x[k], c, pflags, live) && live;\n") + R"(
+            const u64 b = __ballot(p);
+            pass |= (p ? 1u : 0u) << k;
+            rank[k] = (u32)__popcll(b & lt);
+            if (lane == 0) s_off[k * 4 + wave] = (u32)__popcll(b);
         }
+        __syncthreads();
+        if (wave == 0) {
+            // exclusive scan of the PS_ROWS * 4 (row group, wave) counts in
+            // k-major order: lane l owns entries [l * PER, l * PER + PER)
+            constexpr int NE = PS_ROWS * 4, PER = (NE + 63) / 64;
+            u32 cv[PER], tot = 0;
+#pragma unroll
+            for (int q = 0; q < PER; ++q) {
+                const int i = lane * PER + q;
+                cv[q] = i < NE ? s_off[i] : 0u;
+                tot += cv[q];
+            }
+            u32 incl = tot;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const u32 v = (u32)__shfl_up((int)incl, off, 64);
+                if (lane >= off) incl += v;
+            }
+            u32 run = incl - tot;
+#pragma unroll
+            for (int q = 0; q < PER; ++q) {
+                const int i = lane * PER + q;
+                if (i < NE) s_off[i] = run;
+                run += cv[q];
+            }
+            const u64 agg = (u64)__shfl((int)incl, 63, 64);
+            u64 excl = 0;
+            if (t == 0) {
+                if (lane == 0) __hip_atomic_store(status, PS_P | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                if (lane == 0) __hip_atomic_store(status + t, PS_A | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                long long j = t - 1;  // nearest predecessor of this window
+                unsigned polls = 0;
+                for (;;) {
+                    const long long idx = j - lane;
+                    const u64 sw = idx >= 0 ? __hip_atomic_load(status + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                            : PS_P;
+                    const u64 notready = __ballot((sw >> 62) == 0ull);
+                    const u64 isp = __ballot((sw >> 62) == 2ull);
+                    const int pl = isp ? __ffsll((long long)isp) - 1 : 63;  // nearest P (or the whole window)
+                    const u64 upto = pl == 63 ? ~0ull : ((2ull << pl) - 1ull);
+                    if (notready & upto) {  // a predecessor in range has not published yet
+                        if (++polls > (1u << 20)) {
+                            vflags |= 0x80000000u;
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(2);
+                        continue;
+                    }
+                    excl += wave_sum64(((upto >> lane) & 1ull) ? PS_VAL(sw) : 0ull);
+                    if (isp) break;
+                    j -= 64;
+                }
+                if (lane == 0) __hip_atomic_store(status + t, PS_P | (excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            if (lane == 0) {
+                s_base = excl;
+                s_agg = agg;
+            }
+        }
+        __syncthreads();
+        const u64 base = s_base;
+#pragma unroll
+        for (int k = 0; k < PS_ROWS; ++k)
+            if ((pass >> k) & 1u) fq_put(x[k], c, vflags, 1u, o, (long long)(base + s_off[k * 4 + wave] + rank[k]));
+        if (t == ntiles - 1 && tid == 0) *total = base + s_agg;
+        __syncthreads();  // s_off / s_base / s_next reused by the next tile
     }
-    flags = wave_or(flags);
-    if (lane == 0 && flags) atomicOr(fl, flags);
+    pflags = wave_or(pflags);
+    vflags = wave_or(vflags);
+    if (lane == 0 && pflags) atomicOr(fl, pflags);
+    if (lane == 0 && vflags) atomicOr(fl + 1, vflags);
 }
 
 // every row: 16-byte loads and stores of row pairs when the column and every
@@ -1480,7 +1562,7 @@ fq_status get_proj_kernels(int32_t col_dtype, const ProjLaunch &P, ProjKernels *
         Compiled c;
         if (!gen_project_source(P, col_dtype, g, src))
             return fqc::fail(FQ_E_UNSUPPORTED, "fused projection: column/expression types outside the device path");
-        fq_status s = compile(src, dev, c, "fq_jit_pscatter");
+        fq_status s = compile(src, dev, c, "fq_jit_pselect");
         if (s != FQ_OK) return s;
         ProjKernels k;
         if (dev < 0) {  // validated only
@@ -1530,8 +1612,8 @@ fq_status jit_project_bits(int32_t col_dtype, const ProjLaunch &P, uint64_t *d_b
     return FQ_OK;
 }
 
-fq_status jit_project_scatter(int32_t col_dtype, const ProjLaunch &P, const uint64_t *d_bitmap, const uint64_t *intra,
-                              const uint64_t *gpre, int64_t ntiles, uint32_t *d_flag) {
+fq_status jit_project_select(int32_t col_dtype, const ProjLaunch &P, const uint64_t *d_bitmap, uint64_t *status,
+                             uint32_t *ticket, uint32_t *d_flags, uint64_t *d_total) {
     ProjKernels k;
     fq_status s = get_proj_kernels(col_dtype, P, &k);
     if (s != FQ_OK || !k.scatter || P.n == 0) return s;
@@ -1543,8 +1625,18 @@ fq_status jit_project_scatter(int32_t col_dtype, const ProjLaunch &P, const uint
     for (int j = 0; j < FQ_MAX_PROJECT; ++j) outs.p[j] = j < P.n_out ? P.out[j] : nullptr;
     const void *col = P.col;
     long long n = P.n;
-    void *args[] = {&col, &n, &hc, &d_bitmap, &intra, &gpre, &outs, &d_flag};
-    FQ_HIP_TRY(hipModuleLaunchKernel(k.scatter, (unsigned)ntiles, 1, 1, kThreads, 1, 1, 0, P.stream, args, nullptr));
+    const int64_t ntiles = (P.n + select_tile_rows() - 1) / select_tile_rows();
+    void *args[] = {&col, &n, &hc, &d_bitmap, &outs, &status, &ticket, &d_flags, &d_total};
+    static const int wg_per_cu = [] {
+        const char *e = getenv("FQ_SELECT_WG_PER_CU");
+        const int v = e ? atoi(e) : 0;
+        return v >= 1 && v <= 16 ? v : 8;
+    }();
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipGetLastError();
+    const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(ntiles, (int64_t)cus * wg_per_cu));
+    FQ_HIP_TRY(hipModuleLaunchKernel(k.scatter, (unsigned)grid, 1, 1, kThreads, 1, 1, 0, P.stream, args, nullptr));
     g_jit_launches += 1;
     return FQ_OK;
 }

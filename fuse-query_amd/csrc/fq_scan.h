@@ -3,6 +3,8 @@
 // hipRTC-specialised kernel (fq_jit.hip).  Internal; not part of the ABI.
 #pragma once
 
+#include <stdlib.h>
+
 #include "fq_device.h"
 
 namespace fqk {
@@ -110,9 +112,21 @@ struct ProjLaunch {
 
 // predicate -> LSB-first bitmap words; predicate errors OR-ed into *d_flag
 fq_status jit_project_bits(int32_t col_dtype, const ProjLaunch &P, uint64_t *d_bitmap, uint32_t *d_flag);
-// kept rows (bitmap + the compaction's tile prefixes) -> the n_out outputs
-fq_status jit_project_scatter(int32_t col_dtype, const ProjLaunch &P, const uint64_t *d_bitmap, const uint64_t *intra,
-                              const uint64_t *gpre, int64_t ntiles, uint32_t *d_flag);
+// one pass: predicate (or P.pred.bitmap), decoupled look-back over tiles of
+// select_tile_rows() rows for the output offsets, the n_out outputs of the kept
+// rows.  status: one zeroed word per tile; ticket: one zeroed word;
+// d_flags[0] predicate errors, d_flags[1] expression errors (bit 31: the
+// look-back gave up); *d_total = rows kept.
+inline int64_t select_tile_rows() {  // 256 threads x PS_ROWS (FQ_SELECT_ROWS = 8/16/32, tuning)
+    static const int64_t v = [] {
+        const char *e = getenv("FQ_SELECT_ROWS");
+        const int r = e ? atoi(e) : 16;
+        return (int64_t)256 * ((r == 8 || r == 32) ? r : 16);
+    }();
+    return v;
+}
+fq_status jit_project_select(int32_t col_dtype, const ProjLaunch &P, const uint64_t *d_bitmap, uint64_t *status,
+                             uint32_t *ticket, uint32_t *d_flags, uint64_t *d_total);
 // no predicate: every row -> the n_out outputs
 fq_status jit_project_map(int32_t col_dtype, const ProjLaunch &P, uint32_t *d_flag);
 // hipRTC loadable and the policy not FQ_JIT_OFF

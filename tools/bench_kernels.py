@@ -146,6 +146,42 @@ def main():
     rec("aggregate C4 shape (interpreted)", "C4 with FQ_JIT_OFF", ms, 8 * n)
     ops.jit_config(abi.JIT_AUTO, 1 << 22)
 
+    # expression trees (FQ_OP_PUSH / FQ_OPERAND_STACK) in the fused scan
+    from fq_amd.expr import PUSH, STACK
+    vt, _ = chain(abi.DT_UINT64, [("+", 1), PUSH, ("%", 1000), ("*", STACK, True)])
+    ms = timed(lambda: agg(a, value=vt), args.reps)
+    rec("aggregate tree (number+1)*(number%1000)", "sum/max/min of an ArithmeticFunction tree", ms, 8 * n)
+
+    # FilterTransform -> ProjectionTransform fused (fq_filter_project)
+    flag = ops.Workspace(8)
+    readme_pred = predicate(abi.DT_UINT64, [("+", 1), PUSH, ("/", 2), ("+", STACK, True), ("+", 1)], "<", 100)
+    ac2 = a.col()
+    ms = timed(lambda: check(lib.fq_predicate_bitmap(C.byref(ac2), C.byref(readme_pred), C.c_void_p(bm.ptr),
+                                                     flag.ptr, st)), args.reps)
+    rec("predicate_bitmap (number+1)+(number/2)+1<100", "README WHERE, one kernel", ms, 8 * n + n // 8,
+        "includes the host sync for the error flag")
+    pws = ops.Workspace(lib.fq_filter_project_workspace_bytes(n))
+    out2 = ops.empty_column(n, abi.DT_UINT64)
+    p38 = predicate(abi.DT_UINT64, [], "<", (3 * 2**64) // 8)
+    vals = (abi.fq_expr * 2)(chain(abi.DT_UINT64, [("+", 1)])[0], chain(abi.DT_UINT64, [("/", 2)])[0])
+    outs = (C.c_void_p * 2)(out.ptr, out2.ptr)
+    bc2 = b.col()
+
+    def project():
+        check(lib.fq_filter_project(C.byref(bc2), C.byref(p38), vals, 2, outs, C.byref(kept), pws.ptr, pws.nbytes, st))
+
+    ms = timed(project, args.reps)
+    rec("filter_project 3/8 kept -> x+1, x/2", "Filter + Projection fused", ms, 8 * n + 2 * 8 * kept.value,
+        "two passes over the column (bits, scatter) + host sync for out_len")
+    hb = b.to_numpy()[:k]
+    kk = hb[hb < np.uint64((3 * 2**64) // 8)]
+    assert np.array_equal(out.to_numpy()[:len(kk)], kk + np.uint64(1))
+    vals1 = (abi.fq_expr * 1)(chain(abi.DT_UINT64, [("*", 3), ("+", 1)])[0])
+    outs1 = (C.c_void_p * 1)(out.ptr)
+    ms = timed(lambda: check(lib.fq_filter_project(C.byref(ac2), None, vals1, 1, outs1, C.byref(kept), pws.ptr,
+                                                   pws.nbytes, st)), args.reps)
+    rec("filter_project map x*3+1 (no predicate)", "Projection fused", ms, 16 * n, "host sync for out_len")
+
     # GROUP BY (fq_group_aggregate): LDS pre-aggregation, low and high cardinality
     key, _ = chain(abi.DT_UINT64, [("%", 1000)])
     aggs3 = [(abi.AGG_COUNT, abi.DT_UINT64), (abi.AGG_SUM, abi.DT_UINT64), (abi.AGG_MAX, abi.DT_UINT64)]

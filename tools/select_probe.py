@@ -1,0 +1,43 @@
+"""fq_filter_project (3/8 kept, 2 outputs) on a 10 GB column, HIP events."""
+import ctypes as C
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "fuse-query_amd"))
+import torch  # noqa: E402
+
+from fq_amd import abi, ops  # noqa: E402
+from fq_amd._lib import check, lib  # noqa: E402
+from fq_amd.expr import chain, predicate  # noqa: E402
+
+n = 1_250_000_000
+b = ops.splitmix_column(7, 0, n)
+out, out2 = ops.empty_column(n, abi.DT_UINT64), ops.empty_column(n, abi.DT_UINT64)
+pws = ops.Workspace(lib.fq_filter_project_workspace_bytes(n))
+kept = C.c_int64(0)
+st = ops._stream()
+p38 = predicate(abi.DT_UINT64, [], "<", (3 * 2**64) // 8)
+nout = int(os.environ.get("NOUT", "2"))
+vals = (abi.fq_expr * 2)(chain(abi.DT_UINT64, [("+", 1)])[0], chain(abi.DT_UINT64, [("/", 2)])[0])
+outs = (C.c_void_p * 2)(out.ptr, out2.ptr)
+bc = b.col()
+
+
+def project():
+    check(lib.fq_filter_project(C.byref(bc), C.byref(p38), vals, nout, outs, C.byref(kept), pws.ptr, pws.nbytes, st))
+
+
+project()
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+ts = []
+for _ in range(10):
+    e0.record()
+    project()
+    e1.record()
+    e1.synchronize()
+    ts.append(e0.elapsed_time(e1))
+ms = statistics.median(ts)
+nb = 8 * n + nout * 8 * kept.value
+print("WG/CU=%s nout=%d: %.3f ms, %.0f GB/s algorithmic, kept %d" % (os.environ.get("FQ_SELECT_WG_PER_CU", "8"), nout, ms,
+                                                                     nb / ms / 1e6, kept.value), flush=True)
