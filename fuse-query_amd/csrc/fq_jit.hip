@@ -1064,7 +1064,7 @@ void pack_proj_consts(const ProjLaunch &P, HostProjConsts &hc) {
 }
 
 std::string proj_shape_key(const ProjLaunch &P, int32_t tin, int dev) {
-    std::string k = "PROJ" + std::to_string(select_tile_rows());
+    std::string k = "PROJ" + std::to_string(select_threads()) + "x" + std::to_string(select_rows_per_thread());
     auto put = [&k](int32_t v) { k.append(reinterpret_cast<const char *>(&v), sizeof v); };
     put(dev);
     put(tin);
@@ -1102,7 +1102,8 @@ bool gen_project_source(const ProjLaunch &P, int32_t tin, Gen &g, std::string &s
            std::to_string(FQ_MAX_PRED_LEAVES) + "]; Step pl[" + std::to_string(FQ_MAX_PRED_LEAVES) + "][" +
            std::to_string(kSteps) + "]; };\n";
     src += "struct Outs { void *p[" + std::to_string(FQ_MAX_PROJECT) + "]; };\n";
-    src += "#define PS_ROWS " + std::to_string(select_tile_rows() / 256) + "\n";
+    src += "#define PS_ROWS " + std::to_string(select_rows_per_thread()) + "\n#define PS_THREADS " +
+           std::to_string(select_threads()) + "\n";
     src += "typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));\n";
     src += "__device__ __forceinline__ bool fq_pred(TIn x, const Consts &c, u32 &flags, u32 live) {\n";
     src += expr_pred ? pred_body : "    (void)x; (void)c; (void)flags; (void)live;\n    return true;\n";
@@ -1177,7 +1178,11 @@ fq_jit_pbits(const TIn *__restrict__ col, long long n, Consts c, u64 *__restrict
 #ifndef PS_ROWS
 #define PS_ROWS 16
 #endif
-#define PS_TILE (256 * PS_ROWS)
+#ifndef PS_THREADS
+#define PS_THREADS 256
+#endif
+#define PS_WAVES (PS_THREADS / 64)
+#define PS_TILE (PS_THREADS * PS_ROWS)
 #define PS_A (1ull << 62)
 #define PS_P (2ull << 62)
 #define PS_VAL(s) ((s) & ((1ull << 62) - 1ull))
@@ -1190,11 +1195,11 @@ __device__ __forceinline__ u64 wave_sum64(u64 v) {
     }
     return v;
 }
-extern "C" __global__ void __launch_bounds__(256)
+extern "C" __global__ void __launch_bounds__(PS_THREADS)
 fq_jit_pselect(const TIn *__restrict__ col, long long n, Consts c, const u64 *__restrict__ bm, Outs o,
                u64 *__restrict__ status, u32 *__restrict__ ticket, u32 *__restrict__ fl, u64 *__restrict__ total) {
     __shared__ u32 s_next;
-    __shared__ u32 s_off[PS_ROWS * 4];
+    __shared__ u32 s_off[PS_ROWS * PS_WAVES];
     __shared__ u64 s_base, s_agg;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const u64 lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
@@ -1212,13 +1217,13 @@ fq_jit_pselect(const TIn *__restrict__ col, long long n, Consts c, const u64 *__
         TIn x[PS_ROWS];
 #pragma unroll
         for (int k = 0; k < PS_ROWS; ++k) {
-            const long long row = r0 + k * 256 + tid;
+            const long long row = r0 + k * PS_THREADS + tid;
             x[k] = row < n ? __builtin_nontemporal_load(col + row) : TIn(0);
         }
         u32 pass = 0, rank[PS_ROWS];
 #pragma unroll
         for (int k = 0; k < PS_ROWS; ++k) {
-            const long long row = r0 + k * 256 + tid;
+            const long long row = r0 + k * PS_THREADS + tid;
             const u32 live = row < n ? 1u : 0u;
 )" + std::string(P.pred.kind == FQ_PRED_BITMAP
                      ? "            const bool p = live && ((bm[row >> 6] >> (row & 63)) & 1ull);\n            (void)c;\n"
@@ -1226,13 +1231,13 @@ fq_jit_pselect(const TIn *__restrict__ col, long long n, Consts c, const u64 *__
             const u64 b = __ballot(p);
             pass |= (p ? 1u : 0u) << k;
             rank[k] = (u32)__popcll(b & lt);
-            if (lane == 0) s_off[k * 4 + wave] = (u32)__popcll(b);
+            if (lane == 0) s_off[k * PS_WAVES + wave] = (u32)__popcll(b);
         }
         __syncthreads();
         if (wave == 0) {
-            // exclusive scan of the PS_ROWS * 4 (row group, wave) counts in
+            // exclusive scan of the PS_ROWS * PS_WAVES (row group, wave) counts in
             // k-major order: lane l owns entries [l * PER, l * PER + PER)
-            constexpr int NE = PS_ROWS * 4, PER = (NE + 63) / 64;
+            constexpr int NE = PS_ROWS * PS_WAVES, PER = (NE + 63) / 64;
             u32 cv[PER], tot = 0;
 #pragma unroll
             for (int q = 0; q < PER; ++q) {
@@ -1292,7 +1297,7 @@ fq_jit_pselect(const TIn *__restrict__ col, long long n, Consts c, const u64 *__
         const u64 base = s_base;
 #pragma unroll
         for (int k = 0; k < PS_ROWS; ++k)
-            if ((pass >> k) & 1u) fq_put(x[k], c, vflags, 1u, o, (long long)(base + s_off[k * 4 + wave] + rank[k]));
+            if ((pass >> k) & 1u) fq_put(x[k], c, vflags, 1u, o, (long long)(base + s_off[k * PS_WAVES + wave] + rank[k]));
         if (t == ntiles - 1 && tid == 0) *total = base + s_agg;
         __syncthreads();  // s_off / s_base / s_next reused by the next tile
     }
@@ -1636,7 +1641,8 @@ fq_status jit_project_select(int32_t col_dtype, const ProjLaunch &P, const uint6
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     (void)hipGetLastError();
     const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(ntiles, (int64_t)cus * wg_per_cu));
-    FQ_HIP_TRY(hipModuleLaunchKernel(k.scatter, (unsigned)grid, 1, 1, kThreads, 1, 1, 0, P.stream, args, nullptr));
+    FQ_HIP_TRY(hipModuleLaunchKernel(k.scatter, (unsigned)grid, 1, 1, (unsigned)select_threads(), 1, 1, 0, P.stream,
+                                     args, nullptr));
     g_jit_launches += 1;
     return FQ_OK;
 }

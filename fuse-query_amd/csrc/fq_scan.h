@@ -117,14 +117,25 @@ fq_status jit_project_bits(int32_t col_dtype, const ProjLaunch &P, uint64_t *d_b
 // rows.  status: one zeroed word per tile; ticket: one zeroed word;
 // d_flags[0] predicate errors, d_flags[1] expression errors (bit 31: the
 // look-back gave up); *d_total = rows kept.
-inline int64_t select_tile_rows() {  // 256 threads x PS_ROWS (FQ_SELECT_ROWS = 8/16/32, tuning)
-    static const int64_t v = [] {
-        const char *e = getenv("FQ_SELECT_ROWS");
-        const int r = e ? atoi(e) : 16;
-        return (int64_t)256 * ((r == 8 || r == 32) ? r : 16);
+// tile = select_threads() x select_rows_per_thread() rows (FQ_SELECT_THREADS
+// 256/512/1024, FQ_SELECT_ROWS 8/16/32: tuning; tools/select_probe.py)
+inline int select_threads() {
+    static const int v = [] {
+        const char *e = getenv("FQ_SELECT_THREADS");
+        const int t = e ? atoi(e) : 256;
+        return (t == 512 || t == 1024) ? t : 256;
     }();
     return v;
 }
+inline int select_rows_per_thread() {
+    static const int v = [] {
+        const char *e = getenv("FQ_SELECT_ROWS");
+        const int r = e ? atoi(e) : 32;
+        return (r == 8 || r == 16) ? r : 32;
+    }();
+    return v;
+}
+inline int64_t select_tile_rows() { return (int64_t)select_threads() * select_rows_per_thread(); }
 fq_status jit_project_select(int32_t col_dtype, const ProjLaunch &P, const uint64_t *d_bitmap, uint64_t *status,
                              uint32_t *ticket, uint32_t *d_flags, uint64_t *d_total);
 // no predicate: every row -> the n_out outputs
