@@ -277,10 +277,11 @@ __global__ void __launch_bounds__(kThreads)
 // butterfly; the result is deterministic for a given grid.
 template <typename V>
 __global__ void __launch_bounds__(kThreads)
-    agg_finalize_kernel(const Partial *__restrict__ parts, int nparts, uint64_t blocks,
+    agg_finalize_kernel(const Partial *__restrict__ parts, int nparts, uint64_t blocks, uint64_t rows,
                         int32_t vdtype, int empty_if_zero, fq_agg_state *__restrict__ out) {
     Acc<V> acc;
     acc.init();
+    if (threadIdx.x == 0) acc.cnt = rows;  // count-only scans: no column read (nparts == 0)
     for (int i = threadIdx.x; i < nparts; i += kThreads) {
         const Partial p = parts[i];
         acc.sum = acc.sum + from_bits<V>(p.sum);
@@ -580,8 +581,11 @@ static fq_status dispatch_pred(const Launch &L) {
 
 template <typename V>
 static fq_status launch_finalize(const Launch &L, uint64_t blocks, int empty_if_zero, fq_agg_state *d_out) {
+    // L.grid == 0: a count-only scan without predicate or expression -- the
+    // reference's Count adds block.num_rows() (function_aggregator.rs:60-66),
+    // no value is read, so neither is the column
     hipLaunchKernelGGL((agg_finalize_kernel<V>), dim3(1), dim3(kThreads), 0, L.stream, L.parts, L.grid,
-                       blocks, L.vdtype, empty_if_zero, d_out);
+                       blocks, L.grid == 0 ? (uint64_t)L.n : 0ull, L.vdtype, empty_if_zero, d_out);
     FQ_HIP_TRY(hipGetLastError());
     return FQ_OK;
 }
@@ -729,6 +733,10 @@ fq_status fq_aggregate(const fq_col *col, int64_t block_rows, const fq_pred *pre
     if (s != FQ_OK) return s;
     L.stream = (hipStream_t)stream;
     L.parts = (Partial *)d_ws;
+    if (agg_mask == FQ_AGG_COUNT && !chain && L.pred.kind == FQ_PRED_NONE) {
+        L.grid = 0;  // count(column): rows, not values (see launch_finalize)
+        return dispatch_finalize(L, blocks, empty_if_zero, d_out);
+    }
     bool jitted = false;
     const bool tree = (chain && prog_has_tree(L.val)) || pred_has_tree(L.pred);
     s = jit_scan(col->dtype, chain, L, &jitted, tree);

@@ -647,6 +647,16 @@ bool gen_source(const Launch &L, int32_t tin, bool chain, Gen &g, std::string &s
 // enough to find or claim a slot across XCDs.
 // ---------------------------------------------------------------------------
 
+// LDS slot hash of the GROUP BY kernel: 1 (default) keeps consecutive keys in
+// consecutive slots, 0 = Fibonacci hash of the whole key (FQ_GROUP_LDS_LOCAL)
+int group_lds_local() {
+    static const int v = [] {
+        const char *e = getenv("FQ_GROUP_LDS_LOCAL");
+        return e ? (atoi(e) ? 1 : 0) : 1;
+    }();
+    return v;
+}
+
 int lds_slots(int n_aggs, int budget) {
     int s = 16384;
     while (s > 64 && (int64_t)s * 8 * (1 + n_aggs) > budget) s >>= 1;
@@ -672,7 +682,7 @@ void pack_group_consts(const GroupLaunch &G, HostGroupConsts &hc) {
 }
 
 std::string group_shape_key(const GroupLaunch &G, int32_t tin, int dev) {
-    std::string k = "G";
+    std::string k = "G" + std::to_string(group_lds_local());
     auto put = [&k](int32_t v) { k.append(reinterpret_cast<const char *>(&v), sizeof v); };
     auto prog = [&put](const KProg &p) {
         put(p.n);
@@ -735,6 +745,7 @@ bool gen_groupby_source(const GroupLaunch &G, int32_t tin, Gen &g, std::string &
     src += "struct Tab { u64 *keys; u64 *st[" + std::to_string(FQ_MAX_GROUP_AGGS) +
            "]; u32 *hdr; long long mask; int rmask; };\n";
     src += "#define BT " + std::to_string(G.threads) + "\n#define ROWMAP " + std::to_string(G.rowmap) + "\n";
+    src += "#define LDS_LOCAL " + std::to_string(group_lds_local()) + "\n";
     src += "#define PMAX 16\n#define EMPTY 0xffffffffffffffffull\n#define NA " + std::to_string(NA) + "\n#define S " +
            std::to_string(S) + "\n#define LOG2S " + std::to_string(__builtin_ctz((unsigned)S)) + "\n";
     src += R"(
@@ -752,7 +763,15 @@ __device__ __forceinline__ u32 part_of(u64 k, u32 P) {
     return ((((u32)k ^ (u32)(k >> 32)) * 0x2545F491u) >> 26) & (P - 1);
 }
 __device__ __forceinline__ u32 lds_hash(u64 k) {
+#if LDS_LOCAL
+    // low LOG2S bits kept, the rest Fibonacci-hashed onto them: a wave's 64
+    // consecutive keys land in 64 consecutive slots (no LDS bank conflicts),
+    // keys that differ only above the table size still spread
+    const u32 f = (u32)k ^ (u32)(k >> 32);
+    return f + (((f >> LOG2S) * 0x9E3779B1u) >> (32 - LOG2S));
+#else
     return (((u32)k ^ (u32)(k >> 32)) * 0x9E3779B1u) >> (32 - LOG2S);
+#endif
 }
 __device__ __forceinline__ void amax_f64(u64 *p, double v) {
     u64 old = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -390,3 +390,21 @@ def test_limit_over_ten_billion_rows_stops_early():
         assert dt < 5.0, dt
     finally:
         e.close()
+
+
+@pytest.mark.parametrize("n", [0, 1, 9999, 10000, 100001, 80_000_000])
+def test_count_only_reads_no_column(n):
+    # count(number) alone: the reference's Count adds block.num_rows()
+    # (function_aggregator.rs:60-66); the device path counts rows without a scan
+    import fq_ref as R
+    from fq_amd import ops
+    if n:
+        r = q("SELECT count(number) FROM system.numbers_mt(%d)" % n)
+        exp = R.aggregate_query(n, [R.E_fn("count", R.E_field("number"))]) if n <= 100001 else None
+        rows = sum(be - bb + 1 for b, e in R.generate_parts(n) for bb, be in R.numbers_blocks(b, e))
+        assert r.rows == [(rows,)]
+        if exp is not None:
+            assert r.rows == [tuple(v.value for v in exp)]
+    col = ops.numbers_column(0, n)
+    st = ops.aggregate(col, 10000, None, None, abi.AGG_COUNT)
+    assert st.count == n and st.blocks == (n + 9999) // 10000
