@@ -194,6 +194,7 @@ struct Channel {
     std::condition_variable cv_send, cv_recv;
     struct Item {
         bool is_err = false;
+        size_t pipe = 0;  // input index (partition order)
         DataBlock block;
         FQException err{0, ""};
     };
@@ -209,6 +210,13 @@ struct Channel {
         q.push_back(std::move(it));
         cv_recv.notify_one();
         return true;
+    }
+    // errors are queued even after close() (the consumer drains them to pick
+    // the earliest partition's) and never wait for room
+    void send_error(Item it) {
+        std::lock_guard<std::mutex> lk(mu);
+        q.push_back(std::move(it));
+        cv_recv.notify_one();
     }
     void done() {
         std::lock_guard<std::mutex> lk(mu);
@@ -249,7 +257,17 @@ class ChannelStream : public BlockStream {
     bool next(DataBlock &out) override {
         Channel::Item it;
         if (!ch->recv(it)) return false;
-        if (it.is_err) throw it.err;
+        if (it.is_err) {
+            // Several pipes may fail; the reference surfaces whichever error
+            // reaches its channel first (processor_merge.rs:45-63).  Report
+            // the one of the earliest partition instead -- deterministic, and
+            // what a sequential run of the partitions raises first.
+            ch->close();
+            Channel::Item e = std::move(it);
+            while (ch->recv(it))
+                if (it.is_err && it.pipe < e.pipe) e = std::move(it);
+            throw e.err;
+        }
         out = std::move(it.block);
         return true;
     }
@@ -265,10 +283,10 @@ StreamRef MergeProcessor::execute() {
     cs->ch = std::make_shared<Channel>();
     cs->ch->cap = list_.size();
     cs->ch->live = (int)list_.size();
-    for (auto &input : list_) {
+    for (size_t pipe = 0; pipe < list_.size(); ++pipe) {
         std::shared_ptr<Channel> ch = cs->ch;
-        ProcessorRef in = input;
-        rt->pool.submit([in, ch, rt]() {
+        ProcessorRef in = list_[pipe];
+        rt->pool.submit([in, ch, rt, pipe]() {
             try {
                 ExecCtx ctx(rt);
                 StreamRef s = in->execute();
@@ -284,13 +302,15 @@ StreamRef MergeProcessor::execute() {
             } catch (const FQException &e) {
                 Channel::Item it;
                 it.is_err = true;
+                it.pipe = pipe;
                 it.err = e;
-                ch->send(std::move(it));
+                ch->send_error(std::move(it));
             } catch (const std::exception &e) {
                 Channel::Item it;
                 it.is_err = true;
+                it.pipe = pipe;
                 it.err = FQException(FQ_E_INTERNAL, std::string("Internal Error: ") + e.what());
-                ch->send(std::move(it));
+                ch->send_error(std::move(it));
             }
             ch->done();
         });
@@ -381,10 +401,16 @@ StreamRef AggregateFinalTransform::execute() {
     std::vector<FunctionRef> funcs;
     for (auto &f : funcs_) funcs.push_back(f->clone());
     StreamRef in = input_->execute();
+    // Every partial first, then the merge: an error of any partition (the
+    // earliest partition's, see ChannelStream) wins over an error of the
+    // merge itself (e.g. two None sums), as in a run where each partition's
+    // error surfaces before the final sees the other partitions' states.
+    std::vector<DataBlock> partials;
     DataBlock b;
-    while (in->next(b)) {
-        if (b.columns.empty() || !b.columns[0].host) continue;
-        const std::vector<DataValue> &rows = *b.columns[0].host;
+    while (in->next(b)) partials.push_back(std::move(b));
+    for (const DataBlock &pb : partials) {
+        if (pb.columns.empty() || !pb.columns[0].host) continue;
+        const std::vector<DataValue> &rows = *pb.columns[0].host;
         for (size_t i = 0; i < funcs.size() && i < rows.size(); ++i)
             if (rows[i].kind == DataValue::kStruct) funcs[i]->merge_state(rows[i].fields);
     }

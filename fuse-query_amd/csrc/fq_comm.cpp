@@ -23,6 +23,10 @@ struct fq_comm {
 
 namespace {
 
+// first bytes of an exchanged row that carries a rank's error instead of its
+// partial states (those start with "FQS1", pipeline.cpp encode_states)
+constexpr char kErrMagic[5] = "FQE1";
+
 fq_status nccl_fail(ncclResult_t r, const char *what) {
     return fqc::fail(FQ_E_RCCL, std::string("RCCL error: ") + what + ": " + ncclGetErrorString(r));
 }
@@ -104,11 +108,30 @@ fq_status fq_engine_execute_exchange(fq_engine *e, const char *sql, int32_t rank
     *out = nullptr;
     thread_local std::vector<uint8_t> local;
     fq_status st = run_partial(e, sql, rank, world, local);
-    if (st != FQ_OK) return st;
+    if (st != FQ_OK) {
+        // A rank whose partitions fail still takes part in the exchange (the
+        // others would wait in the collective forever): it ships an error
+        // record instead of states, and every rank reports the error of the
+        // lowest failing rank -- the earliest partitions, as on one GPU.
+        const std::string msg = fq_last_error();
+        local.assign(kErrMagic, kErrMagic + 4);
+        const int32_t code = st;
+        local.insert(local.end(), (const uint8_t *)&code, (const uint8_t *)&code + 4);
+        local.insert(local.end(), msg.begin(), msg.begin() + (long)std::min<size_t>(msg.size(), FQ_EXCHANGE_CAP_BYTES - 16));
+    }
     const void *rows = nullptr;
     size_t stride = 0;
-    st = fq_exchange_states(local.data(), local.size(), rank, world, allreduce, user, &rows, &stride);
-    if (st != FQ_OK) return st;
+    fq_status xs = fq_exchange_states(local.data(), local.size(), rank, world, allreduce, user, &rows, &stride);
+    if (xs != FQ_OK) return xs;
+    for (int32_t r = 0; r < world; ++r) {
+        const uint8_t *row = (const uint8_t *)rows + (size_t)r * stride;
+        if (stride >= 8 && memcmp(row, kErrMagic, 4) == 0) {
+            int32_t code;
+            memcpy(&code, row + 4, 4);
+            const char *m = (const char *)row + 8;
+            return fqc::fail(code, std::string(m, strnlen(m, stride - 8)));
+        }
+    }
     return fq_engine_execute_final(e, sql, rows, stride, world, out);
 }
 

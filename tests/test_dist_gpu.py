@@ -31,7 +31,14 @@ def free_port():
     return p
 
 
-def worker(rank, world, port, n, out_q):
+ERROR_SQLS = [
+    # division by zero only in rank 0's partitions (row 0) / only in rank 1's (row 3e6)
+    "SELECT sum(number) FROM system.numbers_mt(%d) WHERE (1000 %% number) = 1000",
+    "SELECT max(number) FROM system.numbers_mt(%d) WHERE (1000 %% (number - 3000000)) = 1000",
+]
+
+
+def worker(rank, world, port, n, out_q, sqls=None):
     for p in (os.path.join(ROOT, "fuse-query_amd"), os.path.join(ROOT, "oracle")):
         sys.path.insert(0, p)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -42,14 +49,41 @@ def worker(rank, world, port, n, out_q):
     from fq_amd import dist as fqd
     from fq_amd.engine import Engine
 
+    from fq_amd import FQError
+
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         with Engine(device=0) as eng:
-            out = [fqd.execute(eng, sql % n).rows for sql in SQLS]
+            out = []
+            for sql in (sqls or SQLS):
+                try:
+                    out.append(fqd.execute(eng, sql % n).rows)
+                except FQError as e:  # every rank must get the error, none may hang
+                    out.append(("error", e.status, str(e)))
         out_q.put((rank, out))
     finally:
         dist.destroy_process_group()
+
+
+def test_an_error_on_one_rank_reaches_every_rank():
+    # a rank whose partitions fail still takes part in the exchange (an error
+    # record instead of states): no rank waits in the collective, all report it
+    world, n = 2, 4_000_000
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=worker, args=(r, world, port, n, q, ERROR_SQLS)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    from fq_amd import abi
+    for rank, out in results:
+        for got in out:
+            assert got == ("error", abi.FQ_E_DIVIDE_BY_ZERO, "Internal Error: Divide by zero error"), (rank, got)
 
 
 def test_two_ranks_on_the_gpu_match_the_oracle():
