@@ -110,12 +110,22 @@ def run_engine(sql):
         return None, str(e)
 
 
-N_CHOICES = [1000, 80000, 100001]
+N_CHOICES = [1000, 80000, 100001, 1_000_003]
 
 
-@pytest.mark.parametrize("seed", range(200))
-def test_random_aggregate_query(seed):
-    rng = random.Random(1000 + seed)
+@pytest.fixture(params=["auto", "always"])
+def jit(request):
+    """AUTO: chains on these small blocks run on the interpreting kernels and
+    trees on hipRTC; ALWAYS: every fused shape is specialised."""
+    from fq_amd import abi, ops
+    ops.jit_config(abi.JIT_ALWAYS if request.param == "always" else abi.JIT_AUTO, 0 if request.param == "always" else 1 << 22)
+    yield request.param
+    ops.jit_config(abi.JIT_AUTO, 1 << 22)
+
+
+@pytest.mark.parametrize("seed", range(150))
+def test_random_aggregate_query(seed, jit):
+    rng = random.Random(1000 + seed + (100000 if jit == "always" else 0))
     n = rng.choice(N_CHOICES)
     items = []
     for _ in range(rng.randint(1, 3)):
