@@ -1190,7 +1190,12 @@ fq_jit_pbits(const TIn *__restrict__ col, long long n, Consts c, u64 *__restrict
 // evaluates the predicate, publishes the tile's kept count (flag A), then
 // wave 0 walks back over the predecessors' status words, 64 per round trip,
 // until it meets an inclusive prefix (flag P), publishes its own (P) and
-// every wave writes its kept rows' outputs at base + rank.  Status
+// every wave writes its kept rows' outputs at base + rank.  (Also publishing
+// the P of the A tiles it walked over measured slower: 3.2 -> 3.9 ms with
+// nothing kept.)  Tickets come from 8 counters, one per XCD (workgroup b
+// draws from counter b % 8 and gets tiles c, c + 8, ...): one counter served
+// ~150K tickets at its ~90 per us ceiling.  The lowest unfinished tile never
+// waits, so every tile is reached.  Status
 // words are 64-bit agent-scope atomics: flag in the top 2 bits, count below.
 // The look-back is bounded: after ~2^20 polls the kernel flags an error
 // (fl[1] bit 31) and moves on, so a wave can never spin forever.

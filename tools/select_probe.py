@@ -17,7 +17,8 @@ out, out2 = ops.empty_column(n, abi.DT_UINT64), ops.empty_column(n, abi.DT_UINT6
 pws = ops.Workspace(lib.fq_filter_project_workspace_bytes(n))
 kept = C.c_int64(0)
 st = ops._stream()
-p38 = predicate(abi.DT_UINT64, [], "<", (3 * 2**64) // 8)
+frac = float(os.environ.get("KEEP", "0.375"))
+p38 = predicate(abi.DT_UINT64, [], "<", min(int(frac * 2**64), 2**64 - 1))
 nout = int(os.environ.get("NOUT", "2"))
 vals = (abi.fq_expr * 2)(chain(abi.DT_UINT64, [("+", 1)])[0], chain(abi.DT_UINT64, [("/", 2)])[0])
 outs = (C.c_void_p * 2)(out.ptr, out2.ptr)
@@ -39,5 +40,5 @@ for _ in range(10):
     ts.append(e0.elapsed_time(e1))
 ms = statistics.median(ts)
 nb = 8 * n + nout * 8 * kept.value
-print("WG/CU=%s nout=%d: %.3f ms, %.0f GB/s algorithmic, kept %d" % (os.environ.get("FQ_SELECT_WG_PER_CU", "8"), nout, ms,
+print("keep=%s WG/CU=%s nout=%d: %.3f ms, %.0f GB/s algorithmic, kept %d" % (os.environ.get("KEEP", "0.375"), os.environ.get("FQ_SELECT_WG_PER_CU", "8"), nout, ms,
                                                                      nb / ms / 1e6, kept.value), flush=True)
