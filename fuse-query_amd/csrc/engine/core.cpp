@@ -346,6 +346,10 @@ Runtime::~Runtime() {
     (void)hipSetDevice(device_);
     for (auto &s : shared_) (void)hipStreamSynchronize(s);
     for (auto &w : all_) {
+        if (w->own) {
+            (void)hipStreamSynchronize(w->own);
+            (void)hipStreamDestroy(w->own);
+        }
         if (w->ws) (void)hipFree(w->ws);
         for (auto ev : w->events) (void)hipEventDestroy(ev);
         for (auto *c : w->slot_chunks) (void)hipHostFree(c);
@@ -436,9 +440,14 @@ std::shared_ptr<DeviceBuffer> DeviceBuffer::alloc_sync(size_t bytes) {
     return b;
 }
 
-ExecCtx::ExecCtx(Runtime *r) : rt(r), res(nullptr), prev_(g_current) {
+ExecCtx::ExecCtx(Runtime *r, bool own_queue) : rt(r), res(nullptr), prev_(g_current) {
     if (rt->has_device()) check_hip(hipSetDevice(rt->device()), "hipSetDevice");
     res = rt->acquire();
+    stream_ = res->stream;
+    if (own_queue && rt->has_device()) {
+        if (!res->own) check_hip(hipStreamCreateWithFlags(&res->own, hipStreamNonBlocking), "hipStreamCreateWithFlags");
+        stream_ = res->own;
+    }
     g_current = this;
 }
 

@@ -143,6 +143,7 @@ struct EngineStats {
 
 struct WorkerRes {
     hipStream_t stream = nullptr;
+    hipStream_t own = nullptr;  // private queue for row pipelines (created on first use)
     std::mutex *launch_mu = nullptr;  // serialises multi-call enqueues on a shared queue
     void *ws = nullptr;               // fq_aggregate workspace
     size_t ws_bytes = 0;
@@ -220,7 +221,10 @@ struct DeviceBuffer {
 // reference, processor_merge.rs:45-63): its device queue and workspaces.
 class ExecCtx {
    public:
-    ExecCtx(Runtime *rt);
+    // own_queue: this context's device work goes to its worker's private
+    // queue instead of the shared one (row pipelines synchronise per morsel,
+    // and a shared queue would make every pipe wait for all the others)
+    explicit ExecCtx(Runtime *rt, bool own_queue = false);
     ~ExecCtx();
     ExecCtx(const ExecCtx &) = delete;
     ExecCtx &operator=(const ExecCtx &) = delete;
@@ -229,11 +233,12 @@ class ExecCtx {
     Runtime *rt;
     WorkerRes *res;
     AggFusion *fusion = nullptr;  // set while an AggregatePartial drains its input
-    hipStream_t stream() const { return res->stream; }
+    hipStream_t stream() const { return stream_; }
     void sync();
 
    private:
     ExecCtx *prev_;
+    hipStream_t stream_ = nullptr;
 };
 
 // ---------------------------------------------------------------------------

@@ -286,9 +286,10 @@ StreamRef MergeProcessor::execute() {
     for (size_t pipe = 0; pipe < list_.size(); ++pipe) {
         std::shared_ptr<Channel> ch = cs->ch;
         ProcessorRef in = list_[pipe];
-        rt->pool.submit([in, ch, rt, pipe]() {
+        const bool own = own_queues_;
+        rt->pool.submit([in, ch, rt, pipe, own]() {
             try {
-                ExecCtx ctx(rt);
+                ExecCtx ctx(rt, own);
                 StreamRef s = in->execute();
                 DataBlock b;
                 // the consumer gone (a satisfied LIMIT dropped the merged
@@ -739,7 +740,7 @@ void Pipeline::add_simple_transform(const std::function<ProcessorRef()> &f) {
 void Pipeline::merge_processor() {
     if (pipes_.empty()) throw_internal("Can't merge processor when the last pipe is empty");
     if (pipes_.back().size() > 1) {
-        auto p = std::make_shared<MergeProcessor>();
+        auto p = std::make_shared<MergeProcessor>(own_queues_);
         for (auto &x : pipes_.back()) p->connect_to(x);
         pipes_.push_back({p});
     }

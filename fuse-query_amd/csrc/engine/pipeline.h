@@ -156,6 +156,7 @@ class EmptyProcessor : public IProcessor {  // processor_empty.rs:14-49
 
 class MergeProcessor : public IProcessor {  // processor_merge.rs:16-94
    public:
+    explicit MergeProcessor(bool own_queues = false) : own_queues_(own_queues) {}
     std::string name() const override { return "MergeProcessor"; }
     void connect_to(ProcessorRef input) override { list_.push_back(std::move(input)); }
     StreamRef execute() override;
@@ -163,6 +164,7 @@ class MergeProcessor : public IProcessor {  // processor_merge.rs:16-94
 
    private:
     std::vector<ProcessorRef> list_;
+    bool own_queues_;  // each input pipe on its worker's private device queue
 };
 
 class SourceTransform : public IProcessor {  // transform_source.rs:14-53
@@ -328,9 +330,12 @@ class Pipeline {
     void merge_processor();
     StreamRef execute();
     std::string display() const;
+    // row pipelines (no aggregate): merged pipes run on private device queues
+    void set_own_queues(bool v) { own_queues_ = v; }
 
    private:
     std::vector<std::vector<ProcessorRef>> pipes_;
+    bool own_queues_ = false;
 };
 
 // serialised partial states (one 16-byte record per DataValue)

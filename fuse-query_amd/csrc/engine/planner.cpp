@@ -609,6 +609,7 @@ Pipeline build_pipeline(const QueryPlan &plan, const QueryContextRef &ctx, bool 
     bool row_pipeline = true;
     for (const PlanNode &n : plan.nodes)
         if (n.kind == PlanNode::kAggregate) row_pipeline = false;
+    p.set_own_queues(row_pipeline);
     for (const PlanNode &n : plan.nodes) {
         switch (n.kind) {
             case PlanNode::kLimit: {
