@@ -657,6 +657,16 @@ int group_lds_local() {
     return v;
 }
 
+// HBM key probe of the GROUP BY kernel: 1 = plain cached read first
+// (FQ_GROUP_KEY_PLAIN), 0 = agent-scope atomic read
+int group_key_plain() {
+    static const int v = [] {
+        const char *e = getenv("FQ_GROUP_KEY_PLAIN");
+        return e ? (atoi(e) ? 1 : 0) : 1;
+    }();
+    return v;
+}
+
 int lds_slots(int n_aggs, int budget) {
     int s = 16384;
     while (s > 64 && (int64_t)s * 8 * (1 + n_aggs) > budget) s >>= 1;
@@ -682,7 +692,7 @@ void pack_group_consts(const GroupLaunch &G, HostGroupConsts &hc) {
 }
 
 std::string group_shape_key(const GroupLaunch &G, int32_t tin, int dev) {
-    std::string k = "G" + std::to_string(group_lds_local());
+    std::string k = "G" + std::to_string(group_lds_local()) + std::to_string(group_key_plain());
     auto put = [&k](int32_t v) { k.append(reinterpret_cast<const char *>(&v), sizeof v); };
     auto prog = [&put](const KProg &p) {
         put(p.n);
@@ -746,6 +756,7 @@ bool gen_groupby_source(const GroupLaunch &G, int32_t tin, Gen &g, std::string &
            "]; u32 *hdr; long long mask; int rmask; };\n";
     src += "#define BT " + std::to_string(G.threads) + "\n#define ROWMAP " + std::to_string(G.rowmap) + "\n";
     src += "#define LDS_LOCAL " + std::to_string(group_lds_local()) + "\n";
+    src += "#define GKEY_PLAIN " + std::to_string(group_key_plain()) + "\n";
     src += "#define PMAX 16\n#define EMPTY 0xffffffffffffffffull\n#define NA " + std::to_string(NA) + "\n#define S " +
            std::to_string(S) + "\n#define LOG2S " + std::to_string(__builtin_ctz((unsigned)S)) + "\n";
     src += R"(
@@ -797,7 +808,14 @@ __device__ long long ginsert(const Tab &t, u64 k) {
     }
     long long h = (long long)(mix(k) & (u64)t.mask);
     for (long long p = 0; p <= t.mask; ++p) {
+#if GKEY_PLAIN
+        // a plain (L2-cached) read: a slot's key is written once (EMPTY ->
+        // key), so a stale value can only be EMPTY, which the CAS below
+        // resolves; a hit never needs the memory-side round trip
+        const u64 cur = t.keys[h];
+#else
         const u64 cur = __hip_atomic_load(&t.keys[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
         if (cur == k) return h;
         if (cur == EMPTY) {
             const u64 old = atomicCAS((unsigned long long *)&t.keys[h], EMPTY, k);
