@@ -131,6 +131,11 @@ fq_status fq_engine_set_option(fq_engine *e, int32_t option, int64_t value) {
             case FQ_OPT_MODULO: e->modulo = value != 0; break;
             case FQ_OPT_PROFILE: e->rt->profile = value != 0; break;
             case FQ_OPT_STREAMS: e->rt->set_streams((int)value); break;
+            case FQ_OPT_CHUNK_ROWS:
+                if (value < 10000 || value % 10000)
+                    throw fq::FQException(FQ_E_INVALID, "FQ_OPT_CHUNK_ROWS must be a positive multiple of 10000");
+                e->ds->numbers()->set_chunk_rows((uint64_t)value);
+                break;
             default: throw fq::FQException(FQ_E_INVALID, "fq_engine_set_option: unknown option");
         }
     });

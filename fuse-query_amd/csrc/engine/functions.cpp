@@ -893,7 +893,11 @@ void AggFusion::end_block() {
         ctx_.rt->stats.scan_launches++;
         ctx_.rt->stats.scan_rows += (uint64_t)g.col.len;
         ctx_.rt->stats.scan_bytes += (uint64_t)g.col.len * (uint64_t)dtype_size(g.col.dtype);
-        keepalive_.push_back(g.col);
+        // a stream-ordered column (hipFreeAsync on the queue the scan was just
+        // enqueued on) may be dropped now: its memory returns to the pool only
+        // after the scan -- so a query over generated chunks holds one chunk per
+        // pipe, not all of them; a synchronously allocated one is kept to finish()
+        if (g.col.dev && !g.col.dev->async) keepalive_.push_back(g.col);
     }
     cur_.clear();
 }

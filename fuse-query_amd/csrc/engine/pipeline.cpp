@@ -114,7 +114,12 @@ class NumbersStream : public BlockStream {
                 return true;
             }
         }
-        const uint64_t n = morsels_ ? std::min(morsel_, rows_ - off_) : rows_ - off_;
+        // row pipelines: growing morsels; aggregates: the resident partition
+        // whole, a generated one in chunk_rows() pieces (bounded HBM; whole
+        // 10,000-row blocks, so the per-block state replay is unchanged)
+        const uint64_t n = morsels_      ? std::min(morsel_, rows_ - off_)
+                           : has_pinned_ ? rows_ - off_
+                                         : std::min(t_->chunk_rows(), rows_ - off_);
         Column col;
         if (has_pinned_) {
             col = pinned_.slice((int64_t)off_, (int64_t)n);

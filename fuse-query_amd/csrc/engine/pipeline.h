@@ -8,6 +8,7 @@
 // MergeProcessor channel like the reference forwards Err items.
 #pragma once
 
+#include <atomic>
 #include <condition_variable>
 #include <deque>
 #include <map>
@@ -92,6 +93,9 @@ class NumbersTable : public ITable {
     static void parse_part(const std::string &name, uint64_t &total, uint64_t &begin, uint64_t &end);
     static uint64_t stream_rows(uint64_t begin, uint64_t end);  // rows NumbersStream yields
     void pin(const std::string &part, Column col);
+    // device block size for partitions that are not resident (FQ_OPT_CHUNK_ROWS)
+    void set_chunk_rows(uint64_t r) { chunk_rows_ = r; }
+    uint64_t chunk_rows() const { return chunk_rows_; }
     void unpin_all();
     bool pinned(const std::string &part, Column &out);
 
@@ -99,6 +103,7 @@ class NumbersTable : public ITable {
     SchemaRef schema_;
     std::mutex mu_;
     std::map<std::string, Column> resident_;
+    std::atomic<uint64_t> chunk_rows_{400000000};
 };
 
 class DataSource {  // datasource.rs:11-62

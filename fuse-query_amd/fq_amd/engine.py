@@ -18,7 +18,7 @@ from .expr import from_bits
 
 P = C.POINTER
 
-OPT_WORKER_THREADS, OPT_MODULO, OPT_PROFILE, OPT_STREAMS = 1, 2, 3, 4
+OPT_WORKER_THREADS, OPT_MODULO, OPT_PROFILE, OPT_STREAMS, OPT_CHUNK_ROWS = 1, 2, 3, 4, 5
 
 ENGINE_SYMBOLS = [
     "fq_engine_create", "fq_engine_destroy", "fq_engine_set_option", "fq_engine_materialize_numbers",

@@ -42,6 +42,10 @@ typedef struct fq_result fq_result;
 #define FQ_OPT_PROFILE 3        /* 1: time every fused scan launch with HIP events */
 #define FQ_OPT_STREAMS 4        /* device queues the pipes share (default 1: the scans are
                                    HBM-bound, concurrency buys nothing and blurs timing) */
+#define FQ_OPT_CHUNK_ROWS 5     /* rows per device block of a numbers_mt partition that is NOT
+                                   resident (a multiple of 10,000; default 400,000,000 = 3.2 GB):
+                                   aggregates over numbers_mt(1e12) stream through bounded HBM
+                                   like the reference's 10,000-row blocks do through RAM */
 
 typedef struct fq_engine_stats {
     uint64_t scan_launches; /* fused aggregate scans launched                    */

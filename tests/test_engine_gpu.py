@@ -408,3 +408,47 @@ def test_count_only_reads_no_column(n):
     col = ops.numbers_column(0, n)
     st = ops.aggregate(col, 10000, None, None, abi.AGG_COUNT)
     assert st.count == n and st.blocks == (n + 9999) // 10000
+
+
+@pytest.mark.parametrize("sql", [
+    "SELECT sum(number)/count(number), max(number), min(number), count(number), sum(number) FROM system.numbers_mt(%d)",
+    "SELECT max(number+1), count(number), min(number*3) FROM system.numbers_mt(%d) WHERE (number%%8)<3",
+    "SELECT sum(number) FROM system.numbers_mt(%d) WHERE number %% 100000 < 3",   # empty blocks -> the reference's error
+    "SELECT sum(number+1) FROM system.numbers_mt(%d) WHERE number %% 7 = 2",
+    "SELECT number%%10, count(number), max(number) FROM system.numbers_mt(%d) GROUP BY number%%10",
+])
+def test_generated_partitions_stream_in_chunks(sql):
+    # numbers_mt partitions that are not resident are read in FQ_OPT_CHUNK_ROWS
+    # device blocks (whole 10,000-row blocks): the same results and errors as
+    # one block per partition
+    from fq_amd import FQError
+    from fq_amd.engine import OPT_CHUNK_ROWS
+    n = 1_000_003
+    e = Engine()
+    try:
+        e.set_option(OPT_CHUNK_ROWS, 30000)
+        try:
+            got = e.execute(sql % n).rows
+        except FQError as ex:
+            got = ("error", str(ex))
+    finally:
+        e.close()
+    try:
+        exp = q(sql % n).rows
+    except FQError as ex:
+        exp = ("error", str(ex))
+    assert got == exp
+    with pytest.raises(FQError):
+        E.set_option(OPT_CHUNK_ROWS, 12345)
+
+
+def test_non_resident_numbers_mt_beyond_hbm():
+    # numbers_mt(4e11): 3.2 TB generated in 3.2 GB chunks -- the reference
+    # streams it through 10,000-row blocks; one device block per partition
+    # would need 400 GB of HBM
+    e = Engine()
+    try:
+        r = e.execute("SELECT count(number), max(number), min(number) FROM system.numbers_mt(400000000000)")
+        assert r.rows == [(400000000000, 399999999999, 0)]
+    finally:
+        e.close()
