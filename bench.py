@@ -188,6 +188,8 @@ def main():
     ap.add_argument("--cpu-sample-rows", type=float, default=4e9)
     ap.add_argument("--cpu-threads", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--streams", type=int, default=1,
+                    help="device queues the pipes share (FQ_OPT_STREAMS); 1 = the scans run back to back")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="nccl = RCCL over xGMI (default); gloo rehearses N ranks on fewer GPUs")
     args = ap.parse_args()
@@ -213,7 +215,7 @@ def main():
 
     # The engine: SQL -> Source x P -> [Filter] -> AggregatePartial x P -> Merge
     # -> AggregateFinal on this GPU (one host thread per pipe, fused scans).
-    eng = Engine(device=local, profile=True)
+    eng = Engine(device=local, profile=True, streams=args.streams)
     mine = shard(generate_parts(n_total), rank, world)
     total_rows = sum(stream_rows(b, e) for _, b, e in mine)
     eng.materialize_numbers(n_total, rank, world)  # SourceTransform's column, resident in HBM
