@@ -342,6 +342,25 @@ static void u64_magic(uint64_t d, uint64_t &magic, uint32_t &shift, uint32_t &ad
     magic = proposed + 1;
 }
 
+// libdivide's u32 round-up magic (branchful form), for K_MODM32_U
+static void u32_magic(uint32_t d, uint32_t &magic, uint32_t &shift, uint32_t &add) {
+    const uint32_t l = 31 - __builtin_clz(d);
+    const uint64_t num = (uint64_t)1 << (32 + l);
+    uint32_t proposed = (uint32_t)(num / d);
+    const uint32_t rem = (uint32_t)(num % d);
+    const uint32_t e = d - rem;
+    if (e < (1u << l)) {
+        add = 0;
+    } else {
+        proposed += proposed;
+        const uint32_t twice_rem = rem + rem;
+        if (twice_rem >= d || twice_rem < rem) proposed += 1;
+        add = 1;
+    }
+    shift = l;
+    magic = proposed + 1;
+}
+
 static bool is_chain_dtype(int32_t dt) {
     return dt == FQ_DT_UINT64 || dt == FQ_DT_INT64 || dt == FQ_DT_FLOAT64;
 }
@@ -448,6 +467,12 @@ fq_status lower_expr(const fq_expr &e, int32_t col_dtype, KProg &out, int32_t &r
                         if (is_pow2(st.bits)) {
                             k.code = K_AND_U;
                             k.magic = st.bits - 1;
+                        } else if (st.bits <= 65535) {
+                            // 32-bit halves: (x>>32)%d * (2^32 % d) + (u32)x % d < 2^32
+                            k.code = K_MODM32_U;
+                            uint32_t m32 = 0;
+                            u32_magic((uint32_t)st.bits, m32, k.shift, k.add);
+                            k.magic = (uint64_t)m32 | ((((uint64_t)1 << 32) % st.bits) << 32);
                         } else {
                             k.code = K_MODM_U;
                             u64_magic(st.bits, k.magic, k.shift, k.add);

@@ -40,6 +40,9 @@ enum Code : int32_t {
     K_DIV_F,  // f64 '/', zero divisor -> DIV_ZERO (arrow 2.0 divide checks is_zero)
     K_MOD_F,
     K_PUSH,  // expression trees: push acc, acc = the column (hipRTC kernels only)
+    K_MODM32_U,  // u64 '%' by a constant d <= 65535: both 32-bit halves reduced with a
+                 // 32-bit magic, recombined as (hi % d) * (2^32 % d) + lo % d (< 2^32)
+                 // and reduced once more -- 32-bit multiplies instead of a 64-bit mul-high
 };
 
 struct KStep {
@@ -176,6 +179,21 @@ __device__ __forceinline__ uint64_t divm_u64(uint64_t x, uint64_t magic, uint32_
     return q >> shift;
 }
 
+// u32 n % d with a 32-bit round-up magic (libdivide u32 method; host-built)
+__device__ __forceinline__ uint32_t modm_u32(uint32_t n, uint32_t magic, uint32_t shift, uint32_t add, uint32_t d) {
+    uint32_t q = __umulhi(n, magic);
+    q = add ? ((((n - q) >> 1) + q) >> shift) : (q >> shift);
+    return n - q * d;
+}
+
+// u64 x % d for d <= 65535 (K_MODM32_U): mm = magic | (2^32 % d) << 32
+__device__ __forceinline__ uint64_t modm32_u64(uint64_t x, uint64_t mm, uint32_t shift, uint32_t add, uint64_t d) {
+    const uint32_t m = (uint32_t)mm, c2 = (uint32_t)(mm >> 32), dd = (uint32_t)d;
+    const uint32_t rh = modm_u32((uint32_t)(x >> 32), m, shift, add, dd);
+    const uint32_t rl = modm_u32((uint32_t)x, m, shift, add, dd);
+    return modm_u32(rh * c2 + rl, m, shift, add, dd);
+}
+
 // Rare, long operations are out-of-line calls so that the unrolled program
 // interpreter stays small enough for the instruction cache (a 64-bit divide
 // or fmod unrolled over E elements is thousands of instructions).
@@ -267,6 +285,10 @@ __device__ __forceinline__ void run_prog(const KProg &p, const TIn (&x)[E], uint
 #pragma unroll
                 for (int j = 0; j < E; ++j)
                     a[j] = a[j] - divm_u64(a[j], st.magic, st.shift, st.add) * st.c;
+                break;
+            case K_MODM32_U:
+#pragma unroll
+                for (int j = 0; j < E; ++j) a[j] = modm32_u64(a[j], st.magic, st.shift, st.add, st.c);
                 break;
             case K_ADD_F:
 #pragma unroll

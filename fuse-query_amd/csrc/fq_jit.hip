@@ -263,6 +263,16 @@ void emit_prog(Gen &g, std::string &body, const KProg &p, int32_t tin, const cha
             }
             case K_SHR_U: body += "    a = a >> (u32)" + g.K("s") + ";\n"; continue;
             case K_AND_U: body += "    a = a & " + g.K("m") + ";\n"; continue;
+            case K_MODM32_U: {
+                const std::string M = g.K("m"), S = g.K("s"), C = g.K("c");
+                const char *q = st.add ? "(((n - q) >> 1) + q) >> sh" : "q >> sh";
+                body += "    { const u32 m = (u32)" + M + ", c2 = (u32)(" + M + " >> 32), sh = (u32)" + S +
+                        ", d = (u32)" + C + ";\n";
+                body += std::string("      auto md = [&](u32 n) -> u32 { u32 q = __umulhi(n, m); q = ") + q +
+                        "; return n - q * d; };\n";
+                body += "      a = (u64)md(md((u32)(a >> 32)) * c2 + md((u32)a)); }\n";
+                continue;
+            }
             case K_DIVM_U:
             case K_MODM_U: {
                 const std::string M = g.K("m"), S = g.K("s");

@@ -127,11 +127,14 @@ def test_numbers_plus_one_with_mod_predicate():
     check_against_oracle(host, abi.DT_UINT64, 10000, pred=pred, value=value)
 
 
-@pytest.mark.parametrize("d", [1, 2, 3, 7, 8, 10, 1000, 1 << 33, (1 << 63) + 1, 2**64 - 1, 0x1234567890abcdef])
+@pytest.mark.parametrize("d", [1, 2, 3, 7, 8, 10, 641, 999, 1000, 1001, 4095, 10000, 65521, 65535, 65537,
+                               1 << 33, (1 << 63) + 1, 2**64 - 1, 0x1234567890abcdef])
 def test_div_mod_by_constant_magic(d):
+    # '%' by d <= 65535 runs on 32-bit halves (K_MODM32_U), larger d on the
+    # 64-bit multiply-high magic
     rng = np.random.default_rng(d & 0xffff)
     host = rng.integers(0, 2**64, size=70_001, dtype=np.uint64)
-    host[:4] = [0, 1, d - 1 if d > 1 else 0, 2**64 - 1]
+    host[:8] = [0, 1, d - 1 if d > 1 else 0, 2**64 - 1, 2**32 - 1, 2**32, (2**32 * d - 1) % 2**64, 2**63]
     for sym, ref in (("/", host // np.uint64(d)), ("%", host % np.uint64(d))):
         value, _ = chain(abi.DT_UINT64, [(sym, d)])
         st = ops.aggregate(ops.from_numpy(host), 0, None, value, ALL)
