@@ -454,6 +454,11 @@ fq_status lower_expr(const fq_expr &e, int32_t col_dtype, KProg &out, int32_t &r
                         if (is_pow2(st.bits)) {
                             k.code = K_SHR_U;
                             k.shift = (uint32_t)__builtin_ctzll(st.bits);
+                        } else if (st.bits <= 65535) {
+                            k.code = K_DIVM32_U;  // 32/16/16-bit long division
+                            uint32_t m32 = 0;
+                            u32_magic((uint32_t)st.bits, m32, k.shift, k.add);
+                            k.magic = m32;
                         } else {
                             k.code = K_DIVM_U;
                             u64_magic(st.bits, k.magic, k.shift, k.add);

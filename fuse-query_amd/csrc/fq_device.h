@@ -43,6 +43,8 @@ enum Code : int32_t {
     K_MODM32_U,  // u64 '%' by a constant d <= 65535: both 32-bit halves reduced with a
                  // 32-bit magic, recombined as (hi % d) * (2^32 % d) + lo % d (< 2^32)
                  // and reduced once more -- 32-bit multiplies instead of a 64-bit mul-high
+    K_DIVM32_U,  // u64 '/' by a constant d <= 65535: long division in 32/16/16-bit digits,
+                 // each step a 32-bit magic divide (every partial dividend < d * 2^16)
 };
 
 struct KStep {
@@ -194,6 +196,22 @@ __device__ __forceinline__ uint64_t modm32_u64(uint64_t x, uint64_t mm, uint32_t
     return modm_u32(rh * c2 + rl, m, shift, add, dd);
 }
 
+__device__ __forceinline__ uint32_t divm_u32(uint32_t n, uint32_t magic, uint32_t shift, uint32_t add) {
+    const uint32_t q = __umulhi(n, magic);
+    return add ? ((((n - q) >> 1) + q) >> shift) : (q >> shift);
+}
+
+// u64 x / d for d <= 65535 (K_DIVM32_U): qh = hi / d, then the remainder and
+// the low word's two 16-bit digits (each partial dividend < d * 2^16 < 2^32)
+__device__ __forceinline__ uint64_t divm32_u64(uint64_t x, uint32_t magic, uint32_t shift, uint32_t add, uint32_t d) {
+    const uint32_t hi = (uint32_t)(x >> 32), lo = (uint32_t)x;
+    const uint32_t qh = divm_u32(hi, magic, shift, add), rh = hi - qh * d;
+    const uint32_t t1 = (rh << 16) | (lo >> 16);
+    const uint32_t q1 = divm_u32(t1, magic, shift, add), r1 = t1 - q1 * d;
+    const uint32_t q0 = divm_u32((r1 << 16) | (lo & 0xffffu), magic, shift, add);
+    return ((uint64_t)qh << 32) | ((q1 << 16) + q0);
+}
+
 // Rare, long operations are out-of-line calls so that the unrolled program
 // interpreter stays small enough for the instruction cache (a 64-bit divide
 // or fmod unrolled over E elements is thousands of instructions).
@@ -289,6 +307,10 @@ __device__ __forceinline__ void run_prog(const KProg &p, const TIn (&x)[E], uint
             case K_MODM32_U:
 #pragma unroll
                 for (int j = 0; j < E; ++j) a[j] = modm32_u64(a[j], st.magic, st.shift, st.add, st.c);
+                break;
+            case K_DIVM32_U:
+#pragma unroll
+                for (int j = 0; j < E; ++j) a[j] = divm32_u64(a[j], (uint32_t)st.magic, st.shift, st.add, (uint32_t)st.c);
                 break;
             case K_ADD_F:
 #pragma unroll

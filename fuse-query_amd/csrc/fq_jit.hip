@@ -273,6 +273,17 @@ void emit_prog(Gen &g, std::string &body, const KProg &p, int32_t tin, const cha
                 body += "      a = (u64)md(md((u32)(a >> 32)) * c2 + md((u32)a)); }\n";
                 continue;
             }
+            case K_DIVM32_U: {
+                const std::string M = g.K("m"), S = g.K("s"), C = g.K("c");
+                const char *q = st.add ? "(((n - q) >> 1) + q) >> sh" : "q >> sh";
+                body += "    { const u32 m = (u32)" + M + ", sh = (u32)" + S + ", d = (u32)" + C + ";\n";
+                body += std::string("      auto dv = [&](u32 n) -> u32 { u32 q = __umulhi(n, m); return ") + q + "; };\n";
+                body += "      const u32 hi = (u32)(a >> 32), lo = (u32)a;\n"
+                        "      const u32 qh = dv(hi), t1 = ((hi - qh * d) << 16) | (lo >> 16);\n"
+                        "      const u32 q1 = dv(t1), q0 = dv(((t1 - q1 * d) << 16) | (lo & 0xffffu));\n"
+                        "      a = ((u64)qh << 32) | (u64)((q1 << 16) + q0); }\n";
+                continue;
+            }
             case K_DIVM_U:
             case K_MODM_U: {
                 const std::string M = g.K("m"), S = g.K("s");

@@ -141,6 +141,12 @@ def main():
     vd, _ = chain(abi.DT_UINT64, [("%", 1000003)])
     ms = timed(lambda: agg(b, value=vd), args.reps)
     rec("aggregate u64 % 1000003 (magic)", "sum/max/min(x % 1000003)", ms, 8 * n)
+    vm, _ = chain(abi.DT_UINT64, [("%", 1000)])
+    ms = timed(lambda: agg(b, value=vm), args.reps)
+    rec("aggregate u64 % 1000 (32-bit halves)", "sum/max/min(x % 1000)", ms, 8 * n)
+    vq, _ = chain(abi.DT_UINT64, [("/", 1000)])
+    ms = timed(lambda: agg(b, value=vq), args.reps)
+    rec("aggregate u64 / 1000 (32-bit long division)", "sum/max/min(x / 1000)", ms, 8 * n)
     ops.jit_config(abi.JIT_OFF)
     ms = timed(lambda: agg(a, pred=p, value=v, mask=abi.AGG_MAX | abi.AGG_COUNT), args.reps)
     rec("aggregate C4 shape (interpreted)", "C4 with FQ_JIT_OFF", ms, 8 * n)
