@@ -54,7 +54,10 @@ fq_status fq_exchange_states(const void *local, size_t len, int32_t rank, int32_
 /* Distributed aggregate query on rank `rank` of `world`: partial on this
  * rank's shard -> exchange through `allreduce` -> AggregateFinal in rank
  * order.  Every rank must call it with the same sql/world.  Covers the
- * queries fq_engine_execute_partial covers (aggregates, GROUP BY).        */
+ * queries fq_engine_execute_partial covers (aggregates, GROUP BY).  A rank
+ * whose partial fails still takes part in the exchange with an error record
+ * ("FQE1", status, message) instead of its states, so no rank waits in the
+ * collective; every rank then returns the error of the lowest failing rank. */
 fq_status fq_engine_execute_exchange(fq_engine *e, const char *sql, int32_t rank, int32_t world,
                                      fq_allreduce_fn allreduce, void *user, fq_result **out);
 
