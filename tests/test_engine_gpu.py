@@ -452,3 +452,22 @@ def test_non_resident_numbers_mt_beyond_hbm():
         assert r.rows == [(400000000000, 399999999999, 0)]
     finally:
         e.close()
+
+
+def test_row_pipeline_over_resident_partitions_matches_generated():
+    # morsels of a materialised partition are slices of its resident column;
+    # the same query over generated partitions must return the same rows
+    n = 40_000_000
+    sql = ("SELECT number, number*3 + number%%7 FROM system.numbers_mt(%d) WHERE number %% 999983 < 2" % n)
+    gen = sorted(q(sql).rows)
+    e = Engine()
+    try:
+        e.materialize_numbers(n)
+        res = sorted(e.execute(sql).rows)
+        lim = e.execute("SELECT number FROM system.numbers_mt(%d) WHERE number %% 999983 = 1 LIMIT 3" % n).rows
+    finally:
+        e.close()
+    assert res == gen
+    assert [r[0] for r in gen] == [x for x in range(n) if x % 999983 < 2]
+    assert all(b == a * 3 + a % 7 for a, b in gen)
+    assert len(lim) == 3 and all(v % 999983 == 1 for (v,) in lim)
