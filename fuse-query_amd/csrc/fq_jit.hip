@@ -205,12 +205,24 @@ void put_pred_key(const KPred &pr, std::string &k) {
     }
 }
 
+// 16-byte vectors per lane in flight in the block-mode scan (FQ_BLOCK_U: 4, 8
+// or 16; tuning)
+int block_mode_vectors() {
+    static const int v = [] {
+        const char *e = getenv("FQ_BLOCK_U");
+        const int u = e ? atoi(e) : 8;
+        return (u == 4 || u == 16) ? u : 8;
+    }();
+    return v;
+}
+
 // Binary shape key: everything the generated source depends on.
 std::string shape_key(const Launch &L, int32_t tin, bool chain, int dev) {
     std::string k;
     k.reserve(256);
     auto put = [&k](int32_t v) { k.append(reinterpret_cast<const char *>(&v), sizeof v); };
     put(dev);
+    put(block_mode_vectors());
     put(tin);
     put(L.vdtype);
     put((int32_t)L.mask);
@@ -487,6 +499,7 @@ bool gen_source(const Launch &L, int32_t tin, bool chain, Gen &g, std::string &s
     src += "}\n";
     src += "__device__ __forceinline__ V fq_val(TIn x, const Consts &c, u32 &flags, u32 live) {\n" + val_body + "}\n";
     const uint32_t m = L.mask;
+    src += "#define BM_U " + std::to_string(block_mode_vectors()) + "\n";
     src += "struct Acc { V sum, mx, mn; u64 cnt; u32 flags; };\n";
     src += "__device__ __forceinline__ u32 fq_acc(Acc &acc, TIn x, long long idx, u32 live, const Consts &c,\n"
            "                                      const u64 *__restrict__ bitmap) {\n"
@@ -579,16 +592,16 @@ bool gen_source(const Launch &L, int32_t tin, bool chain, Gen &g, std::string &s
         if (vec) {
             const long long nv = (e - s) >> 1;
             const u32x4 *__restrict__ bp = (const u32x4 *)(col + s);
-            for (long long v = lane; v < nv; v += 64 * 4) {
-                u32x4 raw[4];
+            for (long long v = lane; v < nv; v += 64 * BM_U) {
+                u32x4 raw[BM_U];
 #pragma unroll
-                for (int k = 0; k < 4; ++k) {
+                for (int k = 0; k < BM_U; ++k) {
                     const long long vk = v + (long long)k * 64;
                     if (vk < nv) raw[k] = __builtin_nontemporal_load(bp + vk);
                     else raw[k] = u32x4{0u, 0u, 0u, 0u};
                 }
 #pragma unroll
-                for (int k = 0; k < 4; ++k) {
+                for (int k = 0; k < BM_U; ++k) {
                     const long long vk = v + (long long)k * 64;
                     const u32 li = vk < nv ? 1u : 0u;
                     TIn x[2];
