@@ -61,7 +61,8 @@ __device__ __forceinline__ void tstore(TAcc a, Partial *out) {
 
 // MAP 0: grid-stride over vectors (production); MAP 1: each workgroup owns a
 // contiguous chunk; MAP 2: grid-stride in units of a workgroup-wide tile of
-// U vectors per lane (tile-contiguous per WG).
+// U vectors per lane (tile-contiguous per WG); MAP 3: MAP 2 within one
+// contiguous eighth of the tiles per XCD.
 template <int U, int NT, int MAP>
 __global__ void tune_scan_kernel(const uint64_t *__restrict__ col, int64_t n, Partial *__restrict__ parts) {
     TAcc a{0, 0, ~0ull, 0};
@@ -106,6 +107,33 @@ __global__ void tune_scan_kernel(const uint64_t *__restrict__ col, int64_t n, Pa
             a.cnt += 2 * U;
         }
         for (; v < e0; v += B) {
+            u32x4_t r = ld16<NT>(vp + v);
+            tacc(a, ((uint64_t)r.y << 32) | r.x);
+            tacc(a, ((uint64_t)r.w << 32) | r.z);
+            a.cnt += 2;
+        }
+    } else if constexpr (MAP == 3) {
+        // XCD-partitioned tiles: workgroup b runs on XCD b % 8 (round-robin
+        // dispatch), XCD x streams the x-th eighth of the tiles, its
+        // workgroups grid-striding through that slice
+        const int64_t tile = (int64_t)U * B;
+        const int64_t ntiles = nvec / tile;
+        const int64_t per = (ntiles + 7) / 8;
+        const int64_t x = blockIdx.x & 7, G8 = gridDim.x >> 3;
+        const int64_t t1 = (x + 1) * per < ntiles ? (x + 1) * per : ntiles;
+        for (int64_t t = x * per + (blockIdx.x >> 3); t < t1; t += G8) {
+            const int64_t base = t * tile + threadIdx.x;
+            u32x4_t r[U];
+#pragma unroll
+            for (int k = 0; k < U; ++k) r[k] = ld16<NT>(vp + base + (int64_t)k * B);
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                tacc(a, ((uint64_t)r[k].y << 32) | r[k].x);
+                tacc(a, ((uint64_t)r[k].w << 32) | r[k].z);
+            }
+            a.cnt += 2 * U;
+        }
+        for (int64_t v = ntiles * tile + (int64_t)blockIdx.x * B + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * B) {
             u32x4_t r = ld16<NT>(vp + v);
             tacc(a, ((uint64_t)r.y << 32) | r.x);
             tacc(a, ((uint64_t)r.w << 32) | r.z);
@@ -156,7 +184,7 @@ extern "C" fq_status fq_tune_scan_u64(const uint64_t *col, int64_t n, int32_t va
     const int U = variant / 100, NT = (variant / 10) % 10, MAP = variant % 10;
 #define FQ_T(u, nt, m) \
     if (U == u && NT == nt && MAP == m) { launch<u, nt, m>(col, n, grid, block, p, st); FQ_HIP_TRY(hipGetLastError()); return FQ_OK; }
-#define FQ_TU(u) FQ_T(u, 0, 0) FQ_T(u, 1, 0) FQ_T(u, 0, 1) FQ_T(u, 1, 1) FQ_T(u, 0, 2) FQ_T(u, 1, 2)
+#define FQ_TU(u) FQ_T(u, 0, 0) FQ_T(u, 1, 0) FQ_T(u, 0, 1) FQ_T(u, 1, 1) FQ_T(u, 0, 2) FQ_T(u, 1, 2) FQ_T(u, 1, 3)
     FQ_TU(1) FQ_TU(2) FQ_TU(4) FQ_TU(8) FQ_TU(16)
 #undef FQ_TU
 #undef FQ_T

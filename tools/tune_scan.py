@@ -87,6 +87,7 @@ def main():
     ap.add_argument("--us", default="2,4,8,16")
     ap.add_argument("--grids", default="2,4,8,16")
     ap.add_argument("--blocks", default="256,512")
+    ap.add_argument("--maps", default="0,1,2,3", help="0 vector grid-stride, 1 chunked, 2 tile-contiguous, 3 XCD-partitioned")
     ap.add_argument("--write", action="store_true", help="sweep the write-side kernels instead")
     args = ap.parse_args()
     if args.write:
@@ -97,9 +98,12 @@ def main():
     stream = ops._stream()
     cus = torch.cuda.get_device_properties(0).multi_processor_count
     configs = []
-    for u, nt, m, g, b in itertools.product([int(x) for x in args.us.split(",")], (0, 1), (0, 1, 2),
+    maps = [int(x) for x in args.maps.split(",")]
+    for u, nt, m, g, b in itertools.product([int(x) for x in args.us.split(",")], (0, 1), maps,
                                             [int(x) for x in args.grids.split(",")],
                                             [int(x) for x in args.blocks.split(",")]):
+        if m == 3 and nt == 0:
+            continue  # the XCD-partitioned map is built non-temporal only
         grid = cus * g * 256 // b
         configs.append((u * 100 + nt * 10 + m, grid, b))
     times = {c: [] for c in configs}
