@@ -10,7 +10,8 @@ Workload (BASELINE.json configs[2], the north_star query):
   FROM system.numbers_mt(1e10 x N_gpus)
 Weak scaling: every GPU owns 1e10 rows = its share [8r/G, 8(r+1)/G) of the
 8 numbers_mt partitions, materialised in HBM before timing (the 8-GPU run is
-configs[4], numbers_mt(8e10)).  One step = the hot path over the resident
+configs[4], numbers_mt(8e10)).  --rows-total 1e10 instead fixes N (strong
+scaling: the 10B-row query split over 1/2/4/8 GPUs).  One step = the hot path over the resident
 column: per partition one fused scan kernel (sum/count/max/min in one read)
 -> partial states -> AggregateFinal merge, across GPUs one RCCL all-reduce of
 the 48-byte states over xGMI.  Rank 0 prints ONE JSON line.
@@ -185,6 +186,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--query", default="c3", choices=sorted(QUERIES))
     ap.add_argument("--rows-per-gpu", type=float, default=1e10)
+    ap.add_argument("--rows-total", type=float, default=None,
+                    help="strong scaling: fix numbers_mt(N) at this N for every GPU count "
+                         "(e.g. 1e10 = the 10B-row metric split over 1/2/4/8 GPUs)")
     ap.add_argument("--cpu-sample-rows", type=float, default=4e9)
     ap.add_argument("--cpu-threads", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -208,8 +212,12 @@ def main():
         else:
             dist.init_process_group("gloo")
 
-    rows_per_gpu = int(args.rows_per_gpu)
-    n_total = rows_per_gpu * world
+    if args.rows_total:
+        n_total = int(args.rows_total)
+        rows_per_gpu = n_total // world
+    else:
+        rows_per_gpu = int(args.rows_per_gpu)
+        n_total = rows_per_gpu * world
     sql, _mask = QUERIES[args.query]
     sql = sql.format(N=n_total)
 
@@ -294,7 +302,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": dt / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.rows_total else "weak",
             "vs_baseline": value / README_ROWS_PER_S[args.query] if args.query in README_ROWS_PER_S else None,
             "vs_baseline_ref": README_REF.get(args.query, "no published reference number for this query"),
             "dtype": "u64",
