@@ -471,3 +471,41 @@ def test_row_pipeline_over_resident_partitions_matches_generated():
     assert [r[0] for r in gen] == [x for x in range(n) if x % 999983 < 2]
     assert all(b == a * 3 + a % 7 for a, b in gen)
     assert len(lim) == 3 and all(v % 999983 == 1 for (v,) in lim)
+
+
+def test_device_block_cache_reuse_across_queries_and_engines():
+    # engine/core.cpp BlockCache: buffers freed on a queue are reused by later
+    # allocations on that queue (morsel outputs, fused-scan states, workspaces).
+    # Interleave row pipelines of different morsel sizes with aggregates, three
+    # rounds, then close the engine (its queues' cached blocks are freed) and
+    # run again on a fresh one: every result stays exact.
+    cases = []
+    for total in (100001, 1_280_000, 5_000_000):
+        exp = [x for x in _stream_rows(total) if x % 31 == 7]
+        cases.append(("SELECT number, number*3 FROM system.numbers_mt(%d) WHERE number %% 31 = 7" % total,
+                      sorted((x, 3 * x) for x in exp)))
+        rows = _stream_rows(total)
+        cases.append(("SELECT sum(number), count(number), max(number) FROM system.numbers_mt(%d)" % total,
+                      [(sum(rows) % 2**64, len(rows), max(rows))]))
+    cases.append(("SELECT number FROM system.numbers_mt(1000000) LIMIT 5", None))
+
+    def run(eng):
+        for sql, exp in cases:
+            r = eng.execute(sql)
+            if exp is None:
+                assert len(r.rows) == 5
+                assert all(0 <= v < 1000000 for (v,) in r.rows)
+            else:
+                assert sorted(r.rows) == exp, sql
+
+    e = Engine()
+    try:
+        for _ in range(3):
+            run(e)
+    finally:
+        e.close()
+    e2 = Engine()
+    try:
+        run(e2)
+    finally:
+        e2.close()
