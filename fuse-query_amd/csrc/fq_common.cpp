@@ -278,3 +278,26 @@ bool cast_scalar(uint64_t bits, int32_t from, int32_t to, uint64_t *out) {
 }
 
 }  // namespace fqc
+
+namespace fqc {
+namespace {
+struct Staging {
+    uint64_t *p = nullptr;
+    bool tried = false;
+    ~Staging() {
+        if (p) (void)hipHostFree(p);
+    }
+};
+thread_local Staging g_staging;
+}  // namespace
+
+uint64_t *host_staging() {
+    if (!g_staging.tried) {
+        g_staging.tried = true;
+        void *p = nullptr;
+        if (hipHostMalloc(&p, 8 * sizeof(uint64_t), hipHostMallocDefault) == hipSuccess) g_staging.p = (uint64_t *)p;
+        else (void)hipGetLastError();
+    }
+    return g_staging.p;
+}
+}  // namespace fqc

@@ -16,6 +16,11 @@ fq_status fail(fq_status st, const std::string &msg);
 // FuseQueryError::Internal(msg) -> "Internal Error: msg"
 fq_status internal(const std::string &msg);
 fq_status hip_fail(hipError_t e, const char *what);
+// 8 words of pinned host memory owned by the calling thread (nullptr if the
+// allocation failed): the staging buffer for the few device-to-host reads of
+// counts and flags per call, which from pageable memory cost ~25 us of host
+// time each (profiles/r01_readme_limit_trace.txt)
+uint64_t *host_staging();
 
 int device_cu_count();  // CUs of the current device (cached per device)
 

@@ -453,7 +453,10 @@ fq_status fq_filter_project(const fq_col *col, const fq_pred *pred, const fq_exp
         return fqc::fail(FQ_E_INVALID, "fq_filter_project: workspace too small");
     const ProjWs w = proj_ws(d_ws, n);
     hipStream_t st = P.stream;
-    uint64_t host[2] = {0, 0};  // kept rows, flag words
+    uint64_t local[2] = {0, 0};
+    uint64_t *const pinned = fqc::host_staging();
+    uint64_t *const host = pinned ? pinned : local;  // kept rows, flag words
+    host[0] = host[1] = 0;
     if (P.pred.kind == FQ_PRED_NONE) {
         FQ_HIP_TRY(hipMemsetAsync(w.flags, 0, 2 * sizeof(uint32_t), st));
         if ((s = jit_project_map(col->dtype, P, w.flags + 1)) != FQ_OK) return s;
@@ -464,7 +467,7 @@ fq_status fq_filter_project(const fq_col *col, const fq_pred *pred, const fq_exp
         if ((s = jit_project_select(col->dtype, P, P.pred.kind == FQ_PRED_BITMAP ? P.pred.bitmap : nullptr, w.status,
                                     w.ticket, w.flags, w.total)) != FQ_OK)
             return s;
-        FQ_HIP_TRY(hipMemcpyAsync(host, w.total, sizeof(host), hipMemcpyDeviceToHost, st));  // total + flag words
+        FQ_HIP_TRY(hipMemcpyAsync(host, w.total, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));  // total + flag words
     }
     FQ_HIP_TRY(hipStreamSynchronize(st));
     const uint32_t pred_flags = (uint32_t)(host[1] & 0xffffffffu), val_flags = (uint32_t)(host[1] >> 32);
@@ -491,10 +494,12 @@ fq_status fq_predicate_bitmap(const fq_col *col, const fq_pred *pred, uint64_t *
     if (!d_bitmap || !d_flag) return fqc::fail(FQ_E_INVALID, "fq_predicate_bitmap: NULL buffer");
     FQ_HIP_TRY(hipMemsetAsync(d_flag, 0, sizeof(uint32_t), P.stream));
     if ((s = jit_project_bits(col->dtype, P, d_bitmap, d_flag)) != FQ_OK) return s;
-    uint32_t h = 0;
-    FQ_HIP_TRY(hipMemcpyAsync(&h, d_flag, sizeof(h), hipMemcpyDeviceToHost, P.stream));
+    uint32_t local = 0;
+    uint64_t *const pinned = fqc::host_staging();
+    uint32_t *const h = pinned ? (uint32_t *)pinned : &local;
+    FQ_HIP_TRY(hipMemcpyAsync(h, d_flag, sizeof(uint32_t), hipMemcpyDeviceToHost, P.stream));
     FQ_HIP_TRY(hipStreamSynchronize(P.stream));
-    return flag_error(h);
+    return flag_error(*h);
 }
 
 fq_status fq_filter_compact(const fq_col *in, const uint64_t *d_bitmap, void *d_out, int64_t *out_len,
@@ -547,10 +552,12 @@ fq_status fq_filter_compact(const fq_col *in, const uint64_t *d_bitmap, void *d_
             break;
     }
     FQ_HIP_TRY(hipGetLastError());
-    uint64_t total = 0;
-    FQ_HIP_TRY(hipMemcpyAsync(&total, gpre + ngroups, sizeof(total), hipMemcpyDeviceToHost, st));
+    uint64_t local = 0;
+    uint64_t *const pinned = fqc::host_staging();
+    uint64_t *const total = pinned ? pinned : &local;
+    FQ_HIP_TRY(hipMemcpyAsync(total, gpre + ngroups, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     FQ_HIP_TRY(hipStreamSynchronize(st));
-    *out_len = (int64_t)total;
+    *out_len = (int64_t)*total;
     return FQ_OK;
 }
 
