@@ -135,6 +135,25 @@ inline int select_rows_per_thread() {
     }();
     return v;
 }
+// s_sleep between look-back polls of a predecessor that has not published
+// (FQ_SELECT_SLEEP 0..8, tuning; default 2)
+inline int select_sleep() {
+    static const int v = [] {
+        const char *e = getenv("FQ_SELECT_SLEEP");
+        const int x = e ? atoi(e) : 2;
+        return (x >= 0 && x <= 8) ? x : 2;
+    }();
+    return v;
+}
+// FQ_SELECT_DIAG=1: tiles skip the look-back (WRONG output offsets) -- only
+// for tools/select_probe.py to price the look-back against the rest
+inline int select_diag() {
+    static const int v = [] {
+        const char *e = getenv("FQ_SELECT_DIAG");
+        return (e && atoi(e) == 1) ? 1 : 0;
+    }();
+    return v;
+}
 inline int64_t select_tile_rows() { return (int64_t)select_threads() * select_rows_per_thread(); }
 fq_status jit_project_select(int32_t col_dtype, const ProjLaunch &P, const uint64_t *d_bitmap, uint64_t *status,
                              uint32_t *ticket, uint32_t *d_flags, uint64_t *d_total);
