@@ -300,6 +300,8 @@ class BlockCache {
         return *c;
     }
     void add_stream(hipStream_t s) {
+        static const bool off = getenv("FQ_NO_BLOCK_CACHE") != nullptr;  // A/B switch: plain stream-ordered pool
+        if (off) return;
         std::lock_guard<std::mutex> lk(mu_);
         free_.emplace(s, std::multimap<size_t, void *>());
     }
