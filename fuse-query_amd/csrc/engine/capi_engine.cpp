@@ -146,6 +146,8 @@ fq_status fq_engine_materialize_numbers(fq_engine *e, uint64_t total, int32_t ra
     if (world < 1 || rank < 0 || rank >= world) return fqc::fail(FQ_E_INVALID, "bad rank/world");
     return guard([&] {
         fq::ExecCtx ctx(e->rt.get());
+        // long-lived columns of up to 10 GB each: give the idle cached blocks back first
+        fq::reclaim_device_memory();
         auto parts = fq::NumbersTable::generate_parts(total);
         const size_t np = parts.size();
         const size_t lo = np * (size_t)rank / (size_t)world, hi = np * (size_t)(rank + 1) / (size_t)world;
@@ -168,6 +170,15 @@ fq_status fq_engine_materialize_numbers(fq_engine *e, uint64_t total, int32_t ra
 fq_status fq_engine_release_numbers(fq_engine *e) {
     if (!e) return fqc::fail(FQ_E_INVALID, "NULL engine");
     return guard([&] { e->ds->numbers()->unpin_all(); });
+}
+
+fq_status fq_engine_trim_memory(fq_engine *e) {
+    if (!e) return fqc::fail(FQ_E_INVALID, "NULL engine");
+    return guard([&] {
+        if (!e->rt->has_device()) return;
+        fq::check_hip(hipSetDevice(e->rt->device()), "hipSetDevice");
+        fq::reclaim_device_memory();
+    });
 }
 
 fq_status fq_engine_execute(fq_engine *e, const char *sql, fq_result **out) {

@@ -287,14 +287,27 @@ const DataField &DataSchema::field_with_name(const std::string &name) const { re
 // --hip-runtime-trace): 20-80 us per hipMallocAsync and up to 2.5 ms per
 // hipFreeAsync of a morsel buffer -- 5.4 of its 6.6 ms.  A block freed on
 // queue S goes to S's free list instead; an allocation on S takes a cached
-// block of S (best fit, at most 1/4 larger).  Reuse stays in S's order, which
-// is exactly the guarantee hipFreeAsync(ptr, S) + hipMallocAsync(S) give, so
-// no event is needed.  Only the runtime's own queues are cached (registered
-// when created, dropped before they are destroyed); at most kCacheBytes.
+// block of S of the same size class.  Reuse stays in S's order: the block is
+// only handed out again to work queued on S after everything S already holds.
+// That is the guarantee hipFreeAsync(ptr, S) + hipMallocAsync(S) give PROVIDED
+// every reader of the block ran on S -- DeviceBuffer's destructor makes S wait
+// for the dropping thread's queue when that is a different one (a block built
+// on a pipe's private queue and read on the consumer's after MergeProcessor);
+// see the invariant at DeviceBuffer in core.h.
+//
+// Sizes are rounded up to classes (4 per power of two, <= 25 % slack) so that
+// blocks of one class are interchangeable; blocks above kMaxBlock are never
+// cached (they are rare and would crowd out the frequent small ones), each
+// queue keeps at most kStreamBytes and the whole cache kCacheBytes.  Every
+// allocation failure -- stream-ordered, hipMalloc or the workspace -- calls
+// reclaim_device_memory(): the cache is flushed and the default pool trimmed
+// to 0, then the allocation is retried once.
 namespace {
 class BlockCache {
    public:
-    static constexpr size_t kCacheBytes = 8ull << 30;
+    static constexpr size_t kCacheBytes = 6ull << 30;
+    static constexpr size_t kStreamBytes = 2ull << 30;
+    static constexpr size_t kMaxBlock = 1ull << 30;
     static BlockCache &get() {
         static BlockCache *c = new BlockCache();  // never destroyed: buffers may outlive statics
         return *c;
@@ -303,27 +316,30 @@ class BlockCache {
         static const bool off = getenv("FQ_NO_BLOCK_CACHE") != nullptr;  // A/B switch: plain stream-ordered pool
         if (off) return;
         std::lock_guard<std::mutex> lk(mu_);
-        free_.emplace(s, std::multimap<size_t, void *>());
+        free_.emplace(s, Queue());
     }
-    // a cached block of s holding `bytes` (its size -> *got), or nullptr
-    void *take(hipStream_t s, size_t bytes, size_t *got) {
+    // a cached block of s of exactly `bytes` (a size class), or nullptr
+    void *take(hipStream_t s, size_t bytes) {
         std::lock_guard<std::mutex> lk(mu_);
         auto f = free_.find(s);
         if (f == free_.end()) return nullptr;
-        auto it = f->second.lower_bound(bytes);
-        if (it == f->second.end() || it->first > bytes + bytes / 4) return nullptr;
+        auto it = f->second.blocks.find(bytes);
+        if (it == f->second.blocks.end()) return nullptr;
         void *p = it->second;
-        *got = it->first;
-        cached_ -= it->first;
-        f->second.erase(it);
+        cached_ -= bytes;
+        f->second.bytes -= bytes;
+        f->second.blocks.erase(it);
         return p;
     }
-    // false: not cached (unregistered queue or cache full), the caller frees
+    // false: not cached (unregistered queue, oversized block or a cap
+    // reached), the caller frees
     bool put(hipStream_t s, void *p, size_t bytes) {
+        if (bytes > kMaxBlock) return false;
         std::lock_guard<std::mutex> lk(mu_);
         auto f = free_.find(s);
-        if (f == free_.end() || cached_ + bytes > kCacheBytes) return false;
-        f->second.emplace(bytes, p);
+        if (f == free_.end() || cached_ + bytes > kCacheBytes || f->second.bytes + bytes > kStreamBytes) return false;
+        f->second.blocks.emplace(bytes, p);
+        f->second.bytes += bytes;
         cached_ += bytes;
         return true;
     }
@@ -332,30 +348,84 @@ class BlockCache {
         std::lock_guard<std::mutex> lk(mu_);
         auto f = free_.find(s);
         if (f == free_.end()) return;
-        for (auto &b : f->second) {
+        for (auto &b : f->second.blocks) {
             (void)hipFree(b.second);
             cached_ -= b.first;
         }
         free_.erase(f);
     }
-    // allocation failure: hand every cached block back to the device pool
+    // hand every cached block back to the device pool (in its queue's order)
     void flush() {
         std::lock_guard<std::mutex> lk(mu_);
         for (auto &f : free_) {
-            if (f.second.empty()) continue;
-            for (auto &b : f.second) (void)hipFreeAsync(b.second, f.first);
-            f.second.clear();
+            if (f.second.blocks.empty()) continue;
+            for (auto &b : f.second.blocks) (void)hipFreeAsync(b.second, f.first);
+            f.second.blocks.clear();
+            f.second.bytes = 0;
             (void)hipStreamSynchronize(f.first);
         }
         cached_ = 0;
     }
+    size_t cached_bytes() {
+        std::lock_guard<std::mutex> lk(mu_);
+        return cached_;
+    }
 
    private:
+    struct Queue {
+        std::multimap<size_t, void *> blocks;
+        size_t bytes = 0;
+    };
     std::mutex mu_;
-    std::unordered_map<hipStream_t, std::multimap<size_t, void *>> free_;
+    std::unordered_map<hipStream_t, Queue> free_;
     size_t cached_ = 0;
 };
+
+// One reusable ordering event per (thread, device) for cross-queue drops.
+hipEvent_t drop_event(int device) {
+    thread_local std::unordered_map<int, hipEvent_t> ev;  // leaked at thread exit (HIP may be gone by then)
+    auto it = ev.find(device);
+    if (it != ev.end()) return it->second;
+    hipEvent_t e = nullptr;
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    ev.emplace(device, e);
+    return e;
+}
+
+// hipMalloc-family call with one reclaim-and-retry on failure
+template <class F> hipError_t alloc_with_reclaim(F f) {
+    hipError_t e = f();
+    if (e == hipSuccess) return e;
+    (void)hipGetLastError();
+    reclaim_device_memory();
+    e = f();
+    if (e != hipSuccess) (void)hipGetLastError();
+    return e;
+}
 }  // namespace
+
+size_t size_class(size_t bytes) {
+    if (bytes <= 256) return 256;
+    const int k = 63 - __builtin_clzll((unsigned long long)(bytes - 1));  // 2^k < bytes <= 2^(k+1)
+    const size_t step = ((size_t)1 << k) / 4;
+    return (bytes + step - 1) / step * step;
+}
+
+void reclaim_device_memory() {
+    BlockCache::get().flush();
+    // every stream-ordered free has to land in the pool before the trim
+    (void)hipDeviceSynchronize();
+    int dev = 0;
+    hipMemPool_t pool;
+    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess)
+        (void)hipMemPoolTrimTo(pool, 0);
+    (void)hipGetLastError();
+}
+
+size_t block_cache_bytes() { return BlockCache::get().cached_bytes(); }
 
 Runtime::Runtime(int device) : device_(device) {
     if (device == kHostOnly) return;  // planning / AggregateFinal merges only
@@ -410,7 +480,7 @@ WorkerRes *Runtime::acquire() {
     w->stream = shared_[q];
     w->launch_mu = shared_mu_[q].get();
     w->ws_bytes = fq_aggregate_workspace_bytes(0);
-    check_hip(hipMalloc(&w->ws, w->ws_bytes), "hipMalloc(workspace)");
+    check_hip(alloc_with_reclaim([&] { return hipMalloc(&w->ws, w->ws_bytes); }), "hipMalloc(workspace)");
     all_.push_back(std::move(w));
     return all_.back().get();
 }
@@ -490,8 +560,20 @@ static thread_local ExecCtx *g_current = nullptr;
 
 DeviceBuffer::~DeviceBuffer() {
     if (!ptr) return;
-    if (!async) (void)hipFree(ptr);
-    else if (!BlockCache::get().put(stream, ptr, bytes)) (void)hipFreeAsync(ptr, stream);
+    if (!async) {
+        (void)hipFree(ptr);
+        return;
+    }
+    // Dropped on another queue than the one it was allocated on (a merged
+    // block read by the consumer): the allocating queue waits for the
+    // dropping thread's queue before the block can be reused or freed there.
+    ExecCtx *c = ExecCtx::current_or_null();
+    if (c && c->rt->has_device() && c->stream() != stream) {
+        hipEvent_t ev = drop_event(c->rt->device());
+        if (ev && hipEventRecord(ev, c->stream()) == hipSuccess) (void)hipStreamWaitEvent(stream, ev, 0);
+        (void)hipGetLastError();
+    }
+    if (!BlockCache::get().put(stream, ptr, bytes)) (void)hipFreeAsync(ptr, stream);
 }
 
 static void require_device() {
@@ -504,20 +586,13 @@ static void require_device() {
 std::shared_ptr<DeviceBuffer> DeviceBuffer::alloc(size_t bytes, hipStream_t st) {
     require_device();
     auto b = std::make_shared<DeviceBuffer>();
-    b->bytes = bytes < 256 ? 256 : bytes;
+    b->bytes = size_class(bytes);
     b->stream = st;
-    size_t got = 0;
-    if ((b->ptr = BlockCache::get().take(st, b->bytes, &got))) {
-        b->bytes = got;
-        return b;
-    }
-    if (hipMallocAsync(&b->ptr, b->bytes, st) != hipSuccess) {
-        (void)hipGetLastError();
-        BlockCache::get().flush();
-        if (hipMallocAsync(&b->ptr, b->bytes, st) == hipSuccess) return b;
-        (void)hipGetLastError();
+    if ((b->ptr = BlockCache::get().take(st, b->bytes))) return b;
+    if (alloc_with_reclaim([&] { return hipMallocAsync(&b->ptr, b->bytes, st); }) != hipSuccess) {
+        b->ptr = nullptr;
         b->async = false;
-        check_hip(hipMalloc(&b->ptr, b->bytes), "hipMalloc");
+        check_hip(alloc_with_reclaim([&] { return hipMalloc(&b->ptr, b->bytes); }), "hipMalloc");
     }
     return b;
 }
@@ -527,7 +602,7 @@ std::shared_ptr<DeviceBuffer> DeviceBuffer::alloc_sync(size_t bytes) {
     auto b = std::make_shared<DeviceBuffer>();
     b->bytes = bytes < 256 ? 256 : bytes;
     b->async = false;
-    check_hip(hipMalloc(&b->ptr, b->bytes), "hipMalloc(table)");
+    check_hip(alloc_with_reclaim([&] { return hipMalloc(&b->ptr, b->bytes); }), "hipMalloc(table)");
     return b;
 }
 

@@ -203,7 +203,18 @@ class Runtime {
     int active_streams_ = 1;
 };
 
-// Device memory released with hipFreeAsync on the stream that owns it.
+// Device memory released with hipFreeAsync on the stream that owns it (or
+// kept in the engine's stream-ordered block cache, core.cpp, for the next
+// allocation of its size class on that stream).
+//
+// Invariant: a stream-ordered buffer may be read on another queue than its
+// allocation queue `stream` only by work queued BEFORE the buffer is dropped
+// by a thread whose ExecCtx is bound to that reading queue.  The destructor
+// then records an event on the dropping thread's queue and makes `stream`
+// wait for it, so the allocation queue's next user of the block (cache reuse
+// or pool reuse after hipFreeAsync) is ordered after those reads.  A buffer
+// read on a queue that is neither `stream` nor the dropping thread's queue
+// must be synchronised by its reader before the last reference goes.
 struct DeviceBuffer {
     void *ptr = nullptr;
     size_t bytes = 0;
@@ -216,6 +227,14 @@ struct DeviceBuffer {
     static std::shared_ptr<DeviceBuffer> alloc(size_t bytes, hipStream_t st);
     static std::shared_ptr<DeviceBuffer> alloc_sync(size_t bytes);  // long-lived tables
 };
+
+// Allocation size class: 256 B minimum, then 4 classes per power of two.
+size_t size_class(size_t bytes);
+// Flush the block cache, wait for the device, trim the default pool to 0:
+// every allocation failure calls it before its one retry; also before large
+// long-lived allocations and through fq_engine_trim_memory.
+void reclaim_device_memory();
+size_t block_cache_bytes();
 
 // Execution context of the thread running a pipe (tokio task in the
 // reference, processor_merge.rs:45-63): its device queue and workspaces.

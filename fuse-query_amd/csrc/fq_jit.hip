@@ -1136,7 +1136,7 @@ void pack_proj_consts(const ProjLaunch &P, HostProjConsts &hc) {
 
 std::string proj_shape_key(const ProjLaunch &P, int32_t tin, int dev) {
     std::string k = "PROJ" + std::to_string(select_threads()) + "x" + std::to_string(select_rows_per_thread()) + "s" +
-                    std::to_string(select_sleep()) + "d" + std::to_string(select_diag());
+                    std::to_string(select_sleep());
     auto put = [&k](int32_t v) { k.append(reinterpret_cast<const char *>(&v), sizeof v); };
     put(dev);
     put(tin);
@@ -1175,7 +1175,7 @@ bool gen_project_source(const ProjLaunch &P, int32_t tin, Gen &g, std::string &s
            std::to_string(kSteps) + "]; };\n";
     src += "struct Outs { void *p[" + std::to_string(FQ_MAX_PROJECT) + "]; };\n";
     src += "#define PS_ROWS " + std::to_string(select_rows_per_thread()) + "\n#define PS_THREADS " +
-           std::to_string(select_threads()) + "\n#define PS_SLEEP " + std::to_string(select_sleep()) + "\n#define PS_DIAG " + std::to_string(select_diag()) + "\n";
+           std::to_string(select_threads()) + "\n#define PS_SLEEP " + std::to_string(select_sleep()) + "\n";
     src += "typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));\n";
     src += "__device__ __forceinline__ bool fq_pred(TIn x, const Consts &c, u32 &flags, u32 live) {\n";
     src += expr_pred ? pred_body : "    (void)x; (void)c; (void)flags; (void)live;\n    return true;\n";
@@ -1261,9 +1261,6 @@ fq_jit_pbits(const TIn *__restrict__ col, long long n, Consts c, u64 *__restrict
 #ifndef PS_SLEEP
 #define PS_SLEEP 2
 #endif
-#ifndef PS_DIAG
-#define PS_DIAG 0
-#endif
 #define PS_WAVES (PS_THREADS / 64)
 #define PS_TILE (PS_THREADS * PS_ROWS)
 #define PS_A (1ull << 62)
@@ -1343,7 +1340,7 @@ fq_jit_pselect(const TIn *__restrict__ col, long long n, Consts c, const u64 *__
             }
             const u64 agg = (u64)__shfl((int)incl, 63, 64);
             u64 excl = 0;
-            if (t == 0 || PS_DIAG == 1) {  // PS_DIAG 1 (diagnostic only, wrong offsets): no look-back
+            if (t == 0) {
                 if (lane == 0) __hip_atomic_store(status + t, PS_P | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             } else {
                 if (lane == 0) __hip_atomic_store(status + t, PS_A | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

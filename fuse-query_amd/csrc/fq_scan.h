@@ -145,15 +145,6 @@ inline int select_sleep() {
     }();
     return v;
 }
-// FQ_SELECT_DIAG=1: tiles skip the look-back (WRONG output offsets) -- only
-// for tools/select_probe.py to price the look-back against the rest
-inline int select_diag() {
-    static const int v = [] {
-        const char *e = getenv("FQ_SELECT_DIAG");
-        return (e && atoi(e) == 1) ? 1 : 0;
-    }();
-    return v;
-}
 inline int64_t select_tile_rows() { return (int64_t)select_threads() * select_rows_per_thread(); }
 fq_status jit_project_select(int32_t col_dtype, const ProjLaunch &P, const uint64_t *d_bitmap, uint64_t *status,
                              uint32_t *ticket, uint32_t *d_flags, uint64_t *d_total);

@@ -22,7 +22,7 @@ OPT_WORKER_THREADS, OPT_MODULO, OPT_PROFILE, OPT_STREAMS, OPT_CHUNK_ROWS = 1, 2,
 
 ENGINE_SYMBOLS = [
     "fq_engine_create", "fq_engine_destroy", "fq_engine_set_option", "fq_engine_materialize_numbers",
-    "fq_engine_release_numbers", "fq_engine_execute", "fq_engine_explain", "fq_engine_execute_partial",
+    "fq_engine_release_numbers", "fq_engine_trim_memory", "fq_engine_execute", "fq_engine_explain", "fq_engine_execute_partial",
     "fq_engine_execute_final", "fq_engine_get_stats", "fq_engine_reset_stats", "fq_result_num_rows",
     "fq_result_num_columns", "fq_result_column_name", "fq_result_column_type", "fq_result_value",
     "fq_result_text", "fq_result_free", "fq_result_mysql_type", "fq_result_values",
@@ -41,6 +41,7 @@ _protos = {
     "fq_engine_set_option": (C.c_int32, [C.c_void_p, C.c_int32, C.c_int64]),
     "fq_engine_materialize_numbers": (C.c_int32, [C.c_void_p, C.c_uint64, C.c_int32, C.c_int32]),
     "fq_engine_release_numbers": (C.c_int32, [C.c_void_p]),
+    "fq_engine_trim_memory": (C.c_int32, [C.c_void_p]),
     "fq_engine_execute": (C.c_int32, [C.c_void_p, C.c_char_p, P(C.c_void_p)]),
     "fq_engine_explain": (C.c_int32, [C.c_void_p, C.c_char_p, C.c_char_p, C.c_size_t, P(C.c_size_t)]),
     "fq_engine_execute_partial": (C.c_int32, [C.c_void_p, C.c_char_p, C.c_int32, C.c_int32, C.c_void_p,
@@ -211,6 +212,10 @@ class Engine:
 
     def release_numbers(self):
         check(lib.fq_engine_release_numbers(self.h))
+
+    def trim_memory(self):
+        """fq_engine_trim_memory: idle cached device blocks back to the driver."""
+        check(lib.fq_engine_trim_memory(self.h))
 
     def execute(self, sql):
         out = C.c_void_p()

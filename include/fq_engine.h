@@ -73,6 +73,13 @@ fq_status fq_engine_set_option(fq_engine *e, int32_t option, int64_t value);
 fq_status fq_engine_materialize_numbers(fq_engine *e, uint64_t total, int32_t rank, int32_t world);
 fq_status fq_engine_release_numbers(fq_engine *e);
 
+/* Hand the engine's idle device memory back to the driver: the stream-ordered
+ * block cache is flushed and the default memory pool trimmed to 0.  The engine
+ * does this by itself before every retry of a failed allocation; a host that
+ * shares the GPU with another allocator (e.g. PyTorch's caching allocator)
+ * calls it before a large allocation of its own.                           */
+fq_status fq_engine_trim_memory(fq_engine *e);
+
 /* Run a SELECT through the whole pipeline on this engine's GPU. */
 fq_status fq_engine_execute(fq_engine *e, const char *sql, fq_result **out);
 

@@ -1,0 +1,74 @@
+"""Device memory held by the engine between queries (stream-ordered block
+cache + the default pool's release threshold) is reclaimed before any
+allocation fails: a materialisation sized above the HBM the driver reports
+free -- but below free + what the engine holds -- succeeds right after a
+streamed row-pipeline query, and fq_engine_trim_memory hands the held memory
+back on demand."""
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+GB = 1 << 30
+
+
+def _free():
+    import torch
+    torch.cuda.synchronize()
+    return torch.cuda.mem_get_info()[0]
+
+
+@pytest.fixture(scope="module")
+def Engine():
+    from fq_amd import ops
+    ops.require_gpu()
+    from fq_amd.engine import Engine as E
+    return E
+
+
+def _stream(e):
+    # full scans through growing morsels (160,000 rows doubling to 327,680,000
+    # per partition): blocks of many size classes freed on the pipes' queues
+    r = e.execute("SELECT number FROM system.numbers_mt(4000000000) WHERE number % 1000000007 = 3")
+    assert sorted(v for (v,) in r.rows) == [3, 1000000010, 2000000017, 3000000024]
+    r = e.execute("SELECT number + 1 FROM system.numbers_mt(2000000000) WHERE number % 999999937 = 0 LIMIT 2")
+    assert len(r.rows) == 2
+
+
+def test_materialize_after_streamed_query_reclaims_held_memory(Engine):
+    import torch
+    torch.cuda.empty_cache()
+    e = Engine()
+    try:
+        before = _free()
+        _stream(e)
+        after = _free()
+        held = before - after
+        assert held >= 0
+        if held < GB // 2:
+            pytest.skip("engine holds %d MB after the query: nothing to reclaim" % (held >> 20))
+        # rows whose columns need more than the free HBM but fit once the held memory is back
+        want = after + held // 2
+        total = (want // 8) // 80000 * 80000
+        e.materialize_numbers(total)
+        r = e.execute("SELECT count(number), max(number) FROM system.numbers_mt(%d)" % total)
+        assert r.rows == [(total, total - 1)]
+        e.release_numbers()
+    finally:
+        e.close()
+
+
+def test_trim_memory_returns_held_memory(Engine):
+    import torch
+    torch.cuda.empty_cache()
+    e = Engine()
+    try:
+        before = _free()
+        _stream(e)
+        held = before - _free()
+        e.trim_memory()
+        released = _free() - (before - held)
+        # everything the queries kept is back, up to allocator granularity
+        assert released >= held - 64 * (1 << 20), (held, released)
+        _stream(e)  # and the engine still runs afterwards
+    finally:
+        e.close()
