@@ -370,8 +370,8 @@ namespace fqk {
 namespace {
 
 // Workspace of fq_filter_project: [total][flag words: predicate,
-// expressions][ticket counter, 128 B line of its own][one look-back status
-// word per tile].
+// expressions][kMaxSelectXcds ticket counters, a 128 B line each][one
+// look-back status word per tile].
 struct ProjWs {
     uint64_t *total;
     uint32_t *flags, *ticket;
@@ -385,7 +385,7 @@ ProjWs proj_ws(void *d_ws, int64_t n) {
     w.total = (uint64_t *)d_ws;
     w.flags = (uint32_t *)(w.total + 1);
     w.ticket = (uint32_t *)(w.total + 2);
-    w.status = w.total + 2 + 16;
+    w.status = w.total + 2 + 16 * kMaxSelectXcds;
     return w;
 }
 
@@ -432,7 +432,7 @@ extern "C" {
 
 size_t fq_filter_project_workspace_bytes(int64_t len) {
     const fqk::ProjWs w = fqk::proj_ws(nullptr, len < 0 ? 0 : len);
-    return (size_t)(2 + 16 + w.ntiles) * sizeof(uint64_t);
+    return (size_t)(2 + 16 * fqk::kMaxSelectXcds + w.ntiles) * sizeof(uint64_t);
 }
 
 fq_status fq_filter_project(const fq_col *col, const fq_pred *pred, const fq_expr *values, int32_t n_out,

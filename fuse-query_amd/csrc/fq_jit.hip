@@ -29,6 +29,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <mutex>
 #include <string>
 #include <unordered_map>
@@ -43,8 +44,16 @@ namespace {
 
 // ---------------------------------------------------------------------------
 // hipRTC, loaded on first use (libfq_amd.so does not link it, so the library
-// still loads where hipRTC is absent).  If torch already loaded its bundled
-// copy, dlopen by SONAME returns that one.
+// still loads where hipRTC is absent).
+//
+// Which compiler: a process that imported torch already holds torch's
+// bundled libhiprtc + libamd_comgr (an older LLVM), and dlopen by SONAME
+// returns those.  That compiler allocated 288 VGPRs for the select kernel
+// that ROCm 7.2's compiles to 61 (one workgroup per CU instead of 7: the
+// Filter+Projection scan ran 3x slower).  So the system ROCm's hipRTC is
+// loaded into a link-map namespace of its own (dlmopen), where it resolves
+// its own comgr; only the code object bytes cross back.  FQ_JIT_RTC=process
+// takes the process's hipRTC instead (A/B).
 // ---------------------------------------------------------------------------
 struct Rtc {
     decltype(&hiprtcCreateProgram) create = nullptr;
@@ -55,12 +64,21 @@ struct Rtc {
     decltype(&hiprtcGetCode) code = nullptr;
     decltype(&hiprtcDestroyProgram) destroy = nullptr;
     bool ok = false;
+    bool isolated = false;  // the system ROCm's hipRTC in its own link-map namespace
 };
 
 const Rtc &rtc() {
     static const Rtc r = [] {
         Rtc x;
-        void *h = dlopen("libhiprtc.so.7", RTLD_NOW | RTLD_GLOBAL);
+        void *h = nullptr;
+        const char *mode = getenv("FQ_JIT_RTC");
+        if (!mode || strcmp(mode, "process") != 0) {
+            const char *root = getenv("ROCM_PATH");
+            const std::string path = std::string(root && *root ? root : "/opt/rocm") + "/lib/libhiprtc.so.7";
+            h = dlmopen(LM_ID_NEWLM, path.c_str(), RTLD_NOW | RTLD_LOCAL);
+            x.isolated = h != nullptr;
+        }
+        if (!h) h = dlopen("libhiprtc.so.7", RTLD_NOW | RTLD_GLOBAL);
         if (!h) h = dlopen("libhiprtc.so", RTLD_NOW | RTLD_GLOBAL);
         if (!h) return x;
         x.create = (decltype(x.create))dlsym(h, "hiprtcCreateProgram");
@@ -1134,9 +1152,51 @@ void pack_proj_consts(const ProjLaunch &P, HostProjConsts &hc) {
     pack_tree_consts(P.pred, hc);
 }
 
+// FQ_SELECT_VARIANT (tuning, tools/select_sweep.sh): bit 0 per-XCD ticket
+// counters (default on).
+int select_variant() {
+    static const int v = [] {
+        const char *e = getenv("FQ_SELECT_VARIANT");
+        const int x = e ? atoi(e) : 1;
+        return (x >= 0 && x <= 1) ? x : 1;
+    }();
+    return v;
+}
+// FQ_SELECT_DEBUG=1 (tuning only): the select kernel counts tiles, polls and
+// cycles per phase into a module global that is printed after each launch
+int select_debug() {
+    static const int v = [] {
+        const char *e = getenv("FQ_SELECT_DEBUG");
+        return (e && atoi(e) == 1) ? 1 : 0;
+    }();
+    return v;
+}
+// FQ_SELECT_LBW: status words per lane per look-back round trip (1/2/4/8;
+// wider windows measured slower: the polls' extra agent-scope loads cost more
+// than the round trips they save, tools/select_sweep.sh)
+int select_lbw() {
+    static const int v = [] {
+        const char *e = getenv("FQ_SELECT_LBW");
+        const int x = e ? atoi(e) : 1;
+        return (x == 2 || x == 4 || x == 8) ? x : 1;
+    }();
+    return v;
+}
+// XCDs of the device (MI355X: 32 CUs each; 8 in SPX mode, fewer in the
+// partitioned modes), at most kMaxSelectXcds ticket counters
+int select_xcds(int dev) {
+    int cus = 256;
+    if (dev >= 0 && hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
+        (void)hipGetLastError();
+        cus = 256;
+    }
+    return std::max(1, std::min(kMaxSelectXcds, cus / 32));
+}
+
 std::string proj_shape_key(const ProjLaunch &P, int32_t tin, int dev) {
     std::string k = "PROJ" + std::to_string(select_threads()) + "x" + std::to_string(select_rows_per_thread()) + "s" +
-                    std::to_string(select_sleep());
+                    std::to_string(select_sleep()) + "v" + std::to_string(select_variant()) + "w" + std::to_string(select_lbw()) + "g" + std::to_string(select_debug()) + "n" +
+                    std::to_string(select_xcds(dev));
     auto put = [&k](int32_t v) { k.append(reinterpret_cast<const char *>(&v), sizeof v); };
     put(dev);
     put(tin);
@@ -1160,7 +1220,7 @@ std::string proj_shape_key(const ProjLaunch &P, int32_t tin, int dev) {
     return k;
 }
 
-bool gen_project_source(const ProjLaunch &P, int32_t tin, Gen &g, std::string &src) {
+bool gen_project_source(const ProjLaunch &P, int32_t tin, int dev, Gen &g, std::string &src) {
     const char *TIn = ctype(tin);
     if (!TIn || P.n_out < 1 || P.n_out > FQ_MAX_PROJECT) return false;
     const int32_t pk = P.pred.kind;
@@ -1175,7 +1235,8 @@ bool gen_project_source(const ProjLaunch &P, int32_t tin, Gen &g, std::string &s
            std::to_string(kSteps) + "]; };\n";
     src += "struct Outs { void *p[" + std::to_string(FQ_MAX_PROJECT) + "]; };\n";
     src += "#define PS_ROWS " + std::to_string(select_rows_per_thread()) + "\n#define PS_THREADS " +
-           std::to_string(select_threads()) + "\n#define PS_SLEEP " + std::to_string(select_sleep()) + "\n";
+           std::to_string(select_threads()) + "\n#define PS_SLEEP " + std::to_string(select_sleep()) +
+           "\n#define PS_XCD " + std::to_string(select_variant() & 1) + "\n#define PS_LBW " + std::to_string(select_lbw()) + "\n#define PS_DEBUG " + std::to_string(select_debug()) + "\n#define PS_NXCD " + std::to_string(select_xcds(dev)) + "\n";
     src += "typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));\n";
     src += "__device__ __forceinline__ bool fq_pred(TIn x, const Consts &c, u32 &flags, u32 live) {\n";
     src += expr_pred ? pred_body : "    (void)x; (void)c; (void)flags; (void)live;\n    return true;\n";
@@ -1236,22 +1297,34 @@ fq_jit_pbits(const TIn *__restrict__ col, long long n, Consts c, u64 *__restrict
     if (lane == 0 && flags) atomicOr(fl, flags);
 }
 
-// Single pass over the column (decoupled look-back): a workgroup takes the
-// next tile of 4,096 rows from a ticket counter (tiles are handed out in
-// order, so every tile it waits on belongs to a workgroup that is already
-// running), loads it (lane-consecutive 8-byte rows, 16 per lane in flight),
-// evaluates the predicate, publishes the tile's kept count (flag A), then
-// wave 0 walks back over the predecessors' status words, 64 per round trip,
-// until it meets an inclusive prefix (flag P), publishes its own (P) and
-// every wave writes its kept rows' outputs at base + rank.  (Also publishing
-// the P of the A tiles it walked over measured slower: 3.2 -> 3.9 ms with
-// nothing kept.)  Tickets come from 8 counters, one per XCD (workgroup b
-// draws from counter b % 8 and gets tiles c, c + 8, ...): one counter served
-// ~150K tickets at its ~90 per us ceiling.  The lowest unfinished tile never
-// waits, so every tile is reached.  Status
-// words are 64-bit agent-scope atomics: flag in the top 2 bits, count below.
-// The look-back is bounded: after ~2^20 polls the kernel flags an error
-// (fl[1] bit 31) and moves on, so a wave can never spin forever.
+// Single pass over the column (decoupled look-back).  A workgroup draws a
+// tile of PS_TILE rows (lane-consecutive 8-byte rows, PS_ROWS per lane in
+// flight), evaluates the predicate (one ballot per 64 rows, kept in LDS),
+// publishes the tile's kept count as flag A; wave 0 walks back over the
+// predecessors' status words, 64 * PS_LBW per round trip, until it meets an
+// inclusive prefix (flag P), publishes its own P; then every wave writes its
+// kept rows' outputs at base + rank.  A workgroup only draws a tile when it
+// can start it at once: a reserved tile whose A waits behind another tile's
+// look-back chains look-backs across workgroups (a prefetching variant that
+// drew the next tile before its look-back measured 3-4x slower; one that
+// held two tiles and published the second's A while the first waited
+// measured no faster -- tools/select_sweep.sh, profiles/r02_select_*).
+//
+// Tickets: one device-scope counter serves ~90 atomics per us (round-1
+// measurement), >= 1.7 ms for the 152,588 tiles of a 10 GB column.  With
+// PS_XCD each XCD draws from its own counter (its own 128-B line; the XCD is
+// the hardware register XCC_ID modulo PS_NXCD = CUs / 32): counter x hands
+// out tiles x, x + N, x + 2N, ...  A workgroup whose counter is exhausted
+// draws from the next XCD's, so every tile is drawn whatever the placement
+// of workgroups on XCDs.  Progress: the lowest unfinished tile is either
+// held by a workgroup -- all its predecessors are done, its look-back
+// completes -- or undrawn, and the next workgroup to finish a tile draws it
+// (counters only grow; a workgroup leaves only when every counter is
+// exhausted).
+// Status words are 64-bit agent-scope atomics: flag in the top 2 bits, count
+// below.  The look-back is bounded: after ~2^20 polls the kernel flags an
+// error (fl[1] bit 31) and moves on, so a wave can never spin forever.
+// LDS state is double-buffered by tile parity: two barriers per tile.
 #ifndef PS_ROWS
 #define PS_ROWS 16
 #endif
@@ -1260,6 +1333,32 @@ fq_jit_pbits(const TIn *__restrict__ col, long long n, Consts c, u64 *__restrict
 #endif
 #ifndef PS_SLEEP
 #define PS_SLEEP 2
+#endif
+#ifndef PS_XCD
+#define PS_XCD 1
+#endif
+#ifndef PS_NXCD
+#define PS_NXCD 8
+#endif
+#ifndef PS_LBW
+#define PS_LBW 1
+#endif
+#ifndef PS_DEBUG
+#define PS_DEBUG 0
+#endif
+#if PS_DEBUG
+// [0] tiles [1] failed polls [2] look-back cycles [3] ticket cycles
+// [4] load+predicate cycles [5] store cycles [6] workgroup cycles [7] windows
+// [8] earliest workgroup start [9] latest start [10] earliest end [11] latest end
+// [12] sum of workgroup wall ticks (100 MHz)
+__device__ unsigned long long ps_dbg[13];
+// per workgroup: start, end (wall clock), XCC_ID, tiles
+__device__ unsigned long long ps_wg[8192][4];
+#define PS_T(v) const long long v = clock64()
+#define PS_ADD(i, x) (X.dbg[i] += (unsigned long long)(x))
+#else
+#define PS_T(v)
+#define PS_ADD(i, x)
 #endif
 #define PS_WAVES (PS_THREADS / 64)
 #define PS_TILE (PS_THREADS * PS_ROWS)
@@ -1275,118 +1374,257 @@ __device__ __forceinline__ u64 wave_sum64(u64 v) {
     }
     return v;
 }
+struct PsShared {
+    u64 bal[2][PS_ROWS][PS_WAVES];   // ballots of the tile in each slot
+    u32 off[2][PS_ROWS * PS_WAVES];  // exclusive in-tile offsets, (row group, wave) k-major
+    u64 base[2], agg[2];
+    long long tk;  // ticket drawn (broadcast)
+};
+struct PsCtx {
+#if PS_DEBUG
+    unsigned long long dbg[8];  // thread 0's per-phase sums, flushed once per workgroup
+#endif
+    const TIn *__restrict__ col;
+    long long n, ntiles;
+    const u64 *__restrict__ bm;
+    u64 *__restrict__ status;
+    u32 *__restrict__ ticket;
+    u32 cls;
+};
+// the next tile for this workgroup (thread 0 only); >= ntiles when none is
+// left.  An exhausted class moves on to the other XCDs' counters, so no tile
+// depends on the hardware placing a workgroup on every XCD.
+__device__ __forceinline__ long long ps_ticket(const PsCtx &X) {
+#if PS_XCD
+    for (u32 i = 0; i < (u32)PS_NXCD; ++i) {
+        const u32 cl = (X.cls + i) % (u32)PS_NXCD;
+        const long long t = (long long)atomicAdd(X.ticket + 32 * cl, 1u) * PS_NXCD + cl;
+        if (t < X.ntiles) return t;
+    }
+    return X.ntiles;
+#else
+    return atomicAdd(X.ticket, 1u);
+#endif
+}
+__device__ __forceinline__ void ps_load(const PsCtx &X, long long t, TIn (&x)[PS_ROWS]) {
+    const long long r0 = t * PS_TILE + threadIdx.x;
+    if (t * PS_TILE + PS_TILE <= X.n) {
+#pragma unroll
+        for (int k = 0; k < PS_ROWS; ++k) x[k] = __builtin_nontemporal_load(X.col + r0 + k * PS_THREADS);
+    } else {
+#pragma unroll
+        for (int k = 0; k < PS_ROWS; ++k) {
+            const long long row = r0 + k * PS_THREADS;
+            x[k] = row < X.n ? __builtin_nontemporal_load(X.col + row) : TIn(0);
+        }
+    }
+}
+// tile t's predicate into slot S: ballots, in-tile offsets, aggregate; wave 0
+// publishes A (tile 0: P, base 0).  Contains one barrier.
+template <int S>
+__device__ __forceinline__ void ps_pred(const PsCtx &X, const Consts &c, PsShared &sh, long long t, const TIn (&x)[PS_ROWS],
+                                        u32 &pflags) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const long long r0 = t * PS_TILE;
+#pragma unroll
+    for (int k = 0; k < PS_ROWS; ++k) {
+        const long long row = r0 + k * PS_THREADS + tid;
+        const u32 live = row < X.n ? 1u : 0u;
+)" + std::string(P.pred.kind == FQ_PRED_BITMAP
+                     ? "        const bool p = live && ((X.bm[row >> 6] >> (row & 63)) & 1ull);\n        (void)c;\n        (void)x;\n        (void)pflags;\n"
+                     : "        const bool p = fq_pred(x[k], c, pflags, live) && live;\n") + R"(
+        const u64 b = __ballot(p);
+        if (lane == 0) {
+            sh.bal[S][k][wave] = b;
+            sh.off[S][k * PS_WAVES + wave] = (u32)__popcll(b);
+        }
+    }
+    __syncthreads();
+    if (wave == 0) {
+        // exclusive scan of the PS_ROWS * PS_WAVES counts: lane l owns
+        // entries [l * PER, l * PER + PER)
+        constexpr int NE = PS_ROWS * PS_WAVES, PER = (NE + 63) / 64;
+        u32 cv[PER], tot = 0;
+#pragma unroll
+        for (int q = 0; q < PER; ++q) {
+            const int i = lane * PER + q;
+            cv[q] = i < NE ? sh.off[S][i] : 0u;
+            tot += cv[q];
+        }
+        u32 incl = tot;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const u32 v = (u32)__shfl_up((int)incl, off, 64);
+            if (lane >= off) incl += v;
+        }
+        u32 run = incl - tot;
+#pragma unroll
+        for (int q = 0; q < PER; ++q) {
+            const int i = lane * PER + q;
+            if (i < NE) sh.off[S][i] = run;
+            run += cv[q];
+        }
+        const u64 agg = (u64)__shfl((int)incl, 63, 64);
+        if (lane == 0) {
+            sh.agg[S] = agg;
+            __hip_atomic_store(X.status + t, (t == 0 ? PS_P : PS_A) | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+// wave 0: advance the look-back of tile t as far as the published words
+// allow; true once the exclusive prefix is in excl (or the poll bound hit).
+// Each lane reads PS_LBW consecutive status words per round trip (lane 0 the
+// nearest), so one round trip covers 64 * PS_LBW predecessors: with ~1,000
+// tiles in flight a look-back walks back over hundreds of A-only tiles
+// before it meets a P.
+__device__ __forceinline__ bool ps_poll(const PsCtx &X, long long &j, u64 &excl, unsigned &polls, u32 &vflags) {
+    const int lane = threadIdx.x & 63;
+    for (;;) {
+        u64 sw[PS_LBW];
+#pragma unroll
+        for (int q = 0; q < PS_LBW; ++q) {
+            const long long idx = j - (long long)lane * PS_LBW - q;
+            sw[q] = idx >= 0 ? __hip_atomic_load(X.status + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : PS_P;
+        }
+        // this lane's words in order of distance: sum up to (and with) its
+        // first P; not-ready words before it
+        u64 lsum = 0;
+        bool lp = false, lnr = false;
+#pragma unroll
+        for (int q = 0; q < PS_LBW; ++q) {
+            if (!lp) {
+                lnr |= (sw[q] >> 62) == 0ull;
+                lsum += PS_VAL(sw[q]);
+                lp = (sw[q] >> 62) == 2ull;
+            }
+        }
+        const u64 isp = __ballot(lp);
+        const u64 notready = __ballot(lnr);
+        const int pl = isp ? __ffsll((long long)isp) - 1 : 63;  // nearest lane with a P (or the whole window)
+        const u64 upto = pl == 63 ? ~0ull : ((2ull << pl) - 1ull);
+        if (notready & upto) {  // a predecessor in range has not published yet
+            if (++polls > (1u << 20)) {
+                vflags |= 0x80000000u;
+                return true;
+            }
+            return false;
+        }
+        excl += wave_sum64(((upto >> lane) & 1ull) ? lsum : 0ull);
+        if (isp) return true;
+        j -= 64 * PS_LBW;
+    }
+}
+// one tile: draw, load, predicate, look back, store; false when none is left
+template <int S>
+__device__ __forceinline__ bool ps_single(PsCtx &X, const Consts &c, const Outs &o, u64 *__restrict__ total,
+                                          PsShared &sh, TIn (&x)[PS_ROWS], u32 &pflags, u32 &vflags) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    PS_T(c0);
+    if (tid == 0) sh.tk = ps_ticket(X);
+    __syncthreads();
+    PS_T(c1);
+    const long long t = sh.tk;
+    if (t >= X.ntiles) return false;
+    ps_load(X, t, x);
+    ps_pred<S>(X, c, sh, t, x, pflags);
+    PS_T(c2);
+    if (wave == 0) {
+        u64 excl = 0;
+        if (t != 0) {
+            long long j = t - 1;
+            unsigned polls = 0;
+            while (!ps_poll(X, j, excl, polls, vflags)) {
+#if PS_SLEEP > 0
+                __builtin_amdgcn_s_sleep(PS_SLEEP);
+#endif
+            }
+#if PS_DEBUG
+            if (lane == 0) {
+                PS_ADD(1, polls);
+                PS_ADD(7, (u64)((t - 1 - j) / 64 + 1));
+            }
+#endif
+        }
+        if (lane == 0) {
+            sh.base[S] = excl;
+            if (t != 0) __hip_atomic_store(X.status + t, PS_P | (excl + sh.agg[S]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    __syncthreads();
+    PS_T(c3);
+    const u64 base = sh.base[S];
+    const u64 lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+#pragma unroll
+    for (int k = 0; k < PS_ROWS; ++k) {
+        const u64 b = sh.bal[S][k][wave];
+        if ((b >> lane) & 1ull)
+            fq_put(x[k], c, vflags, 1u, o, (long long)(base + sh.off[S][k * PS_WAVES + wave] + (u32)__popcll(b & lt)));
+    }
+    if (t == X.ntiles - 1 && tid == 0) *total = base + sh.agg[S];
+#if PS_DEBUG
+    PS_T(c4);
+    if (tid == 0) {
+        PS_ADD(0, 1);
+        PS_ADD(3, c1 - c0);
+        PS_ADD(4, c2 - c1);
+        PS_ADD(2, c3 - c2);
+        PS_ADD(5, c4 - c3);
+    }
+#endif
+    return true;
+}
 extern "C" __global__ void __launch_bounds__(PS_THREADS)
 fq_jit_pselect(const TIn *__restrict__ col, long long n, Consts c, const u64 *__restrict__ bm, Outs o,
                u64 *__restrict__ status, u32 *__restrict__ ticket, u32 *__restrict__ fl, u64 *__restrict__ total) {
-    __shared__ u32 s_next;
-    __shared__ u32 s_off[PS_ROWS * PS_WAVES];
-    __shared__ u64 s_base, s_agg;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const u64 lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-    const long long ntiles = (n + PS_TILE - 1) / PS_TILE;
-    u32 pflags = 0, vflags = 0;
-    for (;;) {
-        // a ticket only when this workgroup can start the tile at once: a
-        // reserved tile that waits behind another one would stall every
-        // look-back that reaches it
-        if (tid == 0) s_next = atomicAdd(ticket, 1u);
-        __syncthreads();
-        const long long t = s_next;
-        if (t >= ntiles) break;
-        const long long r0 = t * PS_TILE;
-        TIn x[PS_ROWS];
-#pragma unroll
-        for (int k = 0; k < PS_ROWS; ++k) {
-            const long long row = r0 + k * PS_THREADS + tid;
-            x[k] = row < n ? __builtin_nontemporal_load(col + row) : TIn(0);
-        }
-        u32 pass = 0, rank[PS_ROWS];
-#pragma unroll
-        for (int k = 0; k < PS_ROWS; ++k) {
-            const long long row = r0 + k * PS_THREADS + tid;
-            const u32 live = row < n ? 1u : 0u;
-)" + std::string(P.pred.kind == FQ_PRED_BITMAP
-                     ? "            const bool p = live && ((bm[row >> 6] >> (row & 63)) & 1ull);\n            (void)c;\n"
-                     : "            const bool p = fq_pred(x[k], c, pflags, live) && live;\n") + R"(
-            const u64 b = __ballot(p);
-            pass |= (p ? 1u : 0u) << k;
-            rank[k] = (u32)__popcll(b & lt);
-            if (lane == 0) s_off[k * PS_WAVES + wave] = (u32)__popcll(b);
-        }
-        __syncthreads();
-        if (wave == 0) {
-            // exclusive scan of the PS_ROWS * PS_WAVES (row group, wave) counts in
-            // k-major order: lane l owns entries [l * PER, l * PER + PER)
-            constexpr int NE = PS_ROWS * PS_WAVES, PER = (NE + 63) / 64;
-            u32 cv[PER], tot = 0;
-#pragma unroll
-            for (int q = 0; q < PER; ++q) {
-                const int i = lane * PER + q;
-                cv[q] = i < NE ? s_off[i] : 0u;
-                tot += cv[q];
-            }
-            u32 incl = tot;
-#pragma unroll
-            for (int off = 1; off < 64; off <<= 1) {
-                const u32 v = (u32)__shfl_up((int)incl, off, 64);
-                if (lane >= off) incl += v;
-            }
-            u32 run = incl - tot;
-#pragma unroll
-            for (int q = 0; q < PER; ++q) {
-                const int i = lane * PER + q;
-                if (i < NE) s_off[i] = run;
-                run += cv[q];
-            }
-            const u64 agg = (u64)__shfl((int)incl, 63, 64);
-            u64 excl = 0;
-            if (t == 0) {
-                if (lane == 0) __hip_atomic_store(status + t, PS_P | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            } else {
-                if (lane == 0) __hip_atomic_store(status + t, PS_A | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                long long j = t - 1;  // nearest predecessor of this window
-                unsigned polls = 0;
-                for (;;) {
-                    const long long idx = j - lane;
-                    const u64 sw = idx >= 0 ? __hip_atomic_load(status + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                            : PS_P;
-                    const u64 notready = __ballot((sw >> 62) == 0ull);
-                    const u64 isp = __ballot((sw >> 62) == 2ull);
-                    const int pl = isp ? __ffsll((long long)isp) - 1 : 63;  // nearest P (or the whole window)
-                    const u64 upto = pl == 63 ? ~0ull : ((2ull << pl) - 1ull);
-                    if (notready & upto) {  // a predecessor in range has not published yet
-                        if (++polls > (1u << 20)) {
-                            vflags |= 0x80000000u;
-                            break;
-                        }
-#if PS_SLEEP > 0
-                        __builtin_amdgcn_s_sleep(PS_SLEEP);
+    __shared__ PsShared sh;
+    PsCtx X;
+    X.col = col;
+    X.n = n;
+    X.ntiles = (n + PS_TILE - 1) / PS_TILE;
+    X.bm = bm;
+    X.status = status;
+    X.ticket = ticket;
+    X.cls = 0;
+#if PS_DEBUG
+    for (int i = 0; i < 8; ++i) X.dbg[i] = 0;
 #endif
-                        continue;
-                    }
-                    excl += wave_sum64(((upto >> lane) & 1ull) ? PS_VAL(sw) : 0ull);
-                    if (isp) break;
-                    j -= 64;
-                }
-                if (lane == 0) __hip_atomic_store(status + t, PS_P | (excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            if (lane == 0) {
-                s_base = excl;
-                s_agg = agg;
-            }
+#if PS_XCD
+    // s_getreg_b32 hwreg(HW_REG_XCC_ID = 20, offset 0, 4 bits)
+    X.cls = ((u32)__builtin_amdgcn_s_getreg((3 << 11) | 20) & 15u) % (u32)PS_NXCD;
+#endif
+    u32 pflags = 0, vflags = 0;
+    PS_T(k0);
+#if PS_DEBUG
+    const unsigned long long w0 = wall_clock64();
+#endif
+    {
+        TIn x[PS_ROWS];
+        while (ps_single<0>(X, c, o, total, sh, x, pflags, vflags) && ps_single<1>(X, c, o, total, sh, x, pflags, vflags)) {
         }
-        __syncthreads();
-        const u64 base = s_base;
-#pragma unroll
-        for (int k = 0; k < PS_ROWS; ++k)
-            if ((pass >> k) & 1u) fq_put(x[k], c, vflags, 1u, o, (long long)(base + s_off[k * PS_WAVES + wave] + rank[k]));
-        if (t == ntiles - 1 && tid == 0) *total = base + s_agg;
-        __syncthreads();  // s_off / s_base / s_next reused by the next tile
     }
+#if PS_DEBUG
+    PS_T(k1);
+    const unsigned long long w1 = wall_clock64();
+    if (threadIdx.x == 0) {
+        PS_ADD(6, k1 - k0);
+        for (int i = 0; i < 8; ++i) atomicAdd(&ps_dbg[i], X.dbg[i]);
+        atomicAdd(&ps_dbg[12], w1 - w0);
+        if (blockIdx.x < 8192) {
+            ps_wg[blockIdx.x][0] = w0;
+            ps_wg[blockIdx.x][1] = w1;
+            ps_wg[blockIdx.x][2] = (u32)__builtin_amdgcn_s_getreg((3 << 11) | 20);
+            ps_wg[blockIdx.x][3] = X.dbg[0];
+        }
+        atomicMin(&ps_dbg[8], w0);
+        atomicMax(&ps_dbg[9], w0);
+        atomicMin(&ps_dbg[10], w1);
+        atomicMax(&ps_dbg[11], w1);
+    }
+#endif
     pflags = wave_or(pflags);
     vflags = wave_or(vflags);
-    if (lane == 0 && pflags) atomicOr(fl, pflags);
-    if (lane == 0 && vflags) atomicOr(fl + 1, vflags);
+    if ((threadIdx.x & 63) == 0 && pflags) atomicOr(fl, pflags);
+    if ((threadIdx.x & 63) == 0 && vflags) atomicOr(fl + 1, vflags);
 }
 
 // every row: 16-byte loads and stores of row pairs when the column and every
@@ -1476,6 +1714,10 @@ fq_status compile(const std::string &src, int dev, Compiled &out, const char *fn
         const std::string p = std::string(d) + "/fq_jit_" + std::to_string(g_compiled.load()) + ".hip";
         if (FILE *f = fopen(p.c_str(), "w")) {
             fwrite(src.data(), 1, src.size(), f);
+            fclose(f);
+        }
+        if (FILE *f = fopen((p + ".co").c_str(), "wb")) {  // the code object hipRTC produced
+            fwrite(code.data(), 1, code.size(), f);
             fclose(f);
         }
     }
@@ -1629,6 +1871,7 @@ namespace {
 
 struct ProjKernels {
     hipFunction_t bits = nullptr, scatter = nullptr, map = nullptr;
+    hipModule_t mod = nullptr;
 };
 std::unordered_map<std::string, ProjKernels> g_proj_cache;
 
@@ -1647,7 +1890,7 @@ fq_status get_proj_kernels(int32_t col_dtype, const ProjLaunch &P, ProjKernels *
         Gen g;
         std::string src;
         Compiled c;
-        if (!gen_project_source(P, col_dtype, g, src))
+        if (!gen_project_source(P, col_dtype, dev, g, src))
             return fqc::fail(FQ_E_UNSUPPORTED, "fused projection: column/expression types outside the device path");
         fq_status s = compile(src, dev, c, "fq_jit_pselect");
         if (s != FQ_OK) return s;
@@ -1657,6 +1900,7 @@ fq_status get_proj_kernels(int32_t col_dtype, const ProjLaunch &P, ProjKernels *
             return FQ_OK;
         }
         k.scatter = c.fn;
+        k.mod = c.mod;
         FQ_HIP_TRY(hipModuleGetFunction(&k.bits, c.mod, "fq_jit_pbits"));
         FQ_HIP_TRY(hipModuleGetFunction(&k.map, c.mod, "fq_jit_pmap"));
         it = g_proj_cache.emplace(key, k).first;
@@ -1726,6 +1970,45 @@ fq_status jit_project_select(int32_t col_dtype, const ProjLaunch &P, const uint6
     FQ_HIP_TRY(hipModuleLaunchKernel(k.scatter, (unsigned)grid, 1, 1, (unsigned)select_threads(), 1, 1, 0, P.stream,
                                      args, nullptr));
     g_jit_launches += 1;
+    if (select_debug() && k.mod) {  // tuning only: print and clear the kernel's phase counters
+        hipDeviceptr_t d = nullptr;
+        size_t bytes = 0;
+        unsigned long long h[13] = {0};
+        if (hipModuleGetGlobal(&d, &bytes, k.mod, "ps_dbg") == hipSuccess && bytes == sizeof h) {
+            (void)hipStreamSynchronize(P.stream);
+            (void)hipMemcpyDtoH(h, d, sizeof h);
+            fprintf(stderr, "[select-debug] grid %lld tiles %llu polls/tile %.2f windows/tile %.2f | per tile (cycles): ticket %.0f load+pred %.0f lookback %.0f store %.0f | wg cycles %.0f\n",
+                    (long long)grid, h[0], (double)h[1] / h[0], (double)h[7] / h[0], (double)h[3] / h[0], (double)h[4] / h[0],
+                    (double)h[2] / h[0], (double)h[5] / h[0], (double)h[6] / grid);
+            fprintf(stderr, "[select-debug] workgroup starts spread %.1f us, ends spread %.1f us, first start -> last end %.1f us (100 MHz wall clock)\n",
+                    (double)(h[9] - h[8]) / 100.0, (double)(h[11] - h[10]) / 100.0, (double)(h[11] - h[8]) / 100.0);
+            int occ = -1;
+            (void)hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k.scatter, select_threads(), 0);
+            int nregs = -1, lds = -1, scratch = -1;
+            (void)hipFuncGetAttribute(&nregs, HIP_FUNC_ATTRIBUTE_NUM_REGS, k.scatter);
+            (void)hipFuncGetAttribute(&lds, HIP_FUNC_ATTRIBUTE_SHARED_SIZE_BYTES, k.scatter);
+            (void)hipFuncGetAttribute(&scratch, HIP_FUNC_ATTRIBUTE_LOCAL_SIZE_BYTES, k.scatter);
+            fprintf(stderr, "[select-debug] occupancy %d workgroups/CU (regs %d, lds %d, scratch %d)\n", occ, nregs, lds, scratch);
+            fprintf(stderr, "[select-debug] mean workgroup life %.1f us, s_memtime rate %.0f MHz\n",
+                    (double)h[12] / grid / 100.0, (double)h[6] / (double)h[12] * 100.0);
+            if (const char *path = getenv("FQ_SELECT_DEBUG_WG")) {
+                std::vector<unsigned long long> w((size_t)grid * 4);
+                hipDeviceptr_t dw = nullptr;
+                size_t wb = 0;
+                if (hipModuleGetGlobal(&dw, &wb, k.mod, "ps_wg") == hipSuccess &&
+                    hipMemcpyDtoH(w.data(), dw, w.size() * 8) == hipSuccess)
+                    if (FILE *f = fopen(path, "w")) {
+                        for (long long b = 0; b < grid; ++b)
+                            fprintf(f, "%lld %llu %llu %llu %llu\n", b, w[b * 4], w[b * 4 + 1], w[b * 4 + 2], w[b * 4 + 3]);
+                        fclose(f);
+                    }
+            }
+            unsigned long long z[13] = {0};
+            z[8] = z[10] = ~0ull;
+            (void)hipMemcpyHtoD(d, z, sizeof z);
+        }
+        (void)hipGetLastError();
+    }
     return FQ_OK;
 }
 

@@ -118,7 +118,7 @@ fq_status jit_project_bits(int32_t col_dtype, const ProjLaunch &P, uint64_t *d_b
 // d_flags[0] predicate errors, d_flags[1] expression errors (bit 31: the
 // look-back gave up); *d_total = rows kept.
 // tile = select_threads() x select_rows_per_thread() rows (FQ_SELECT_THREADS
-// 256/512/1024, FQ_SELECT_ROWS 8/16/32: tuning; tools/select_probe.py)
+// 256/512/1024, FQ_SELECT_ROWS 8/16/32: tuning; tools/select_sweep.sh)
 inline int select_threads() {
     static const int v = [] {
         const char *e = getenv("FQ_SELECT_THREADS");
@@ -136,15 +136,17 @@ inline int select_rows_per_thread() {
     return v;
 }
 // s_sleep between look-back polls of a predecessor that has not published
-// (FQ_SELECT_SLEEP 0..8, tuning; default 2)
+// (FQ_SELECT_SLEEP 0..127, tuning; default 2)
 inline int select_sleep() {
     static const int v = [] {
         const char *e = getenv("FQ_SELECT_SLEEP");
         const int x = e ? atoi(e) : 2;
-        return (x >= 0 && x <= 8) ? x : 2;
+        return (x >= 0 && x <= 127) ? x : 2;
     }();
     return v;
 }
+// ticket counters of fq_jit_pselect (one per XCD, each on its own 128-B line)
+constexpr int kMaxSelectXcds = 16;
 inline int64_t select_tile_rows() { return (int64_t)select_threads() * select_rows_per_thread(); }
 fq_status jit_project_select(int32_t col_dtype, const ProjLaunch &P, const uint64_t *d_bitmap, uint64_t *status,
                              uint32_t *ticket, uint32_t *d_flags, uint64_t *d_total);
