@@ -49,6 +49,22 @@ fq_status guard(F &&f) {
     }
 }
 
+// A GROUP BY table ran out of slots: the next attempt gets 16x the slots of
+// the table that filled (plan_group_by's sample-based size is the floor).
+bool grow_group_table(fq_engine *e, const fq::FQException &ex, int attempt) {
+    if (ex.status != FQ_E_TABLE_FULL || attempt >= 4) return false;
+    const int64_t used = std::max(e->rt->group_capacity.load(), e->rt->group_used_capacity.load());
+    if (used >= ((int64_t)1 << 30)) return false;
+    e->rt->group_capacity.store(used * 16);
+    return true;
+}
+
+// the grown floor lasts for one statement's re-runs only
+struct GroupCapacityReset {
+    fq_engine *e;
+    ~GroupCapacityReset() { e->rt->group_capacity.store(4096); }
+};
+
 fq::QueryContextRef make_ctx(fq_engine *e, int rank, int world) {
     auto c = std::make_shared<fq::QueryContext>();
     c->worker_threads = e->worker_threads;
@@ -200,6 +216,7 @@ fq_status fq_engine_execute(fq_engine *e, const char *sql, fq_result **out) {
             r->cols[0].push_back(fq::DataValue::string(p.display()));
             r->rows = 2;
         } else {
+            GroupCapacityReset reset{e};
             for (int attempt = 0;; ++attempt) {
                 fq::Pipeline p = fq::build_pipeline(plan, qctx);
                 const int64_t t1 = fq::now_ns();
@@ -210,9 +227,7 @@ fq_status fq_engine_execute(fq_engine *e, const char *sql, fq_result **out) {
                     while (s->next(b)) append_block(r.get(), b, ctx);
                 } catch (const fq::FQException &ex) {
                     // a GROUP BY table ran out of slots: re-run with 16x the slots
-                    const int64_t cap = e->rt->group_capacity.load();
-                    if (ex.status != FQ_E_TABLE_FULL || attempt >= 4 || cap >= ((int64_t)1 << 30)) throw;
-                    e->rt->group_capacity.store(cap * 16);
+                    if (!grow_group_table(e, ex, attempt)) throw;
                     r = std::make_unique<fq_result>();
                     continue;
                 }
@@ -261,6 +276,7 @@ fq_status fq_engine_execute_partial(fq_engine *e, const char *sql, int32_t rank,
         fq::QueryPlan partial = plan;
         while (!partial.nodes.empty() && partial.nodes.back().kind == fq::PlanNode::kLimit) partial.nodes.pop_back();
         std::vector<std::vector<fq::DataValue>> per_func;
+        GroupCapacityReset reset{e};
         for (int attempt = 0;; ++attempt) {
             per_func.clear();
             try {
@@ -272,9 +288,7 @@ fq_status fq_engine_execute_partial(fq_engine *e, const char *sql, int32_t rank,
                     for (const auto &v : rows) per_func.push_back(v.fields);
                 }
             } catch (const fq::FQException &ex) {  // GROUP BY table full: 16x the slots
-                const int64_t cap = e->rt->group_capacity.load();
-                if (ex.status != FQ_E_TABLE_FULL || attempt >= 4 || cap >= ((int64_t)1 << 30)) throw;
-                e->rt->group_capacity.store(cap * 16);
+                if (!grow_group_table(e, ex, attempt)) throw;
                 continue;
             }
             break;

@@ -190,6 +190,8 @@ class Runtime {
     // GROUP BY table slots for the next query (grows x16 when a query fills
     // its table; the query is then re-run)
     std::atomic<int64_t> group_capacity{4096};
+    // slots of the last GROUP BY table sized (a TABLE_FULL re-run grows from it)
+    std::atomic<int64_t> group_used_capacity{0};
     ThreadPool pool;
 
    private:

@@ -480,6 +480,59 @@ DataValue fold_leaf(uint32_t op, const DataValue &a, const DataValue &b) {
 
 }  // namespace
 
+// GROUP BY sizing from a sample of the first block: the distinct keys among
+// its first kGroupSampleRows passing rows (a count-only table).  A sample
+// whose keys repeat (distinct <= half the rows) has seen about all the groups
+// of a block; one that is still mostly distinct grows with the rows.  Beyond
+// 3,072 groups per launch (3/4 of an LDS table) the launches go through the
+// radix-partitioned kernels with about 2,048 groups per bin; the table gets
+// twice the expected groups in slots (a TABLE_FULL re-run grows it 16x).
+namespace {
+constexpr int64_t kGroupSampleRows = 1 << 21;
+
+struct GroupPlan {
+    int64_t capacity = 4096;
+    int log2_parts = 0;
+};
+
+int64_t next_pow2(int64_t v) {
+    int64_t p = 64;
+    while (p < v && p < ((int64_t)1 << 30)) p <<= 1;
+    return p;
+}
+
+GroupPlan plan_group_by(const fq_group_table &d, const fq_col &c, const fq_pred *pred, const fq_expr *key,
+                        ExecCtx &ctx) {
+    const int64_t rows = std::min<int64_t>(c.len, kGroupSampleRows);
+    fq_group_table t{};
+    t.capacity = next_pow2(2 * rows);
+    t.key_dtype = d.key_dtype;
+    t.n_aggs = 1;
+    t.kinds[0] = FQ_AGG_COUNT;
+    t.dtypes[0] = FQ_DT_UINT64;
+    auto mem = DeviceBuffer::alloc(fq_group_table_bytes(t.capacity, 1), ctx.stream());
+    t.d_mem = mem->ptr;
+    fq_col sample = c;
+    sample.len = rows;
+    {
+        std::lock_guard<std::mutex> lk(*ctx.res->launch_mu);
+        check_fq(fq_group_table_init(&t, ctx.stream()));
+        check_fq(fq_group_aggregate(&t, &sample, pred, key, nullptr, ctx.stream()));
+    }
+    int64_t g = 0;
+    check_fq(fq_group_table_count(&t, &g, ctx.stream()));  // synchronises
+    const int64_t per_launch =
+        2 * g <= rows ? 2 * g : (int64_t)((double)g * (double)c.len / (double)std::max<int64_t>(rows, 1));
+    GroupPlan p;
+    p.capacity = next_pow2(std::max<int64_t>(4096, 2 * per_launch));
+    if (per_launch > 3072) {
+        p.log2_parts = 1;
+        while (p.log2_parts < 8 && (per_launch >> p.log2_parts) > 2048) ++p.log2_parts;
+    }
+    return p;
+}
+}  // namespace
+
 StreamRef GroupByPartialTransform::execute() {
     ExecCtx &ctx = ExecCtx::current();
     std::vector<FunctionRef> funcs;
@@ -531,7 +584,6 @@ StreamRef GroupByPartialTransform::execute() {
             if (!shared_->ready) {
                 fq_group_table &d = shared_->desc;
                 d = fq_group_table{};
-                d.capacity = ctx.rt->group_capacity.load();
                 d.key_dtype = kc.out_dtype;
                 d.n_aggs = (int32_t)leaves.size();
                 shared_->leaf_ops.clear();
@@ -546,6 +598,11 @@ StreamRef GroupByPartialTransform::execute() {
                     d.dtypes[0] = FQ_DT_UINT64;
                     shared_->dummy_count = true;
                 }
+                const GroupPlan gp = plan_group_by(d, c, has_pred ? fp.get() : nullptr,
+                                                   kc.expr.n_steps ? &kc.expr : nullptr, ctx);
+                d.capacity = std::max<int64_t>(ctx.rt->group_capacity.load(), gp.capacity);
+                ctx.rt->group_used_capacity.store(d.capacity);
+                shared_->log2_parts = gp.log2_parts;
                 shared_->mem = DeviceBuffer::alloc(fq_group_table_bytes(d.capacity, d.n_aggs), ctx.stream());
                 d.d_mem = shared_->mem->ptr;
                 {
@@ -570,11 +627,25 @@ StreamRef GroupByPartialTransform::execute() {
             check_fq(fq_group_aggregate(&probe, &empty, has_pred ? fp.get() : nullptr,
                                         kc.expr.n_steps ? &kc.expr : nullptr, vals, ctx.stream()));
         }
+        const int lp = shared_->log2_parts;
+        std::shared_ptr<DeviceBuffer> ws;
+        if (lp > 0) {
+            const size_t need = fq_group_partition_workspace_bytes(c.len, lp);
+            std::lock_guard<std::mutex> lk(shared_->mu);
+            auto &slot = shared_->part_ws[ctx.stream()];
+            if (!slot || slot->bytes < need) slot = DeviceBuffer::alloc(need, ctx.stream());
+            ws = slot;
+        }
         {
             std::lock_guard<std::mutex> lk(*ctx.res->launch_mu);
             if (prof) check_hip(hipEventRecord(e0, ctx.stream()), "hipEventRecord");
-            check_fq(fq_group_aggregate(&shared_->desc, &c, has_pred ? fp.get() : nullptr,
-                                        kc.expr.n_steps ? &kc.expr : nullptr, vals, ctx.stream()));
+            if (lp > 0)
+                check_fq(fq_group_aggregate_partitioned(&shared_->desc, &c, has_pred ? fp.get() : nullptr,
+                                                        kc.expr.n_steps ? &kc.expr : nullptr, vals, lp, ws->ptr,
+                                                        ws->bytes, ctx.stream()));
+            else
+                check_fq(fq_group_aggregate(&shared_->desc, &c, has_pred ? fp.get() : nullptr,
+                                            kc.expr.n_steps ? &kc.expr : nullptr, vals, ctx.stream()));
             if (prof) check_hip(hipEventRecord(e1, ctx.stream()), "hipEventRecord");
         }
         if (prof) timed.push_back({e0, e1});

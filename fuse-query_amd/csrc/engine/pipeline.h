@@ -262,6 +262,11 @@ struct GroupByShared {
     std::shared_ptr<DeviceBuffer> mem;
     std::vector<uint32_t> leaf_ops;  // per table aggregate
     bool dummy_count = false;        // no aggregate: a Count keeps the table valid
+    int log2_parts = 0;              // > 0: radix-partitioned launches (high cardinality)
+    // their workspace (~8 B per row), one per device queue: the pipes that
+    // share a queue run its launches in order, so they share the memory
+    // instead of mapping a fresh block per pipe
+    std::map<hipStream_t, std::shared_ptr<DeviceBuffer>> part_ws;
 };
 
 class GroupByPartialTransform : public IProcessor {

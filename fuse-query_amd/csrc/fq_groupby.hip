@@ -185,39 +185,61 @@ static fq_status read_header(const TableView &v, uint32_t &flags, uint64_t &coun
     return FQ_OK;
 }
 
-}  // namespace fqk
-
-extern "C" {
-
-size_t fq_group_table_bytes(int64_t capacity, int32_t n_aggs) {
-    if (capacity < 0 || n_aggs < 0) return 0;
-    return fqk::kHdrBytes + (size_t)(capacity + 1) * 8u * (size_t)(1 + n_aggs * fqk::group_replicas(capacity));
+// Exclusive scan of the (bin, workgroup) row counts of fq_jit_ghist, bin
+// major, into their offsets in the partitioned buffer, and the bin starts.
+// One workgroup: P * grid <= 256 * 1024 entries.
+__global__ void __launch_bounds__(1024)
+    group_part_scan_kernel(const uint32_t *__restrict__ hist, uint64_t *__restrict__ off, uint64_t *__restrict__ bins,
+                           int P, int grid) {
+    __shared__ uint64_t sh[1024];
+    const int64_t N = (int64_t)P * grid;
+    const int64_t per = (N + 1023) / 1024;
+    const int64_t b = (int64_t)threadIdx.x * per, e = b + per < N ? b + per : N;
+    uint64_t s = 0;
+    for (int64_t i = b; i < e; ++i) s += hist[i];
+    sh[threadIdx.x] = s;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+        const uint64_t v = (int)threadIdx.x >= o ? sh[threadIdx.x - o] : 0;
+        __syncthreads();
+        sh[threadIdx.x] += v;
+        __syncthreads();
+    }
+    uint64_t run = sh[threadIdx.x] - s;
+    for (int64_t i = b; i < e; ++i) {
+        off[i] = run;
+        run += hist[i];
+    }
+    __syncthreads();
+    for (int p = threadIdx.x; p <= P; p += 1024) bins[p] = p < P ? off[(int64_t)p * grid] : sh[1023];
 }
 
-fq_status fq_group_table_init(const fq_group_table *t, void *stream) {
-    using namespace fqk;
-    TableView v;
-    fq_status s = view(t, v);
-    if (s != FQ_OK) return s;
-    hipStream_t st = (hipStream_t)stream;
-    FQ_HIP_TRY(hipMemsetAsync(v.hdr, 0, kHdrBytes, st));
-    InitArgs a{};
-    a.keys = v.keys;
-    a.n_aggs = t->n_aggs;
-    a.slots = t->capacity + 1;
-    a.replicas = v.replicas;
-    for (int i = 0; i < t->n_aggs; ++i) {
-        a.states[i] = v.states[i];
-        a.ident[i] = identity_bits(t->kinds[i], t->dtypes[i]);
-    }
-    hipLaunchKernelGGL(group_init_kernel, dim3(small_grid(a.slots * a.replicas)), dim3(256), 0, st, a);
+fq_status launch_group_part_scan(const GroupPartition &X, hipStream_t stream) {
+    hipLaunchKernelGGL(group_part_scan_kernel, dim3(1), dim3(1024), 0, stream, X.hist, X.off, X.bins, 1 << X.log2p,
+                       X.grid);
     FQ_HIP_TRY(hipGetLastError());
     return FQ_OK;
 }
 
-fq_status fq_group_aggregate(const fq_group_table *t, const fq_col *col, const fq_pred *pred,
-                             const fq_expr *key_expr, const fq_expr *values, void *stream) {
-    using namespace fqk;
+// Workspace of fq_group_aggregate_partitioned:
+// [hist u32 P x kMaxPartGrid][off u64 P x kMaxPartGrid][bins u64 P + 1][vals u64 len]
+static size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
+static size_t part_ws_bytes(int64_t len, int log2p, GroupPartition *X, void *ws) {
+    const size_t P = (size_t)1 << log2p;
+    const size_t h = align256(P * kMaxPartGrid * 4), o = align256(P * kMaxPartGrid * 8), b = align256((P + 1) * 8);
+    if (X) {
+        char *m = (char *)ws;
+        X->hist = (uint32_t *)m;
+        X->off = (uint64_t *)(m + h);
+        X->bins = (uint64_t *)(m + h + o);
+        X->vals = m + h + o + b;
+    }
+    return h + o + b + align256((size_t)(len > 0 ? len : 0) * 8);
+}
+
+// validation + lowering shared by both aggregate entry points
+static fq_status prepare_group(const fq_group_table *t, const fq_col *col, const fq_pred *pred,
+                               const fq_expr *key_expr, const fq_expr *values, void *stream, GroupLaunch &G) {
     TableView v;
     fq_status s = view(t, v);
     if (s != FQ_OK) return s;
@@ -227,7 +249,7 @@ fq_status fq_group_aggregate(const fq_group_table *t, const fq_col *col, const f
     if (fqc::dtype_size(col->dtype) != 8 || !fqc::dtype_is_numeric(col->dtype))
         return fqc::fail(FQ_E_UNSUPPORTED, "GROUP BY needs a 64-bit column on the device path");
     if ((uintptr_t)col->data & 7u) return fqc::fail(FQ_E_INVALID, "fq_group_aggregate: misaligned column");
-    GroupLaunch G{};
+    G = GroupLaunch{};
     G.col = col->data;
     G.n = col->len;
     s = lower_pred(pred, col->dtype, col->len, true, G.pred);
@@ -263,7 +285,6 @@ fq_status fq_group_aggregate(const fq_group_table *t, const fq_col *col, const f
     const uintptr_t mis = ((uintptr_t)col->data) & 15u;
     G.head = mis ? 1 : 0;
     if (G.head > G.n) G.head = G.n;
-    const int64_t nvec = (G.n - G.head) / 2;
     // one 1,024-thread workgroup per CU with a 128 KB LDS table: 16 waves
     // share one table (tools/groupby_sweep.py: 256-thread workgroups with a
     // 64 KB table each, 2 per CU, ran 1,000 groups x 3 aggregates in 2.98 ms
@@ -271,11 +292,89 @@ fq_status fq_group_aggregate(const fq_group_table *t, const fq_col *col, const f
     G.lds_bytes = 128 * 1024;
     G.threads = 1024;
     G.rowmap = 1;
+    const int64_t nvec = (G.n - G.head) / 2;
     int64_t grid = (nvec + 4 * G.threads - 1) / (4 * G.threads);
     if (grid < 1) grid = 1;
     const int64_t cap = (int64_t)fqc::device_cu_count();
     G.grid = (int)(grid < cap ? grid : cap);
+    return FQ_OK;
+}
+
+}  // namespace fqk
+
+extern "C" {
+
+size_t fq_group_table_bytes(int64_t capacity, int32_t n_aggs) {
+    if (capacity < 0 || n_aggs < 0) return 0;
+    return fqk::kHdrBytes + (size_t)(capacity + 1) * 8u * (size_t)(1 + n_aggs * fqk::group_replicas(capacity));
+}
+
+fq_status fq_group_table_init(const fq_group_table *t, void *stream) {
+    using namespace fqk;
+    TableView v;
+    fq_status s = view(t, v);
+    if (s != FQ_OK) return s;
+    hipStream_t st = (hipStream_t)stream;
+    FQ_HIP_TRY(hipMemsetAsync(v.hdr, 0, kHdrBytes, st));
+    InitArgs a{};
+    a.keys = v.keys;
+    a.n_aggs = t->n_aggs;
+    a.slots = t->capacity + 1;
+    a.replicas = v.replicas;
+    for (int i = 0; i < t->n_aggs; ++i) {
+        a.states[i] = v.states[i];
+        a.ident[i] = identity_bits(t->kinds[i], t->dtypes[i]);
+    }
+    hipLaunchKernelGGL(group_init_kernel, dim3(small_grid(a.slots * a.replicas)), dim3(256), 0, st, a);
+    FQ_HIP_TRY(hipGetLastError());
+    return FQ_OK;
+}
+
+fq_status fq_group_aggregate(const fq_group_table *t, const fq_col *col, const fq_pred *pred,
+                             const fq_expr *key_expr, const fq_expr *values, void *stream) {
+    using namespace fqk;
+    GroupLaunch G;
+    fq_status s = prepare_group(t, col, pred, key_expr, values, stream, G);
+    if (s != FQ_OK) return s;
     return jit_groupby(col->dtype, G);
+}
+
+size_t fq_group_partition_workspace_bytes(int64_t len, int32_t log2_parts) {
+    if (log2_parts < 1 || log2_parts > 8) return 0;
+    return fqk::part_ws_bytes(len, log2_parts, nullptr, nullptr);
+}
+
+fq_status fq_group_aggregate_partitioned(const fq_group_table *t, const fq_col *col, const fq_pred *pred,
+                                         const fq_expr *key_expr, const fq_expr *values, int32_t log2_parts,
+                                         void *d_ws, size_t ws_bytes, void *stream) {
+    using namespace fqk;
+    if (log2_parts < 1 || log2_parts > 8)
+        return fqc::fail(FQ_E_INVALID, "fq_group_aggregate_partitioned: log2_parts must be in [1, 8]");
+    GroupLaunch G;
+    fq_status s = prepare_group(t, col, pred, key_expr, values, stream, G);
+    if (s != FQ_OK) return s;
+    if (G.n > 0 && (!d_ws || ws_bytes < part_ws_bytes(G.n, log2_parts, nullptr, nullptr)))
+        return fqc::fail(FQ_E_INVALID, "fq_group_aggregate_partitioned: workspace too small");
+    if (((uintptr_t)d_ws) & 255u) return fqc::fail(FQ_E_INVALID, "fq_group_aggregate_partitioned: workspace not 256-B aligned");
+    GroupPartition X{};
+    X.log2p = log2_parts;
+    part_ws_bytes(G.n, log2_parts, &X, d_ws);
+    // the histogram and the partition kernel walk the same tiles with the
+    // same workgroups; two 1,024-thread workgroups per CU (fq_jit_gpart's
+    // 76 KB of LDS; FQ_GPART_WG_PER_CU tunes it)
+    static const int wg_per_cu = [] {
+        const char *e = getenv("FQ_GPART_WG_PER_CU");
+        const int x = e ? atoi(e) : 2;
+        return x >= 1 && x <= 4 ? x : 2;
+    }();
+    const int64_t tile = (int64_t)G.threads * 8;
+    const int64_t ntiles = (G.n + tile - 1) / tile;
+    int64_t g = (int64_t)fqc::device_cu_count() * wg_per_cu;
+    if (g > kMaxPartGrid) g = kMaxPartGrid;
+    if (g > ntiles) g = ntiles;
+    X.grid = (int)(g < 1 ? 1 : g);
+    X.bins_grid = fqc::device_cu_count();
+    return jit_groupby_partitioned(col->dtype, G, X);
 }
 
 fq_status fq_group_table_count(const fq_group_table *t, int64_t *groups, void *stream) {

@@ -792,6 +792,205 @@ std::string state_update(int32_t kind, int32_t dt, const std::string &P, const s
     }
 }
 
+// High-cardinality GROUP BY (fq_group_aggregate_partitioned): more groups
+// than an LDS table holds make every row an HBM atomic (100,000 groups x 3
+// aggregates: 149 ms per 10 GB).  Instead the passing rows are radix-
+// partitioned by key hash into P = 2^log2p bins, then aggregated bin by bin,
+// so every workgroup's LDS table only sees the groups of one bin:
+//   fq_jit_ghist   read the column, per-workgroup histogram of bins (LDS);
+//   (scan)         exclusive offsets per (bin, workgroup), fq_groupby.hip;
+//   fq_jit_gpart   read the column again (same tiles, same workgroups), LDS
+//                  counting sort of each 8,192-row tile by bin, each bin's run
+//                  written contiguously at the workgroup's cursor for it;
+//   fq_jit_groupby_bins  the partitioned rows split evenly over the
+//                  workgroups, cut at bin boundaries: LDS table per bin slice,
+//                  flushed to the HBM table (whose home slot is the mixer's top
+//                  bits, so a bin's groups share 1/P of the table).
+// HBM bytes per row: 8 (hist) + 8 + 8 (part) + 8 (bins) = 32 B for a passing
+// row (16 B for a filtered-out one), against 8 B + 3 random atomics.
+const char *kGroupPartitionKernels = R"(
+#define GP_ROWS 8
+#define GP_TILE (BT * GP_ROWS)
+__device__ __forceinline__ u32 gbin(u64 k, int log2p) { return (u32)(mix(k) >> (64 - log2p)); }
+__device__ __forceinline__ u32 wave_or32(u32 f) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) f |= (u32)__shfl_xor((int)f, off, 64);
+    return f;
+}
+
+__device__ __forceinline__ void gp_load(const TIn *__restrict__ col, long long n, long long tt, TIn (&x)[GP_ROWS]) {
+    const long long r0 = tt * GP_TILE + threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < GP_ROWS; ++k) {
+        const long long row = r0 + (long long)k * BT;
+        x[k] = row < n ? __builtin_nontemporal_load(col + row) : TIn(0);
+    }
+}
+
+extern "C" __global__ void __launch_bounds__(BT)
+fq_jit_ghist(const TIn *__restrict__ col, long long n, const u64 *__restrict__ bitmap, Consts c,
+             u32 *__restrict__ hist, int log2p, u32 *__restrict__ hdr) {
+    __shared__ u32 s_h[256];
+    const int P = 1 << log2p;
+    for (int i = threadIdx.x; i < P; i += BT) s_h[i] = 0;
+    __syncthreads();
+    u32 flags = 0;
+    const long long ntiles = (n + GP_TILE - 1) / GP_TILE;
+    for (long long tt = blockIdx.x; tt < ntiles; tt += gridDim.x) {
+        const long long r0 = tt * GP_TILE + threadIdx.x;
+        TIn x[GP_ROWS];
+#pragma unroll
+        for (int k = 0; k < GP_ROWS; ++k) {
+            const long long row = r0 + (long long)k * BT;
+            x[k] = row < n ? __builtin_nontemporal_load(col + row) : TIn(0);
+        }
+#pragma unroll
+        for (int k = 0; k < GP_ROWS; ++k) {
+            const long long row = r0 + (long long)k * BT;
+            if (row >= n) continue;
+            Row r;
+            fq_prep(x[k], row, c, bitmap, flags, r);
+            if (r.pass) atomicAdd(&s_h[gbin(r.k, log2p)], 1u);
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < P; i += BT) hist[(long long)i * gridDim.x + blockIdx.x] = s_h[i];
+    flags = wave_or32(flags);
+    if ((threadIdx.x & 63) == 0 && flags) atomicOr(&hdr[0], flags);
+}
+
+extern "C" __global__ void __launch_bounds__(BT)
+fq_jit_gpart(const TIn *__restrict__ col, long long n, const u64 *__restrict__ bitmap, Consts c,
+             const u64 *__restrict__ off, TIn *__restrict__ out, int log2p) {
+    __shared__ TIn s_stage[GP_TILE];
+    __shared__ unsigned char s_bin[GP_TILE];
+    __shared__ u32 s_cnt[256], s_start[256], s_tot;
+    __shared__ u64 s_cur[256];
+    const int P = 1 << log2p;
+    for (int i = threadIdx.x; i < P; i += BT) s_cur[i] = off[(long long)i * gridDim.x + blockIdx.x];
+    u32 flags = 0;  // errors were reported by fq_jit_ghist over the same rows
+    const long long ntiles = (n + GP_TILE - 1) / GP_TILE;
+    // (a prefetched next tile and one ballot per bin for small P both
+    // measured slower here: the registers halve the occupancy, and LDS
+    // atomics on few counters beat a ballot loop)
+    for (long long tt = blockIdx.x; tt < ntiles; tt += gridDim.x) {
+        for (int i = threadIdx.x; i < P; i += BT) s_cnt[i] = 0;
+        __syncthreads();
+        const long long r0 = tt * GP_TILE + threadIdx.x;
+        TIn x[GP_ROWS];
+        gp_load(col, n, tt, x);
+        u32 bin[GP_ROWS], rank[GP_ROWS], pass = 0;
+#pragma unroll
+        for (int k = 0; k < GP_ROWS; ++k) {
+            const long long row = r0 + (long long)k * BT;
+            bin[k] = 0;
+            rank[k] = 0;
+            if (row >= n) continue;
+            Row r;
+            fq_prep(x[k], row, c, bitmap, flags, r);
+            if (!r.pass) continue;
+            bin[k] = gbin(r.k, log2p);
+            rank[k] = atomicAdd(&s_cnt[bin[k]], 1u);
+            pass |= 1u << k;
+        }
+        __syncthreads();
+        if (threadIdx.x < 64) {  // exclusive scan of the P <= 256 bin counts: 4 per lane
+            const int l = threadIdx.x;
+            u32 v[4], t = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int i = l * 4 + q;
+                v[q] = i < P ? s_cnt[i] : 0u;
+                t += v[q];
+            }
+            u32 incl = t;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const u32 y = (u32)__shfl_up((int)incl, o, 64);
+                if (l >= o) incl += y;
+            }
+            u32 run = incl - t;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int i = l * 4 + q;
+                if (i < P) s_start[i] = run;
+                run += v[q];
+            }
+            if (l == 63) s_tot = incl;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < GP_ROWS; ++k) {
+            if (!((pass >> k) & 1u)) continue;
+            const u32 pos = s_start[bin[k]] + rank[k];
+            s_stage[pos] = x[k];
+            s_bin[pos] = (unsigned char)bin[k];
+        }
+        __syncthreads();
+        const u32 kept = s_tot;
+        for (u32 i = threadIdx.x; i < kept; i += BT) {
+            const u32 b = s_bin[i];
+            __builtin_nontemporal_store(s_stage[i], out + s_cur[b] + (i - s_start[b]));
+        }
+        __syncthreads();
+        for (int i = threadIdx.x; i < P; i += BT) s_cur[i] += s_cnt[i];
+    }
+}
+
+extern "C" __global__ void __launch_bounds__(BT)
+fq_jit_groupby_bins(const TIn *__restrict__ vals, const u64 *__restrict__ bins, int log2p, Consts c, Tab t) {
+    __shared__ u64 s_keys[S];
+    __shared__ u64 s_st[NA][S];
+    __shared__ int s_bypass[2];
+    Tab tr = t;
+    const long long roff = (long long)(blockIdx.x & t.rmask) * (t.mask + 2);
+    for (int a = 0; a < NA; ++a) tr.st[a] += roff;
+    const int P = 1 << log2p;
+    const long long total = (long long)bins[P];
+    // this workgroup's even share of the partitioned rows, cut at bin boundaries
+    const long long per = (total + gridDim.x - 1) / gridDim.x;
+    long long lo = (long long)blockIdx.x * per;
+    const long long hi = lo + per < total ? lo + per : total;
+    int p = 0;
+    while (p < P && (long long)bins[p + 1] <= lo) ++p;
+    u32 flags = 0;
+    while (lo < hi && p < P) {
+        const long long e = (long long)bins[p + 1] < hi ? (long long)bins[p + 1] : hi;
+        if (e > lo) {
+            fq_lds_reset(s_keys, s_st, s_bypass);
+            __syncthreads();
+            // rows [lo, e) as tiles of GP_TILE from lo; the next tile's loads
+            // are in flight while this one goes through the LDS table
+            const TIn *__restrict__ sv = vals + lo;
+            const long long sn = e - lo, nt = (sn + GP_TILE - 1) / GP_TILE;
+            TIn nxt[GP_ROWS];
+            gp_load(sv, sn, 0, nxt);
+            for (long long ti = 0; ti < nt; ++ti) {
+                const long long r0 = lo + ti * GP_TILE + threadIdx.x;
+                TIn x[GP_ROWS];
+#pragma unroll
+                for (int k = 0; k < GP_ROWS; ++k) x[k] = nxt[k];
+                if (ti + 1 < nt) gp_load(sv, sn, ti + 1, nxt);
+                Row r[GP_ROWS];
+#pragma unroll
+                for (int k = 0; k < GP_ROWS; ++k) fq_prep_all(x[k], r0 + (long long)k * BT < e ? 1u : 0u, c, flags, r[k]);
+                u64 cur[GP_ROWS];
+#pragma unroll
+                for (int j = 0; j < GP_ROWS; ++j) cur[j] = fq_first(r[j], s_keys);
+#pragma unroll
+                for (int j = 0; j < GP_ROWS; ++j) fq_commit(r[j], cur[j], tr, s_keys, s_st, s_bypass);
+            }
+            __syncthreads();
+            fq_flush(tr, s_keys, s_st);
+            __syncthreads();
+            lo = e;
+        }
+        ++p;
+    }
+    if (flags) atomicOr(&t.hdr[0], flags);
+}
+)";
+
 bool gen_groupby_source(const GroupLaunch &G, int32_t tin, Gen &g, std::string &src) {
     const char *TIn = ctype(tin);
     if (!TIn || (G.key_dtype != FQ_DT_UINT64 && G.key_dtype != FQ_DT_INT64)) return false;
@@ -858,7 +1057,10 @@ __device__ long long ginsert(const Tab &t, u64 k) {
         atomicOr(&t.hdr[1], 1u);
         return t.mask + 1;
     }
-    long long h = (long long)(mix(k) & (u64)t.mask);
+    // home slot = the top log2(capacity) bits of the mixer, so the keys of
+    // partition bin b (its top log2(P) bits, fq_jit_gpart) live in one
+    // contiguous 1/P of the table
+    long long h = (long long)(mix(k) >> __clzll(t.mask));
     for (long long p = 0; p <= t.mask; ++p) {
 #if GKEY_PLAIN
         // a plain (L2-cached) read: a slot's key is written once (EMPTY ->
@@ -926,6 +1128,13 @@ __device__ long long ginsert(const Tab &t, u64 k) {
         if (G.kinds[a] != FQ_AGG_COUNT)
             row += "    r.v" + std::to_string(a) + " = fq_val" + std::to_string(a) + "(x, c, flags, r.pass);\n";
     row += "    r.h = (int)(lds_hash(r.k) & (u32)(S - 1));\n}\n";
+    // rows of the partitioned buffer already passed the predicate
+    row += "__device__ __forceinline__ void fq_prep_all(TIn x, u32 live, const Consts &c, u32 &flags, Row &r) {\n"
+           "    r.pass = live;\n    r.k = fq_key(x, c, flags, live);\n";
+    for (int a = 0; a < NA; ++a)
+        if (G.kinds[a] != FQ_AGG_COUNT)
+            row += "    r.v" + std::to_string(a) + " = fq_val" + std::to_string(a) + "(x, c, flags, live);\n";
+    row += "    r.h = (int)(lds_hash(r.k) & (u32)(S - 1));\n}\n";
     row += "__device__ __forceinline__ u64 fq_first(const Row &r, const u64 *s_keys) {\n"
            "    return (r.pass && r.k != EMPTY) ? s_keys[r.h] : EMPTY;\n}\n";
     row += "__device__ __forceinline__ void fq_commit(const Row &r, u64 cur0, const Tab &t, u64 *s_keys,\n"
@@ -974,6 +1183,35 @@ __device__ long long ginsert(const Tab &t, u64 k) {
            "    fq_commit(r, fq_first(r, s_keys), t, s_keys, s_st, s_bypass);\n}\n";
     src += row;
 
+    // LDS table reset and flush (every kernel that aggregates through LDS)
+    src += "__device__ __forceinline__ void fq_lds_reset(u64 *s_keys, u64 (*s_st)[S], int *s_bypass) {\n"
+           "    if (threadIdx.x < 2) s_bypass[threadIdx.x] = 0;\n"
+           "    for (int i = threadIdx.x; i < S; i += BT) {\n        s_keys[i] = EMPTY;\n";
+    for (int a = 0; a < NA; ++a)
+        src += "        s_st[" + std::to_string(a) + "][i] = " + identity(G.kinds[a], G.dtypes[a]) + ";\n";
+    src += "    }\n}\n";
+    src += R"(// this workgroup's groups into the HBM table
+__device__ __forceinline__ void fq_flush(const Tab &tr, const u64 *s_keys, u64 (*s_st)[S]) {
+    for (int i = threadIdx.x; i < S; i += BT) {
+        const u64 k = s_keys[i];
+        if (k == EMPTY) continue;
+        const long long gs = ginsert(tr, k);
+        if (gs < 0) continue;
+)";
+    for (int a = 0; a < NA; ++a) {
+        const std::string sa = "s_st[" + std::to_string(a) + "][i]";
+        std::string v;
+        if (G.kinds[a] == FQ_AGG_COUNT) {
+            src += "        atomicAdd((unsigned long long *)&tr.st[" + std::to_string(a) + "][gs], (unsigned long long)" + sa +
+                   ");\n";
+            continue;
+        }
+        if (G.dtypes[a] == FQ_DT_FLOAT64) v = "__builtin_bit_cast(double, " + sa + ")";
+        else v = "(" + std::string(ctype(G.dtypes[a])) + ")" + sa;
+        src += "        " + state_update(G.kinds[a], G.dtypes[a], "&tr.st[" + std::to_string(a) + "][gs]", v) + "\n";
+    }
+    src += "    }\n}\n";
+
     // kernel
     src += R"(
 extern "C" __global__ void __launch_bounds__(BT)
@@ -982,13 +1220,7 @@ fq_jit_groupby(const TIn *__restrict__ col, long long n, long long head, const u
     __shared__ u64 s_keys[S];
     __shared__ u64 s_st[NA][S];
     __shared__ int s_bypass[2];  // [0] bypass flag, [1] slots claimed
-    if (threadIdx.x < 2) s_bypass[threadIdx.x] = 0;
-    for (int i = threadIdx.x; i < S; i += BT) {
-        s_keys[i] = EMPTY;
-)";
-    for (int a = 0; a < NA; ++a)
-        src += "        s_st[" + std::to_string(a) + "][i] = " + identity(G.kinds[a], G.dtypes[a]) + ";\n";
-    src += R"(    }
+    fq_lds_reset(s_keys, s_st, s_bypass);
     __syncthreads();
     // this workgroup's replica of the HBM states
     Tab tr = t;
@@ -1101,26 +1333,10 @@ fq_jit_groupby(const TIn *__restrict__ col, long long n, long long head, const u
     }
     if (flags) atomicOr(&t.hdr[0], flags);
     __syncthreads();
-    // flush this workgroup's groups into the HBM table
-    for (int i = threadIdx.x; i < S; i += BT) {
-        const u64 k = s_keys[i];
-        if (k == EMPTY) continue;
-        const long long gs = ginsert(tr, k);
-        if (gs < 0) continue;
+    fq_flush(tr, s_keys, s_st);
+}
 )";
-    for (int a = 0; a < NA; ++a) {
-        const std::string sa = "s_st[" + std::to_string(a) + "][i]";
-        std::string v;
-        if (G.kinds[a] == FQ_AGG_COUNT) {
-            src += "        atomicAdd((unsigned long long *)&tr.st[" + std::to_string(a) + "][gs], (unsigned long long)" + sa +
-                   ");\n";
-            continue;
-        }
-        if (G.dtypes[a] == FQ_DT_FLOAT64) v = "__builtin_bit_cast(double, " + sa + ")";
-        else v = "(" + std::string(ctype(G.dtypes[a])) + ")" + sa;
-        src += "        " + state_update(G.kinds[a], G.dtypes[a], "&tr.st[" + std::to_string(a) + "][gs]", v) + "\n";
-    }
-    src += "    }\n}\n";
+    src += kGroupPartitionKernels;
     return true;
 }
 
@@ -1816,7 +2032,15 @@ fq_status jit_scan(int32_t col_dtype, bool chain, const Launch &L, bool *used, b
 }
 
 
-fq_status jit_groupby(int32_t col_dtype, const GroupLaunch &G) {
+namespace {
+
+struct GroupFns {
+    hipFunction_t agg = nullptr, hist = nullptr, part = nullptr, bins = nullptr;
+};
+std::unordered_map<std::string, GroupFns> g_group_cache;
+
+// the shape's module (compiled once): *out stays empty when only validated
+fq_status get_group_fns(int32_t col_dtype, const GroupLaunch &G, GroupFns *out) {
     fq_status err;
     if (!load_rtc(FQ_JIT_ALWAYS, &err)) return err;
     int dev = -1;
@@ -1825,45 +2049,93 @@ fq_status jit_groupby(int32_t col_dtype, const GroupLaunch &G) {
         dev = -1;
     }
     const std::string key = group_shape_key(G, col_dtype, dev);
-    hipFunction_t fn = nullptr;
-    {
-        std::lock_guard<std::mutex> lk(g_mu);
-        auto it = g_cache.find(key);
-        if (it == g_cache.end()) {
-            Gen g;
-            std::string src;
-            Compiled c;
-            if (!gen_groupby_source(G, col_dtype, g, src))
-                return fqc::fail(FQ_E_UNSUPPORTED, "GROUP BY: key/aggregate types outside the device path");
-            fq_status s = compile(src, dev, c, "fq_jit_groupby");
-            if (s != FQ_OK) return s;
-            c.ok = true;
-            if (dev < 0) return FQ_OK;  // validated only
-            it = g_cache.emplace(key, c).first;
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto it = g_group_cache.find(key);
+    if (it == g_group_cache.end()) {
+        Gen g;
+        std::string src;
+        Compiled c;
+        if (!gen_groupby_source(G, col_dtype, g, src))
+            return fqc::fail(FQ_E_UNSUPPORTED, "GROUP BY: key/aggregate types outside the device path");
+        fq_status s = compile(src, dev, c, "fq_jit_groupby");
+        if (s != FQ_OK) return s;
+        if (dev < 0) {  // validated only
+            *out = GroupFns{};
+            return FQ_OK;
         }
-        fn = it->second.fn;
+        GroupFns f;
+        f.agg = c.fn;
+        FQ_HIP_TRY(hipModuleGetFunction(&f.hist, c.mod, "fq_jit_ghist"));
+        FQ_HIP_TRY(hipModuleGetFunction(&f.part, c.mod, "fq_jit_gpart"));
+        FQ_HIP_TRY(hipModuleGetFunction(&f.bins, c.mod, "fq_jit_groupby_bins"));
+        it = g_group_cache.emplace(key, f).first;
     }
-    if (!G.col || G.n == 0) return FQ_OK;
-    HostGroupConsts hc;
-    pack_group_consts(G, hc);
-    struct {
-        uint64_t *keys;
-        uint64_t *st[FQ_MAX_GROUP_AGGS];
-        uint32_t *hdr;
-        long long mask;
-        int rmask;
-    } tab;
+    *out = it->second;
+    return FQ_OK;
+}
+
+struct GroupTab {
+    uint64_t *keys;
+    uint64_t *st[FQ_MAX_GROUP_AGGS];
+    uint32_t *hdr;
+    long long mask;
+    int rmask;
+};
+
+GroupTab group_tab(const GroupLaunch &G) {
+    GroupTab tab;
     tab.keys = G.keys;
     for (int a = 0; a < FQ_MAX_GROUP_AGGS; ++a) tab.st[a] = G.states[a];
     tab.hdr = G.hdr;
     tab.mask = (long long)G.capacity - 1;
     tab.rmask = group_replicas(G.capacity) - 1;
+    return tab;
+}
+
+}  // namespace
+
+fq_status jit_groupby(int32_t col_dtype, const GroupLaunch &G) {
+    GroupFns f;
+    fq_status s = get_group_fns(col_dtype, G, &f);
+    if (s != FQ_OK || !f.agg || !G.col || G.n == 0) return s;
+    HostGroupConsts hc;
+    pack_group_consts(G, hc);
+    GroupTab tab = group_tab(G);
     const void *col = G.col;
     long long n = G.n, head = G.head;
     const uint64_t *bitmap = G.pred.bitmap;
     void *args[] = {&col, &n, &head, &bitmap, &hc, &tab};
-    FQ_HIP_TRY(hipModuleLaunchKernel(fn, (unsigned)G.grid, 1, 1, (unsigned)G.threads, 1, 1, 0, G.stream, args, nullptr));
+    FQ_HIP_TRY(hipModuleLaunchKernel(f.agg, (unsigned)G.grid, 1, 1, (unsigned)G.threads, 1, 1, 0, G.stream, args, nullptr));
     g_jit_launches += 1;
+    return FQ_OK;
+}
+
+fq_status jit_groupby_partitioned(int32_t col_dtype, const GroupLaunch &G, const GroupPartition &X) {
+    GroupFns f;
+    fq_status s = get_group_fns(col_dtype, G, &f);
+    if (s != FQ_OK || !f.agg || !G.col || G.n == 0) return s;
+    HostGroupConsts hc;
+    pack_group_consts(G, hc);
+    GroupTab tab = group_tab(G);
+    const void *col = G.col;
+    long long n = G.n;
+    const uint64_t *bitmap = G.pred.bitmap;
+    int log2p = X.log2p;
+    uint32_t *hist = X.hist;
+    uint32_t *hdr = G.hdr;
+    void *a1[] = {&col, &n, &bitmap, &hc, &hist, &log2p, &hdr};
+    FQ_HIP_TRY(hipModuleLaunchKernel(f.hist, (unsigned)X.grid, 1, 1, (unsigned)G.threads, 1, 1, 0, G.stream, a1, nullptr));
+    if ((s = launch_group_part_scan(X, G.stream)) != FQ_OK) return s;
+    const uint64_t *off = X.off;
+    void *vals = X.vals;
+    void *a2[] = {&col, &n, &bitmap, &hc, &off, &vals, &log2p};
+    FQ_HIP_TRY(hipModuleLaunchKernel(f.part, (unsigned)X.grid, 1, 1, (unsigned)G.threads, 1, 1, 0, G.stream, a2, nullptr));
+    const void *cvals = X.vals;
+    const uint64_t *bins = X.bins;
+    void *a3[] = {&cvals, &bins, &log2p, &hc, &tab};
+    FQ_HIP_TRY(hipModuleLaunchKernel(f.bins, (unsigned)X.bins_grid, 1, 1, (unsigned)G.threads, 1, 1, 0, G.stream, a3,
+                                     nullptr));
+    g_jit_launches += 3;
     return FQ_OK;
 }
 

@@ -95,6 +95,23 @@ struct GroupLaunch {
 // Launches the hipRTC-specialised group-by kernel for G.
 fq_status jit_groupby(int32_t col_dtype, const GroupLaunch &G);
 
+// The partitioned (high-cardinality) path of fq_group_aggregate_partitioned:
+// histogram -> scan -> partition -> per-bin aggregation, in the caller's
+// workspace (fq_groupby.hip lays it out).
+constexpr int kMaxPartGrid = 1024;  // workgroups of the histogram / partition kernels
+struct GroupPartition {
+    int log2p;        // 1..8: P = 2^log2p bins
+    int grid;         // workgroups of fq_jit_ghist and fq_jit_gpart (the same tiles)
+    int bins_grid;    // workgroups of fq_jit_groupby_bins
+    uint32_t *hist;   // [P][grid] rows per (bin, workgroup)
+    uint64_t *off;    // [P][grid] their exclusive offsets
+    uint64_t *bins;   // [P + 1] bin starts in vals
+    void *vals;       // the passing rows, grouped by bin
+};
+fq_status jit_groupby_partitioned(int32_t col_dtype, const GroupLaunch &G, const GroupPartition &X);
+// exclusive scan of X.hist into X.off and X.bins (one workgroup; fq_groupby.hip)
+fq_status launch_group_part_scan(const GroupPartition &X, hipStream_t stream);
+
 // One fq_filter_project / fq_predicate_bitmap call (fq_filter.hip ->
 // fq_jit.hip): FilterTransform's predicate and ProjectionTransform's
 // expressions over one 64-bit column, hipRTC-specialised per shape.

@@ -20,7 +20,7 @@ GPU_SYMBOLS = [
     "fq_filter_compact", "fq_state_merge", "fq_jit_config", "fq_jit_get_stats", "fq_jit_prepare",
     "fq_group_table_bytes", "fq_group_table_init", "fq_group_aggregate", "fq_group_table_count",
     "fq_group_table_extract", "fq_logic", "fq_filter_project_workspace_bytes", "fq_filter_project",
-    "fq_predicate_bitmap",
+    "fq_predicate_bitmap", "fq_group_partition_workspace_bytes", "fq_group_aggregate_partitioned",
 ]
 
 
@@ -82,6 +82,9 @@ _protos = {
     "fq_group_table_init": (C.c_int32, [P(abi.fq_group_table), vp]),
     "fq_group_aggregate": (C.c_int32, [P(abi.fq_group_table), P(abi.fq_col), P(abi.fq_pred), P(abi.fq_expr),
                                        P(abi.fq_expr), vp]),
+    "fq_group_partition_workspace_bytes": (C.c_size_t, [C.c_int64, C.c_int32]),
+    "fq_group_aggregate_partitioned": (C.c_int32, [P(abi.fq_group_table), P(abi.fq_col), P(abi.fq_pred),
+                                                   P(abi.fq_expr), P(abi.fq_expr), C.c_int32, vp, C.c_size_t, vp]),
     "fq_group_table_count": (C.c_int32, [P(abi.fq_group_table), P(C.c_int64), vp]),
     "fq_group_table_extract": (C.c_int32, [P(abi.fq_group_table), vp, P(C.c_void_p), C.c_int64, P(C.c_int64),
                                            vp]),

@@ -318,14 +318,23 @@ class GroupTable:
         self.aggs = list(aggs)
         check(lib.fq_group_table_init(C.byref(self.desc), _stream(stream)))
 
-    def aggregate(self, col, pred=None, key=None, values=None, stream=None):
+    def aggregate(self, col, pred=None, key=None, values=None, stream=None, log2_parts=0):
+        """fq_group_aggregate, or with log2_parts > 0 the radix-partitioned
+        fq_group_aggregate_partitioned (2^log2_parts bins)."""
         c = col.col()
         vals = (abi.fq_expr * abi.MAX_GROUP_AGGS)()
         for i, v in enumerate(values or []):
             if v is not None:
                 vals[i] = v
-        check(lib.fq_group_aggregate(C.byref(self.desc), C.byref(c), C.byref(pred) if pred is not None else None,
-                                     C.byref(key) if key is not None else None, vals, _stream(stream)))
+        p = C.byref(pred) if pred is not None else None
+        k = C.byref(key) if key is not None else None
+        if not log2_parts:
+            check(lib.fq_group_aggregate(C.byref(self.desc), C.byref(c), p, k, vals, _stream(stream)))
+            return
+        ws = Workspace(lib.fq_group_partition_workspace_bytes(col.len, log2_parts))
+        check(lib.fq_group_aggregate_partitioned(C.byref(self.desc), C.byref(c), p, k, vals, log2_parts, ws.ptr,
+                                                 ws.nbytes, _stream(stream)))
+        self._ws = ws  # alive until the next call (the launch is asynchronous)
 
     def count(self, stream=None):
         n = C.c_int64(0)

@@ -297,3 +297,112 @@ def test_sql_group_by_with_logic_predicate(eng):
     w = R.E_bin("and", R.E_bin("<", R.E_bin("%", N, _c(8)), _c(3)), R.E_bin(">", N, _c(100)))
     exp = R.group_by_query(total, R.E_bin("%", N, _c(4)), [R.E_fn("count", N), R.E_fn("max", N)], where=w)
     assert r.rows == exp
+
+
+# ---- radix-partitioned high-cardinality path (fq_group_aggregate_partitioned) ----
+
+def run_parts(col, aggs, log2p, key=None, values=None, pred=None, key_dtype=U, capacity=1 << 12, blocks=1):
+    t = ops.GroupTable(capacity, aggs, key_dtype)
+    for _ in range(blocks):
+        t.aggregate(col, pred, key, values, log2_parts=log2p)
+    keys, states = t.extract()
+    if key_dtype == I:
+        keys = keys.view(np.int64)
+    st = decode(states, [dt for _, dt in aggs])
+    return {int(k): [st[a][i] for a in range(len(aggs))] for i, k in enumerate(keys)}
+
+
+@pytest.mark.parametrize("mod,log2p", [(7, 1), (1000, 3), (100_000, 6), (2_000_000, 8), (None, 8)])
+def test_partitioned_matches_numpy(mod, log2p):
+    # 2 blocks into one table: rows of both, every group once, all aggregate kinds
+    n = 3_000_017
+    col = ops.splitmix_column(0x5A, 3, n)
+    x = col.to_numpy()
+    key = chain(U, [("%", mod)])[0] if mod else None
+    vf, _ = chain(U, [("*", 0.25)])
+    aggs = [(abi.AGG_COUNT, U), (abi.AGG_SUM, U), (abi.AGG_MAX, U), (abi.AGG_MIN, U), (abi.AGG_SUM, F)]
+    groups = min(n, mod or n)
+    got = run_parts(col, aggs, log2p, key=key, values=[None, None, None, None, vf], capacity=4 * groups, blocks=2)
+    xx = np.concatenate([x, x])
+    k = xx % np.uint64(mod) if mod else xx
+    xf = xx.astype(np.float64) * 0.25
+    exp = np_groupby(k, [None, xx, xx, xx, xf], [a for a, _ in aggs])
+    bound = {g: 1e-12 * abs(e[4]) * 4 + 1e-9 for g, e in exp.items()}
+    compare(got, exp, [a for a, _ in aggs], [d for _, d in aggs], bound)
+
+
+def test_partitioned_equals_lds_path_bit_exact():
+    # integer states: the partitioned path and the plain kernel agree exactly
+    n = 5_000_003
+    col = ops.splitmix_column(0x31, 0, n)
+    key, _ = chain(U, [("%", 4096)])
+    aggs = [(abi.AGG_COUNT, U), (abi.AGG_SUM, U), (abi.AGG_MIN, U)]
+    a = run(col, aggs, key=key, capacity=1 << 14)
+    b = run_parts(col, aggs, 4, key=key, capacity=1 << 14)
+    assert a == b
+
+
+def test_partitioned_predicates_and_misaligned_column():
+    n = 1_000_001
+    base = ops.numbers_column(0, n + 1)
+    x = np.arange(1, n + 1, dtype=np.uint64)
+    col = ops.DeviceColumn(base.buf, n, U, 8)  # rows 1..n: 8-byte aligned, not 16
+    key, _ = chain(U, [("%", 50_000)])
+    v, _ = chain(U, [("+", 1)])
+    aggs = [(abi.AGG_MAX, U), (abi.AGG_COUNT, U)]
+    pred = predicate(U, [("%", 8)], "<", 3)
+    got = run_parts(col, aggs, 5, key=key, values=[v, None], pred=pred, capacity=1 << 17)
+    m = (x % np.uint64(8)) < 3
+    exp = np_groupby((x % np.uint64(50_000))[m], [(x + np.uint64(1))[m], None], [abi.AGG_MAX, abi.AGG_COUNT])
+    compare(got, exp, [abi.AGG_MAX, abi.AGG_COUNT], [U, U])
+    # bitmap predicate: rows by index
+    bm = ops.compare("<", col, 700_000)
+    p = abi.fq_pred()
+    p.kind = abi.PRED_BITMAP
+    p.bitmap = bm.ptr
+    got = run_parts(col, [(abi.AGG_COUNT, U)], 5, key=key, pred=p, capacity=1 << 17)
+    m = x < np.uint64(700_000)
+    exp = np_groupby((x % np.uint64(50_000))[m], [None], [abi.AGG_COUNT])
+    compare(got, exp, [abi.AGG_COUNT], [U])
+
+
+def test_partitioned_signed_keys_small_inputs_and_errors():
+    col = ops.numbers_column(0, 300_000)
+    x = np.arange(300_000, dtype=np.int64)
+    key, kdt = chain(U, [("-", (150_000, "Int64"))])  # negative and positive Int64 keys, all distinct
+    aggs = [(abi.AGG_SUM, I), (abi.AGG_COUNT, U)]
+    v, _ = chain(U, [("-", (7, "Int64"))])
+    got = run_parts(col, aggs, 7, key=key, values=[v, None], key_dtype=I, capacity=1 << 20)
+    assert len(got) == 300_000
+    assert got[-150_000] == [-7, 1] and got[149_999] == [299_992, 1]
+    for n in (0, 1, 63, 8191, 8193):  # fewer rows than one tile / than the workgroups
+        c = ops.numbers_column(5, n)
+        g = run_parts(c, [(abi.AGG_COUNT, U)], 2, capacity=1 << 14) if n else {}
+        assert g == {5 + i: [1] for i in range(n)}
+    key, _ = chain(U, [("%", 2), ("/", 7, True)])  # 7 / (number % 2): zero on even rows
+    t = ops.GroupTable(64, [(abi.AGG_COUNT, U)])
+    t.aggregate(col, key=key, log2_parts=3)
+    with pytest.raises(ops.FQError) as ei:
+        t.count()
+    assert str(ei.value) == "Internal Error: Divide by zero error"
+    with pytest.raises(ops.FQError):
+        t.aggregate(col, key=key, log2_parts=9)
+
+
+def test_sql_high_cardinality_group_by_takes_the_partitioned_path(eng):
+    # 50,000 groups per partition: the engine's sample sees more groups than an
+    # LDS table holds and launches the radix-partitioned kernels
+    total = 2_400_000
+    j0 = ops.jit_stats()["jit_launches"]
+    r = eng.execute("SELECT number%%50000, count(number), max(number), sum(number) FROM system.numbers_mt(%d) "
+                    "WHERE number%%3 < 2 GROUP BY number%%50000" % total)
+    assert ops.jit_stats()["jit_launches"] - j0 >= 3 * 8  # ghist + gpart + bins per partition
+    x = np.arange(total, dtype=np.uint64)
+    x = x[x % np.uint64(3) < 2]
+    exp = np_groupby(x % np.uint64(50000), [None, x, x], [abi.AGG_COUNT, abi.AGG_MAX, abi.AGG_SUM])
+    assert len(r.rows) == len(exp)
+    for k, cnt, mx, sm in r.rows:
+        assert [cnt, mx, sm] == [int(v) for v in exp[k]]
+    # keys only, every key distinct
+    r = eng.execute("SELECT number FROM system.numbers_mt(400000) GROUP BY number")
+    assert r.rows == [(i,) for i in range(400000)]

@@ -1,5 +1,7 @@
 """GROUP BY throughput vs number of groups and aggregates over one numbers_mt
-partition (python tools/groupby_sweep.py [rows] [mods] [naggs] [launches]); one line per shape.
+partition (python tools/groupby_sweep.py [rows] [mods] [naggs] [launches] [log2_parts]); one line per shape.
+log2_parts > 0 runs the radix-partitioned path (fq_group_aggregate_partitioned);
+"auto" picks ceil(log2(groups / 2048)) in [1, 8] for groups above 3,072 (as the engine does).
 With launches L > 1 the column is aggregated L times into one table (as the
 engine does for the partitions of one query); the time is per launch."""
 import sys, os, ctypes as C, statistics
@@ -21,16 +23,29 @@ def timed(fn, reps=5):
 MODS = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else [8, 64, 1000, 4096, 100000]
 NAGGS = [int(x) for x in sys.argv[3].split(",")] if len(sys.argv) > 3 else [1, 3]
 L = int(sys.argv[4]) if len(sys.argv) > 4 else 1
+PARTS = sys.argv[5] if len(sys.argv) > 5 else "0"
+
+
+def log2_parts(groups):
+    if PARTS != "auto":
+        return int(PARTS)
+    if groups <= 3072:
+        return 0
+    p = 1
+    while p < 8 and (groups >> p) > 2048:
+        p += 1
+    return p
 for mod in MODS:
     for naggs in NAGGS:
         key, _ = chain(U, [("%", mod)])
         aggs = [(abi.AGG_COUNT, U), (abi.AGG_SUM, U), (abi.AGG_MAX, U)][:naggs]
-        gt = ops.GroupTable(max(64, 4 * mod), aggs)
+        gt = ops.GroupTable(max(64, 4 * min(mod, n)), aggs)
+        lp = log2_parts(min(mod, n))
         if L == 1:
             def f():
-                check(lib.fq_group_table_init(C.byref(gt.desc), st)); gt.aggregate(a, key=key)
+                check(lib.fq_group_table_init(C.byref(gt.desc), st)); gt.aggregate(a, key=key, log2_parts=lp)
             ms = timed(f)
-            print("mod=%6d aggs=%d  %.3f ms  %.1f G rows/s" % (mod, naggs, ms, n / ms / 1e6), flush=True)
+            print("mod=%6d aggs=%d parts=2^%d  %.3f ms  %.1f G rows/s" % (mod, naggs, lp, ms, n / ms / 1e6), flush=True)
             continue
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(L + 1)]
         per = []
@@ -38,11 +53,11 @@ for mod in MODS:
             check(lib.fq_group_table_init(C.byref(gt.desc), st))
             ev[0].record()
             for i in range(L):
-                gt.aggregate(a, key=key)
+                gt.aggregate(a, key=key, log2_parts=lp)
                 ev[i + 1].record()
             ev[L].synchronize()
             per.append([ev[i].elapsed_time(ev[i + 1]) for i in range(L)])
         first = statistics.median(p[0] for p in per)
         rest = statistics.median(statistics.mean(p[1:]) for p in per)
-        print("mod=%6d aggs=%d launches=%d  first %.3f ms, then %.3f ms/launch (%.1f G rows/s)"
-              % (mod, naggs, L, first, rest, n / rest / 1e6), flush=True)
+        print("mod=%6d aggs=%d parts=2^%d launches=%d  first %.3f ms, then %.3f ms/launch (%.1f G rows/s)"
+              % (mod, naggs, lp, L, first, rest, n / rest / 1e6), flush=True)
