@@ -485,7 +485,7 @@ DataValue fold_leaf(uint32_t op, const DataValue &a, const DataValue &b) {
 // whose keys repeat (distinct <= half the rows) has seen about all the groups
 // of a block; one that is still mostly distinct grows with the rows.  Beyond
 // 3,072 groups per launch (3/4 of an LDS table) the launches go through the
-// radix-partitioned kernels with about 2,048 groups per bin; the table gets
+// radix-partitioned kernels with about 1,024 groups per bin; the table gets
 // twice the expected groups in slots (a TABLE_FULL re-run grows it 16x).
 namespace {
 constexpr int64_t kGroupSampleRows = 1 << 21;
@@ -525,9 +525,9 @@ GroupPlan plan_group_by(const fq_group_table &d, const fq_col &c, const fq_pred 
         2 * g <= rows ? 2 * g : (int64_t)((double)g * (double)c.len / (double)std::max<int64_t>(rows, 1));
     GroupPlan p;
     p.capacity = next_pow2(std::max<int64_t>(4096, 2 * per_launch));
-    if (per_launch > 3072) {
-        p.log2_parts = 1;
-        while (p.log2_parts < 8 && (per_launch >> p.log2_parts) > 2048) ++p.log2_parts;
+    if (per_launch > 3072) {  // ~1,024 groups per bin (tools/groupby_sweep.py: 100,000 groups x 3
+        p.log2_parts = 1;       // aggregates, P = 64/128/256: 13.3/12.4/13.8 ms per 10 GB)
+        while (p.log2_parts < 8 && (per_launch >> p.log2_parts) > 1024) ++p.log2_parts;
     }
     return p;
 }

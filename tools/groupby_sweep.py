@@ -1,7 +1,7 @@
 """GROUP BY throughput vs number of groups and aggregates over one numbers_mt
 partition (python tools/groupby_sweep.py [rows] [mods] [naggs] [launches] [log2_parts]); one line per shape.
 log2_parts > 0 runs the radix-partitioned path (fq_group_aggregate_partitioned);
-"auto" picks ceil(log2(groups / 2048)) in [1, 8] for groups above 3,072 (as the engine does).
+"auto" picks ceil(log2(groups / 1024)) in [1, 8] for groups above 3,072 (as the engine does).
 With launches L > 1 the column is aggregated L times into one table (as the
 engine does for the partitions of one query); the time is per launch."""
 import sys, os, ctypes as C, statistics
@@ -12,7 +12,8 @@ from fq_amd._lib import check, lib
 from fq_amd.expr import chain
 U = abi.DT_UINT64
 n = int(float(sys.argv[1])) if len(sys.argv) > 1 else 1_250_000_000
-a = ops.numbers_column(0, n)
+# RANDOM=1: a splitmix64 column (keys in random order) instead of numbers_mt's iota
+a = ops.splitmix_column(0x5EED, 0, n) if os.environ.get("RANDOM") == "1" else ops.numbers_column(0, n)
 st = ops._stream()
 def timed(fn, reps=5):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -32,7 +33,7 @@ def log2_parts(groups):
     if groups <= 3072:
         return 0
     p = 1
-    while p < 8 and (groups >> p) > 2048:
+    while p < 8 and (groups >> p) > 1024:
         p += 1
     return p
 for mod in MODS:
