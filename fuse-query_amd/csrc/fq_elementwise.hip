@@ -13,6 +13,7 @@
 // into its scan (fq_aggregate.hip) and only falls back here for expression
 // shapes the fused chain cannot express.
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 
 #include <string>
 
@@ -247,11 +248,15 @@ __device__ __forceinline__ uint64_t spread32(uint32_t v) {
 }
 
 // A wave compares 8 x 128 rows per iteration (lane l holds rows 2l and 2l+1
-// of each 128-row segment in one 16-byte load; 8 loads in flight), turns each
-// segment's two ballots into two bitmap words on the scalar unit, and lanes
-// 0..15 store the 16 words (128 contiguous bytes).  `ngroups` = whole
-// 1024-row groups.  (4 segments: 5.2 TB/s; 8: 6.1 TB/s.)
-template <typename TC, int CMP, bool LSC, bool RSC>
+// of each 128-row segment in one 16-byte load; 8 loads in flight) and lanes
+// 0..15 store the segments' 16 bitmap words (128 contiguous bytes).
+// `ngroups` = whole 1024-row groups.  (4 segments: 5.2 TB/s; 8: 6.1 TB/s.)
+// Bit r of a segment's words belongs to lane r >> 1: one ds_bpermute hands
+// lane l the two results of lane l >> 1 (word 0) and of lane 32 + (l >> 1)
+// (word 1), so each word is a single ballot; interleaving two 32-bit ballots
+// on the scalar unit instead (spread32, 4 per segment) cost 1.68 vs 1.55 ms
+// per 10 GB (tools/bench_kernels.py; FQ_CMP_SPREAD=1 keeps it for A/B).
+template <typename TC, int CMP, bool LSC, bool RSC, bool SPREAD>
 __global__ void __launch_bounds__(256)
     compare_vec_kernel(const TC *__restrict__ l, uint64_t lc, const TC *__restrict__ r, uint64_t rc,
                        uint64_t *__restrict__ bitmap, int64_t ngroups) {
@@ -279,10 +284,19 @@ __global__ void __launch_bounds__(256)
             else x[0] = x[1] = lconst;
             if constexpr (!RSC) __builtin_memcpy(y, &b[k], 16);
             else y[0] = y[1] = rconst;
-            const uint64_t b0 = __ballot(compare<TC>(CMP, x[0], y[0]));
-            const uint64_t b1 = __ballot(compare<TC>(CMP, x[1], y[1]));
-            const uint64_t w0 = spread32((uint32_t)b0) | (spread32((uint32_t)b1) << 1);
-            const uint64_t w1 = spread32((uint32_t)(b0 >> 32)) | (spread32((uint32_t)(b1 >> 32)) << 1);
+            uint64_t w0, w1;
+            if constexpr (SPREAD) {
+                const uint64_t b0 = __ballot(compare<TC>(CMP, x[0], y[0]));
+                const uint64_t b1 = __ballot(compare<TC>(CMP, x[1], y[1]));
+                w0 = spread32((uint32_t)b0) | (spread32((uint32_t)b1) << 1);
+                w1 = spread32((uint32_t)(b0 >> 32)) | (spread32((uint32_t)(b1 >> 32)) << 1);
+            } else {
+                const int two = (compare<TC>(CMP, x[0], y[0]) ? 1 : 0) | (compare<TC>(CMP, x[1], y[1]) ? 2 : 0);
+                const int lo = __builtin_amdgcn_ds_bpermute((lane >> 1) << 2, two);
+                const int hi = __builtin_amdgcn_ds_bpermute((32 + (lane >> 1)) << 2, two);
+                w0 = __ballot((lo >> (lane & 1)) & 1);
+                w1 = __ballot((hi >> (lane & 1)) & 1);
+            }
             mine = lane == 2 * k ? w0 : mine;
             mine = lane == 2 * k + 1 ? w1 : mine;
         }
@@ -296,9 +310,16 @@ static void launch_vec_op(bool lsc, bool rsc, const void *l, uint64_t lc, const 
     const TC *L = (const TC *)l, *R = (const TC *)r;
     if constexpr (CMPK) {
         uint64_t *bm = (uint64_t *)out;
-        if (lsc) hipLaunchKernelGGL((compare_vec_kernel<TC, OP, true, false>), dim3(grid), dim3(256), 0, st, L, lc, R, rc, bm, units);
-        else if (rsc) hipLaunchKernelGGL((compare_vec_kernel<TC, OP, false, true>), dim3(grid), dim3(256), 0, st, L, lc, R, rc, bm, units);
-        else hipLaunchKernelGGL((compare_vec_kernel<TC, OP, false, false>), dim3(grid), dim3(256), 0, st, L, lc, R, rc, bm, units);
+        static const bool spread = getenv("FQ_CMP_SPREAD") != nullptr;  // A/B: the scalar-unit interleave
+        if (spread) {
+            if (lsc) hipLaunchKernelGGL((compare_vec_kernel<TC, OP, true, false, true>), dim3(grid), dim3(256), 0, st, L, lc, R, rc, bm, units);
+            else if (rsc) hipLaunchKernelGGL((compare_vec_kernel<TC, OP, false, true, true>), dim3(grid), dim3(256), 0, st, L, lc, R, rc, bm, units);
+            else hipLaunchKernelGGL((compare_vec_kernel<TC, OP, false, false, true>), dim3(grid), dim3(256), 0, st, L, lc, R, rc, bm, units);
+        } else {
+            if (lsc) hipLaunchKernelGGL((compare_vec_kernel<TC, OP, true, false, false>), dim3(grid), dim3(256), 0, st, L, lc, R, rc, bm, units);
+            else if (rsc) hipLaunchKernelGGL((compare_vec_kernel<TC, OP, false, true, false>), dim3(grid), dim3(256), 0, st, L, lc, R, rc, bm, units);
+            else hipLaunchKernelGGL((compare_vec_kernel<TC, OP, false, false, false>), dim3(grid), dim3(256), 0, st, L, lc, R, rc, bm, units);
+        }
         (void)flag;
     } else {
         TC *O = (TC *)out;
@@ -438,8 +459,16 @@ static fq_status launch_fast(bool cmp, int32_t tc, EwArgs &a) {
     const int64_t rows_per_unit = cmp ? 1024 : (int64_t)kEwU * 256 * 2;
     const int64_t units = a.n / rows_per_unit;
     if (units == 0) return FQ_OK;
-    const int64_t cap = (int64_t)fqc::device_cu_count() * 2;
-    // arith: one tile per workgroup iteration; compare: one 512-row group per wave
+    // workgroups per CU: arith 8, compare 2 (tools/probes/ew_wg_sweep.sh, one box:
+    // arith u64 + const 3.57/3.49/3.44/3.38 ms at 1/2/4/8, compare 1.68/1.71/1.75/1.73);
+    // FQ_EW_WG_PER_CU overrides both (tuning)
+    static const int wg_override = [] {
+        const char *e = getenv("FQ_EW_WG_PER_CU");
+        const int x = e ? atoi(e) : 0;
+        return x >= 1 && x <= 16 ? x : 0;
+    }();
+    const int64_t cap = (int64_t)fqc::device_cu_count() * (wg_override ? wg_override : (cmp ? 2 : 8));
+    // arith: one tile per workgroup iteration; compare: one 1,024-row group per wave
     const int64_t want = cmp ? (units + 3) / 4 : units;
     const int grid = (int)(want < cap ? want : cap);
     switch (tc) {
