@@ -194,7 +194,8 @@ def main():
     ap.add_argument("--rows-total", type=float, default=None,
                     help="strong scaling: fix numbers_mt(N) at this N for every GPU count "
                          "(e.g. 1e10 = the 10B-row metric split over 1/2/4/8 GPUs)")
-    ap.add_argument("--cpu-sample-rows", type=float, default=4e9)
+    ap.add_argument("--cpu-sample-rows", type=float, default=1e10,
+                    help="rows of the CPU-baseline sample (1e10 = the whole workload: ~12 s of CPU work on 8 threads)")
     ap.add_argument("--cpu-threads", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--streams", type=int, default=1,

@@ -1,6 +1,7 @@
 // C ABI of the engine (include/fq_engine.h).
 #include <string.h>
 
+#include <iterator>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -107,7 +108,8 @@ void append_block(fq_result *r, const fq::DataBlock &b0, fq::ExecCtx &ctx) {
         std::vector<fq::DataValue> v = b.columns[c].to_host(ctx.stream());
         if (b.columns[c].dtype == FQ_DT_NULL && v.empty()) v.assign((size_t)b.columns[c].len, fq::DataValue::null());
         n = std::max<int64_t>(n, (int64_t)v.size());
-        r->cols[c].insert(r->cols[c].end(), v.begin(), v.end());
+        if (r->cols[c].empty()) r->cols[c] = std::move(v);
+        else r->cols[c].insert(r->cols[c].end(), std::make_move_iterator(v.begin()), std::make_move_iterator(v.end()));
     }
     r->rows += n;
 }

@@ -4,6 +4,7 @@
 #include <string.h>
 
 #include <exception>
+#include <algorithm>
 #include <map>
 
 namespace fq {
@@ -478,6 +479,28 @@ DataValue fold_leaf(uint32_t op, const DataValue &a, const DataValue &b) {
     return b_better ? b : a;
 }
 
+// One leaf's states over the rows of a GROUP BY final: 64-bit words plus a
+// Some/None flag per row (exchanged states may be None; device ones never)
+struct FlatLeaf {
+    DataType dtype = FQ_DT_NULL;
+    std::vector<uint64_t> bits;
+    std::vector<uint8_t> some;
+    DataValue value(uint32_t r) const {
+        return some[r] ? DataValue::some(dtype, bits[r]) : DataValue::none(dtype);
+    }
+    // row `to` = fold_leaf(row `to`, row `from`)
+    void fold_into(uint32_t op, uint32_t to, uint32_t from) {
+        if (!some[from]) return;
+        if (!some[to]) {
+            bits[to] = bits[from];
+            some[to] = 1;
+            return;
+        }
+        const DataValue v = fold_leaf(op, DataValue::some(dtype, bits[to]), DataValue::some(dtype, bits[from]));
+        bits[to] = v.bits;
+    }
+};
+
 }  // namespace
 
 // GROUP BY sizing from a sample of the first block: the distinct keys among
@@ -673,29 +696,41 @@ StreamRef GroupByFinalTransform::execute() {
     for (auto &f : funcs_) funcs.push_back(f->clone());
     const std::vector<AggregatorFunction *> leaves = leaves_of(funcs);
     StreamRef in = input_->execute();
-    // groups: key -> leaf states; exchanged partial rows arrive as Struct
-    // rows [key, leaf states...] (fq_engine_execute_final)
-    std::map<std::pair<int, uint64_t>, std::vector<DataValue>> host_groups;  // ordered by key
+    // Groups as flat arrays: one row per (key, leaf states) from the device
+    // table and from exchanged partial rows (Struct rows [key, leaf states...],
+    // fq_engine_execute_final); sorted by key, equal keys folded.
+    const size_t nl = leaves.size();
     DataType kdt = FQ_DT_NULL;
-    auto order_key = [&kdt](uint64_t k) {
-        // (sign bucket, bits) orders Int64 keys numerically and UInt64 keys as unsigned
-        if (kdt == FQ_DT_INT64) return std::make_pair((int64_t)k < 0 ? 0 : 1, k);
-        return std::make_pair(1, k);
-    };
+    std::vector<uint64_t> keys;
+    std::vector<FlatLeaf> ls(nl);
     DataBlock b;
-    std::vector<std::vector<DataValue>> exchanged;
+    std::vector<const std::vector<DataValue> *> exchanged;
+    std::vector<DataBlock> held;  // keeps the exchanged rows alive
     while (in->next(b)) {
         if (b.columns.empty() || !b.columns[0].host) continue;
         for (const auto &row : *b.columns[0].host)
-            if (row.kind == DataValue::kStruct && !row.fields.empty()) exchanged.push_back(row.fields);
+            if (row.kind == DataValue::kStruct && !row.fields.empty()) exchanged.push_back(&row.fields);
+        held.push_back(b);
+    }
+    if (shared_->ready) kdt = shared_->desc.key_dtype;
+    else if (!exchanged.empty()) kdt = (*exchanged[0])[0].dtype;
+    for (const std::vector<DataValue> *rp : exchanged) {
+        const std::vector<DataValue> &row = *rp;
+        if (row.size() != 1 + nl) throw_status(FQ_E_INVALID, "GROUP BY: malformed partial state row");
+        keys.push_back(row[0].bits);
+        for (size_t a = 0; a < nl; ++a) {
+            const DataValue &v = row[a + 1];
+            if (ls[a].dtype == FQ_DT_NULL && v.kind == DataValue::kSome) ls[a].dtype = v.dtype;
+            ls[a].bits.push_back(v.bits);
+            ls[a].some.push_back(v.kind == DataValue::kSome ? 1 : 0);
+        }
     }
     if (shared_->ready) {
         const fq_group_table &d = shared_->desc;
-        kdt = d.key_dtype;
         int64_t groups = 0;
         check_fq(fq_group_table_count(&d, &groups, ctx.stream()));
         const int64_t n = groups > 0 ? groups : 1;
-        auto keys = DeviceBuffer::alloc((size_t)n * 8, ctx.stream());
+        auto kbuf = DeviceBuffer::alloc((size_t)n * 8, ctx.stream());
         std::vector<std::shared_ptr<DeviceBuffer>> st;
         uint64_t *ptrs[FQ_MAX_GROUP_AGGS] = {};
         for (int a = 0; a < d.n_aggs; ++a) {
@@ -703,55 +738,87 @@ StreamRef GroupByFinalTransform::execute() {
             ptrs[a] = (uint64_t *)st.back()->ptr;
         }
         int64_t got = 0;
-        check_fq(fq_group_table_extract(&d, (uint64_t *)keys->ptr, ptrs, n, &got, ctx.stream()));
-        std::vector<uint64_t> hk((size_t)got);
-        std::vector<std::vector<uint64_t>> hs((size_t)d.n_aggs, std::vector<uint64_t>((size_t)got));
+        check_fq(fq_group_table_extract(&d, (uint64_t *)kbuf->ptr, ptrs, n, &got, ctx.stream()));
+        const size_t at = keys.size();  // after the exchanged rows (the fold order)
+        keys.resize(at + (size_t)got);
+        for (size_t a = 0; a < nl; ++a) {
+            ls[a].dtype = leaves[a]->op() == FQ_AGG_COUNT ? FQ_DT_UINT64 : (DataType)d.dtypes[a];
+            ls[a].bits.resize(at + (size_t)got);
+            ls[a].some.resize(at + (size_t)got, 1);
+        }
         if (got > 0) {
-            check_hip(hipMemcpyAsync(hk.data(), keys->ptr, (size_t)got * 8, hipMemcpyDeviceToHost, ctx.stream()),
+            check_hip(hipMemcpyAsync(keys.data() + at, kbuf->ptr, (size_t)got * 8, hipMemcpyDeviceToHost,
+                                     ctx.stream()),
                       "hipMemcpyAsync");
-            for (int a = 0; a < d.n_aggs; ++a)
-                check_hip(hipMemcpyAsync(hs[(size_t)a].data(), st[(size_t)a]->ptr, (size_t)got * 8,
-                                         hipMemcpyDeviceToHost, ctx.stream()),
+            for (size_t a = 0; a < nl; ++a)
+                check_hip(hipMemcpyAsync(ls[a].bits.data() + at, st[a]->ptr, (size_t)got * 8, hipMemcpyDeviceToHost,
+                                         ctx.stream()),
                           "hipMemcpyAsync");
             ctx.sync();
         }
-        for (int64_t g = 0; g < got; ++g) {
-            std::vector<DataValue> row;
-            row.push_back(DataValue::some(kdt, hk[(size_t)g]));
-            for (size_t a = 0; a < leaves.size(); ++a)
-                row.push_back(leaf_value(leaves[a]->op(), (DataType)d.dtypes[a], hs[a][(size_t)g]));
-            exchanged.push_back(std::move(row));
-        }
     }
-    for (auto &row : exchanged) {
-        if (row.size() != 1 + leaves.size()) throw_status(FQ_E_INVALID, "GROUP BY: malformed partial state row");
-        if (kdt == FQ_DT_NULL) kdt = row[0].dtype;
-        auto ok = order_key(row[0].bits);
-        auto it = host_groups.find(ok);
-        if (it == host_groups.end()) {
-            host_groups.emplace(ok, std::move(row));
-            continue;
-        }
-        for (size_t a = 0; a < leaves.size(); ++a) it->second[a + 1] = fold_leaf(leaves[a]->op(), it->second[a + 1], row[a + 1]);
+    // sort by key (Int64 numerically: the sign bit flipped orders it as
+    // unsigned), then fold each run of equal keys into its first row
+    const uint64_t flip = kdt == FQ_DT_INT64 ? (1ull << 63) : 0ull;
+    std::vector<std::pair<uint64_t, uint32_t>> order(keys.size());
+    for (size_t i = 0; i < keys.size(); ++i) order[i] = {keys[i] ^ flip, (uint32_t)i};
+    std::sort(order.begin(), order.end());
+    std::vector<uint32_t> rows;  // one source row per group, in key order
+    rows.reserve(order.size());
+    for (size_t i = 0; i < order.size();) {
+        const uint32_t r0 = order[i].second;
+        size_t j = i + 1;
+        for (; j < order.size() && order[j].first == order[i].first; ++j)
+            for (size_t a = 0; a < nl; ++a) ls[a].fold_into(leaves[a]->op(), r0, order[j].second);
+        rows.push_back(r0);
+        i = j;
     }
     DataBlock out;
     out.schema = schema_;
+    const size_t ng = rows.size();
     if (emit_states_) {
-        std::vector<DataValue> rows;
-        for (auto &kv : host_groups) rows.push_back(DataValue::make_struct(kv.second));
-        out.columns.push_back(Column::host_values(FQ_DT_NULL, std::move(rows)));
+        std::vector<DataValue> srows;
+        srows.reserve(ng);
+        for (uint32_t r : rows) {
+            std::vector<DataValue> row;
+            row.reserve(1 + nl);
+            row.push_back(DataValue::some(kdt, keys[r]));
+            for (size_t a = 0; a < nl; ++a) row.push_back(ls[a].value(r));
+            srows.push_back(DataValue::make_struct(std::move(row)));
+        }
+        out.columns.push_back(Column::host_values(FQ_DT_NULL, std::move(srows)));
         return std::make_unique<DataBlockStream>(std::vector<DataBlock>{out});
     }
-    // key column, then each aggregate expression evaluated from its leaves
+    // key column, then each aggregate expression evaluated from its leaves;
+    // an expression that IS one leaf (count(x), sum(x) ...) is that leaf's
+    // states as they stand (merge_result returns the state)
     std::vector<std::vector<DataValue>> cols(1 + funcs.size());
-    for (auto &kv : host_groups) {
-        const std::vector<DataValue> &row = kv.second;
-        cols[0].push_back(row[0]);
-        for (size_t a = 0; a < leaves.size(); ++a) leaves[a]->set_state(row[a + 1]);
-        for (size_t f = 0; f < funcs.size(); ++f) {
-            const DataValue v = funcs[f]->merge_result();
-            if (v.kind == DataValue::kNone) throw_internal("DataValue to array cannot be NONE NULL");
-            cols[f + 1].push_back(v);
+    for (auto &c : cols) c.reserve(ng);
+    for (uint32_t r : rows) cols[0].push_back(DataValue::some(kdt, keys[r]));
+    std::vector<int> direct(funcs.size(), -1);
+    bool any_tree = false;
+    for (size_t f = 0; f < funcs.size(); ++f) {
+        for (size_t a = 0; a < nl; ++a)
+            if (funcs[f].get() == static_cast<Function *>(leaves[a])) direct[f] = (int)a;
+        any_tree |= direct[f] < 0;
+    }
+    for (size_t f = 0; f < funcs.size(); ++f) {
+        if (direct[f] < 0) continue;
+        const FlatLeaf &L = ls[(size_t)direct[f]];
+        for (uint32_t r : rows) {
+            if (!L.some[r]) throw_internal("DataValue to array cannot be NONE NULL");
+            cols[f + 1].push_back(DataValue::some(L.dtype, L.bits[r]));
+        }
+    }
+    if (any_tree) {
+        for (uint32_t r : rows) {
+            for (size_t a = 0; a < nl; ++a) leaves[a]->set_state(ls[a].value(r));
+            for (size_t f = 0; f < funcs.size(); ++f) {
+                if (direct[f] >= 0) continue;
+                DataValue v = funcs[f]->merge_result();
+                if (v.kind == DataValue::kNone) throw_internal("DataValue to array cannot be NONE NULL");
+                cols[f + 1].push_back(std::move(v));
+            }
         }
     }
     for (size_t c = 0; c < cols.size(); ++c) {

@@ -113,7 +113,7 @@ class Result:
                     continue
                 cols.append(_column_values(ptr, c, nrow))
             self.columns = cols
-            self.rows = [tuple(col[r] for col in cols) for r in range(nrow)]
+            self.rows = list(zip(*cols)) if cols else [() for _ in range(nrow)]
             # what the reference's MySQL writer sends (mysql_stream.rs:21-84) is
             # read on first use (mysql_types / mysql_error), like the text form
             self._mysql = None
