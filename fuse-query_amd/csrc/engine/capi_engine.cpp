@@ -154,6 +154,11 @@ fq_status fq_engine_set_option(fq_engine *e, int32_t option, int64_t value) {
                     throw fq::FQException(FQ_E_INVALID, "FQ_OPT_CHUNK_ROWS must be a positive multiple of 10000");
                 e->ds->numbers()->set_chunk_rows((uint64_t)value);
                 break;
+            case FQ_OPT_GROUP_CHUNK_ROWS:
+                if (value < 64 || value % 64)
+                    throw fq::FQException(FQ_E_INVALID, "FQ_OPT_GROUP_CHUNK_ROWS must be a positive multiple of 64");
+                e->rt->group_chunk_rows.store(value);
+                break;
             default: throw fq::FQException(FQ_E_INVALID, "fq_engine_set_option: unknown option");
         }
     });

@@ -651,9 +651,16 @@ StreamRef GroupByPartialTransform::execute() {
                                         kc.expr.n_steps ? &kc.expr : nullptr, vals, ctx.stream()));
         }
         const int lp = shared_->log2_parts;
+        // radix-partitioned launches go over the block in chunks of
+        // FQ_OPT_GROUP_CHUNK_ROWS rows (a multiple of 64: bitmap predicates
+        // are offset by whole words): the partition workspace (~8 B per row)
+        // stays under 1 GB, which the device block cache keeps for the next
+        // query on this queue (a 10 GB one was mapped afresh per query:
+        // hipMallocAsync up to 540 ms, tools/batch_r02c.sh)
+        const int64_t chunk = lp > 0 ? std::min<int64_t>(c.len, ctx.rt->group_chunk_rows.load()) : c.len;
         std::shared_ptr<DeviceBuffer> ws;
         if (lp > 0) {
-            const size_t need = fq_group_partition_workspace_bytes(c.len, lp);
+            const size_t need = fq_group_partition_workspace_bytes(chunk, lp);
             std::lock_guard<std::mutex> lk(shared_->mu);
             auto &slot = shared_->part_ws[ctx.stream()];
             if (!slot || slot->bytes < need) slot = DeviceBuffer::alloc(need, ctx.stream());
@@ -662,11 +669,19 @@ StreamRef GroupByPartialTransform::execute() {
         {
             std::lock_guard<std::mutex> lk(*ctx.res->launch_mu);
             if (prof) check_hip(hipEventRecord(e0, ctx.stream()), "hipEventRecord");
-            if (lp > 0)
-                check_fq(fq_group_aggregate_partitioned(&shared_->desc, &c, has_pred ? fp.get() : nullptr,
-                                                        kc.expr.n_steps ? &kc.expr : nullptr, vals, lp, ws->ptr,
-                                                        ws->bytes, ctx.stream()));
-            else
+            if (lp > 0) {
+                fq_pred pc{};
+                if (has_pred) pc = *fp.get();
+                for (int64_t off = 0; off < c.len; off += chunk) {
+                    fq_col cc = c;
+                    cc.data = (char *)c.data + off * 8;
+                    cc.len = std::min(chunk, c.len - off);
+                    if (has_pred && pc.kind == FQ_PRED_BITMAP) pc.bitmap = fp.get()->bitmap + off / 64;
+                    check_fq(fq_group_aggregate_partitioned(&shared_->desc, &cc, has_pred ? &pc : nullptr,
+                                                            kc.expr.n_steps ? &kc.expr : nullptr, vals, lp, ws->ptr,
+                                                            ws->bytes, ctx.stream()));
+                }
+            } else
                 check_fq(fq_group_aggregate(&shared_->desc, &c, has_pred ? fp.get() : nullptr,
                                             kc.expr.n_steps ? &kc.expr : nullptr, vals, ctx.stream()));
             if (prof) check_hip(hipEventRecord(e1, ctx.stream()), "hipEventRecord");

@@ -106,10 +106,11 @@ struct GroupPartition {
     uint32_t *hist;   // [P][grid] rows per (bin, workgroup)
     uint64_t *off;    // [P][grid] their exclusive offsets
     uint64_t *bins;   // [P + 1] bin starts in vals
+    uint64_t *tot;    // [P] rows per bin (scratch of the scan)
     void *vals;       // the passing rows, grouped by bin
 };
 fq_status jit_groupby_partitioned(int32_t col_dtype, const GroupLaunch &G, const GroupPartition &X);
-// exclusive scan of X.hist into X.off and X.bins (one workgroup; fq_groupby.hip)
+// exclusive scan of X.hist into X.off and X.bins (two launches of P workgroups; fq_groupby.hip)
 fq_status launch_group_part_scan(const GroupPartition &X, hipStream_t stream);
 
 // One fq_filter_project / fq_predicate_bitmap call (fq_filter.hip ->

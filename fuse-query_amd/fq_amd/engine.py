@@ -9,6 +9,7 @@ Projection / Limit) on the gfx950 kernels.
         r.rows   -> [(1310651184, 9999999999, 0)]
 """
 import ctypes as C
+import gc
 
 import numpy as np
 
@@ -18,7 +19,7 @@ from .expr import from_bits
 
 P = C.POINTER
 
-OPT_WORKER_THREADS, OPT_MODULO, OPT_PROFILE, OPT_STREAMS, OPT_CHUNK_ROWS = 1, 2, 3, 4, 5
+OPT_WORKER_THREADS, OPT_MODULO, OPT_PROFILE, OPT_STREAMS, OPT_CHUNK_ROWS, OPT_GROUP_CHUNK_ROWS = 1, 2, 3, 4, 5, 6
 
 ENGINE_SYMBOLS = [
     "fq_engine_create", "fq_engine_destroy", "fq_engine_set_option", "fq_engine_materialize_numbers",
@@ -113,7 +114,16 @@ class Result:
                     continue
                 cols.append(_column_values(ptr, c, nrow))
             self.columns = cols
-            self.rows = list(zip(*cols)) if cols else [() for _ in range(nrow)]
+            # 1e5-row results: the cyclic GC would rescan the young tuples
+            # over and over while they are built (5x the build itself)
+            gc_was = gc.isenabled()
+            if nrow > 10000:
+                gc.disable()
+            try:
+                self.rows = list(zip(*cols)) if cols else [() for _ in range(nrow)]
+            finally:
+                if gc_was:
+                    gc.enable()
             # what the reference's MySQL writer sends (mysql_stream.rs:21-84) is
             # read on first use (mysql_types / mysql_error), like the text form
             self._mysql = None

@@ -46,6 +46,9 @@ typedef struct fq_result fq_result;
                                    resident (a multiple of 10,000; default 400,000,000 = 3.2 GB):
                                    aggregates over numbers_mt(1e12) stream through bounded HBM
                                    like the reference's 10,000-row blocks do through RAM */
+#define FQ_OPT_GROUP_CHUNK_ROWS 6 /* rows per radix-partitioned GROUP BY launch (a positive
+                                   multiple of 64; default 120,000,000: a ~0.96 GB partition
+                                   workspace, which the device block cache keeps per queue) */
 
 typedef struct fq_engine_stats {
     uint64_t scan_launches; /* fused aggregate scans launched                    */

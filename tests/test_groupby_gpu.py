@@ -406,3 +406,31 @@ def test_sql_high_cardinality_group_by_takes_the_partitioned_path(eng):
     # keys only, every key distinct
     r = eng.execute("SELECT number FROM system.numbers_mt(400000) GROUP BY number")
     assert r.rows == [(i,) for i in range(400000)]
+
+
+@pytest.mark.parametrize("chunk", [64 * 1001, 64 * 4096])
+def test_sql_partitioned_group_by_in_chunks(chunk):
+    # FQ_OPT_GROUP_CHUNK_ROWS: each partition's radix-partitioned launches go
+    # over slices of the block; results equal the unchunked path (and numpy)
+    from fq_amd._lib import FQError
+    from fq_amd.engine import OPT_GROUP_CHUNK_ROWS, Engine
+    total = 2_400_000
+    sql = ("SELECT number%%50000, count(number), max(number), sum(number), min(number+7) "
+           "FROM system.numbers_mt(%d) WHERE number%%3 < 2 GROUP BY number%%50000" % total)
+    with Engine() as e:
+        whole = e.execute(sql).rows
+    with Engine() as e:
+        e.set_option(OPT_GROUP_CHUNK_ROWS, chunk)
+        j0 = ops.jit_stats()["jit_launches"]
+        got = e.execute(sql).rows
+        assert ops.jit_stats()["jit_launches"] - j0 >= 3 * 8 * 2  # >= 2 chunks per partition
+        with pytest.raises(FQError):
+            e.set_option(OPT_GROUP_CHUNK_ROWS, 100)
+    assert got == whole
+    x = np.arange(total, dtype=np.uint64)
+    x = x[x % np.uint64(3) < 2]
+    exp = np_groupby(x % np.uint64(50000), [None, x, x, x + np.uint64(7)],
+                     [abi.AGG_COUNT, abi.AGG_MAX, abi.AGG_SUM, abi.AGG_MIN])
+    assert len(got) == len(exp)
+    for k, *v in got:
+        assert v == [int(t) for t in exp[k]]

@@ -23,24 +23,49 @@ assert hip.hipHostGetDevicePointer(C.byref(dptr), C.c_void_p(host_out.data_ptr()
 s = torch.cuda.current_stream()
 
 
+# events: 0 none, 1 torch (hipEventDefault), 2 hipEventDisableSystemFence,
+# 3 hipEventReleaseToDevice -- what a timing pair costs between two scans
+FLAGS = {2: 0x20000000, 3: 0x40000000}
+_pool = {k: [] for k in FLAGS}
+
+
+def hip_event(kind, i):
+    pool = _pool[kind]
+    while len(pool) <= i:
+        e = C.c_void_p()
+        assert hip.hipEventCreateWithFlags(C.byref(e), C.c_uint(FLAGS[kind])) == 0
+        pool.append(e)
+    return pool[i]
+
+
+def rec(kind, i):
+    e = hip_event(kind, i)
+    assert hip.hipEventRecord(e, C.c_void_p(s.cuda_stream)) == 0
+    return e
+
+
 def run(to_host, events):
     evs = []
     for i, c in enumerate(cols):
-        if events:
+        if events == 1:
             e0 = torch.cuda.Event(enable_timing=True)
             e0.record(s)
+        elif events > 1:
+            e0 = rec(events, 2 * i)
         out = (dptr.value + 48 * i) if to_host else (dev_out.data_ptr() + 48 * i)
         cc = c.col()
         check(lib.fq_aggregate(C.byref(cc), 10000, None, None, 0xF, C.c_void_p(out), ws.ptr, ws.nbytes,
                                C.c_void_p(s.cuda_stream)))
-        if events:
+        if events == 1:
             e1 = torch.cuda.Event(enable_timing=True)
             e1.record(s)
             evs.append((e0, e1))
+        elif events > 1:
+            evs.append((e0, rec(events, 2 * i + 1)))
 
 
 for to_host in (0, 1):
-    for events in (0, 1):
+    for events in (0, 1, 2, 3):
         for _ in range(2):
             run(to_host, events)
         torch.cuda.synchronize()

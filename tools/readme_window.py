@@ -14,6 +14,8 @@ SQLS = {
     "readme": "select (number+1) as c1, number/2 as c2 from system.numbers_mt(10000000000) where (c1+c2+1) < 100 limit 3",
     "filter_limit": "select number, number*3 from system.numbers_mt(10000000000) where number % 1000 = 999 limit 100",
     "c3": "SELECT sum(number)/count(number), max(number), min(number) FROM system.numbers_mt(10000000000)",
+    "g2": "SELECT number%100000, count(number), sum(number), max(number) FROM system.numbers_mt(10000000000) "
+          "GROUP BY number%100000",
 }
 sql = SQLS[sys.argv[1] if len(sys.argv) > 1 else "readme"]
 e = Engine(device=0)
