@@ -725,6 +725,20 @@ int lds_slots(int n_aggs, int budget) {
     return s;
 }
 
+// Dense keys: a UInt64 key whose last step is `% d` by a constant d <= S
+// lies in [0, d), so its LDS slot IS the key -- no hash, no probe, no claim
+// (1 for the shape; d goes with the launch, so d > S takes the hashed shape)
+int dense_of(const GroupLaunch &G) {
+    if (G.key_dtype != FQ_DT_UINT64 || G.key.n < 1) return 0;
+    const KStep &st = G.key.s[G.key.n - 1];
+    if (st.operand != FQ_OPERAND_CONST || st.reversed || st.dtype != FQ_DT_UINT64) return 0;
+    uint64_t d = 0;
+    if (st.code == K_AND_U) d = st.magic + 1;
+    else if (st.code == K_MODM32_U || st.code == K_MODM_U) d = st.c;
+    else return 0;
+    return (d >= 1 && d <= (uint64_t)lds_slots(G.n_aggs, G.lds_bytes)) ? 1 : 0;
+}
+
 struct HostGroupConsts {
     uint64_t rhs;
     HostStep p[kSteps], k[kSteps], v[FQ_MAX_GROUP_AGGS][kSteps];
@@ -763,6 +777,7 @@ std::string group_shape_key(const GroupLaunch &G, int32_t tin, int dev) {
     put_pred_key(G.pred, k);
     prog(G.key);
     put(G.lds_bytes);
+    put(dense_of(G));
     put(G.threads);
     put(G.rowmap);
     put(G.n_aggs);
@@ -1008,6 +1023,13 @@ bool gen_groupby_source(const GroupLaunch &G, int32_t tin, Gen &g, std::string &
     src += "#define BT " + std::to_string(G.threads) + "\n#define ROWMAP " + std::to_string(G.rowmap) + "\n";
     src += "#define LDS_LOCAL " + std::to_string(group_lds_local()) + "\n";
     src += "#define GKEY_PLAIN " + std::to_string(group_key_plain()) + "\n";
+    // dense keys (see dense_of): a COUNT state doubles as the slot's
+    // occupancy, else the key is stored (a plain write, every writer writes
+    // the same value)
+    int dense_cnt = -1;
+    for (int a = 0; a < NA && dense_cnt < 0; ++a)
+        if (G.kinds[a] == FQ_AGG_COUNT) dense_cnt = a;
+    src += "#define DENSE " + std::to_string(dense_of(G)) + "\n#define DENSE_CNT " + std::to_string(dense_cnt) + "\n";
     src += "#define PMAX 16\n#define EMPTY 0xffffffffffffffffull\n#define NA " + std::to_string(NA) + "\n#define S " +
            std::to_string(S) + "\n#define LOG2S " + std::to_string(__builtin_ctz((unsigned)S)) + "\n";
     src += R"(
@@ -1127,18 +1149,25 @@ __device__ long long ginsert(const Tab &t, u64 k) {
     for (int a = 0; a < NA; ++a)
         if (G.kinds[a] != FQ_AGG_COUNT)
             row += "    r.v" + std::to_string(a) + " = fq_val" + std::to_string(a) + "(x, c, flags, r.pass);\n";
-    row += "    r.h = (int)(lds_hash(r.k) & (u32)(S - 1));\n}\n";
+    row += "#if DENSE\n    r.h = (int)r.k;\n#else\n    r.h = (int)(lds_hash(r.k) & (u32)(S - 1));\n#endif\n}\n";
     // rows of the partitioned buffer already passed the predicate
     row += "__device__ __forceinline__ void fq_prep_all(TIn x, u32 live, const Consts &c, u32 &flags, Row &r) {\n"
            "    r.pass = live;\n    r.k = fq_key(x, c, flags, live);\n";
     for (int a = 0; a < NA; ++a)
         if (G.kinds[a] != FQ_AGG_COUNT)
             row += "    r.v" + std::to_string(a) + " = fq_val" + std::to_string(a) + "(x, c, flags, live);\n";
-    row += "    r.h = (int)(lds_hash(r.k) & (u32)(S - 1));\n}\n";
+    row += "#if DENSE\n    r.h = (int)r.k;\n#else\n    r.h = (int)(lds_hash(r.k) & (u32)(S - 1));\n#endif\n}\n";
     row += "__device__ __forceinline__ u64 fq_first(const Row &r, const u64 *s_keys) {\n"
-           "    return (r.pass && r.k != EMPTY) ? s_keys[r.h] : EMPTY;\n}\n";
+           "#if DENSE\n    (void)r; (void)s_keys;\n    return EMPTY;\n#else\n"
+           "    return (r.pass && r.k != EMPTY) ? s_keys[r.h] : EMPTY;\n#endif\n}\n";
     row += "__device__ __forceinline__ void fq_commit(const Row &r, u64 cur0, const Tab &t, u64 *s_keys,\n"
-           "    u64 (*s_st)[S], int *s_bypass) {\n    if (!r.pass) return;\n    const u64 k = r.k;\n";
+           "    u64 (*s_st)[S], int *s_bypass) {\n    if (!r.pass) return;\n";
+    row += "#if DENSE\n    (void)cur0; (void)t; (void)s_bypass;\n    const int slot = r.h;\n#if DENSE_CNT < 0\n"
+           "    s_keys[slot] = r.k;\n#endif\n";
+    for (int a = 0; a < NA; ++a)
+        row += "    " + state_update(G.kinds[a], G.dtypes[a], "&s_st[" + std::to_string(a) + "][slot]",
+                                     "r.v" + std::to_string(a)) + "\n";
+    row += "#else\n    const u64 k = r.k;\n";
     row += R"(    int slot = -1;
     if (k != EMPTY) {
         // Once the LDS table is 3/4 full (more groups than it holds) it stops
@@ -1174,7 +1203,7 @@ __device__ long long ginsert(const Tab &t, u64 k) {
     for (int a = 0; a < NA; ++a)
         row += "            " + state_update(G.kinds[a], G.dtypes[a], "&t.st[" + std::to_string(a) + "][gs]",
                                              "r.v" + std::to_string(a)) + "\n";
-    row += "        }\n    }\n}\n";
+    row += "        }\n    }\n#endif\n}\n";
     row += "__device__ __forceinline__ void fq_row(TIn x, long long idx, const Consts &c, const Tab &t,\n"
            "    const u64 *__restrict__ bitmap, u64 *s_keys, u64 (*s_st)[S], u32 &flags, int *s_bypass, u32 P,\n"
            "    u32 part) {\n"
@@ -1193,8 +1222,13 @@ __device__ long long ginsert(const Tab &t, u64 k) {
     src += R"(// this workgroup's groups into the HBM table
 __device__ __forceinline__ void fq_flush(const Tab &tr, const u64 *s_keys, u64 (*s_st)[S]) {
     for (int i = threadIdx.x; i < S; i += BT) {
+#if DENSE && DENSE_CNT >= 0
+        if (s_st[DENSE_CNT][i] == 0) continue;
+        const u64 k = (u64)i;
+#else
         const u64 k = s_keys[i];
         if (k == EMPTY) continue;
+#endif
         const long long gs = ginsert(tr, k);
         if (gs < 0) continue;
 )";
@@ -1235,7 +1269,7 @@ fq_jit_groupby(const TIn *__restrict__ col, long long n, long long head, const u
     // (only past the LDS saturation point, 3/4 of S; beyond PMAX partitions
     // the rows are cheaper to send to the HBM table than to re-read)
     u32 P = 1;
-    if (seen > (u32)(S * 3 / 4))
+    if (!DENSE && seen > (u32)(S * 3 / 4))  // (dense keys never outgrow the table)
         while (P <= PMAX && P * (u32)(S / 2) < seen) P <<= 1;
     if (P > PMAX || gridDim.x % P) P = 1;
     const u32 part = blockIdx.x & (P - 1);

@@ -103,6 +103,10 @@ GROUP_SHAPES = [
     ("identity_key", U64, [], [(abi.AGG_COUNT, U64, None)], U64),
     ("eight_aggs", U64, [("/", 7)], [(abi.AGG_COUNT, U64, None)] * 8, U64),
     ("f64_column", F64, None, [(abi.AGG_SUM, F64, None)], None),
+    # dense keys (slot = key): with a COUNT as occupancy, without (key stored)
+    ("dense_pow2_no_count", U64, [("*", 3), ("%", 16)], [(abi.AGG_SUM, U64, None), (abi.AGG_MIN, U64, None)], U64),
+    ("dense_magic_count", U64, [("%", 4000)], [(abi.AGG_MAX, U64, None), (abi.AGG_COUNT, U64, None)], U64),
+    ("dense_too_wide", U64, [("%", 100000)], [(abi.AGG_COUNT, U64, None)], U64),
 ]
 
 
