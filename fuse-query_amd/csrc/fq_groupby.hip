@@ -286,6 +286,15 @@ static size_t part_ws_bytes(int64_t len, int log2p, GroupPartition *X, void *ws)
     return h + o + b + align256((size_t)(len > 0 ? len : 0) * 8);
 }
 
+// tuning knobs of the GROUP BY launch (tools/groupby_sweep.py); the
+// defaults are the measured best, out-of-range values fall back to them
+static int tune_env(const char *name, int def, int lo, int hi) {
+    const char *e = getenv(name);
+    if (!e) return def;
+    const int v = atoi(e);
+    return (v >= lo && v <= hi) ? v : def;
+}
+
 // validation + lowering shared by both aggregate entry points
 static fq_status prepare_group(const fq_group_table *t, const fq_col *col, const fq_pred *pred,
                                const fq_expr *key_expr, const fq_expr *values, void *stream, GroupLaunch &G) {
@@ -338,13 +347,13 @@ static fq_status prepare_group(const fq_group_table *t, const fq_col *col, const
     // share one table (tools/groupby_sweep.py: 256-thread workgroups with a
     // 64 KB table each, 2 per CU, ran 1,000 groups x 3 aggregates in 2.98 ms
     // against 2.25 ms here, and the table holds twice the groups)
-    G.lds_bytes = 128 * 1024;
-    G.threads = 1024;
-    G.rowmap = 1;
+    G.lds_bytes = tune_env("FQ_GROUP_LDS_KB", 128, 8, 160) * 1024;
+    G.threads = tune_env("FQ_GROUP_THREADS", 1024, 256, 1024) & ~255;
+    G.rowmap = tune_env("FQ_GROUP_ROWMAP", 1, 0, 1);
     const int64_t nvec = (G.n - G.head) / 2;
     int64_t grid = (nvec + 4 * G.threads - 1) / (4 * G.threads);
     if (grid < 1) grid = 1;
-    const int64_t cap = (int64_t)fqc::device_cu_count();
+    const int64_t cap = (int64_t)fqc::device_cu_count() * tune_env("FQ_GROUP_WG_PER_CU", 1, 1, 8);
     G.grid = (int)(grid < cap ? grid : cap);
     return FQ_OK;
 }
