@@ -526,6 +526,13 @@ int64_t next_pow2(int64_t v) {
 
 GroupPlan plan_group_by(const fq_group_table &d, const fq_col &c, const fq_pred *pred, const fq_expr *key,
                         ExecCtx &ctx) {
+    // dense keys (`key % d` that the kernel's LDS table indexes directly):
+    // at most d groups, never the partitioned path, no sample needed
+    if (const int64_t dk = key ? fq_group_dense_keys(c.dtype, key, d.n_aggs) : 0) {
+        GroupPlan p;
+        p.capacity = next_pow2(std::max<int64_t>(4096, 2 * dk));
+        return p;
+    }
     const int64_t rows = std::min<int64_t>(c.len, kGroupSampleRows);
     fq_group_table t{};
     t.capacity = next_pow2(2 * rows);

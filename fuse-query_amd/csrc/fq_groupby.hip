@@ -295,6 +295,8 @@ static int tune_env(const char *name, int def, int lo, int hi) {
     return (v >= lo && v <= hi) ? v : def;
 }
 
+static int group_lds_bytes() { return tune_env("FQ_GROUP_LDS_KB", 128, 8, 160) * 1024; }
+
 // validation + lowering shared by both aggregate entry points
 static fq_status prepare_group(const fq_group_table *t, const fq_col *col, const fq_pred *pred,
                                const fq_expr *key_expr, const fq_expr *values, void *stream, GroupLaunch &G) {
@@ -347,7 +349,7 @@ static fq_status prepare_group(const fq_group_table *t, const fq_col *col, const
     // share one table (tools/groupby_sweep.py: 256-thread workgroups with a
     // 64 KB table each, 2 per CU, ran 1,000 groups x 3 aggregates in 2.98 ms
     // against 2.25 ms here, and the table holds twice the groups)
-    G.lds_bytes = tune_env("FQ_GROUP_LDS_KB", 128, 8, 160) * 1024;
+    G.lds_bytes = group_lds_bytes();
     G.threads = tune_env("FQ_GROUP_THREADS", 1024, 256, 1024) & ~255;
     G.rowmap = tune_env("FQ_GROUP_ROWMAP", 1, 0, 1);
     const int64_t nvec = (G.n - G.head) / 2;
@@ -395,6 +397,15 @@ fq_status fq_group_aggregate(const fq_group_table *t, const fq_col *col, const f
     fq_status s = prepare_group(t, col, pred, key_expr, values, stream, G);
     if (s != FQ_OK) return s;
     return jit_groupby(col->dtype, G);
+}
+
+int64_t fq_group_dense_keys(int32_t col_dtype, const fq_expr *key_expr, int32_t n_aggs) {
+    using namespace fqk;
+    if (!key_expr || key_expr->n_steps < 1 || n_aggs < 1 || n_aggs > FQ_MAX_GROUP_AGGS) return 0;
+    KProg k;
+    int32_t kdt = col_dtype;
+    if (lower_expr(*key_expr, col_dtype, k, kdt) != FQ_OK) return 0;
+    return group_dense_bound(k, kdt, n_aggs, group_lds_bytes());
 }
 
 size_t fq_group_partition_workspace_bytes(int64_t len, int32_t log2_parts) {

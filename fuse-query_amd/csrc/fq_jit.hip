@@ -728,15 +728,22 @@ int lds_slots(int n_aggs, int budget) {
 // Dense keys: a UInt64 key whose last step is `% d` by a constant d <= S
 // lies in [0, d), so its LDS slot IS the key -- no hash, no probe, no claim
 // (1 for the shape; d goes with the launch, so d > S takes the hashed shape)
-int dense_of(const GroupLaunch &G) {
-    if (G.key_dtype != FQ_DT_UINT64 || G.key.n < 1) return 0;
-    const KStep &st = G.key.s[G.key.n - 1];
+}  // namespace
+
+int64_t group_dense_bound(const KProg &key, int32_t key_dtype, int n_aggs, int lds_bytes) {
+    if (key_dtype != FQ_DT_UINT64 || key.n < 1) return 0;
+    const KStep &st = key.s[key.n - 1];
     if (st.operand != FQ_OPERAND_CONST || st.reversed || st.dtype != FQ_DT_UINT64) return 0;
     uint64_t d = 0;
     if (st.code == K_AND_U) d = st.magic + 1;
     else if (st.code == K_MODM32_U || st.code == K_MODM_U) d = st.c;
     else return 0;
-    return (d >= 1 && d <= (uint64_t)lds_slots(G.n_aggs, G.lds_bytes)) ? 1 : 0;
+    return (d >= 1 && d <= (uint64_t)lds_slots(n_aggs, lds_bytes)) ? (int64_t)d : 0;
+}
+
+namespace {
+int dense_of(const GroupLaunch &G) {
+    return group_dense_bound(G.key, G.key_dtype, G.n_aggs, G.lds_bytes) > 0 ? 1 : 0;
 }
 
 struct HostGroupConsts {

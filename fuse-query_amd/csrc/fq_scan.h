@@ -92,6 +92,10 @@ struct GroupLaunch {
     hipStream_t stream;
 };
 
+// Keys of a dense GROUP BY key (a UInt64 key ending in `% d`, d <= the LDS
+// slots for n_aggs states in lds_bytes): d, else 0 (fq_jit.hip)
+int64_t group_dense_bound(const KProg &key, int32_t key_dtype, int n_aggs, int lds_bytes);
+
 // Launches the hipRTC-specialised group-by kernel for G.
 fq_status jit_groupby(int32_t col_dtype, const GroupLaunch &G);
 

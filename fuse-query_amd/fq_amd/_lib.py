@@ -21,6 +21,7 @@ GPU_SYMBOLS = [
     "fq_group_table_bytes", "fq_group_table_init", "fq_group_aggregate", "fq_group_table_count",
     "fq_group_table_extract", "fq_logic", "fq_filter_project_workspace_bytes", "fq_filter_project",
     "fq_predicate_bitmap", "fq_group_partition_workspace_bytes", "fq_group_aggregate_partitioned",
+    "fq_group_dense_keys",
 ]
 
 
@@ -83,6 +84,7 @@ _protos = {
     "fq_group_aggregate": (C.c_int32, [P(abi.fq_group_table), P(abi.fq_col), P(abi.fq_pred), P(abi.fq_expr),
                                        P(abi.fq_expr), vp]),
     "fq_group_partition_workspace_bytes": (C.c_size_t, [C.c_int64, C.c_int32]),
+    "fq_group_dense_keys": (C.c_int64, [C.c_int32, P(abi.fq_expr), C.c_int32]),
     "fq_group_aggregate_partitioned": (C.c_int32, [P(abi.fq_group_table), P(abi.fq_col), P(abi.fq_pred),
                                                    P(abi.fq_expr), P(abi.fq_expr), C.c_int32, vp, C.c_size_t, vp]),
     "fq_group_table_count": (C.c_int32, [P(abi.fq_group_table), P(C.c_int64), vp]),

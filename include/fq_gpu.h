@@ -387,6 +387,11 @@ size_t fq_group_partition_workspace_bytes(int64_t len, int32_t log2_parts);
 fq_status fq_group_aggregate_partitioned(const fq_group_table *t, const fq_col *col, const fq_pred *pred,
                                          const fq_expr *key_expr, const fq_expr *values, int32_t log2_parts,
                                          void *d_ws, size_t ws_bytes, void *stream);
+/* Dense keys: when key_expr over a column of col_dtype is a UInt64 key
+ * ending in `% d` by a constant and d fits the kernel's LDS table for n_aggs
+ * states, the kernel indexes that table by the key itself (no hashing, never
+ * saturated) and the query has at most d groups: returns d, else 0. */
+int64_t fq_group_dense_keys(int32_t col_dtype, const fq_expr *key_expr, int32_t n_aggs);
 /* Number of groups (synchronises stream); FQ_E_TABLE_FULL if any insert
  * found no free slot, FQ_E_DIVIDE_BY_ZERO / FQ_E_UNSUPPORTED for the flags
  * fq_aggregate reports. */

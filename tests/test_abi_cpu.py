@@ -104,3 +104,23 @@ def test_no_gpu_calls_fail_loudly_without_device():
     from fq_amd._lib import FQError
     with pytest.raises(FQError):
         ops.require_gpu()
+
+
+def test_group_dense_keys_host():
+    # UInt64 keys ending in `% d` with d within the LDS table: the kernel
+    # indexes its table by key (host-only lowering, no device needed)
+    from fq_amd.expr import chain
+    U = abi.DT_UINT64
+
+    def dense(steps, n_aggs=3, dt=U):
+        key, _ = chain(dt, steps)
+        return lib.fq_group_dense_keys(dt, C.byref(key), n_aggs)
+
+    assert dense([("%", 1000)]) == 1000
+    assert dense([("*", 3), ("%", 16)]) == 16          # power of two: an AND
+    assert dense([("%", 8)], n_aggs=8) == 8
+    assert dense([("%", 100000)]) == 0                 # more keys than LDS slots
+    assert dense([("%", 1000), ("+", 1)]) == 0         # not the last step
+    assert dense([("/", 1000)]) == 0
+    assert dense([("-", (5, "Int64")), ("%", (10, "Int64"))], dt=U) == 0  # Int64 key
+    assert lib.fq_group_dense_keys(U, None, 3) == 0
