@@ -9,6 +9,8 @@ operator, expected outputs / error texts) from its Rust test sources:
   src/datavalues/data_value_aggregate_test.rs    scalar state merges
   src/datavalues/data_value_arithmetic_test.rs   scalar add
   src/datavalues/data_array_logic_test.rs        and / or over Boolean arrays
+  src/functions/function_arithmetic_test.rs      ArithmeticFunction over a block's fields
+  src/functions/function_comparison_test.rs      ComparisonFunction over a block's fields
 
 Only literal values are read (the XArray::from(vec![...]) and
 DataValue::X(Some(..)) literals of each table row); nothing is executed.
@@ -184,6 +186,35 @@ def tests_in(path, struct):
     return out
 
 
+def function_tests(path, fn):
+    """Function-level tables (function_arithmetic_test.rs, function_comparison_test.rs):
+    the block's columns (named by the schema order a, b, c), the display
+    (which names the two argument fields), the expected array or error."""
+    src = open(os.path.join(REF, path)).read()
+    fm = re.search(r"fn %s\(\)" % fn, src)
+    body_fn = src[fm.end():]
+    out = []
+    for m in re.finditer(r"\bTest \{", body_fn):
+        if body_fn[m.start() - 7:m.start()].strip().startswith("struct"):
+            continue
+        body, _ = block(body_fn, m.end() - 1)
+        if "name:" not in body:
+            continue
+        line = src[:fm.end()].count("\n") + body_fn[:m.start()].count("\n") + 1
+        t = {"fn": fn, "line": line, "name": json.loads(field(body, "name")[1]),
+             "op": OPS[field(body, "op")[1].split("::")[-1]],
+             "display": json.loads(field(body, "display")[1]),
+             "nullable": field(body, "nullable")[1] == "true",
+             "error": json.loads(field(body, "error")[1])}
+        bi = body.index("DataBlock::create(")
+        inner, _ = block(body, bi + len("DataBlock::create"))
+        cols = split_top(inner)[1]
+        t["columns"] = [literal(x) for x in split_top(block(cols, cols.index("["))[0])]
+        t["expect"] = literal(field(body, "expect")[1])
+        out.append(t)
+    return out
+
+
 def main():
     data = {
         "generator": "tests/golden/make_golden.py (parses the literal tables of the reference's tests)",
@@ -194,6 +225,10 @@ def main():
         "value_aggregate": tests_in("src/datavalues/data_value_aggregate_test.rs", "ScalarTest"),
         "value_arithmetic": tests_in("src/datavalues/data_value_arithmetic_test.rs", "ScalarTest"),
         "array_logic": tests_in("src/datavalues/data_array_logic_test.rs", "ArrayTest"),
+        "function_arithmetic": function_tests("src/functions/function_arithmetic_test.rs",
+                                              "test_arithmetic_function"),
+        "function_comparison": function_tests("src/functions/function_comparison_test.rs",
+                                              "test_comparison_function"),
     }
     for k, v in data.items():
         if isinstance(v, list):

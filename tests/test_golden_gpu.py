@@ -152,3 +152,18 @@ def test_logic_lengths(n):
     words = ops.logic("or", A, B).buf[: ((n + 63) // 64) * 8].cpu().numpy().view(np.uint64)
     if n % 64:
         assert int(words[-1]) >> (n % 64) == 0  # bits past len cleared
+
+
+FUNCTION_TABLES = GOLDEN["function_arithmetic"] + GOLDEN["function_comparison"]
+
+
+@pytest.mark.parametrize("t", FUNCTION_TABLES, ids=ids(FUNCTION_TABLES))
+def test_golden_function_tables_on_gpu(t):
+    # function_arithmetic_test.rs / function_comparison_test.rs: the display
+    # names the two fields of the block (schema order a, b, c); the product
+    # kernel over those device columns gives the expected array and type
+    lhs, op, rhs = t["display"].split(" ")
+    cols = {n: column(c) for n, c in zip("abc", t["columns"])}
+    got = ops.compare(op, cols[lhs], cols[rhs]) if op in ("=", "<", "<=", ">", ">=") else \
+        ops.arith(op, cols[lhs], cols[rhs])
+    assert same(got, t["expect"]), (got.to_numpy(), t["expect"])

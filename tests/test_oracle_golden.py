@@ -131,7 +131,30 @@ def test_function_logic_display_and_eval():
 def test_golden_fixture_covers_all_tables():
     n = {k: len(v) for k, v in GOLDEN.items() if isinstance(v, list)}
     assert n == {"array_arithmetic": 12, "array_comparison": 17, "array_aggregate": 3,
-                 "value_aggregate": 3, "value_arithmetic": 1, "array_logic": 2}
+                 "value_aggregate": 3, "value_arithmetic": 1, "array_logic": 2,
+                 "function_arithmetic": 5, "function_comparison": 1}
+
+
+FUNCTION_TABLES = GOLDEN["function_arithmetic"] + GOLDEN["function_comparison"]
+
+
+def function_block(t):
+    """The table's block: columns a, b, c in schema order (the arrays as the
+    test builds them, whatever the schema's declared types)."""
+    return R.Block({n: lit(c) for n, c in zip("abc", t["columns"])})
+
+
+@pytest.mark.parametrize("t", FUNCTION_TABLES, ids=ids(FUNCTION_TABLES))
+def test_golden_function_tables(t):
+    # function_arithmetic_test.rs:28-160 / function_comparison_test.rs:25-85:
+    # Function over two fields -> display, nullable, eval = expect
+    lhs, op, rhs = t["display"].split(" ")
+    assert op == t["op"]
+    f = R.to_function(R.E_bin(op, R.E_field(lhs), R.E_field(rhs)))
+    assert f.display() == t["display"]
+    assert t["nullable"] is False and t["error"] == ""
+    got = f.eval(function_block(t))
+    assert same_array(got, t["expect"]), (got.to_list(), t["expect"])
 
 
 # ---- function_aggregator_test.rs:5-192 (partial/merge protocol) -----------
