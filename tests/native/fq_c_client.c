@@ -1,0 +1,115 @@
+/* A plain C host of the drop-in boundary: what the Rust FFI of INTEGRATION.md
+ * does, without Python or torch in the process.  Links libfq_amd.so and the
+ * HIP runtime only (tests/native/Makefile; tests/test_c_client_gpu.py runs it
+ * on the GPU box).
+ *
+ *  1. kernel ABI: hipMalloc a numbers_mt partition, fq_fill_numbers_u64
+ *     (NumbersStream::poll_next, numbers_stream.rs:65-83), one fused
+ *     fq_aggregate (AggregatorFunction::accumulate for sum/count/max/min,
+ *     function_aggregator.rs:57-100) -> fq_agg_state, checked against the
+ *     closed forms of begin..begin+n-1;
+ *  2. error texts through fq_last_error (a NULL column);
+ *  3. engine ABI: fq_engine_create -> materialise numbers_mt(N) -> the C3
+ *     statement through fq_engine_execute -> fq_result values, checked
+ *     against the closed forms.
+ * Prints one "OK ..." line per check; exits non-zero on the first failure. */
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <hip/hip_runtime_api.h>
+
+#include "fq_engine.h"
+#include "fq_gpu.h"
+
+#define CHECK(cond, ...)                           \
+    do {                                           \
+        if (!(cond)) {                             \
+            fprintf(stderr, "FAIL: " __VA_ARGS__); \
+            fprintf(stderr, "\n");                 \
+            exit(1);                               \
+        }                                          \
+    } while (0)
+
+static void kernel_abi(uint64_t begin, uint64_t n) {
+    hipStream_t st;
+    CHECK(hipStreamCreate(&st) == hipSuccess, "hipStreamCreate");
+    uint64_t *col = NULL;
+    fq_agg_state *d_state = NULL;
+    void *ws = NULL;
+    const size_t ws_bytes = fq_aggregate_workspace_bytes((int64_t)n);
+    CHECK(hipMalloc((void **)&col, n * 8) == hipSuccess, "hipMalloc column");
+    CHECK(hipMalloc((void **)&d_state, sizeof(fq_agg_state)) == hipSuccess, "hipMalloc state");
+    CHECK(hipMalloc(&ws, ws_bytes) == hipSuccess, "hipMalloc workspace");
+    CHECK(fq_fill_numbers_u64(col, begin, n, st) == FQ_OK, "fill: %s", fq_last_error());
+    fq_col c = {col, (int64_t)n, FQ_DT_UINT64, 0};
+    const uint32_t mask = FQ_AGG_SUM | FQ_AGG_COUNT | FQ_AGG_MAX | FQ_AGG_MIN;
+    CHECK(fq_aggregate(&c, 10000, NULL, NULL, mask, d_state, ws, ws_bytes, st) == FQ_OK, "aggregate: %s",
+          fq_last_error());
+    fq_agg_state s;
+    CHECK(hipMemcpyAsync(&s, d_state, sizeof s, hipMemcpyDeviceToHost, st) == hipSuccess, "copy state");
+    CHECK(hipStreamSynchronize(st) == hipSuccess, "sync");
+    /* sum of begin .. begin+n-1, wrapping mod 2^64 */
+    const unsigned __int128 last = (unsigned __int128)begin + n - 1;
+    const uint64_t sum = (uint64_t)(((unsigned __int128)begin + last) * n / 2);
+    CHECK(s.sum == sum && s.count == n && s.max == begin + n - 1 && s.min == begin,
+          "state %llu/%llu/%llu/%llu", (unsigned long long)s.sum, (unsigned long long)s.count,
+          (unsigned long long)s.max, (unsigned long long)s.min);
+    printf("OK kernel abi: fq_fill_numbers_u64 + fq_aggregate over %llu rows from %llu: sum %llu count %llu "
+           "max %llu min %llu\n",
+           (unsigned long long)n, (unsigned long long)begin, (unsigned long long)s.sum, (unsigned long long)s.count,
+           (unsigned long long)s.max, (unsigned long long)s.min);
+    /* error path: a NULL column is rejected with a message */
+    CHECK(fq_aggregate(NULL, 10000, NULL, NULL, mask, d_state, ws, ws_bytes, st) != FQ_OK &&
+              strlen(fq_last_error()) > 0,
+          "NULL column accepted");
+    printf("OK error text: %s\n", fq_last_error());
+    (void)hipFree(ws);
+    (void)hipFree(d_state);
+    (void)hipFree(col);
+    (void)hipStreamDestroy(st);
+}
+
+static uint64_t value_u64(const fq_result *r, int32_t col) {
+    fq_value v;
+    CHECK(fq_result_value(r, 0, col, &v) == FQ_OK && v.is_some && v.dtype == FQ_DT_UINT64, "result value %d", col);
+    return v.bits;
+}
+
+static void engine_abi(uint64_t total) {
+    fq_engine *e = NULL;
+    CHECK(fq_engine_create(0, &e) == FQ_OK, "engine: %s", fq_last_error());
+    CHECK(fq_engine_materialize_numbers(e, total, 0, 1) == FQ_OK, "materialise: %s", fq_last_error());
+    char sql[256];
+    snprintf(sql, sizeof sql,
+             "SELECT sum(number)/count(number), max(number), min(number) FROM system.numbers_mt(%llu)",
+             (unsigned long long)total);
+    fq_result *r = NULL;
+    CHECK(fq_engine_execute(e, sql, &r) == FQ_OK, "execute: %s", fq_last_error());
+    CHECK(fq_result_num_rows(r) == 1 && fq_result_num_columns(r) == 3, "result shape");
+    const uint64_t sum = (uint64_t)((unsigned __int128)total * (total - 1) / 2);
+    const uint64_t avg = value_u64(r, 0), mx = value_u64(r, 1), mn = value_u64(r, 2);
+    CHECK(avg == sum / total && mx == total - 1 && mn == 0, "C3 = %llu %llu %llu", (unsigned long long)avg,
+          (unsigned long long)mx, (unsigned long long)mn);
+    printf("OK engine abi: %s -> [%s = %llu, %s = %llu, %s = %llu]\n", sql, fq_result_column_name(r, 0),
+           (unsigned long long)avg, fq_result_column_name(r, 1), (unsigned long long)mx,
+           fq_result_column_name(r, 2), (unsigned long long)mn);
+    fq_result_free(r);
+    /* the reference's error for an unknown function, through the same ABI */
+    CHECK(fq_engine_execute(e, "SELECT foo(number) FROM system.numbers_mt(10)", &r) != FQ_OK, "unknown function");
+    printf("OK engine error: %s\n", fq_last_error());
+    fq_engine_destroy(e);
+}
+
+int main(int argc, char **argv) {
+    const uint64_t n = argc > 1 ? strtoull(argv[1], NULL, 10) : 100000003ull;
+    const uint64_t total = argc > 2 ? strtoull(argv[2], NULL, 10) : 1000000000ull;
+    int32_t devices = 0;
+    CHECK(fq_abi_version() > 0 && fq_device_count(&devices) == FQ_OK && devices > 0, "abi version / devices: %s",
+          fq_last_error());
+    printf("OK abi version %d, %d device(s)\n", fq_abi_version(), devices);
+    kernel_abi(1250000000ull, n);
+    engine_abi(total);
+    return 0;
+}
