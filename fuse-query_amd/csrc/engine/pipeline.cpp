@@ -512,6 +512,7 @@ struct FlatLeaf {
 // twice the expected groups in slots (a TABLE_FULL re-run grows it 16x).
 namespace {
 constexpr int64_t kGroupSampleRows = 1 << 21;
+constexpr int64_t kGroupMinSlots = 1 << 16;
 
 struct GroupPlan {
     int64_t capacity = 4096;
@@ -525,7 +526,7 @@ int64_t next_pow2(int64_t v) {
 }
 
 GroupPlan plan_group_by(const fq_group_table &d, const fq_col &c, const fq_pred *pred, const fq_expr *key,
-                        ExecCtx &ctx) {
+                        int64_t blocks, ExecCtx &ctx) {
     // dense keys (`key % d` that the kernel's LDS table indexes directly):
     // at most d groups, never the partitioned path, no sample needed
     if (const int64_t dk = key ? fq_group_dense_keys(c.dtype, key, d.n_aggs) : 0) {
@@ -551,10 +552,17 @@ GroupPlan plan_group_by(const fq_group_table &d, const fq_col &c, const fq_pred 
     }
     int64_t g = 0;
     check_fq(fq_group_table_count(&t, &g, ctx.stream()));  // synchronises
+    const bool repeats = 2 * g <= rows;
     const int64_t per_launch =
-        2 * g <= rows ? 2 * g : (int64_t)((double)g * (double)c.len / (double)std::max<int64_t>(rows, 1));
+        repeats ? 2 * g : (int64_t)((double)g * (double)c.len / (double)std::max<int64_t>(rows, 1));
     GroupPlan p;
-    p.capacity = next_pow2(std::max<int64_t>(4096, 2 * per_launch));
+    // at least 2^16 slots (~32 MB with 3 states and 16 replicas; init and
+    // extract stay in the tens of microseconds): clustered keys -- each
+    // partition its own key range, number / 1000000 -- show few groups in
+    // the sample but many per query, and a full table costs a re-run
+    // keys that keep coming (mostly distinct in the sample, GROUP BY number)
+    // differ from block to block as well: the table holds every block's
+    p.capacity = next_pow2(std::max<int64_t>(kGroupMinSlots, 2 * per_launch * (repeats ? 1 : blocks)));
     if (per_launch > 3072) {  // ~1,024 groups per bin (tools/groupby_sweep.py: 100,000 groups x 3
         p.log2_parts = 1;       // aggregates, P = 64/128/256: 13.3/12.4/13.8 ms per 10 GB)
         while (p.log2_parts < 8 && (per_launch >> p.log2_parts) > 1024) ++p.log2_parts;
@@ -629,7 +637,7 @@ StreamRef GroupByPartialTransform::execute() {
                     shared_->dummy_count = true;
                 }
                 const GroupPlan gp = plan_group_by(d, c, has_pred ? fp.get() : nullptr,
-                                                   kc.expr.n_steps ? &kc.expr : nullptr, ctx);
+                                                   kc.expr.n_steps ? &kc.expr : nullptr, shared_->blocks_hint, ctx);
                 d.capacity = std::max<int64_t>(ctx.rt->group_capacity.load(), gp.capacity);
                 ctx.rt->group_used_capacity.store(d.capacity);
                 shared_->log2_parts = gp.log2_parts;

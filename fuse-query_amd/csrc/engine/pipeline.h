@@ -263,6 +263,7 @@ struct GroupByShared {
     std::vector<uint32_t> leaf_ops;  // per table aggregate
     bool dummy_count = false;        // no aggregate: a Count keeps the table valid
     int log2_parts = 0;              // > 0: radix-partitioned launches (high cardinality)
+    int64_t blocks_hint = 1;         // numbers_mt partitions of this rank (planner)
     // their workspace (~8 B per row), one per device queue: the pipes that
     // share a queue run its launches in order, so they share the memory
     // instead of mapping a fresh block per pipe

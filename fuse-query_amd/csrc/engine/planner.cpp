@@ -636,6 +636,13 @@ Pipeline build_pipeline(const QueryPlan &plan, const QueryContextRef &ctx, bool 
                     if (n.groups.size() != 1)
                         throw_status(FQ_E_UNSUPPORTED, "GROUP BY supports one key expression on the device path");
                     auto shared = std::make_shared<GroupByShared>();
+                    // partitions this rank reads (sizes the table when every
+                    // block brings keys of its own)
+                    for (const PlanNode &src : plan.nodes)
+                        if (src.kind == PlanNode::kReadSource) {
+                            const size_t np = src.read.partitions.size(), w = (size_t)std::max(1, ctx->world);
+                            shared->blocks_hint = (int64_t)std::max<size_t>(1, (np + w - 1) / w);
+                        }
                     auto funcs = [&]() {
                         std::vector<FunctionRef> fs;
                         for (const auto &e : n.exprs) fs.push_back(e.to_function(ctx->factory));

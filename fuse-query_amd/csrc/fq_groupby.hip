@@ -7,7 +7,8 @@
 //
 // Table layout in the caller's device memory (all 64-bit words):
 //   [0, 64)                     header: u32 flags (state flags | 256 = full),
-//                               u32 sentinel-used, u64 scratch counter
+//                               u32 sentinel-used, u64 scratch counter,
+//                               u32 groups claimed, u32 "an LDS table saturated"
 //   keys[capacity + 1]          0xFFFF...FF = empty; slot `capacity` holds the
 //                               key 0xFFFF...FF itself when it occurs
 //   states[a][r][capacity + 1]  per aggregate a and replica r < R (see

@@ -719,6 +719,18 @@ int group_key_plain() {
     return v;
 }
 
+// GROUP BY tile order: 1 (default) = one contiguous run of tiles per
+// workgroup, 0 = grid stride over tiles (FQ_GROUP_CHUNKED; tools/
+// group_shapes_probe.py: % 1000 keys 1.569 -> 1.531 ms per 10 GB, % 4093
+// 1.656 -> 1.605)
+int group_chunked() {
+    static const int v = [] {
+        const char *e = getenv("FQ_GROUP_CHUNKED");
+        return e ? (atoi(e) ? 1 : 0) : 1;
+    }();
+    return v;
+}
+
 int lds_slots(int n_aggs, int budget) {
     int s = 16384;
     while (s > 64 && (int64_t)s * 8 * (1 + n_aggs) > budget) s >>= 1;
@@ -765,7 +777,8 @@ void pack_group_consts(const GroupLaunch &G, HostGroupConsts &hc) {
 }
 
 std::string group_shape_key(const GroupLaunch &G, int32_t tin, int dev) {
-    std::string k = "G" + std::to_string(group_lds_local()) + std::to_string(group_key_plain());
+    std::string k = "G" + std::to_string(group_lds_local()) + std::to_string(group_key_plain()) +
+                    std::to_string(group_chunked());
     auto put = [&k](int32_t v) { k.append(reinterpret_cast<const char *>(&v), sizeof v); };
     auto prog = [&put](const KProg &p) {
         put(p.n);
@@ -801,7 +814,8 @@ std::string group_shape_key(const GroupLaunch &G, int32_t tin, int dev) {
 std::string state_update(int32_t kind, int32_t dt, const std::string &P, const std::string &v) {
     const char *T = dt == FQ_DT_INT64 ? "long long" : (dt == FQ_DT_FLOAT64 ? "double" : "unsigned long long");
     switch (kind) {
-        case FQ_AGG_COUNT: return "atomicAdd((unsigned long long *)(" + P + "), 1ull);";
+        case FQ_AGG_COUNT:  // v = the rows to count ("" = one)
+            return "atomicAdd((unsigned long long *)(" + P + "), " + (v.empty() ? std::string("1ull") : "(unsigned long long)(" + v + ")") + ");";
         case FQ_AGG_SUM:
             if (dt == FQ_DT_FLOAT64) return "atomicAdd((double *)(" + P + "), " + v + ");";
             return "atomicAdd((unsigned long long *)(" + P + "), (unsigned long long)(" + v + "));";
@@ -996,11 +1010,13 @@ fq_jit_groupby_bins(const TIn *__restrict__ vals, const u64 *__restrict__ bins, 
                 Row r[GP_ROWS];
 #pragma unroll
                 for (int k = 0; k < GP_ROWS; ++k) fq_prep_all(x[k], r0 + (long long)k * BT < e ? 1u : 0u, c, flags, r[k]);
+                u32 cnt[GP_ROWS];
+                fq_runs(r, cnt);
                 u64 cur[GP_ROWS];
 #pragma unroll
                 for (int j = 0; j < GP_ROWS; ++j) cur[j] = fq_first(r[j], s_keys);
 #pragma unroll
-                for (int j = 0; j < GP_ROWS; ++j) fq_commit(r[j], cur[j], tr, s_keys, s_st, s_bypass);
+                for (int j = 0; j < GP_ROWS; ++j) fq_commit_lane(r[j], cur[j], tr, s_keys, s_st, s_bypass, (u64)cnt[j]);
             }
             __syncthreads();
             fq_flush(tr, s_keys, s_st);
@@ -1030,6 +1046,7 @@ bool gen_groupby_source(const GroupLaunch &G, int32_t tin, Gen &g, std::string &
     src += "#define BT " + std::to_string(G.threads) + "\n#define ROWMAP " + std::to_string(G.rowmap) + "\n";
     src += "#define LDS_LOCAL " + std::to_string(group_lds_local()) + "\n";
     src += "#define GKEY_PLAIN " + std::to_string(group_key_plain()) + "\n";
+    src += "#define GCHUNK " + std::to_string(group_chunked()) + "\n";
     // dense keys (see dense_of): a COUNT state doubles as the slot's
     // occupancy, else the key is stored (a plain write, every writer writes
     // the same value)
@@ -1167,13 +1184,13 @@ __device__ long long ginsert(const Tab &t, u64 k) {
     row += "__device__ __forceinline__ u64 fq_first(const Row &r, const u64 *s_keys) {\n"
            "#if DENSE\n    (void)r; (void)s_keys;\n    return EMPTY;\n#else\n"
            "    return (r.pass && r.k != EMPTY) ? s_keys[r.h] : EMPTY;\n#endif\n}\n";
-    row += "__device__ __forceinline__ void fq_commit(const Row &r, u64 cur0, const Tab &t, u64 *s_keys,\n"
-           "    u64 (*s_st)[S], int *s_bypass) {\n    if (!r.pass) return;\n";
+    row += "__device__ __forceinline__ void fq_commit_lane(const Row &r, u64 cur0, const Tab &t, u64 *s_keys,\n"
+           "    u64 (*s_st)[S], int *s_bypass, u64 cnt) {\n    if (!r.pass) return;\n";
     row += "#if DENSE\n    (void)cur0; (void)t; (void)s_bypass;\n    const int slot = r.h;\n#if DENSE_CNT < 0\n"
            "    s_keys[slot] = r.k;\n#endif\n";
     for (int a = 0; a < NA; ++a)
         row += "    " + state_update(G.kinds[a], G.dtypes[a], "&s_st[" + std::to_string(a) + "][slot]",
-                                     "r.v" + std::to_string(a)) + "\n";
+                                     G.kinds[a] == FQ_AGG_COUNT ? "cnt" : "r.v" + std::to_string(a)) + "\n";
     row += "#else\n    const u64 k = r.k;\n";
     row += R"(    int slot = -1;
     if (k != EMPTY) {
@@ -1205,12 +1222,38 @@ __device__ long long ginsert(const Tab &t, u64 k) {
 )";
     for (int a = 0; a < NA; ++a)
         row += "        " + state_update(G.kinds[a], G.dtypes[a], "&s_st[" + std::to_string(a) + "][slot]",
-                                         "r.v" + std::to_string(a)) + "\n";
+                                         G.kinds[a] == FQ_AGG_COUNT ? "cnt" : "r.v" + std::to_string(a)) + "\n";
     row += "    } else {\n        const long long gs = ginsert(t, k);\n        if (gs >= 0) {\n";
     for (int a = 0; a < NA; ++a)
         row += "            " + state_update(G.kinds[a], G.dtypes[a], "&t.st[" + std::to_string(a) + "][gs]",
-                                             "r.v" + std::to_string(a)) + "\n";
+                                             G.kinds[a] == FQ_AGG_COUNT ? "cnt" : "r.v" + std::to_string(a)) + "\n";
     row += "        }\n    }\n#endif\n}\n";
+    row += "__device__ __forceinline__ void fq_commit(const Row &r, u64 cur0, const Tab &t, u64 *s_keys,\n"
+           "    u64 (*s_st)[S], int *s_bypass) {\n"
+           "    fq_commit_lane(r, cur0, t, s_keys, s_st, s_bypass, 1ull);\n}\n";
+    // Runs of equal keys among a lane's rows of one tile (clustered keys such
+    // as number / 1000000: a lane's rows are 1,024 apart, so all of them
+    // share a key) are merged in registers first and committed once: 64
+    // lanes' LDS atomics on one address serialise otherwise (12 ms against
+    // 1.6 ms per 10 GB, tools/group_shapes_probe.py).  cnt[j] = rows merged
+    // into row j (0 for a row merged away or not passing).
+    // (Only when some lane's first two rows share a key -- one compare and a
+    // ballot per tile, so scattered keys skip the chain: `% 1000` keys 1.587
+    // -> 1.556 ms per 10 GB.)
+    row += "template <int N> __device__ __forceinline__ void fq_runs(Row (&r)[N], u32 (&cnt)[N]) {\n"
+           "#pragma unroll\n    for (int j = 0; j < N; ++j) cnt[j] = r[j].pass;\n"
+           "    if (!__ballot(r[0].pass && r[1].pass && r[0].k == r[1].k)) return;\n"
+           "#pragma unroll\n    for (int j = N - 1; j > 0; --j) {\n"
+           "        if (r[j].pass && r[j - 1].pass && r[j].k == r[j - 1].k) {\n";
+    for (int a = 0; a < NA; ++a) {
+        if (G.kinds[a] == FQ_AGG_COUNT) continue;
+        const std::string A = std::to_string(a);
+        row += "            r[j - 1].v" + A + " = " +
+               (G.kinds[a] == FQ_AGG_SUM ? "r[j - 1].v" + A + " + r[j].v" + A
+                                         : std::string(G.kinds[a] == FQ_AGG_MAX ? "vmax" : "vmin") + "(r[j - 1].v" + A +
+                                               ", r[j].v" + A + ")") + ";\n";
+    }
+    row += "            cnt[j - 1] += cnt[j];\n            cnt[j] = 0;\n            r[j].pass = 0;\n        }\n    }\n}\n";
     row += "__device__ __forceinline__ void fq_row(TIn x, long long idx, const Consts &c, const Tab &t,\n"
            "    const u64 *__restrict__ bitmap, u64 *s_keys, u64 (*s_st)[S], u32 &flags, int *s_bypass, u32 P,\n"
            "    u32 part) {\n"
@@ -1275,8 +1318,12 @@ fq_jit_groupby(const TIn *__restrict__ col, long long n, long long head, const u
     const u32 seen = __hip_atomic_load(&t.hdr[4], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // (only past the LDS saturation point, 3/4 of S; beyond PMAX partitions
     // the rows are cheaper to send to the HBM table than to re-read)
+    // and only once a launch saw an LDS table saturate (hdr[5]): keys that
+    // differ from block to block (clustered, number / 1000000) fill the HBM
+    // table without crowding any one launch's LDS
+    const u32 saturated = __hip_atomic_load(&t.hdr[5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     u32 P = 1;
-    if (!DENSE && seen > (u32)(S * 3 / 4))  // (dense keys never outgrow the table)
+    if (!DENSE && saturated && seen > (u32)(S * 3 / 4))  // (dense keys never outgrow the table)
         while (P <= PMAX && P * (u32)(S / 2) < seen) P <<= 1;
     if (P > PMAX || gridDim.x % P) P = 1;
     const u32 part = blockIdx.x & (P - 1);
@@ -1292,18 +1339,26 @@ fq_jit_groupby(const TIn *__restrict__ col, long long n, long long head, const u
     const TIn *__restrict__ cp = col + head;
     const long long TV = 4 * BT;  // vectors (pairs) per tile, as below
     const long long ntiles = nvec / TV;
+#if GCHUNK
+    // one contiguous run of tiles per workgroup: clustered keys then meet a
+    // workgroup's LDS table a few at a time, so its flush stays small
+    const long long per = (ntiles + RG - 1) / RG, t_lo = rb * per, t_hi = t_lo + per < ntiles ? t_lo + per : ntiles;
+    const long long t_step = 1;
+#else
+    const long long t_lo = rb, t_hi = ntiles, t_step = RG;
+#endif
     TIn nxt[8];
-    if (rb < ntiles) {
+    if (t_lo < t_hi) {
 #pragma unroll
         for (int k = 0; k < 8; ++k)
-            nxt[k] = __builtin_nontemporal_load(cp + rb * TV * 2 + threadIdx.x + (long long)k * BT);
+            nxt[k] = __builtin_nontemporal_load(cp + t_lo * TV * 2 + threadIdx.x + (long long)k * BT);
     }
-    for (long long tt = rb; tt < ntiles; tt += RG) {
+    for (long long tt = t_lo; tt < t_hi; tt += t_step) {
         TIn raw[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) raw[k] = nxt[k];
-        const long long tn = tt + RG;
-        if (tn < ntiles) {
+        const long long tn = tt + t_step;
+        if (tn < t_hi) {
 #pragma unroll
             for (int k = 0; k < 8; ++k) nxt[k] = __builtin_nontemporal_load(cp + tn * TV * 2 + threadIdx.x + (long long)k * BT);
         }
@@ -1313,11 +1368,13 @@ fq_jit_groupby(const TIn *__restrict__ col, long long n, long long head, const u
             fq_prep(raw[k], head + tt * TV * 2 + threadIdx.x + (long long)k * BT, c, bitmap, flags, r[k]);
             if (P > 1 && part_of(r[k].k, P) != part) r[k].pass = 0;
         }
+        u32 cnt[8];
+        fq_runs(r, cnt);
         u64 cur[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) cur[j] = fq_first(r[j], s_keys);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) fq_commit(r[j], cur[j], tr, s_keys, s_st, s_bypass);
+        for (int j = 0; j < 8; ++j) fq_commit_lane(r[j], cur[j], tr, s_keys, s_st, s_bypass, (u64)cnt[j]);
     }
 #else
     const long long TV = 4 * BT;
@@ -1352,11 +1409,13 @@ fq_jit_groupby(const TIn *__restrict__ col, long long n, long long head, const u
             if (P > 1 && part_of(r[2 * k].k, P) != part) r[2 * k].pass = 0;
             if (P > 1 && part_of(r[2 * k + 1].k, P) != part) r[2 * k + 1].pass = 0;
         }
+        u32 cnt[8];
+        fq_runs(r, cnt);
         u64 cur[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) cur[j] = fq_first(r[j], s_keys);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) fq_commit(r[j], cur[j], tr, s_keys, s_st, s_bypass);
+        for (int j = 0; j < 8; ++j) fq_commit_lane(r[j], cur[j], tr, s_keys, s_st, s_bypass, (u64)cnt[j]);
     }
 #endif
     for (long long v = ntiles * TV + g; v < nvec; v += T) {
@@ -1374,6 +1433,7 @@ fq_jit_groupby(const TIn *__restrict__ col, long long n, long long head, const u
     }
     if (flags) atomicOr(&t.hdr[0], flags);
     __syncthreads();
+    if (threadIdx.x == 0 && s_bypass[0]) atomicOr(&t.hdr[5], 1u);
     fq_flush(tr, s_keys, s_st);
 }
 )";

@@ -269,10 +269,18 @@ def test_sql_group_by_f64_and_keys_only(eng):
     assert r.rows == [(k,) for k in range(7)]
 
 
-def test_sql_group_by_grows_a_full_table(eng):
-    # 100k distinct keys: 4096 slots -> TABLE_FULL -> re-run with 16x, twice
+def test_sql_group_by_sizes_distinct_keys(eng):
+    # 160,000 distinct keys (GROUP BY number): the sample sees keys that keep
+    # coming, the table is sized for every partition's
     r = eng.execute("SELECT number, count(number) FROM system.numbers_mt(160000) GROUP BY number")
     assert len(r.rows) == 160000 and r.rows[0] == (0, 1) and r.rows[-1] == (159999, 1)
+
+
+def test_sql_group_by_grows_a_full_table(eng):
+    # clustered keys: each partition repeats its own 25,000 keys, so the sample
+    # sizes 131,072 slots for 200,000 groups -> TABLE_FULL -> re-run with 16x
+    r = eng.execute("SELECT number/2, count(number), min(number) FROM system.numbers_mt(400000) GROUP BY number/2")
+    assert len(r.rows) == 200000 and r.rows[0] == (0, 2, 0) and r.rows[-1] == (199999, 2, 399998)
 
 
 def test_sql_group_by_limit_and_explain(eng):
