@@ -719,6 +719,30 @@ int group_key_plain() {
     return v;
 }
 
+// wave-uniform key runs merged across the wave (fq_wave_runs): 1 (default),
+// 0 = off (FQ_GROUP_WAVE_RUNS; tools/group_shapes_probe.py)
+int group_wave_runs() {
+    static const int v = [] {
+        const char *e = getenv("FQ_GROUP_WAVE_RUNS");
+        const int x = e ? atoi(e) : 1;
+        return x >= 0 && x <= 2 ? x : 1;
+    }();
+    return v;
+}
+
+// clustered-key row layout of the GROUP BY kernel (mode 1 in fq_jit_groupby):
+// chosen per workgroup from its first tile when a wave's 512 rows change key
+// at most this often (default 160: runs of ~4+ rows), 0 = never
+// (FQ_GROUP_CLUSTER; tools/group_shapes_probe.py)
+int group_cluster() {
+    static const int v = [] {
+        const char *e = getenv("FQ_GROUP_CLUSTER");
+        const int x = e ? atoi(e) : 160;
+        return x >= 0 && x <= 512 ? x : 160;
+    }();
+    return v;
+}
+
 // GROUP BY tile order: 1 (default) = one contiguous run of tiles per
 // workgroup, 0 = grid stride over tiles (FQ_GROUP_CHUNKED; tools/
 // group_shapes_probe.py: % 1000 keys 1.569 -> 1.531 ms per 10 GB, % 4093
@@ -778,7 +802,8 @@ void pack_group_consts(const GroupLaunch &G, HostGroupConsts &hc) {
 
 std::string group_shape_key(const GroupLaunch &G, int32_t tin, int dev) {
     std::string k = "G" + std::to_string(group_lds_local()) + std::to_string(group_key_plain()) +
-                    std::to_string(group_chunked());
+                    std::to_string(group_chunked()) + std::to_string(group_wave_runs()) +
+                    std::to_string(group_cluster());
     auto put = [&k](int32_t v) { k.append(reinterpret_cast<const char *>(&v), sizeof v); };
     auto prog = [&put](const KProg &p) {
         put(p.n);
@@ -1029,7 +1054,7 @@ fq_jit_groupby_bins(const TIn *__restrict__ vals, const u64 *__restrict__ bins, 
 }
 )";
 
-bool gen_groupby_source(const GroupLaunch &G, int32_t tin, Gen &g, std::string &src) {
+bool gen_groupby_source(const GroupLaunch &G, int32_t tin, Gen &g, std::string &src, bool cluster = true) {
     const char *TIn = ctype(tin);
     if (!TIn || (G.key_dtype != FQ_DT_UINT64 && G.key_dtype != FQ_DT_INT64)) return false;
     if (G.n_aggs < 1 || G.n_aggs > FQ_MAX_GROUP_AGGS) return false;
@@ -1047,6 +1072,10 @@ bool gen_groupby_source(const GroupLaunch &G, int32_t tin, Gen &g, std::string &
     src += "#define LDS_LOCAL " + std::to_string(group_lds_local()) + "\n";
     src += "#define GKEY_PLAIN " + std::to_string(group_key_plain()) + "\n";
     src += "#define GCHUNK " + std::to_string(group_chunked()) + "\n";
+    src += "#define GWAVE " + std::to_string(group_wave_runs()) + "\n";
+    src += "#define GCLUSTER " + std::to_string(cluster && group_cluster() > 0 && fqc::dtype_size(tin) == 8 &&
+                                                          G.lds_bytes + G.threads * 16 <= 160 * 1024 ? 1 : 0) + "\n";
+    src += "#define GCLUSTER_CHANGES " + std::to_string(group_cluster() > 0 ? group_cluster() : 160) + "\n";
     // dense keys (see dense_of): a COUNT state doubles as the slot's
     // occupancy, else the key is stored (a plain write, every writer writes
     // the same value)
@@ -1057,6 +1086,7 @@ bool gen_groupby_source(const GroupLaunch &G, int32_t tin, Gen &g, std::string &
     src += "#define PMAX 16\n#define EMPTY 0xffffffffffffffffull\n#define NA " + std::to_string(NA) + "\n#define S " +
            std::to_string(S) + "\n#define LOG2S " + std::to_string(__builtin_ctz((unsigned)S)) + "\n";
     src += R"(
+template <int V> struct IC { static constexpr int value = V; };
 __device__ __forceinline__ u64 mix(u64 z) {
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
@@ -1240,9 +1270,9 @@ __device__ long long ginsert(const Tab &t, u64 k) {
     // (Only when some lane's first two rows share a key -- one compare and a
     // ballot per tile, so scattered keys skip the chain: `% 1000` keys 1.587
     // -> 1.556 ms per 10 GB.)
-    row += "template <int N> __device__ __forceinline__ void fq_runs(Row (&r)[N], u32 (&cnt)[N]) {\n"
+    row += "template <int N> __device__ __forceinline__ bool fq_runs(Row (&r)[N], u32 (&cnt)[N]) {\n"
            "#pragma unroll\n    for (int j = 0; j < N; ++j) cnt[j] = r[j].pass;\n"
-           "    if (!__ballot(r[0].pass && r[1].pass && r[0].k == r[1].k)) return;\n"
+           "    if (!__ballot(r[0].pass && r[1].pass && r[0].k == r[1].k)) return false;\n"
            "#pragma unroll\n    for (int j = N - 1; j > 0; --j) {\n"
            "        if (r[j].pass && r[j - 1].pass && r[j].k == r[j - 1].k) {\n";
     for (int a = 0; a < NA; ++a) {
@@ -1253,7 +1283,75 @@ __device__ long long ginsert(const Tab &t, u64 k) {
                                          : std::string(G.kinds[a] == FQ_AGG_MAX ? "vmax" : "vmin") + "(r[j - 1].v" + A +
                                                ", r[j].v" + A + ")") + ";\n";
     }
-    row += "            cnt[j - 1] += cnt[j];\n            cnt[j] = 0;\n            r[j].pass = 0;\n        }\n    }\n}\n";
+    row += "            cnt[j - 1] += cnt[j];\n            cnt[j] = 0;\n            r[j].pass = 0;\n        }\n    }\n    return true;\n}\n";
+    // Runs of equal keys across a wave: a slot whose passing lanes (64
+    // consecutive rows) all hold one key -- runs of 64+ rows, e.g.
+    // (number / 1000) % 1000 -- is reduced across the wave in registers (DPP
+    // within each 16-lane row, readlane across the four) and committed by one
+    // lane; 64 lanes' LDS atomics on one slot serialise otherwise (12.2 ms
+    // against 1.5 ms per 10 GB).  Gate per tile: lanes 0 and 63 of the first
+    // or last slot share a key.
+    row += R"(template <int C> __device__ __forceinline__ u32 dpp32(u32 v) {
+    return (u32)__builtin_amdgcn_mov_dpp((int)v, C, 0xf, 0xf, false);
+}
+template <typename T, int C> __device__ __forceinline__ T dppT(T v) {
+    if constexpr (sizeof(T) == 4) {
+        return __builtin_bit_cast(T, dpp32<C>(__builtin_bit_cast(u32, v)));
+    } else {
+        const u64 b = __builtin_bit_cast(u64, v);
+        return __builtin_bit_cast(T, ((u64)dpp32<C>((u32)(b >> 32)) << 32) | dpp32<C>((u32)b));
+    }
+}
+template <typename T> __device__ __forceinline__ T rlane(T v, int l) {
+    if constexpr (sizeof(T) == 4) {
+        return __builtin_bit_cast(T, (u32)__builtin_amdgcn_readlane((int)__builtin_bit_cast(u32, v), l));
+    } else {
+        const u64 b = __builtin_bit_cast(u64, v);
+        const u32 lo = (u32)__builtin_amdgcn_readlane((int)(u32)b, l), hi = (u32)__builtin_amdgcn_readlane((int)(u32)(b >> 32), l);
+        return __builtin_bit_cast(T, ((u64)hi << 32) | lo);
+    }
+}
+struct WSum { template <typename T> __device__ __forceinline__ T operator()(T a, T b) const { return a + b; } };
+// NaN never wins, as with the HBM / LDS f64 max/min atomics (v > old)
+struct WMax { template <typename T> __device__ __forceinline__ T operator()(T a, T b) const { return (b > a || a != a) ? b : a; } };
+struct WMin { template <typename T> __device__ __forceinline__ T operator()(T a, T b) const { return (b < a || a != a) ? b : a; } };
+// every lane's v combined; quad_perm xor 1, xor 2, row_ror 4, 8 -> each
+// 16-lane row's total in every lane of it, then the four rows by readlane
+template <typename T, typename OP> __device__ __forceinline__ T wave_all(T v, OP op) {
+    v = op(v, dppT<T, 0xb1>(v));
+    v = op(v, dppT<T, 0x4e>(v));
+    v = op(v, dppT<T, 0x124>(v));
+    v = op(v, dppT<T, 0x128>(v));
+    return op(op(rlane(v, 0), rlane(v, 16)), op(rlane(v, 32), rlane(v, 48)));
+}
+// Up to GWAVE keys per slot (2: a run boundary inside the 64 rows) are
+// merged; a key held by fewer than 8 passing lanes commits lane by lane.
+template <int N> __device__ __forceinline__ void fq_wave_runs(Row (&r)[N], u32 (&cnt)[N]) {
+    if (rlane(r[0].k, 0) != rlane(r[0].k, 63) && rlane(r[N - 1].k, 0) != rlane(r[N - 1].k, 63)) return;
+    const int lane = (int)(threadIdx.x & 63);
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        u64 act = __ballot(r[j].pass != 0);
+#pragma unroll
+        for (int it = 0; it < GWAVE; ++it) {
+        if (__popcll(act) < 8) break;
+        const int l0 = __builtin_ctzll(act);
+        const u64 kk = rlane(r[j].k, l0);
+        const u64 same = __ballot(r[j].pass != 0 && r[j].k == kk);
+        if (__popcll(same) < 8) break;
+        act &= ~same;
+        const bool in = (same >> lane) & 1ull;
+        const u32 tot = wave_all(in ? cnt[j] : 0u, WSum());
+)";
+    for (int a = 0; a < NA; ++a) {
+        if (G.kinds[a] == FQ_AGG_COUNT) continue;
+        const std::string A = std::to_string(a), V = ctype(G.dtypes[a]);
+        const char *op = G.kinds[a] == FQ_AGG_SUM ? "WSum()" : (G.kinds[a] == FQ_AGG_MAX ? "WMax()" : "WMin()");
+        row += "        { const " + V + " w = wave_all(in ? r[j].v" + A + " : __builtin_bit_cast(" + V + ", (u64)" +
+               identity(G.kinds[a], G.dtypes[a]) + "), " + op + ");\n          if (lane == l0) r[j].v" + A + " = w; }\n";
+    }
+    row += "        if (lane == l0) {\n            cnt[j] = tot;\n        } else if (in) {\n            cnt[j] = 0;\n"
+           "            r[j].pass = 0;\n        }\n        }\n    }\n}\n";
     row += "__device__ __forceinline__ void fq_row(TIn x, long long idx, const Consts &c, const Tab &t,\n"
            "    const u64 *__restrict__ bitmap, u64 *s_keys, u64 (*s_st)[S], u32 &flags, int *s_bypass, u32 P,\n"
            "    u32 part) {\n"
@@ -1347,34 +1445,136 @@ fq_jit_groupby(const TIn *__restrict__ col, long long n, long long head, const u
 #else
     const long long t_lo = rb, t_hi = ntiles, t_step = RG;
 #endif
+    // Row layout per tile: mode 0 = lane-consecutive rows (row k * BT + tid:
+    // a wave's 64 keys of one LDS access are 64 consecutive rows); mode 1 =
+    // eight consecutive rows per lane (row 8 * tid + j), so runs of equal keys
+    // merge in the lane's registers (fq_runs) and then across the wave
+    // (fq_wave_runs) instead of 64 lanes serialising on one LDS slot.  Mode 1
+    // loads each wave's 512 rows coalesced (slot k = rows 64k + lane of the
+    // wave's chunk) and transposes them through 1 KB of LDS per wave in four
+    // rounds of 128 rows (per-lane 64-B loads ran at 2.6 ms per 10 GB).  The
+    // workgroup picks the mode once, from its first tile: mode 1 when most
+    // waves see at most GCLUSTER_CHANGES key changes over their 512 rows and
+    // their lanes' rows BT apart differ (scattered keys stay in mode 0, where
+    // mode 1 would put a lane's eight neighbouring keys on eight slots per
+    // lane; runs longer than BT rows already merge in mode 0).  Each mode has
+    // its own loop, so mode 0 is the plain kernel.
     TIn nxt[8];
-    if (t_lo < t_hi) {
+    const long long tile_rows = TV * 2;
+    auto gload = [&](long long tile, auto M) {
+        if constexpr (decltype(M)::value == 1) {
+            const TIn *__restrict__ q = cp + tile * tile_rows + (long long)(threadIdx.x >> 6) * 512 + (threadIdx.x & 63);
 #pragma unroll
-        for (int k = 0; k < 8; ++k)
-            nxt[k] = __builtin_nontemporal_load(cp + t_lo * TV * 2 + threadIdx.x + (long long)k * BT);
-    }
-    for (long long tt = t_lo; tt < t_hi; tt += t_step) {
-        TIn raw[8];
+            for (int k = 0; k < 8; ++k) nxt[k] = __builtin_nontemporal_load(q + 64 * k);
+        } else {
 #pragma unroll
-        for (int k = 0; k < 8; ++k) raw[k] = nxt[k];
-        const long long tn = tt + t_step;
-        if (tn < t_hi) {
-#pragma unroll
-            for (int k = 0; k < 8; ++k) nxt[k] = __builtin_nontemporal_load(cp + tn * TV * 2 + threadIdx.x + (long long)k * BT);
+            for (int k = 0; k < 8; ++k) nxt[k] = __builtin_nontemporal_load(cp + tile * tile_rows + threadIdx.x + (long long)k * BT);
         }
+    };
+#if GCLUSTER
+    __shared__ u64 s_tr[BT / 64][128];
+#endif
+    // mode 1: nxt (the wave's rows 64k + lane) -> raw (rows 8 * lane + i)
+    // through 1 KB of LDS per wave; nxt is free again for the next tile's
+    // loads, so raw, nxt and the transpose never hold three tiles of registers
+    auto transpose = [&](TIn (&raw)[8]) {
+#if GCLUSTER
+        const int w = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            s_tr[w][lane] = __builtin_bit_cast(u64, nxt[2 * p]);
+            s_tr[w][64 + lane] = __builtin_bit_cast(u64, nxt[2 * p + 1]);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if ((lane >> 4) == p) {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) raw[i] = __builtin_bit_cast(TIn, s_tr[w][8 * (lane & 15) + i]);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+#else
+        (void)raw;
+#endif
+    };
+    // one tile's rows through the LDS table
+    auto work = [&](auto M, long long tt, TIn (&raw)[8]) {
+        constexpr int mode = decltype(M)::value;
         Row r[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-            fq_prep(raw[k], head + tt * TV * 2 + threadIdx.x + (long long)k * BT, c, bitmap, flags, r[k]);
+            const long long row = mode ? (long long)threadIdx.x * 8 + k : threadIdx.x + (long long)k * BT;
+            fq_prep(raw[k], head + tt * tile_rows + row, c, bitmap, flags, r[k]);
             if (P > 1 && part_of(r[k].k, P) != part) r[k].pass = 0;
         }
         u32 cnt[8];
         fq_runs(r, cnt);
+#if GWAVE
+        if constexpr (mode == 1) fq_wave_runs(r, cnt);
+#endif
         u64 cur[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) cur[j] = fq_first(r[j], s_keys);
 #pragma unroll
         for (int j = 0; j < 8; ++j) fq_commit_lane(r[j], cur[j], tr, s_keys, s_st, s_bypass, (u64)cnt[j]);
+    };
+    auto loop = [&](auto M, long long from) {
+        for (long long tt = from; tt < t_hi; tt += t_step) {
+            TIn raw[8];
+            if constexpr (decltype(M)::value == 1) {
+                transpose(raw);
+            } else {
+#pragma unroll
+                for (int k = 0; k < 8; ++k) raw[k] = nxt[k];
+            }
+            const long long tn = tt + t_step;
+            if (tn < t_hi) gload(tn, M);
+            work(M, tt, raw);
+        }
+    };
+    if (t_lo < t_hi) {
+        // the first tile in mode 0 decides the layout of the rest
+        gload(t_lo, IC<0>());
+        TIn raw[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) raw[k] = nxt[k];
+        int nmode = 0;
+#if GCLUSTER
+        {
+            __shared__ int s_vote;
+            const int lane = (int)(threadIdx.x & 63);
+            u32 vf = 0, changes = 0;
+            u64 k0 = 0, k1 = 0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const u64 kk = fq_key(raw[k], c, vf, 1u);
+                const u64 prev = ((u64)(u32)__shfl_up((int)(u32)(kk >> 32), 1, 64) << 32) | (u32)__shfl_up((int)(u32)kk, 1, 64);
+                changes += (u32)__popcll(__ballot(lane > 0 && kk != prev));
+                if (k == 0) k0 = kk;
+                if (k == 1) k1 = kk;
+            }
+            // runs longer than BT rows already merge in mode 0 (a lane's rows
+            // are BT apart): keep it
+            const u32 far = (u32)__popcll(__ballot(k0 == k1));
+            if (threadIdx.x == 0) s_vote = 0;
+            __syncthreads();
+            if (lane == 0 && changes <= GCLUSTER_CHANGES && far < 32) atomicAdd(&s_vote, 1);
+            __syncthreads();
+            nmode = s_vote * 2 > BT / 64 ? 1 : 0;
+        }
+#endif
+        if (t_lo + t_step < t_hi) {
+            if (nmode) gload(t_lo + t_step, IC<1>());
+            else gload(t_lo + t_step, IC<0>());
+        }
+        work(IC<0>(), t_lo, raw);
+#if GCLUSTER
+        if (nmode) loop(IC<1>(), t_lo + t_step);
+        else
+#endif
+        loop(IC<0>(), t_lo + t_step);
     }
 #else
     const long long TV = 4 * BT;
@@ -1410,7 +1610,12 @@ fq_jit_groupby(const TIn *__restrict__ col, long long n, long long head, const u
             if (P > 1 && part_of(r[2 * k + 1].k, P) != part) r[2 * k + 1].pass = 0;
         }
         u32 cnt[8];
-        fq_runs(r, cnt);
+        const bool lane_runs = fq_runs(r, cnt);
+#if GWAVE
+        if (!lane_runs) fq_wave_runs(r, cnt);
+#else
+        (void)lane_runs;
+#endif
         u64 cur[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) cur[j] = fq_first(r[j], s_keys);
@@ -2160,6 +2365,24 @@ fq_status get_group_fns(int32_t col_dtype, const GroupLaunch &G, GroupFns *out) 
             return fqc::fail(FQ_E_UNSUPPORTED, "GROUP BY: key/aggregate types outside the device path");
         fq_status s = compile(src, dev, c, "fq_jit_groupby");
         if (s != FQ_OK) return s;
+        int scratch = 0;
+        if (dev >= 0 && hipFuncGetAttribute(&scratch, HIP_FUNC_ATTRIBUTE_LOCAL_SIZE_BYTES, c.fn) == hipSuccess &&
+            scratch > 0) {
+            // The clustered-key layout (mode 1) must not cost the shape
+            // register spills: 64-bit magic keys (number / 1e7) left 1,024
+            // threads with 52 bytes of scratch and ran 1.8 -> 2.4 ms per
+            // 10 GB in mode 0.  Their runs are longer than a lane's rows
+            // apart, where mode 0 merges them anyway -- recompile without it.
+            (void)hipModuleUnload(c.mod);
+            c = Compiled{};
+            src.clear();
+            Gen g2;
+            if (!gen_groupby_source(G, col_dtype, g2, src, false))
+                return fqc::fail(FQ_E_UNSUPPORTED, "GROUP BY: key/aggregate types outside the device path");
+            s = compile(src, dev, c, "fq_jit_groupby");
+            if (s != FQ_OK) return s;
+        }
+        (void)hipGetLastError();
         if (dev < 0) {  // validated only
             *out = GroupFns{};
             return FQ_OK;

@@ -117,6 +117,59 @@ def test_filtered_group_by_c4_shape():
     compare(got, exp, [abi.AGG_MAX, abi.AGG_COUNT], [U, U])
 
 
+@pytest.mark.parametrize("length", [3, 4, 20, 100, 1000, 70000])
+def test_clustered_key_runs_match_numpy(length):
+    # keys constant over runs of `length` consecutive rows: a workgroup whose
+    # first tile shows such runs switches to eight consecutive rows per lane
+    # (LDS transpose, in-lane and wave-wide merging, fq_jit_groupby mode 1;
+    # shapes whose kernel would spill registers keep mode 0 only, so the
+    # aggregates here are the spill-free integer ones); start 123 puts the
+    # runs off the tile grid, the odd length leaves a tail, the predicate
+    # removes rows from inside runs
+    n = 6_000_013
+    col = ops.numbers_column(123, n)
+    x = np.arange(123, 123 + n, dtype=np.uint64)
+    key, _ = chain(U, [("/", length), ("%", 1000)])
+    pred = predicate(U, [("%", 7)], "<", 5)
+    aggs = [(abi.AGG_COUNT, U), (abi.AGG_SUM, U), (abi.AGG_MAX, U), (abi.AGG_MIN, U)]
+    got = run(col, aggs, key=key, values=[None] * 4, pred=pred)
+    m = (x % np.uint64(7)) < 5
+    xm = x[m]
+    exp = np_groupby((xm // np.uint64(length)) % np.uint64(1000), [None, xm, xm, xm], [a for a, _ in aggs])
+    compare(got, exp, [a for a, _ in aggs], [U] * 4)
+
+
+def test_clustered_f64_and_signed_states_match_numpy():
+    # the same over f64 / Int64 values (whichever mode their kernel takes)
+    n = 4_000_037
+    col = ops.numbers_column(5, n)
+    x = np.arange(5, 5 + n, dtype=np.uint64)
+    key, _ = chain(U, [("/", 100), ("%", 1000)])
+    vf, _ = chain(U, [("*", 1.5)])
+    vi, _ = chain(U, [("-", (7, "Int64"))])
+    aggs = [(abi.AGG_COUNT, U), (abi.AGG_SUM, F), (abi.AGG_MAX, F), (abi.AGG_MIN, I)]
+    got = run(col, aggs, key=key, values=[None, vf, vf, vi])
+    k = (x // np.uint64(100)) % np.uint64(1000)
+    xf = x.astype(np.float64) * 1.5
+    exp = np_groupby(k, [None, xf, xf, x.astype(np.int64) - 7], [a for a, _ in aggs])
+    bound = {int(g): 1e-12 * float(np.abs(xf[k == g]).sum()) for g in np.unique(k)}
+    compare(got, exp, [a for a, _ in aggs], [d for _, d in aggs], bound)
+
+
+def test_clustered_sorted_random_column_matches_numpy():
+    # a sorted column of random values with random run lengths (1..300),
+    # grouped by the value itself: clustered keys that are not a function of
+    # the row index
+    rng = np.random.default_rng(0xC1)
+    vals = np.sort(rng.integers(0, 1 << 40, 40_000, dtype=np.uint64))
+    x = np.repeat(vals, rng.integers(1, 300, len(vals)))[:5_000_011]
+    col = ops.from_numpy(x)
+    aggs = [(abi.AGG_COUNT, U), (abi.AGG_SUM, U), (abi.AGG_MAX, U)]
+    got = run(col, aggs, values=[None] * 3, capacity=1 << 17)
+    exp = np_groupby(x, [None, x, x], [a for a, _ in aggs])
+    compare(got, exp, [a for a, _ in aggs], [U] * 3)
+
+
 def test_high_cardinality_bypasses_lds():
     n = 1_000_003
     col = ops.splitmix_column(0x77, 5, n)

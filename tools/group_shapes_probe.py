@@ -14,7 +14,9 @@ from fq_amd.engine import Engine  # noqa: E402
 
 N = 10**10
 KEYS = ["number%1000", "number%4093", "(number*7)%1000", "number/1000000", "number/10000000", "number/100000000",
-        "(number/1000)%1000", "number%8"]
+        "(number/1000)%1000", "number%8", "(number/100)%1000", "(number/20)%1000", "(number/4)%1000", "(number/3)%1000"]
+if os.environ.get("KEYS"):  # e.g. KEYS="number%1000;(number/1000)%1000"
+    KEYS = os.environ["KEYS"].split(";")
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 3
 e = Engine(device=0, profile=True)
 e.materialize_numbers(N)
