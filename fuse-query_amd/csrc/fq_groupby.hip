@@ -260,7 +260,7 @@ __global__ void __launch_bounds__(kScanThreads)
 }
 
 fq_status launch_group_part_scan(const GroupPartition &X, hipStream_t stream) {
-    const int P = 1 << X.log2p;
+    const int P = 1 << (X.log2p & 255);  // (bits 8..15: the range-bin shift)
     if (X.grid > kMaxPartGrid) return fqc::fail(FQ_E_INTERNAL, "partition scan: grid above kMaxPartGrid");
     hipLaunchKernelGGL(group_part_total_kernel, dim3(P), dim3(kScanThreads), 0, stream, X.hist, X.tot, X.grid);
     FQ_HIP_TRY(hipGetLastError());
@@ -428,7 +428,24 @@ fq_status fq_group_aggregate_partitioned(const fq_group_table *t, const fq_col *
     if (((uintptr_t)d_ws) & 255u) return fqc::fail(FQ_E_INVALID, "fq_group_aggregate_partitioned: workspace not 256-B aligned");
     GroupPartition X{};
     X.log2p = log2_parts;
-    part_ws_bytes(G.n, log2_parts, &X, d_ws);
+    // Keys known to lie in [0, d) (`% d`, `& (d - 1)`) are binned by range
+    // when d fits the 2^log2_parts bins with at most S keys each: bin = key >>
+    // shift, and each bin's LDS table is indexed by the key's low bits (no
+    // hash, no probe, no claim).  The kernels get log2p | shift << 8.
+    // profiles/r02_groupby_range_bins.txt
+    int lp_arg = log2_parts;
+    const int64_t d = group_key_range(G.key, G.key_dtype);
+    const int64_t S = group_lds_slots(G.n_aggs, G.lds_bytes);
+    if (d > 0 && tune_env("FQ_GROUP_RANGE_BINS", 1, 0, 1)) {
+        int sh = 0;
+        while (((int64_t)1 << log2_parts << sh) < d) ++sh;
+        if (((int64_t)1 << sh) <= S) {
+            G.range_bins = 1;
+            lp_arg = log2_parts | (sh << 8);
+        }
+    }
+    part_ws_bytes(G.n, X.log2p, &X, d_ws);
+    X.log2p = lp_arg;
     // the histogram and the partition kernel walk the same tiles with the
     // same workgroups; two 1,024-thread workgroups per CU (fq_jit_gpart's
     // 76 KB of LDS; FQ_GPART_WG_PER_CU tunes it)

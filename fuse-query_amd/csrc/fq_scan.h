@@ -88,6 +88,8 @@ struct GroupLaunch {
     int lds_bytes;  // LDS hash table budget per workgroup (sets S and the occupancy)
     int threads;    // workgroup size
     int rowmap;     // 1: lane-consecutive rows (8-byte loads), 0: row pairs per lane (16-byte loads)
+    int range_bins; // partitioned path: bin = key >> log2(S) and LDS slot = key & (S - 1) (a UInt64
+                    // key below d <= P * S: `% d`), else bins by the key's hash
     int grid;
     hipStream_t stream;
 };
@@ -95,6 +97,10 @@ struct GroupLaunch {
 // Keys of a dense GROUP BY key (a UInt64 key ending in `% d`, d <= the LDS
 // slots for n_aggs states in lds_bytes): d, else 0 (fq_jit.hip)
 int64_t group_dense_bound(const KProg &key, int32_t key_dtype, int n_aggs, int lds_bytes);
+// d for a UInt64 key ending in `% d` / `& (d - 1)` (keys in [0, d)), else 0;
+// and the LDS table slots S for n_aggs states in lds_bytes
+int64_t group_key_range(const KProg &key, int32_t key_dtype);
+int group_lds_slots(int n_aggs, int lds_bytes);
 
 // Launches the hipRTC-specialised group-by kernel for G.
 fq_status jit_groupby(int32_t col_dtype, const GroupLaunch &G);
@@ -104,7 +110,7 @@ fq_status jit_groupby(int32_t col_dtype, const GroupLaunch &G);
 // workspace (fq_groupby.hip lays it out).
 constexpr int kMaxPartGrid = 1024;  // workgroups of the histogram / partition kernels
 struct GroupPartition {
-    int log2p;        // 1..8: P = 2^log2p bins
+    int log2p;        // bits 0..7: 1..8, P = 2^log2p bins; bits 8..15: the key shift of range bins
     int grid;         // workgroups of fq_jit_ghist and fq_jit_gpart (the same tiles)
     int bins_grid;    // workgroups of fq_jit_groupby_bins
     uint32_t *hist;   // [P][grid] rows per (bin, workgroup)

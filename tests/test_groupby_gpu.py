@@ -373,9 +373,11 @@ def run_parts(col, aggs, log2p, key=None, values=None, pred=None, key_dtype=U, c
     return {int(k): [st[a][i] for a in range(len(aggs))] for i, k in enumerate(keys)}
 
 
-@pytest.mark.parametrize("mod,log2p", [(7, 1), (1000, 3), (100_000, 6), (2_000_000, 8), (None, 8)])
+@pytest.mark.parametrize("mod,log2p", [(7, 1), (1000, 3), (65_536, 6), (100_000, 6), (2_000_000, 8), (None, 8)])
 def test_partitioned_matches_numpy(mod, log2p):
-    # 2 blocks into one table: rows of both, every group once, all aggregate kinds
+    # 2 blocks into one table: rows of both, every group once, all aggregate kinds;
+    # `% d` keys with d <= P * S take range bins (65,536: the `& mask` form),
+    # 2,000,000 and the identity key hash bins
     n = 3_000_017
     col = ops.splitmix_column(0x5A, 3, n)
     x = col.to_numpy()
