@@ -564,3 +564,230 @@ int32_t fqo_column_partial(const void *col, int32_t col_dtype, int64_t len, int6
     if (t.err.status && errbuf && errlen > 0) snprintf(errbuf, (size_t)errlen, "%s", t.err.msg);
     return t.err.status;
 }
+
+/* ------------------------------------------------------------------ */
+/* GROUP BY (no reference transform: plan_parser.rs:284-308 plans       */
+/* group_expr, pipeline_builder.rs:50-66 ignores it).  The semantics are */
+/* the ungrouped path's per group (fq_ref.py group_by_query states them); */
+/* here a plain CPU hash aggregation over the same 10,000-row blocks:     */
+/* per block materialise, filter, key = key.eval(block), every argument   */
+/* .eval(block), then one open-addressing table insert per row; one      */
+/* table per partition thread, merged after the join.  CPU baseline of    */
+/* the device GROUP BY (bench.py --query g1/g2) and a large-N checker.   */
+/* ------------------------------------------------------------------ */
+#define GEMPTY 0xffffffffffffffffull
+typedef struct {
+    uint64_t *keys;   /* cap slots, GEMPTY = free */
+    uint64_t *st;     /* cap * n_aggs state bits */
+    uint64_t *cnt;    /* rows per group (COUNT states and "seen") */
+    uint64_t cap, used;
+    int has_empty_key; /* the GEMPTY key itself, kept aside */
+    uint64_t empty_cnt, *empty_st;
+} gtab_t;
+
+static uint64_t gmix(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+static uint64_t gident(int32_t op, int32_t dt) {
+    if (op == FQ_AGG_COUNT || op == FQ_AGG_SUM) return 0;
+    if (dt == FQ_DT_FLOAT64) return op == FQ_AGG_MAX ? 0xfff0000000000000ull : 0x7ff0000000000000ull;
+    if (dt == FQ_DT_INT64) return op == FQ_AGG_MAX ? 0x8000000000000000ull : 0x7fffffffffffffffull;
+    return op == FQ_AGG_MAX ? 0ull : ~0ull;
+}
+
+static void gupdate(uint64_t *s, int32_t op, int32_t dt, uint64_t v) {
+    if (op == FQ_AGG_SUM) {
+        *s = dt == FQ_DT_FLOAT64 ? of_f(as_f(*s) + as_f(v)) : *s + v; /* u64/i64 wrap (macros.rs:174) */
+    } else if (op == FQ_AGG_MAX || op == FQ_AGG_MIN) {
+        const int mx = op == FQ_AGG_MAX;
+        int take;
+        if (dt == FQ_DT_FLOAT64) take = mx ? as_f(v) > as_f(*s) : as_f(v) < as_f(*s);
+        else if (dt == FQ_DT_INT64) take = mx ? (int64_t)v > (int64_t)*s : (int64_t)v < (int64_t)*s;
+        else take = mx ? v > *s : v < *s;
+        if (take) *s = v;
+    }
+}
+
+static int gtab_init(gtab_t *t, uint64_t cap, int32_t n_aggs) {
+    memset(t, 0, sizeof(*t));
+    uint64_t c = 1024;
+    while (c < cap) c <<= 1;
+    t->cap = c;
+    t->keys = (uint64_t *)malloc(c * 8);
+    t->st = (uint64_t *)malloc(c * 8 * (size_t)(n_aggs > 0 ? n_aggs : 1));
+    t->cnt = (uint64_t *)calloc(c, 8);
+    t->empty_st = (uint64_t *)malloc(8 * (size_t)(n_aggs > 0 ? n_aggs : 1));
+    if (!t->keys || !t->st || !t->cnt || !t->empty_st) return -1;
+    memset(t->keys, 0xff, c * 8);
+    return 0;
+}
+
+static void gtab_free(gtab_t *t) {
+    free(t->keys);
+    free(t->st);
+    free(t->cnt);
+    free(t->empty_st);
+}
+
+/* slot of key k (claimed if new); NULL when the table is full */
+static uint64_t *gtab_slot(gtab_t *t, uint64_t k, int32_t n_aggs, const int32_t *ops, const int32_t *dts,
+                           uint64_t **cnt) {
+    if (k == GEMPTY) {
+        if (!t->has_empty_key) {
+            t->has_empty_key = 1;
+            for (int a = 0; a < n_aggs; ++a) t->empty_st[a] = gident(ops[a], dts[a]);
+        }
+        *cnt = &t->empty_cnt;
+        return t->empty_st;
+    }
+    uint64_t h = gmix(k) & (t->cap - 1);
+    for (uint64_t p = 0; p < t->cap; ++p) {
+        if (t->keys[h] == k) break;
+        if (t->keys[h] == GEMPTY) {
+            if ((t->used + 1) * 4 > t->cap * 3) return NULL;
+            t->keys[h] = k;
+            t->used++;
+            for (int a = 0; a < n_aggs; ++a) t->st[h * (uint64_t)n_aggs + (uint64_t)a] = gident(ops[a], dts[a]);
+            break;
+        }
+        h = (h + 1) & (t->cap - 1);
+    }
+    *cnt = &t->cnt[h];
+    return &t->st[h * (uint64_t)n_aggs];
+}
+
+typedef struct {
+    uint64_t total;
+    int32_t part, src, n_aggs;
+    uint64_t seed;
+    const fq_pred *pred;
+    const fq_expr *key;
+    const int32_t *ops, *dts;
+    const fq_expr *args;
+    gtab_t tab;
+    err_t err;
+} gjob_t;
+
+static int group_block_fn(void *ctx, uint64_t b, uint64_t e) {
+    gjob_t *j = (gjob_t *)ctx;
+    arr_t blk = arr_new((int64_t)(e - b + 1), FQ_DT_UINT64), filtered, key;
+    arr_t vals[FQ_MAX_GROUP_AGGS];
+    key.v = NULL;
+    for (int a = 0; a < FQ_MAX_GROUP_AGGS; ++a) vals[a].v = NULL;
+    for (uint64_t i = b; i <= e; ++i) blk.v[i - b] = j->src == FQO_SRC_SPLITMIX ? fqo_splitmix64(j->seed, i) : i;
+    const arr_t *x = &blk;
+    int rc = 0;
+    if (j->pred && j->pred->kind == FQ_PRED_EXPR) {
+        if (filter_block(j->pred, &blk, &filtered, &j->err)) rc = j->err.status;
+        else x = &filtered;
+    }
+    if (!rc && eval_chain(j->key, x, &key, &j->err)) rc = j->err.status;
+    for (int a = 0; !rc && a < j->n_aggs; ++a)
+        if (eval_chain(&j->args[a], x, &vals[a], &j->err)) rc = j->err.status;
+    for (int64_t i = 0; !rc && i < x->n; ++i) {
+        uint64_t *cnt;
+        uint64_t *s = gtab_slot(&j->tab, key.v[i], j->n_aggs, j->ops, j->dts, &cnt);
+        if (!s) {
+            rc = set_err(&j->err, FQ_E_TABLE_FULL, "GROUP BY: CPU table full");
+            break;
+        }
+        *cnt += 1;
+        for (int a = 0; a < j->n_aggs; ++a)
+            if (j->ops[a] == FQ_AGG_COUNT) s[a] += 1;
+            else gupdate(&s[a], j->ops[a], j->dts[a], vals[a].v[i]);
+    }
+    for (int a = 0; a < FQ_MAX_GROUP_AGGS; ++a)
+        if (vals[a].v) arr_free(&vals[a]);
+    if (key.v) arr_free(&key);
+    if (x == &filtered) arr_free(&filtered);
+    arr_free(&blk);
+    return rc;
+}
+
+static void *group_thread(void *arg) {
+    gjob_t *j = (gjob_t *)arg;
+    uint64_t b, e;
+    fqo_partition_range(j->total, j->part, &b, &e);
+    numbers_blocks(b, e, group_block_fn, j);
+    return NULL;
+}
+
+int32_t fqo_numbers_group(uint64_t total, int32_t src, uint64_t seed, const fq_pred *pred, const fq_expr *key,
+                          int32_t n_aggs, const int32_t *agg_ops, const int32_t *agg_dtypes, const fq_expr *agg_args,
+                          int32_t n_threads, uint64_t cap_groups, uint64_t *out_keys, uint64_t *out_states,
+                          uint64_t *out_groups, char *errbuf, int32_t errlen) {
+    const int32_t np = fqo_num_partitions(total);
+    *out_groups = 0;
+    if (n_aggs < 1 || n_aggs > FQ_MAX_GROUP_AGGS) return FQ_E_INVALID;
+    gjob_t *jobs = (gjob_t *)calloc((size_t)np, sizeof(gjob_t));
+    int32_t rc = 0;
+    for (int32_t i = 0; i < np && !rc; ++i) {
+        jobs[i].total = total;
+        jobs[i].part = i;
+        jobs[i].src = src;
+        jobs[i].seed = seed;
+        jobs[i].pred = pred;
+        jobs[i].key = key;
+        jobs[i].n_aggs = n_aggs;
+        jobs[i].ops = agg_ops;
+        jobs[i].dts = agg_dtypes;
+        jobs[i].args = agg_args;
+        if (gtab_init(&jobs[i].tab, cap_groups * 2, n_aggs)) rc = FQ_E_INTERNAL;
+    }
+    if (n_threads <= 0 || n_threads > np) n_threads = np;
+    pthread_t *th = (pthread_t *)calloc((size_t)n_threads, sizeof(pthread_t));
+    for (int32_t w = 0; !rc && w < np; w += n_threads) {
+        const int32_t k = (np - w) < n_threads ? (np - w) : n_threads;
+        for (int32_t i = 0; i < k; ++i) pthread_create(&th[i], NULL, group_thread, &jobs[w + i]);
+        for (int32_t i = 0; i < k; ++i) pthread_join(th[i], NULL);
+    }
+    free(th);
+    for (int32_t i = 0; i < np && !rc; ++i)
+        if (jobs[i].err.status) {
+            rc = jobs[i].err.status;
+            if (errbuf && errlen > 0) snprintf(errbuf, (size_t)errlen, "%s", jobs[i].err.msg);
+        }
+    /* merge the partition tables in partition order into table 0 */
+    for (int32_t i = 1; i < np && !rc; ++i) {
+        gtab_t *t = &jobs[i].tab;
+        for (uint64_t h = 0; h <= t->cap && !rc; ++h) {
+            const int empty_key = h == t->cap;
+            if (empty_key ? !t->has_empty_key : t->keys[h] == GEMPTY) continue;
+            const uint64_t k = empty_key ? GEMPTY : t->keys[h];
+            const uint64_t *src_st = empty_key ? t->empty_st : &t->st[h * (uint64_t)n_aggs];
+            uint64_t *cnt;
+            uint64_t *s = gtab_slot(&jobs[0].tab, k, n_aggs, agg_ops, agg_dtypes, &cnt);
+            if (!s) {
+                rc = FQ_E_TABLE_FULL;
+                break;
+            }
+            *cnt += empty_key ? t->empty_cnt : t->cnt[h];
+            for (int a = 0; a < n_aggs; ++a)
+                if (agg_ops[a] == FQ_AGG_COUNT) s[a] += src_st[a];
+                else gupdate(&s[a], agg_ops[a], agg_dtypes[a], src_st[a]);
+        }
+    }
+    if (!rc) {
+        gtab_t *t = &jobs[0].tab;
+        uint64_t g = 0;
+        for (uint64_t h = 0; h <= t->cap; ++h) {
+            const int empty_key = h == t->cap;
+            if (empty_key ? !t->has_empty_key : t->keys[h] == GEMPTY) continue;
+            if (g >= cap_groups) {
+                rc = FQ_E_TABLE_FULL;
+                break;
+            }
+            out_keys[g] = empty_key ? GEMPTY : t->keys[h];
+            memcpy(&out_states[g * (uint64_t)n_aggs], empty_key ? t->empty_st : &t->st[h * (uint64_t)n_aggs],
+                   8 * (size_t)n_aggs);
+            ++g;
+        }
+        *out_groups = g;
+    }
+    for (int32_t i = 0; i < np; ++i) gtab_free(&jobs[i].tab);
+    free(jobs);
+    return rc;
+}

@@ -79,6 +79,17 @@ int32_t fqo_column_partial(const void *col, int32_t col_dtype, int64_t len, int6
                            const fq_expr *agg_args, fqo_state *out_states, char *errbuf,
                            int32_t errlen);
 
+/* GROUP BY over numbers_mt(total) (no reference transform; the ungrouped
+ * path's semantics per group): per partition thread, per 10,000-row block
+ * materialise, filter, key.eval, argument.eval, then one hash-table insert
+ * per row; the partition tables merge in partition order.  Writes up to
+ * cap_groups (key, n_aggs state bits) rows, unordered; *out_groups = groups.
+ * agg_dtypes: the state types (UInt64 / Int64 / Float64).                   */
+int32_t fqo_numbers_group(uint64_t total, int32_t src, uint64_t seed, const fq_pred *pred, const fq_expr *key,
+                          int32_t n_aggs, const int32_t *agg_ops, const int32_t *agg_dtypes, const fq_expr *agg_args,
+                          int32_t n_threads, uint64_t cap_groups, uint64_t *out_keys, uint64_t *out_states,
+                          uint64_t *out_groups, char *errbuf, int32_t errlen);
+
 #ifdef __cplusplus
 }
 #endif

@@ -58,6 +58,10 @@ def load(native=False):
     lib.fqo_column_partial.argtypes = [
         C.c_void_p, C.c_int32, C.c_int64, C.c_int64, P(abi.fq_pred), C.c_int32, P(C.c_int32),
         P(abi.fq_expr), P(fqo_state), C.c_char_p, C.c_int32]
+    lib.fqo_numbers_group.restype = C.c_int32
+    lib.fqo_numbers_group.argtypes = [
+        C.c_uint64, C.c_int32, C.c_uint64, P(abi.fq_pred), P(abi.fq_expr), C.c_int32, P(C.c_int32), P(C.c_int32),
+        P(abi.fq_expr), C.c_int32, C.c_uint64, C.c_void_p, C.c_void_p, P(C.c_uint64), C.c_char_p, C.c_int32]
     return lib
 
 
@@ -129,6 +133,31 @@ def column_partial(arr, dtype, block_rows, aggs, pred=None):
     if rc:
         raise OracleError(rc, err.value.decode())
     return [states[a] for a in range(n)]
+
+
+def numbers_group(total, key, aggs, pred=None, src=SRC_NUMBERS, seed=0, threads=0, cap_groups=1 << 20,
+                  native=False):
+    """GROUP BY over numbers_mt(total): key = fq_expr over the column (None =
+    the column), aggs = [(agg_op, state dtype, fq_expr or None)].  Returns
+    (keys uint64[groups], states uint64[groups, len(aggs)]), unordered."""
+    import numpy as np
+    L = lib(native)
+    n = len(aggs)
+    ops = (C.c_int32 * n)(*[a for a, _, _ in aggs])
+    dts = (C.c_int32 * n)(*[d for _, d, _ in aggs])
+    args = (abi.fq_expr * n)(*[(e if e is not None else _identity(abi.DT_UINT64)) for _, _, e in aggs])
+    k = key if key is not None else _identity(abi.DT_UINT64)
+    keys = np.zeros(cap_groups, np.uint64)
+    states = np.zeros((cap_groups, n), np.uint64)
+    groups = C.c_uint64(0)
+    err = C.create_string_buffer(512)
+    rc = L.fqo_numbers_group(total, src, seed, C.byref(pred) if pred is not None else None, C.byref(k), n, ops, dts,
+                             args, threads, cap_groups, keys.ctypes.data, states.ctypes.data, C.byref(groups), err,
+                             512)
+    if rc:
+        raise OracleError(rc, err.value.decode())
+    g = groups.value
+    return keys[:g], states[:g]
 
 
 # ---------------------------------------------------------------------------

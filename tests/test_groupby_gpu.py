@@ -497,3 +497,27 @@ def test_sql_partitioned_group_by_in_chunks(chunk):
     assert len(got) == len(exp)
     for k, *v in got:
         assert v == [int(t) for t in exp[k]]
+
+
+@pytest.mark.parametrize("key_sql,key_steps,groups", [
+    ("(number*7)%100003", [("*", 7), ("%", 100003)], 100003),  # hashed bins (64-bit magic key)
+    ("number%65536", [("%", 65536)], 65536),                    # range bins (`& mask` form)
+    ("(number/300)%5000", [("/", 300), ("%", 5000)], 5000),     # clustered runs, partitioned or LDS
+])
+def test_sql_group_by_matches_c_oracle_at_scale(eng, key_sql, key_steps, groups):
+    # 4e7 rows through SQL (engine: sample -> LDS table or radix-partitioned
+    # launches) against the C GROUP BY restatement (oracle/fq_oracle.c
+    # fqo_numbers_group) over the same numbers_mt blocks
+    import oracle_c
+    total = 40_000_000
+    r = eng.execute("SELECT %s, count(number), sum(number), max(number+1), min(number) FROM system.numbers_mt(%d) "
+                    "WHERE number%%5 < 3 GROUP BY %s" % (key_sql, total, key_sql))
+    key = chain(U, key_steps)[0]
+    pred = predicate(U, [("%", 5)], "<", 3)
+    aggs = [(abi.AGG_COUNT, U, None), (abi.AGG_SUM, U, None), (abi.AGG_MAX, U, chain(U, [("+", 1)])[0]),
+            (abi.AGG_MIN, U, None)]
+    keys, st = oracle_c.numbers_group(total, key, aggs, pred=pred, threads=8, cap_groups=2 * groups)
+    o = np.argsort(keys)
+    exp = [(int(k),) + tuple(int(x) for x in s) for k, s in zip(keys[o], st[o])]
+    assert len(r.rows) == len(exp)
+    assert [tuple(row) for row in r.rows] == exp

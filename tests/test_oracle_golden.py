@@ -270,3 +270,42 @@ def test_splitmix_column_oracle():
     col = np.array([L.fqo_splitmix64(7, i) for i in range(30000)], dtype=np.uint64)
     st = oracle_c.column_partial(col, abi.DT_UINT64, 10000, [(abi.AGG_SUM, None), (abi.AGG_MAX, None)])
     assert st[0].bits == int(col.sum(dtype=np.uint64)) and st[1].bits == int(col.max())
+
+
+@pytest.mark.parametrize("total", [100001, 1_000_000, 2_400_000])
+def test_c_group_by_matches_numpy_oracle(total):
+    # the C GROUP BY (bench.py's GROUP BY CPU baseline) against fq_ref's
+    # statement of the GROUP BY semantics, on numbers_mt sizes that drop rows
+    # (100001: the NumbersStream quirk) and with a filter
+    U = abi.DT_UINT64
+    key = chain(U, [("%", 37)])[0]
+    pred = predicate(U, [("%", 8)], "<", 3)
+    v1 = chain(U, [("+", 1)])[0]
+    aggs = [(abi.AGG_COUNT, U, None), (abi.AGG_SUM, U, None), (abi.AGG_MAX, U, v1), (abi.AGG_MIN, U, None)]
+    keys, st = oracle_c.numbers_group(total, key, aggs, pred=pred, threads=8, cap_groups=64)
+    o = np.argsort(keys)
+    got = [(int(k),) + tuple(int(x) for x in s) for k, s in zip(keys[o], st[o])]
+    N = R.E_field("number")
+    c = R.E_const
+    exp = R.group_by_query(total, R.E_bin("%", N, c(37)),
+                           [R.E_fn("count", N), R.E_fn("sum", N), R.E_fn("max", R.E_bin("+", N, c(1))),
+                            R.E_fn("min", N)],
+                           where=R.E_bin("<", R.E_bin("%", N, c(8)), c(3)))
+    assert got == [tuple(r) for r in exp]
+
+
+def test_c_group_by_closed_form_and_errors():
+    U = abi.DT_UINT64
+    n, m = 8_000_000, 1000
+    keys, st = oracle_c.numbers_group(n, chain(U, [("%", m)])[0],
+                                      [(abi.AGG_COUNT, U, None), (abi.AGG_SUM, U, None), (abi.AGG_MAX, U, None)],
+                                      threads=8, cap_groups=2 * m)
+    per = n // m
+    o = np.argsort(keys)
+    assert [(int(k), int(a), int(b), int(x)) for k, (a, b, x) in zip(keys[o], st[o])] == \
+        [(k, per, (k * per + m * per * (per - 1) // 2) % 2**64, k + m * (per - 1)) for k in range(m)]
+    with pytest.raises(oracle_c.OracleError):  # more groups than the caller's buffer
+        oracle_c.numbers_group(100_000, None, [(abi.AGG_COUNT, U, None)], threads=8, cap_groups=1000)
+    with pytest.raises(oracle_c.OracleError) as ei:  # 7 / (number % 2): divide by zero
+        oracle_c.numbers_group(10_000, chain(U, [("%", 2), ("/", 7, True)])[0], [(abi.AGG_COUNT, U, None)])
+    assert "Divide by zero" in str(ei.value)
