@@ -69,6 +69,12 @@ QUERIES = {
            "GROUP BY number%100000", 0),
 }
 GROUP_MOD = {"g1": 1000, "g2": 100000}
+# not a BASELINE config: FilterTransform -> ProjectionTransform (SURVEY 8f rank
+# 1), the README's expressions without its LIMIT.  Its result is 3.75e9 rows x 2
+# columns (60 GB): measured at the C ABI the engine's ProjectionTransform calls
+# per block (fq_filter_project over each resident numbers_mt partition, outputs
+# in HBM), checked by kept count and per-column wrapping sums (closed forms).
+PROJECT_SQL = "SELECT number+1, number/2 FROM system.numbers_mt({N}) WHERE (number%8)<3"
 
 
 def closed_form(query, n):
@@ -98,6 +104,20 @@ def closed_form(query, n):
     while top % 8 >= 3:
         top -= 1
     return [top + 1]
+
+
+def project_closed_form(b, e):
+    """(kept rows, sum(number+1), sum(number/2)) over rows b..e with number%8 < 3."""
+    kept = s1 = s2 = 0
+    for c in range(3):
+        j0 = max(0, -(-(b - c) // 8))
+        j1 = (e - c) // 8 if e >= c else -1
+        cnt = max(0, j1 - j0 + 1)
+        sj = (j0 + j1) * cnt // 2
+        kept += cnt
+        s1 += 8 * sj + cnt * (c + 1)
+        s2 += 4 * sj + cnt * (c // 2)
+    return kept, s1 % U64, s2 % U64
 
 
 def log(rank, *a):
@@ -184,6 +204,153 @@ def cpu_baseline(sample_rows, threads, query="c3"):
     }
 
 
+def cpu_baseline_project(sample_rows, threads):
+    """Filter -> Projection on the host cores: oracle/fq_oracle.c
+    fqo_numbers_project (per 10,000-row block: compaction, then each
+    expression into its own array), over numbers_mt(sample_rows)."""
+    import oracle_c
+    from fq_amd.expr import chain, predicate
+    native = True
+    try:
+        oracle_c.build(native=True)
+    except Exception:
+        native = False
+    U = abi.DT_UINT64
+    pred = predicate(U, [("%", 8)], "<", 3)
+    outs = [chain(U, [("+", 1)])[0], chain(U, [("/", 2)])[0]]
+    n = sample_rows - sample_rows % 80_000
+    oracle_c.numbers_project(8_000_000, outs, pred=pred, threads=threads, native=native)  # warm
+    t0 = time.perf_counter()
+    kept, sums = oracle_c.numbers_project(n, outs, pred=pred, threads=threads, native=native)
+    dt = time.perf_counter() - t0
+    assert (kept, sums[0], sums[1]) == project_closed_form(0, n - 1), "cpu baseline parity"
+    return {
+        "value": n / dt, "unit": "rows/s", "cores": threads, "kind": "port",
+        "sample": "P1 over numbers_mt(%d): 8 partitions, one thread per partition, 10,000-row blocks regenerated "
+                  "per block, FilterTransform compaction then each projected expression into its own array "
+                  "(transform_filter.rs:38-55, transform_projection.rs:45-56; oracle/fq_oracle.c "
+                  "fqo_numbers_project, %s); %.2f s wall on %s (nproc=%d)"
+                  % (n, "-O3 -march=native" if native else "-O3 -march=x86-64-v2", dt, _cpu_model(),
+                     os.cpu_count() or 0),
+    }
+
+
+def run_project(args, rank, world):
+    """--query p1: fq_filter_project over this rank's resident numbers_mt
+    partitions, outputs in HBM; one step = every partition once."""
+    import ctypes as C
+
+    from fq_amd._lib import check, lib
+    from fq_amd.expr import chain, predicate
+    if args.rows_total:
+        n_total = int(args.rows_total)
+    else:
+        n_total = int(args.rows_per_gpu) * world
+    sql = PROJECT_SQL.format(N=n_total)
+    mine = shard(generate_parts(n_total), rank, world)
+    U = abi.DT_UINT64
+    cols, expect = [], []
+    for _, b, e in mine:
+        rows = stream_rows(b, e)
+        if rows != e - b + 1:
+            raise SystemExit("p1 needs numbers_mt(N) with whole 10,000-row blocks per partition")
+        cols.append(ops.numbers_column(b, rows))
+        expect.append(project_closed_form(b, e))
+    maxr = max(c.len for c in cols)
+    outs = [ops.empty_column(maxr, U), ops.empty_column(maxr, U)]
+    ws = ops.Workspace(lib.fq_filter_project_workspace_bytes(maxr))
+    pred = predicate(U, [("%", 8)], "<", 3)
+    exprs = (abi.fq_expr * 2)(chain(U, [("+", 1)])[0], chain(U, [("/", 2)])[0])
+    ptrs = (C.c_void_p * 2)(outs[0].ptr, outs[1].ptr)
+    kept = C.c_int64(0)
+    stream = torch.cuda.current_stream()
+    sp = C.c_void_p(stream.cuda_stream)
+    torch.cuda.synchronize()
+    total_rows = sum(c.len for c in cols)
+    log(rank, "p1: %d partitions, %d rows (%.1f GB) resident on rank %d" % (len(cols), total_rows, total_rows * 8 / 1e9,
+                                                                           rank))
+
+    def launch(col):
+        c = col.col()
+        check(lib.fq_filter_project(C.byref(c), C.byref(pred), exprs, 2, ptrs, C.byref(kept), ws.ptr, ws.nbytes, sp))
+        return kept.value
+
+    def wsum(col_out, n):
+        return int(col_out.buf[:n * 8].view(torch.int64).sum().item()) % U64
+
+    for _ in range(max(args.warmup, 1)):
+        for col, exp in zip(cols, expect):
+            k = launch(col)
+            got = (k, wsum(outs[0], k), wsum(outs[1], k))
+            if got != exp:
+                raise SystemExit("PARITY FAILURE: got %r expected %r" % (got, exp))
+    log(rank, "result: kept rows and per-column wrapping sums == closed form on every partition")
+    evs = []
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    kept_total = 0
+    for _ in range(args.steps):
+        for col in cols:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            kept_total += launch(col)
+            e1.record(stream)
+            evs.append((e0, e1, col.len))
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda" if args.dist_backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    k_last = kept.value
+    if (k_last, wsum(outs[0], k_last), wsum(outs[1], k_last)) != expect[-1]:
+        raise SystemExit("PARITY FAILURE after the timed steps")
+    ms = [e0.elapsed_time(e1) for e0, e1, _ in evs]
+    avg_ms = sum(ms) / len(ms)
+    kept_per_launch = kept_total / len(evs)
+    rows_per_launch = sum(r for _, _, r in evs) / len(evs)
+    bytes_per_launch = 8 * rows_per_launch + 16 * kept_per_launch
+    achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
+    value = n_total * args.steps / dt
+    if rank == 0:
+        traffic = None
+        pmc = latest_pmc_traffic("fq_jit_pselect", "p1")
+        if pmc and pmc[1]:
+            traffic = pmc[0] * rows_per_launch / pmc[1]
+        out = {
+            "metric": METRIC, "value": value, "unit": "rows/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "strong" if args.rows_total else "weak", "vs_baseline": None,
+            "vs_baseline_ref": "no published reference number for this query",
+            "dtype": "u64", "data": "synthetic: system.numbers_mt iota column (u64), resident in HBM before timing",
+            "config": {"workload": sql, "query": "p1", "rows_per_gpu": total_rows, "rows_total": n_total,
+                       "partitions_per_gpu": len(cols), "block_rows": BLOCK_SIZE,
+                       "path": "fq_filter_project per resident partition (the C ABI call of the engine's "
+                               "ProjectionTransform): predicate, decoupled look-back, both expressions, outputs in HBM",
+                       "parallelism": "dp%d (numbers_mt partitions sharded)" % world},
+            "achieved_hbm_gbps": achieved, "kernel_ms_per_launch": avg_ms, "scan_launches_per_step": len(cols),
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
+                         "kernel": "fq_jit_pselect (fq_filter_project, hipRTC-specialised), one launch per partition; "
+                                   "algorithmic bytes = 8 B per row read + 16 B per kept row written",
+                         "bytes_per_launch": bytes_per_launch},
+            "result": {"kept_rows_per_step": kept_total // args.steps},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            try:
+                out["cpu_baseline"] = cpu_baseline_project(int(args.cpu_sample_rows or 1e10), args.cpu_threads)
+            except Exception as e:  # report, never hide
+                out["cpu_baseline"] = {"error": repr(e)}
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def _cpu_model():
     cpu = platform.processor() or platform.machine()
     try:
@@ -236,14 +403,14 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--query", default="c3", choices=sorted(QUERIES))
+    ap.add_argument("--query", default="c3", choices=sorted(list(QUERIES) + ["p1"]))
     ap.add_argument("--rows-per-gpu", type=float, default=1e10)
     ap.add_argument("--rows-total", type=float, default=None,
                     help="strong scaling: fix numbers_mt(N) at this N for every GPU count "
                          "(e.g. 1e10 = the 10B-row metric split over 1/2/4/8 GPUs)")
     ap.add_argument("--cpu-sample-rows", type=float, default=None,
-                    help="rows of the CPU-baseline sample (default: the whole 1e10-row workload for the aggregate "
-                         "queries, ~1.5 s on the box's 8 threads; 1.6e9 rows for GROUP BY, a hash insert per row)")
+                    help="rows of the CPU-baseline sample (default: the whole 1e10-row workload, ~1.5 s on the "
+                         "box's 8 threads for c3, ~5 s for p1; 4e9 rows for GROUP BY, a hash insert per row, ~3-10 s)")
     ap.add_argument("--cpu-threads", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--streams", type=int, default=1,
@@ -266,6 +433,8 @@ def main():
         else:
             dist.init_process_group("gloo")
 
+    if args.query == "p1":
+        return run_project(args, rank, world)
     if args.rows_total:
         n_total = int(args.rows_total)
         rows_per_gpu = n_total // world
@@ -405,7 +574,7 @@ def main():
         dist.barrier()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
-            sample = args.cpu_sample_rows or (1.6e9 if args.query in GROUP_MOD else 1e10)
+            sample = args.cpu_sample_rows or (4e9 if args.query in GROUP_MOD else 1e10)
             out["cpu_baseline"] = cpu_baseline(int(sample), args.cpu_threads, args.query)
         except Exception as e:  # report, never hide
             out["cpu_baseline"] = {"error": repr(e)}

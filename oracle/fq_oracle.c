@@ -791,3 +791,91 @@ int32_t fqo_numbers_group(uint64_t total, int32_t src, uint64_t seed, const fq_p
     free(jobs);
     return rc;
 }
+
+/* ------------------------------------------------------------------ */
+/* FilterTransform -> ProjectionTransform over numbers_mt               */
+/* (transform_filter.rs:38-55, transform_projection.rs:45-56): per      */
+/* 10,000-row block materialise, filter_record_batch (compaction), then */
+/* every projected expression evaluated into its own array.  The arrays */
+/* are folded into per-output wrapping sums of the value bits (the      */
+/* result would be 16 B per kept row: the checker compares sums and the */
+/* kept count with closed forms).  CPU baseline of bench.py --query p1.  */
+/* ------------------------------------------------------------------ */
+typedef struct {
+    uint64_t total;
+    int32_t part, n_out;
+    const fq_pred *pred;
+    const fq_expr *outs;
+    uint64_t kept, sums[FQ_MAX_PROJECT];
+    err_t err;
+} pjob_t;
+
+static int project_block_fn(void *ctx, uint64_t b, uint64_t e) {
+    pjob_t *j = (pjob_t *)ctx;
+    arr_t blk = arr_new((int64_t)(e - b + 1), FQ_DT_UINT64), filtered;
+    for (uint64_t i = b; i <= e; ++i) blk.v[i - b] = i;
+    const arr_t *x = &blk;
+    int rc = 0;
+    if (j->pred && j->pred->kind == FQ_PRED_EXPR) {
+        if (filter_block(j->pred, &blk, &filtered, &j->err)) rc = j->err.status;
+        else x = &filtered;
+    }
+    if (!rc) j->kept += (uint64_t)x->n;
+    for (int o = 0; !rc && o < j->n_out; ++o) {
+        arr_t v;
+        if (eval_chain(&j->outs[o], x, &v, &j->err)) {
+            rc = j->err.status;
+            break;
+        }
+        uint64_t s = 0;
+        for (int64_t i = 0; i < v.n; ++i) s += v.v[i];
+        j->sums[o] += s;
+        arr_free(&v);
+    }
+    if (x == &filtered) arr_free(&filtered);
+    arr_free(&blk);
+    return rc;
+}
+
+static void *project_thread(void *arg) {
+    pjob_t *j = (pjob_t *)arg;
+    uint64_t b, e;
+    fqo_partition_range(j->total, j->part, &b, &e);
+    numbers_blocks(b, e, project_block_fn, j);
+    return NULL;
+}
+
+int32_t fqo_numbers_project(uint64_t total, const fq_pred *pred, int32_t n_out, const fq_expr *outs,
+                            int32_t n_threads, uint64_t *out_kept, uint64_t *out_sums, char *errbuf, int32_t errlen) {
+    const int32_t np = fqo_num_partitions(total);
+    if (n_out < 1 || n_out > FQ_MAX_PROJECT) return FQ_E_INVALID;
+    pjob_t *jobs = (pjob_t *)calloc((size_t)np, sizeof(pjob_t));
+    for (int32_t i = 0; i < np; ++i) {
+        jobs[i].total = total;
+        jobs[i].part = i;
+        jobs[i].n_out = n_out;
+        jobs[i].pred = pred;
+        jobs[i].outs = outs;
+    }
+    if (n_threads <= 0 || n_threads > np) n_threads = np;
+    pthread_t *th = (pthread_t *)calloc((size_t)n_threads, sizeof(pthread_t));
+    for (int32_t w = 0; w < np; w += n_threads) {
+        const int32_t k = (np - w) < n_threads ? (np - w) : n_threads;
+        for (int32_t i = 0; i < k; ++i) pthread_create(&th[i], NULL, project_thread, &jobs[w + i]);
+        for (int32_t i = 0; i < k; ++i) pthread_join(th[i], NULL);
+    }
+    free(th);
+    int32_t rc = 0;
+    *out_kept = 0;
+    for (int o = 0; o < n_out; ++o) out_sums[o] = 0;
+    for (int32_t i = 0; i < np; ++i) {
+        if (jobs[i].err.status && !rc) {
+            rc = jobs[i].err.status;
+            if (errbuf && errlen > 0) snprintf(errbuf, (size_t)errlen, "%s", jobs[i].err.msg);
+        }
+        *out_kept += jobs[i].kept;
+        for (int o = 0; o < n_out; ++o) out_sums[o] += jobs[i].sums[o];
+    }
+    free(jobs);
+    return rc;
+}

@@ -90,6 +90,13 @@ int32_t fqo_numbers_group(uint64_t total, int32_t src, uint64_t seed, const fq_p
                           int32_t n_threads, uint64_t cap_groups, uint64_t *out_keys, uint64_t *out_states,
                           uint64_t *out_groups, char *errbuf, int32_t errlen);
 
+/* FilterTransform -> ProjectionTransform over numbers_mt(total), per
+ * 10,000-row block (compaction, then every expression into its own array),
+ * one thread per partition; the outputs folded into *out_kept and per-output
+ * wrapping sums of the value bits (out_sums[n_out]).                         */
+int32_t fqo_numbers_project(uint64_t total, const fq_pred *pred, int32_t n_out, const fq_expr *outs,
+                            int32_t n_threads, uint64_t *out_kept, uint64_t *out_sums, char *errbuf, int32_t errlen);
+
 #ifdef __cplusplus
 }
 #endif

@@ -62,6 +62,9 @@ def load(native=False):
     lib.fqo_numbers_group.argtypes = [
         C.c_uint64, C.c_int32, C.c_uint64, P(abi.fq_pred), P(abi.fq_expr), C.c_int32, P(C.c_int32), P(C.c_int32),
         P(abi.fq_expr), C.c_int32, C.c_uint64, C.c_void_p, C.c_void_p, P(C.c_uint64), C.c_char_p, C.c_int32]
+    lib.fqo_numbers_project.restype = C.c_int32
+    lib.fqo_numbers_project.argtypes = [C.c_uint64, P(abi.fq_pred), C.c_int32, P(abi.fq_expr), C.c_int32,
+                                        P(C.c_uint64), P(C.c_uint64), C.c_char_p, C.c_int32]
     return lib
 
 
@@ -158,6 +161,22 @@ def numbers_group(total, key, aggs, pred=None, src=SRC_NUMBERS, seed=0, threads=
         raise OracleError(rc, err.value.decode())
     g = groups.value
     return keys[:g], states[:g]
+
+
+def numbers_project(total, outs, pred=None, threads=0, native=False):
+    """Filter -> Projection over numbers_mt(total): outs = [fq_expr or None].
+    Returns (kept rows, [wrapping sum of each output's value bits])."""
+    L = lib(native)
+    n = len(outs)
+    ex = (abi.fq_expr * n)(*[(e if e is not None else _identity(abi.DT_UINT64)) for e in outs])
+    kept = C.c_uint64(0)
+    sums = (C.c_uint64 * n)()
+    err = C.create_string_buffer(512)
+    rc = L.fqo_numbers_project(total, C.byref(pred) if pred is not None else None, n, ex, threads, C.byref(kept),
+                               sums, err, 512)
+    if rc:
+        raise OracleError(rc, err.value.decode())
+    return kept.value, list(sums)
 
 
 # ---------------------------------------------------------------------------

@@ -309,3 +309,19 @@ def test_c_group_by_closed_form_and_errors():
     with pytest.raises(oracle_c.OracleError) as ei:  # 7 / (number % 2): divide by zero
         oracle_c.numbers_group(10_000, chain(U, [("%", 2), ("/", 7, True)])[0], [(abi.AGG_COUNT, U, None)])
     assert "Divide by zero" in str(ei.value)
+
+
+def test_c_filter_projection_closed_form():
+    # the C Filter -> Projection restatement (bench.py --query p1's CPU
+    # baseline): kept rows and wrapping sums of number+1, number/2 over the
+    # rows with number%8 < 3, against numpy over fq_ref's NumbersStream blocks
+    # on a quirky size (100001 drops rows)
+    U = abi.DT_UINT64
+    pred = predicate(U, [("%", 8)], "<", 3)
+    outs = [chain(U, [("+", 1)])[0], chain(U, [("/", 2)])[0]]
+    for total in (100001, 800_000):
+        kept, sums = oracle_c.numbers_project(total, outs, pred=pred, threads=8)
+        x = np.concatenate([np.asarray(b.cols["number"].values, dtype=np.uint64) for b in R.numbers_stream(total)])
+        x = x[(x % np.uint64(8)) < 3]
+        assert kept == len(x)
+        assert sums == [int((x + np.uint64(1)).sum(dtype=np.uint64)), int((x // np.uint64(2)).sum(dtype=np.uint64))]
