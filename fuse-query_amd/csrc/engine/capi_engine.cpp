@@ -1,6 +1,7 @@
 // C ABI of the engine (include/fq_engine.h).
 #include <string.h>
 
+#include <functional>
 #include <iterator>
 #include <memory>
 #include <mutex>
@@ -291,8 +292,9 @@ fq_status fq_engine_execute_partial(fq_engine *e, const char *sql, int32_t rank,
                 fq::StreamRef s = p.execute();
                 fq::DataBlock b;
                 while (s->next(b)) {
-                    const auto &rows = *b.columns.at(0).host;
-                    for (const auto &v : rows) per_func.push_back(v.fields);
+                    auto &rows = *b.columns.at(0).host;  // this block is ours: move the rows out
+                    per_func.reserve(per_func.size() + rows.size());
+                    for (auto &v : rows) per_func.push_back(std::move(v.fields));
                 }
             } catch (const fq::FQException &ex) {  // GROUP BY table full: 16x the slots
                 if (!grow_group_table(e, ex, attempt)) throw;
@@ -300,7 +302,10 @@ fq_status fq_engine_execute_partial(fq_engine *e, const char *sql, int32_t rank,
             }
             break;
         }
-        const std::vector<uint8_t> enc = fq::encode_states(per_func);
+        // GROUP BY rows travel as flat arrays when they can (fq::encode_group_rows)
+        std::vector<uint8_t> enc;
+        if (!aggregate_node(partial)->groups.empty()) enc = fq::encode_group_rows(per_func);
+        if (enc.empty()) enc = fq::encode_states(per_func);
         *len = enc.size();
         if (!buf || cap < enc.size())
             throw fq::FQException(FQ_E_INVALID, "fq_engine_execute_partial: buffer too small (need " +
@@ -309,6 +314,86 @@ fq_status fq_engine_execute_partial(fq_engine *e, const char *sql, int32_t rank,
         e->rt->stats.queries++;
     });
 }
+
+}  // extern "C"
+
+namespace {
+
+// The cross-GPU GROUP BY final: every rank's flat rows into one fresh device
+// table (sized for all of them), ready for GroupByFinalTransform's extract.
+// Empty when there are no rows at all (the host path makes the empty result).
+std::shared_ptr<fq::GroupByShared> merge_group_rows_on_device(
+    fq_engine *e, const fq::PlanNode &agg, const fq::QueryContext &qctx, int32_t world,
+    const std::function<const uint8_t *(int32_t)> &row_ptr, size_t stride, fq::ExecCtx &ctx) {
+    (void)e;
+    std::vector<fq::AggregatorFunction *> leaves;
+    std::vector<fq::FunctionRef> fs;
+    for (const auto &x : agg.exprs) fs.push_back(x.to_function(qctx.factory));
+    for (auto &f : fs) f->collect_aggregators(leaves);
+    const size_t nl = leaves.size();
+    std::vector<fq::GroupRows> parts;
+    size_t total = 0;
+    fq::DataType kdt = FQ_DT_NULL;
+    std::vector<fq::DataType> dts(nl, FQ_DT_NULL);
+    for (int32_t r = 0; r < world; ++r) {
+        parts.push_back(fq::decode_group_rows(row_ptr(r), stride));
+        const fq::GroupRows &g = parts.back();
+        if (g.keys.empty()) continue;
+        if (g.st.size() != nl) throw fq::FQException(FQ_E_INVALID, "GROUP BY: malformed partial state row");
+        kdt = g.key_dtype;
+        dts = g.dtypes;
+        total += g.keys.size();
+    }
+    if (total == 0) return nullptr;
+    if (kdt != FQ_DT_UINT64 && kdt != FQ_DT_INT64) return nullptr;  // the host path reports it
+    auto shared = std::make_shared<fq::GroupByShared>();
+    fq_group_table &d = shared->desc;
+    d = fq_group_table{};
+    d.key_dtype = kdt;
+    if (nl == 0) {  // keys only: a dummy Count keeps the table valid
+        d.n_aggs = 1;
+        d.kinds[0] = FQ_AGG_COUNT;
+        d.dtypes[0] = FQ_DT_UINT64;
+        shared->dummy_count = true;
+    } else {
+        d.n_aggs = (int32_t)nl;
+        for (size_t a = 0; a < nl; ++a) {
+            d.kinds[a] = (int32_t)leaves[a]->op();
+            d.dtypes[a] = leaves[a]->op() == FQ_AGG_COUNT ? FQ_DT_UINT64 : dts[a];
+            shared->leaf_ops.push_back(leaves[a]->op());
+        }
+    }
+    int64_t cap = 64;
+    while (cap < (int64_t)(2 * total)) cap <<= 1;
+    d.capacity = cap;
+    shared->mem = fq::DeviceBuffer::alloc(fq_group_table_bytes(cap, d.n_aggs), ctx.stream());
+    d.d_mem = shared->mem->ptr;
+    fq::check_fq(fq_group_table_init(&d, ctx.stream()));
+    // all ranks' rows back to back: keys[total], then each state array
+    const size_t na = (size_t)d.n_aggs;
+    std::vector<uint64_t> host(total * (1 + na), 0);
+    size_t at = 0;
+    for (const fq::GroupRows &g : parts) {
+        const size_t n = g.keys.size();
+        std::copy(g.keys.begin(), g.keys.end(), host.begin() + (long)at);
+        for (size_t a = 0; a < nl; ++a) std::copy(g.st[a].begin(), g.st[a].end(), host.begin() + (long)((1 + a) * total + at));
+        at += n;
+    }
+    auto stage = fq::DeviceBuffer::alloc(host.size() * 8, ctx.stream());
+    fq::check_hip(hipMemcpyAsync(stage->ptr, host.data(), host.size() * 8, hipMemcpyHostToDevice, ctx.stream()),
+                  "hipMemcpyAsync");
+    const uint64_t *dk = (const uint64_t *)stage->ptr;
+    const uint64_t *ds[FQ_MAX_GROUP_AGGS] = {};
+    for (size_t a = 0; a < na; ++a) ds[a] = dk + (1 + a) * total;
+    fq::check_fq(fq_group_table_merge(&d, dk, ds, (int64_t)total, ctx.stream()));
+    ctx.sync();  // the staging copy's host vector and the stage buffer go out of scope
+    shared->ready = true;
+    return shared;
+}
+
+}  // namespace
+
+extern "C" {
 
 fq_status fq_engine_execute_final(fq_engine *e, const char *sql, const void *states, size_t stride, int32_t world,
                                   fq_result **out) {
@@ -320,11 +405,32 @@ fq_status fq_engine_execute_final(fq_engine *e, const char *sql, const void *sta
         fq::QueryPlan plan = plan_for(e, sql, *qctx);
         const fq::PlanNode *agg = aggregate_node(plan);
         if (plan.explain || !agg) throw fq::FQException(FQ_E_UNSUPPORTED, "distributed execution covers aggregate queries only");
+        const bool grouped = !agg->groups.empty();
+        auto row_ptr = [&](int32_t r) { return (const uint8_t *)states + (size_t)r * stride; };
+        // GROUP BY with every rank's rows as flat arrays and a GPU here: the
+        // rows are merged into one device table (fq_group_table_merge) that
+        // the final transform then extracts, as after a local GROUP BY
+        std::shared_ptr<fq::GroupByShared> merged;
+        if (grouped && e->rt->has_device()) {
+            bool flat = true;
+            for (int32_t r = 0; r < world && flat; ++r) flat = fq::is_group_rows(row_ptr(r), stride);
+            if (flat) merged = merge_group_rows_on_device(e, *agg, *qctx, world, row_ptr, stride, ctx);
+        }
         std::vector<fq::DataBlock> blocks;
-        for (int32_t r = 0; r < world; ++r) {
-            auto per_func = fq::decode_states((const uint8_t *)states + (size_t)r * stride, stride);
+        for (int32_t r = 0; r < world && !merged; ++r) {
             std::vector<fq::DataValue> rows;
-            for (auto &v : per_func) rows.push_back(fq::DataValue::make_struct(std::move(v)));
+            if (fq::is_group_rows(row_ptr(r), stride)) {
+                const fq::GroupRows g = fq::decode_group_rows(row_ptr(r), stride);
+                for (size_t i = 0; i < g.keys.size(); ++i) {
+                    std::vector<fq::DataValue> row;
+                    row.push_back(fq::DataValue::some(g.key_dtype, g.keys[i]));
+                    for (size_t a = 0; a < g.st.size(); ++a) row.push_back(fq::DataValue::some(g.dtypes[a], g.st[a][i]));
+                    rows.push_back(fq::DataValue::make_struct(std::move(row)));
+                }
+            } else {
+                auto per_func = fq::decode_states(row_ptr(r), stride);
+                for (auto &v : per_func) rows.push_back(fq::DataValue::make_struct(std::move(v)));
+            }
             fq::DataBlock b;
             b.schema = agg->schema;
             b.columns.push_back(fq::Column::host_values(FQ_DT_NULL, std::move(rows)));
@@ -335,9 +441,9 @@ fq_status fq_engine_execute_final(fq_engine *e, const char *sql, const void *sta
         p.add_simple_transform([&]() -> fq::ProcessorRef {
             std::vector<fq::FunctionRef> fs;
             for (const auto &x : agg->exprs) fs.push_back(x.to_function(qctx->factory));
-            if (!agg->groups.empty())  // merge exchanged groups by key on the host
-                return std::make_shared<fq::GroupByFinalTransform>(agg->schema, fs,
-                                                                   std::make_shared<fq::GroupByShared>(), false);
+            if (grouped)  // merged on the device, or exchanged groups merged by key on the host
+                return std::make_shared<fq::GroupByFinalTransform>(
+                    agg->schema, fs, merged ? merged : std::make_shared<fq::GroupByShared>(), false);
             return std::make_shared<fq::AggregateFinalTransform>(agg->schema, fs);
         });
         for (const auto &n : plan.nodes)

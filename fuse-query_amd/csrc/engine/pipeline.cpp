@@ -787,21 +787,28 @@ StreamRef GroupByFinalTransform::execute() {
             ctx.sync();
         }
     }
-    // sort by key (Int64 numerically: the sign bit flipped orders it as
-    // unsigned), then fold each run of equal keys into its first row
-    const uint64_t flip = kdt == FQ_DT_INT64 ? (1ull << 63) : 0ull;
-    std::vector<std::pair<uint64_t, uint32_t>> order(keys.size());
-    for (size_t i = 0; i < keys.size(); ++i) order[i] = {keys[i] ^ flip, (uint32_t)i};
-    std::sort(order.begin(), order.end());
     std::vector<uint32_t> rows;  // one source row per group, in key order
-    rows.reserve(order.size());
-    for (size_t i = 0; i < order.size();) {
-        const uint32_t r0 = order[i].second;
-        size_t j = i + 1;
-        for (; j < order.size() && order[j].first == order[i].first; ++j)
-            for (size_t a = 0; a < nl; ++a) ls[a].fold_into(leaves[a]->op(), r0, order[j].second);
-        rows.push_back(r0);
-        i = j;
+    if (emit_states_ && exchanged.empty()) {
+        // partial states of this rank's own table: the keys are unique and
+        // the receiving final merges and orders them, so no sort here
+        rows.resize(keys.size());
+        for (size_t i = 0; i < keys.size(); ++i) rows[i] = (uint32_t)i;
+    } else {
+        // sort by key (Int64 numerically: the sign bit flipped orders it as
+        // unsigned), then fold each run of equal keys into its first row
+        const uint64_t flip = kdt == FQ_DT_INT64 ? (1ull << 63) : 0ull;
+        std::vector<std::pair<uint64_t, uint32_t>> order(keys.size());
+        for (size_t i = 0; i < keys.size(); ++i) order[i] = {keys[i] ^ flip, (uint32_t)i};
+        std::sort(order.begin(), order.end());
+        rows.reserve(order.size());
+        for (size_t i = 0; i < order.size();) {
+            const uint32_t r0 = order[i].second;
+            size_t j = i + 1;
+            for (; j < order.size() && order[j].first == order[i].first; ++j)
+                for (size_t a = 0; a < nl; ++a) ls[a].fold_into(leaves[a]->op(), r0, order[j].second);
+            rows.push_back(r0);
+            i = j;
+        }
     }
     DataBlock out;
     out.schema = schema_;
@@ -996,6 +1003,66 @@ std::vector<std::vector<DataValue>> decode_states(const uint8_t *p, size_t n) {
         out.push_back(std::move(vals));
     }
     return out;
+}
+
+// "FQG1", u32 n_leaves, u64 n, i32 key dtype, i32 pad, i32 leaf dtypes
+// [n_leaves] (padded to 8 B), keys[n], states[leaf][n]
+std::vector<uint8_t> encode_group_rows(const std::vector<std::vector<DataValue>> &rows) {
+    const size_t nl = rows.empty() ? 0 : rows[0].size() - 1;
+    if (!rows.empty() && rows[0].empty()) return {};
+    std::vector<DataType> dts(nl, FQ_DT_NULL);
+    DataType kdt = FQ_DT_NULL;
+    for (const auto &r : rows) {
+        if (r.size() != nl + 1) return {};
+        for (size_t a = 0; a <= nl; ++a) {
+            const DataValue &v = r[a];
+            if (v.kind != DataValue::kSome || dtype_size(v.dtype) != 8 || v.dtype == FQ_DT_UTF8) return {};
+            DataType &want = a == 0 ? kdt : dts[a - 1];
+            if (want == FQ_DT_NULL) want = v.dtype;
+            else if (want != v.dtype) return {};
+        }
+    }
+    const size_t n = rows.size(), hdr = 24 + ((nl * 4 + 7) / 8) * 8;
+    std::vector<uint8_t> out(hdr + n * 8 * (1 + nl));
+    memcpy(out.data(), "FQG1", 4);
+    const uint32_t nl32 = (uint32_t)nl;
+    const uint64_t n64 = n;
+    const int32_t kd[2] = {kdt, 0};
+    memcpy(out.data() + 4, &nl32, 4);
+    memcpy(out.data() + 8, &n64, 8);
+    memcpy(out.data() + 16, kd, 8);
+    for (size_t a = 0; a < nl; ++a) memcpy(out.data() + 24 + a * 4, &dts[a], 4);
+    uint64_t *k = (uint64_t *)(out.data() + hdr);
+    for (size_t i = 0; i < n; ++i) k[i] = rows[i][0].bits;
+    for (size_t a = 0; a < nl; ++a) {
+        uint64_t *s = k + (1 + a) * n;
+        for (size_t i = 0; i < n; ++i) s[i] = rows[i][a + 1].bits;
+    }
+    return out;
+}
+
+bool is_group_rows(const uint8_t *p, size_t n) { return n >= 24 && memcmp(p, "FQG1", 4) == 0; }
+
+GroupRows decode_group_rows(const uint8_t *p, size_t n) {
+    if (!is_group_rows(p, n)) throw_status(FQ_E_INVALID, "GROUP BY partial rows: bad header");
+    uint32_t nl;
+    uint64_t rows;
+    int32_t kd[2];
+    memcpy(&nl, p + 4, 4);
+    memcpy(&rows, p + 8, 8);
+    memcpy(kd, p + 16, 8);
+    const size_t hdr = 24 + ((size_t)nl * 4 + 7) / 8 * 8;
+    if (nl > FQ_MAX_GROUP_AGGS || hdr + rows * 8 * (1 + (size_t)nl) > n)
+        throw_status(FQ_E_INVALID, "GROUP BY partial rows: truncated");
+    GroupRows g;
+    g.key_dtype = kd[0];
+    g.dtypes.resize(nl);
+    for (uint32_t a = 0; a < nl; ++a) memcpy(&g.dtypes[a], p + 24 + a * 4, 4);
+    const uint64_t *k = (const uint64_t *)(p + hdr);
+    g.keys.assign(k, k + rows);
+    g.st.resize(nl);
+    for (uint32_t a = 0; a < nl; ++a) g.st[a].assign(k + (1 + a) * rows, k + (2 + a) * rows);
+    return g;
 }
 
 }  // namespace fq

@@ -353,4 +353,19 @@ class Pipeline {
 std::vector<uint8_t> encode_states(const std::vector<std::vector<DataValue>> &per_func);
 std::vector<std::vector<DataValue>> decode_states(const uint8_t *p, size_t n);
 
+// GROUP BY partial states as flat arrays ("FQG1"): rows [key, leaf states...]
+// that are all 64-bit Some values -- what a GPU table holds -- travel as
+// keys[n] + states[leaf][n] (8 B per value instead of a 16-B DataValue record),
+// and the final merges them on the device (fq_group_table_merge).
+struct GroupRows {
+    DataType key_dtype = FQ_DT_NULL;
+    std::vector<DataType> dtypes;           // per leaf
+    std::vector<uint64_t> keys;             // n
+    std::vector<std::vector<uint64_t>> st;  // [leaf][n]
+};
+// empty when some row is not encodable (a None state, a Struct, Utf8 ...)
+std::vector<uint8_t> encode_group_rows(const std::vector<std::vector<DataValue>> &rows);
+bool is_group_rows(const uint8_t *p, size_t n);
+GroupRows decode_group_rows(const uint8_t *p, size_t n);
+
 }  // namespace fq

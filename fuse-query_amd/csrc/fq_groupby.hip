@@ -166,6 +166,79 @@ __global__ void __launch_bounds__(256) group_extract_kernel(ExtractArgs a) {
     }
 }
 
+// fq_group_table_merge: exchanged rows into a table (replica 0 of each
+// state; extract folds the replicas).  A key's home slot is its 64-bit mixer
+// mod the capacity, linear probing, claimed with a CAS (keys only go EMPTY ->
+// key); the sentinel key has its own slot (cap) and header flag, as in the
+// generated kernels' ginsert.
+struct MergeArgs {
+    const uint64_t *in_keys;
+    const uint64_t *in_states[FQ_MAX_GROUP_AGGS];
+    uint64_t *keys;
+    uint64_t *states[FQ_MAX_GROUP_AGGS];
+    int32_t kinds[FQ_MAX_GROUP_AGGS];
+    int32_t dtypes[FQ_MAX_GROUP_AGGS];
+    int32_t n_aggs;
+    int64_t n, cap;
+    uint32_t *hdr;
+};
+
+__device__ __forceinline__ uint64_t merge_mix(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ void atomic_fold(int32_t kind, int32_t dt, uint64_t *p, uint64_t v) {
+    if (kind == FQ_AGG_COUNT || (kind == FQ_AGG_SUM && dt != FQ_DT_FLOAT64)) {
+        atomicAdd((unsigned long long *)p, (unsigned long long)v);
+        return;
+    }
+    uint64_t old = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (;;) {
+        const uint64_t nv = fold(kind, dt, old, v);
+        if (nv == old) return;
+        const uint64_t prev = atomicCAS((unsigned long long *)p, old, nv);
+        if (prev == old) return;
+        old = prev;
+    }
+}
+
+__global__ void __launch_bounds__(256) group_merge_kernel(MergeArgs a) {
+    const int64_t T = (int64_t)gridDim.x * blockDim.x;
+    const uint64_t mask = (uint64_t)a.cap - 1;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += T) {
+        const uint64_t k = a.in_keys[i];
+        int64_t slot = -1;
+        if (k == kEmpty) {
+            atomicOr(&a.hdr[1], 1u);
+            slot = a.cap;
+        } else {
+            uint64_t h = merge_mix(k) & mask;
+            for (int64_t p = 0; p < a.cap; ++p) {
+                const uint64_t cur = __hip_atomic_load(&a.keys[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (cur == k) {
+                    slot = (int64_t)h;
+                    break;
+                }
+                if (cur == kEmpty) {
+                    const uint64_t old = atomicCAS((unsigned long long *)&a.keys[h], kEmpty, k);
+                    if (old == kEmpty || old == k) {
+                        slot = (int64_t)h;
+                        break;
+                    }
+                }
+                h = (h + 1) & mask;
+            }
+        }
+        if (slot < 0) {
+            atomicOr(&a.hdr[0], 256u);  // table full (read_header reports FQ_E_TABLE_FULL)
+            continue;
+        }
+        for (int s = 0; s < a.n_aggs; ++s) atomic_fold(a.kinds[s], a.dtypes[s], &a.states[s][slot], a.in_states[s][i]);
+    }
+}
+
 static int small_grid(int64_t work) {
     const int64_t cap = (int64_t)fqc::device_cu_count() * 4;
     int64_t g = (work + 255) / 256;
@@ -518,6 +591,34 @@ fq_status fq_group_table_extract(const fq_group_table *t, uint64_t *d_keys, uint
     if (s != FQ_OK) return s;
     if ((int64_t)c > cap) return fqc::fail(FQ_E_INVALID, "fq_group_table_extract: output arrays too small");
     *groups = (int64_t)c;
+    return FQ_OK;
+}
+
+fq_status fq_group_table_merge(const fq_group_table *t, const uint64_t *d_keys, const uint64_t *const *d_states,
+                               int64_t n, void *stream) {
+    using namespace fqk;
+    if (n < 0) return fqc::fail(FQ_E_INVALID, "fq_group_table_merge: negative row count");
+    if (n > 0 && (!d_keys || !d_states)) return fqc::fail(FQ_E_INVALID, "fq_group_table_merge: NULL argument");
+    TableView v;
+    fq_status s = view(t, v);
+    if (s != FQ_OK) return s;
+    if (n == 0) return FQ_OK;
+    MergeArgs a{};
+    a.in_keys = d_keys;
+    a.keys = v.keys;
+    a.n_aggs = t->n_aggs;
+    for (int i = 0; i < t->n_aggs; ++i) {
+        if (!d_states[i]) return fqc::fail(FQ_E_INVALID, "fq_group_table_merge: NULL state array");
+        a.in_states[i] = d_states[i];
+        a.states[i] = v.states[i];
+        a.kinds[i] = t->kinds[i];
+        a.dtypes[i] = t->dtypes[i];
+    }
+    a.n = n;
+    a.cap = v.cap;
+    a.hdr = v.hdr;
+    hipLaunchKernelGGL(group_merge_kernel, dim3(small_grid(n)), dim3(256), 0, (hipStream_t)stream, a);
+    FQ_HIP_TRY(hipGetLastError());
     return FQ_OK;
 }
 

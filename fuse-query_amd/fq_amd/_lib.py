@@ -21,7 +21,7 @@ GPU_SYMBOLS = [
     "fq_group_table_bytes", "fq_group_table_init", "fq_group_aggregate", "fq_group_table_count",
     "fq_group_table_extract", "fq_logic", "fq_filter_project_workspace_bytes", "fq_filter_project",
     "fq_predicate_bitmap", "fq_group_partition_workspace_bytes", "fq_group_aggregate_partitioned",
-    "fq_group_dense_keys",
+    "fq_group_dense_keys", "fq_group_table_merge",
 ]
 
 
@@ -90,6 +90,7 @@ _protos = {
     "fq_group_table_count": (C.c_int32, [P(abi.fq_group_table), P(C.c_int64), vp]),
     "fq_group_table_extract": (C.c_int32, [P(abi.fq_group_table), vp, P(C.c_void_p), C.c_int64, P(C.c_int64),
                                            vp]),
+    "fq_group_table_merge": (C.c_int32, [P(abi.fq_group_table), vp, P(C.c_void_p), C.c_int64, vp]),
 }
 for _name, (_res, _args) in _protos.items():
     _f = getattr(lib, _name)

@@ -336,6 +336,16 @@ class GroupTable:
                                                  ws.nbytes, _stream(stream)))
         self._ws = ws  # alive until the next call (the launch is asynchronous)
 
+    def merge(self, keys, states, stream=None):
+        """fq_group_table_merge: host uint64 keys[n] and per-aggregate uint64
+        states[n] (state bits) folded into this table."""
+        n = len(keys)
+        dk = torch.from_numpy(np.ascontiguousarray(keys, dtype=np.uint64).view(np.int64)).cuda()
+        ds = [torch.from_numpy(np.ascontiguousarray(s, dtype=np.uint64).view(np.int64)).cuda() for s in states]
+        ptrs = (C.c_void_p * max(len(ds), 1))(*[t.data_ptr() for t in ds])
+        check(lib.fq_group_table_merge(C.byref(self.desc), C.c_void_p(dk.data_ptr()), ptrs, n, _stream(stream)))
+        torch.cuda.synchronize()
+
     def count(self, stream=None):
         n = C.c_int64(0)
         check(lib.fq_group_table_count(C.byref(self.desc), C.byref(n), _stream(stream)))

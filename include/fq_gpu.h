@@ -402,6 +402,14 @@ fq_status fq_group_table_count(const fq_group_table *t, int64_t *groups, void *s
  * output arrays. */
 fq_status fq_group_table_extract(const fq_group_table *t, uint64_t *d_keys, uint64_t *const *d_states,
                                  int64_t cap, int64_t *groups, void *stream);
+/* Merge n (key, state) rows -- d_keys[n] and d_states[a][n] as the table's
+ * state bits, e.g. other GPUs' extracted tables -- into t: a new key claims a
+ * slot, an existing one folds with the table's kinds (Count / Sum add, Max /
+ * Min keep the extreme), atomically.  The cross-GPU AggregateFinal of a GROUP
+ * BY (no reference counterpart: the reference has no GROUP BY execution).
+ * A table too small for the keys reports FQ_E_TABLE_FULL on count/extract.  */
+fq_status fq_group_table_merge(const fq_group_table *t, const uint64_t *d_keys, const uint64_t *const *d_states,
+                               int64_t n, void *stream);
 
 #ifdef __cplusplus
 }

@@ -521,3 +521,52 @@ def test_sql_group_by_matches_c_oracle_at_scale(eng, key_sql, key_steps, groups)
     exp = [(int(k),) + tuple(int(x) for x in s) for k, s in zip(keys[o], st[o])]
     assert len(r.rows) == len(exp)
     assert [tuple(row) for row in r.rows] == exp
+
+
+def test_table_merge_folds_exchanged_rows():
+    # fq_group_table_merge (the cross-GPU GROUP BY final): three "ranks'"
+    # extracted tables folded into one fresh table equal the group-by of all
+    # rows; every kind and state type, repeated keys
+    rng = np.random.default_rng(11)
+    aggs = [(abi.AGG_COUNT, U), (abi.AGG_SUM, U), (abi.AGG_MAX, I), (abi.AGG_MIN, F), (abi.AGG_SUM, F)]
+    parts = []
+    for r in range(3):
+        n = 200_000
+        x = rng.integers(0, 1 << 62, n, dtype=np.uint64)
+        col = ops.from_numpy(x)
+        key, _ = chain(U, [("%", 5000)])
+        vi, _ = chain(U, [("%", 1000), ("-", (500, "Int64"))])
+        vf, _ = chain(U, [("%", 1000), ("*", 0.5)])
+        t = ops.GroupTable(1 << 14, aggs)
+        t.aggregate(col, key=key, values=[None, None, vi, vf, vf])
+        parts.append((x, t.extract()))
+    m = ops.GroupTable(1 << 14, aggs)
+    for _, (k, st) in parts:
+        m.merge(k, st)
+    keys, states = m.extract()
+    got = {int(k): [s[i] for s in decode(states, [d for _, d in aggs])] for i, k in enumerate(keys)}
+    allx = np.concatenate([x for x, _ in parts])
+    k = allx % np.uint64(5000)
+    xi = (allx % np.uint64(1000)).astype(np.int64) - 500
+    xf = (allx % np.uint64(1000)).astype(np.float64) * 0.5
+    exp = np_groupby(k, [None, allx, xi, xf, xf], [a for a, _ in aggs])
+    bound = {g: 1e-9 * abs(e[4]) + 1e-9 for g, e in exp.items()}
+    compare(got, exp, [a for a, _ in aggs], [d for _, d in aggs], bound)
+    # a table too small for the merged keys reports TABLE_FULL
+    tiny = ops.GroupTable(64, aggs)
+    tiny.merge(parts[0][1][0], parts[0][1][1])
+    with pytest.raises(ops.FQError):
+        tiny.count()
+
+
+def test_table_merge_sentinel_key_and_empty_input():
+    # the all-ones key (the table's EMPTY marker) has its own slot
+    aggs = [(abi.AGG_COUNT, U), (abi.AGG_MAX, U)]
+    m = ops.GroupTable(64, aggs)
+    E1 = 0xFFFFFFFFFFFFFFFF
+    m.merge(np.array([E1, 7, E1], dtype=np.uint64), [np.array([2, 1, 3], dtype=np.uint64),
+                                                     np.array([10, 4, 30], dtype=np.uint64)])
+    m.merge(np.array([], dtype=np.uint64), [np.array([], dtype=np.uint64)] * 2)
+    keys, states = m.extract()
+    got = {int(k): [int(states[0][i]), int(states[1][i])] for i, k in enumerate(keys)}
+    assert got == {E1: [5, 30], 7: [1, 4]}
