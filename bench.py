@@ -471,7 +471,32 @@ def main():
             comm.close()
             comm = None
 
+    # One step on one GPU is what a host binding the C ABI does
+    # (INTEGRATION.md): fq_engine_execute, then the one result row's values
+    # through fq_result_value -- no Python Result object (its ~50 us of
+    # interpreter work per step is harness, not query).
+    import ctypes as C
+
+    from fq_amd._lib import check as _check
+    from fq_amd._lib import lib as _lib
+    sql_b = sql.encode()
+    val = abi.fq_value()
+
+    def c_row():
+        out = C.c_void_p()
+        _check(_lib.fq_engine_execute(eng.h, sql_b, C.byref(out)))
+        try:
+            row = []
+            for c in range(_lib.fq_result_num_columns(out)):
+                _check(_lib.fq_result_value(out, 0, c, C.byref(val)))
+                row.append(val.bits if val.is_some else None)
+            return row
+        finally:
+            _lib.fq_result_free(out)
+
     def step():
+        if world == 1 and args.query not in GROUP_MOD:
+            return c_row()
         r = eng.execute(sql) if world == 1 else fqd.execute(eng, sql, comm)
         return r.rows if args.query in GROUP_MOD else list(r.rows[0])
 
