@@ -168,3 +168,40 @@ def test_exchange_protocol_ragged_lengths(lens):
         for r, row in enumerate(rows):
             exp = bytes((r * 31 + i) % 251 + 1 for i in range(lens[r]))
             assert len(row) == stride and row[:lens[r]] == exp and not any(row[lens[r]:]), (rank, r)
+
+
+def test_group_by_final_merges_flat_rows_on_the_host():
+    # execute_final on a host-only engine over three ranks' GROUP BY rows in
+    # the flat wire format ("FQG1", pipeline.cpp encode_group_rows): Int64
+    # keys (negative and positive), keys shared between ranks, more groups
+    # than the final's radix-sort threshold; the merge folds equal keys
+    # (count/sum add, max keeps the largest) and orders by key
+    import random
+    import struct
+
+    sys.path.insert(0, os.path.join(ROOT, "fuse-query_amd"))
+    from fq_amd import abi
+    from fq_amd.engine import Engine
+
+    def fqg1(rows):
+        nl = 3
+        out = b"FQG1" + struct.pack("<IQii", nl, len(rows), abi.DT_INT64, 0)
+        out += struct.pack("<3i", abi.DT_UINT64, abi.DT_UINT64, abi.DT_UINT64) + b"\0" * 4
+        out += struct.pack("<%dq" % len(rows), *[r[0] for r in rows])
+        for a in range(nl):
+            out += struct.pack("<%dQ" % len(rows), *[r[1 + a] for r in rows])
+        return out
+
+    rng = random.Random(5)
+    ranks, exp = [], {}
+    for _ in range(3):
+        keys = rng.sample(range(-30000, 30000), 9000)
+        rows = [(k, rng.randint(1, 9), rng.randint(0, 2**63), rng.randint(0, 2**64 - 1)) for k in keys]
+        ranks.append(fqg1(rows))
+        for k, c, s, m in rows:
+            e = exp.get(k)
+            exp[k] = (c, s, m) if e is None else (e[0] + c, (e[1] + s) % 2**64, max(e[2], m))
+    sql = "SELECT number%97, count(number), sum(number), max(number) FROM system.numbers_mt(1000) GROUP BY number%97"
+    with Engine(device=-1) as eng:
+        rows = eng.execute_final(sql, ranks).rows
+    assert rows == [(k,) + exp[k] for k in sorted(exp)]
