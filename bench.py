@@ -35,7 +35,7 @@ import torch.distributed as dist  # noqa: E402
 
 from fq_amd import abi, ops  # noqa: E402
 from fq_amd import dist as fqd  # noqa: E402
-from fq_amd.engine import Engine  # noqa: E402
+from fq_amd.engine import OPT_GROUP_CHUNK_ROWS, Engine  # noqa: E402
 from fq_amd.numbers import BLOCK_SIZE, generate_parts, shard, stream_rows  # noqa: E402
 
 METRIC = "rows/s + achieved HBM GB/s on 10B-row numbers_mt agg, 1/2/4/8 GPUs"
@@ -138,9 +138,11 @@ def latest_pmc_traffic(kernel_substr, query):
             d = json.load(open(f))
         except Exception:
             continue
-        for k in d.get("kernels", []):
-            if kernel_substr in k.get("name", "") and k.get("hbm_bytes_per_launch"):
-                return k["hbm_bytes_per_launch"], k.get("rows_per_launch"), os.path.basename(f)
+        subs = [kernel_substr] if isinstance(kernel_substr, str) else list(kernel_substr)
+        ks = [k for k in d.get("kernels", []) if k.get("hbm_bytes_per_launch") and
+              any(x in k.get("name", "") for x in subs)]
+        if ks:  # several names: one launch of each per unit (the partitioned GROUP BY's kernel set)
+            return sum(k["hbm_bytes_per_launch"] for k in ks), ks[0].get("rows_per_launch"), os.path.basename(f)
     return None
 
 
@@ -415,6 +417,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--streams", type=int, default=1,
                     help="device queues the pipes share (FQ_OPT_STREAMS); 1 = the scans run back to back")
+    ap.add_argument("--group-chunk-rows", type=int, default=None,
+                    help="rows per radix-partitioned GROUP BY launch (FQ_OPT_GROUP_CHUNK_ROWS; tuning)")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="nccl = RCCL over xGMI (default); gloo rehearses N ranks on fewer GPUs")
     args = ap.parse_args()
@@ -447,6 +451,8 @@ def main():
     # The engine: SQL -> Source x P -> [Filter] -> AggregatePartial x P -> Merge
     # -> AggregateFinal on this GPU (one host thread per pipe, fused scans).
     eng = Engine(device=local, profile=True, streams=args.streams)
+    if args.group_chunk_rows:
+        eng.set_option(OPT_GROUP_CHUNK_ROWS, args.group_chunk_rows)
     mine = shard(generate_parts(n_total), rank, world)
     total_rows = sum(stream_rows(b, e) for _, b, e in mine)
     eng.materialize_numbers(n_total, rank, world)  # SourceTransform's column, resident in HBM
@@ -562,7 +568,9 @@ def main():
     out = None
     if rank == 0:
         traffic = None
-        pmc = latest_pmc_traffic(kernel, args.query)
+        # the partitioned GROUP BY (g2): gpart + block scatter + bins per chunk
+        pmc = latest_pmc_traffic(("fq_jit_gpart", "group_blk_", "fq_jit_groupby_bins") if args.query == "g2"
+                                 else kernel, args.query)
         if pmc and pmc[1]:
             traffic = pmc[0] * rows_per_launch / pmc[1]  # HBM bytes per launch, scaled to this launch size
         out = {
@@ -606,7 +614,7 @@ def main():
                 "traffic": traffic,
                 "kernel": ("fq_group_aggregate (fq_jit_groupby, hipRTC-specialised), one launch per partition"
                            if args.query == "g1" else
-                           "fq_group_aggregate_partitioned (fq_jit_ghist + fq_jit_gpart + fq_jit_groupby_bins), "
+                           "fq_group_aggregate_partitioned (fq_jit_gpart + block grouping + fq_jit_groupby_bins), "
                            "one set per partition; achieved = the column's 8 B/row over the set"
                            if args.query == "g2" else
                            "fq_aggregate fused scan (%s + finalize), one launch per partition%s"

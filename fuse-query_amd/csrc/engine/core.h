@@ -193,7 +193,7 @@ class Runtime {
     // slots of the last GROUP BY table sized (a TABLE_FULL re-run grows from it)
     std::atomic<int64_t> group_used_capacity{0};
     // rows per radix-partitioned GROUP BY launch (FQ_OPT_GROUP_CHUNK_ROWS)
-    std::atomic<int64_t> group_chunk_rows{120000000};
+    std::atomic<int64_t> group_chunk_rows{500000000};
     ThreadPool pool;
 
    private:

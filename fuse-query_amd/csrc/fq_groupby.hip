@@ -30,6 +30,7 @@ namespace fqk {
 
 constexpr uint64_t kEmpty = ~0ull;
 constexpr uint32_t kFull = 256u;
+constexpr uint32_t kPartOverflow = 512u;  // fq_jit_gpart: more blocks than the workspace bound (never expected)
 constexpr size_t kHdrBytes = 64;
 
 struct TableView {
@@ -253,111 +254,140 @@ static fq_status read_header(const TableView &v, uint32_t &flags, uint64_t &coun
     flags = (uint32_t)(h[0] & 0xffffffffu);
     count = h[1];
     if (flags & kFull) return fqc::fail(FQ_E_TABLE_FULL, "GROUP BY hash table is full");
+    if (flags & kPartOverflow) return fqc::fail(FQ_E_INTERNAL, "GROUP BY partition workspace overflow");
     if (flags & FQ_STATE_DIV_ZERO) return fqc::fail(FQ_E_DIVIDE_BY_ZERO, "Internal Error: Divide by zero error");
     if (flags & FQ_STATE_CAST_NULL)
         return fqc::fail(FQ_E_UNSUPPORTED, "cast produced nulls (nulls are not supported on the device path)");
     return FQ_OK;
 }
 
-// Exclusive scan of the (bin, workgroup) row counts of fq_jit_ghist, bin
-// major, into their offsets in the partitioned buffer, and the bin starts.
-// Two launches of P workgroups (one per bin, grid <= 1024 counts each, four
-// consecutive counts per thread: coalesced): the bin totals, then every bin
-// sums the totals before it and scans its own row.  (One 1,024-thread
-// workgroup walking strided ranges took 0.22-0.29 ms per launch, paid again
-// by every chunk of a chunked query.)
-constexpr int kScanThreads = 256;
-static_assert(kMaxPartGrid <= 4 * kScanThreads, "four counts per thread");
+// The blocks of fq_jit_gpart grouped by bin, for fq_jit_groupby_bins: one
+// 256-thread workgroup scans the P <= 256 per-bin block counts into the bin
+// starts, then a scatter over the workgroup regions' blocks (used[w] of each
+// region's q, read on the device) places each block number -- with its rows,
+// order[i] = block | rows << 32 -- at its bin's cursor.  The scatter ranks in
+// LDS first: one global atomic per (workgroup, bin).  Block order within a
+// bin is arbitrary.
+constexpr int kBlkThreads = 256;
+constexpr int kBlkPerThread = 4;
 
-template <typename T>
-__device__ __forceinline__ T block_sum(T v, T *sh) {
-#pragma unroll
-    for (int o = kWave / 2; o > 0; o >>= 1) v += (T)shfl_xor64((uint64_t)v, o);
-    const int w = threadIdx.x / kWave;
+__global__ void __launch_bounds__(kBlkThreads)
+    group_blk_scan_kernel(const uint32_t *__restrict__ bin_blocks, uint32_t *__restrict__ bstart,
+                          uint32_t *__restrict__ cursor, int P) {
+    __shared__ uint32_t s[kBlkThreads];
+    const int t = threadIdx.x;
+    const uint32_t v = t < P ? bin_blocks[t] : 0u;
+    s[t] = v;
     __syncthreads();
-    if ((threadIdx.x & (kWave - 1)) == 0) sh[w] = v;
-    __syncthreads();
-    T t = 0;
-#pragma unroll
-    for (int i = 0; i < kScanThreads / kWave; ++i) t += sh[i];
-    return t;
-}
-
-__global__ void __launch_bounds__(kScanThreads)
-    group_part_total_kernel(const uint32_t *__restrict__ hist, uint64_t *__restrict__ tot, int grid) {
-    __shared__ uint64_t sh[kScanThreads / kWave];
-    const uint32_t *row = hist + (int64_t)blockIdx.x * grid;
-    uint64_t s = 0;
-    for (int i = threadIdx.x; i < grid; i += kScanThreads) s += row[i];
-    s = block_sum(s, sh);
-    if (threadIdx.x == 0) tot[blockIdx.x] = s;
-}
-
-__global__ void __launch_bounds__(kScanThreads)
-    group_part_offset_kernel(const uint32_t *__restrict__ hist, const uint64_t *__restrict__ tot,
-                             uint64_t *__restrict__ off, uint64_t *__restrict__ bins, int P, int grid) {
-    __shared__ uint64_t sh[kScanThreads / kWave];
-    __shared__ uint64_t s_scan[kScanThreads];
-    const int b = blockIdx.x, t = threadIdx.x;
-    // this bin's start: the totals of the bins before it
-    uint64_t before = 0;
-    for (int i = t; i < b; i += kScanThreads) before += tot[i];
-    const uint64_t start = block_sum(before, sh);
-    // this bin's row: thread t owns counts 4t .. 4t+3
-    const uint32_t *row = hist + (int64_t)b * grid;
-    uint64_t c[4], mine = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int i = 4 * t + k;
-        c[k] = i < grid ? row[i] : 0u;
-        mine += c[k];
-    }
-    s_scan[t] = mine;
-    __syncthreads();
-    for (int o = 1; o < kScanThreads; o <<= 1) {
-        const uint64_t v = t >= o ? s_scan[t - o] : 0;
+    for (int o = 1; o < kBlkThreads; o <<= 1) {
+        const uint32_t y = t >= o ? s[t - o] : 0u;
         __syncthreads();
-        s_scan[t] += v;
+        s[t] += y;
         __syncthreads();
     }
-    uint64_t run = start + s_scan[t] - mine;
-    uint64_t *orow = off + (int64_t)b * grid;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int i = 4 * t + k;
-        if (i < grid) orow[i] = run;
-        run += c[k];
+    if (t < P) {
+        bstart[t] = s[t] - v;
+        cursor[t] = s[t] - v;
     }
-    if (t == 0) bins[b] = start;
-    if (t == kScanThreads - 1 && b == P - 1) bins[P] = start + s_scan[t];
+    if (t == P - 1) bstart[P] = s[t];
 }
 
-fq_status launch_group_part_scan(const GroupPartition &X, hipStream_t stream) {
+__global__ void __launch_bounds__(kBlkThreads)
+    group_blk_scatter_kernel(const uint32_t *__restrict__ used, const uint32_t *__restrict__ blk_bin,
+                             const uint32_t *__restrict__ blk_fill, uint32_t *__restrict__ cursor,
+                             uint64_t *__restrict__ order, uint32_t q, uint32_t slots) {
+    __shared__ uint32_t s_cnt[256], s_base[256];
+    const uint32_t first = blockIdx.x * (uint32_t)(kBlkThreads * kBlkPerThread);
+    s_cnt[threadIdx.x] = 0;
+    __syncthreads();
+    uint32_t bin[kBlkPerThread], rank[kBlkPerThread];
+    bool ok[kBlkPerThread];
+#pragma unroll
+    for (int k = 0; k < kBlkPerThread; ++k) {
+        const uint32_t i = first + k * kBlkThreads + threadIdx.x;
+        ok[k] = i < slots && i - (i / q) * q < used[i / q];
+        bin[k] = ok[k] ? blk_bin[i] : 0u;
+        rank[k] = ok[k] ? atomicAdd(&s_cnt[bin[k]], 1u) : 0u;
+    }
+    __syncthreads();
+    const uint32_t c = s_cnt[threadIdx.x];
+    if (c) s_base[threadIdx.x] = atomicAdd(&cursor[threadIdx.x], c);
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kBlkPerThread; ++k) {
+        const uint32_t i = first + k * kBlkThreads + threadIdx.x;
+        if (ok[k]) order[s_base[bin[k]] + rank[k]] = (uint64_t)i | ((uint64_t)blk_fill[i] << 32);
+    }
+}
+
+fq_status launch_group_part_blocks(const GroupPartition &X, hipStream_t stream) {
     const int P = 1 << (X.log2p & 255);  // (bits 8..15: the range-bin shift)
-    if (X.grid > kMaxPartGrid) return fqc::fail(FQ_E_INTERNAL, "partition scan: grid above kMaxPartGrid");
-    hipLaunchKernelGGL(group_part_total_kernel, dim3(P), dim3(kScanThreads), 0, stream, X.hist, X.tot, X.grid);
+    hipLaunchKernelGGL(group_blk_scan_kernel, dim3(1), dim3(kBlkThreads), 0, stream, X.bin_blocks, X.bstart,
+                       X.cursor, P);
     FQ_HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(group_part_offset_kernel, dim3(P), dim3(kScanThreads), 0, stream, X.hist, X.tot, X.off,
-                       X.bins, P, X.grid);
+    const uint32_t per = kBlkThreads * kBlkPerThread, slots = (uint32_t)X.grid * X.q;
+    const uint32_t grid = (slots + per - 1) / per;
+    hipLaunchKernelGGL(group_blk_scatter_kernel, dim3(grid > 0 ? grid : 1), dim3(kBlkThreads), 0, stream, X.used,
+                       X.blk_bin, X.blk_fill, X.cursor, X.order, X.q, slots);
     FQ_HIP_TRY(hipGetLastError());
     return FQ_OK;
 }
 
+// Workgroups of fq_jit_gpart for len rows: two 1,024-thread workgroups per CU
+// (its 77 KB of LDS; FQ_GPART_WG_PER_CU tunes it), at most one per 8-row tile
+// of 256 threads -- the bound the workspace is sized by
+static int part_wg_per_cu() {
+    static const int v = [] {
+        const char *e = getenv("FQ_GPART_WG_PER_CU");
+        const int x = e ? atoi(e) : 2;
+        return x >= 1 && x <= 4 ? x : 2;
+    }();
+    return v;
+}
+static int64_t part_grid_bound(int64_t len) {
+    int64_t g = (int64_t)fqc::device_cu_count() * part_wg_per_cu();
+    if (g > kMaxPartGrid) g = kMaxPartGrid;
+    const int64_t tiles = (len + 2047) / 2048;
+    if (g > tiles) g = tiles;
+    return g < 1 ? 1 : g;
+}
+
+// Region of one fq_jit_gpart workgroup: the blocks of its tiles' rows (grid-
+// stride tiles of tile_rows), every (workgroup, bin) chain being full blocks
+// but its last
+static uint32_t part_region_blocks(int64_t len, int64_t tile_rows, int grid, int P) {
+    const int64_t tiles = (len + tile_rows - 1) / tile_rows, per = (tiles + grid - 1) / grid;
+    return (uint32_t)((per * tile_rows + kPartBlockRows - 1) / kPartBlockRows + P);
+}
+
 // Workspace of fq_group_aggregate_partitioned:
-// [hist u32 P x kMaxPartGrid][off u64 P x kMaxPartGrid][bins u64 P + 1, tot u64 P][vals u64 len]
+// [head: used u32 x kMaxPartGrid, blocks per bin u32 x 256][bstart u32 x 257, cursor u32 x 256]
+// [blk_bin u32 x B][blk_fill u32 x B][order u64 x B][vals: B blocks of kPartBlockRows rows]
+// with B blocks bounding grid x part_region_blocks for any grid <= the bound
+// g and tiles <= 8,192 rows (1,024 threads x 8): ceil(len / kPartBlockRows)
+// + (g + 1) x 8,192 / kPartBlockRows + g x (P + 1) + 1
 static size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
 static size_t part_ws_bytes(int64_t len, int log2p, GroupPartition *X, void *ws) {
-    const size_t P = (size_t)1 << log2p;
-    const size_t h = align256(P * kMaxPartGrid * 4), o = align256(P * kMaxPartGrid * 8), b = align256((2 * P + 1) * 8);
+    const size_t P = (size_t)1 << log2p, n = (size_t)(len > 0 ? len : 0);
+    const size_t g = (size_t)part_grid_bound(len);
+    const size_t B = (n + kPartBlockRows - 1) / kPartBlockRows + (g + 1) * (8192 / kPartBlockRows) + g * (P + 1) + 1;
+    const size_t head = align256((kMaxPartGrid + 256) * 4), sc = align256((257 + 256) * 4);
+    const size_t bb = align256(B * 4), ord = align256(B * 8), vals = align256(B * kPartBlockRows * 8);
     if (X) {
         char *m = (char *)ws;
-        X->hist = (uint32_t *)m;
-        X->off = (uint64_t *)(m + h);
-        X->bins = (uint64_t *)(m + h + o);
-        X->tot = X->bins + P + 1;
-        X->vals = m + h + o + b;
+        X->head = (uint32_t *)m;
+        X->head_bytes = head;
+        X->used = X->head;
+        X->bin_blocks = X->head + kMaxPartGrid;
+        X->bstart = (uint32_t *)(m + head);
+        X->cursor = X->bstart + 257;
+        X->blk_bin = (uint32_t *)(m + head + sc);
+        X->blk_fill = (uint32_t *)(m + head + sc + bb);
+        X->order = (uint64_t *)(m + head + sc + 2 * bb);
+        X->vals = m + head + sc + 2 * bb + ord;
+        X->max_blocks = (uint32_t)B;
     }
-    return h + o + b + align256((size_t)(len > 0 ? len : 0) * 8);
+    return head + sc + 2 * bb + ord + vals;
 }
 
 // tuning knobs of the GROUP BY launch (tools/groupby_sweep.py); the
@@ -519,20 +549,16 @@ fq_status fq_group_aggregate_partitioned(const fq_group_table *t, const fq_col *
     }
     part_ws_bytes(G.n, X.log2p, &X, d_ws);
     X.log2p = lp_arg;
-    // the histogram and the partition kernel walk the same tiles with the
-    // same workgroups; two 1,024-thread workgroups per CU (fq_jit_gpart's
-    // 76 KB of LDS; FQ_GPART_WG_PER_CU tunes it)
-    static const int wg_per_cu = [] {
-        const char *e = getenv("FQ_GPART_WG_PER_CU");
-        const int x = e ? atoi(e) : 2;
-        return x >= 1 && x <= 4 ? x : 2;
-    }();
+    // the partition kernel's grid: within the bound the workspace holds
+    // chains for (part_grid_bound)
     const int64_t tile = (int64_t)G.threads * 8;
     const int64_t ntiles = (G.n + tile - 1) / tile;
-    int64_t g = (int64_t)fqc::device_cu_count() * wg_per_cu;
-    if (g > kMaxPartGrid) g = kMaxPartGrid;
+    int64_t g = part_grid_bound(G.n);
     if (g > ntiles) g = ntiles;
     X.grid = (int)(g < 1 ? 1 : g);
+    X.q = part_region_blocks(G.n, tile, X.grid, 1 << log2_parts);
+    if ((uint64_t)X.q * (uint64_t)X.grid > X.max_blocks)
+        return fqc::fail(FQ_E_INTERNAL, "fq_group_aggregate_partitioned: partition regions exceed the workspace");
     X.bins_grid = fqc::device_cu_count();
     return jit_groupby_partitioned(col->dtype, G, X);
 }

@@ -864,22 +864,27 @@ std::string state_update(int32_t kind, int32_t dt, const std::string &P, const s
 // High-cardinality GROUP BY (fq_group_aggregate_partitioned): more groups
 // than an LDS table holds make every row an HBM atomic (100,000 groups x 3
 // aggregates: 149 ms per 10 GB).  Instead the passing rows are radix-
-// partitioned by key hash into P = 2^log2p bins, then aggregated bin by bin,
-// so every workgroup's LDS table only sees the groups of one bin:
-//   fq_jit_ghist   read the column, per-workgroup histogram of bins (LDS);
-//   (scan)         exclusive offsets per (bin, workgroup), fq_groupby.hip;
-//   fq_jit_gpart   read the column again (same tiles, same workgroups), LDS
-//                  counting sort of each 8,192-row tile by bin, each bin's run
-//                  written contiguously at the workgroup's cursor for it;
-//   fq_jit_groupby_bins  the partitioned rows split evenly over the
-//                  workgroups, cut at bin boundaries: LDS table per bin slice,
-//                  flushed to the HBM table (whose home slot is the mixer's top
-//                  bits, so a bin's groups share 1/P of the table).
-// HBM bytes per row: 8 (hist) + 8 + 8 (part) + 8 (bins) = 32 B for a passing
-// row (16 B for a filtered-out one), against 8 B + 3 random atomics.
+// partitioned by key (range or hash) into P = 2^log2p bins, then aggregated
+// bin by bin, so every workgroup's LDS table only sees the groups of one bin:
+//   fq_jit_gpart   read the column once, LDS counting sort of each 8,192-row
+//                  tile by bin; each (workgroup, bin) appends its run to a
+//                  chain of GP_BLK-row blocks taken from the workgroup's own
+//                  region of the workspace (an LDS counter: no histogram
+//                  pass, no global atomic per tile -- one shared counter put
+//                  ~2 us of cross-XCD atomic latency on every tile);
+//   (blocks)       the blocks grouped by bin, fq_groupby.hip (a P-bin scan
+//                  and a scatter of ~rows/256 block numbers);
+//   fq_jit_groupby_bins  the blocks split evenly over the workgroups, cut at
+//                  bin boundaries: LDS table per bin slice, flushed to the HBM
+//                  table (whose home slot is the mixer's top bits, so a bin's
+//                  groups share 1/P of the table).
+// HBM bytes per passing row: 8 (read) + 8 (blocks written) + 8 (blocks read)
+// = 24 B (8 B for a filtered-out one), against 8 B + 3 random atomics; the
+// histogram pass this replaces read the column once more (32 B per row).
 const char *kGroupPartitionKernels = R"(
 #define GP_ROWS 8
 #define GP_TILE (BT * GP_ROWS)
+#define GP_TBLK (GP_TILE / GP_BLK)
 // The kernels' log2p argument carries the bin shift of range bins in bits
 // 8..15: keys in [0, d), d <= P << shift, 2^shift <= S: bin b holds the keys
 // [b << shift, (b + 1) << shift), so its LDS table is indexed by the key's
@@ -895,23 +900,10 @@ __device__ __forceinline__ u32 wave_or32(u32 f) {
     return f;
 }
 
-// Bin counts: with range bins consecutive keys share a bin, so a wave's
+// Bin ranks: with range bins consecutive keys share a bin, so a wave's
 // passing lanes usually all hit one counter -- one LDS atomic for the wave
 // (ranks = its base + the lane's place among them) instead of 64 serialised
-// ones (ghist 0.15 -> 0.38 ms per chunk before this)
-__device__ __forceinline__ void gp_count(u32 *h, u32 b, bool p) {
-#if RANGE_BINS
-    const u64 act = __ballot(p);
-    if (!act) return;
-    const int l0 = __builtin_ctzll(act);
-    const u32 b0 = (u32)__builtin_amdgcn_readlane((int)b, l0);
-    if (__ballot(p && b == b0) == act) {
-        if ((int)(threadIdx.x & 63) == l0) atomicAdd(&h[b0], (u32)__popcll(act));
-        return;
-    }
-#endif
-    if (p) atomicAdd(&h[b], 1u);
-}
+// ones
 __device__ __forceinline__ u32 gp_rank(u32 *cnt, u32 b, bool p) {
 #if RANGE_BINS
     const u64 act = __ballot(p);
@@ -937,57 +929,33 @@ __device__ __forceinline__ void gp_load(const TIn *__restrict__ col, long long n
     }
 }
 
-extern "C" __global__ void __launch_bounds__(BT)
-fq_jit_ghist(const TIn *__restrict__ col, long long n, const u64 *__restrict__ bitmap, Consts c,
-             u32 *__restrict__ hist, int log2p, u32 *__restrict__ hdr) {
-    __shared__ u32 s_h[256];
-    const int P = 1 << (log2p & 255);
-    for (int i = threadIdx.x; i < P; i += BT) s_h[i] = 0;
-    __syncthreads();
-    u32 flags = 0;
-    const long long ntiles = (n + GP_TILE - 1) / GP_TILE;
-    for (long long tt = blockIdx.x; tt < ntiles; tt += gridDim.x) {
-        const long long r0 = tt * GP_TILE + threadIdx.x;
-        TIn x[GP_ROWS];
-#pragma unroll
-        for (int k = 0; k < GP_ROWS; ++k) {
-            const long long row = r0 + (long long)k * BT;
-            x[k] = row < n ? __builtin_nontemporal_load(col + row) : TIn(0);
-        }
-#pragma unroll
-        for (int k = 0; k < GP_ROWS; ++k) {
-            const long long row = r0 + (long long)k * BT;
-            bool p = false;
-            u32 b = 0;
-            if (row < n) {
-                Row r;
-                fq_prep(x[k], row, c, bitmap, flags, r);
-                p = r.pass != 0;
-                b = gbin(r.k, log2p);
-            }
-            gp_count(s_h, b, p);
-        }
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < P; i += BT) hist[(long long)i * gridDim.x + blockIdx.x] = s_h[i];
-    flags = wave_or32(flags);
-    if ((threadIdx.x & 63) == 0 && flags) atomicOr(&hdr[0], flags);
-}
-
+// Workgroup w owns blocks [w * q, (w + 1) * q): used[w] of them taken;
+// bin_blocks[b]: blocks of bin b; blk_bin / blk_fill: each block's bin and
+// rows (GP_BLK but for the last block of a chain)
 extern "C" __global__ void __launch_bounds__(BT)
 fq_jit_gpart(const TIn *__restrict__ col, long long n, const u64 *__restrict__ bitmap, Consts c,
-             const u64 *__restrict__ off, TIn *__restrict__ out, int log2p) {
+             u32 *__restrict__ used, u32 *__restrict__ bin_blocks, u32 *__restrict__ blk_bin,
+             u32 *__restrict__ blk_fill, unsigned q, TIn *__restrict__ out, int log2p,
+             u32 *__restrict__ hdr) {
+#if !RANGE_BINS
     __shared__ TIn s_stage[GP_TILE];
     __shared__ unsigned char s_bin[GP_TILE];
-    __shared__ u32 s_cnt[256], s_start[256], s_tot;
-    __shared__ u64 s_cur[256];
+    __shared__ u32 s_start[256], s_tot;
+#endif
+    __shared__ u32 s_cnt[256];
+    // per bin: the chain's current block and its rows, the first of the
+    // blocks taken for this tile, blocks taken in all
+    __shared__ u32 s_blk[256], s_fill[256], s_nb[256], s_nblk[256], s_next;
     const int P = 1 << (log2p & 255);
-    for (int i = threadIdx.x; i < P; i += BT) s_cur[i] = off[(long long)i * gridDim.x + blockIdx.x];
-    u32 flags = 0;  // errors were reported by fq_jit_ghist over the same rows
+    for (int i = threadIdx.x; i < P; i += BT) {
+        s_blk[i] = 0xffffffffu;
+        s_fill[i] = GP_BLK;  // full: the first row takes a block
+        s_nblk[i] = 0;
+    }
+    if (threadIdx.x == 0) s_next = 0;
+    const u32 region = blockIdx.x * q;
+    u32 flags = 0;
     const long long ntiles = (n + GP_TILE - 1) / GP_TILE;
-    // (a prefetched next tile and one ballot per bin for small P both
-    // measured slower here: the registers halve the occupancy, and LDS
-    // atomics on few counters beat a ballot loop)
     for (long long tt = blockIdx.x; tt < ntiles; tt += gridDim.x) {
         for (int i = threadIdx.x; i < P; i += BT) s_cnt[i] = 0;
         __syncthreads();
@@ -1010,14 +978,18 @@ fq_jit_gpart(const TIn *__restrict__ col, long long n, const u64 *__restrict__ b
             if (p) pass |= 1u << k;
         }
         __syncthreads();
+#if RANGE_BINS
+        const int t0 = 0;  // every thread takes blocks (no tile scan)
+#else
+        const int t0 = 64;
         if (threadIdx.x < 64) {  // exclusive scan of the P <= 256 bin counts: 4 per lane
             const int l = threadIdx.x;
             u32 v[4], t = 0;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int i = l * 4 + q;
-                v[q] = i < P ? s_cnt[i] : 0u;
-                t += v[q];
+            for (int qq = 0; qq < 4; ++qq) {
+                const int i = l * 4 + qq;
+                v[qq] = i < P ? s_cnt[i] : 0u;
+                t += v[qq];
             }
             u32 incl = t;
 #pragma unroll
@@ -1027,14 +999,53 @@ fq_jit_gpart(const TIn *__restrict__ col, long long n, const u64 *__restrict__ b
             }
             u32 run = incl - t;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int i = l * 4 + q;
+            for (int qq = 0; qq < 4; ++qq) {
+                const int i = l * 4 + qq;
                 if (i < P) s_start[i] = run;
-                run += v[q];
+                run += v[qq];
             }
             if (l == 63) s_tot = incl;
         }
+#endif
+        // the blocks this tile's run of bin b spills into, consecutive numbers
+        // from the workgroup's region; bin b's chain is kept by thread t0 + b
+        // (mod BT - t0) throughout
+        if ((int)threadIdx.x >= t0) {
+            for (int b = (int)threadIdx.x - t0; b < P; b += BT - t0) {
+                const u32 cnt = s_cnt[b], f = s_fill[b];
+                if (!cnt || f + cnt <= GP_BLK) continue;
+                const u32 need = (f + cnt - 1) / GP_BLK;
+                u32 base = atomicAdd(&s_next, need);
+                if (base + need > q) {  // cannot happen within the region bound; never write past it
+                    flags |= 512u;
+                    base = 0xffffffffu;
+                } else {
+                    base += region;
+                    for (u32 j = 0; j < need; ++j) {
+                        blk_bin[base + j] = (u32)b;
+                        blk_fill[base + j] = GP_BLK;
+                    }
+                    s_nblk[b] += need;
+                }
+                s_nb[b] = base;
+            }
+        }
         __syncthreads();
+#if RANGE_BINS
+        // straight from the registers: a wave's passing lanes mostly hold
+        // consecutive ranks of one bin (gp_rank), so the stores coalesce
+        // without the LDS staging the hash bins need (one barrier and 72 KB
+        // of LDS less)
+#pragma unroll
+        for (int k = 0; k < GP_ROWS; ++k) {
+            if (!((pass >> k) & 1u)) continue;
+            const u32 b = bin[k], o = s_fill[b] + rank[k];
+            u32 blk = o < GP_BLK ? s_blk[b] : s_nb[b];
+            if (blk == 0xffffffffu) continue;  // (workspace overflow, reported)
+            if (o >= GP_BLK) blk += o / GP_BLK - 1u;
+            __builtin_nontemporal_store(x[k], out + (long long)blk * GP_BLK + (o & (GP_BLK - 1)));
+        }
+#else
 #pragma unroll
         for (int k = 0; k < GP_ROWS; ++k) {
             if (!((pass >> k) & 1u)) continue;
@@ -1046,50 +1057,118 @@ fq_jit_gpart(const TIn *__restrict__ col, long long n, const u64 *__restrict__ b
         const u32 kept = s_tot;
         for (u32 i = threadIdx.x; i < kept; i += BT) {
             const u32 b = s_bin[i];
-            __builtin_nontemporal_store(s_stage[i], out + s_cur[b] + (i - s_start[b]));
+            const u32 o = s_fill[b] + (i - s_start[b]);  // place in the chain from its current block
+            u32 blk = o < GP_BLK ? s_blk[b] : s_nb[b];
+            if (blk == 0xffffffffu) continue;  // (workspace overflow, reported)
+            if (o >= GP_BLK) blk += o / GP_BLK - 1u;
+            __builtin_nontemporal_store(s_stage[i], out + (long long)blk * GP_BLK + (o & (GP_BLK - 1)));
         }
+#endif
         __syncthreads();
-        for (int i = threadIdx.x; i < P; i += BT) s_cur[i] += s_cnt[i];
+        for (int b = threadIdx.x; b < P; b += BT) {
+            const u32 cnt = s_cnt[b], t = s_fill[b] + cnt;
+            if (!cnt) continue;
+            if (t > GP_BLK) {
+                const u32 need = (t - 1) / GP_BLK;
+                s_blk[b] = s_nb[b] == 0xffffffffu ? 0xffffffffu : s_nb[b] + need - 1u;
+                s_fill[b] = t - need * GP_BLK;
+            } else {
+                s_fill[b] = t;
+            }
+        }
     }
+    __syncthreads();
+#if RANGE_BINS
+    const int t0 = 0;
+#else
+    const int t0 = 64;
+#endif
+    if ((int)threadIdx.x >= t0)
+        for (int b = (int)threadIdx.x - t0; b < P; b += BT - t0) {
+            if (s_blk[b] != 0xffffffffu) blk_fill[s_blk[b]] = s_fill[b];
+            if (s_nblk[b]) atomicAdd(&bin_blocks[b], s_nblk[b]);
+        }
+    if (threadIdx.x == 0) used[blockIdx.x] = s_next < q ? s_next : q;
+    flags = wave_or32(flags);
+    if ((threadIdx.x & 63) == 0 && flags) atomicOr(&hdr[0], flags);
+}
+
+// rows of tile ti of a bin slice: row j of the tile is row j % GP_BLK of the
+// slice's block ti * GP_TBLK + j / GP_BLK (a wave's 64 rows lie in one block:
+// 512 contiguous bytes), whose order entry (block | rows << 32) is staged in
+// LDS with those of the next GP_ORD_TILES - 1 tiles: the row loads wait on
+// LDS, not on a dependent HBM load
+#define GP_ORD 1024
+#define GP_ORD_TILES (GP_ORD / GP_TBLK)
+__device__ __forceinline__ u32 gb_load(const TIn *__restrict__ vals, const u64 *s_ord, long long ti,
+                                       TIn (&x)[GP_ROWS]) {
+    u32 live = 0;
+    const int t0 = (int)(ti % GP_ORD_TILES) * GP_TBLK;
+#pragma unroll
+    for (int k = 0; k < GP_ROWS; ++k) {
+        const int j = k * BT + (int)threadIdx.x;
+        const int off = j & (GP_BLK - 1);
+        const u64 ent = s_ord[t0 + j / GP_BLK];
+        x[k] = TIn(0);
+        if ((u32)off < (u32)(ent >> 32)) {
+            x[k] = __builtin_nontemporal_load(vals + (long long)(u32)ent * GP_BLK + off);
+            live |= 1u << k;
+        }
+    }
+    return live;
+}
+__device__ __forceinline__ void gb_stage(u64 *s_ord, const u64 *__restrict__ order, long long lo, long long e,
+                                         long long ti) {
+    const long long b0 = lo + ti * GP_TBLK;
+    for (int i = threadIdx.x; i < GP_ORD; i += BT) s_ord[i] = b0 + i < e ? order[b0 + i] : 0ull;
 }
 
 extern "C" __global__ void __launch_bounds__(BT)
-fq_jit_groupby_bins(const TIn *__restrict__ vals, const u64 *__restrict__ bins, int log2p, Consts c, Tab t) {
+fq_jit_groupby_bins(const TIn *__restrict__ vals, const u64 *__restrict__ order, const u32 *__restrict__ bstart,
+                    int log2p, Consts c, Tab t) {
     __shared__ u64 s_keys[S];
     __shared__ u64 s_st[NA][S];
     __shared__ int s_bypass[2];
+    __shared__ u64 s_ord[GP_ORD];
     Tab tr = t;
     const long long roff = (long long)(blockIdx.x & t.rmask) * (t.mask + 2);
     for (int a = 0; a < NA; ++a) tr.st[a] += roff;
     const int P = 1 << (log2p & 255);
-    const long long total = (long long)bins[P];
-    // this workgroup's even share of the partitioned rows, cut at bin boundaries
+    const long long total = (long long)bstart[P];
+    // this workgroup's even share of the blocks, cut at bin boundaries
     const long long per = (total + gridDim.x - 1) / gridDim.x;
     long long lo = (long long)blockIdx.x * per;
     const long long hi = lo + per < total ? lo + per : total;
     int p = 0;
-    while (p < P && (long long)bins[p + 1] <= lo) ++p;
+    while (p < P && (long long)bstart[p + 1] <= lo) ++p;
     u32 flags = 0;
     while (lo < hi && p < P) {
-        const long long e = (long long)bins[p + 1] < hi ? (long long)bins[p + 1] : hi;
+        const long long e = (long long)bstart[p + 1] < hi ? (long long)bstart[p + 1] : hi;
         if (e > lo) {
             fq_lds_reset(s_keys, s_st, s_bypass);
+            gb_stage(s_ord, order, lo, e, 0);
             __syncthreads();
-            // rows [lo, e) as tiles of GP_TILE from lo; the next tile's loads
-            // are in flight while this one goes through the LDS table
-            const TIn *__restrict__ sv = vals + lo;
-            const long long sn = e - lo, nt = (sn + GP_TILE - 1) / GP_TILE;
+            // blocks [lo, e) as tiles of GP_TBLK blocks; the next tile's
+            // loads are in flight while this one goes through the LDS table
+            const long long nt = (e - lo + GP_TBLK - 1) / GP_TBLK;
             TIn nxt[GP_ROWS];
-            gp_load(sv, sn, 0, nxt);
+            u32 nlive = gb_load(vals, s_ord, 0, nxt);
             for (long long ti = 0; ti < nt; ++ti) {
-                const long long r0 = lo + ti * GP_TILE + threadIdx.x;
                 TIn x[GP_ROWS];
 #pragma unroll
                 for (int k = 0; k < GP_ROWS; ++k) x[k] = nxt[k];
-                if (ti + 1 < nt) gp_load(sv, sn, ti + 1, nxt);
+                const u32 live = nlive;
+                if (ti + 1 < nt) {
+                    if ((ti + 1) % GP_ORD_TILES == 0) {  // (uniform) the next GP_ORD entries
+                        __syncthreads();
+                        gb_stage(s_ord, order, lo, e, ti + 1);
+                        __syncthreads();
+                    }
+                    nlive = gb_load(vals, s_ord, ti + 1, nxt);
+                }
                 Row r[GP_ROWS];
 #pragma unroll
-                for (int k = 0; k < GP_ROWS; ++k) fq_prep_all(x[k], r0 + (long long)k * BT < e ? 1u : 0u, c, flags, r[k]);
+                for (int k = 0; k < GP_ROWS; ++k) fq_prep_all(x[k], (live >> k) & 1u, c, flags, r[k]);
                 u32 cnt[GP_ROWS];
                 fq_runs(r, cnt);
 #if RANGE_BINS
@@ -1134,6 +1213,7 @@ bool gen_groupby_source(const GroupLaunch &G, int32_t tin, Gen &g, std::string &
     src += "#define GCHUNK " + std::to_string(group_chunked()) + "\n";
     src += "#define GWAVE " + std::to_string(group_wave_runs()) + "\n";
     src += "#define RANGE_BINS " + std::to_string(G.range_bins ? 1 : 0) + "\n";
+    src += "#define GP_BLK " + std::to_string(kPartBlockRows) + "\n";
     src += "#define GCLUSTER " + std::to_string(cluster && group_cluster() > 0 && fqc::dtype_size(tin) == 8 &&
                                                           G.lds_bytes + G.threads * 16 <= 160 * 1024 ? 1 : 0) + "\n";
     src += "#define GCLUSTER_CHANGES " + std::to_string(group_cluster() > 0 ? group_cluster() : 160) + "\n";
@@ -2411,7 +2491,7 @@ fq_status jit_scan(int32_t col_dtype, bool chain, const Launch &L, bool *used, b
 namespace {
 
 struct GroupFns {
-    hipFunction_t agg = nullptr, hist = nullptr, part = nullptr, bins = nullptr;
+    hipFunction_t agg = nullptr, part = nullptr, bins = nullptr;
 };
 std::unordered_map<std::string, GroupFns> g_group_cache;
 
@@ -2459,7 +2539,6 @@ fq_status get_group_fns(int32_t col_dtype, const GroupLaunch &G, GroupFns *out) 
         }
         GroupFns f;
         f.agg = c.fn;
-        FQ_HIP_TRY(hipModuleGetFunction(&f.hist, c.mod, "fq_jit_ghist"));
         FQ_HIP_TRY(hipModuleGetFunction(&f.part, c.mod, "fq_jit_gpart"));
         FQ_HIP_TRY(hipModuleGetFunction(&f.bins, c.mod, "fq_jit_groupby_bins"));
         it = g_group_cache.emplace(key, f).first;
@@ -2515,21 +2594,21 @@ fq_status jit_groupby_partitioned(int32_t col_dtype, const GroupLaunch &G, const
     long long n = G.n;
     const uint64_t *bitmap = G.pred.bitmap;
     int log2p = X.log2p;
-    uint32_t *hist = X.hist;
-    uint32_t *hdr = G.hdr;
-    void *a1[] = {&col, &n, &bitmap, &hc, &hist, &log2p, &hdr};
-    FQ_HIP_TRY(hipModuleLaunchKernel(f.hist, (unsigned)X.grid, 1, 1, (unsigned)G.threads, 1, 1, 0, G.stream, a1, nullptr));
-    if ((s = launch_group_part_scan(X, G.stream)) != FQ_OK) return s;
-    const uint64_t *off = X.off;
+    uint32_t *used = X.used, *bin_blocks = X.bin_blocks, *blk_bin = X.blk_bin, *blk_fill = X.blk_fill;
+    unsigned q = X.q;
     void *vals = X.vals;
-    void *a2[] = {&col, &n, &bitmap, &hc, &off, &vals, &log2p};
-    FQ_HIP_TRY(hipModuleLaunchKernel(f.part, (unsigned)X.grid, 1, 1, (unsigned)G.threads, 1, 1, 0, G.stream, a2, nullptr));
+    uint32_t *hdr = G.hdr;
+    FQ_HIP_TRY(hipMemsetAsync(X.head, 0, X.head_bytes, G.stream));
+    void *a1[] = {&col, &n, &bitmap, &hc, &used, &bin_blocks, &blk_bin, &blk_fill, &q, &vals, &log2p, &hdr};
+    FQ_HIP_TRY(hipModuleLaunchKernel(f.part, (unsigned)X.grid, 1, 1, (unsigned)G.threads, 1, 1, 0, G.stream, a1, nullptr));
+    if ((s = launch_group_part_blocks(X, G.stream)) != FQ_OK) return s;
     const void *cvals = X.vals;
-    const uint64_t *bins = X.bins;
-    void *a3[] = {&cvals, &bins, &log2p, &hc, &tab};
-    FQ_HIP_TRY(hipModuleLaunchKernel(f.bins, (unsigned)X.bins_grid, 1, 1, (unsigned)G.threads, 1, 1, 0, G.stream, a3,
+    const uint64_t *order = X.order;
+    const uint32_t *bstart = X.bstart;
+    void *a2[] = {&cvals, &order, &bstart, &log2p, &hc, &tab};
+    FQ_HIP_TRY(hipModuleLaunchKernel(f.bins, (unsigned)X.bins_grid, 1, 1, (unsigned)G.threads, 1, 1, 0, G.stream, a2,
                                      nullptr));
-    g_jit_launches += 3;
+    g_jit_launches += 2;
     return FQ_OK;
 }
 

@@ -106,22 +106,31 @@ int group_lds_slots(int n_aggs, int lds_bytes);
 fq_status jit_groupby(int32_t col_dtype, const GroupLaunch &G);
 
 // The partitioned (high-cardinality) path of fq_group_aggregate_partitioned:
-// histogram -> scan -> partition -> per-bin aggregation, in the caller's
-// workspace (fq_groupby.hip lays it out).
-constexpr int kMaxPartGrid = 1024;  // workgroups of the histogram / partition kernels
+// partition into block chains -> blocks grouped by bin -> per-bin
+// aggregation, in the caller's workspace (fq_groupby.hip lays it out).
+constexpr int kMaxPartGrid = 1024;    // workgroups of the partition kernel
+constexpr int kPartBlockRows = 256;   // rows per partition block (2 KB of u64)
 struct GroupPartition {
-    int log2p;        // bits 0..7: 1..8, P = 2^log2p bins; bits 8..15: the key shift of range bins
-    int grid;         // workgroups of fq_jit_ghist and fq_jit_gpart (the same tiles)
-    int bins_grid;    // workgroups of fq_jit_groupby_bins
-    uint32_t *hist;   // [P][grid] rows per (bin, workgroup)
-    uint64_t *off;    // [P][grid] their exclusive offsets
-    uint64_t *bins;   // [P + 1] bin starts in vals
-    uint64_t *tot;    // [P] rows per bin (scratch of the scan)
-    void *vals;       // the passing rows, grouped by bin
+    int log2p;            // bits 0..7: 1..8, P = 2^log2p bins; bits 8..15: the key shift of range bins
+    int grid;             // workgroups of fq_jit_gpart
+    int bins_grid;        // workgroups of fq_jit_groupby_bins
+    uint32_t max_blocks;  // blocks the workspace holds
+    uint32_t q;           // blocks per workgroup region: workgroup w of fq_jit_gpart owns [w q, (w + 1) q)
+    uint32_t *head;       // [kMaxPartGrid] blocks used per region + [256] blocks per bin: zeroed per launch
+    size_t head_bytes;
+    uint32_t *used;       // [grid] (head)
+    uint32_t *bin_blocks; // [P] blocks per bin (head + kMaxPartGrid)
+    uint32_t *bstart;     // [P + 1] each bin's first entry in order
+    uint32_t *cursor;     // [P] scatter cursors
+    uint32_t *blk_bin;    // [max_blocks] each block's bin
+    uint32_t *blk_fill;   // [max_blocks] its rows
+    uint64_t *order;      // [max_blocks] block | rows << 32, grouped by bin
+    void *vals;           // max_blocks x kPartBlockRows rows
 };
 fq_status jit_groupby_partitioned(int32_t col_dtype, const GroupLaunch &G, const GroupPartition &X);
-// exclusive scan of X.hist into X.off and X.bins (two launches of P workgroups; fq_groupby.hip)
-fq_status launch_group_part_scan(const GroupPartition &X, hipStream_t stream);
+// the blocks of fq_jit_gpart grouped by bin: a scan of X.bin_blocks into
+// X.bstart, then a scatter of the block numbers into X.order (fq_groupby.hip)
+fq_status launch_group_part_blocks(const GroupPartition &X, hipStream_t stream);
 
 // One fq_filter_project / fq_predicate_bitmap call (fq_filter.hip ->
 // fq_jit.hip): FilterTransform's predicate and ProjectionTransform's

@@ -365,9 +365,11 @@ class GroupTable:
         return k, [t[: out.value].cpu().numpy().view(np.uint64) for t in sts]
 
 
-def group_compile_check(col_dtype, aggs, key=None, values=None, pred=None, key_dtype=abi.DT_UINT64):
+def group_compile_check(col_dtype, aggs, key=None, values=None, pred=None, key_dtype=abi.DT_UINT64, log2_parts=0):
     """Generate + compile the group-by kernel for a shape (no GPU needed: a
-    zero-length call compiles the source for gfx950 without loading it)."""
+    zero-length call compiles the source for gfx950 without loading it);
+    log2_parts > 0 through fq_group_aggregate_partitioned (range bins for a
+    `% d` key, else hash bins)."""
     d = abi.fq_group_table()
     d.d_mem = 0x1000  # never dereferenced for a zero-length column
     d.capacity = 64
@@ -381,5 +383,9 @@ def group_compile_check(col_dtype, aggs, key=None, values=None, pred=None, key_d
     for i, v in enumerate(values or []):
         if v is not None:
             vals[i] = v
-    check(lib.fq_group_aggregate(C.byref(d), C.byref(c), C.byref(pred) if pred is not None else None,
-                                 C.byref(key) if key is not None else None, vals, None))
+    p = C.byref(pred) if pred is not None else None
+    k = C.byref(key) if key is not None else None
+    if log2_parts:
+        check(lib.fq_group_aggregate_partitioned(C.byref(d), C.byref(c), p, k, vals, log2_parts, None, 0, None))
+    else:
+        check(lib.fq_group_aggregate(C.byref(d), C.byref(c), p, k, vals, None))

@@ -47,7 +47,7 @@ typedef struct fq_result fq_result;
                                    aggregates over numbers_mt(1e12) stream through bounded HBM
                                    like the reference's 10,000-row blocks do through RAM */
 #define FQ_OPT_GROUP_CHUNK_ROWS 6 /* rows per radix-partitioned GROUP BY launch (a positive
-                                   multiple of 64; default 120,000,000: a ~0.96 GB partition
+                                   multiple of 64; default 500,000,000: a ~4.3 GB partition
                                    workspace, which the device block cache keeps per queue) */
 
 typedef struct fq_engine_stats {

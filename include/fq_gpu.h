@@ -375,14 +375,15 @@ fq_status fq_group_table_init(const fq_group_table *t, void *stream);
 fq_status fq_group_aggregate(const fq_group_table *t, const fq_col *col, const fq_pred *pred,
                              const fq_expr *key_expr, const fq_expr *values, void *stream);
 /* High-cardinality variant: the rows kept by pred are radix-partitioned by
- * key hash into 2^log2_parts bins (1..8) -- one histogram read and one
- * read + write pass over col into d_ws -- and then aggregated bin by bin, so
- * each workgroup's LDS table only meets the groups of one bin (about
- * groups / 2^log2_parts of them).  Same table, results and errors as
- * fq_group_aggregate; 32 B of HBM traffic per kept row instead of 8 B plus
- * random HBM atomics once the groups outgrow LDS.  d_ws: 256-B aligned, at
- * least fq_group_partition_workspace_bytes(col->len, log2_parts) bytes
- * (about 8 B per row).  Asynchronous. */
+ * key (range for a `% d` key, else hash) into 2^log2_parts bins (1..8) -- one
+ * read + write pass over col into 2 KB block chains in d_ws, the blocks then
+ * grouped by bin -- and then aggregated bin by bin, so each workgroup's LDS
+ * table only meets the groups of one bin (about groups / 2^log2_parts of
+ * them).  Same table, results and errors as fq_group_aggregate; 24 B of HBM
+ * traffic per kept row instead of 8 B plus random HBM atomics once the groups
+ * outgrow LDS.  d_ws: 256-B aligned, at least
+ * fq_group_partition_workspace_bytes(col->len, log2_parts) bytes (about 8 B
+ * per row plus ~2 KB per (workgroup, bin) chain).  Asynchronous. */
 size_t fq_group_partition_workspace_bytes(int64_t len, int32_t log2_parts);
 fq_status fq_group_aggregate_partitioned(const fq_group_table *t, const fq_col *col, const fq_pred *pred,
                                          const fq_expr *key_expr, const fq_expr *values, int32_t log2_parts,

@@ -459,7 +459,7 @@ def test_sql_high_cardinality_group_by_takes_the_partitioned_path(eng):
     j0 = ops.jit_stats()["jit_launches"]
     r = eng.execute("SELECT number%%50000, count(number), max(number), sum(number) FROM system.numbers_mt(%d) "
                     "WHERE number%%3 < 2 GROUP BY number%%50000" % total)
-    assert ops.jit_stats()["jit_launches"] - j0 >= 3 * 8  # ghist + gpart + bins per partition
+    assert ops.jit_stats()["jit_launches"] - j0 >= 2 * 8  # gpart + bins per partition
     x = np.arange(total, dtype=np.uint64)
     x = x[x % np.uint64(3) < 2]
     exp = np_groupby(x % np.uint64(50000), [None, x, x], [abi.AGG_COUNT, abi.AGG_MAX, abi.AGG_SUM])
@@ -486,7 +486,7 @@ def test_sql_partitioned_group_by_in_chunks(chunk):
         e.set_option(OPT_GROUP_CHUNK_ROWS, chunk)
         j0 = ops.jit_stats()["jit_launches"]
         got = e.execute(sql).rows
-        assert ops.jit_stats()["jit_launches"] - j0 >= 3 * 8 * 2  # >= 2 chunks per partition
+        assert ops.jit_stats()["jit_launches"] - j0 >= 2 * 8 * 2  # gpart + bins, >= 2 chunks per partition
         with pytest.raises(FQError):
             e.set_option(OPT_GROUP_CHUNK_ROWS, 100)
     assert got == whole

@@ -123,6 +123,17 @@ def test_groupby_shapes_compile(name, dt, key_steps, aggs, kdt):
     ops.group_compile_check(dt, spec, key=key, values=values, pred=pred, key_dtype=kdt)
 
 
+@pytest.mark.parametrize("key_steps,log2p", [([("%", 100000)], 8), ([("*", 7), ("%", 100000)], 5),
+                                             ([("/", 3)], 6), ([("-", (5, "Int64"))], 1)],
+                         ids=["range_bins", "range_bins_p32", "hash_bins", "signed_hash_bins"])
+def test_partitioned_groupby_shapes_compile(key_steps, log2p):
+    # fq_jit_gpart (block chains) + fq_jit_groupby_bins, range and hash bins
+    key, kdt = chain(U64, key_steps)
+    aggs = [(abi.AGG_COUNT, U64), (abi.AGG_SUM, U64), (abi.AGG_MAX, U64)]
+    pred = predicate(U64, [("%", 8)], "<", 3)
+    ops.group_compile_check(U64, aggs, key=key, values=[None] * 3, pred=pred, key_dtype=kdt, log2_parts=log2p)
+
+
 def test_predicate_tree_shapes_compile():
     from fq_amd.expr import pred_tree
     t = pred_tree(U64, [([("%", 8)], "<", 3), ([], ">", 1000), ([("%", 97)], "=", 0)], [0, 1, "and", 2, "or"])
