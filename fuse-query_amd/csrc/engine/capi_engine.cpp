@@ -15,10 +15,37 @@
 #include "pipeline.h"
 #include "planner.h"
 
+// One result column: DataValues, or (flat) the 64-bit words of values that
+// are all Some of one type -- GROUP BY results, kept flat from the final to
+// fq_result_values
+struct ResultCol {
+    std::vector<fq::DataValue> v;
+    std::vector<uint64_t> flat;
+    int32_t flat_dtype = -1;  // >= 0: the column is flat
+    bool is_flat() const { return flat_dtype >= 0; }
+    size_t size() const { return is_flat() ? flat.size() : v.size(); }
+    bool empty() const { return size() == 0; }
+    fq::DataValue value(size_t i) const {
+        return is_flat() ? fq::DataValue::some((fq::DataType)flat_dtype, flat[i]) : v[i];
+    }
+    fq_value abi(size_t i) const { return is_flat() ? value(i).to_abi() : v[i].to_abi(); }
+    void to_values() {  // a DataValue block joins a flat column
+        if (!is_flat()) return;
+        v.reserve(flat.size());
+        for (uint64_t b : flat) v.push_back(fq::DataValue::some((fq::DataType)flat_dtype, b));
+        flat.clear();
+        flat_dtype = -1;
+    }
+    void push_back(fq::DataValue x) {
+        to_values();
+        v.push_back(std::move(x));
+    }
+};
+
 struct fq_result {
     std::vector<std::string> names;
     std::vector<int32_t> types;
-    std::vector<std::vector<fq::DataValue>> cols;
+    std::vector<ResultCol> cols;
     int64_t rows = 0;
     mutable std::vector<std::string> text;  // fq_result_text storage
 };
@@ -95,8 +122,10 @@ fq::QueryPlan plan_for(fq_engine *e, const char *sql, const fq::QueryContext &qc
     return plan;
 }
 
-void append_block(fq_result *r, const fq::DataBlock &b0, fq::ExecCtx &ctx) {
-    fq::DataBlock b = fq::materialize(b0, ctx);
+// Host rows of the block are moved in when the block holds the only
+// reference to them (streams hand their blocks over), else copied.
+void append_block(fq_result *r, fq::DataBlock b0, fq::ExecCtx &ctx) {
+    fq::DataBlock b = b0.filter ? fq::materialize(b0, ctx) : std::move(b0);
     if (r->names.empty()) {
         for (const auto &f : b.schema->fields) {
             r->names.push_back(f.name);
@@ -106,11 +135,27 @@ void append_block(fq_result *r, const fq::DataBlock &b0, fq::ExecCtx &ctx) {
     }
     int64_t n = 0;
     for (size_t c = 0; c < b.columns.size() && c < r->cols.size(); ++c) {
-        std::vector<fq::DataValue> v = b.columns[c].to_host(ctx.stream());
-        if (b.columns[c].dtype == FQ_DT_NULL && v.empty()) v.assign((size_t)b.columns[c].len, fq::DataValue::null());
+        fq::Column &col = b.columns[c];
+        ResultCol &rc = r->cols[c];
+        if (col.flat && (rc.empty() || (rc.is_flat() && rc.flat_dtype == col.dtype))) {
+            std::vector<uint64_t> f = col.flat.use_count() == 1 ? std::move(*col.flat) : *col.flat;
+            n = std::max<int64_t>(n, (int64_t)f.size());
+            if (rc.empty()) {
+                rc.v.clear();
+                rc.flat = std::move(f);
+                rc.flat_dtype = col.dtype;
+            } else {
+                rc.flat.insert(rc.flat.end(), f.begin(), f.end());
+            }
+            continue;
+        }
+        std::vector<fq::DataValue> v =
+            col.host && col.host.use_count() == 1 ? std::move(*col.host) : col.to_host(ctx.stream());
+        if (col.dtype == FQ_DT_NULL && v.empty()) v.assign((size_t)col.len, fq::DataValue::null());
         n = std::max<int64_t>(n, (int64_t)v.size());
-        if (r->cols[c].empty()) r->cols[c] = std::move(v);
-        else r->cols[c].insert(r->cols[c].end(), std::make_move_iterator(v.begin()), std::make_move_iterator(v.end()));
+        rc.to_values();
+        if (rc.v.empty()) rc.v = std::move(v);
+        else rc.v.insert(rc.v.end(), std::make_move_iterator(v.begin()), std::make_move_iterator(v.end()));
     }
     r->rows += n;
 }
@@ -232,7 +277,7 @@ fq_status fq_engine_execute(fq_engine *e, const char *sql, fq_result **out) {
                 try {
                     fq::StreamRef s = p.execute();
                     fq::DataBlock b;
-                    while (s->next(b)) append_block(r.get(), b, ctx);
+                    while (s->next(b)) append_block(r.get(), std::move(b), ctx);
                 } catch (const fq::FQException &ex) {
                     // a GROUP BY table ran out of slots: re-run with 16x the slots
                     if (!grow_group_table(e, ex, attempt)) throw;
@@ -454,7 +499,7 @@ fq_status fq_engine_execute_final(fq_engine *e, const char *sql, const void *sta
         auto r = std::make_unique<fq_result>();
         fq::StreamRef s = p.execute();
         fq::DataBlock b;
-        while (s->next(b)) append_block(r.get(), b, ctx);
+        while (s->next(b)) append_block(r.get(), std::move(b), ctx);
         *out = r.release();
     });
 }
@@ -520,21 +565,29 @@ fq_status fq_result_value(const fq_result *r, int64_t row, int32_t col, fq_value
     if (!r || !out || col < 0 || col >= (int32_t)r->cols.size() || row < 0 ||
         row >= (int64_t)r->cols[(size_t)col].size())
         return fqc::fail(FQ_E_INVALID, "fq_result_value: out of range");
-    *out = r->cols[(size_t)col][(size_t)row].to_abi();
+    *out = r->cols[(size_t)col].abi((size_t)row);
     return FQ_OK;
 }
 fq_status fq_result_values(const fq_result *r, int32_t col, fq_value *out, int64_t n) {
     if (!r || (!out && n > 0) || col < 0 || col >= (int32_t)r->cols.size() || n < 0 ||
         n > (int64_t)r->cols[(size_t)col].size())
         return fqc::fail(FQ_E_INVALID, "fq_result_values: out of range");
-    const auto &c = r->cols[(size_t)col];
-    for (int64_t i = 0; i < n; ++i) out[i] = c[(size_t)i].to_abi();
+    const ResultCol &c = r->cols[(size_t)col];
+    if (c.is_flat()) {
+        const fq_value proto = fq::DataValue::some((fq::DataType)c.flat_dtype, 0).to_abi();
+        for (int64_t i = 0; i < n; ++i) {
+            out[i] = proto;
+            out[i].bits = c.flat[(size_t)i];
+        }
+        return FQ_OK;
+    }
+    for (int64_t i = 0; i < n; ++i) out[i] = c.v[(size_t)i].to_abi();
     return FQ_OK;
 }
 const char *fq_result_text(const fq_result *r, int64_t row, int32_t col) {
     if (!r || col < 0 || col >= (int32_t)r->cols.size() || row < 0 || row >= (int64_t)r->cols[(size_t)col].size())
         return nullptr;
-    r->text.push_back(r->cols[(size_t)col][(size_t)row].debug());
+    r->text.push_back(r->cols[(size_t)col].value((size_t)row).debug());
     return r->text.back().c_str();
 }
 void fq_result_free(fq_result *r) { delete r; }

@@ -669,6 +669,14 @@ Column Column::host_values(DataType dt, std::vector<DataValue> rows) {
     return c;
 }
 
+Column Column::host_flat(DataType dt, std::vector<uint64_t> bits) {
+    Column c;
+    c.dtype = dt;
+    c.len = (int64_t)bits.size();
+    c.flat = std::make_shared<std::vector<uint64_t>>(std::move(bits));
+    return c;
+}
+
 Column Column::slice(int64_t start, int64_t n) const {
     Column c = *this;
     if (start < 0) start = 0;
@@ -677,6 +685,8 @@ Column Column::slice(int64_t start, int64_t n) const {
     c.len = n;
     if (host) {
         c.host = std::make_shared<std::vector<DataValue>>(host->begin() + start, host->begin() + start + n);
+    } else if (flat) {
+        c.flat = std::make_shared<std::vector<uint64_t>>(flat->begin() + start, flat->begin() + start + n);
     } else if (dev) {
         if (dtype == FQ_DT_BOOLEAN) {
             if (start % 64) throw_internal("bitmap slices must start on a 64-row boundary");
@@ -690,6 +700,12 @@ Column Column::slice(int64_t start, int64_t n) const {
 
 std::vector<DataValue> Column::to_host(hipStream_t st) const {
     if (host) return *host;
+    if (flat) {
+        std::vector<DataValue> out;
+        out.reserve(flat->size());
+        for (uint64_t b : *flat) out.push_back(DataValue::some(dtype, b));
+        return out;
+    }
     std::vector<DataValue> out;
     if (!dev || len == 0) {
         if (dtype == FQ_DT_NULL) out.assign((size_t)len, DataValue::null());

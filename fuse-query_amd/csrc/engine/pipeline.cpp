@@ -753,6 +753,14 @@ StreamRef GroupByPartialTransform::execute() {
 
 StreamRef GroupByFinalTransform::execute() {
     ExecCtx &ctx = ExecCtx::current();
+    static const bool trace = getenv("FQ_TRACE_GROUP_FINAL") != nullptr;  // phase times on stderr (tools)
+    int64_t tp = now_ns();
+    auto phase = [&](const char *what) {
+        if (!trace) return;
+        const int64_t t = now_ns();
+        fprintf(stderr, "[group final] %-8s %8.3f ms\n", what, (t - tp) * 1e-6);
+        tp = t;
+    };
     std::vector<FunctionRef> funcs;
     for (auto &f : funcs_) funcs.push_back(f->clone());
     const std::vector<AggregatorFunction *> leaves = leaves_of(funcs);
@@ -773,6 +781,7 @@ StreamRef GroupByFinalTransform::execute() {
             if (row.kind == DataValue::kStruct && !row.fields.empty()) exchanged.push_back(&row.fields);
         held.push_back(b);
     }
+    phase("input");
     if (shared_->ready) kdt = shared_->desc.key_dtype;
     else if (!exchanged.empty()) kdt = (*exchanged[0])[0].dtype;
     for (const std::vector<DataValue> *rp : exchanged) {
@@ -818,6 +827,7 @@ StreamRef GroupByFinalTransform::execute() {
             ctx.sync();
         }
     }
+    phase("fetch");
     std::vector<uint32_t> rows;  // one source row per group, in key order
     if (emit_states_ && exchanged.empty()) {
         // partial states of this rank's own table: the keys are unique and
@@ -841,6 +851,7 @@ StreamRef GroupByFinalTransform::execute() {
             i = j;
         }
     }
+    phase("sort");
     DataBlock out;
     out.schema = schema_;
     const size_t ng = rows.size();
@@ -859,10 +870,14 @@ StreamRef GroupByFinalTransform::execute() {
     }
     // key column, then each aggregate expression evaluated from its leaves;
     // an expression that IS one leaf (count(x), sum(x) ...) is that leaf's
-    // states as they stand (merge_result returns the state)
+    // states as they stand (merge_result returns the state).  The key and
+    // such leaves are flat host columns (all Some); trees are DataValues.
     std::vector<std::vector<DataValue>> cols(1 + funcs.size());
-    for (auto &c : cols) c.reserve(ng);
-    for (uint32_t r : rows) cols[0].push_back(DataValue::some(kdt, keys[r]));
+    std::vector<std::vector<uint64_t>> flat(1 + funcs.size());
+    std::vector<DataType> flat_dt(1 + funcs.size(), FQ_DT_NULL);
+    flat[0].resize(ng);
+    flat_dt[0] = kdt;
+    for (size_t i = 0; i < ng; ++i) flat[0][i] = keys[rows[i]];
     std::vector<int> direct(funcs.size(), -1);
     bool any_tree = false;
     for (size_t f = 0; f < funcs.size(); ++f) {
@@ -871,11 +886,18 @@ StreamRef GroupByFinalTransform::execute() {
         any_tree |= direct[f] < 0;
     }
     for (size_t f = 0; f < funcs.size(); ++f) {
-        if (direct[f] < 0) continue;
+        if (direct[f] < 0) {
+            cols[f + 1].reserve(ng);
+            continue;
+        }
         const FlatLeaf &L = ls[(size_t)direct[f]];
-        for (uint32_t r : rows) {
+        std::vector<uint64_t> &fc = flat[f + 1];
+        fc.resize(ng);
+        flat_dt[f + 1] = L.dtype;
+        for (size_t i = 0; i < ng; ++i) {
+            const uint32_t r = rows[i];
             if (!L.some[r]) throw_internal("DataValue to array cannot be NONE NULL");
-            cols[f + 1].push_back(DataValue::some(L.dtype, L.bits[r]));
+            fc[i] = L.bits[r];
         }
     }
     if (any_tree) {
@@ -891,9 +913,18 @@ StreamRef GroupByFinalTransform::execute() {
     }
     for (size_t c = 0; c < cols.size(); ++c) {
         DataType dt = c < schema_->fields.size() ? schema_->fields[c].dtype : FQ_DT_NULL;
+        if (flat_dt[c] != FQ_DT_NULL && ng > 0) {  // the states' own type, as the DataValue path had it
+            out.columns.push_back(Column::host_flat(flat_dt[c], std::move(flat[c])));
+            continue;
+        }
+        if (c == 0 || (c > 0 && direct[c - 1] >= 0)) {  // no groups: an empty column of the schema's type
+            out.columns.push_back(Column::host_values(dt, {}));
+            continue;
+        }
         if (!cols[c].empty() && cols[c][0].kind == DataValue::kSome) dt = cols[c][0].dtype;
         out.columns.push_back(Column::host_values(dt, std::move(cols[c])));
     }
+    phase("build");
     return std::make_unique<DataBlockStream>(std::vector<DataBlock>{out});
 }
 

@@ -39,7 +39,7 @@ class DataBlockStream : public BlockStream {
     explicit DataBlockStream(std::vector<DataBlock> blocks) : blocks_(std::move(blocks)) {}
     bool next(DataBlock &out) override {
         if (i_ >= blocks_.size()) return false;
-        out = blocks_[i_++];
+        out = std::move(blocks_[i_++]);  // read once: the consumer gets the only reference
         return true;
     }
 
