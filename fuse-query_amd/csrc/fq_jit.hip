@@ -1183,7 +1183,7 @@ fq_jit_groupby_bins(const TIn *__restrict__ vals, const u64 *__restrict__ order,
 #endif
             }
             __syncthreads();
-            fq_flush(tr, s_keys, s_st);
+            fq_flush(tr, s_keys, s_st, (u64)p << (log2p >> 8), (1ull << (log2p >> 8)) - 1ull);
             __syncthreads();
             lo = e;
         }
@@ -1401,9 +1401,12 @@ __device__ long long ginsert(const Tab &t, u64 k) {
     row += "        }\n    }\n#endif\n}\n";
     // range bins (fq_jit_groupby_bins): the slot is the key's low LOG2S bits;
     // the key is stored for the flush (a plain write: every writer of a slot
-    // writes the same key)
+    // writes the same key) -- unless a COUNT state marks the occupied slots,
+    // when the flush rebuilds the key from the bin and the slot (one LDS
+    // write per row less)
     row += "__device__ __forceinline__ void fq_commit_range(const Row &r, u64 *s_keys, u64 (*s_st)[S], u64 cnt) {\n"
-           "    if (!r.pass) return;\n    const int slot = (int)(r.k & (u64)(S - 1));\n    s_keys[slot] = r.k;\n";
+           "    if (!r.pass) return;\n    const int slot = (int)(r.k & (u64)(S - 1));\n"
+           "#if DENSE_CNT < 0\n    s_keys[slot] = r.k;\n#endif\n";
     for (int a = 0; a < NA; ++a)
         row += "    " + state_update(G.kinds[a], G.dtypes[a], "&s_st[" + std::to_string(a) + "][slot]",
                                      G.kinds[a] == FQ_AGG_COUNT ? "cnt" : "r.v" + std::to_string(a)) + "\n";
@@ -1518,11 +1521,16 @@ template <int N> __device__ __forceinline__ void fq_wave_runs(Row (&r)[N], u32 (
         src += "        s_st[" + std::to_string(a) + "][i] = " + identity(G.kinds[a], G.dtypes[a]) + ";\n";
     src += "    }\n}\n";
     src += R"(// this workgroup's groups into the HBM table
-__device__ __forceinline__ void fq_flush(const Tab &tr, const u64 *s_keys, u64 (*s_st)[S]) {
+// (range bins: the slice's keys are kbin | (slot & kmask))
+__device__ __forceinline__ void fq_flush(const Tab &tr, const u64 *s_keys, u64 (*s_st)[S], u64 kbin = 0,
+                                         u64 kmask = 0) {
     for (int i = threadIdx.x; i < S; i += BT) {
 #if DENSE && DENSE_CNT >= 0
         if (s_st[DENSE_CNT][i] == 0) continue;
         const u64 k = (u64)i;
+#elif RANGE_BINS && DENSE_CNT >= 0
+        if (s_st[DENSE_CNT][i] == 0) continue;
+        const u64 k = kbin | ((u64)i & kmask);
 #else
         const u64 k = s_keys[i];
         if (k == EMPTY) continue;

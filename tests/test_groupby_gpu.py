@@ -394,6 +394,45 @@ def test_partitioned_matches_numpy(mod, log2p):
     compare(got, exp, [a for a, _ in aggs], [d for _, d in aggs], bound)
 
 
+@pytest.mark.parametrize("steps,pred", [
+    ([("/", 1_000_000_000)], False),   # hash bins, one key: every row in one bin
+    ([("/", 5000), ("%", 3)], False),  # range bins, runs of 5,000 rows: a tile's rows mostly one bin
+    ([("%", 2)], True),                # range bins, two keys, a predicate keeping 3/8 of the rows
+])
+def test_partitioned_skewed_bins(steps, pred):
+    # block chains under skew: a tile's whole run in one bin spills into many
+    # blocks at once; the workspace bound (full blocks but each chain's last)
+    # holds; results equal numpy
+    n = 3_000_017
+    col = ops.numbers_column(0, n)
+    x = np.arange(n, dtype=np.uint64)
+    key, _ = chain(U, steps)
+    aggs = [(abi.AGG_COUNT, U), (abi.AGG_SUM, U), (abi.AGG_MAX, U)]
+    p = predicate(U, [("%", 8)], "<", 3) if pred else None
+    got = run_parts(col, aggs, 8, key=key, pred=p, capacity=1 << 12)
+    k = x
+    for op, d in steps:
+        k = k // np.uint64(d) if op == "/" else k % np.uint64(d)
+    m = (x % np.uint64(8)) < 3 if pred else np.ones(n, dtype=bool)
+    exp = np_groupby(k[m], [None, x[m], x[m]], [a for a, _ in aggs])
+    compare(got, exp, [a for a, _ in aggs], [d for _, d in aggs])
+
+
+@pytest.mark.parametrize("with_count", [True, False])
+def test_partitioned_range_bins_with_and_without_count(with_count):
+    # range bins: with a COUNT state the flush rebuilds each key from its bin
+    # and LDS slot (no key written per row); without one the key is stored
+    n = 2_000_003
+    col = ops.splitmix_column(0x77, 1, n)
+    x = col.to_numpy()
+    key, _ = chain(U, [("%", 90_000)])
+    aggs = ([(abi.AGG_COUNT, U)] if with_count else []) + [(abi.AGG_MAX, U), (abi.AGG_SUM, U)]
+    got = run_parts(col, aggs, 7, key=key, capacity=1 << 18)
+    exp = np_groupby(x % np.uint64(90_000), [None if a == abi.AGG_COUNT else x for a, _ in aggs],
+                     [a for a, _ in aggs])
+    compare(got, exp, [a for a, _ in aggs], [d for _, d in aggs])
+
+
 def test_partitioned_equals_lds_path_bit_exact():
     # integer states: the partitioned path and the plain kernel agree exactly
     n = 5_000_003
