@@ -344,11 +344,15 @@ static int part_wg_per_cu() {
     }();
     return v;
 }
+static int tune_env(const char *name, int def, int lo, int hi);
+static int group_threads() { return tune_env("FQ_GROUP_THREADS", 1024, 256, 1024) & ~255; }
+// (at least 4 tiles per workgroup: every workgroup's region holds a partial
+// block per bin, P x 2 KB, which for a small column would outweigh its rows)
 static int64_t part_grid_bound(int64_t len) {
     int64_t g = (int64_t)fqc::device_cu_count() * part_wg_per_cu();
     if (g > kMaxPartGrid) g = kMaxPartGrid;
-    const int64_t tiles = (len + 2047) / 2048;
-    if (g > tiles) g = tiles;
+    const int64_t tile = (int64_t)group_threads() * 8, tiles = (len + tile - 1) / tile;
+    if (g > (tiles + 3) / 4) g = (tiles + 3) / 4;
     return g < 1 ? 1 : g;
 }
 
@@ -454,7 +458,7 @@ static fq_status prepare_group(const fq_group_table *t, const fq_col *col, const
     // 64 KB table each, 2 per CU, ran 1,000 groups x 3 aggregates in 2.98 ms
     // against 2.25 ms here, and the table holds twice the groups)
     G.lds_bytes = group_lds_bytes();
-    G.threads = tune_env("FQ_GROUP_THREADS", 1024, 256, 1024) & ~255;
+    G.threads = group_threads();
     G.rowmap = tune_env("FQ_GROUP_ROWMAP", 1, 0, 1);
     const int64_t nvec = (G.n - G.head) / 2;
     int64_t grid = (nvec + 4 * G.threads - 1) / (4 * G.threads);

@@ -124,3 +124,22 @@ def test_group_dense_keys_host():
     assert dense([("/", 1000)]) == 0
     assert dense([("-", (5, "Int64")), ("%", (10, "Int64"))], dt=U) == 0  # Int64 key
     assert lib.fq_group_dense_keys(U, None, 3) == 0
+
+
+def test_partition_workspace_bytes_bound():
+    # fq_group_partition_workspace_bytes: 0 outside log2_parts 1..8; at least
+    # the rows' 8 B each, growing with the rows; the per-(workgroup, bin)
+    # block slack stays small beside a small column (>= 4 tiles per workgroup)
+    from fq_amd._lib import lib
+    assert lib.fq_group_partition_workspace_bytes(1000, 0) == 0
+    assert lib.fq_group_partition_workspace_bytes(1000, 9) == 0
+    prev = 0
+    for n in (0, 1, 1_000_000, 2_400_000, 120_000_000, 500_000_000):
+        b = lib.fq_group_partition_workspace_bytes(n, 8)
+        assert b >= 8 * n and b >= prev
+        # slack: <= 2 KB per (workgroup, bin) chain and per tile of the grid
+        # (<= 1,024 workgroups), plus the block tables' 16 B per block
+        assert b <= 8 * n * 1.01 + (640 << 20), (n, b)
+        if n <= 2_400_000:
+            assert b <= 8 * n + (64 << 20), (n, b)
+        prev = b
