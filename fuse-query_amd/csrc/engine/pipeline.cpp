@@ -703,7 +703,16 @@ StreamRef GroupByPartialTransform::execute() {
         // stays under 1 GB, which the device block cache keeps for the next
         // query on this queue (a 10 GB one was mapped afresh per query:
         // hipMallocAsync up to 540 ms, tools/batch_r02c.sh)
-        const int64_t chunk = lp > 0 ? std::min<int64_t>(c.len, ctx.rt->group_chunk_rows.load()) : c.len;
+        // (split evenly, no short tail chunk: a 1.25e9-row partition as 3 x
+        // 4.17e8 ran 5.32 ms per 10 GB, as 5e8 + 5e8 + 2.5e8 5.72-5.76 on
+        // another box -- profiles/r02_s4_g2_chunks.txt)
+        int64_t chunk = c.len;
+        if (lp > 0) {
+            const int64_t cap = std::max<int64_t>(64, ctx.rt->group_chunk_rows.load());
+            const int64_t pieces = (c.len + cap - 1) / cap;
+            chunk = std::min<int64_t>(cap, ((c.len + pieces - 1) / pieces + 63) / 64 * 64);
+            if (chunk < 1) chunk = 1;
+        }
         std::shared_ptr<DeviceBuffer> ws;
         if (lp > 0) {
             const size_t need = fq_group_partition_workspace_bytes(chunk, lp);

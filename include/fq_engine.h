@@ -47,8 +47,9 @@ typedef struct fq_result fq_result;
                                    aggregates over numbers_mt(1e12) stream through bounded HBM
                                    like the reference's 10,000-row blocks do through RAM */
 #define FQ_OPT_GROUP_CHUNK_ROWS 6 /* rows per radix-partitioned GROUP BY launch (a positive
-                                   multiple of 64; default 500,000,000: a ~4.3 GB partition
-                                   workspace, which the device block cache keeps per queue) */
+                                   multiple of 64; default 500,000,000: at most a ~4.3 GB
+                                   partition workspace, which the device block cache keeps per
+                                   queue; a block is split into equal chunks of at most this) */
 
 typedef struct fq_engine_stats {
     uint64_t scan_launches; /* fused aggregate scans launched                    */
