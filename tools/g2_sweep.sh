@@ -23,9 +23,9 @@ PY
   return $rc
 }
 run default FQ_X=0 && \
-run chunk625M FQ_X=0 -- --group-chunk-rows 625000000 && \
-run chunk500M FQ_X=0 -- --group-chunk-rows 500000000 && \
+run bins2 FQ_GBINS_PER_CU=2 && \
+run bins4 FQ_GBINS_PER_CU=4 && \
 run default_b FQ_X=0 && \
-run chunk625M_b FQ_X=0 -- --group-chunk-rows 625000000 && \
-run chunk500M_b FQ_X=0 -- --group-chunk-rows 500000000 && \
+run bins2_b FQ_GBINS_PER_CU=2 && \
+run bins4_b FQ_GBINS_PER_CU=4 && \
 true || (cd /tmp && timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 "$R/bench.py" --query g2 --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/prof.json" 2> "$OUT/prof.err")
