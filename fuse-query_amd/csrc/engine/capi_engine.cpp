@@ -62,6 +62,9 @@ struct fq_engine {
     std::unordered_map<std::string, fq::QueryPlan> plans;
 };
 
+// the Function-handle ABI (capi_function.cpp) runs its device calls here
+fq::Runtime *fq_engine_runtime(fq_engine *e) { return e->rt.get(); }
+
 namespace {
 
 template <typename F>

@@ -127,6 +127,90 @@ const char *fq_result_text(const fq_result *r, int64_t row, int32_t col);
 fq_status fq_result_mysql_type(const fq_result *r, int32_t col, int32_t *out);
 void fq_result_free(fq_result *r);
 
+/* ---- Function handles: the reference's expression/aggregate trait surface ----
+ * A Rust host that keeps its own transforms binds these in place of its
+ * `Function` enum (src/functions/function.rs:28-131); the engine's
+ * AggregatePartial/AggregateFinal run the same C++ objects.
+ *
+ *   fq_function_field        FieldFunction::try_create        function_field.rs:20-25
+ *   fq_function_constant     ConstantFunction::try_create     function_constant.rs:20-24
+ *   fq_function_create       ScalarFunctionFactory::get       function_factory.rs:14-40
+ *                            (+ - * / = < > <= >= and or; the aggregators
+ *                             count min max sum, AggregatorFunction::try_create
+ *                             function_aggregator.rs:24-36)
+ *   fq_function_clone        #[derive(Clone)] (deep: the aggregate state too)
+ *   fq_function_display      fmt::Debug of Function             function.rs:134-146
+ *   fq_function_return_type / nullable / set_depth / eval / accumulate /
+ *   accumulate_result / merge_state / merge_result
+ *                            Function::*                        function.rs:28-131
+ *
+ * Blocks are the caller's device columns (Arrow PrimitiveArray value buffers,
+ * Boolean as LSB-first bitmap words), borrowed for the call.  eval and
+ * accumulate run on the engine's GPU; the state protocol (accumulate_result,
+ * merge_state, merge_result) is host work, as in the reference, and also works
+ * on a host-only engine.                                                     */
+typedef struct fq_function fq_function;
+
+typedef struct fq_block {
+    int32_t n_columns;
+    const char *const *names; /* DataSchema field names                       */
+    const fq_col *columns;    /* device columns of equal len                  */
+} fq_block;
+
+/* A DataValue of any type (data_value.rs:20-38), Utf8 included.
+ * kind: FQ_SCALAR_NULL = DataValue::Null, FQ_SCALAR_NONE = X(None),
+ * FQ_SCALAR_SOME = X(Some(v)); numeric/Boolean payloads in `bits` (fq_value
+ * encoding), Utf8 in str/str_len.  Scalars the library returns point into
+ * thread-local storage valid until the thread's next call that returns one. */
+#define FQ_SCALAR_NULL 0
+#define FQ_SCALAR_NONE 1
+#define FQ_SCALAR_SOME 2
+typedef struct fq_scalar {
+    int32_t kind;
+    int32_t dtype;
+    uint64_t bits;
+    const char *str;
+    uint64_t str_len;
+} fq_scalar;
+
+fq_status fq_function_field(const char *name, fq_function **out);
+fq_status fq_function_constant(const fq_scalar *value, fq_function **out);
+/* name: an operator or function name as the factory resolves it
+ * (case-insensitive); args are cloned, the caller keeps its handles.
+ * Errors as the reference: "Internal Error: Unsupported Function: <name>";
+ * '%' resolves too (the FQ_OP_MOD extension, FQ_OPT_MODULO's default).    */
+fq_status fq_function_create(const char *name, fq_function *const *args, int32_t n_args, fq_function **out);
+fq_status fq_function_clone(const fq_function *f, fq_function **out);
+void fq_function_free(fq_function *f);
+/* NUL-terminated display text; *len = its length (needed cap = len + 1)     */
+fq_status fq_function_display(const fq_function *f, char *buf, size_t cap, size_t *len);
+fq_status fq_function_set_depth(fq_function *f, uint64_t depth);
+/* schema = the block's names with its columns' dtypes (nullable false)     */
+fq_status fq_function_return_type(const fq_function *f, const fq_block *schema, int32_t *out);
+fq_status fq_function_nullable(const fq_function *f, const fq_block *schema, int32_t *out);
+/* DataColumnarValue result: an array is copied into d_out (device memory of
+ * `cap` bytes; the needed size is reported in *out_bytes, FQ_E_INVALID when
+ * cap is short), *is_array = 1, *out_dtype and *out_len describe it; a scalar
+ * result sets *is_array = 0 and *scalar.  Work runs on the engine's queue
+ * and is complete when the call returns.                                    */
+fq_status fq_function_eval(fq_engine *e, fq_function *f, const fq_block *b, void *d_out, size_t cap,
+                           size_t *out_bytes, int32_t *out_dtype, int64_t *out_len, int32_t *is_array,
+                           fq_scalar *scalar);
+fq_status fq_function_accumulate(fq_engine *e, fq_function *f, const fq_block *b);
+/* states: the function's partial state vector (aggregates in depth order);
+ * *n = its length (FQ_E_INVALID when cap is short, *n = the size needed)   */
+fq_status fq_function_accumulate_result(const fq_function *f, fq_scalar *states, size_t cap, size_t *n);
+fq_status fq_function_merge_state(fq_function *f, const fq_scalar *states, size_t n);
+fq_status fq_function_merge_result(const fq_function *f, fq_scalar *out);
+
+/* Scalar DataValue ops (the merge arithmetic of AggregateFinal):
+ *   fq_data_value_arithmetic_op   data_value_arithmetic.rs:10-27 (op FQ_OP_*)
+ *   fq_data_value_aggregate_op    data_value_aggregate.rs:8-101  (agg FQ_AGG_*)
+ * Errors carry the reference's texts, e.g. "Internal Error: Unsupported
+ * data_value_sum for data type: left:Utf8, right:Int8".                    */
+fq_status fq_data_value_arithmetic_op(int32_t op, const fq_scalar *l, const fq_scalar *r, fq_scalar *out);
+fq_status fq_data_value_aggregate_op(uint32_t agg, const fq_scalar *l, const fq_scalar *r, fq_scalar *out);
+
 #ifdef __cplusplus
 }
 #endif

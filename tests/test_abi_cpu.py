@@ -143,3 +143,9 @@ def test_partition_workspace_bytes_bound():
         if n <= 2_400_000:
             assert b <= 8 * n + (64 << 20), (n, b)
         prev = b
+
+
+def test_engine_and_function_symbol_lists_match_header():
+    from fq_amd.engine import ENGINE_SYMBOLS
+    from fq_amd.functions import FUNCTION_SYMBOLS
+    assert sorted(ENGINE_SYMBOLS + FUNCTION_SYMBOLS) == declared_symbols("fq_engine.h")
