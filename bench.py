@@ -38,6 +38,9 @@ from fq_amd import dist as fqd  # noqa: E402
 from fq_amd.engine import OPT_GROUP_CHUNK_ROWS, Engine  # noqa: E402
 from fq_amd.numbers import BLOCK_SIZE, generate_parts, shard, stream_rows  # noqa: E402
 
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+from srchash import kernel_sources_sha256  # noqa: E402
+
 METRIC = "rows/s + achieved HBM GB/s on 10B-row numbers_mt agg, 1/2/4/8 GPUs"
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # reference README.md:57 / :62 (8 vCPU KVM), BASELINE.md section 1: the only
@@ -125,25 +128,38 @@ def log(rank, *a):
         print("[bench]", *a, file=sys.stderr, flush=True)
 
 
-def latest_pmc_traffic(kernel_substr, query):
-    """HBM bytes per launch from the newest committed rocprofv3 --pmc summary
-    of this query (profiles/*pmc_<query>[_.]*.json, written by
-    tools/pmc_summary.py with the gfx950 FETCH_SIZE x2 correction already
-    applied); None when absent."""
+def latest_pmc_traffic(kernel_substr, query, rows_per_launch):
+    """(HBM bytes per launch scaled to rows_per_launch, provenance) from the
+    newest committed rocprofv3 --pmc summary of this query (profiles/
+    *pmc_<query>[_.]*.json, tools/pmc_summary.py, gfx950 FETCH_SIZE x2
+    correction applied).  The summary must have been measured on the current
+    kernel sources (its kernel_sources_sha256): otherwise traffic is None and
+    the provenance says the file is stale."""
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_%s.json" % query)) +
                    glob.glob(os.path.join(ROOT, "profiles", "*pmc_%s_*.json" % query)),
                    key=os.path.basename)
+    subs = [kernel_substr] if isinstance(kernel_substr, str) else list(kernel_substr)
+    cur = kernel_sources_sha256()
     for f in reversed(files):
         try:
             d = json.load(open(f))
         except Exception:
             continue
-        subs = [kernel_substr] if isinstance(kernel_substr, str) else list(kernel_substr)
         ks = [k for k in d.get("kernels", []) if k.get("hbm_bytes_per_launch") and
               any(x in k.get("name", "") for x in subs)]
-        if ks:  # several names: one launch of each per unit (the partitioned GROUP BY's kernel set)
-            return sum(k["hbm_bytes_per_launch"] for k in ks), ks[0].get("rows_per_launch"), os.path.basename(f)
-    return None
+        if not ks:
+            continue
+        src = {"file": "profiles/" + os.path.basename(f), "measured_at_commit": d.get("measured_at_commit"),
+               "kernel_sources_sha256": d.get("kernel_sources_sha256")}
+        if d.get("kernel_sources_sha256") != cur:
+            src["status"] = "stale: kernel sources changed since this PMC pass (current %s)" % cur[:12]
+            return None, src
+        src["status"] = "current kernel sources"
+        # several names: one launch of each per unit (the partitioned GROUP BY's kernel set)
+        per = sum(k["hbm_bytes_per_launch"] for k in ks)
+        rows = ks[0].get("rows_per_launch")
+        return (per * rows_per_launch / rows if rows else None), src
+    return None, {"status": "no PMC summary for this query in profiles/"}
 
 
 def cpu_baseline(sample_rows, threads, query="c3"):
@@ -319,10 +335,7 @@ def run_project(args, rank, world):
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
     value = n_total * args.steps / dt
     if rank == 0:
-        traffic = None
-        pmc = latest_pmc_traffic("fq_jit_pselect", "p1")
-        if pmc and pmc[1]:
-            traffic = pmc[0] * rows_per_launch / pmc[1]
+        traffic, traffic_src = latest_pmc_traffic("fq_jit_pselect", "p1", rows_per_launch)
         out = {
             "metric": METRIC, "value": value, "unit": "rows/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,
@@ -336,7 +349,7 @@ def run_project(args, rank, world):
                        "parallelism": "dp%d (numbers_mt partitions sharded)" % world},
             "achieved_hbm_gbps": achieved, "kernel_ms_per_launch": avg_ms, "scan_launches_per_step": len(cols),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
+                         "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": "fq_jit_pselect (fq_filter_project, hipRTC-specialised), one launch per partition; "
                                    "algorithmic bytes = 8 B per row read + 16 B per kept row written",
                          "bytes_per_launch": bytes_per_launch},
@@ -347,6 +360,8 @@ def run_project(args, rank, world):
                 out["cpu_baseline"] = cpu_baseline_project(int(args.cpu_sample_rows or 1e10), args.cpu_threads)
             except Exception as e:  # report, never hide
                 out["cpu_baseline"] = {"error": repr(e)}
+        if args.tuned:
+            out["tune"] = args.tuned
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
@@ -421,7 +436,15 @@ def main():
                     help="rows per radix-partitioned GROUP BY launch (FQ_OPT_GROUP_CHUNK_ROWS; tuning)")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="nccl = RCCL over xGMI (default); gloo rehearses N ranks on fewer GPUs")
+    ap.add_argument("--tune", action="append", default=[], metavar="KNOB=VALUE",
+                    help="launch-shape knob through fq_tune_set (abi.TUNE names; sweeps only, the defaults "
+                         "are the measured best)")
     args = ap.parse_args()
+    args.tuned = {}
+    for kv in args.tune:
+        k, v = kv.split("=", 1)
+        ops.tune_set(k.upper(), int(v))
+        args.tuned[k.upper()] = int(v)
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -567,12 +590,9 @@ def main():
     value = n_total * args.steps / dt
     out = None
     if rank == 0:
-        traffic = None
         # the partitioned GROUP BY (g2): gpart + block scatter + bins per chunk
-        pmc = latest_pmc_traffic(("fq_jit_gpart", "group_blk_", "fq_jit_groupby_bins") if args.query == "g2"
-                                 else kernel, args.query)
-        if pmc and pmc[1]:
-            traffic = pmc[0] * rows_per_launch / pmc[1]  # HBM bytes per launch, scaled to this launch size
+        traffic, traffic_src = latest_pmc_traffic(("fq_jit_gpart", "group_blk_", "fq_jit_groupby_bins")
+                                                  if args.query == "g2" else kernel, args.query, rows_per_launch)
         out = {
             "metric": METRIC,
             "value": value,
@@ -612,6 +632,7 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBPS,
                 "traffic": traffic,
+                "traffic_source": traffic_src,
                 "kernel": ("fq_group_aggregate (fq_jit_groupby, hipRTC-specialised), one launch per partition"
                            if args.query == "g1" else
                            "fq_group_aggregate_partitioned (fq_jit_gpart + block grouping + fq_jit_groupby_bins), "
@@ -638,6 +659,8 @@ def main():
         except Exception as e:  # report, never hide
             out["cpu_baseline"] = {"error": repr(e)}
     if rank == 0:
+        if args.tuned:
+            out["tune"] = args.tuned
         print(json.dumps(out), flush=True)
     if comm is not None:
         comm.close()

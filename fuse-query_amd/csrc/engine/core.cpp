@@ -313,8 +313,7 @@ class BlockCache {
         return *c;
     }
     void add_stream(hipStream_t s) {
-        static const bool off = getenv("FQ_NO_BLOCK_CACHE") != nullptr;  // A/B switch: plain stream-ordered pool
-        if (off) return;
+        if (!fqc::knob(FQ_TUNE_BLOCK_CACHE)) return;  // A/B switch: plain stream-ordered pool
         std::lock_guard<std::mutex> lk(mu_);
         free_.emplace(s, Queue());
     }

@@ -762,14 +762,6 @@ StreamRef GroupByPartialTransform::execute() {
 
 StreamRef GroupByFinalTransform::execute() {
     ExecCtx &ctx = ExecCtx::current();
-    static const bool trace = getenv("FQ_TRACE_GROUP_FINAL") != nullptr;  // phase times on stderr (tools)
-    int64_t tp = now_ns();
-    auto phase = [&](const char *what) {
-        if (!trace) return;
-        const int64_t t = now_ns();
-        fprintf(stderr, "[group final] %-8s %8.3f ms\n", what, (t - tp) * 1e-6);
-        tp = t;
-    };
     std::vector<FunctionRef> funcs;
     for (auto &f : funcs_) funcs.push_back(f->clone());
     const std::vector<AggregatorFunction *> leaves = leaves_of(funcs);
@@ -790,7 +782,6 @@ StreamRef GroupByFinalTransform::execute() {
             if (row.kind == DataValue::kStruct && !row.fields.empty()) exchanged.push_back(&row.fields);
         held.push_back(b);
     }
-    phase("input");
     if (shared_->ready) kdt = shared_->desc.key_dtype;
     else if (!exchanged.empty()) kdt = (*exchanged[0])[0].dtype;
     for (const std::vector<DataValue> *rp : exchanged) {
@@ -836,7 +827,6 @@ StreamRef GroupByFinalTransform::execute() {
             ctx.sync();
         }
     }
-    phase("fetch");
     std::vector<uint32_t> rows;  // one source row per group, in key order
     if (emit_states_ && exchanged.empty()) {
         // partial states of this rank's own table: the keys are unique and
@@ -860,7 +850,6 @@ StreamRef GroupByFinalTransform::execute() {
             i = j;
         }
     }
-    phase("sort");
     DataBlock out;
     out.schema = schema_;
     const size_t ng = rows.size();
@@ -933,7 +922,6 @@ StreamRef GroupByFinalTransform::execute() {
         if (!cols[c].empty() && cols[c][0].kind == DataValue::kSome) dt = cols[c][0].dtype;
         out.columns.push_back(Column::host_values(dt, std::move(cols[c])));
     }
-    phase("build");
     return std::make_unique<DataBlockStream>(std::vector<DataBlock>{out});
 }
 

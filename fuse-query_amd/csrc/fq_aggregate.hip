@@ -313,15 +313,8 @@ __global__ void __launch_bounds__(kThreads)
 
 static bool is_pow2(uint64_t v) { return v && !(v & (v - 1)); }
 
-// Workgroups per CU for the flat scan; FQ_SCAN_WG_PER_CU overrides (tuning).
-static int scan_wg_per_cu() {
-    static const int v = [] {
-        const char *e = getenv("FQ_SCAN_WG_PER_CU");
-        const int x = e ? atoi(e) : 0;
-        return (x >= 1 && x <= 16) ? x : 2;
-    }();
-    return v;
-}
+// Workgroups per CU for the flat scan (FQ_TUNE_SCAN_WG_PER_CU, default 2).
+static int scan_wg_per_cu() { return (int)fqc::knob(FQ_TUNE_SCAN_WG_PER_CU); }
 
 // libdivide's u64 round-up magic (branchful form)
 static void u64_magic(uint64_t d, uint64_t &magic, uint32_t &shift, uint32_t &add) {

@@ -255,7 +255,7 @@ __device__ __forceinline__ uint64_t spread32(uint32_t v) {
 // lane l the two results of lane l >> 1 (word 0) and of lane 32 + (l >> 1)
 // (word 1), so each word is a single ballot; interleaving two 32-bit ballots
 // on the scalar unit instead (spread32, 4 per segment) cost 1.68 vs 1.55 ms
-// per 10 GB (tools/bench_kernels.py; FQ_CMP_SPREAD=1 keeps it for A/B).
+// per 10 GB (tools/bench_kernels.py; FQ_TUNE_CMP_SPREAD=1 keeps it for A/B).
 template <typename TC, int CMP, bool LSC, bool RSC, bool SPREAD>
 __global__ void __launch_bounds__(256)
     compare_vec_kernel(const TC *__restrict__ l, uint64_t lc, const TC *__restrict__ r, uint64_t rc,
@@ -310,7 +310,7 @@ static void launch_vec_op(bool lsc, bool rsc, const void *l, uint64_t lc, const 
     const TC *L = (const TC *)l, *R = (const TC *)r;
     if constexpr (CMPK) {
         uint64_t *bm = (uint64_t *)out;
-        static const bool spread = getenv("FQ_CMP_SPREAD") != nullptr;  // A/B: the scalar-unit interleave
+        const bool spread = fqc::knob(FQ_TUNE_CMP_SPREAD) != 0;  // A/B: the scalar-unit interleave
         if (spread) {
             if (lsc) hipLaunchKernelGGL((compare_vec_kernel<TC, OP, true, false, true>), dim3(grid), dim3(256), 0, st, L, lc, R, rc, bm, units);
             else if (rsc) hipLaunchKernelGGL((compare_vec_kernel<TC, OP, false, true, true>), dim3(grid), dim3(256), 0, st, L, lc, R, rc, bm, units);
@@ -461,12 +461,8 @@ static fq_status launch_fast(bool cmp, int32_t tc, EwArgs &a) {
     if (units == 0) return FQ_OK;
     // workgroups per CU: arith 8, compare 2 (tools/probes/ew_wg_sweep.sh, one box:
     // arith u64 + const 3.57/3.49/3.44/3.38 ms at 1/2/4/8, compare 1.68/1.71/1.75/1.73);
-    // FQ_EW_WG_PER_CU overrides both (tuning)
-    static const int wg_override = [] {
-        const char *e = getenv("FQ_EW_WG_PER_CU");
-        const int x = e ? atoi(e) : 0;
-        return x >= 1 && x <= 16 ? x : 0;
-    }();
+    // FQ_TUNE_EW_WG_PER_CU overrides both (tuning)
+    const int wg_override = (int)fqc::knob(FQ_TUNE_EW_WG_PER_CU);
     const int64_t cap = (int64_t)fqc::device_cu_count() * (wg_override ? wg_override : (cmp ? 2 : 8));
     // arith: one tile per workgroup iteration; compare: one 1,024-row group per wave
     const int64_t want = cmp ? (units + 3) / 4 : units;

@@ -334,18 +334,10 @@ fq_status launch_group_part_blocks(const GroupPartition &X, hipStream_t stream) 
 }
 
 // Workgroups of fq_jit_gpart for len rows: two 1,024-thread workgroups per CU
-// (its 77 KB of LDS; FQ_GPART_WG_PER_CU tunes it), at most one per 8-row tile
-// of 256 threads -- the bound the workspace is sized by
-static int part_wg_per_cu() {
-    static const int v = [] {
-        const char *e = getenv("FQ_GPART_WG_PER_CU");
-        const int x = e ? atoi(e) : 2;
-        return x >= 1 && x <= 4 ? x : 2;
-    }();
-    return v;
-}
-static int tune_env(const char *name, int def, int lo, int hi);
-static int group_threads() { return tune_env("FQ_GROUP_THREADS", 1024, 256, 1024) & ~255; }
+// (its 77 KB of LDS; FQ_TUNE_GPART_WG_PER_CU tunes it), at most one per 8-row tile
+// of 256 threads -- the bound the workspace is sized by (FQ_TUNE_GPART_WG_PER_CU)
+static int part_wg_per_cu() { return (int)fqc::knob(FQ_TUNE_GPART_WG_PER_CU); }
+static int group_threads() { return (int)fqc::knob(FQ_TUNE_GROUP_THREADS); }
 // (at least 4 tiles per workgroup: every workgroup's region holds a partial
 // block per bin, P x 2 KB, which for a small column would outweigh its rows)
 static int64_t part_grid_bound(int64_t len) {
@@ -394,16 +386,8 @@ static size_t part_ws_bytes(int64_t len, int log2p, GroupPartition *X, void *ws)
     return head + sc + 2 * bb + ord + vals;
 }
 
-// tuning knobs of the GROUP BY launch (tools/groupby_sweep.py); the
-// defaults are the measured best, out-of-range values fall back to them
-static int tune_env(const char *name, int def, int lo, int hi) {
-    const char *e = getenv(name);
-    if (!e) return def;
-    const int v = atoi(e);
-    return (v >= lo && v <= hi) ? v : def;
-}
-
-static int group_lds_bytes() { return tune_env("FQ_GROUP_LDS_KB", 128, 8, 160) * 1024; }
+// LDS table budget of the GROUP BY launch (FQ_TUNE_GROUP_LDS_KB; tools/groupby_sweep.py)
+static int group_lds_bytes() { return (int)fqc::knob(FQ_TUNE_GROUP_LDS_KB) * 1024; }
 
 // validation + lowering shared by both aggregate entry points
 static fq_status prepare_group(const fq_group_table *t, const fq_col *col, const fq_pred *pred,
@@ -459,11 +443,11 @@ static fq_status prepare_group(const fq_group_table *t, const fq_col *col, const
     // against 2.25 ms here, and the table holds twice the groups)
     G.lds_bytes = group_lds_bytes();
     G.threads = group_threads();
-    G.rowmap = tune_env("FQ_GROUP_ROWMAP", 1, 0, 1);
+    G.rowmap = (int)fqc::knob(FQ_TUNE_GROUP_ROWMAP);
     const int64_t nvec = (G.n - G.head) / 2;
     int64_t grid = (nvec + 4 * G.threads - 1) / (4 * G.threads);
     if (grid < 1) grid = 1;
-    const int64_t cap = (int64_t)fqc::device_cu_count() * tune_env("FQ_GROUP_WG_PER_CU", 1, 1, 8);
+    const int64_t cap = (int64_t)fqc::device_cu_count() * fqc::knob(FQ_TUNE_GROUP_WG_PER_CU);
     G.grid = (int)(grid < cap ? grid : cap);
     return FQ_OK;
 }
@@ -543,7 +527,7 @@ fq_status fq_group_aggregate_partitioned(const fq_group_table *t, const fq_col *
     int lp_arg = log2_parts;
     const int64_t d = group_key_range(G.key, G.key_dtype);
     const int64_t S = group_lds_slots(G.n_aggs, G.lds_bytes);
-    if (d > 0 && tune_env("FQ_GROUP_RANGE_BINS", 1, 0, 1)) {
+    if (d > 0 && fqc::knob(FQ_TUNE_GROUP_RANGE_BINS)) {
         int sh = 0;
         while (((int64_t)1 << log2_parts << sh) < d) ++sh;
         if (((int64_t)1 << sh) <= S) {

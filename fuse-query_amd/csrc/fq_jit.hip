@@ -71,8 +71,7 @@ const Rtc &rtc() {
     static const Rtc r = [] {
         Rtc x;
         void *h = nullptr;
-        const char *mode = getenv("FQ_JIT_RTC");
-        if (!mode || strcmp(mode, "process") != 0) {
+        if (fqc::knob(FQ_TUNE_JIT_ISOLATED)) {
             const char *root = getenv("ROCM_PATH");
             const std::string path = std::string(root && *root ? root : "/opt/rocm") + "/lib/libhiprtc.so.7";
             h = dlmopen(LM_ID_NEWLM, path.c_str(), RTLD_NOW | RTLD_LOCAL);
@@ -223,16 +222,9 @@ void put_pred_key(const KPred &pr, std::string &k) {
     }
 }
 
-// 16-byte vectors per lane in flight in the block-mode scan (FQ_BLOCK_U: 4, 8
-// or 16; tuning)
-int block_mode_vectors() {
-    static const int v = [] {
-        const char *e = getenv("FQ_BLOCK_U");
-        const int u = e ? atoi(e) : 8;
-        return (u == 4 || u == 16) ? u : 8;
-    }();
-    return v;
-}
+// 16-byte vectors per lane in flight in the block-mode scan (FQ_TUNE_BLOCK_U:
+// 4, 8 or 16)
+int block_mode_vectors() { return (int)fqc::knob(FQ_TUNE_BLOCK_U); }
 
 // Binary shape key: everything the generated source depends on.
 std::string shape_key(const Launch &L, int32_t tin, bool chain, int dev) {
@@ -700,60 +692,28 @@ bool gen_source(const Launch &L, int32_t tin, bool chain, Gen &g, std::string &s
 // ---------------------------------------------------------------------------
 
 // LDS slot hash of the GROUP BY kernel: 1 (default) keeps consecutive keys in
-// consecutive slots, 0 = Fibonacci hash of the whole key (FQ_GROUP_LDS_LOCAL)
-int group_lds_local() {
-    static const int v = [] {
-        const char *e = getenv("FQ_GROUP_LDS_LOCAL");
-        return e ? (atoi(e) ? 1 : 0) : 1;
-    }();
-    return v;
-}
+// consecutive slots, 0 = Fibonacci hash of the whole key (FQ_TUNE_GROUP_LDS_LOCAL)
+int group_lds_local() { return (int)fqc::knob(FQ_TUNE_GROUP_LDS_LOCAL); }
 
 // HBM key probe of the GROUP BY kernel: 1 = plain cached read first
-// (FQ_GROUP_KEY_PLAIN), 0 = agent-scope atomic read
-int group_key_plain() {
-    static const int v = [] {
-        const char *e = getenv("FQ_GROUP_KEY_PLAIN");
-        return e ? (atoi(e) ? 1 : 0) : 1;
-    }();
-    return v;
-}
+// (FQ_TUNE_GROUP_KEY_PLAIN), 0 = agent-scope atomic read
+int group_key_plain() { return (int)fqc::knob(FQ_TUNE_GROUP_KEY_PLAIN); }
 
 // wave-uniform key runs merged across the wave (fq_wave_runs): 1 (default),
-// 0 = off (FQ_GROUP_WAVE_RUNS; tools/group_shapes_probe.py)
-int group_wave_runs() {
-    static const int v = [] {
-        const char *e = getenv("FQ_GROUP_WAVE_RUNS");
-        const int x = e ? atoi(e) : 1;
-        return x >= 0 && x <= 2 ? x : 1;
-    }();
-    return v;
-}
+// 0 = off (FQ_TUNE_GROUP_WAVE_RUNS; tools/group_shapes_probe.py)
+int group_wave_runs() { return (int)fqc::knob(FQ_TUNE_GROUP_WAVE_RUNS); }
 
 // clustered-key row layout of the GROUP BY kernel (mode 1 in fq_jit_groupby):
 // chosen per workgroup from its first tile when a wave's 512 rows change key
 // at most this often (default 160: runs of ~4+ rows), 0 = never
-// (FQ_GROUP_CLUSTER; tools/group_shapes_probe.py)
-int group_cluster() {
-    static const int v = [] {
-        const char *e = getenv("FQ_GROUP_CLUSTER");
-        const int x = e ? atoi(e) : 160;
-        return x >= 0 && x <= 512 ? x : 160;
-    }();
-    return v;
-}
+// (FQ_TUNE_GROUP_CLUSTER; tools/group_shapes_probe.py)
+int group_cluster() { return (int)fqc::knob(FQ_TUNE_GROUP_CLUSTER); }
 
 // GROUP BY tile order: 1 (default) = one contiguous run of tiles per
-// workgroup, 0 = grid stride over tiles (FQ_GROUP_CHUNKED; tools/
+// workgroup, 0 = grid stride over tiles (FQ_TUNE_GROUP_CHUNKED; tools/
 // group_shapes_probe.py: % 1000 keys 1.569 -> 1.531 ms per 10 GB, % 4093
 // 1.656 -> 1.605)
-int group_chunked() {
-    static const int v = [] {
-        const char *e = getenv("FQ_GROUP_CHUNKED");
-        return e ? (atoi(e) ? 1 : 0) : 1;
-    }();
-    return v;
-}
+int group_chunked() { return (int)fqc::knob(FQ_TUNE_GROUP_CHUNKED); }
 
 int lds_slots(int n_aggs, int budget) {
     int s = 16384;
@@ -1832,36 +1792,19 @@ void pack_proj_consts(const ProjLaunch &P, HostProjConsts &hc) {
     pack_tree_consts(P.pred, hc);
 }
 
-// FQ_SELECT_VARIANT (tuning, tools/select_sweep.sh): bit 0 per-XCD ticket
+// FQ_TUNE_SELECT_VARIANT (tuning, tools/select_sweep.sh): bit 0 per-XCD ticket
 // counters (default on).
-int select_variant() {
-    static const int v = [] {
-        const char *e = getenv("FQ_SELECT_VARIANT");
-        const int x = e ? atoi(e) : 1;
-        return (x >= 0 && x <= 1) ? x : 1;
-    }();
-    return v;
-}
-// FQ_SELECT_DEBUG=1 (tuning only): the select kernel counts tiles, polls and
+int select_variant() { return (int)fqc::knob(FQ_TUNE_SELECT_VARIANT); }
+// FQ_TUNE_SELECT_DEBUG=1 (tuning only): the select kernel counts tiles, polls and
 // cycles per phase into a module global that is printed after each launch
-int select_debug() {
-    static const int v = [] {
-        const char *e = getenv("FQ_SELECT_DEBUG");
-        return (e && atoi(e) == 1) ? 1 : 0;
-    }();
-    return v;
-}
-// FQ_SELECT_LBW: status words per lane per look-back round trip (1/2/4/8;
+int select_debug() { return (int)fqc::knob(FQ_TUNE_SELECT_DEBUG); }
+// the last debug launch's counters (fq_tune_select_counters)
+std::mutex g_select_counters_mu;
+uint64_t g_select_counters[FQ_TUNE_SELECT_COUNTERS] = {};
+// FQ_TUNE_SELECT_LBW: status words per lane per look-back round trip (1/2/4/8;
 // wider windows measured slower: the polls' extra agent-scope loads cost more
 // than the round trips they save, tools/select_sweep.sh)
-int select_lbw() {
-    static const int v = [] {
-        const char *e = getenv("FQ_SELECT_LBW");
-        const int x = e ? atoi(e) : 1;
-        return (x == 2 || x == 4 || x == 8) ? x : 1;
-    }();
-    return v;
-}
+int select_lbw() { return (int)fqc::knob(FQ_TUNE_SELECT_LBW); }
 // XCDs of the device (MI355X: 32 CUs each; 8 in SPX mode, fewer in the
 // partitioned modes), at most kMaxSelectXcds ticket counters
 int select_xcds(int dev) {
@@ -2390,8 +2333,8 @@ fq_status compile(const std::string &src, int dev, Compiled &out, const char *fn
     const auto t1 = std::chrono::steady_clock::now();
     g_compile_us += (int64_t)std::chrono::duration_cast<std::chrono::microseconds>(t1 - t0).count();
     g_compiled += 1;
-    if (const char *d = getenv("FQ_JIT_DUMP")) {
-        const std::string p = std::string(d) + "/fq_jit_" + std::to_string(g_compiled.load()) + ".hip";
+    if (const std::string d = fqc::jit_dump_dir(); !d.empty()) {
+        const std::string p = d + "/fq_jit_" + std::to_string(g_compiled.load()) + ".hip";
         if (FILE *f = fopen(p.c_str(), "w")) {
             fwrite(src.data(), 1, src.size(), f);
             fclose(f);
@@ -2711,11 +2654,7 @@ fq_status jit_project_select(int32_t col_dtype, const ProjLaunch &P, const uint6
     long long n = P.n;
     const int64_t ntiles = (P.n + select_tile_rows() - 1) / select_tile_rows();
     void *args[] = {&col, &n, &hc, &d_bitmap, &outs, &status, &ticket, &d_flags, &d_total};
-    static const int wg_per_cu = [] {
-        const char *e = getenv("FQ_SELECT_WG_PER_CU");
-        const int v = e ? atoi(e) : 0;
-        return v >= 1 && v <= 16 ? v : 8;
-    }();
+    const int wg_per_cu = (int)fqc::knob(FQ_TUNE_SELECT_WG_PER_CU);
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     (void)hipGetLastError();
@@ -2723,40 +2662,17 @@ fq_status jit_project_select(int32_t col_dtype, const ProjLaunch &P, const uint6
     FQ_HIP_TRY(hipModuleLaunchKernel(k.scatter, (unsigned)grid, 1, 1, (unsigned)select_threads(), 1, 1, 0, P.stream,
                                      args, nullptr));
     g_jit_launches += 1;
-    if (select_debug() && k.mod) {  // tuning only: print and clear the kernel's phase counters
+    if (select_debug() && k.mod) {  // tuning only: keep and clear the kernel's phase counters
         hipDeviceptr_t d = nullptr;
         size_t bytes = 0;
-        unsigned long long h[13] = {0};
+        unsigned long long h[FQ_TUNE_SELECT_COUNTERS] = {0};
         if (hipModuleGetGlobal(&d, &bytes, k.mod, "ps_dbg") == hipSuccess && bytes == sizeof h) {
             (void)hipStreamSynchronize(P.stream);
-            (void)hipMemcpyDtoH(h, d, sizeof h);
-            fprintf(stderr, "[select-debug] grid %lld tiles %llu polls/tile %.2f windows/tile %.2f | per tile (cycles): ticket %.0f load+pred %.0f lookback %.0f store %.0f | wg cycles %.0f\n",
-                    (long long)grid, h[0], (double)h[1] / h[0], (double)h[7] / h[0], (double)h[3] / h[0], (double)h[4] / h[0],
-                    (double)h[2] / h[0], (double)h[5] / h[0], (double)h[6] / grid);
-            fprintf(stderr, "[select-debug] workgroup starts spread %.1f us, ends spread %.1f us, first start -> last end %.1f us (100 MHz wall clock)\n",
-                    (double)(h[9] - h[8]) / 100.0, (double)(h[11] - h[10]) / 100.0, (double)(h[11] - h[8]) / 100.0);
-            int occ = -1;
-            (void)hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k.scatter, select_threads(), 0);
-            int nregs = -1, lds = -1, scratch = -1;
-            (void)hipFuncGetAttribute(&nregs, HIP_FUNC_ATTRIBUTE_NUM_REGS, k.scatter);
-            (void)hipFuncGetAttribute(&lds, HIP_FUNC_ATTRIBUTE_SHARED_SIZE_BYTES, k.scatter);
-            (void)hipFuncGetAttribute(&scratch, HIP_FUNC_ATTRIBUTE_LOCAL_SIZE_BYTES, k.scatter);
-            fprintf(stderr, "[select-debug] occupancy %d workgroups/CU (regs %d, lds %d, scratch %d)\n", occ, nregs, lds, scratch);
-            fprintf(stderr, "[select-debug] mean workgroup life %.1f us, s_memtime rate %.0f MHz\n",
-                    (double)h[12] / grid / 100.0, (double)h[6] / (double)h[12] * 100.0);
-            if (const char *path = getenv("FQ_SELECT_DEBUG_WG")) {
-                std::vector<unsigned long long> w((size_t)grid * 4);
-                hipDeviceptr_t dw = nullptr;
-                size_t wb = 0;
-                if (hipModuleGetGlobal(&dw, &wb, k.mod, "ps_wg") == hipSuccess &&
-                    hipMemcpyDtoH(w.data(), dw, w.size() * 8) == hipSuccess)
-                    if (FILE *f = fopen(path, "w")) {
-                        for (long long b = 0; b < grid; ++b)
-                            fprintf(f, "%lld %llu %llu %llu %llu\n", b, w[b * 4], w[b * 4 + 1], w[b * 4 + 2], w[b * 4 + 3]);
-                        fclose(f);
-                    }
+            if (hipMemcpyDtoH(h, d, sizeof h) == hipSuccess) {
+                std::lock_guard<std::mutex> lk(g_select_counters_mu);
+                for (int i = 0; i < FQ_TUNE_SELECT_COUNTERS; ++i) g_select_counters[i] = h[i];
             }
-            unsigned long long z[13] = {0};
+            unsigned long long z[FQ_TUNE_SELECT_COUNTERS] = {0};
             z[8] = z[10] = ~0ull;
             (void)hipMemcpyHtoD(d, z, sizeof z);
         }
@@ -2797,6 +2713,13 @@ fq_status fq_jit_config(int32_t mode, int64_t min_rows) {
     if (min_rows < 0) return fqc::fail(FQ_E_INVALID, "fq_jit_config: negative min_rows");
     fqk::g_mode.store(mode);
     fqk::g_min_rows.store(min_rows);
+    return FQ_OK;
+}
+
+fq_status fq_tune_select_counters(uint64_t *out, int32_t n) {
+    if (!out || n < 0 || n > FQ_TUNE_SELECT_COUNTERS) return fqc::fail(FQ_E_INVALID, "fq_tune_select_counters: bad argument");
+    std::lock_guard<std::mutex> lk(fqk::g_select_counters_mu);
+    for (int32_t i = 0; i < n; ++i) out[i] = fqk::g_select_counters[i];
     return FQ_OK;
 }
 

@@ -5,6 +5,7 @@
 
 #include <stdlib.h>
 
+#include "fq_common.h"
 #include "fq_device.h"
 
 namespace fqk {
@@ -154,34 +155,13 @@ fq_status jit_project_bits(int32_t col_dtype, const ProjLaunch &P, uint64_t *d_b
 // rows.  status: one zeroed word per tile; ticket: one zeroed word;
 // d_flags[0] predicate errors, d_flags[1] expression errors (bit 31: the
 // look-back gave up); *d_total = rows kept.
-// tile = select_threads() x select_rows_per_thread() rows (FQ_SELECT_THREADS
-// 256/512/1024, FQ_SELECT_ROWS 8/16/32: tuning; tools/select_sweep.sh)
-inline int select_threads() {
-    static const int v = [] {
-        const char *e = getenv("FQ_SELECT_THREADS");
-        const int t = e ? atoi(e) : 256;
-        return (t == 512 || t == 1024) ? t : 256;
-    }();
-    return v;
-}
-inline int select_rows_per_thread() {
-    static const int v = [] {
-        const char *e = getenv("FQ_SELECT_ROWS");
-        const int r = e ? atoi(e) : 32;
-        return (r == 8 || r == 16) ? r : 32;
-    }();
-    return v;
-}
+// tile = select_threads() x select_rows_per_thread() rows (FQ_TUNE_SELECT_THREADS
+// 256/512/1024, FQ_TUNE_SELECT_ROWS 8/16/32: tuning; tools/select_sweep.sh)
+inline int select_threads() { return (int)fqc::knob(FQ_TUNE_SELECT_THREADS); }
+inline int select_rows_per_thread() { return (int)fqc::knob(FQ_TUNE_SELECT_ROWS); }
 // s_sleep between look-back polls of a predecessor that has not published
-// (FQ_SELECT_SLEEP 0..127, tuning; default 2)
-inline int select_sleep() {
-    static const int v = [] {
-        const char *e = getenv("FQ_SELECT_SLEEP");
-        const int x = e ? atoi(e) : 2;
-        return (x >= 0 && x <= 127) ? x : 2;
-    }();
-    return v;
-}
+// (FQ_TUNE_SELECT_SLEEP 0..127, tuning; default 2)
+inline int select_sleep() { return (int)fqc::knob(FQ_TUNE_SELECT_SLEEP); }
 // ticket counters of fq_jit_pselect (one per XCD, each on its own 128-B line)
 constexpr int kMaxSelectXcds = 16;
 inline int64_t select_tile_rows() { return (int64_t)select_threads() * select_rows_per_thread(); }

@@ -21,7 +21,8 @@ GPU_SYMBOLS = [
     "fq_group_table_bytes", "fq_group_table_init", "fq_group_aggregate", "fq_group_table_count",
     "fq_group_table_extract", "fq_logic", "fq_filter_project_workspace_bytes", "fq_filter_project",
     "fq_predicate_bitmap", "fq_group_partition_workspace_bytes", "fq_group_aggregate_partitioned",
-    "fq_group_dense_keys", "fq_group_table_merge",
+    "fq_group_dense_keys", "fq_group_table_merge", "fq_tune_set", "fq_tune_get", "fq_tune_reset",
+    "fq_tune_select_counters", "fq_tune_jit_dump_dir",
 ]
 
 
@@ -91,6 +92,11 @@ _protos = {
     "fq_group_table_extract": (C.c_int32, [P(abi.fq_group_table), vp, P(C.c_void_p), C.c_int64, P(C.c_int64),
                                            vp]),
     "fq_group_table_merge": (C.c_int32, [P(abi.fq_group_table), vp, P(C.c_void_p), C.c_int64, vp]),
+    "fq_tune_set": (C.c_int32, [C.c_int32, C.c_int64]),
+    "fq_tune_get": (C.c_int64, [C.c_int32]),
+    "fq_tune_reset": (C.c_int32, []),
+    "fq_tune_select_counters": (C.c_int32, [P(C.c_uint64), C.c_int32]),
+    "fq_tune_jit_dump_dir": (C.c_int32, [C.c_char_p]),
 }
 for _name, (_res, _args) in _protos.items():
     _f = getattr(lib, _name)

@@ -389,3 +389,22 @@ def group_compile_check(col_dtype, aggs, key=None, values=None, pred=None, key_d
         check(lib.fq_group_aggregate_partitioned(C.byref(d), C.byref(c), p, k, vals, log2_parts, None, 0, None))
     else:
         check(lib.fq_group_aggregate(C.byref(d), C.byref(c), p, k, vals, None))
+
+
+def tune_set(name, value):
+    """fq_tune_set by knob name (abi.TUNE); tuning tools only."""
+    check(lib.fq_tune_set(abi.TUNE[name], int(value)))
+
+
+def tune_get(name):
+    return int(lib.fq_tune_get(abi.TUNE[name]))
+
+
+def tune_reset():
+    check(lib.fq_tune_reset())
+
+
+def tune_select_counters():
+    out = (C.c_uint64 * abi.TUNE_SELECT_COUNTERS)()
+    check(lib.fq_tune_select_counters(out, abi.TUNE_SELECT_COUNTERS))
+    return list(out)

@@ -336,6 +336,53 @@ fq_status fq_jit_get_stats(fq_jit_stats *out);
 fq_status fq_jit_prepare(const fq_col *col, int64_t block_rows, const fq_pred *pred,
                          const fq_expr *value, uint32_t agg_mask, int32_t *specialised);
 
+/* ---- Launch-shape knobs (tuning tools only; no reference counterpart) ----
+ * Every knob has a compiled-in default, the measured best on MI355X
+ * (DESIGN.md "Launch-shape knobs" names the sweep each came from).  The
+ * library reads no environment variable for them and never prints: the sweep
+ * tools (bench.py --tune, tools/) set them here.  Knobs read by a hipRTC
+ * kernel are part of its shape key, so a change applies from the next launch. */
+#define FQ_TUNE_SCAN_WG_PER_CU 0     /* fused aggregate scan: workgroups per CU, 2 (1..16)      */
+#define FQ_TUNE_EW_WG_PER_CU 1       /* arith/compare kernels: 0 = per-op defaults (8/2), 1..16 */
+#define FQ_TUNE_CMP_SPREAD 2         /* compare kernel scalar-unit interleave: 0 (0/1)           */
+#define FQ_TUNE_GPART_WG_PER_CU 3    /* GROUP BY partition kernel: workgroups per CU, 2 (1..4)   */
+#define FQ_TUNE_GROUP_THREADS 4      /* GROUP BY kernels: threads per workgroup, 1024 (256..1024 step 256) */
+#define FQ_TUNE_GROUP_LDS_KB 5       /* GROUP BY LDS table budget, 128 (8..160)                  */
+#define FQ_TUNE_BLOCK_U 6            /* block-mode scan: 16-B vectors per lane in flight, 8 (4/8/16) */
+#define FQ_TUNE_GROUP_LDS_LOCAL 7    /* LDS slot hash keeps consecutive keys adjacent: 1 (0/1)   */
+#define FQ_TUNE_GROUP_KEY_PLAIN 8    /* HBM key probe reads plain before atomic: 1 (0/1)          */
+#define FQ_TUNE_GROUP_WAVE_RUNS 9    /* wave-uniform key runs merged across the wave: 1 (0..2)    */
+#define FQ_TUNE_GROUP_CLUSTER 10     /* clustered row layout threshold (key changes/wave): 160 (0..512) */
+#define FQ_TUNE_GROUP_CHUNKED 11     /* contiguous tile runs per workgroup: 1 (0/1)               */
+#define FQ_TUNE_SELECT_VARIANT 12    /* filter+projection: per-XCD ticket counters, 1 (0/1)       */
+#define FQ_TUNE_SELECT_DEBUG 13      /* filter+projection: count phase cycles (fq_tune_select_counters), 0 (0/1) */
+#define FQ_TUNE_SELECT_LBW 14        /* look-back status words per lane per poll, 1 (1/2/4/8)     */
+#define FQ_TUNE_SELECT_WG_PER_CU 15  /* filter+projection workgroups per CU, 8 (1..16)            */
+#define FQ_TUNE_SELECT_THREADS 16    /* filter+projection threads per workgroup, 256 (256/512/1024) */
+#define FQ_TUNE_SELECT_ROWS 17       /* filter+projection rows per thread per tile, 32 (8/16/32)  */
+#define FQ_TUNE_SELECT_SLEEP 18      /* s_sleep between look-back polls, 2 (0..127)              */
+#define FQ_TUNE_BLOCK_CACHE 19       /* engine's stream-ordered device block cache, 1 (0/1)       */
+#define FQ_TUNE_JIT_ISOLATED 20      /* hipRTC loaded in its own link namespace, 1 (0/1; before the first compile) */
+#define FQ_TUNE_GROUP_ROWMAP 21      /* GROUP BY LDS kernel row map: 1 (0/1)                     */
+#define FQ_TUNE_GROUP_WG_PER_CU 22   /* GROUP BY LDS kernel workgroups per CU: 1 (1..8)           */
+#define FQ_TUNE_GROUP_RANGE_BINS 23  /* partitioned GROUP BY: range bins for `% d` keys, 1 (0/1) */
+#define FQ_TUNE_COUNT 24
+/* FQ_E_INVALID for an unknown knob or a value outside the knob's set */
+fq_status fq_tune_set(int32_t knob, int64_t value);
+/* the knob's current value; -1 for an unknown knob */
+int64_t fq_tune_get(int32_t knob);
+/* every knob back to its default */
+fq_status fq_tune_reset(void);
+/* Counters of the last fq_jit_pselect launch made with FQ_TUNE_SELECT_DEBUG
+ * = 1 (FQ_TUNE_SELECT_COUNTERS words: tiles, polls, look-back, ticket,
+ * load+predicate, store cycles, workgroup cycles, look-back windows, first/last
+ * workgroup start, first/last end, summed workgroup life); n <= that.       */
+#define FQ_TUNE_SELECT_COUNTERS 13
+fq_status fq_tune_select_counters(uint64_t *out, int32_t n);
+/* dir != NULL: every hipRTC source compiled from now on is written to dir
+ * (with its code object) for ISA inspection; NULL turns it off.            */
+fq_status fq_tune_jit_dump_dir(const char *dir);
+
 /* ---- GROUP BY hash aggregation (NO reference counterpart:
  * plan_parser.rs:284-308 plans group_expr but pipeline_builder.rs:50-66 builds
  * AggregatePartial/Final from aggr_expr only, so the reference has no grouped

@@ -149,3 +149,31 @@ def test_engine_and_function_symbol_lists_match_header():
     from fq_amd.engine import ENGINE_SYMBOLS
     from fq_amd.functions import FUNCTION_SYMBOLS
     assert sorted(ENGINE_SYMBOLS + FUNCTION_SYMBOLS) == declared_symbols("fq_engine.h")
+
+
+def test_tuning_knobs_defaults_set_reset():
+    from fq_amd import ops
+    assert ops.tune_get("SCAN_WG_PER_CU") == 2 and ops.tune_get("SELECT_LBW") == 1
+    assert ops.tune_get("SELECT_THREADS") == 256 and ops.tune_get("GROUP_LDS_KB") == 128
+    ops.tune_set("SELECT_LBW", 4)
+    assert ops.tune_get("SELECT_LBW") == 4
+    for name, bad in [("SELECT_LBW", 3), ("SELECT_THREADS", 768), ("GROUP_THREADS", 300), ("SCAN_WG_PER_CU", 0)]:
+        with pytest.raises(Exception, match="outside knob"):
+            ops.tune_set(name, bad)
+    ops.tune_reset()
+    assert ops.tune_get("SELECT_LBW") == 1
+    assert lib.fq_tune_get(99) == -1
+
+
+def test_product_reads_no_tuning_environment_and_never_prints():
+    # the only environment the library reads is the documented JIT policy
+    # (FQ_JIT, FQ_JIT_MIN_ROWS) and where ROCm lives; knobs go through fq_tune_set
+    csrc = os.path.join(ROOT, "fuse-query_amd", "csrc")
+    envs, prints = set(), []
+    for d, _, files in os.walk(csrc):
+        for f in files:
+            src = open(os.path.join(d, f)).read()
+            envs |= set(re.findall(r'getenv\("(\w+)"\)', src))
+            prints += [(f, m) for m in re.findall(r"\b(f?printf|puts|std::cerr|std::cout)\s*(?:\(|<<)", src)]
+    assert envs == {"FQ_JIT", "FQ_JIT_MIN_ROWS", "ROCM_PATH"}
+    assert not prints, prints

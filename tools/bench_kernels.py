@@ -23,6 +23,9 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from fq_amd import abi, ops  # noqa: E402
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import knobs  # noqa: E402
+knobs.apply_env()
 from fq_amd._lib import check, lib  # noqa: E402
 from fq_amd.expr import chain, predicate  # noqa: E402
 

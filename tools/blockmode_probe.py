@@ -9,6 +9,9 @@ import torch  # noqa: E402
 
 from fq_amd import abi, ops  # noqa: E402
 from fq_amd._lib import check, lib  # noqa: E402
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import knobs  # noqa: E402
+knobs.apply_env()
 from fq_amd.expr import chain, predicate  # noqa: E402
 
 n = 1_250_000_000
@@ -36,4 +39,4 @@ for _ in range(15):
     e1.synchronize()
     ts.append(e0.elapsed_time(e1))
 ms = statistics.median(ts)
-print("FQ_BLOCK_U=%s: %.3f ms, %.0f GB/s" % (os.environ.get("FQ_BLOCK_U", "8"), ms, 8 * n / ms / 1e6), flush=True)
+print("FQ_BLOCK_U=%s: %.3f ms, %.0f GB/s" % (os.environ.get("FQ_TUNE_BLOCK_U", "8"), ms, 8 * n / ms / 1e6), flush=True)

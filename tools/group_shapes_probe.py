@@ -11,6 +11,9 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(
 import torch  # noqa: E402
 
 from fq_amd.engine import Engine  # noqa: E402
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import knobs  # noqa: E402
+knobs.apply_env()
 
 N = 10**10
 KEYS = ["number%1000", "number%4093", "(number*7)%1000", "number/1000000", "number/10000000", "number/100000000",

@@ -9,6 +9,9 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(
 import torch
 from fq_amd import abi, ops
 from fq_amd._lib import check, lib
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import knobs  # noqa: E402
+knobs.apply_env()
 from fq_amd.expr import chain
 U = abi.DT_UINT64
 n = int(float(sys.argv[1])) if len(sys.argv) > 1 else 1_250_000_000

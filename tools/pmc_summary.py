@@ -11,8 +11,12 @@ usage: pmc_summary.py OUT.json ROWS_PER_LAUNCH counter_collection.csv [...]
 """
 import csv
 import json
+import os
 import sys
 from collections import defaultdict
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from srchash import kernel_sources_sha256  # noqa: E402
 
 
 def main():
@@ -43,7 +47,7 @@ def main():
             k["traffic_over_algorithmic"] = k["hbm_bytes_per_launch"] / (8.0 * rows_per_launch)
         kernels.append(k)
     json.dump({"source": files, "correction": "read = 2 x FETCH_SIZE KB (gfx950), write = WRITE_SIZE KB",
-               "kernels": kernels}, open(out, "w"), indent=1)
+               "kernel_sources_sha256": kernel_sources_sha256(), "kernels": kernels}, open(out, "w"), indent=1)
     for k in kernels:
         print(k["name"][:90], {c: round(v, 3) for c, v in k.items() if isinstance(v, float)})
 

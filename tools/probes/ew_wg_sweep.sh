@@ -1,4 +1,4 @@
-for w in 1 2 4 8; do FQ_EW_WG_PER_CU=$w timeout -k 10 300 python tools/bench_kernels.py > gpurun_out/k_w$w.json 2>/dev/null || exit 1; done
+for w in 1 2 4 8; do FQ_TUNE_EW_WG_PER_CU=$w timeout -k 10 300 python tools/bench_kernels.py > gpurun_out/k_w$w.json 2>/dev/null || exit 1; done
 python3 - <<'PY'
 import json
 for w in (1,2,4,8):

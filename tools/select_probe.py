@@ -9,6 +9,9 @@ import torch  # noqa: E402
 
 from fq_amd import abi, ops  # noqa: E402
 from fq_amd._lib import check, lib  # noqa: E402
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import knobs  # noqa: E402
+knobs.apply_env()
 from fq_amd.expr import chain, predicate  # noqa: E402
 
 n = 1_250_000_000
@@ -27,6 +30,12 @@ bc = b.col()
 
 def project():
     check(lib.fq_filter_project(C.byref(bc), C.byref(p38), vals, nout, outs, C.byref(kept), pws.ptr, pws.nbytes, st))
+    if ops.tune_get("SELECT_DEBUG"):  # the library keeps the counters; the tool prints them
+        h = ops.tune_select_counters()
+        t = max(h[0], 1)
+        print("[select-debug] tiles %d polls/tile %.2f windows/tile %.2f | per tile (cycles): ticket %.0f "
+              "load+pred %.0f lookback %.0f store %.0f | wg life %.1f us" %
+              (h[0], h[1] / t, h[7] / t, h[3] / t, h[4] / t, h[2] / t, h[5] / t, h[12] / 100.0), flush=True)
 
 
 project()
@@ -40,5 +49,5 @@ for _ in range(10):
     ts.append(e0.elapsed_time(e1))
 ms = statistics.median(ts)
 nb = 8 * n + nout * 8 * kept.value
-print("keep=%s WG/CU=%s nout=%d: %.3f ms, %.0f GB/s algorithmic, kept %d" % (os.environ.get("KEEP", "0.375"), os.environ.get("FQ_SELECT_WG_PER_CU", "8"), nout, ms,
+print("keep=%s WG/CU=%s nout=%d: %.3f ms, %.0f GB/s algorithmic, kept %d" % (os.environ.get("KEEP", "0.375"), os.environ.get("FQ_TUNE_SELECT_WG_PER_CU", "8"), nout, ms,
                                                                      nb / ms / 1e6, kept.value), flush=True)

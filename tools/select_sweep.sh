@@ -13,7 +13,7 @@ for v in ${VARIANTS:-0 1 2 3}; do
   for wg in ${WGS:-8}; do
     for keep in ${KEEPS:-0.375 0}; do
       echo -n "sleep=$sl variant=$v lbw=$lbw threads=$th rows=$rows " >> $OUT
-      FQ_SELECT_SLEEP=$sl FQ_SELECT_LBW=$lbw FQ_SELECT_VARIANT=$v FQ_SELECT_THREADS=$th FQ_SELECT_ROWS=$rows FQ_SELECT_WG_PER_CU=$wg KEEP=$keep timeout -k 10 120 python tools/select_probe.py >> $OUT 2>>gpurun_out/select_sweep.err || exit $?
+      FQ_TUNE_SELECT_SLEEP=$sl FQ_TUNE_SELECT_LBW=$lbw FQ_TUNE_SELECT_VARIANT=$v FQ_TUNE_SELECT_THREADS=$th FQ_TUNE_SELECT_ROWS=$rows FQ_TUNE_SELECT_WG_PER_CU=$wg KEEP=$keep timeout -k 10 120 python tools/select_probe.py >> $OUT 2>>gpurun_out/select_sweep.err || exit $?
     done
   done
  done
