@@ -205,3 +205,83 @@ def test_group_by_final_merges_flat_rows_on_the_host():
     with Engine(device=-1) as eng:
         rows = eng.execute_final(sql, ranks).rows
     assert rows == [(k,) + exp[k] for k in sorted(exp)]
+
+
+# ---- the C5 shape: 8 ranks, numbers_mt(8e10), one partition per rank --------
+
+def closed_form_states(parts):
+    """Per-rank partial states of SQL's four functions over `parts`, in closed
+    form (a rank's NumbersStream rows are contiguous from each partition's
+    begin, numbers.stream_rows); Null states when the rank owns nothing (no
+    merge_state ever reached them, function_aggregator.rs:24-36)."""
+    import fq_ref as R
+    if not parts:
+        return [[R.Value("Null", None)] * 2, [R.Value("Null", None)], [R.Value("Null", None)],
+                [R.Value("Null", None)]]
+    from fq_amd.numbers import stream_rows
+    s = c = 0
+    mx, mn = 0, None
+    for _, b, e in parts:
+        rows = stream_rows(b, e)
+        s += rows * (2 * b + rows - 1) // 2
+        c += rows
+        mx = max(mx, b + rows - 1)
+        mn = b if mn is None else min(mn, b)
+    u = lambda x: R.Value("UInt64", x % 2**64)  # noqa: E731
+    return [[u(s), u(c)], [u(mx)], [u(mn)], [u(c)]]
+
+
+def c5_worker(rank, world, port, n, out_q):
+    for p in (os.path.join(ROOT, "fuse-query_amd"), os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")):
+        sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+
+    from fq_amd import dist as fqd
+    from fq_amd.engine import Engine
+    from fq_amd.numbers import generate_parts, shard
+    from test_engine_cpu import encode_states
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        mine = shard(generate_parts(n), rank, world)
+        everyone = fqd.allgather_states(encode_states(closed_form_states(mine)))
+        with Engine(device=-1) as eng:
+            rows = eng.execute_final(SQL % n, everyone).rows
+        out_q.put((rank, [name for name, _, _ in mine], rows))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n", [80_000_000_000, 7])
+def test_world8_c5_shards_exchange_and_final(n):
+    """BASELINE configs[4] at world 8 over gloo: numbers_table.rs:29-55 names
+    8 partitions and rank r owns exactly partition r; at N=7 there is one
+    partition "7-0-6" and only rank 7 owns it (shard [8r/G, 8(r+1)/G)), the
+    other 7 ranks ship Null states.  Every rank's AggregateFinal over the
+    exchanged states equals the closed form (processor_merge.rs:45-63 merges
+    the partial streams in any order; the state merge is order-free)."""
+    from fq_amd.numbers import generate_parts
+    world = 8
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=c5_worker, args=(r, world, port, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = sorted(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    names = [nm for nm, _, _ in generate_parts(n)]
+    if n == 7:
+        assert names == ["7-0-6"]
+        assert [owned for _, owned, _ in results] == [[]] * 7 + [["7-0-6"]]
+    else:
+        assert [owned for _, owned, _ in results] == [[names[r]] for r in range(8)]
+        assert names[7] == "80000000000-70000000000-79999999999"
+    s = n * (n - 1) // 2 % 2**64
+    exp = [(s // n, n - 1, 0, n)]
+    for rank, _, rows in results:
+        assert rows == exp, (rank, rows, exp)

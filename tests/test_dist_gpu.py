@@ -167,3 +167,33 @@ def test_native_rccl_comm_single_rank():
     assert dev_ok
     for dist_rows, local_rows in out:
         assert dist_rows == local_rows
+
+
+def test_world8_bench_rehearsal_on_one_gpu():
+    """bench.py's world > 1 path at the C5 shape: 8 ranks (torch.distributed.run,
+    gloo) share the box's one GPU, numbers_mt(1e10) split into one 10 GB
+    partition per rank (80 GB resident in total), the partial states exchanged
+    through the native protocol, every rank's final checked against the closed
+    form inside bench.py (it exits non-zero on a mismatch).  The driver's 8-GPU
+    run differs only in the transport (RCCL) and one GPU per rank."""
+    import json
+    import subprocess
+    n = 10_000_000_000
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", "8", "--rows-total", str(n), "--dist-backend", "gloo",
+           "--steps", "2", "--warmup", "1", "--no-cpu-baseline"]
+    env = dict(os.environ, OMP_NUM_THREADS="2")
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=280, env=env, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    out = json.loads(lines[0])
+    if os.path.isdir(os.path.join(ROOT, "gpurun_out")):  # evidence for profiles/
+        with open(os.path.join(ROOT, "gpurun_out", "world8_rehearsal.json"), "w") as fh:
+            fh.write(lines[0] + "\n")
+    assert out["n_gpus"] == 8 and out["scaling"] == "strong"
+    assert out["config"]["rows_total"] == n and out["config"]["partitions_per_gpu"] == 1
+    s = n * (n - 1) // 2 % 2**64
+    assert out["result"] == [s // n, n - 1, 0]
+    assert "== closed form" in p.stderr
