@@ -342,6 +342,29 @@ class BlockCache {
         cached_ += bytes;
         return true;
     }
+    // The queue's one kept workspace (the partitioned GROUP BY's ~4 GB, above
+    // kMaxBlock and the queue cap): the next query's launches on the queue take
+    // it back instead of mapping it afresh (hipMallocAsync of GBs: up to 540 ms)
+    void *take_workspace(hipStream_t s, size_t min_bytes, size_t *bytes) {
+        std::lock_guard<std::mutex> lk(mu_);
+        auto f = free_.find(s);
+        if (f == free_.end() || !f->second.ws || f->second.ws_bytes < min_bytes) return nullptr;
+        void *p = f->second.ws;
+        *bytes = f->second.ws_bytes;
+        cached_ -= f->second.ws_bytes;
+        f->second.ws = nullptr;
+        f->second.ws_bytes = 0;
+        return p;
+    }
+    bool put_workspace(hipStream_t s, void *p, size_t bytes) {
+        std::lock_guard<std::mutex> lk(mu_);
+        auto f = free_.find(s);
+        if (f == free_.end() || f->second.ws) return false;
+        f->second.ws = p;
+        f->second.ws_bytes = bytes;
+        cached_ += bytes;
+        return true;
+    }
     // s is idle and about to be destroyed: free its blocks, stop caching on it
     void drop_stream(hipStream_t s) {
         std::lock_guard<std::mutex> lk(mu_);
@@ -351,16 +374,23 @@ class BlockCache {
             (void)hipFree(b.second);
             cached_ -= b.first;
         }
+        if (f->second.ws) {
+            (void)hipFree(f->second.ws);
+            cached_ -= f->second.ws_bytes;
+        }
         free_.erase(f);
     }
     // hand every cached block back to the device pool (in its queue's order)
     void flush() {
         std::lock_guard<std::mutex> lk(mu_);
         for (auto &f : free_) {
-            if (f.second.blocks.empty()) continue;
+            if (f.second.blocks.empty() && !f.second.ws) continue;
             for (auto &b : f.second.blocks) (void)hipFreeAsync(b.second, f.first);
+            if (f.second.ws) (void)hipFreeAsync(f.second.ws, f.first);
             f.second.blocks.clear();
             f.second.bytes = 0;
+            f.second.ws = nullptr;
+            f.second.ws_bytes = 0;
             (void)hipStreamSynchronize(f.first);
         }
         cached_ = 0;
@@ -374,6 +404,8 @@ class BlockCache {
     struct Queue {
         std::multimap<size_t, void *> blocks;
         size_t bytes = 0;
+        void *ws = nullptr;  // take_workspace / put_workspace
+        size_t ws_bytes = 0;
     };
     std::mutex mu_;
     std::unordered_map<hipStream_t, Queue> free_;
@@ -572,7 +604,9 @@ DeviceBuffer::~DeviceBuffer() {
         if (ev && hipEventRecord(ev, c->stream()) == hipSuccess) (void)hipStreamWaitEvent(stream, ev, 0);
         (void)hipGetLastError();
     }
-    if (!BlockCache::get().put(stream, ptr, bytes)) (void)hipFreeAsync(ptr, stream);
+    const bool kept = workspace ? BlockCache::get().put_workspace(stream, ptr, bytes)
+                                : BlockCache::get().put(stream, ptr, bytes);
+    if (!kept) (void)hipFreeAsync(ptr, stream);
 }
 
 static void require_device() {
@@ -592,6 +626,25 @@ std::shared_ptr<DeviceBuffer> DeviceBuffer::alloc(size_t bytes, hipStream_t st) 
         b->ptr = nullptr;
         b->async = false;
         check_hip(alloc_with_reclaim([&] { return hipMalloc(&b->ptr, b->bytes); }), "hipMalloc");
+    }
+    return b;
+}
+
+std::shared_ptr<DeviceBuffer> DeviceBuffer::alloc_workspace(size_t bytes, hipStream_t st) {
+    require_device();
+    auto b = std::make_shared<DeviceBuffer>();
+    b->stream = st;
+    b->workspace = true;
+    size_t got = 0;
+    if ((b->ptr = BlockCache::get().take_workspace(st, bytes, &got))) {
+        b->bytes = got;
+        return b;
+    }
+    b->bytes = size_class(bytes);
+    if (alloc_with_reclaim([&] { return hipMallocAsync(&b->ptr, b->bytes, st); }) != hipSuccess) {
+        b->ptr = nullptr;
+        b->async = false;
+        check_hip(alloc_with_reclaim([&] { return hipMalloc(&b->ptr, b->bytes); }), "hipMalloc(workspace)");
     }
     return b;
 }

@@ -224,12 +224,17 @@ struct DeviceBuffer {
     size_t bytes = 0;
     hipStream_t stream = nullptr;
     bool async = true;
+    bool workspace = false;  // alloc_workspace: kept per queue across queries
     DeviceBuffer() = default;
     DeviceBuffer(const DeviceBuffer &) = delete;
     DeviceBuffer &operator=(const DeviceBuffer &) = delete;
     ~DeviceBuffer();
     static std::shared_ptr<DeviceBuffer> alloc(size_t bytes, hipStream_t st);
     static std::shared_ptr<DeviceBuffer> alloc_sync(size_t bytes);  // long-lived tables
+    // A large per-launch workspace: the block cache keeps ONE per queue across
+    // queries (outside its block caps; flushed by reclaim_device_memory), so
+    // the next query on the queue reuses it (>= bytes; ->bytes is its size)
+    static std::shared_ptr<DeviceBuffer> alloc_workspace(size_t bytes, hipStream_t st);
 };
 
 // Allocation size class: 256 B minimum, then 4 classes per power of two.

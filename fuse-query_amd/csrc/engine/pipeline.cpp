@@ -699,10 +699,11 @@ StreamRef GroupByPartialTransform::execute() {
         const int lp = shared_->log2_parts;
         // radix-partitioned launches go over the block in chunks of
         // FQ_OPT_GROUP_CHUNK_ROWS rows (a multiple of 64: bitmap predicates
-        // are offset by whole words): the partition workspace (~8 B per row)
-        // stays under 1 GB, which the device block cache keeps for the next
-        // query on this queue (a 10 GB one was mapped afresh per query:
-        // hipMallocAsync up to 540 ms, tools/batch_r02c.sh)
+        // are offset by whole words): the partition workspace (~8.6 B per row,
+        // ~4.3 GB at the default 5e8) is the queue's kept workspace in the
+        // device block cache (DeviceBuffer::alloc_workspace), so the next
+        // query on this queue reuses it (mapping GBs afresh per query cost up
+        // to 540 ms of hipMallocAsync)
         // (split evenly, no short tail chunk: a 1.25e9-row partition as 3 x
         // 4.17e8 ran 5.32 ms per 10 GB, as 5e8 + 5e8 + 2.5e8 5.72-5.76 on
         // another box -- profiles/r02_s4_g2_chunks.txt)
@@ -718,7 +719,7 @@ StreamRef GroupByPartialTransform::execute() {
             const size_t need = fq_group_partition_workspace_bytes(chunk, lp);
             std::lock_guard<std::mutex> lk(shared_->mu);
             auto &slot = shared_->part_ws[ctx.stream()];
-            if (!slot || slot->bytes < need) slot = DeviceBuffer::alloc(need, ctx.stream());
+            if (!slot || slot->bytes < need) slot = DeviceBuffer::alloc_workspace(need, ctx.stream());
             ws = slot;
         }
         {
@@ -1111,7 +1112,8 @@ GroupRows decode_group_rows(const uint8_t *p, size_t n) {
     memcpy(&rows, p + 8, 8);
     memcpy(kd, p + 16, 8);
     const size_t hdr = 24 + ((size_t)nl * 4 + 7) / 8 * 8;
-    if (nl > FQ_MAX_GROUP_AGGS || hdr + rows * 8 * (1 + (size_t)nl) > n)
+    // by division: `rows` comes off the wire and a product could wrap
+    if (nl > FQ_MAX_GROUP_AGGS || hdr > n || rows > (n - hdr) / (8 * (1 + (uint64_t)nl)))
         throw_status(FQ_E_INVALID, "GROUP BY partial rows: truncated");
     GroupRows g;
     g.key_dtype = kd[0];

@@ -215,7 +215,9 @@ __global__ void __launch_bounds__(256) group_merge_kernel(MergeArgs a) {
             atomicOr(&a.hdr[1], 1u);
             slot = a.cap;
         } else {
-            uint64_t h = merge_mix(k) & mask;
+            // the home slot ginsert (fq_jit.hip) uses -- the top log2(cap) bits of
+            // the mixer -- so merged rows meet the keys aggregated into the same table
+            uint64_t h = mask ? merge_mix(k) >> __clzll(mask) : 0;
             for (int64_t p = 0; p < a.cap; ++p) {
                 const uint64_t cur = __hip_atomic_load(&a.keys[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (cur == k) {
@@ -295,7 +297,7 @@ __global__ void __launch_bounds__(kBlkThreads)
 __global__ void __launch_bounds__(kBlkThreads)
     group_blk_scatter_kernel(const uint32_t *__restrict__ used, const uint32_t *__restrict__ blk_bin,
                              const uint32_t *__restrict__ blk_fill, uint32_t *__restrict__ cursor,
-                             uint64_t *__restrict__ order, uint32_t q, uint32_t slots) {
+                             uint64_t *__restrict__ order, uint32_t q, uint32_t slots, uint32_t P) {
     __shared__ uint32_t s_cnt[256], s_base[256];
     const uint32_t first = blockIdx.x * (uint32_t)(kBlkThreads * kBlkPerThread);
     s_cnt[threadIdx.x] = 0;
@@ -307,6 +309,8 @@ __global__ void __launch_bounds__(kBlkThreads)
         const uint32_t i = first + k * kBlkThreads + threadIdx.x;
         ok[k] = i < slots && i - (i / q) * q < used[i / q];
         bin[k] = ok[k] ? blk_bin[i] : 0u;
+        ok[k] = ok[k] && bin[k] < P;  // never index s_cnt with a block the partition kernel did not write
+        if (!ok[k]) bin[k] = 0u;
         rank[k] = ok[k] ? atomicAdd(&s_cnt[bin[k]], 1u) : 0u;
     }
     __syncthreads();
@@ -328,7 +332,7 @@ fq_status launch_group_part_blocks(const GroupPartition &X, hipStream_t stream) 
     const uint32_t per = kBlkThreads * kBlkPerThread, slots = (uint32_t)X.grid * X.q;
     const uint32_t grid = (slots + per - 1) / per;
     hipLaunchKernelGGL(group_blk_scatter_kernel, dim3(grid > 0 ? grid : 1), dim3(kBlkThreads), 0, stream, X.used,
-                       X.blk_bin, X.blk_fill, X.cursor, X.order, X.q, slots);
+                       X.blk_bin, X.blk_fill, X.cursor, X.order, X.q, slots, (uint32_t)P);
     FQ_HIP_TRY(hipGetLastError());
     return FQ_OK;
 }

@@ -285,3 +285,23 @@ def test_world8_c5_shards_exchange_and_final(n):
     exp = [(s // n, n - 1, 0, n)]
     for rank, _, rows in results:
         assert rows == exp, (rank, rows, exp)
+
+
+def test_group_rows_with_a_wrapping_row_count_are_rejected():
+    # a row count whose byte size wraps 64 bits must not pass the length check
+    # (pipeline.cpp decode_group_rows; the buffer crosses fq_engine_execute_final)
+    import struct
+
+    sys.path.insert(0, os.path.join(ROOT, "fuse-query_amd"))
+    from fq_amd import abi
+    from fq_amd._lib import FQError
+    from fq_amd.engine import Engine
+
+    nl = 3
+    rows = (1 << 61) + 1  # 8 * (1 + nl) * rows = 2^66 + 32: wraps to 32
+    bad = b"FQG1" + struct.pack("<IQii", nl, rows, abi.DT_UINT64, 0)
+    bad += struct.pack("<3i", abi.DT_UINT64, abi.DT_UINT64, abi.DT_UINT64) + b"\0" * 4 + b"\0" * 64
+    sql = "SELECT number%97, count(number), sum(number), max(number) FROM system.numbers_mt(1000) GROUP BY number%97"
+    with Engine(device=-1) as eng:
+        with pytest.raises(FQError, match="truncated"):
+            eng.execute_final(sql, [bad])

@@ -598,6 +598,32 @@ def test_table_merge_folds_exchanged_rows():
         tiny.count()
 
 
+@pytest.mark.parametrize("log2p", [0, 4])
+def test_aggregate_merge_aggregate_into_one_table(log2p):
+    # fq_group_aggregate(_partitioned) and fq_group_table_merge into the SAME
+    # table, in both orders: every key must reach its one slot (both inserts
+    # start probing at the same home slot), so keys stay unique and the states
+    # fold across the writers
+    rng = np.random.default_rng(23)
+    aggs = [(abi.AGG_COUNT, U), (abi.AGG_SUM, U), (abi.AGG_MAX, U)]
+    key, _ = chain(U, [("%", 3000)])
+    xs = [rng.integers(0, 1 << 62, 300_000, dtype=np.uint64) for _ in range(3)]
+    src = ops.GroupTable(1 << 13, aggs)
+    src.aggregate(ops.from_numpy(xs[1]), key=key, values=[None, None, None])
+    mk, ms = src.extract()
+    t = ops.GroupTable(1 << 13, aggs)
+    t.aggregate(ops.from_numpy(xs[0]), key=key, values=[None, None, None], log2_parts=log2p)
+    t.merge(mk, ms)
+    t.aggregate(ops.from_numpy(xs[2]), key=key, values=[None, None, None], log2_parts=log2p)
+    t.merge(mk, ms)  # and the merged rows once more, after the second aggregate
+    keys, states = t.extract()
+    assert len(np.unique(keys)) == len(keys) == 3000
+    got = {int(k): [s[i] for s in decode(states, [d for _, d in aggs])] for i, k in enumerate(keys)}
+    allx = np.concatenate([xs[0], xs[1], xs[2], xs[1]])
+    exp = np_groupby(allx % np.uint64(3000), [None, allx, allx], [a for a, _ in aggs])
+    compare(got, exp, [a for a, _ in aggs], [d for _, d in aggs])
+
+
 def test_table_merge_sentinel_key_and_empty_input():
     # the all-ones key (the table's EMPTY marker) has its own slot
     aggs = [(abi.AGG_COUNT, U), (abi.AGG_MAX, U)]
