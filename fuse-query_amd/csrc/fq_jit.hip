@@ -1944,15 +1944,17 @@ fq_jit_pbits(const TIn *__restrict__ col, long long n, Consts c, u64 *__restrict
 //
 // Tickets: one device-scope counter serves ~90 atomics per us (round-1
 // measurement), >= 1.7 ms for the 152,588 tiles of a 10 GB column.  With
-// PS_XCD each XCD draws from its own counter (its own 128-B line; the XCD is
-// the hardware register XCC_ID modulo PS_NXCD = CUs / 32): counter x hands
-// out tiles x, x + N, x + 2N, ...  A workgroup whose counter is exhausted
-// draws from the next XCD's, so every tile is drawn whatever the placement
-// of workgroups on XCDs.  Progress: the lowest unfinished tile is either
-// held by a workgroup -- all its predecessors are done, its look-back
-// completes -- or undrawn, and the next workgroup to finish a tile draws it
-// (counters only grow; a workgroup leaves only when every counter is
-// exhausted).
+// PS_XCD the workgroups fall into X.ncls classes by blockIdx (blocks are dealt
+// round-robin over the XCDs, so a class is in practice one XCD's workgroups;
+// ncls <= the grid, and the host sizes the grid to the resident capacity):
+// counter x hands out tiles x, x + ncls, ...  A workgroup whose counter is
+// exhausted draws from the next class's, and leaves only when every counter
+// is exhausted.  Progress: the lowest drawn-but-unfinished tile m needs every
+// tile below it drawn; a class whose counter is below m has resident
+// workgroups, none holding a tile below m (else m is not lowest), so they are
+// drawing and the class advances.  (Classes read from the hardware XCC_ID, as
+// in round 2, could leave a class with no resident workgroup: its tiles would
+// never be drawn and every look-back past them would hit the poll bound.)
 // Status words are 64-bit agent-scope atomics: flag in the top 2 bits, count
 // below.  The look-back is bounded: after ~2^20 polls the kernel flags an
 // error (fl[1] bit 31) and moves on, so a wave can never spin forever.
@@ -2021,16 +2023,15 @@ struct PsCtx {
     const u64 *__restrict__ bm;
     u64 *__restrict__ status;
     u32 *__restrict__ ticket;
-    u32 cls;
+    u32 cls, ncls;
 };
 // the next tile for this workgroup (thread 0 only); >= ntiles when none is
-// left.  An exhausted class moves on to the other XCDs' counters, so no tile
-// depends on the hardware placing a workgroup on every XCD.
+// left.  An exhausted class moves on to the other classes' counters.
 __device__ __forceinline__ long long ps_ticket(const PsCtx &X) {
 #if PS_XCD
-    for (u32 i = 0; i < (u32)PS_NXCD; ++i) {
-        const u32 cl = (X.cls + i) % (u32)PS_NXCD;
-        const long long t = (long long)atomicAdd(X.ticket + 32 * cl, 1u) * PS_NXCD + cl;
+    for (u32 i = 0; i < X.ncls; ++i) {
+        const u32 cl = (X.cls + i) % X.ncls;
+        const long long t = (long long)atomicAdd(X.ticket + 32 * cl, 1u) * X.ncls + cl;
         if (t < X.ntiles) return t;
     }
     return X.ntiles;
@@ -2216,13 +2217,10 @@ fq_jit_pselect(const TIn *__restrict__ col, long long n, Consts c, const u64 *__
     X.bm = bm;
     X.status = status;
     X.ticket = ticket;
-    X.cls = 0;
+    X.ncls = gridDim.x < (unsigned)PS_NXCD ? gridDim.x : (unsigned)PS_NXCD;
+    X.cls = blockIdx.x % X.ncls;
 #if PS_DEBUG
     for (int i = 0; i < 8; ++i) X.dbg[i] = 0;
-#endif
-#if PS_XCD
-    // s_getreg_b32 hwreg(HW_REG_XCC_ID = 20, offset 0, 4 bits)
-    X.cls = ((u32)__builtin_amdgcn_s_getreg((3 << 11) | 20) & 15u) % (u32)PS_NXCD;
 #endif
     u32 pflags = 0, vflags = 0;
     PS_T(k0);
@@ -2667,8 +2665,27 @@ fq_status jit_project_select(int32_t col_dtype, const ProjLaunch &P, const uint6
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     (void)hipGetLastError();
-    const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(ntiles, (int64_t)cus * wg_per_cu));
-    FQ_HIP_TRY(hipModuleLaunchKernel(k.scatter, (unsigned)grid, 1, 1, (unsigned)select_threads(), 1, 1, 0, P.stream,
+    // every workgroup resident (the ticket classes' progress argument needs it):
+    // at most the occupancy the compiled kernel allows per CU
+    hipFunction_t fn = k.scatter;
+    const int threads = select_threads();
+    static std::mutex occ_mu;
+    static std::unordered_map<hipFunction_t, int> occ_cache;
+    int occ = 0;
+    {
+        std::lock_guard<std::mutex> lk(occ_mu);
+        auto it = occ_cache.find(fn);
+        if (it != occ_cache.end()) {
+            occ = it->second;
+        } else {
+            if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, threads, 0) != hipSuccess) occ = 1;
+            (void)hipGetLastError();
+            occ = std::max(1, occ);
+            occ_cache.emplace(fn, occ);
+        }
+    }
+    const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(ntiles, (int64_t)cus * std::min(wg_per_cu, occ)));
+    FQ_HIP_TRY(hipModuleLaunchKernel(fn, (unsigned)grid, 1, 1, (unsigned)threads, 1, 1, 0, P.stream,
                                      args, nullptr));
     g_jit_launches += 1;
     if (select_debug() && k.mod) {  // tuning only: keep and clear the kernel's phase counters

@@ -11,3 +11,12 @@ for p in (ROOT, os.path.join(ROOT, "fuse-query_amd"), os.path.join(ROOT, "oracle
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (run with -m gpu)")
+
+
+def pytest_sessionstart(session):
+    # sweeps re-run the GPU suites under a launch-shape knob (FQ_TUNE_<KNOB>=v,
+    # tools/knobs.py); the library itself reads no environment for them
+    if any(k.startswith("FQ_TUNE_") for k in os.environ):
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        import knobs
+        knobs.apply_env()
