@@ -134,12 +134,13 @@ def latest_pmc_traffic(kernel_substr, query, rows_per_launch):
     *pmc_<query>[_.]*.json, tools/pmc_summary.py, gfx950 FETCH_SIZE x2
     correction applied).  The summary must have been measured on the current
     kernel sources (its kernel_sources_sha256): otherwise traffic is None and
-    the provenance says the file is stale."""
+    the provenance says the file is stale.  The fingerprint covers the
+    query's own kernel sources (tools/srchash.py QUERY_SOURCES)."""
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_%s.json" % query)) +
                    glob.glob(os.path.join(ROOT, "profiles", "*pmc_%s_*.json" % query)),
                    key=os.path.basename)
     subs = [kernel_substr] if isinstance(kernel_substr, str) else list(kernel_substr)
-    cur = kernel_sources_sha256()
+    cur = kernel_sources_sha256(query)
     for f in reversed(files):
         try:
             d = json.load(open(f))
@@ -150,8 +151,8 @@ def latest_pmc_traffic(kernel_substr, query, rows_per_launch):
         if not ks:
             continue
         src = {"file": "profiles/" + os.path.basename(f), "measured_at_commit": d.get("measured_at_commit"),
-               "kernel_sources_sha256": d.get("kernel_sources_sha256")}
-        if d.get("kernel_sources_sha256") != cur:
+               "query_sources_sha256": d.get("query_sources_sha256")}
+        if d.get("query_sources_sha256") != cur:
             src["status"] = "stale: kernel sources changed since this PMC pass (current %s)" % cur[:12]
             return None, src
         src["status"] = "current kernel sources"

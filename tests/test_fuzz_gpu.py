@@ -123,7 +123,7 @@ def jit(request):
     ops.jit_config(abi.JIT_AUTO, 1 << 22)
 
 
-@pytest.mark.parametrize("seed", range(150))
+@pytest.mark.parametrize("seed", range(64))
 def test_random_aggregate_query(seed, jit):
     rng = random.Random(1000 + seed + (100000 if jit == "always" else 0))
     n = rng.choice(N_CHOICES)
@@ -145,7 +145,7 @@ def test_random_aggregate_query(seed, jit):
     assert len(got) == 1 and all(same(g, x) for g, x in zip(got[0], exp)), (sql, got, exp)
 
 
-@pytest.mark.parametrize("seed", range(100))
+@pytest.mark.parametrize("seed", range(48))
 def test_random_projection_query(seed):
     rng = random.Random(5000 + seed)
     n = rng.choice([1000, 100001])
@@ -173,7 +173,7 @@ def gen_int_expr(rng, depth):
     return "number", R.E_field("number")
 
 
-@pytest.mark.parametrize("seed", range(40))
+@pytest.mark.parametrize("seed", range(20))
 def test_random_group_by_query(seed):
     # GROUP BY has no reference transform: fq_ref.group_by_query states the
     # device path's semantics with the reference's Function machinery

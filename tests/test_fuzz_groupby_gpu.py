@@ -50,7 +50,7 @@ def gen_key(rng):
             "modmul": [("%", min(m, 5000)), ("*", a)]}[shape]
 
 
-@pytest.mark.parametrize("seed", range(40))
+@pytest.mark.parametrize("seed", range(16))
 def test_random_group_by_at_scale_matches_c_oracle(seed):
     import oracle_c
     from fq_amd import abi

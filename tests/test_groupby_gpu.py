@@ -25,29 +25,33 @@ def setup_module():
     ops = _ops
 
 
-def np_groupby(keys, vals_list, kinds):
-    """-> {key: [state per aggregate]} with the device's state semantics."""
+def np_groupby_arrays(keys, vals_list, kinds):
+    """-> (sorted distinct keys, [state array per aggregate]) with the device's
+    state semantics (wrapping integer sums, f64 sums in sorted-key order)."""
     order = np.argsort(keys, kind="stable")
     k = keys[order]
     uniq, start = np.unique(k, return_index=True)
-    out = {}
-    bounds = list(start) + [len(k)]
-    for gi, key in enumerate(uniq):
-        sl = order[bounds[gi]:bounds[gi + 1]]
-        st = []
-        for kind, vals in zip(kinds, vals_list):
-            if kind == abi.AGG_COUNT:
-                st.append(len(sl))
-                continue
-            v = vals[sl]
-            if kind == abi.AGG_SUM:
-                st.append(v.sum(dtype=v.dtype) if v.dtype != np.float64 else float(np.sum(v)))
-            elif kind == abi.AGG_MAX:
-                st.append(v.max())
-            else:
-                st.append(v.min())
-        out[int(key)] = st
-    return out
+    counts = np.diff(np.append(start, len(k)))
+    out = []
+    for kind, vals in zip(kinds, vals_list):
+        if kind == abi.AGG_COUNT:
+            out.append(counts.astype(np.uint64))
+            continue
+        v = vals[order]
+        if kind == abi.AGG_SUM:
+            out.append(np.add.reduceat(v, start) if v.dtype != np.float64 else np.add.reduceat(v, start))
+        elif kind == abi.AGG_MAX:
+            out.append(np.maximum.reduceat(v, start))
+        else:
+            out.append(np.minimum.reduceat(v, start))
+    return uniq, out
+
+
+def np_groupby(keys, vals_list, kinds):
+    """-> {key: [state per aggregate]} with the device's state semantics."""
+    uniq, st = np_groupby_arrays(keys, vals_list, kinds)
+    cols = [a.tolist() for a in st]
+    return {int(key): [c[i] for c in cols] for i, key in enumerate(uniq.tolist())}
 
 
 def decode(states, dts):
@@ -373,6 +377,17 @@ def run_parts(col, aggs, log2p, key=None, values=None, pred=None, key_dtype=U, c
     return {int(k): [st[a][i] for a in range(len(aggs))] for i, k in enumerate(keys)}
 
 
+def run_parts_arrays(col, aggs, log2p, key=None, values=None, capacity=1 << 12, blocks=1):
+    """-> (keys ascending, [decoded state array per aggregate]) of the table."""
+    t = ops.GroupTable(capacity, aggs, U)
+    for _ in range(blocks):
+        t.aggregate(col, None, key, values, log2_parts=log2p)
+    keys, states = t.extract()
+    st = decode(states, [dt for _, dt in aggs])
+    o = np.argsort(keys, kind="stable")
+    return keys[o], [a[o] for a in st]
+
+
 @pytest.mark.parametrize("mod,log2p", [(7, 1), (1000, 3), (65_536, 6), (100_000, 6), (2_000_000, 8), (None, 8)])
 def test_partitioned_matches_numpy(mod, log2p):
     # 2 blocks into one table: rows of both, every group once, all aggregate kinds;
@@ -385,13 +400,17 @@ def test_partitioned_matches_numpy(mod, log2p):
     vf, _ = chain(U, [("*", 0.25)])
     aggs = [(abi.AGG_COUNT, U), (abi.AGG_SUM, U), (abi.AGG_MAX, U), (abi.AGG_MIN, U), (abi.AGG_SUM, F)]
     groups = min(n, mod or n)
-    got = run_parts(col, aggs, log2p, key=key, values=[None, None, None, None, vf], capacity=4 * groups, blocks=2)
+    gk, gs = run_parts_arrays(col, aggs, log2p, key=key, values=[None, None, None, None, vf], capacity=4 * groups,
+                              blocks=2)
     xx = np.concatenate([x, x])
     k = xx % np.uint64(mod) if mod else xx
     xf = xx.astype(np.float64) * 0.25
-    exp = np_groupby(k, [None, xx, xx, xx, xf], [a for a, _ in aggs])
-    bound = {g: 1e-12 * abs(e[4]) * 4 + 1e-9 for g, e in exp.items()}
-    compare(got, exp, [a for a, _ in aggs], [d for _, d in aggs], bound)
+    ek, es = np_groupby_arrays(k, [None, xx, xx, xx, xf], [a for a, _ in aggs])
+    assert np.array_equal(gk, ek), (len(gk), len(ek))
+    for a in range(4):  # integer states bit for bit
+        assert np.array_equal(gs[a], es[a]), a
+    # f64 sums: atomic add order is unspecified -- 1e-12 relative per group
+    assert np.all(np.abs(gs[4] - es[4]) <= 4e-12 * np.abs(es[4]) + 1e-9)
 
 
 @pytest.mark.parametrize("steps,pred", [
