@@ -233,6 +233,7 @@ fq_status fq_engine_materialize_numbers(fq_engine *e, uint64_t total, int32_t ra
             c.len = (int64_t)rows;
             c.dev = fq::DeviceBuffer::alloc_sync(rows * 8);
             fq::check_fq(fq_fill_numbers_u64((uint64_t *)c.dptr(), b, rows, ctx.stream()));
+            c.iota = true;
             ctx.sync();
             e->ds->numbers()->pin(parts[i].name, c);
         }

@@ -282,6 +282,8 @@ struct Column {
     // (GROUP BY results: 100,000 groups x 4 columns as DataValues cost ~15 ms
     // to build, copy and free); to_host() expands them
     std::shared_ptr<std::vector<uint64_t>> flat;
+    // consecutive integers v[0], v[0] + 1, ... (a numbers_mt block; slices keep it)
+    bool iota = false;
 
     bool on_device() const { return (bool)dev; }
     void *dptr() const { return dev ? (char *)dev->ptr + offset : nullptr; }

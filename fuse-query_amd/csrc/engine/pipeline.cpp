@@ -128,6 +128,7 @@ class NumbersStream : public BlockStream {
             ExecCtx &ctx = ExecCtx::current();
             col = Column::device(FQ_DT_UINT64, (int64_t)n, ctx.stream());
             check_fq(fq_fill_numbers_u64((uint64_t *)col.dptr(), begin_ + off_, n, ctx.stream()));
+            col.iota = true;
         }
         off_ += n;
         morsel_ = std::min(morsel_ * 2, NumbersTable::kMorselMax);
@@ -733,8 +734,10 @@ StreamRef GroupByPartialTransform::execute() {
                     cc.data = (char *)c.data + off * 8;
                     cc.len = std::min(chunk, c.len - off);
                     if (has_pred && pc.kind == FQ_PRED_BITMAP) pc.bitmap = fp.get()->bitmap + off / 64;
+                    // a numbers_mt chunk's values lie within 2^31 of its first: 4-byte partition rows
+                    const int32_t lpf = lp | (col.iota && cc.len <= ((int64_t)1 << 31) ? FQ_GROUP_NARROW_ROWS : 0);
                     check_fq(fq_group_aggregate_partitioned(&shared_->desc, &cc, has_pred ? &pc : nullptr,
-                                                            kc.expr.n_steps ? &kc.expr : nullptr, vals, lp, ws->ptr,
+                                                            kc.expr.n_steps ? &kc.expr : nullptr, vals, lpf, ws->ptr,
                                                             ws->bytes, ctx.stream()));
                 }
             } else

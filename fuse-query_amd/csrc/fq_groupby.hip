@@ -31,6 +31,7 @@ namespace fqk {
 constexpr uint64_t kEmpty = ~0ull;
 constexpr uint32_t kFull = 256u;
 constexpr uint32_t kPartOverflow = 512u;  // fq_jit_gpart: more blocks than the workspace bound (never expected)
+constexpr uint32_t kNarrowOverflow = 1024u;  // fq_jit_gpart: a value outside col[0] +- 2^31 (FQ_GROUP_NARROW_ROWS)
 constexpr size_t kHdrBytes = 64;
 
 struct TableView {
@@ -257,6 +258,8 @@ static fq_status read_header(const TableView &v, uint32_t &flags, uint64_t &coun
     count = h[1];
     if (flags & kFull) return fqc::fail(FQ_E_TABLE_FULL, "GROUP BY hash table is full");
     if (flags & kPartOverflow) return fqc::fail(FQ_E_INTERNAL, "GROUP BY partition workspace overflow");
+    if (flags & kNarrowOverflow)
+        return fqc::fail(FQ_E_INVALID, "GROUP BY narrow rows: a value outside col[0] +- 2^31 (FQ_GROUP_NARROW_ROWS)");
     if (flags & FQ_STATE_DIV_ZERO) return fqc::fail(FQ_E_DIVIDE_BY_ZERO, "Internal Error: Divide by zero error");
     if (flags & FQ_STATE_CAST_NULL)
         return fqc::fail(FQ_E_UNSUPPORTED, "cast produced nulls (nulls are not supported on the device path)");
@@ -505,6 +508,7 @@ int64_t fq_group_dense_keys(int32_t col_dtype, const fq_expr *key_expr, int32_t 
 }
 
 size_t fq_group_partition_workspace_bytes(int64_t len, int32_t log2_parts) {
+    log2_parts &= ~FQ_GROUP_NARROW_ROWS;
     if (log2_parts < 1 || log2_parts > 8) return 0;
     return fqk::part_ws_bytes(len, log2_parts, nullptr, nullptr);
 }
@@ -513,11 +517,15 @@ fq_status fq_group_aggregate_partitioned(const fq_group_table *t, const fq_col *
                                          const fq_expr *key_expr, const fq_expr *values, int32_t log2_parts,
                                          void *d_ws, size_t ws_bytes, void *stream) {
     using namespace fqk;
+    const bool narrow = (log2_parts & FQ_GROUP_NARROW_ROWS) != 0;
+    log2_parts &= ~FQ_GROUP_NARROW_ROWS;
     if (log2_parts < 1 || log2_parts > 8)
         return fqc::fail(FQ_E_INVALID, "fq_group_aggregate_partitioned: log2_parts must be in [1, 8]");
     GroupLaunch G;
     fq_status s = prepare_group(t, col, pred, key_expr, values, stream, G);
     if (s != FQ_OK) return s;
+    // 4-byte rows for 8-byte integer columns the caller vouches for
+    G.narrow = narrow && (col->dtype == FQ_DT_UINT64 || col->dtype == FQ_DT_INT64) ? 1 : 0;
     if (G.n > 0 && (!d_ws || ws_bytes < part_ws_bytes(G.n, log2_parts, nullptr, nullptr)))
         return fqc::fail(FQ_E_INVALID, "fq_group_aggregate_partitioned: workspace too small");
     if (((uintptr_t)d_ws) & 255u) return fqc::fail(FQ_E_INVALID, "fq_group_aggregate_partitioned: workspace not 256-B aligned");

@@ -793,6 +793,7 @@ std::string group_shape_key(const GroupLaunch &G, int32_t tin, int dev) {
     put(G.threads);
     put(G.rowmap);
     put(G.range_bins);
+    put(G.narrow);
     put(G.n_aggs);
     for (int a = 0; a < G.n_aggs; ++a) {
         put(G.kinds[a]);
@@ -841,8 +842,27 @@ std::string state_update(int32_t kind, int32_t dt, const std::string &P, const s
 // HBM bytes per passing row: 8 (read) + 8 (blocks written) + 8 (blocks read)
 // = 24 B (8 B for a filtered-out one), against 8 B + 3 random atomics; the
 // histogram pass this replaces read the column once more (32 B per row).
+// With GP_NARROW (FQ_GROUP_NARROW_ROWS: the caller vouches that every value
+// lies within 2^31 of col[0], as a numbers_mt block's do) the blocks hold
+// 4-byte offsets from col[0] - 2^31: 8 + 4 + 4 = 16 B per passing row; a
+// value outside the range sets flag 1024 and the launch reports it.
 const char *kGroupPartitionKernels = R"(
 #define GP_ROWS 8
+#if GP_NARROW
+typedef u32 PRow;  // a kept row in the blocks: its offset from col[0] - 2^31
+__device__ __forceinline__ u64 gp_vbase(const TIn *__restrict__ col) { return (u64)col[0] - 0x80000000ull; }
+__device__ __forceinline__ PRow gp_pack(TIn x, u64 vbase, u32 &flags) {
+    const u64 d = (u64)x - vbase;
+    if (d >> 32) flags |= 1024u;
+    return (PRow)d;
+}
+__device__ __forceinline__ TIn gp_unpack(PRow v, u64 vbase) { return (TIn)(vbase + (u64)v); }
+#else
+typedef TIn PRow;
+__device__ __forceinline__ u64 gp_vbase(const TIn *__restrict__) { return 0; }
+__device__ __forceinline__ PRow gp_pack(TIn x, u64, u32 &) { return x; }
+__device__ __forceinline__ TIn gp_unpack(PRow v, u64) { return v; }
+#endif
 #define GP_TILE (BT * GP_ROWS)
 #define GP_TBLK (GP_TILE / GP_BLK)
 // The kernels' log2p argument carries the bin shift of range bins in bits
@@ -895,8 +915,9 @@ __device__ __forceinline__ void gp_load(const TIn *__restrict__ col, long long n
 extern "C" __global__ void __launch_bounds__(BT)
 fq_jit_gpart(const TIn *__restrict__ col, long long n, const u64 *__restrict__ bitmap, Consts c,
              u32 *__restrict__ used, u32 *__restrict__ bin_blocks, u32 *__restrict__ blk_bin,
-             u32 *__restrict__ blk_fill, unsigned q, TIn *__restrict__ out, int log2p,
+             u32 *__restrict__ blk_fill, unsigned q, PRow *__restrict__ out, int log2p,
              u32 *__restrict__ hdr) {
+    const u64 vbase = n > 0 ? gp_vbase(col) : 0ull;
 #if !RANGE_BINS
     __shared__ TIn s_stage[GP_TILE];
     __shared__ unsigned char s_bin[GP_TILE];
@@ -1012,7 +1033,7 @@ fq_jit_gpart(const TIn *__restrict__ col, long long n, const u64 *__restrict__ b
             u32 blk = o < GP_BLK ? s_blk[b] : s_nb[b];
             if (blk == 0xffffffffu) continue;  // (workspace overflow, reported)
             if (o >= GP_BLK) blk += o / GP_BLK - 1u;
-            __builtin_nontemporal_store(x[k], out + (long long)blk * GP_BLK + (o & (GP_BLK - 1)));
+            __builtin_nontemporal_store(gp_pack(x[k], vbase, flags), out + (long long)blk * GP_BLK + (o & (GP_BLK - 1)));
         }
 #else
 #pragma unroll
@@ -1030,7 +1051,7 @@ fq_jit_gpart(const TIn *__restrict__ col, long long n, const u64 *__restrict__ b
             u32 blk = o < GP_BLK ? s_blk[b] : s_nb[b];
             if (blk == 0xffffffffu) continue;  // (workspace overflow, reported)
             if (o >= GP_BLK) blk += o / GP_BLK - 1u;
-            __builtin_nontemporal_store(s_stage[i], out + (long long)blk * GP_BLK + (o & (GP_BLK - 1)));
+            __builtin_nontemporal_store(gp_pack(s_stage[i], vbase, flags), out + (long long)blk * GP_BLK + (o & (GP_BLK - 1)));
         }
 #endif
         __syncthreads();
@@ -1069,7 +1090,7 @@ fq_jit_gpart(const TIn *__restrict__ col, long long n, const u64 *__restrict__ b
 // LDS, not on a dependent HBM load
 #define GP_ORD 1024
 #define GP_ORD_TILES (GP_ORD / GP_TBLK)
-__device__ __forceinline__ u32 gb_load(const TIn *__restrict__ vals, const u64 *s_ord, long long ti,
+__device__ __forceinline__ u32 gb_load(const PRow *__restrict__ vals, u64 vbase, const u64 *s_ord, long long ti,
                                        TIn (&x)[GP_ROWS]) {
     u32 live = 0;
     const int t0 = (int)(ti % GP_ORD_TILES) * GP_TBLK;
@@ -1080,7 +1101,7 @@ __device__ __forceinline__ u32 gb_load(const TIn *__restrict__ vals, const u64 *
         const u64 ent = s_ord[t0 + j / GP_BLK];
         x[k] = TIn(0);
         if ((u32)off < (u32)(ent >> 32)) {
-            x[k] = __builtin_nontemporal_load(vals + (long long)(u32)ent * GP_BLK + off);
+            x[k] = gp_unpack(__builtin_nontemporal_load(vals + (long long)(u32)ent * GP_BLK + off), vbase);
             live |= 1u << k;
         }
     }
@@ -1093,8 +1114,9 @@ __device__ __forceinline__ void gb_stage(u64 *s_ord, const u64 *__restrict__ ord
 }
 
 extern "C" __global__ void __launch_bounds__(BT)
-fq_jit_groupby_bins(const TIn *__restrict__ vals, const u64 *__restrict__ order, const u32 *__restrict__ bstart,
-                    int log2p, Consts c, Tab t) {
+fq_jit_groupby_bins(const PRow *__restrict__ vals, const u64 *__restrict__ order, const u32 *__restrict__ bstart,
+                    int log2p, Consts c, Tab t, const TIn *__restrict__ col) {
+    const u64 vbase = gp_vbase(col);  // the launch has rows, so col[0] exists
     __shared__ u64 s_keys[S];
     __shared__ u64 s_st[NA][S];
     __shared__ int s_bypass[2];
@@ -1121,7 +1143,7 @@ fq_jit_groupby_bins(const TIn *__restrict__ vals, const u64 *__restrict__ order,
             // loads are in flight while this one goes through the LDS table
             const long long nt = (e - lo + GP_TBLK - 1) / GP_TBLK;
             TIn nxt[GP_ROWS];
-            u32 nlive = gb_load(vals, s_ord, 0, nxt);
+            u32 nlive = gb_load(vals, vbase, s_ord, 0, nxt);
             for (long long ti = 0; ti < nt; ++ti) {
                 TIn x[GP_ROWS];
 #pragma unroll
@@ -1133,7 +1155,7 @@ fq_jit_groupby_bins(const TIn *__restrict__ vals, const u64 *__restrict__ order,
                         gb_stage(s_ord, order, lo, e, ti + 1);
                         __syncthreads();
                     }
-                    nlive = gb_load(vals, s_ord, ti + 1, nxt);
+                    nlive = gb_load(vals, vbase, s_ord, ti + 1, nxt);
                 }
                 Row r[GP_ROWS];
 #pragma unroll
@@ -1182,6 +1204,7 @@ bool gen_groupby_source(const GroupLaunch &G, int32_t tin, Gen &g, std::string &
     src += "#define GCHUNK " + std::to_string(group_chunked()) + "\n";
     src += "#define GWAVE " + std::to_string(group_wave_runs()) + "\n";
     src += "#define RANGE_BINS " + std::to_string(G.range_bins ? 1 : 0) + "\n";
+    src += "#define GP_NARROW " + std::to_string(G.narrow ? 1 : 0) + "\n";
     src += "#define GP_BLK " + std::to_string(kPartBlockRows) + "\n";
     src += "#define GCLUSTER " + std::to_string(cluster && group_cluster() > 0 && fqc::dtype_size(tin) == 8 &&
                                                           G.lds_bytes + G.threads * 16 <= 160 * 1024 ? 1 : 0) + "\n";
@@ -2563,7 +2586,7 @@ fq_status jit_groupby_partitioned(int32_t col_dtype, const GroupLaunch &G, const
     const void *cvals = X.vals;
     const uint64_t *order = X.order;
     const uint32_t *bstart = X.bstart;
-    void *a2[] = {&cvals, &order, &bstart, &log2p, &hc, &tab};
+    void *a2[] = {&cvals, &order, &bstart, &log2p, &hc, &tab, &col};
     FQ_HIP_TRY(hipModuleLaunchKernel(f.bins, (unsigned)X.bins_grid, 1, 1, (unsigned)G.threads, 1, 1, 0, G.stream, a2,
                                      nullptr));
     g_jit_launches += 2;

@@ -89,6 +89,7 @@ struct GroupLaunch {
     int lds_bytes;  // LDS hash table budget per workgroup (sets S and the occupancy)
     int threads;    // workgroup size
     int rowmap;     // 1: lane-consecutive rows (8-byte loads), 0: row pairs per lane (16-byte loads)
+    int narrow;     // partitioned path: 4-byte rows (offsets from col[0] - 2^31, FQ_GROUP_NARROW_ROWS)
     int range_bins; // partitioned path: bin = key >> log2(S) and LDS slot = key & (S - 1) (a UInt64
                     // key below d <= P * S: `% d`), else bins by the key's hash
     int grid;
@@ -126,7 +127,7 @@ struct GroupPartition {
     uint32_t *blk_bin;    // [max_blocks] each block's bin
     uint32_t *blk_fill;   // [max_blocks] its rows
     uint64_t *order;      // [max_blocks] block | rows << 32, grouped by bin
-    void *vals;           // max_blocks x kPartBlockRows rows
+    void *vals;           // max_blocks x kPartBlockRows rows (8-byte values, or 4-byte offsets when narrow)
 };
 fq_status jit_groupby_partitioned(int32_t col_dtype, const GroupLaunch &G, const GroupPartition &X);
 // the blocks of fq_jit_gpart grouped by bin: a scan of X.bin_blocks into

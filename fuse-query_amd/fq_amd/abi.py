@@ -106,6 +106,7 @@ class fq_jit_stats(C.Structure):
 JIT_OFF, JIT_AUTO, JIT_ALWAYS = 0, 1, 2
 
 MAX_GROUP_AGGS = 8
+GROUP_NARROW_ROWS = 0x10000  # fq_group_aggregate_partitioned: 4-byte partition rows
 FQ_E_TABLE_FULL = 8
 
 

@@ -318,9 +318,10 @@ class GroupTable:
         self.aggs = list(aggs)
         check(lib.fq_group_table_init(C.byref(self.desc), _stream(stream)))
 
-    def aggregate(self, col, pred=None, key=None, values=None, stream=None, log2_parts=0):
+    def aggregate(self, col, pred=None, key=None, values=None, stream=None, log2_parts=0, narrow=False):
         """fq_group_aggregate, or with log2_parts > 0 the radix-partitioned
-        fq_group_aggregate_partitioned (2^log2_parts bins)."""
+        fq_group_aggregate_partitioned (2^log2_parts bins; narrow: the caller
+        vouches every value lies within 2^31 of the first, FQ_GROUP_NARROW_ROWS)."""
         c = col.col()
         vals = (abi.fq_expr * abi.MAX_GROUP_AGGS)()
         for i, v in enumerate(values or []):
@@ -332,7 +333,8 @@ class GroupTable:
             check(lib.fq_group_aggregate(C.byref(self.desc), C.byref(c), p, k, vals, _stream(stream)))
             return
         ws = Workspace(lib.fq_group_partition_workspace_bytes(col.len, log2_parts))
-        check(lib.fq_group_aggregate_partitioned(C.byref(self.desc), C.byref(c), p, k, vals, log2_parts, ws.ptr,
+        lp = log2_parts | (abi.GROUP_NARROW_ROWS if narrow else 0)
+        check(lib.fq_group_aggregate_partitioned(C.byref(self.desc), C.byref(c), p, k, vals, lp, ws.ptr,
                                                  ws.nbytes, _stream(stream)))
         self._ws = ws  # alive until the next call (the launch is asynchronous)
 

@@ -643,6 +643,41 @@ def test_aggregate_merge_aggregate_into_one_table(log2p):
     compare(got, exp, [a for a, _ in aggs], [d for _, d in aggs])
 
 
+@pytest.mark.parametrize("mod,log2p,pred", [(100_000, 6, False), (None, 8, False), (5000, 4, True)])
+def test_narrow_partition_rows_match_wide(mod, log2p, pred):
+    # FQ_GROUP_NARROW_ROWS (4-byte offsets from col[0] - 2^31 in the blocks):
+    # the same table as the 8-byte rows over a numbers_mt-like block, with
+    # range bins, hash bins and a predicate, first values near 2^40 (offsets
+    # wrap through 0) and near 2^64 - 2^31 (the base wraps)
+    for first in (2**40 - 1000, 2**64 - 2**31 + 77):
+        n = 2_000_003
+        col = ops.numbers_column(first, n)
+        key = chain(U, [("%", mod)])[0] if mod else None
+        p = predicate(U, [("%", 8)], "<", 3) if pred else None
+        aggs = [(abi.AGG_COUNT, U), (abi.AGG_SUM, U), (abi.AGG_MAX, U), (abi.AGG_MIN, U)]
+        res = []
+        for narrow in (False, True):
+            t = ops.GroupTable(4 * min(n, mod or n), aggs)
+            t.aggregate(col, p, key, [None] * 4, log2_parts=log2p, narrow=narrow)
+            keys, st = t.extract()
+            o = np.argsort(keys, kind="stable")
+            res.append((keys[o], [x[o] for x in st]))
+        assert np.array_equal(res[0][0], res[1][0]) and len(res[0][0]) > 0
+        for a in range(4):
+            assert np.array_equal(res[0][1][a], res[1][1][a]), (first, a)
+
+
+def test_narrow_partition_rows_refuse_values_out_of_range():
+    # a value more than 2^31 from col[0]: reported, never aggregated wrongly
+    x = np.arange(100_000, dtype=np.uint64)
+    x[77_777] += np.uint64(2**33)
+    col = ops.from_numpy(x)
+    t = ops.GroupTable(1 << 18, [(abi.AGG_COUNT, U)])
+    t.aggregate(col, None, chain(U, [("%", 1000)])[0], [None], log2_parts=4, narrow=True)
+    with pytest.raises(ops.FQError, match="narrow rows"):
+        t.count()
+
+
 def test_table_merge_sentinel_key_and_empty_input():
     # the all-ones key (the table's EMPTY marker) has its own slot
     aggs = [(abi.AGG_COUNT, U), (abi.AGG_MAX, U)]
