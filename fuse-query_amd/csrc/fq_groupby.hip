@@ -525,7 +525,7 @@ fq_status fq_group_aggregate_partitioned(const fq_group_table *t, const fq_col *
     fq_status s = prepare_group(t, col, pred, key_expr, values, stream, G);
     if (s != FQ_OK) return s;
     // 4-byte rows for 8-byte integer columns the caller vouches for
-    G.narrow = narrow && (col->dtype == FQ_DT_UINT64 || col->dtype == FQ_DT_INT64) ? 1 : 0;
+    G.narrow = narrow && fqc::knob(FQ_TUNE_GROUP_NARROW) && (col->dtype == FQ_DT_UINT64 || col->dtype == FQ_DT_INT64) ? 1 : 0;
     if (G.n > 0 && (!d_ws || ws_bytes < part_ws_bytes(G.n, log2_parts, nullptr, nullptr)))
         return fqc::fail(FQ_E_INVALID, "fq_group_aggregate_partitioned: workspace too small");
     if (((uintptr_t)d_ws) & 255u) return fqc::fail(FQ_E_INVALID, "fq_group_aggregate_partitioned: workspace not 256-B aligned");

@@ -857,11 +857,31 @@ __device__ __forceinline__ PRow gp_pack(TIn x, u64 vbase, u32 &flags) {
     return (PRow)d;
 }
 __device__ __forceinline__ TIn gp_unpack(PRow v, u64 vbase) { return (TIn)(vbase + (u64)v); }
+// 4-byte rows: plain accesses (GP_NT_NARROW 1: non-temporal, as the 8-byte rows)
+#ifndef GP_NT_NARROW
+#define GP_NT_NARROW 0
+#endif
+__device__ __forceinline__ void gp_store(PRow *p, PRow v) {
+#if GP_NT_NARROW
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
+}
+__device__ __forceinline__ PRow gp_fetch(const PRow *p) {
+#if GP_NT_NARROW
+    return __builtin_nontemporal_load(p);
+#else
+    return *p;
+#endif
+}
 #else
 typedef TIn PRow;
 __device__ __forceinline__ u64 gp_vbase(const TIn *__restrict__) { return 0; }
 __device__ __forceinline__ PRow gp_pack(TIn x, u64, u32 &) { return x; }
 __device__ __forceinline__ TIn gp_unpack(PRow v, u64) { return v; }
+__device__ __forceinline__ void gp_store(PRow *p, PRow v) { __builtin_nontemporal_store(v, p); }
+__device__ __forceinline__ PRow gp_fetch(const PRow *p) { return __builtin_nontemporal_load(p); }
 #endif
 #define GP_TILE (BT * GP_ROWS)
 #define GP_TBLK (GP_TILE / GP_BLK)
@@ -912,7 +932,9 @@ __device__ __forceinline__ void gp_load(const TIn *__restrict__ col, long long n
 // Workgroup w owns blocks [w * q, (w + 1) * q): used[w] of them taken;
 // bin_blocks[b]: blocks of bin b; blk_bin / blk_fill: each block's bin and
 // rows (GP_BLK but for the last block of a chain)
-extern "C" __global__ void __launch_bounds__(BT)
+// two 1,024-thread workgroups per CU = 8 waves per SIMD, which needs <= 80
+// SGPRs (84 admit 7 waves: one workgroup, and the pass ran 1.1 -> 1.5 ms)
+extern "C" __global__ void __launch_bounds__(BT) __attribute__((amdgpu_waves_per_eu(BT >= 1024 ? 8 : 1)))
 fq_jit_gpart(const TIn *__restrict__ col, long long n, const u64 *__restrict__ bitmap, Consts c,
              u32 *__restrict__ used, u32 *__restrict__ bin_blocks, u32 *__restrict__ blk_bin,
              u32 *__restrict__ blk_fill, unsigned q, PRow *__restrict__ out, int log2p,
@@ -1033,7 +1055,7 @@ fq_jit_gpart(const TIn *__restrict__ col, long long n, const u64 *__restrict__ b
             u32 blk = o < GP_BLK ? s_blk[b] : s_nb[b];
             if (blk == 0xffffffffu) continue;  // (workspace overflow, reported)
             if (o >= GP_BLK) blk += o / GP_BLK - 1u;
-            __builtin_nontemporal_store(gp_pack(x[k], vbase, flags), out + (long long)blk * GP_BLK + (o & (GP_BLK - 1)));
+            gp_store(out + (long long)blk * GP_BLK + (o & (GP_BLK - 1)), gp_pack(x[k], vbase, flags));
         }
 #else
 #pragma unroll
@@ -1051,7 +1073,7 @@ fq_jit_gpart(const TIn *__restrict__ col, long long n, const u64 *__restrict__ b
             u32 blk = o < GP_BLK ? s_blk[b] : s_nb[b];
             if (blk == 0xffffffffu) continue;  // (workspace overflow, reported)
             if (o >= GP_BLK) blk += o / GP_BLK - 1u;
-            __builtin_nontemporal_store(gp_pack(s_stage[i], vbase, flags), out + (long long)blk * GP_BLK + (o & (GP_BLK - 1)));
+            gp_store(out + (long long)blk * GP_BLK + (o & (GP_BLK - 1)), gp_pack(s_stage[i], vbase, flags));
         }
 #endif
         __syncthreads();
@@ -1094,6 +1116,27 @@ __device__ __forceinline__ u32 gb_load(const PRow *__restrict__ vals, u64 vbase,
                                        TIn (&x)[GP_ROWS]) {
     u32 live = 0;
     const int t0 = (int)(ti % GP_ORD_TILES) * GP_TBLK;
+#if GP_NARROW
+    // four adjacent 4-byte rows per lane and load: 16-byte accesses (one
+    // 4-byte row per lane per load ran the pass 0.60 -> 1.04 ms per 4.2e8
+    // rows, two per 8-byte load 0.71 ms; swapping rows across the wave so
+    // consecutive lanes hold consecutive rows cost more than it saved)
+#pragma unroll
+    for (int k = 0; k < GP_ROWS / 4; ++k) {
+        const int j = 4 * (k * BT + (int)threadIdx.x);  // this lane's first row
+        const int off = j & (GP_BLK - 1);
+        const u64 ent = s_ord[t0 + j / GP_BLK];
+        const u32 fill = (u32)(ent >> 32);
+        u32x4 four = {0u, 0u, 0u, 0u};
+        if ((u32)off < fill) four = __builtin_nontemporal_load((const u32x4 *)(vals + (long long)(u32)ent * GP_BLK + off));
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const bool lv = (u32)(off + q) < fill;
+            x[4 * k + q] = lv ? gp_unpack(four[q], vbase) : TIn(0);
+            live |= (lv ? 1u : 0u) << (4 * k + q);
+        }
+    }
+#else
 #pragma unroll
     for (int k = 0; k < GP_ROWS; ++k) {
         const int j = k * BT + (int)threadIdx.x;
@@ -1101,10 +1144,11 @@ __device__ __forceinline__ u32 gb_load(const PRow *__restrict__ vals, u64 vbase,
         const u64 ent = s_ord[t0 + j / GP_BLK];
         x[k] = TIn(0);
         if ((u32)off < (u32)(ent >> 32)) {
-            x[k] = gp_unpack(__builtin_nontemporal_load(vals + (long long)(u32)ent * GP_BLK + off), vbase);
+            x[k] = gp_unpack(gp_fetch(vals + (long long)(u32)ent * GP_BLK + off), vbase);
             live |= 1u << k;
         }
     }
+#endif
     return live;
 }
 __device__ __forceinline__ void gb_stage(u64 *s_ord, const u64 *__restrict__ order, long long lo, long long e,
@@ -1205,7 +1249,9 @@ bool gen_groupby_source(const GroupLaunch &G, int32_t tin, Gen &g, std::string &
     src += "#define GWAVE " + std::to_string(group_wave_runs()) + "\n";
     src += "#define RANGE_BINS " + std::to_string(G.range_bins ? 1 : 0) + "\n";
     src += "#define GP_NARROW " + std::to_string(G.narrow ? 1 : 0) + "\n";
-    src += "#define GP_BLK " + std::to_string(kPartBlockRows) + "\n";
+    // blocks are 2 KB either way: 256 8-byte rows, or 512 narrow ones (1 KB
+    // blocks measured 1.11 -> 1.53 ms per 4.2e8-row partition pass)
+    src += "#define GP_BLK " + std::to_string(kPartBlockRows * (G.narrow ? 2 : 1)) + "\n";
     src += "#define GCLUSTER " + std::to_string(cluster && group_cluster() > 0 && fqc::dtype_size(tin) == 8 &&
                                                           G.lds_bytes + G.threads * 16 <= 160 * 1024 ? 1 : 0) + "\n";
     src += "#define GCLUSTER_CHANGES " + std::to_string(group_cluster() > 0 ? group_cluster() : 160) + "\n";

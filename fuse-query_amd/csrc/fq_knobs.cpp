@@ -43,6 +43,7 @@ constexpr KnobDef kDefs[FQ_TUNE_COUNT] = {
     {1, 0, 1, 1, false},         // GROUP_ROWMAP
     {1, 1, 8, 1, false},         // GROUP_WG_PER_CU
     {1, 0, 1, 1, false},         // GROUP_RANGE_BINS
+    {1, 0, 1, 1, false},         // GROUP_NARROW
 };
 
 std::atomic<int64_t> g_val[FQ_TUNE_COUNT] = {};

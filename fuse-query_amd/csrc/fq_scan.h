@@ -111,7 +111,7 @@ fq_status jit_groupby(int32_t col_dtype, const GroupLaunch &G);
 // partition into block chains -> blocks grouped by bin -> per-bin
 // aggregation, in the caller's workspace (fq_groupby.hip lays it out).
 constexpr int kMaxPartGrid = 1024;    // workgroups of the partition kernel
-constexpr int kPartBlockRows = 256;   // rows per partition block (2 KB of u64)
+constexpr int kPartBlockRows = 256;   // rows per partition block (2 KB of u64; narrow blocks hold 2x the rows)
 struct GroupPartition {
     int log2p;            // bits 0..7: 1..8, P = 2^log2p bins; bits 8..15: the key shift of range bins
     int grid;             // workgroups of fq_jit_gpart

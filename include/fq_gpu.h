@@ -366,7 +366,8 @@ fq_status fq_jit_prepare(const fq_col *col, int64_t block_rows, const fq_pred *p
 #define FQ_TUNE_GROUP_ROWMAP 21      /* GROUP BY LDS kernel row map: 1 (0/1)                     */
 #define FQ_TUNE_GROUP_WG_PER_CU 22   /* GROUP BY LDS kernel workgroups per CU: 1 (1..8)           */
 #define FQ_TUNE_GROUP_RANGE_BINS 23  /* partitioned GROUP BY: range bins for `% d` keys, 1 (0/1) */
-#define FQ_TUNE_COUNT 24
+#define FQ_TUNE_GROUP_NARROW 24      /* partitioned GROUP BY: honour FQ_GROUP_NARROW_ROWS, 1 (0/1) */
+#define FQ_TUNE_COUNT 25
 /* FQ_E_INVALID for an unknown knob or a value outside the knob's set */
 fq_status fq_tune_set(int32_t knob, int64_t value);
 /* the knob's current value; -1 for an unknown knob */
