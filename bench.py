@@ -217,7 +217,9 @@ def cpu_baseline(sample_rows, threads, query="c3"):
         "value": n / dt, "unit": "rows/s", "cores": threads, "kind": "port",
         "sample": "%s query over numbers_mt(%d): 8 partitions, one thread per partition, "
                   "10,000-row blocks regenerated per block, one pass per aggregator%s "
-                  "(oracle/fq_oracle.c, %s); %.2f s wall on %s (nproc=%d)"
+                  "(oracle/fq_oracle.c, %s); %.2f s wall on %s (nproc=%d).  A lower bound on the reference's own "
+                  "CPU cost: the port keeps its per-block state machine but not its per-block 1-row arrays, "
+                  "serde_json partial states or tokio channel hand-offs (README.md:62 quotes 6.40 s for C3 on 8 vCPUs)"
                   % (query.upper(), n, ", constant broadcast + filter compaction per block" if pred else "", "-O3 -march=native" if native else "-O3 -march=x86-64-v2", dt, cpu,
                      os.cpu_count() or 0),
     }
@@ -248,7 +250,8 @@ def cpu_baseline_project(sample_rows, threads):
         "sample": "P1 over numbers_mt(%d): 8 partitions, one thread per partition, 10,000-row blocks regenerated "
                   "per block, FilterTransform compaction then each projected expression into its own array "
                   "(transform_filter.rs:38-55, transform_projection.rs:45-56; oracle/fq_oracle.c "
-                  "fqo_numbers_project, %s); %.2f s wall on %s (nproc=%d)"
+                  "fqo_numbers_project, %s); %.2f s wall on %s (nproc=%d).  A lower bound on the reference's own "
+                  "CPU cost (no arrow RecordBatch per block, no tokio hand-offs)"
                   % (n, "-O3 -march=native" if native else "-O3 -march=x86-64-v2", dt, _cpu_model(),
                      os.cpu_count() or 0),
     }
