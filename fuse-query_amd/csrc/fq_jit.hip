@@ -1120,7 +1120,11 @@ __device__ __forceinline__ u32 gb_load(const PRow *__restrict__ vals, u64 vbase,
     // four adjacent 4-byte rows per lane and load: 16-byte accesses (one
     // 4-byte row per lane per load ran the pass 0.60 -> 1.04 ms per 4.2e8
     // rows, two per 8-byte load 0.71 ms; swapping rows across the wave so
-    // consecutive lanes hold consecutive rows cost more than it saved)
+    // consecutive lanes hold consecutive rows cost more than it saved).
+    // Slot q of lane L takes the lane's row (q + L / 4) % 4: consecutive keys
+    // 4 apart across lanes would put a 16-lane group's 8-byte LDS updates on
+    // 4 bank pairs (4-way conflicts); rotated they cover all 16.
+    const u32 rot = (threadIdx.x >> 2) & 3u;
 #pragma unroll
     for (int k = 0; k < GP_ROWS / 4; ++k) {
         const int j = 4 * (k * BT + (int)threadIdx.x);  // this lane's first row
@@ -1129,10 +1133,13 @@ __device__ __forceinline__ u32 gb_load(const PRow *__restrict__ vals, u64 vbase,
         const u32 fill = (u32)(ent >> 32);
         u32x4 four = {0u, 0u, 0u, 0u};
         if ((u32)off < fill) four = __builtin_nontemporal_load((const u32x4 *)(vals + (long long)(u32)ent * GP_BLK + off));
+        const u32x4 r1 = (rot & 1u) ? u32x4{four[1], four[2], four[3], four[0]} : four;
+        const u32x4 r2 = (rot & 2u) ? u32x4{r1[2], r1[3], r1[0], r1[1]} : r1;
+        const u32 nl = (u32)off < fill ? fill - (u32)off : 0u;  // live rows from off (>= 4: all)
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const bool lv = (u32)(off + q) < fill;
-            x[4 * k + q] = lv ? gp_unpack(four[q], vbase) : TIn(0);
+            const bool lv = ((q + rot) & 3u) < nl;
+            x[4 * k + q] = lv ? gp_unpack(r2[q], vbase) : TIn(0);
             live |= (lv ? 1u : 0u) << (4 * k + q);
         }
     }
