@@ -21,15 +21,18 @@
 // fq_agg_state bits for the same grid; tests/test_kernels_gpu.py checks both
 // against the oracle.
 #include <dlfcn.h>
+#include <pthread.h>
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
 
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <mutex>
 #include <string>
 #include <unordered_map>
@@ -67,27 +70,82 @@ struct Rtc {
     bool isolated = false;  // the system ROCm's hipRTC in its own link-map namespace
 };
 
+// Every hipRTC call runs on one thread of its own (64 MB stack), the one
+// that loaded it: the namespace's own libc copy then serves a single thread.
+// Sources with inline asm (the partition kernel's LDS-DMA path) compiled from
+// several threads -- the engine's workers -- crashed the process inside
+// hipRTC (SIGSEGV); on one thread, or with the process's hipRTC, they compile
+// (tests/test_jit_cpu.py::test_compiles_from_many_threads reproduces it).
+class RtcThread {
+  public:
+    static RtcThread &get() {
+        static RtcThread *t = new RtcThread;  // never destroyed: the thread outlives static teardown
+        return *t;
+    }
+    void run(const std::function<void()> &f) {
+        std::lock_guard<std::mutex> one(call_mu_);  // one job at a time
+        if (!ok_) {
+            f();
+            return;
+        }
+        std::unique_lock<std::mutex> lk(mu_);
+        job_ = &f;
+        done_ = false;
+        cv_.notify_all();
+        cv_.wait(lk, [this] { return done_; });
+    }
+
+  private:
+    RtcThread() {
+        pthread_attr_t a;
+        pthread_attr_init(&a);
+        pthread_attr_setstacksize(&a, (size_t)64 << 20);
+        pthread_t t;
+        ok_ = pthread_create(&t, &a, &RtcThread::main, this) == 0;
+        pthread_attr_destroy(&a);
+        if (ok_) pthread_detach(t);
+    }
+    static void *main(void *self) {
+        RtcThread &t = *(RtcThread *)self;
+        std::unique_lock<std::mutex> lk(t.mu_);
+        for (;;) {
+            t.cv_.wait(lk, [&t] { return t.job_ != nullptr; });
+            (*t.job_)();
+            t.job_ = nullptr;
+            t.done_ = true;
+            t.cv_.notify_all();
+        }
+        return nullptr;
+    }
+    std::mutex call_mu_, mu_;
+    std::condition_variable cv_;
+    const std::function<void()> *job_ = nullptr;
+    bool done_ = false, ok_ = false;
+};
+
 const Rtc &rtc() {
     static const Rtc r = [] {
         Rtc x;
-        void *h = nullptr;
-        if (fqc::knob(FQ_TUNE_JIT_ISOLATED)) {
-            const char *root = getenv("ROCM_PATH");
-            const std::string path = std::string(root && *root ? root : "/opt/rocm") + "/lib/libhiprtc.so.7";
-            h = dlmopen(LM_ID_NEWLM, path.c_str(), RTLD_NOW | RTLD_LOCAL);
-            x.isolated = h != nullptr;
-        }
-        if (!h) h = dlopen("libhiprtc.so.7", RTLD_NOW | RTLD_GLOBAL);
-        if (!h) h = dlopen("libhiprtc.so", RTLD_NOW | RTLD_GLOBAL);
-        if (!h) return x;
-        x.create = (decltype(x.create))dlsym(h, "hiprtcCreateProgram");
-        x.compile = (decltype(x.compile))dlsym(h, "hiprtcCompileProgram");
-        x.log_size = (decltype(x.log_size))dlsym(h, "hiprtcGetProgramLogSize");
-        x.log = (decltype(x.log))dlsym(h, "hiprtcGetProgramLog");
-        x.code_size = (decltype(x.code_size))dlsym(h, "hiprtcGetCodeSize");
-        x.code = (decltype(x.code))dlsym(h, "hiprtcGetCode");
-        x.destroy = (decltype(x.destroy))dlsym(h, "hiprtcDestroyProgram");
-        x.ok = x.create && x.compile && x.log_size && x.log && x.code_size && x.code && x.destroy;
+        RtcThread::get().run([&x] {
+            void *h = nullptr;
+            if (fqc::knob(FQ_TUNE_JIT_ISOLATED)) {
+                const char *root = getenv("ROCM_PATH");
+                const std::string path = std::string(root && *root ? root : "/opt/rocm") + "/lib/libhiprtc.so.7";
+                h = dlmopen(LM_ID_NEWLM, path.c_str(), RTLD_NOW | RTLD_LOCAL);
+                x.isolated = h != nullptr;
+            }
+            if (!h) h = dlopen("libhiprtc.so.7", RTLD_NOW | RTLD_GLOBAL);
+            if (!h) h = dlopen("libhiprtc.so", RTLD_NOW | RTLD_GLOBAL);
+            if (!h) return;
+            x.create = (decltype(x.create))dlsym(h, "hiprtcCreateProgram");
+            x.compile = (decltype(x.compile))dlsym(h, "hiprtcCompileProgram");
+            x.log_size = (decltype(x.log_size))dlsym(h, "hiprtcGetProgramLogSize");
+            x.log = (decltype(x.log))dlsym(h, "hiprtcGetProgramLog");
+            x.code_size = (decltype(x.code_size))dlsym(h, "hiprtcGetCodeSize");
+            x.code = (decltype(x.code))dlsym(h, "hiprtcGetCode");
+            x.destroy = (decltype(x.destroy))dlsym(h, "hiprtcDestroyProgram");
+            x.ok = x.create && x.compile && x.log_size && x.log && x.code_size && x.code && x.destroy;
+        });
         return x;
     }();
     return r;
@@ -770,7 +828,7 @@ void pack_group_consts(const GroupLaunch &G, HostGroupConsts &hc) {
 std::string group_shape_key(const GroupLaunch &G, int32_t tin, int dev) {
     std::string k = "G" + std::to_string(group_lds_local()) + std::to_string(group_key_plain()) +
                     std::to_string(group_chunked()) + std::to_string(group_wave_runs()) +
-                    std::to_string(group_cluster());
+                    std::to_string(group_cluster()) + std::to_string(fqc::knob(FQ_TUNE_GROUP_PREFETCH));
     auto put = [&k](int32_t v) { k.append(reinterpret_cast<const char *>(&v), sizeof v); };
     auto prog = [&put](const KProg &p) {
         put(p.n);
@@ -846,7 +904,7 @@ std::string state_update(int32_t kind, int32_t dt, const std::string &P, const s
 // lies within 2^31 of col[0], as a numbers_mt block's do) the blocks hold
 // 4-byte offsets from col[0] - 2^31: 8 + 4 + 4 = 16 B per passing row; a
 // value outside the range sets flag 1024 and the launch reports it.
-const char *kGroupPartitionKernels = R"(
+const char *kGroupPartitionKernels = R"GP(
 #define GP_ROWS 8
 #if GP_NARROW
 typedef u32 PRow;  // a kept row in the blocks: its offset from col[0] - 2^31
@@ -920,11 +978,47 @@ __device__ __forceinline__ u32 gp_rank(u32 *cnt, u32 b, bool p) {
     return p ? atomicAdd(&cnt[b], 1u) : 0u;
 }
 
+#if GP_PREFETCH
+// Row k of a thread in tile tt: wave w holds the tile's rows [w * 64 * GP_ROWS,
+// (w + 1) * 64 * GP_ROWS) -- one contiguous 4 KB run per wave, which its own
+// LDS-DMA loads fill (no other wave reads it: no barrier between the reads of
+// one tile and the DMA of the next)
+__device__ __forceinline__ long long gp_row(long long tt, int k) {
+    return tt * GP_TILE + (long long)(threadIdx.x >> 6) * (64 * GP_ROWS) + k * 64 + (threadIdx.x & 63);
+}
+// LDS-only barrier: __syncthreads()' fence would wait for the DMA in flight
+// (vmcnt(0)); the loop's barriers order LDS state only
+__device__ __forceinline__ void gp_sync() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+// the wave's 64 * GP_ROWS rows of tile tt into its LDS run: GP_ROWS / 2
+// global_load_lds_dwordx4, two rows per lane each (a full tile only).  In asm,
+// so the compiler's wait counting neither sees it nor drains it early: the
+// reader waits with vmcnt(0) itself.
+__device__ __forceinline__ void gp_dma(const TIn *__restrict__ col, long long tt, TIn *s_rows) {
+    const int w = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
+    const TIn *src = col + tt * GP_TILE + (long long)w * (64 * GP_ROWS) + 2 * lane;
+    const u32 dst0 = (u32)(size_t)(__attribute__((address_space(3))) TIn *)(s_rows + w * (64 * GP_ROWS));
+#pragma unroll
+    for (int i = 0; i < GP_ROWS / 2; ++i) {
+        const u32 dst = (u32)__builtin_amdgcn_readfirstlane((int)(dst0 + i * 1024u));
+        u32 keep;
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(src + i * 128), "s"(dst) : "memory");
+    }
+}
+#else
+__device__ __forceinline__ long long gp_row(long long tt, int k) {
+    return tt * GP_TILE + (long long)k * BT + threadIdx.x;
+}
+__device__ __forceinline__ void gp_sync() { __syncthreads(); }
+#endif
 __device__ __forceinline__ void gp_load(const TIn *__restrict__ col, long long n, long long tt, TIn (&x)[GP_ROWS]) {
-    const long long r0 = tt * GP_TILE + threadIdx.x;
 #pragma unroll
     for (int k = 0; k < GP_ROWS; ++k) {
-        const long long row = r0 + (long long)k * BT;
+        const long long row = gp_row(tt, k);
         x[k] = row < n ? __builtin_nontemporal_load(col + row) : TIn(0);
     }
 }
@@ -933,7 +1027,10 @@ __device__ __forceinline__ void gp_load(const TIn *__restrict__ col, long long n
 // bin_blocks[b]: blocks of bin b; blk_bin / blk_fill: each block's bin and
 // rows (GP_BLK but for the last block of a chain)
 // two 1,024-thread workgroups per CU = 8 waves per SIMD, which needs <= 80
-// SGPRs (84 admit 7 waves: one workgroup, and the pass ran 1.1 -> 1.5 ms)
+// SGPRs (84 admit 7 waves: one workgroup, and the pass ran 1.1 -> 1.5 ms).
+// Loading the next tile's rows into registers while this one is ranked and
+// stored ran it 1.09 -> 1.81 ms per 4.2e8 narrow rows (64 VGPRs: spills);
+// GP_PREFETCH loads them into LDS instead.
 extern "C" __global__ void __launch_bounds__(BT) __attribute__((amdgpu_waves_per_eu(BT >= 1024 ? 8 : 1)))
 fq_jit_gpart(const TIn *__restrict__ col, long long n, const u64 *__restrict__ bitmap, Consts c,
              u32 *__restrict__ used, u32 *__restrict__ bin_blocks, u32 *__restrict__ blk_bin,
@@ -967,28 +1064,61 @@ fq_jit_gpart(const TIn *__restrict__ col, long long n, const u64 *__restrict__ b
     const u32 region = blockIdx.x * q;
     u32 flags = 0;
     const long long ntiles = (n + GP_TILE - 1) / GP_TILE;
+#if GP_PREFETCH
+    // the next tile's rows land in LDS while this one is ranked and stored
+    // (full tiles of a 16-byte aligned column; the last, partial tile and an
+    // unaligned column take plain loads)
+    __shared__ TIn s_rows[GP_TILE];
+    const long long nfull = ((size_t)col & 15) || GP_PREFETCH == 2 ? 0 : n / GP_TILE;
+    if ((long long)blockIdx.x < nfull) gp_dma(col, blockIdx.x, s_rows);
+#endif
     for (long long tt = blockIdx.x; tt < ntiles; tt += gridDim.x) {
         for (int i = threadIdx.x; i < P; i += BT) s_cnt[i] = 0;
-        __syncthreads();
-        const long long r0 = tt * GP_TILE + threadIdx.x;
         TIn x[GP_ROWS];
+#if GP_PREFETCH
+        TIn *mine = s_rows + (threadIdx.x >> 6) * (64 * GP_ROWS) + (threadIdx.x & 63);
+        if (tt < nfull) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this tile's DMA (and older stores)
+        } else {  // through the same LDS run, so x never comes from a plain load (whose use would
+                  // make the compiler wait vmcnt(0), draining the DMA, at every row)
+            TIn y[GP_ROWS];
+            gp_load(col, n, tt, y);
+#pragma unroll
+            for (int k = 0; k < GP_ROWS; ++k) mine[k * 64] = y[k];
+        }
+#pragma unroll
+        for (int k = 0; k < GP_ROWS; ++k) x[k] = mine[k * 64];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // read before the next DMA overwrites it
+#if GP_PREFETCH == 3
+        if (tt < nfull)
+#pragma unroll
+            for (int k = 0; k < GP_ROWS; ++k)
+                if (__builtin_nontemporal_load(col + gp_row(tt, k)) != x[k]) flags |= 2048u;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+        if (tt + gridDim.x < nfull) gp_dma(col, tt + gridDim.x, s_rows);
+        gp_sync();
+#else
+        __syncthreads();
         gp_load(col, n, tt, x);
-        u32 bin[GP_ROWS], rank[GP_ROWS], pass = 0;
+#endif
+        // per row: bin | rank << 8 (P <= 256 bins, rank < GP_TILE), one register instead of two
+        u32 br[GP_ROWS], pass = 0;
 #pragma unroll
         for (int k = 0; k < GP_ROWS; ++k) {
-            const long long row = r0 + (long long)k * BT;
+            const long long row = gp_row(tt, k);
             bool p = false;
-            bin[k] = 0;
+            u32 bk = 0;
             if (row < n) {
                 Row r;
                 fq_prep(x[k], row, c, bitmap, flags, r);
                 p = r.pass != 0;
-                if (p) bin[k] = gbin(r.k, log2p);
+                if (p) bk = gbin(r.k, log2p);
             }
-            rank[k] = gp_rank(s_cnt, bin[k], p);
+            br[k] = bk | gp_rank(s_cnt, bk, p) << 8;
             if (p) pass |= 1u << k;
         }
-        __syncthreads();
+        gp_sync();
 #if RANGE_BINS
         const int t0 = 0;  // every thread takes blocks (no tile scan)
 #else
@@ -1042,7 +1172,7 @@ fq_jit_gpart(const TIn *__restrict__ col, long long n, const u64 *__restrict__ b
                 s_nb[b] = base;
             }
         }
-        __syncthreads();
+        gp_sync();
 #if RANGE_BINS
         // straight from the registers: a wave's passing lanes mostly hold
         // consecutive ranks of one bin (gp_rank), so the stores coalesce
@@ -1051,7 +1181,7 @@ fq_jit_gpart(const TIn *__restrict__ col, long long n, const u64 *__restrict__ b
 #pragma unroll
         for (int k = 0; k < GP_ROWS; ++k) {
             if (!((pass >> k) & 1u)) continue;
-            const u32 b = bin[k], o = s_fill[b] + rank[k];
+            const u32 b = br[k] & 255u, o = s_fill[b] + (br[k] >> 8);
             u32 blk = o < GP_BLK ? s_blk[b] : s_nb[b];
             if (blk == 0xffffffffu) continue;  // (workspace overflow, reported)
             if (o >= GP_BLK) blk += o / GP_BLK - 1u;
@@ -1061,11 +1191,11 @@ fq_jit_gpart(const TIn *__restrict__ col, long long n, const u64 *__restrict__ b
 #pragma unroll
         for (int k = 0; k < GP_ROWS; ++k) {
             if (!((pass >> k) & 1u)) continue;
-            const u32 pos = s_start[bin[k]] + rank[k];
+            const u32 pos = s_start[br[k] & 255u] + (br[k] >> 8);
             s_stage[pos] = x[k];
-            s_bin[pos] = (unsigned char)bin[k];
+            s_bin[pos] = (unsigned char)(br[k] & 255u);
         }
-        __syncthreads();
+        gp_sync();
         const u32 kept = s_tot;
         for (u32 i = threadIdx.x; i < kept; i += BT) {
             const u32 b = s_bin[i];
@@ -1076,7 +1206,7 @@ fq_jit_gpart(const TIn *__restrict__ col, long long n, const u64 *__restrict__ b
             gp_store(out + (long long)blk * GP_BLK + (o & (GP_BLK - 1)), gp_pack(s_stage[i], vbase, flags));
         }
 #endif
-        __syncthreads();
+        gp_sync();
         for (int b = threadIdx.x; b < P; b += BT) {
             const u32 cnt = s_cnt[b], t = s_fill[b] + cnt;
             if (!cnt) continue;
@@ -1233,7 +1363,7 @@ fq_jit_groupby_bins(const PRow *__restrict__ vals, const u64 *__restrict__ order
     }
     if (flags) atomicOr(&t.hdr[0], flags);
 }
-)";
+)GP";
 
 bool gen_groupby_source(const GroupLaunch &G, int32_t tin, Gen &g, std::string &src, bool cluster = true) {
     const char *TIn = ctype(tin);
@@ -1256,6 +1386,8 @@ bool gen_groupby_source(const GroupLaunch &G, int32_t tin, Gen &g, std::string &
     src += "#define GWAVE " + std::to_string(group_wave_runs()) + "\n";
     src += "#define RANGE_BINS " + std::to_string(G.range_bins ? 1 : 0) + "\n";
     src += "#define GP_NARROW " + std::to_string(G.narrow ? 1 : 0) + "\n";
+    // (range bins only: the hash bins' 72 KB staging leaves no LDS for it)
+    src += "#define GP_PREFETCH " + std::to_string(G.range_bins ? fqc::knob(FQ_TUNE_GROUP_PREFETCH) : 0) + "\n";
     // blocks are 2 KB either way: 256 8-byte rows, or 512 narrow ones (1 KB
     // blocks measured 1.11 -> 1.53 ms per 4.2e8-row partition pass)
     src += "#define GP_BLK " + std::to_string(kPartBlockRows * (G.narrow ? 2 : 1)) + "\n";
@@ -2390,25 +2522,43 @@ std::string device_arch(int dev) {
 fq_status compile(const std::string &src, int dev, Compiled &out, const char *fn_name = "fq_jit_scan") {
     const Rtc &r = rtc();
     const auto t0 = std::chrono::steady_clock::now();
-    hiprtcProgram prog;
-    if (r.create(&prog, src.c_str(), "fq_jit_scan.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS)
-        return fqc::fail(FQ_E_INTERNAL, "hipRTC: cannot create program");
+    const std::string dump = fqc::jit_dump_dir();
+    const std::string dump_path = dump.empty() ? "" : dump + "/fq_jit_" + std::to_string(g_compiled.load() + 1) + ".hip";
+    if (!dump.empty())  // the source before compiling: a compiler that crashes leaves it behind
+        if (FILE *f = fopen(dump_path.c_str(), "w")) {
+            fwrite(src.data(), 1, src.size(), f);
+            fclose(f);
+        }
     const std::string arch = "--offload-arch=" + (dev >= 0 ? device_arch(dev) : std::string("gfx950"));
-    const char *opts[] = {arch.c_str(), "-O3", "-std=c++17"};
-    const hiprtcResult cr = r.compile(prog, 3, opts);
-    if (cr != HIPRTC_SUCCESS) {
+    std::vector<char> code;
+    std::string log;
+    int stage = 0;  // 1: create failed, 2: compile failed (log), 3: code
+    RtcThread::get().run([&] {
+        hiprtcProgram prog;
+        if (r.create(&prog, src.c_str(), "fq_jit_scan.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
+            stage = 1;
+            return;
+        }
+        const char *opts[] = {arch.c_str(), "-O3", "-std=c++17"};
+        if (r.compile(prog, 3, opts) != HIPRTC_SUCCESS) {
+            size_t n = 0;
+            r.log_size(prog, &n);
+            log.assign(n + 1, '\0');
+            r.log(prog, &log[0]);
+            r.destroy(&prog);
+            stage = 2;
+            return;
+        }
         size_t n = 0;
-        r.log_size(prog, &n);
-        std::string log(n + 1, '\0');
-        r.log(prog, &log[0]);
+        r.code_size(prog, &n);
+        code.resize(n);
+        r.code(prog, code.data());
         r.destroy(&prog);
+        stage = 3;
+    });
+    if (stage == 1) return fqc::fail(FQ_E_INTERNAL, "hipRTC: cannot create program");
+    if (stage == 2)
         return fqc::fail(FQ_E_INTERNAL, "hipRTC compile of the fused scan failed: " + log + "\n--- source ---\n" + src);
-    }
-    size_t n = 0;
-    r.code_size(prog, &n);
-    std::vector<char> code(n);
-    r.code(prog, code.data());
-    r.destroy(&prog);
     if (dev >= 0) {
         FQ_HIP_TRY(hipModuleLoadData(&out.mod, code.data()));
         FQ_HIP_TRY(hipModuleGetFunction(&out.fn, out.mod, fn_name));
@@ -2416,17 +2566,11 @@ fq_status compile(const std::string &src, int dev, Compiled &out, const char *fn
     const auto t1 = std::chrono::steady_clock::now();
     g_compile_us += (int64_t)std::chrono::duration_cast<std::chrono::microseconds>(t1 - t0).count();
     g_compiled += 1;
-    if (const std::string d = fqc::jit_dump_dir(); !d.empty()) {
-        const std::string p = d + "/fq_jit_" + std::to_string(g_compiled.load()) + ".hip";
-        if (FILE *f = fopen(p.c_str(), "w")) {
-            fwrite(src.data(), 1, src.size(), f);
-            fclose(f);
-        }
-        if (FILE *f = fopen((p + ".co").c_str(), "wb")) {  // the code object hipRTC produced
+    if (!dump.empty())
+        if (FILE *f = fopen((dump_path + ".co").c_str(), "wb")) {  // the code object hipRTC produced
             fwrite(code.data(), 1, code.size(), f);
             fclose(f);
         }
-    }
     return FQ_OK;
 }
 

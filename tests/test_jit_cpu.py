@@ -4,6 +4,7 @@ gfx950 through fq_jit_prepare (no GPU needed -- the code object is built but
 not loaded).  GPU parity of the compiled kernels against the oracle is in
 tests/test_kernels_gpu.py, which runs every case interpreted and specialised."""
 import ctypes as C
+import os
 
 import pytest
 
@@ -250,3 +251,51 @@ def test_oracle_tree_matches_numpy(i):
     from fq_amd.expr import from_bits
     assert from_bits(st[0].bits, vdt) == max(vals)
     assert from_bits(st[1].bits, vdt) == min(vals)
+
+
+MANY_THREADS = r"""
+import sys, threading
+sys.path.insert(0, sys.argv[1])
+from fq_amd import abi, ops
+from fq_amd.expr import chain, predicate
+U64 = abi.DT_UINT64
+ops.tune_set("GROUP_PREFETCH", 1)  # the partition kernel's inline-asm LDS-DMA path
+errors = []
+
+def compile_shape(j):
+    try:
+        key, kdt = chain(U64, [("+", 1)] * (1 + j % 4) + [("%", 100000)])
+        aggs = [(abi.AGG_COUNT, U64)] + [(abi.AGG_MAX, U64)] * (j // 4 % 4)
+        pred = predicate(U64, [("%", 8)], "<", 3) if j >= 16 else None
+        ops.group_compile_check(U64, aggs, key=key, values=[None] * len(aggs), pred=pred, key_dtype=kdt,
+                                log2_parts=6)
+    except Exception as e:
+        errors.append(e)
+
+for r in range(2):
+    ts = [threading.Thread(target=compile_shape, args=(r * 8 + w,)) for w in range(8)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+assert not errors, errors
+print("compiled", ops.jit_stats()["kernels_compiled"])
+"""
+
+
+def test_compiles_from_many_threads():
+    # hipRTC is loaded into a link-map namespace of its own; compiles issued
+    # from many fresh threads (the engine's workers) crashed the process inside
+    # hipRTC until every call went through its one compiler thread (fq_jit.hip
+    # RtcThread).  16 distinct shapes (key chain length x aggregate count x
+    # predicate), each compiled on a thread of its own, 8 at a time, in a child
+    # process without the comgr cache (cached code objects never reach the
+    # compiler; the namespace's libc reads the environment only when loaded).
+    import subprocess
+    import sys
+    pkg = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "fuse-query_amd")
+    env = dict(os.environ, AMD_COMGR_CACHE="0")
+    r = subprocess.run([sys.executable, "-c", MANY_THREADS, pkg], env=env, capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, (r.returncode, r.stdout[-2000:], r.stderr[-2000:])
+    assert "compiled 16" in r.stdout, r.stdout
