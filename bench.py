@@ -258,8 +258,14 @@ def cpu_baseline_project(sample_rows, threads):
 
 
 def run_project(args, rank, world):
-    """--query p1: fq_filter_project over this rank's resident numbers_mt
-    partitions, outputs in HBM; one step = every partition once."""
+    """--query p1: FilterTransform -> ProjectionTransform over this rank's
+    resident numbers_mt partitions, outputs in HBM; one step = every partition
+    once.  Default path: fq_filter_project_blocks over the partition's
+    10,000-row blocks (the reference filters and projects block by block,
+    transform_filter.rs:38-55 on each numbers_stream.rs block): block b's kept
+    rows at output rows [b * 10,000, + count[b]).  --project-path contiguous:
+    fq_filter_project (one contiguous output per partition, decoupled
+    look-back); the line reports that kernel's time beside the default's."""
     import ctypes as C
 
     from fq_amd._lib import check, lib
@@ -278,9 +284,12 @@ def run_project(args, rank, world):
             raise SystemExit("p1 needs numbers_mt(N) with whole 10,000-row blocks per partition")
         cols.append(ops.numbers_column(b, rows))
         expect.append(project_closed_form(b, e))
+    blocks = args.project_path == "blocks"
     maxr = max(c.len for c in cols)
     outs = [ops.empty_column(maxr, U), ops.empty_column(maxr, U)]
-    ws = ops.Workspace(lib.fq_filter_project_workspace_bytes(maxr))
+    nb_max = -(-maxr // BLOCK_SIZE)
+    counts = ops.Workspace(8 * nb_max)
+    ws = ops.Workspace(max(lib.fq_filter_project_workspace_bytes(maxr), lib.fq_filter_project_blocks_workspace_bytes()))
     pred = predicate(U, [("%", 8)], "<", 3)
     exprs = (abi.fq_expr * 2)(chain(U, [("+", 1)])[0], chain(U, [("/", 2)])[0])
     ptrs = (C.c_void_p * 2)(outs[0].ptr, outs[1].ptr)
@@ -289,21 +298,36 @@ def run_project(args, rank, world):
     sp = C.c_void_p(stream.cuda_stream)
     torch.cuda.synchronize()
     total_rows = sum(c.len for c in cols)
-    log(rank, "p1: %d partitions, %d rows (%.1f GB) resident on rank %d" % (len(cols), total_rows, total_rows * 8 / 1e9,
-                                                                           rank))
+    log(rank, "p1 (%s): %d partitions, %d rows (%.1f GB) resident on rank %d" % (
+        args.project_path, len(cols), total_rows, total_rows * 8 / 1e9, rank))
 
-    def launch(col):
+    def launch(col, use_blocks=blocks):
         c = col.col()
-        check(lib.fq_filter_project(C.byref(c), C.byref(pred), exprs, 2, ptrs, C.byref(kept), ws.ptr, ws.nbytes, sp))
+        if use_blocks:
+            check(lib.fq_filter_project_blocks(C.byref(c), BLOCK_SIZE, C.byref(pred), exprs, 2, ptrs, counts.ptr,
+                                               C.byref(kept), ws.ptr, ws.nbytes, sp))
+        else:
+            check(lib.fq_filter_project(C.byref(c), C.byref(pred), exprs, 2, ptrs, C.byref(kept), ws.ptr, ws.nbytes,
+                                        sp))
         return kept.value
 
-    def wsum(col_out, n):
-        return int(col_out.buf[:n * 8].view(torch.int64).sum().item()) % U64
+    def checked(col, use_blocks=blocks):
+        """(kept, wrapping sum of each output over its valid rows) of one launch:
+        outputs zeroed first, so rows past a block's count add nothing."""
+        for o in outs:
+            o.buf.zero_()
+        k = launch(col, use_blocks)
+        n = col.len if use_blocks else k
+        sums = tuple(int(o.buf[:n * 8].view(torch.int64).sum().item()) % U64 for o in outs)
+        if use_blocks:
+            nb = -(-col.len // BLOCK_SIZE)
+            if int(counts.buf[:8 * nb].view(torch.int64).sum().item()) != k:
+                raise SystemExit("PARITY FAILURE: block counts do not add up to the kept rows")
+        return (k,) + sums
 
     for _ in range(max(args.warmup, 1)):
         for col, exp in zip(cols, expect):
-            k = launch(col)
-            got = (k, wsum(outs[0], k), wsum(outs[1], k))
+            got = checked(col)
             if got != exp:
                 raise SystemExit("PARITY FAILURE: got %r expected %r" % (got, exp))
     log(rank, "result: kept rows and per-column wrapping sums == closed form on every partition")
@@ -328,8 +352,7 @@ def run_project(args, rank, world):
         t = torch.tensor([dt], dtype=torch.float64, device="cuda" if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-    k_last = kept.value
-    if (k_last, wsum(outs[0], k_last), wsum(outs[1], k_last)) != expect[-1]:
+    if checked(cols[-1]) != expect[-1]:
         raise SystemExit("PARITY FAILURE after the timed steps")
     ms = [e0.elapsed_time(e1) for e0, e1, _ in evs]
     avg_ms = sum(ms) / len(ms)
@@ -338,8 +361,32 @@ def run_project(args, rank, world):
     bytes_per_launch = 8 * rows_per_launch + 16 * kept_per_launch
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
     value = n_total * args.steps / dt
+    other = None
+    if rank == 0 and blocks and not args.no_contiguous_ref:
+        # the contiguous-output kernel on the same partition, for reference
+        if checked(cols[0], False) != expect[0]:
+            raise SystemExit("PARITY FAILURE (contiguous path)")
+        cms = []
+        for _ in range(3):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            launch(cols[0], False)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            cms.append(e0.elapsed_time(e1))
+        cb = 8 * cols[0].len + 16 * kept.value
+        other = {"path": "fq_filter_project (one contiguous output per partition, decoupled look-back, fq_jit_pselect)",
+                 "kernel_ms_per_launch": sum(cms) / len(cms),
+                 "frac": cb / (sum(cms) / len(cms) * 1e-3) / 1e9 / HBM_PEAK_GBPS}
     if rank == 0:
-        traffic, traffic_src = latest_pmc_traffic("fq_jit_pselect", "p1", rows_per_launch)
+        kname = "fq_jit_pblocks" if blocks else "fq_jit_pselect"
+        traffic, traffic_src = latest_pmc_traffic(kname, "p1", rows_per_launch)
+        path = ("fq_filter_project_blocks per resident partition: the partition's 10,000-row blocks filtered and "
+                "projected block by block as the reference does (transform_filter.rs:38-55 per numbers_stream.rs "
+                "block), block b's kept rows at output rows [b * 10,000, + count[b]), per-block counts in HBM"
+                if blocks else
+                "fq_filter_project per resident partition: predicate, decoupled look-back, both expressions, one "
+                "contiguous output per partition")
         out = {
             "metric": METRIC, "value": value, "unit": "rows/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,
@@ -347,18 +394,18 @@ def run_project(args, rank, world):
             "vs_baseline_ref": "no published reference number for this query",
             "dtype": "u64", "data": "synthetic: system.numbers_mt iota column (u64), resident in HBM before timing",
             "config": {"workload": sql, "query": "p1", "rows_per_gpu": total_rows, "rows_total": n_total,
-                       "partitions_per_gpu": len(cols), "block_rows": BLOCK_SIZE,
-                       "path": "fq_filter_project per resident partition (the C ABI call of the engine's "
-                               "ProjectionTransform): predicate, decoupled look-back, both expressions, outputs in HBM",
+                       "partitions_per_gpu": len(cols), "block_rows": BLOCK_SIZE, "path": path,
                        "parallelism": "dp%d (numbers_mt partitions sharded)" % world},
             "achieved_hbm_gbps": achieved, "kernel_ms_per_launch": avg_ms, "scan_launches_per_step": len(cols),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel": "fq_jit_pselect (fq_filter_project, hipRTC-specialised), one launch per partition; "
-                                   "algorithmic bytes = 8 B per row read + 16 B per kept row written",
+                         "kernel": "%s (hipRTC-specialised), one launch per partition; algorithmic bytes = 8 B per "
+                                   "row read + 16 B per kept row written" % kname,
                          "bytes_per_launch": bytes_per_launch},
             "result": {"kept_rows_per_step": kept_total // args.steps},
         }
+        if other:
+            out["contiguous_output"] = other
         if world == 1 and not args.no_cpu_baseline:
             try:
                 out["cpu_baseline"] = cpu_baseline_project(int(args.cpu_sample_rows or 1e10), args.cpu_threads)
@@ -434,6 +481,11 @@ def main():
                          "box's 8 threads for c3, ~5 s for p1; 4e9 rows for GROUP BY, a hash insert per row, ~3-10 s)")
     ap.add_argument("--cpu-threads", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--project-path", default="blocks", choices=("blocks", "contiguous"),
+                    help="p1: block-stream output (fq_filter_project_blocks, default) or one contiguous output "
+                         "per partition (fq_filter_project)")
+    ap.add_argument("--no-contiguous-ref", action="store_true",
+                    help="p1: skip timing the contiguous-output kernel beside the block-stream one")
     ap.add_argument("--streams", type=int, default=1,
                     help="device queues the pipes share (FQ_OPT_STREAMS); 1 = the scans run back to back")
     ap.add_argument("--group-chunk-rows", type=int, default=None,

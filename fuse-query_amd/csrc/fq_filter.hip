@@ -369,6 +369,12 @@ size_t fq_filter_workspace_bytes(int64_t len) {
 namespace fqk {
 namespace {
 
+// block b of a block stream with every row kept holds min(B, n - b * B) rows
+__global__ void block_lengths_kernel(int64_t *__restrict__ counts, int64_t nb, int64_t B, int64_t n) {
+    for (int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; b < nb; b += (int64_t)gridDim.x * blockDim.x)
+        counts[b] = b * B + B <= n ? B : n - b * B;
+}
+
 // Workspace of fq_filter_project: [total][flag words: predicate,
 // expressions][kMaxSelectXcds ticket counters, a 128 B line each][one
 // look-back status word per tile].
@@ -468,6 +474,59 @@ fq_status fq_filter_project(const fq_col *col, const fq_pred *pred, const fq_exp
                                     w.ticket, w.flags, w.total)) != FQ_OK)
             return s;
         FQ_HIP_TRY(hipMemcpyAsync(host, w.total, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));  // total + flag words
+    }
+    FQ_HIP_TRY(hipStreamSynchronize(st));
+    const uint32_t pred_flags = (uint32_t)(host[1] & 0xffffffffu), val_flags = (uint32_t)(host[1] >> 32);
+    if ((s = flag_error(pred_flags)) != FQ_OK) return s;  // FilterTransform runs first
+    if ((s = flag_error(val_flags)) != FQ_OK) return s;
+    *out_len = (int64_t)host[0];
+    return FQ_OK;
+}
+
+size_t fq_filter_project_blocks_workspace_bytes(void) { return 2 * sizeof(uint64_t); }  // total, flag words
+
+fq_status fq_filter_project_blocks(const fq_col *col, int64_t block_rows, const fq_pred *pred, const fq_expr *values,
+                                   int32_t n_out, void *const *d_out, int64_t *d_counts, int64_t *out_len, void *d_ws,
+                                   size_t ws_bytes, void *stream) {
+    using namespace fqk;
+    static_assert(FQ_PROJECT_MIN_BLOCK_ROWS == kProjectBlockTile, "the ABI's minimum block is the kernel's tile");
+    if (!out_len) return fqc::fail(FQ_E_INVALID, "fq_filter_project_blocks: NULL out_len");
+    *out_len = 0;
+    if (block_rows < FQ_PROJECT_MIN_BLOCK_ROWS)
+        return fqc::fail(FQ_E_INVALID, "fq_filter_project_blocks: block_rows below FQ_PROJECT_MIN_BLOCK_ROWS");
+    ProjLaunch P;
+    fq_status s = lower_projection(col, pred, values, n_out, d_out, stream, P);
+    if (s != FQ_OK) return s;
+    if (n_out < 1) return fqc::fail(FQ_E_INVALID, "fq_filter_project_blocks: no outputs");
+    if (!jit_project_available())
+        return fqc::fail(FQ_E_UNSUPPORTED, "fq_filter_project_blocks: hipRTC unavailable or the JIT is off");
+    if ((s = jit_project_prepare(col->dtype, P)) != FQ_OK) return s;
+    const int64_t n = col->len;
+    if (n == 0) return FQ_OK;
+    if (!d_counts) return fqc::fail(FQ_E_INVALID, "fq_filter_project_blocks: NULL block counts");
+    if (!d_ws || ws_bytes < fq_filter_project_blocks_workspace_bytes())
+        return fqc::fail(FQ_E_INVALID, "fq_filter_project_blocks: workspace too small");
+    uint64_t *const total = (uint64_t *)d_ws;
+    uint32_t *const flags = (uint32_t *)(total + 1);
+    hipStream_t st = P.stream;
+    uint64_t local[2] = {0, 0};
+    uint64_t *const pinned = fqc::host_staging();
+    uint64_t *const host = pinned ? pinned : local;  // kept rows, flag words
+    host[0] = host[1] = 0;
+    const int64_t nb = (n + block_rows - 1) / block_rows;
+    FQ_HIP_TRY(hipMemsetAsync(d_ws, 0, fq_filter_project_blocks_workspace_bytes(), st));
+    if (P.pred.kind == FQ_PRED_NONE) {  // every row kept: outputs in place, counts = block lengths
+        if ((s = jit_project_map(col->dtype, P, flags + 1)) != FQ_OK) return s;
+        hipLaunchKernelGGL(block_lengths_kernel, dim3((unsigned)std::min<int64_t>((nb + 255) / 256, 4096)), dim3(256), 0,
+                           st, d_counts, nb, block_rows, n);
+        FQ_HIP_TRY(hipGetLastError());
+        FQ_HIP_TRY(hipMemcpyAsync(&host[1], flags, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+        host[0] = (uint64_t)n;
+    } else {
+        if ((s = jit_project_blocks(col->dtype, P, block_rows, P.pred.kind == FQ_PRED_BITMAP ? P.pred.bitmap : nullptr,
+                                    d_counts, flags, total)) != FQ_OK)
+            return s;
+        FQ_HIP_TRY(hipMemcpyAsync(host, total, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     }
     FQ_HIP_TRY(hipStreamSynchronize(st));
     const uint32_t pred_flags = (uint32_t)(host[1] & 0xffffffffu), val_flags = (uint32_t)(host[1] >> 32);

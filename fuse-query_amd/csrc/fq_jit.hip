@@ -2060,6 +2060,138 @@ std::string proj_shape_key(const ProjLaunch &P, int32_t tin, int dev) {
     return k;
 }
 
+// fq_jit_pblocks (fq_filter_project_blocks): Filter -> Projection over a
+// stream of DataBlocks of B rows, the way the reference runs both transforms
+// (ExpressionStream applies FilterTransform::expression_executor to each
+// numbers block, transform_filter.rs:38-55, numbers_stream.rs:29, then
+// transform_projection.rs:45-56): block b's kept rows go, in order, to output
+// rows [b * B, b * B + count[b]) -- an output block starts where its input
+// block does, so no block's offsets depend on another block's count and no
+// workgroup waits on another (no ticket, no look-back: fq_jit_pselect's
+// contiguous output needs both).  A workgroup owns a contiguous run of whole
+// blocks ([nb * w / G, nb * (w + 1) / G)) and walks it in full tiles of 8,192
+// rows that ignore block edges; B >= the tile, so a tile holds at most one
+// block edge: rows before it go to the open block at its running count
+// (carry), rows after it start the next block.  The edge's in-tile rank comes
+// from the tile's ballots and exclusive group offsets in LDS (double-buffered
+// by tile parity: two barriers per tile).
+std::string gen_project_blocks_kernel(bool bitmap_pred) {
+    std::string s = R"(
+#define PB_THREADS 256
+#define PB_ROWS 32
+#define PB_WAVES (PB_THREADS / 64)
+#define PB_TILE (PB_THREADS * PB_ROWS)
+#define PB_NE (PB_ROWS * PB_WAVES)
+struct PbShared {
+    u64 bal[2][PB_NE];      // ballot of 64-row group i = k * PB_WAVES + wave (tile rows [64 i, 64 i + 64))
+    u32 off[2][PB_NE + 1];  // exclusive in-tile offset of each group; [PB_NE]: the tile's kept rows
+};
+extern "C" __global__ void __launch_bounds__(PB_THREADS)
+fq_jit_pblocks(const TIn *__restrict__ col, long long n, long long B, Consts c, const u64 *__restrict__ bm, Outs o,
+               long long *__restrict__ counts, u32 *__restrict__ fl, unsigned long long *__restrict__ total) {
+    __shared__ PbShared sh;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const long long nb = (n + B - 1) / B;
+    const long long b_lo = nb * (long long)blockIdx.x / gridDim.x, b_hi = nb * ((long long)blockIdx.x + 1) / gridDim.x;
+    const long long end = b_hi * B < n ? b_hi * B : n;
+    long long cur = b_lo;  // the open block
+    u64 carry = 0, kept = 0;  // its kept rows so far; the workgroup's
+    u32 pflags = 0, vflags = 0;
+    const u64 lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    int par = 0;
+    for (long long r0 = b_lo * B; r0 < end; r0 += PB_TILE, par ^= 1) {
+        u64 *__restrict__ bal = sh.bal[par];
+        u32 *__restrict__ off = sh.off[par];
+        TIn x[PB_ROWS];
+        const long long rt = r0 + tid;
+        if (r0 + PB_TILE <= end) {
+#pragma unroll
+            for (int k = 0; k < PB_ROWS; ++k) x[k] = __builtin_nontemporal_load(col + rt + k * PB_THREADS);
+        } else {
+#pragma unroll
+            for (int k = 0; k < PB_ROWS; ++k) {
+                const long long row = rt + k * PB_THREADS;
+                x[k] = row < end ? __builtin_nontemporal_load(col + row) : TIn(0);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < PB_ROWS; ++k) {
+            const long long row = rt + k * PB_THREADS;
+            const u32 live = row < end ? 1u : 0u;
+)";
+    s += bitmap_pred ? "            const bool p = live && ((bm[row >> 6] >> (row & 63)) & 1ull);\n"
+                       "            (void)c;\n"
+                     : "            const bool p = fq_pred(x[k], c, pflags, live) && live;\n";
+    s += R"(
+            const u64 b = __ballot(p);
+            if (lane == 0) {
+                bal[k * PB_WAVES + wave] = b;
+                off[k * PB_WAVES + wave] = (u32)__popcll(b);
+            }
+        }
+        __syncthreads();
+        if (wave == 0) {
+            constexpr int PER = (PB_NE + 63) / 64;
+            u32 cv[PER], tot = 0;
+#pragma unroll
+            for (int q = 0; q < PER; ++q) {
+                cv[q] = off[lane * PER + q];
+                tot += cv[q];
+            }
+            u32 incl = tot;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const u32 v = (u32)__shfl_up((int)incl, d, 64);
+                if (lane >= d) incl += v;
+            }
+            u32 run = incl - tot;
+#pragma unroll
+            for (int q = 0; q < PER; ++q) {
+                off[lane * PER + q] = run;
+                run += cv[q];
+            }
+            if (lane == 63) off[PB_NE] = incl;
+        }
+        __syncthreads();
+        const u32 tot = off[PB_NE];
+        // the open block's edge: inside the tile (or at its end) when e <= PB_TILE
+        const long long bnd = (cur + 1) * B < n ? (cur + 1) * B : n;
+        const long long e = bnd - r0;
+        u32 re = tot;  // kept rows of the tile before the edge
+        if (e < PB_TILE) {
+            const int g = (int)(e >> 6), bit = (int)(e & 63);
+            re = off[g] + (u32)__popcll(bal[g] & ((1ull << bit) - 1ull));
+        }
+        // kept rows before the edge have in-tile ranks < re, the rest >= re
+        const long long before = cur * B + (long long)carry;  // output row of in-tile rank 0
+        const long long after = (cur + 1) * B - (long long)re;  // ... for ranks past the edge
+#pragma unroll
+        for (int k = 0; k < PB_ROWS; ++k) {
+            const u64 b = bal[k * PB_WAVES + wave];
+            if ((b >> lane) & 1ull) {
+                const u32 rank = off[k * PB_WAVES + wave] + (u32)__popcll(b & lt);
+                fq_put(x[k], c, vflags, 1u, o, (rank < re ? before : after) + (long long)rank);
+            }
+        }
+        kept += tot;
+        if (e <= PB_TILE) {
+            if (tid == 0) counts[cur] = (long long)(carry + re);
+            carry = tot - re;
+            ++cur;
+        } else {
+            carry += tot;
+        }
+    }
+    pflags = wave_or(pflags);
+    vflags = wave_or(vflags);
+    if (lane == 0 && pflags) atomicOr(fl, pflags);
+    if (lane == 0 && vflags) atomicOr(fl + 1, vflags);
+    if (tid == 0 && kept) atomicAdd(total, (unsigned long long)kept);
+}
+)";
+    return s;
+}
+
 bool gen_project_source(const ProjLaunch &P, int32_t tin, int dev, Gen &g, std::string &src) {
     const char *TIn = ctype(tin);
     if (!TIn || P.n_out < 1 || P.n_out > FQ_MAX_PROJECT) return false;
@@ -2497,6 +2629,7 @@ fq_jit_pmap(const TIn *__restrict__ col, long long n, Consts c, Outs o, int alig
     if ((threadIdx.x & 63) == 0 && flags) atomicOr(fl, flags);
 }
 )";
+    src += gen_project_blocks_kernel(P.pred.kind == FQ_PRED_BITMAP);
     return true;
 }
 
@@ -2793,7 +2926,7 @@ fq_status jit_groupby_partitioned(int32_t col_dtype, const GroupLaunch &G, const
 namespace {
 
 struct ProjKernels {
-    hipFunction_t bits = nullptr, scatter = nullptr, map = nullptr;
+    hipFunction_t bits = nullptr, scatter = nullptr, map = nullptr, blocks = nullptr;
     hipModule_t mod = nullptr;
 };
 std::unordered_map<std::string, ProjKernels> g_proj_cache;
@@ -2826,6 +2959,7 @@ fq_status get_proj_kernels(int32_t col_dtype, const ProjLaunch &P, ProjKernels *
         k.mod = c.mod;
         FQ_HIP_TRY(hipModuleGetFunction(&k.bits, c.mod, "fq_jit_pbits"));
         FQ_HIP_TRY(hipModuleGetFunction(&k.map, c.mod, "fq_jit_pmap"));
+        FQ_HIP_TRY(hipModuleGetFunction(&k.blocks, c.mod, "fq_jit_pblocks"));
         it = g_proj_cache.emplace(key, k).first;
     }
     *out = it->second;
@@ -2924,6 +3058,51 @@ fq_status jit_project_select(int32_t col_dtype, const ProjLaunch &P, const uint6
         }
         (void)hipGetLastError();
     }
+    return FQ_OK;
+}
+
+fq_status jit_project_blocks(int32_t col_dtype, const ProjLaunch &P, int64_t block_rows, const uint64_t *d_bitmap,
+                             int64_t *d_counts, uint32_t *d_flags, uint64_t *d_total) {
+    ProjKernels k;
+    fq_status s = get_proj_kernels(col_dtype, P, &k);
+    if (s != FQ_OK || !k.blocks || P.n == 0) return s;
+    if (block_rows < kProjectBlockTile) return fqc::fail(FQ_E_INVALID, "jit_project_blocks: block_rows below the tile");
+    HostProjConsts hc;
+    pack_proj_consts(P, hc);
+    struct {
+        void *p[FQ_MAX_PROJECT];
+    } outs;
+    for (int j = 0; j < FQ_MAX_PROJECT; ++j) outs.p[j] = j < P.n_out ? P.out[j] : nullptr;
+    const void *col = P.col;
+    long long n = P.n, B = block_rows;
+    const int64_t nb = (P.n + block_rows - 1) / block_rows;
+    void *args[] = {&col, &n, &B, &hc, &d_bitmap, &outs, &d_counts, &d_flags, &d_total};
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipGetLastError();
+    // one wave of workgroups (each owns an equal run of whole blocks): a grid
+    // above the resident capacity would leave a second, partial wave
+    static std::mutex occ_mu;
+    static std::unordered_map<hipFunction_t, int> occ_cache;
+    int occ = 0;
+    {
+        std::lock_guard<std::mutex> lk(occ_mu);
+        auto it = occ_cache.find(k.blocks);
+        if (it != occ_cache.end()) {
+            occ = it->second;
+        } else {
+            if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k.blocks, kProjectBlockThreads, 0) != hipSuccess)
+                occ = 1;
+            (void)hipGetLastError();
+            occ = std::max(1, occ);
+            occ_cache.emplace(k.blocks, occ);
+        }
+    }
+    const int wg_per_cu = (int)fqc::knob(FQ_TUNE_SELECT_BLOCKS_WG_PER_CU);
+    const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(nb, (int64_t)cus * std::min(wg_per_cu, occ)));
+    FQ_HIP_TRY(hipModuleLaunchKernel(k.blocks, (unsigned)grid, 1, 1, kProjectBlockThreads, 1, 1, 0, P.stream, args,
+                                     nullptr));
+    g_jit_launches += 1;
     return FQ_OK;
 }
 

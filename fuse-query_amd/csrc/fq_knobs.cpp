@@ -44,6 +44,8 @@ constexpr KnobDef kDefs[FQ_TUNE_COUNT] = {
     {1, 1, 8, 1, false},         // GROUP_WG_PER_CU
     {1, 0, 1, 1, false},         // GROUP_RANGE_BINS
     {1, 0, 1, 1, false},         // GROUP_NARROW
+    {8, 1, 16, 1, false},        // SELECT_BLOCKS_WG_PER_CU
+    {0, 0, 3, 1, false},         // GROUP_PREFETCH
 };
 
 std::atomic<int64_t> g_val[FQ_TUNE_COUNT] = {};

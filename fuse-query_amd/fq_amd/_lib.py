@@ -22,7 +22,8 @@ GPU_SYMBOLS = [
     "fq_group_table_extract", "fq_logic", "fq_filter_project_workspace_bytes", "fq_filter_project",
     "fq_predicate_bitmap", "fq_group_partition_workspace_bytes", "fq_group_aggregate_partitioned",
     "fq_group_dense_keys", "fq_group_table_merge", "fq_tune_set", "fq_tune_get", "fq_tune_reset",
-    "fq_tune_select_counters", "fq_tune_jit_dump_dir",
+    "fq_tune_select_counters", "fq_tune_jit_dump_dir", "fq_filter_project_blocks_workspace_bytes",
+    "fq_filter_project_blocks",
 ]
 
 
@@ -79,6 +80,9 @@ _protos = {
     "fq_filter_project_workspace_bytes": (C.c_size_t, [C.c_int64]),
     "fq_filter_project": (C.c_int32, [P(abi.fq_col), P(abi.fq_pred), P(abi.fq_expr), C.c_int32, P(vp),
                                       P(C.c_int64), vp, C.c_size_t, vp]),
+    "fq_filter_project_blocks_workspace_bytes": (C.c_size_t, []),
+    "fq_filter_project_blocks": (C.c_int32, [P(abi.fq_col), C.c_int64, P(abi.fq_pred), P(abi.fq_expr), C.c_int32,
+                                             P(vp), vp, P(C.c_int64), vp, C.c_size_t, vp]),
     "fq_predicate_bitmap": (C.c_int32, [P(abi.fq_col), P(abi.fq_pred), vp, vp, vp]),
     "fq_group_table_bytes": (C.c_size_t, [C.c_int64, C.c_int32]),
     "fq_group_table_init": (C.c_int32, [P(abi.fq_group_table), vp]),

@@ -238,6 +238,35 @@ def filter_project(col, pred, values, stream=None):
     return outs
 
 
+def filter_project_blocks(col, block_rows, pred, values, stream=None):
+    """FilterTransform -> ProjectionTransform over a stream of DataBlocks of
+    block_rows rows (fq_filter_project_blocks): -> ([DeviceColumn of col.len
+    rows per output], per-block kept counts as an int64 numpy array).  Block
+    b's kept rows are rows [b * block_rows, + counts[b]) of each output."""
+    require_gpu()
+    n_out = len(values)
+    exprs = (abi.fq_expr * n_out)()
+    outs = []
+    for j, v in enumerate(values):
+        if v is None:
+            v = abi.fq_expr()
+            v.n_steps = 0
+            v.out_dtype = col.dtype
+        exprs[j] = v
+        outs.append(empty_column(col.len, v.out_dtype))
+    ptrs = (C.c_void_p * max(n_out, 1))(*[o.ptr for o in outs])
+    nb = -(-col.len // block_rows) if block_rows > 0 else 0
+    counts = Workspace(max(8 * nb, 8))
+    ws = Workspace(lib.fq_filter_project_blocks_workspace_bytes())
+    n = C.c_int64(0)
+    c = col.col()
+    check(lib.fq_filter_project_blocks(C.byref(c), block_rows, C.byref(pred) if pred is not None else None, exprs,
+                                       n_out, ptrs, counts.ptr, C.byref(n), ws.ptr, ws.nbytes, _stream(stream)))
+    cnt = counts.buf[:8 * nb].view(torch.int64).cpu().numpy() if nb else np.zeros(0, np.int64)
+    assert int(cnt.sum()) == n.value
+    return outs, cnt
+
+
 def predicate_bitmap(col, pred, stream=None):
     """FilterTransform's predicate as a Boolean column (fq_predicate_bitmap)."""
     require_gpu()

@@ -289,6 +289,27 @@ fq_status fq_filter_compact(const fq_col *in, const uint64_t *d_bitmap, void *d_
 size_t fq_filter_project_workspace_bytes(int64_t len);
 fq_status fq_filter_project(const fq_col *col, const fq_pred *pred, const fq_expr *values, int32_t n_out,
                             void *const *d_out, int64_t *out_len, void *d_ws, size_t ws_bytes, void *stream);
+/* ---- FilterTransform -> ProjectionTransform over a stream of DataBlocks ----
+ * The reference runs both transforms block by block: ExpressionStream applies
+ * FilterTransform::expression_executor (transform_filter.rs:38-55) to every
+ * block the numbers stream yields (numbers_stream.rs:29-48, 10,000 rows), then
+ * ProjectionTransform (transform_projection.rs:45-56) to each filtered block.
+ * This is that loop over a batch of blocks in one call: `col` holds
+ * ceil(len / block_rows) blocks of block_rows consecutive rows (the last may
+ * be short); block b's kept rows are written in order to
+ * d_out[j][b * block_rows + r] for r < d_counts[b] (device int64, one per
+ * block): each output block starts where its input block does, so no block
+ * waits on another's count.  d_out[j] must hold len rows; rows of a block past
+ * its count are left as they were.  block_rows >= FQ_PROJECT_MIN_BLOCK_ROWS
+ * (the kernel's tile); blocks are independent, so a call runs on up to
+ * ceil(len / block_rows) workgroups.  *out_len = rows kept over all blocks.
+ * Predicate kinds, expressions and the error order are fq_filter_project's.
+ * Synchronises `stream`.                                                    */
+#define FQ_PROJECT_MIN_BLOCK_ROWS 8192
+size_t fq_filter_project_blocks_workspace_bytes(void);
+fq_status fq_filter_project_blocks(const fq_col *col, int64_t block_rows, const fq_pred *pred,
+                                   const fq_expr *values, int32_t n_out, void *const *d_out, int64_t *d_counts,
+                                   int64_t *out_len, void *d_ws, size_t ws_bytes, void *stream);
 /* FilterTransform's predicate alone as a Boolean column: LSB-first bitmap of
  * ceil(len/64) words, bits past len cleared (one kernel instead of one
  * fq_arith per expression node plus fq_compare).  d_flag: 4 bytes of device
@@ -367,7 +388,9 @@ fq_status fq_jit_prepare(const fq_col *col, int64_t block_rows, const fq_pred *p
 #define FQ_TUNE_GROUP_WG_PER_CU 22   /* GROUP BY LDS kernel workgroups per CU: 1 (1..8)           */
 #define FQ_TUNE_GROUP_RANGE_BINS 23  /* partitioned GROUP BY: range bins for `% d` keys, 1 (0/1) */
 #define FQ_TUNE_GROUP_NARROW 24      /* partitioned GROUP BY: honour FQ_GROUP_NARROW_ROWS, 1 (0/1) */
-#define FQ_TUNE_COUNT 25
+#define FQ_TUNE_SELECT_BLOCKS_WG_PER_CU 25 /* block-stream filter+projection workgroups per CU, 8 (1..16) */
+#define FQ_TUNE_GROUP_PREFETCH 26     /* partition kernel: next tile by LDS DMA, 0 (0..3; experimental) */
+#define FQ_TUNE_COUNT 27
 /* FQ_E_INVALID for an unknown knob or a value outside the knob's set */
 fq_status fq_tune_set(int32_t knob, int64_t value);
 /* the knob's current value; -1 for an unknown knob */
