@@ -483,7 +483,7 @@ fq_status fq_filter_project(const fq_col *col, const fq_pred *pred, const fq_exp
     return FQ_OK;
 }
 
-size_t fq_filter_project_blocks_workspace_bytes(void) { return 2 * sizeof(uint64_t); }  // total, flag words
+size_t fq_filter_project_blocks_workspace_bytes(void) { return 3 * sizeof(uint64_t); }  // total, flags, ticket
 
 fq_status fq_filter_project_blocks(const fq_col *col, int64_t block_rows, const fq_pred *pred, const fq_expr *values,
                                    int32_t n_out, void *const *d_out, int64_t *d_counts, int64_t *out_len, void *d_ws,
@@ -524,7 +524,7 @@ fq_status fq_filter_project_blocks(const fq_col *col, int64_t block_rows, const 
         host[0] = (uint64_t)n;
     } else {
         if ((s = jit_project_blocks(col->dtype, P, block_rows, P.pred.kind == FQ_PRED_BITMAP ? P.pred.bitmap : nullptr,
-                                    d_counts, flags, total)) != FQ_OK)
+                                    d_counts, flags, total, (uint32_t *)(total + 2))) != FQ_OK)
             return s;
         FQ_HIP_TRY(hipMemcpyAsync(host, total, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     }

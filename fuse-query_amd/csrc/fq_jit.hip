@@ -2036,7 +2036,8 @@ int select_xcds(int dev) {
 std::string proj_shape_key(const ProjLaunch &P, int32_t tin, int dev) {
     std::string k = "PROJ" + std::to_string(select_threads()) + "x" + std::to_string(select_rows_per_thread()) + "s" +
                     std::to_string(select_sleep()) + "v" + std::to_string(select_variant()) + "w" + std::to_string(select_lbw()) + "g" + std::to_string(select_debug()) + "n" +
-                    std::to_string(select_xcds(dev));
+                    std::to_string(select_xcds(dev)) + "r" + std::to_string(fqc::knob(FQ_TUNE_SELECT_BLOCKS_RUN)) + "d" +
+                    std::to_string(fqc::knob(FQ_TUNE_SELECT_BLOCKS_DRAW));
     auto put = [&k](int32_t v) { k.append(reinterpret_cast<const char *>(&v), sizeof v); };
     put(dev);
     put(tin);
@@ -2076,29 +2077,57 @@ std::string proj_shape_key(const ProjLaunch &P, int32_t tin, int dev) {
 // from the tile's ballots and exclusive group offsets in LDS (double-buffered
 // by tile parity: two barriers per tile).
 std::string gen_project_blocks_kernel(bool bitmap_pred) {
-    std::string s = R"(
+    std::string s = "#define PB_RUN " + std::to_string(fqc::knob(FQ_TUNE_SELECT_BLOCKS_RUN)) + "\n#define PB_DRAW " +
+                    std::to_string(fqc::knob(FQ_TUNE_SELECT_BLOCKS_DRAW)) + "\n";
+    s += R"(
 #define PB_THREADS 256
 #define PB_ROWS 32
 #define PB_WAVES (PB_THREADS / 64)
 #define PB_TILE (PB_THREADS * PB_ROWS)
 #define PB_NE (PB_ROWS * PB_WAVES)
+#ifndef PB_RUN
+#define PB_RUN 0
+#endif
 struct PbShared {
     u64 bal[2][PB_NE];      // ballot of 64-row group i = k * PB_WAVES + wave (tile rows [64 i, 64 i + 64))
     u32 off[2][PB_NE + 1];  // exclusive in-tile offset of each group; [PB_NE]: the tile's kept rows
 };
 extern "C" __global__ void __launch_bounds__(PB_THREADS)
 fq_jit_pblocks(const TIn *__restrict__ col, long long n, long long B, Consts c, const u64 *__restrict__ bm, Outs o,
-               long long *__restrict__ counts, u32 *__restrict__ fl, unsigned long long *__restrict__ total) {
+               long long *__restrict__ counts, u32 *__restrict__ fl, unsigned long long *__restrict__ total,
+               u32 *__restrict__ ticket) {
     __shared__ PbShared sh;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const long long nb = (n + B - 1) / B;
-    const long long b_lo = nb * (long long)blockIdx.x / gridDim.x, b_hi = nb * ((long long)blockIdx.x + 1) / gridDim.x;
-    const long long end = b_hi * B < n ? b_hi * B : n;
-    long long cur = b_lo;  // the open block
-    u64 carry = 0, kept = 0;  // its kept rows so far; the workgroup's
+    u64 kept = 0;  // the workgroup's kept rows
     u32 pflags = 0, vflags = 0;
     const u64 lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     int par = 0;
+#if PB_RUN && PB_DRAW
+    // runs of PB_RUN blocks drawn in order: the runs in flight are adjacent
+    __shared__ long long s_run;
+    const long long nruns = (nb + PB_RUN - 1) / PB_RUN;
+    for (;;) {
+        if (tid == 0) s_run = (long long)atomicAdd(ticket, 1u);
+        __syncthreads();
+        const long long run = s_run;
+        if (run >= nruns) break;
+        const long long b_lo = run * PB_RUN, b_hi = b_lo + PB_RUN < nb ? b_lo + PB_RUN : nb;
+#elif PB_RUN
+    // runs of PB_RUN blocks dealt round-robin: the runs in flight are adjacent
+    (void)ticket;
+    const long long nruns = (nb + PB_RUN - 1) / PB_RUN;
+    for (long long run = blockIdx.x; run < nruns; run += gridDim.x) {
+        const long long b_lo = run * PB_RUN, b_hi = b_lo + PB_RUN < nb ? b_lo + PB_RUN : nb;
+#else
+    // one contiguous run of whole blocks per workgroup
+    (void)ticket;
+    {
+        const long long b_lo = nb * (long long)blockIdx.x / gridDim.x, b_hi = nb * ((long long)blockIdx.x + 1) / gridDim.x;
+#endif
+    const long long end = b_hi * B < n ? b_hi * B : n;
+    long long cur = b_lo;  // the open block
+    u64 carry = 0;         // its kept rows so far
     for (long long r0 = b_lo * B; r0 < end; r0 += PB_TILE, par ^= 1) {
         u64 *__restrict__ bal = sh.bal[par];
         u32 *__restrict__ off = sh.off[par];
@@ -2181,6 +2210,7 @@ fq_jit_pblocks(const TIn *__restrict__ col, long long n, long long B, Consts c, 
         } else {
             carry += tot;
         }
+    }
     }
     pflags = wave_or(pflags);
     vflags = wave_or(vflags);
@@ -3062,7 +3092,7 @@ fq_status jit_project_select(int32_t col_dtype, const ProjLaunch &P, const uint6
 }
 
 fq_status jit_project_blocks(int32_t col_dtype, const ProjLaunch &P, int64_t block_rows, const uint64_t *d_bitmap,
-                             int64_t *d_counts, uint32_t *d_flags, uint64_t *d_total) {
+                             int64_t *d_counts, uint32_t *d_flags, uint64_t *d_total, uint32_t *d_ticket) {
     ProjKernels k;
     fq_status s = get_proj_kernels(col_dtype, P, &k);
     if (s != FQ_OK || !k.blocks || P.n == 0) return s;
@@ -3076,7 +3106,7 @@ fq_status jit_project_blocks(int32_t col_dtype, const ProjLaunch &P, int64_t blo
     const void *col = P.col;
     long long n = P.n, B = block_rows;
     const int64_t nb = (P.n + block_rows - 1) / block_rows;
-    void *args[] = {&col, &n, &B, &hc, &d_bitmap, &outs, &d_counts, &d_flags, &d_total};
+    void *args[] = {&col, &n, &B, &hc, &d_bitmap, &outs, &d_counts, &d_flags, &d_total, &d_ticket};
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     (void)hipGetLastError();
@@ -3099,7 +3129,9 @@ fq_status jit_project_blocks(int32_t col_dtype, const ProjLaunch &P, int64_t blo
         }
     }
     const int wg_per_cu = (int)fqc::knob(FQ_TUNE_SELECT_BLOCKS_WG_PER_CU);
-    const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(nb, (int64_t)cus * std::min(wg_per_cu, occ)));
+    const int64_t run = fqc::knob(FQ_TUNE_SELECT_BLOCKS_RUN);
+    const int64_t units = run > 0 ? (nb + run - 1) / run : nb;
+    const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(units, (int64_t)cus * std::min(wg_per_cu, occ)));
     FQ_HIP_TRY(hipModuleLaunchKernel(k.blocks, (unsigned)grid, 1, 1, kProjectBlockThreads, 1, 1, 0, P.stream, args,
                                      nullptr));
     g_jit_launches += 1;

@@ -46,6 +46,8 @@ constexpr KnobDef kDefs[FQ_TUNE_COUNT] = {
     {1, 0, 1, 1, false},         // GROUP_NARROW
     {8, 1, 16, 1, false},        // SELECT_BLOCKS_WG_PER_CU
     {0, 0, 3, 1, false},         // GROUP_PREFETCH
+    {1, 0, 4096, 1, false},      // SELECT_BLOCKS_RUN
+    {1, 0, 1, 1, false},         // SELECT_BLOCKS_DRAW
 };
 
 std::atomic<int64_t> g_val[FQ_TUNE_COUNT] = {};

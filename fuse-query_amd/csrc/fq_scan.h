@@ -171,11 +171,11 @@ fq_status jit_project_select(int32_t col_dtype, const ProjLaunch &P, const uint6
 // stream of DataBlocks of block_rows rows (fq_filter_project_blocks): block b's
 // kept rows -> output rows [b * block_rows, + d_counts[b]); tiles of
 // kProjectBlockTile rows (kProjectBlockThreads threads), block_rows >= the tile;
-// d_flags / *d_total as jit_project_select (zeroed by the caller)
+// d_flags / *d_total / *d_ticket as jit_project_select (zeroed by the caller)
 constexpr int kProjectBlockThreads = 256;
 constexpr int64_t kProjectBlockTile = 256 * 32;
 fq_status jit_project_blocks(int32_t col_dtype, const ProjLaunch &P, int64_t block_rows, const uint64_t *d_bitmap,
-                             int64_t *d_counts, uint32_t *d_flags, uint64_t *d_total);
+                             int64_t *d_counts, uint32_t *d_flags, uint64_t *d_total, uint32_t *d_ticket);
 // no predicate: every row -> the n_out outputs
 fq_status jit_project_map(int32_t col_dtype, const ProjLaunch &P, uint32_t *d_flag);
 // hipRTC loadable and the policy not FQ_JIT_OFF
