@@ -2037,7 +2037,8 @@ std::string proj_shape_key(const ProjLaunch &P, int32_t tin, int dev) {
     std::string k = "PROJ" + std::to_string(select_threads()) + "x" + std::to_string(select_rows_per_thread()) + "s" +
                     std::to_string(select_sleep()) + "v" + std::to_string(select_variant()) + "w" + std::to_string(select_lbw()) + "g" + std::to_string(select_debug()) + "n" +
                     std::to_string(select_xcds(dev)) + "r" + std::to_string(fqc::knob(FQ_TUNE_SELECT_BLOCKS_RUN)) + "d" +
-                    std::to_string(fqc::knob(FQ_TUNE_SELECT_BLOCKS_DRAW));
+                    std::to_string(fqc::knob(FQ_TUNE_SELECT_BLOCKS_DRAW)) + "b" + std::to_string(fqc::knob(FQ_TUNE_SELECT_BLOCKS_ROWS)) +
+                    "t" + std::to_string(fqc::knob(FQ_TUNE_SELECT_NT));
     auto put = [&k](int32_t v) { k.append(reinterpret_cast<const char *>(&v), sizeof v); };
     put(dev);
     put(tin);
@@ -2061,41 +2062,77 @@ std::string proj_shape_key(const ProjLaunch &P, int32_t tin, int dev) {
     return k;
 }
 
-// fq_jit_pblocks (fq_filter_project_blocks): Filter -> Projection over a
-// stream of DataBlocks of B rows, the way the reference runs both transforms
-// (ExpressionStream applies FilterTransform::expression_executor to each
-// numbers block, transform_filter.rs:38-55, numbers_stream.rs:29, then
+// fq_jit_pblocks (fq_filter_project_blocks): Filter ->
+// Projection over a stream of DataBlocks of B rows, the way the reference runs
+// both transforms (ExpressionStream applies FilterTransform::expression_executor
+// to each numbers block, transform_filter.rs:38-55, numbers_stream.rs:29, then
 // transform_projection.rs:45-56): block b's kept rows go, in order, to output
 // rows [b * B, b * B + count[b]) -- an output block starts where its input
 // block does, so no block's offsets depend on another block's count and no
-// workgroup waits on another (no ticket, no look-back: fq_jit_pselect's
-// contiguous output needs both).  A workgroup owns a contiguous run of whole
-// blocks ([nb * w / G, nb * (w + 1) / G)) and walks it in full tiles of 8,192
-// rows that ignore block edges; B >= the tile, so a tile holds at most one
-// block edge: rows before it go to the open block at its running count
-// (carry), rows after it start the next block.  The edge's in-tile rank comes
-// from the tile's ballots and exclusive group offsets in LDS (double-buffered
-// by tile parity: two barriers per tile).
+// workgroup waits on another (no look-back: fq_jit_pselect's contiguous output
+// needs one).  Workgroups draw runs of PB_RUN whole blocks from a counter, so
+// the runs in flight are adjacent (one static range per workgroup, or runs
+// dealt round-robin, measured 7-10 % slower: profiles/r03_s3_blocks_sweeps.txt),
+// and walk a run in tiles of PB_THREADS x PB_ROWS rows that ignore block
+// edges; B >= the tile, so a tile holds at most one block edge: rows before it
+// go to the open block at its running count (carry), rows after it start the
+// next block.  Kept rows before the edge are exactly those of in-tile rank <
+// re, the edge's rank, read from the tile's ballots and exclusive group
+// offsets in LDS (double-buffered by tile parity: two barriers per tile).
+// Outputs are written with nontemporal stores (PB_NT; 3.42 -> 3.12 ms per
+// 10 GB, no change for the look-back kernel).  16-byte row-pair loads (two
+// ballots per 128 rows, each lane storing its two kept rows) measured 4.52
+// against 3.10 ms: a wave's stores then interleave and no longer combine.
 std::string gen_project_blocks_kernel(bool bitmap_pred) {
     std::string s = "#define PB_RUN " + std::to_string(fqc::knob(FQ_TUNE_SELECT_BLOCKS_RUN)) + "\n#define PB_DRAW " +
-                    std::to_string(fqc::knob(FQ_TUNE_SELECT_BLOCKS_DRAW)) + "\n";
+                    std::to_string(fqc::knob(FQ_TUNE_SELECT_BLOCKS_DRAW)) + "\n#define PB_ROWS " +
+                    std::to_string(fqc::knob(FQ_TUNE_SELECT_BLOCKS_ROWS)) + "\n#define PB_NT " +
+                    std::to_string(fqc::knob(FQ_TUNE_SELECT_NT) & 1) + "\n";
     s += R"(
 #define PB_THREADS 256
-#define PB_ROWS 32
 #define PB_WAVES (PB_THREADS / 64)
 #define PB_TILE (PB_THREADS * PB_ROWS)
-#define PB_NE (PB_ROWS * PB_WAVES)
-#ifndef PB_RUN
-#define PB_RUN 0
+#define PB_NE (PB_ROWS * PB_WAVES)  // 64-row ballots per tile
+#if PB_NT
+#define PB_PUT fq_put_nt
+#else
+#define PB_PUT fq_put
 #endif
 struct PbShared {
     u64 bal[2][PB_NE];      // ballot of 64-row group i = k * PB_WAVES + wave (tile rows [64 i, 64 i + 64))
     u32 off[2][PB_NE + 1];  // exclusive in-tile offset of each group; [PB_NE]: the tile's kept rows
 };
-extern "C" __global__ void __launch_bounds__(PB_THREADS)
-fq_jit_pblocks(const TIn *__restrict__ col, long long n, long long B, Consts c, const u64 *__restrict__ bm, Outs o,
-               long long *__restrict__ counts, u32 *__restrict__ fl, unsigned long long *__restrict__ total,
-               u32 *__restrict__ ticket) {
+// exclusive scan of the ng group counts in off[] by wave 0; off[PB_NE] = total
+__device__ __forceinline__ void pb_scan(u32 *__restrict__ off, int ng, int lane) {
+    constexpr int PER = (PB_NE + 63) / 64;
+    u32 cv[PER], tot = 0;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        cv[q] = lane * PER + q < ng ? off[lane * PER + q] : 0u;
+        tot += cv[q];
+    }
+    u32 incl = tot;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const u32 v = (u32)__shfl_up((int)incl, d, 64);
+        if (lane >= d) incl += v;
+    }
+    u32 run = incl - tot;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        if (lane * PER + q < ng) off[lane * PER + q] = run;
+        run += cv[q];
+    }
+    if (lane == 63) off[PB_NE] = incl;
+}
+)";
+    const std::string pred8 = bitmap_pred ? "            const bool p = live && ((bm[row >> 6] >> (row & 63)) & 1ull);\n"
+                                            "            (void)c;\n"
+                                          : "            const bool p = fq_pred(x[k], c, pflags, live) && live;\n";
+    s += R"(extern "C" __global__ void __launch_bounds__(PB_THREADS)
+fq_jit_pblocks(const TIn *__restrict__ col, long long n, long long B, Consts c,
+    const u64 *__restrict__ bm, Outs o, long long *__restrict__ counts, u32 *__restrict__ fl,
+    unsigned long long *__restrict__ total, u32 *__restrict__ ticket) {
     __shared__ PbShared sh;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const long long nb = (n + B - 1) / B;
@@ -2104,7 +2141,6 @@ fq_jit_pblocks(const TIn *__restrict__ col, long long n, long long B, Consts c, 
     const u64 lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     int par = 0;
 #if PB_RUN && PB_DRAW
-    // runs of PB_RUN blocks drawn in order: the runs in flight are adjacent
     __shared__ long long s_run;
     const long long nruns = (nb + PB_RUN - 1) / PB_RUN;
     for (;;) {
@@ -2114,13 +2150,11 @@ fq_jit_pblocks(const TIn *__restrict__ col, long long n, long long B, Consts c, 
         if (run >= nruns) break;
         const long long b_lo = run * PB_RUN, b_hi = b_lo + PB_RUN < nb ? b_lo + PB_RUN : nb;
 #elif PB_RUN
-    // runs of PB_RUN blocks dealt round-robin: the runs in flight are adjacent
     (void)ticket;
     const long long nruns = (nb + PB_RUN - 1) / PB_RUN;
     for (long long run = blockIdx.x; run < nruns; run += gridDim.x) {
         const long long b_lo = run * PB_RUN, b_hi = b_lo + PB_RUN < nb ? b_lo + PB_RUN : nb;
 #else
-    // one contiguous run of whole blocks per workgroup
     (void)ticket;
     {
         const long long b_lo = nb * (long long)blockIdx.x / gridDim.x, b_hi = nb * ((long long)blockIdx.x + 1) / gridDim.x;
@@ -2131,6 +2165,8 @@ fq_jit_pblocks(const TIn *__restrict__ col, long long n, long long B, Consts c, 
     for (long long r0 = b_lo * B; r0 < end; r0 += PB_TILE, par ^= 1) {
         u64 *__restrict__ bal = sh.bal[par];
         u32 *__restrict__ off = sh.off[par];
+)";
+    s += R"(
         TIn x[PB_ROWS];
         const long long rt = r0 + tid;
         if (r0 + PB_TILE <= end) {
@@ -2147,11 +2183,7 @@ fq_jit_pblocks(const TIn *__restrict__ col, long long n, long long B, Consts c, 
         for (int k = 0; k < PB_ROWS; ++k) {
             const long long row = rt + k * PB_THREADS;
             const u32 live = row < end ? 1u : 0u;
-)";
-    s += bitmap_pred ? "            const bool p = live && ((bm[row >> 6] >> (row & 63)) & 1ull);\n"
-                       "            (void)c;\n"
-                     : "            const bool p = fq_pred(x[k], c, pflags, live) && live;\n";
-    s += R"(
+)" + pred8 + R"(
             const u64 b = __ballot(p);
             if (lane == 0) {
                 bal[k * PB_WAVES + wave] = b;
@@ -2159,28 +2191,7 @@ fq_jit_pblocks(const TIn *__restrict__ col, long long n, long long B, Consts c, 
             }
         }
         __syncthreads();
-        if (wave == 0) {
-            constexpr int PER = (PB_NE + 63) / 64;
-            u32 cv[PER], tot = 0;
-#pragma unroll
-            for (int q = 0; q < PER; ++q) {
-                cv[q] = off[lane * PER + q];
-                tot += cv[q];
-            }
-            u32 incl = tot;
-#pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-                const u32 v = (u32)__shfl_up((int)incl, d, 64);
-                if (lane >= d) incl += v;
-            }
-            u32 run = incl - tot;
-#pragma unroll
-            for (int q = 0; q < PER; ++q) {
-                off[lane * PER + q] = run;
-                run += cv[q];
-            }
-            if (lane == 63) off[PB_NE] = incl;
-        }
+        if (wave == 0) pb_scan(off, PB_NE, lane);
         __syncthreads();
         const u32 tot = off[PB_NE];
         // the open block's edge: inside the tile (or at its end) when e <= PB_TILE
@@ -2199,9 +2210,11 @@ fq_jit_pblocks(const TIn *__restrict__ col, long long n, long long B, Consts c, 
             const u64 b = bal[k * PB_WAVES + wave];
             if ((b >> lane) & 1ull) {
                 const u32 rank = off[k * PB_WAVES + wave] + (u32)__popcll(b & lt);
-                fq_put(x[k], c, vflags, 1u, o, (rank < re ? before : after) + (long long)rank);
+                PB_PUT(x[k], c, vflags, 1u, o, (rank < re ? before : after) + (long long)rank);
             }
         }
+)";
+    s += R"(
         kept += tot;
         if (e <= PB_TILE) {
             if (tid == 0) counts[cur] = (long long)(carry + re);
@@ -2238,7 +2251,8 @@ bool gen_project_source(const ProjLaunch &P, int32_t tin, int dev, Gen &g, std::
     src += "struct Outs { void *p[" + std::to_string(FQ_MAX_PROJECT) + "]; };\n";
     src += "#define PS_ROWS " + std::to_string(select_rows_per_thread()) + "\n#define PS_THREADS " +
            std::to_string(select_threads()) + "\n#define PS_SLEEP " + std::to_string(select_sleep()) +
-           "\n#define PS_XCD " + std::to_string(select_variant() & 1) + "\n#define PS_LBW " + std::to_string(select_lbw()) + "\n#define PS_DEBUG " + std::to_string(select_debug()) + "\n#define PS_NXCD " + std::to_string(select_xcds(dev)) + "\n";
+           "\n#define PS_XCD " + std::to_string(select_variant() & 1) + "\n#define PS_LBW " + std::to_string(select_lbw()) + "\n#define PS_DEBUG " + std::to_string(select_debug()) + "\n#define PS_NXCD " + std::to_string(select_xcds(dev)) + "\n#define PS_NT " +
+           std::to_string((fqc::knob(FQ_TUNE_SELECT_NT) >> 1) & 1) + "\n";
     src += "typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));\n";
     src += "__device__ __forceinline__ bool fq_pred(TIn x, const Consts &c, u32 &flags, u32 live) {\n";
     src += expr_pred ? pred_body : "    (void)x; (void)c; (void)flags; (void)live;\n    return true;\n";
@@ -2246,6 +2260,8 @@ bool gen_project_source(const ProjLaunch &P, int32_t tin, int dev, Gen &g, std::
     // every output: its value function and its 64-bit store
     std::string put_all = "__device__ __forceinline__ void fq_put(TIn x, const Consts &c, u32 &flags, u32 live, const Outs &o,\n"
                           "                                       long long pos) {\n";
+    std::string put_nt = "__device__ __forceinline__ void fq_put_nt(TIn x, const Consts &c, u32 &flags, u32 live, const Outs &o,\n"
+                         "                                          long long pos) {\n";
     std::string vals_pair = "__device__ __forceinline__ void fq_put2(TIn x0, TIn x1, const Consts &c, u32 &flags, const Outs &o,\n"
                             "                                        long long pair) {\n";
     for (int j = 0; j < P.n_out; ++j) {
@@ -2258,11 +2274,12 @@ bool gen_project_source(const ProjLaunch &P, int32_t tin, int dev, Gen &g, std::
         src += std::string("__device__ __forceinline__ ") + V + " fq_val" + J + "(TIn x, const Consts &c, u32 &flags, u32 live) {\n" +
                "    (void)live;\n" + body + "}\n";
         put_all += std::string("    ((") + V + " *)o.p[" + J + "])[pos] = fq_val" + J + "(x, c, flags, live);\n";
+        put_nt += std::string("    __builtin_nontemporal_store(fq_val") + J + "(x, c, flags, live), ((" + V + " *)o.p[" + J + "]) + pos);\n";
         vals_pair += std::string("    { const ") + V + " a = fq_val" + J + "(x0, c, flags, 1u), b = fq_val" + J +
                      "(x1, c, flags, 1u);\n      __builtin_nontemporal_store(u64x2{__builtin_bit_cast(u64, a), "
                      "__builtin_bit_cast(u64, b)}, ((u64x2 *)o.p[" + J + "]) + pair); }\n";
     }
-    src += put_all + "}\n" + vals_pair + "}\n";
+    src += put_all + "}\n" + put_nt + "}\n" + vals_pair + "}\n";
     src += R"(
 __device__ __forceinline__ u32 wave_or(u32 f) {
 #pragma unroll
@@ -2561,7 +2578,11 @@ __device__ __forceinline__ bool ps_single(PsCtx &X, const Consts &c, const Outs 
     for (int k = 0; k < PS_ROWS; ++k) {
         const u64 b = sh.bal[S][k][wave];
         if ((b >> lane) & 1ull)
+#if PS_NT
+            fq_put_nt(x[k], c, vflags, 1u, o, (long long)(base + sh.off[S][k * PS_WAVES + wave] + (u32)__popcll(b & lt)));
+#else
             fq_put(x[k], c, vflags, 1u, o, (long long)(base + sh.off[S][k * PS_WAVES + wave] + (u32)__popcll(b & lt)));
+#endif
     }
     if (t == X.ntiles - 1 && tid == 0) *total = base + sh.agg[S];
 #if PS_DEBUG
@@ -3107,6 +3128,7 @@ fq_status jit_project_blocks(int32_t col_dtype, const ProjLaunch &P, int64_t blo
     long long n = P.n, B = block_rows;
     const int64_t nb = (P.n + block_rows - 1) / block_rows;
     void *args[] = {&col, &n, &B, &hc, &d_bitmap, &outs, &d_counts, &d_flags, &d_total, &d_ticket};
+    hipFunction_t fn = k.blocks;
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     (void)hipGetLastError();
@@ -3117,22 +3139,22 @@ fq_status jit_project_blocks(int32_t col_dtype, const ProjLaunch &P, int64_t blo
     int occ = 0;
     {
         std::lock_guard<std::mutex> lk(occ_mu);
-        auto it = occ_cache.find(k.blocks);
+        auto it = occ_cache.find(fn);
         if (it != occ_cache.end()) {
             occ = it->second;
         } else {
-            if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k.blocks, kProjectBlockThreads, 0) != hipSuccess)
+            if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kProjectBlockThreads, 0) != hipSuccess)
                 occ = 1;
             (void)hipGetLastError();
             occ = std::max(1, occ);
-            occ_cache.emplace(k.blocks, occ);
+            occ_cache.emplace(fn, occ);
         }
     }
     const int wg_per_cu = (int)fqc::knob(FQ_TUNE_SELECT_BLOCKS_WG_PER_CU);
     const int64_t run = fqc::knob(FQ_TUNE_SELECT_BLOCKS_RUN);
     const int64_t units = run > 0 ? (nb + run - 1) / run : nb;
     const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(units, (int64_t)cus * std::min(wg_per_cu, occ)));
-    FQ_HIP_TRY(hipModuleLaunchKernel(k.blocks, (unsigned)grid, 1, 1, kProjectBlockThreads, 1, 1, 0, P.stream, args,
+    FQ_HIP_TRY(hipModuleLaunchKernel(fn, (unsigned)grid, 1, 1, kProjectBlockThreads, 1, 1, 0, P.stream, args,
                                      nullptr));
     g_jit_launches += 1;
     return FQ_OK;

@@ -48,6 +48,8 @@ constexpr KnobDef kDefs[FQ_TUNE_COUNT] = {
     {0, 0, 3, 1, false},         // GROUP_PREFETCH
     {1, 0, 4096, 1, false},      // SELECT_BLOCKS_RUN
     {1, 0, 1, 1, false},         // SELECT_BLOCKS_DRAW
+    {32, 8, 32, 1, true},        // SELECT_BLOCKS_ROWS
+    {1, 0, 3, 1, false},         // SELECT_NT
 };
 
 std::atomic<int64_t> g_val[FQ_TUNE_COUNT] = {};

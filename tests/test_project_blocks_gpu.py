@@ -226,3 +226,19 @@ def test_block_full_size_closed_forms():
         v = o.buf[:8 * br * nb].view(torch.int64).view(nb, br)
         got = torch.where(mask, v, torch.zeros_like(v)).sum(dim=1).cpu().numpy().astype(np.uint64)
         assert got.tolist() == [int(x) % (1 << 64) for x in s]
+
+
+
+@pytest.mark.parametrize("offset", [0, 1])
+@pytest.mark.parametrize("block_rows", [TILE, 10_000, 10_001, 65_536])
+def test_block_column_views(offset, block_rows):
+    """A column view starting 8 bytes into its buffer (not 16-byte aligned) and
+    a 16-byte aligned one, block sizes even and odd."""
+    n = 10_000 * 23 + 7
+    host = np.arange(n + offset, dtype=np.uint64) * np.uint64(7) + np.uint64(3)
+    full = ops.from_numpy(host)
+    col = ops.DeviceColumn(full.buf, n, U64, offset=8 * offset)
+    h = host[offset:]
+    keep = h % np.uint64(5) < np.uint64(2)
+    _check(h, keep, predicate(U64, [("%", 5)], "<", 2), [chain(U64, [("+", 1)])[0], None],
+           [lambda k: k + np.uint64(1), lambda k: k], block_rows, col=col)
