@@ -513,12 +513,12 @@ fq_status fq_filter_project_blocks(const fq_col *col, int64_t block_rows, const 
     uint64_t *const pinned = fqc::host_staging();
     uint64_t *const host = pinned ? pinned : local;  // kept rows, flag words
     host[0] = host[1] = 0;
-    const int64_t nb = (n + block_rows - 1) / block_rows;
+    const int64_t nb = block_rows >= n ? 1 : (n + block_rows - 1) / block_rows;
     FQ_HIP_TRY(hipMemsetAsync(d_ws, 0, fq_filter_project_blocks_workspace_bytes(), st));
     if (P.pred.kind == FQ_PRED_NONE) {  // every row kept: outputs in place, counts = block lengths
         if ((s = jit_project_map(col->dtype, P, flags + 1)) != FQ_OK) return s;
         hipLaunchKernelGGL(block_lengths_kernel, dim3((unsigned)std::min<int64_t>((nb + 255) / 256, 4096)), dim3(256), 0,
-                           st, d_counts, nb, block_rows, n);
+                           st, d_counts, nb, std::min(block_rows, n), n);
         FQ_HIP_TRY(hipGetLastError());
         FQ_HIP_TRY(hipMemcpyAsync(&host[1], flags, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
         host[0] = (uint64_t)n;

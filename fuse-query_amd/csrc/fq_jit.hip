@@ -3125,8 +3125,9 @@ fq_status jit_project_blocks(int32_t col_dtype, const ProjLaunch &P, int64_t blo
     } outs;
     for (int j = 0; j < FQ_MAX_PROJECT; ++j) outs.p[j] = j < P.n_out ? P.out[j] : nullptr;
     const void *col = P.col;
-    long long n = P.n, B = block_rows;
-    const int64_t nb = (P.n + block_rows - 1) / block_rows;
+    // a block longer than the column is the whole column (one block; keeps n + B in range)
+    long long n = P.n, B = std::min<int64_t>(block_rows, P.n);
+    const int64_t nb = (P.n + B - 1) / B;
     void *args[] = {&col, &n, &B, &hc, &d_bitmap, &outs, &d_counts, &d_flags, &d_total, &d_ticket};
     hipFunction_t fn = k.blocks;
     int dev = 0, cus = 256;

@@ -255,7 +255,7 @@ def filter_project_blocks(col, block_rows, pred, values, stream=None):
         exprs[j] = v
         outs.append(empty_column(col.len, v.out_dtype))
     ptrs = (C.c_void_p * max(n_out, 1))(*[o.ptr for o in outs])
-    nb = -(-col.len // block_rows) if block_rows > 0 else 0
+    nb = (1 if block_rows >= col.len else -(-col.len // block_rows)) if block_rows > 0 and col.len > 0 else 0
     counts = Workspace(max(8 * nb, 8))
     ws = Workspace(lib.fq_filter_project_blocks_workspace_bytes())
     n = C.c_int64(0)

@@ -183,6 +183,10 @@ def test_block_error_order_and_refusals():
     keep = host % 8 >= 1  # filtered out: no error, the projection sees kept rows only
     _check(host, keep, predicate(U64, [("%", 8)], ">=", 1), [val], [lambda k: np.uint64(100) // (k % np.uint64(8))],
            10_000, col=col)
+    # a block longer than the column: one block (no overflow of len + block_rows)
+    outs, counts = ops.filter_project_blocks(col, 2**63 - 1, predicate(U64, [("%", 8)], "<", 3), [None])
+    assert counts.tolist() == [int((host % 8 < 3).sum())]
+    assert np.array_equal(outs[0].to_numpy()[:counts[0]], host[host % 8 < 3])
     with pytest.raises(ops.FQError) as ei:
         ops.filter_project_blocks(col, TILE - 1, predicate(U64, [], ">", 1), [None])
     assert ei.value.status == abi.FQ_E_INVALID
