@@ -72,10 +72,11 @@ struct Rtc {
 
 // Every hipRTC call runs on one thread of its own (64 MB stack), the one
 // that loaded it: the namespace's own libc copy then serves a single thread.
-// Sources with inline asm (the partition kernel's LDS-DMA path) compiled from
-// several threads -- the engine's workers -- crashed the process inside
-// hipRTC (SIGSEGV); on one thread, or with the process's hipRTC, they compile
-// (tests/test_jit_cpu.py::test_compiles_from_many_threads reproduces it).
+// Sources with inline asm (round 3's since-removed LDS-DMA path in the
+// partition kernel) compiled from several threads -- the engine's workers --
+// crashed the process inside hipRTC (SIGSEGV); on one thread, or with the
+// process's hipRTC, they compile (tests/test_jit_cpu.py::
+// test_compiles_from_many_threads compiles 16 shapes from fresh threads).
 class RtcThread {
   public:
     static RtcThread &get() {
@@ -828,7 +829,7 @@ void pack_group_consts(const GroupLaunch &G, HostGroupConsts &hc) {
 std::string group_shape_key(const GroupLaunch &G, int32_t tin, int dev) {
     std::string k = "G" + std::to_string(group_lds_local()) + std::to_string(group_key_plain()) +
                     std::to_string(group_chunked()) + std::to_string(group_wave_runs()) +
-                    std::to_string(group_cluster()) + std::to_string(fqc::knob(FQ_TUNE_GROUP_PREFETCH));
+                    std::to_string(group_cluster());
     auto put = [&k](int32_t v) { k.append(reinterpret_cast<const char *>(&v), sizeof v); };
     auto prog = [&put](const KProg &p) {
         put(p.n);
@@ -978,43 +979,9 @@ __device__ __forceinline__ u32 gp_rank(u32 *cnt, u32 b, bool p) {
     return p ? atomicAdd(&cnt[b], 1u) : 0u;
 }
 
-#if GP_PREFETCH
-// Row k of a thread in tile tt: wave w holds the tile's rows [w * 64 * GP_ROWS,
-// (w + 1) * 64 * GP_ROWS) -- one contiguous 4 KB run per wave, which its own
-// LDS-DMA loads fill (no other wave reads it: no barrier between the reads of
-// one tile and the DMA of the next)
-__device__ __forceinline__ long long gp_row(long long tt, int k) {
-    return tt * GP_TILE + (long long)(threadIdx.x >> 6) * (64 * GP_ROWS) + k * 64 + (threadIdx.x & 63);
-}
-// LDS-only barrier: __syncthreads()' fence would wait for the DMA in flight
-// (vmcnt(0)); the loop's barriers order LDS state only
-__device__ __forceinline__ void gp_sync() {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-}
-// the wave's 64 * GP_ROWS rows of tile tt into its LDS run: GP_ROWS / 2
-// global_load_lds_dwordx4, two rows per lane each (a full tile only).  In asm,
-// so the compiler's wait counting neither sees it nor drains it early: the
-// reader waits with vmcnt(0) itself.
-__device__ __forceinline__ void gp_dma(const TIn *__restrict__ col, long long tt, TIn *s_rows) {
-    const int w = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
-    const TIn *src = col + tt * GP_TILE + (long long)w * (64 * GP_ROWS) + 2 * lane;
-    const u32 dst0 = (u32)(size_t)(__attribute__((address_space(3))) TIn *)(s_rows + w * (64 * GP_ROWS));
-#pragma unroll
-    for (int i = 0; i < GP_ROWS / 2; ++i) {
-        const u32 dst = (u32)__builtin_amdgcn_readfirstlane((int)(dst0 + i * 1024u));
-        u32 keep;
-        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                     : "=&s"(keep) : "v"(src + i * 128), "s"(dst) : "memory");
-    }
-}
-#else
 __device__ __forceinline__ long long gp_row(long long tt, int k) {
     return tt * GP_TILE + (long long)k * BT + threadIdx.x;
 }
-__device__ __forceinline__ void gp_sync() { __syncthreads(); }
-#endif
 __device__ __forceinline__ void gp_load(const TIn *__restrict__ col, long long n, long long tt, TIn (&x)[GP_ROWS]) {
 #pragma unroll
     for (int k = 0; k < GP_ROWS; ++k) {
@@ -1030,7 +997,8 @@ __device__ __forceinline__ void gp_load(const TIn *__restrict__ col, long long n
 // SGPRs (84 admit 7 waves: one workgroup, and the pass ran 1.1 -> 1.5 ms).
 // Loading the next tile's rows into registers while this one is ranked and
 // stored ran it 1.09 -> 1.81 ms per 4.2e8 narrow rows (64 VGPRs: spills);
-// GP_PREFETCH loads them into LDS instead.
+// loading them into LDS by LDS-DMA instead measured within 1 % of the plain
+// loads (round 3, profiles/r03_s3_g2_prefetch_ab.txt) and was removed.
 extern "C" __global__ void __launch_bounds__(BT) __attribute__((amdgpu_waves_per_eu(BT >= 1024 ? 8 : 1)))
 fq_jit_gpart(const TIn *__restrict__ col, long long n, const u64 *__restrict__ bitmap, Consts c,
              u32 *__restrict__ used, u32 *__restrict__ bin_blocks, u32 *__restrict__ blk_bin,
@@ -1064,44 +1032,11 @@ fq_jit_gpart(const TIn *__restrict__ col, long long n, const u64 *__restrict__ b
     const u32 region = blockIdx.x * q;
     u32 flags = 0;
     const long long ntiles = (n + GP_TILE - 1) / GP_TILE;
-#if GP_PREFETCH
-    // the next tile's rows land in LDS while this one is ranked and stored
-    // (full tiles of a 16-byte aligned column; the last, partial tile and an
-    // unaligned column take plain loads)
-    __shared__ TIn s_rows[GP_TILE];
-    const long long nfull = ((size_t)col & 15) || GP_PREFETCH == 2 ? 0 : n / GP_TILE;
-    if ((long long)blockIdx.x < nfull) gp_dma(col, blockIdx.x, s_rows);
-#endif
     for (long long tt = blockIdx.x; tt < ntiles; tt += gridDim.x) {
         for (int i = threadIdx.x; i < P; i += BT) s_cnt[i] = 0;
         TIn x[GP_ROWS];
-#if GP_PREFETCH
-        TIn *mine = s_rows + (threadIdx.x >> 6) * (64 * GP_ROWS) + (threadIdx.x & 63);
-        if (tt < nfull) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this tile's DMA (and older stores)
-        } else {  // through the same LDS run, so x never comes from a plain load (whose use would
-                  // make the compiler wait vmcnt(0), draining the DMA, at every row)
-            TIn y[GP_ROWS];
-            gp_load(col, n, tt, y);
-#pragma unroll
-            for (int k = 0; k < GP_ROWS; ++k) mine[k * 64] = y[k];
-        }
-#pragma unroll
-        for (int k = 0; k < GP_ROWS; ++k) x[k] = mine[k * 64];
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // read before the next DMA overwrites it
-#if GP_PREFETCH == 3
-        if (tt < nfull)
-#pragma unroll
-            for (int k = 0; k < GP_ROWS; ++k)
-                if (__builtin_nontemporal_load(col + gp_row(tt, k)) != x[k]) flags |= 2048u;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
-        if (tt + gridDim.x < nfull) gp_dma(col, tt + gridDim.x, s_rows);
-        gp_sync();
-#else
         __syncthreads();
         gp_load(col, n, tt, x);
-#endif
         // per row: bin | rank << 8 (P <= 256 bins, rank < GP_TILE), one register instead of two
         u32 br[GP_ROWS], pass = 0;
 #pragma unroll
@@ -1118,7 +1053,7 @@ fq_jit_gpart(const TIn *__restrict__ col, long long n, const u64 *__restrict__ b
             br[k] = bk | gp_rank(s_cnt, bk, p) << 8;
             if (p) pass |= 1u << k;
         }
-        gp_sync();
+        __syncthreads();
 #if RANGE_BINS
         const int t0 = 0;  // every thread takes blocks (no tile scan)
 #else
@@ -1172,7 +1107,7 @@ fq_jit_gpart(const TIn *__restrict__ col, long long n, const u64 *__restrict__ b
                 s_nb[b] = base;
             }
         }
-        gp_sync();
+        __syncthreads();
 #if RANGE_BINS
         // straight from the registers: a wave's passing lanes mostly hold
         // consecutive ranks of one bin (gp_rank), so the stores coalesce
@@ -1195,7 +1130,7 @@ fq_jit_gpart(const TIn *__restrict__ col, long long n, const u64 *__restrict__ b
             s_stage[pos] = x[k];
             s_bin[pos] = (unsigned char)(br[k] & 255u);
         }
-        gp_sync();
+        __syncthreads();
         const u32 kept = s_tot;
         for (u32 i = threadIdx.x; i < kept; i += BT) {
             const u32 b = s_bin[i];
@@ -1206,7 +1141,7 @@ fq_jit_gpart(const TIn *__restrict__ col, long long n, const u64 *__restrict__ b
             gp_store(out + (long long)blk * GP_BLK + (o & (GP_BLK - 1)), gp_pack(s_stage[i], vbase, flags));
         }
 #endif
-        gp_sync();
+        __syncthreads();
         for (int b = threadIdx.x; b < P; b += BT) {
             const u32 cnt = s_cnt[b], t = s_fill[b] + cnt;
             if (!cnt) continue;
@@ -1387,7 +1322,6 @@ bool gen_groupby_source(const GroupLaunch &G, int32_t tin, Gen &g, std::string &
     src += "#define RANGE_BINS " + std::to_string(G.range_bins ? 1 : 0) + "\n";
     src += "#define GP_NARROW " + std::to_string(G.narrow ? 1 : 0) + "\n";
     // (range bins only: the hash bins' 72 KB staging leaves no LDS for it)
-    src += "#define GP_PREFETCH " + std::to_string(G.range_bins ? fqc::knob(FQ_TUNE_GROUP_PREFETCH) : 0) + "\n";
     // blocks are 2 KB either way: 256 8-byte rows, or 512 narrow ones (1 KB
     // blocks measured 1.11 -> 1.53 ms per 4.2e8-row partition pass)
     src += "#define GP_BLK " + std::to_string(kPartBlockRows * (G.narrow ? 2 : 1)) + "\n";

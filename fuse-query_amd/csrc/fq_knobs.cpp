@@ -45,7 +45,6 @@ constexpr KnobDef kDefs[FQ_TUNE_COUNT] = {
     {1, 0, 1, 1, false},         // GROUP_RANGE_BINS
     {1, 0, 1, 1, false},         // GROUP_NARROW
     {8, 1, 16, 1, false},        // SELECT_BLOCKS_WG_PER_CU
-    {0, 0, 3, 1, false},         // GROUP_PREFETCH
     {1, 0, 4096, 1, false},      // SELECT_BLOCKS_RUN
     {1, 0, 1, 1, false},         // SELECT_BLOCKS_DRAW
     {32, 8, 32, 1, true},        // SELECT_BLOCKS_ROWS

@@ -126,7 +126,7 @@ TUNE = {
     "GROUP_CLUSTER": 10, "GROUP_CHUNKED": 11, "SELECT_VARIANT": 12, "SELECT_DEBUG": 13, "SELECT_LBW": 14,
     "SELECT_WG_PER_CU": 15, "SELECT_THREADS": 16, "SELECT_ROWS": 17, "SELECT_SLEEP": 18, "BLOCK_CACHE": 19,
     "JIT_ISOLATED": 20, "GROUP_ROWMAP": 21, "GROUP_WG_PER_CU": 22, "GROUP_RANGE_BINS": 23, "GROUP_NARROW": 24,
-    "SELECT_BLOCKS_WG_PER_CU": 25, "GROUP_PREFETCH": 26, "SELECT_BLOCKS_RUN": 27, "SELECT_BLOCKS_DRAW": 28, "SELECT_BLOCKS_ROWS": 29,
-    "SELECT_NT": 30,
+    "SELECT_BLOCKS_WG_PER_CU": 25, "SELECT_BLOCKS_RUN": 26, "SELECT_BLOCKS_DRAW": 27, "SELECT_BLOCKS_ROWS": 28,
+    "SELECT_NT": 29,
 }
 TUNE_SELECT_COUNTERS = 13

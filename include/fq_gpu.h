@@ -389,12 +389,11 @@ fq_status fq_jit_prepare(const fq_col *col, int64_t block_rows, const fq_pred *p
 #define FQ_TUNE_GROUP_RANGE_BINS 23  /* partitioned GROUP BY: range bins for `% d` keys, 1 (0/1) */
 #define FQ_TUNE_GROUP_NARROW 24      /* partitioned GROUP BY: honour FQ_GROUP_NARROW_ROWS, 1 (0/1) */
 #define FQ_TUNE_SELECT_BLOCKS_WG_PER_CU 25 /* block-stream filter+projection workgroups per CU, 8 (1..16) */
-#define FQ_TUNE_GROUP_PREFETCH 26     /* partition kernel: next tile by LDS DMA, 0 (0..3; experimental) */
-#define FQ_TUNE_SELECT_BLOCKS_RUN 27  /* block-stream filter+projection: blocks per drawn run, 0 = one static run per workgroup */
-#define FQ_TUNE_SELECT_BLOCKS_DRAW 28 /* block-stream runs drawn from a counter (1) or dealt round-robin (0) */
-#define FQ_TUNE_SELECT_BLOCKS_ROWS 29 /* block-stream rows per thread per tile, 32 (8/16/32; tile = 256 x rows) */
-#define FQ_TUNE_SELECT_NT 30          /* nontemporal output stores: bit 0 block-stream, bit 1 contiguous kernel */
-#define FQ_TUNE_COUNT 31
+#define FQ_TUNE_SELECT_BLOCKS_RUN 26  /* block-stream filter+projection: blocks per run, 1 (0 = one static run per workgroup) */
+#define FQ_TUNE_SELECT_BLOCKS_DRAW 27 /* block-stream runs drawn from a counter (1) or dealt round-robin (0), 1 */
+#define FQ_TUNE_SELECT_BLOCKS_ROWS 28 /* block-stream rows per thread per tile, 32 (8/16/32; tile = 256 x rows) */
+#define FQ_TUNE_SELECT_NT 29          /* nontemporal output stores: bit 0 block-stream, bit 1 contiguous kernel; 1 */
+#define FQ_TUNE_COUNT 30
 /* FQ_E_INVALID for an unknown knob or a value outside the knob's set */
 fq_status fq_tune_set(int32_t knob, int64_t value);
 /* the knob's current value; -1 for an unknown knob */

@@ -259,7 +259,6 @@ sys.path.insert(0, sys.argv[1])
 from fq_amd import abi, ops
 from fq_amd.expr import chain, predicate
 U64 = abi.DT_UINT64
-ops.tune_set("GROUP_PREFETCH", 1)  # the partition kernel's inline-asm LDS-DMA path
 errors = []
 
 def compile_shape(j):
