@@ -286,7 +286,8 @@ def run_project(args, rank, world):
         expect.append(project_closed_form(b, e))
     blocks = args.project_path == "blocks"
     maxr = max(c.len for c in cols)
-    outs = [ops.empty_column(maxr, U), ops.empty_column(maxr, U)]
+    alloc = ops.contiguous_column if args.p1_outputs == "contiguous" else ops.empty_column
+    outs = [alloc(maxr, U), alloc(maxr, U)]
     nb_max = -(-maxr // BLOCK_SIZE)
     counts = ops.Workspace(8 * nb_max)
     ws = ops.Workspace(max(lib.fq_filter_project_workspace_bytes(maxr), lib.fq_filter_project_blocks_workspace_bytes()))
@@ -395,6 +396,8 @@ def run_project(args, rank, world):
             "dtype": "u64", "data": "synthetic: system.numbers_mt iota column (u64), resident in HBM before timing",
             "config": {"workload": sql, "query": "p1", "rows_per_gpu": total_rows, "rows_total": n_total,
                        "partitions_per_gpu": len(cols), "block_rows": BLOCK_SIZE, "path": path,
+                       "outputs": "physically contiguous HBM (hipDeviceMallocContiguous)" if args.p1_outputs ==
+                                  "contiguous" else "torch caching-allocator buffers",
                        "parallelism": "dp%d (numbers_mt partitions sharded)" % world},
             "achieved_hbm_gbps": achieved, "kernel_ms_per_launch": avg_ms, "scan_launches_per_step": len(cols),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
@@ -484,6 +487,8 @@ def main():
     ap.add_argument("--project-path", default="blocks", choices=("blocks", "contiguous"),
                     help="p1: block-stream output (fq_filter_project_blocks, default) or one contiguous output "
                          "per partition (fq_filter_project)")
+    ap.add_argument("--p1-outputs", default="contiguous", choices=("contiguous", "torch"),
+                    help="p1: output columns in physically contiguous HBM (default) or torch buffers")
     ap.add_argument("--no-contiguous-ref", action="store_true",
                     help="p1: skip timing the contiguous-output kernel beside the block-stream one")
     ap.add_argument("--streams", type=int, default=1,

@@ -73,6 +73,38 @@ def empty_column(n, dtype, device=None):
     return DeviceColumn(buf, n, dtype)
 
 
+class _RawDevice:
+    """A device allocation presented to torch through __cuda_array_interface__."""
+
+    def __init__(self, ptr, nbytes):
+        self.__cuda_array_interface__ = {"shape": (nbytes,), "typestr": "|u1", "data": (ptr, False), "version": 2}
+
+
+_hip = None
+
+
+def contiguous_column(n, dtype):
+    """A column in physically contiguous HBM (hipExtMallocWithFlags with
+    hipDeviceMallocContiguous), freed with its tensor.  Output buffers of the
+    block-stream Filter -> Projection run faster more often in such memory
+    (profiles/r03_s3_output_placement.txt); the kernels accept any device memory."""
+    global _hip
+    require_gpu()
+    import weakref
+    if _hip is None:
+        _hip = C.CDLL("libamdhip64.so.7")  # torch's HIP runtime, already loaded (see _lib._load)
+        _hip.hipExtMallocWithFlags.argtypes = [C.POINTER(C.c_void_p), C.c_size_t, C.c_uint]
+        _hip.hipFree.argtypes = [C.c_void_p]
+    nb = max(((n + 63) // 64) * 8 if dtype == abi.DT_BOOLEAN else n * ELEM_SIZE[dtype], 16)
+    p = C.c_void_p()
+    rc = _hip.hipExtMallocWithFlags(C.byref(p), nb, 0x4)  # hipDeviceMallocContiguous
+    if rc != 0:
+        raise FQError(abi.FQ_E_HIP, "hipExtMallocWithFlags(hipDeviceMallocContiguous, %d bytes) failed: %d" % (nb, rc))
+    buf = torch.as_tensor(_RawDevice(p.value, nb), device="cuda")
+    weakref.finalize(buf, _hip.hipFree, C.c_void_p(p.value))
+    return DeviceColumn(buf, n, dtype)
+
+
 def from_numpy(arr, dtype=None):
     require_gpu()
     arr = np.ascontiguousarray(arr)
