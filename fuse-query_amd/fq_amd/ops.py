@@ -101,7 +101,8 @@ def contiguous_column(n, dtype):
     if rc != 0:
         raise FQError(abi.FQ_E_HIP, "hipExtMallocWithFlags(hipDeviceMallocContiguous, %d bytes) failed: %d" % (nb, rc))
     buf = torch.as_tensor(_RawDevice(p.value, nb), device="cuda")
-    weakref.finalize(buf, _hip.hipFree, C.c_void_p(p.value))
+    fin = weakref.finalize(buf, _hip.hipFree, C.c_void_p(p.value))
+    fin.atexit = False  # never call into HIP during interpreter shutdown; process exit releases it
     return DeviceColumn(buf, n, dtype)
 
 
