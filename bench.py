@@ -141,7 +141,8 @@ def latest_pmc_traffic(kernel_substr, query, rows_per_launch):
                    key=os.path.basename)
     subs = [kernel_substr] if isinstance(kernel_substr, str) else list(kernel_substr)
     cur = kernel_sources_sha256(query)
-    for f in reversed(files):
+    stale = None
+    for f in reversed(files):  # the last by name measured on the current sources; else report the last one
         try:
             d = json.load(open(f))
         except Exception:
@@ -153,13 +154,17 @@ def latest_pmc_traffic(kernel_substr, query, rows_per_launch):
         src = {"file": "profiles/" + os.path.basename(f), "measured_at_commit": d.get("measured_at_commit"),
                "query_sources_sha256": d.get("query_sources_sha256")}
         if d.get("query_sources_sha256") != cur:
-            src["status"] = "stale: kernel sources changed since this PMC pass (current %s)" % cur[:12]
-            return None, src
+            if stale is None:
+                src["status"] = "stale: kernel sources changed since this PMC pass (current %s)" % cur[:12]
+                stale = src
+            continue
         src["status"] = "current kernel sources"
         # several names: one launch of each per unit (the partitioned GROUP BY's kernel set)
         per = sum(k["hbm_bytes_per_launch"] for k in ks)
         rows = ks[0].get("rows_per_launch")
         return (per * rows_per_launch / rows if rows else None), src
+    if stale is not None:
+        return None, stale
     return None, {"status": "no PMC summary for this query in profiles/"}
 
 
