@@ -979,6 +979,15 @@ __device__ __forceinline__ u32 gp_rank(u32 *cnt, u32 b, bool p) {
     return p ? atomicAdd(&cnt[b], 1u) : 0u;
 }
 
+#if GP_MOD32
+__device__ __forceinline__ u32 gp_key32(TIn x, u64 mbase, u32 d, u64 M, u32 cb) {
+    const u64 low = M * (u64)(u32)((u64)x - mbase);
+    const u64 t = ((u64)(u32)low * d) >> 32;
+    const u32 r = (u32)(((low >> 32) * d + t) >> 32);
+    const u32 k = cb + r;  // cb, r < d: a sum >= d, or one that wrapped 32 bits, loses one d
+    return k >= d || k < cb ? k - d : k;
+}
+#endif
 __device__ __forceinline__ long long gp_row(long long tt, int k) {
     return tt * GP_TILE + (long long)k * BT + threadIdx.x;
 }
@@ -1005,6 +1014,17 @@ fq_jit_gpart(const TIn *__restrict__ col, long long n, const u64 *__restrict__ b
              u32 *__restrict__ blk_fill, unsigned q, PRow *__restrict__ out, int log2p,
              u32 *__restrict__ hdr) {
     const u64 vbase = n > 0 ? gp_vbase(col) : 0ull;
+#if GP_MOD32
+    // key = x % d for a 4-byte row: x = mbase + a with a < 2^32 (mbase = the
+    // narrow rows' base, or 0 when that base would wrap: the values then lie
+    // below 2^32), so x % d = (mbase % d + a % d) mod d, a % d by Lemire's
+    // direct remainder (M = floor((2^64 - 1) / d) + 1, exact for 32-bit a and d)
+    const u64 c0 = n > 0 ? (u64)col[0] : 0ull;
+    const u64 mbase = c0 >= 0x80000000ull ? c0 - 0x80000000ull : 0ull;
+    const u32 md = (u32)c.k[0].c;
+    const u64 mM = 0xffffffffffffffffull / (u64)md + 1ull;
+    const u32 mcb = (u32)(mbase % (u64)md);
+#endif
 #if !RANGE_BINS
     __shared__ TIn s_stage[GP_TILE];
     __shared__ unsigned char s_bin[GP_TILE];
@@ -1039,6 +1059,55 @@ fq_jit_gpart(const TIn *__restrict__ col, long long n, const u64 *__restrict__ b
         gp_load(col, n, tt, x);
         // per row: bin | rank << 8 (P <= 256 bins, rank < GP_TILE), one register instead of two
         u32 br[GP_ROWS], pass = 0;
+#if RANGE_BINS && GP_RANK_BATCH
+        // bins of all rows first, then every row's rank atomic issued before
+        // any return is read (one LDS round trip per tile, not one per row)
+#pragma unroll
+        for (int k = 0; k < GP_ROWS; ++k) {
+            const long long row = gp_row(tt, k);
+            u32 bk = 0;
+            if (row < n) {
+                Row r;
+                fq_prep(x[k], row, c, bitmap, flags, r);
+                if (r.pass) {
+#if GP_MOD32
+                    bk = gp_key32(x[k], mbase, md, mM, mcb) >> (u32)(log2p >> 8);
+#else
+                    bk = gbin(r.k, log2p);
+#endif
+                    pass |= 1u << k;
+                }
+            }
+            br[k] = bk;
+        }
+        u32 rv[GP_ROWS], uni = 0;
+        const int lane = (int)(threadIdx.x & 63);
+#pragma unroll
+        for (int k = 0; k < GP_ROWS; ++k) {
+            const bool p = (pass >> k) & 1u;
+            const u64 act = __ballot(p);
+            rv[k] = 0u;
+            if (!act) continue;
+            const int l0 = __builtin_ctzll(act);
+            const u32 b0 = (u32)__builtin_amdgcn_readlane((int)br[k], l0);
+            if (__ballot(p && br[k] == b0) == act) {
+                uni |= 1u << k;
+                if (lane == l0) rv[k] = atomicAdd(&s_cnt[b0], (u32)__popcll(act));
+            } else if (p) {
+                rv[k] = atomicAdd(&s_cnt[br[k]], 1u);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < GP_ROWS; ++k) {
+            u32 r = rv[k];
+            if ((uni >> k) & 1u) {
+                const u64 act = __ballot((pass >> k) & 1u);
+                r = (u32)__builtin_amdgcn_readlane((int)r, __builtin_ctzll(act)) +
+                    (u32)__popcll(act & ((1ull << lane) - 1ull));
+            }
+            br[k] |= r << 8;
+        }
+#else
 #pragma unroll
         for (int k = 0; k < GP_ROWS; ++k) {
             const long long row = gp_row(tt, k);
@@ -1053,6 +1122,7 @@ fq_jit_gpart(const TIn *__restrict__ col, long long n, const u64 *__restrict__ b
             br[k] = bk | gp_rank(s_cnt, bk, p) << 8;
             if (p) pass |= 1u << k;
         }
+#endif
         __syncthreads();
 #if RANGE_BINS
         const int t0 = 0;  // every thread takes blocks (no tile scan)
@@ -1321,6 +1391,18 @@ bool gen_groupby_source(const GroupLaunch &G, int32_t tin, Gen &g, std::string &
     src += "#define GWAVE " + std::to_string(group_wave_runs()) + "\n";
     src += "#define RANGE_BINS " + std::to_string(G.range_bins ? 1 : 0) + "\n";
     src += "#define GP_NARROW " + std::to_string(G.narrow ? 1 : 0) + "\n";
+    {
+        // partition pass, range bins over 4-byte rows: a `% d` key (d < 2^32)
+        // from the row's 32-bit offset, and the rows' rank atomics issued
+        // together.  Per 4.2e8-row chunk of g2 on one box: 1.137 ms with
+        // neither, 1.132 with the batched ranks alone, 1.136 with the 32-bit
+        // key alone, 1.044 with both (profiles/r03_s4_gpart_ab.txt)
+        const KStep &ks = G.key.s[0];
+        const bool mod32 = G.narrow && G.range_bins && tin == FQ_DT_UINT64 && G.key.n == 1 &&
+                           (ks.code == K_MODM_U || ks.code == K_MODM32_U) && ks.operand == FQ_OPERAND_CONST &&
+                           !ks.reversed && ks.c >= 1 && ks.c <= 0xffffffffull;
+        src += "#define GP_MOD32 " + std::to_string(mod32 ? 1 : 0) + "\n#define GP_RANK_BATCH 1\n";
+    }
     // (range bins only: the hash bins' 72 KB staging leaves no LDS for it)
     // blocks are 2 KB either way: 256 8-byte rows, or 512 narrow ones (1 KB
     // blocks measured 1.11 -> 1.53 ms per 4.2e8-row partition pass)

@@ -667,6 +667,25 @@ def test_narrow_partition_rows_match_wide(mod, log2p, pred):
             assert np.array_equal(res[0][1][a], res[1][1][a]), (first, a)
 
 
+@pytest.mark.parametrize("mod,log2p", [(7, 4), (99_991, 5), (1_000_000, 8)])
+def test_narrow_range_bin_key_from_row_offset(mod, log2p):
+    # range bins over 4-byte rows compute `number % d` from the row's 32-bit
+    # offset (fq_jit_gpart GP_MOD32): blocks starting below 2^31 (the offset
+    # base would wrap, so the values themselves are the offsets), at 2^31 - 10
+    # (crossing 2^31) and above 2^32, against numpy
+    aggs = [(abi.AGG_COUNT, U), (abi.AGG_SUM, U), (abi.AGG_MAX, U)]
+    for first in (0, 2**31 - 10, 2**33 + 5):
+        n = 1_500_007
+        x = np.arange(first, first + n, dtype=np.uint64)
+        t = ops.GroupTable(4 * min(n, mod), aggs)
+        t.aggregate(ops.numbers_column(first, n), None, chain(U, [("%", mod)])[0], [None] * 3,
+                    log2_parts=log2p, narrow=True)
+        keys, states = t.extract()
+        got = {int(k): [s[i] for s in decode(states, [d for _, d in aggs])] for i, k in enumerate(keys)}
+        exp = np_groupby(x % np.uint64(mod), [None, x, x], [a for a, _ in aggs])
+        compare(got, exp, [a for a, _ in aggs], [d for _, d in aggs])
+
+
 def test_narrow_partition_rows_refuse_values_out_of_range():
     # a value more than 2^31 from col[0]: reported, never aggregated wrongly
     x = np.arange(100_000, dtype=np.uint64)
