@@ -980,12 +980,25 @@ __device__ __forceinline__ u32 gp_rank(u32 *cnt, u32 b, bool p) {
 }
 
 #if GP_MOD32
-__device__ __forceinline__ u32 gp_key32(TIn x, u64 mbase, u32 d, u64 M, u32 cb) {
-    const u64 low = M * (u64)(u32)((u64)x - mbase);
-    const u64 t = ((u64)(u32)low * d) >> 32;
-    const u32 r = (u32)(((low >> 32) * d + t) >> 32);
-    const u32 k = cb + r;  // cb, r < d: a sum >= d, or one that wrapped 32 bits, loses one d
-    return k >= d || k < cb ? k - d : k;
+// key = x % d for a 4-byte row: x = mbase + a with a < 2^32 (mbase = the
+// narrow rows' base, or 0 when that base would wrap: the values then lie
+// below 2^32), so x % d = (mbase % d + a % d) mod d, a % d by Lemire's direct
+// remainder (M = floor((2^64 - 1) / d) + 1, exact for 32-bit a and d)
+struct GMod { u64 mbase, M; u32 d, cb; };
+__device__ __forceinline__ GMod gp_mod_init(u64 c0, const Consts &c) {
+    GMod m;
+    m.mbase = c0 >= 0x80000000ull ? c0 - 0x80000000ull : 0ull;
+    m.d = (u32)c.k[0].c;
+    m.M = 0xffffffffffffffffull / (u64)m.d + 1ull;
+    m.cb = (u32)(m.mbase % (u64)m.d);
+    return m;
+}
+__device__ __forceinline__ u32 gp_key32(TIn x, const GMod &m) {
+    const u64 low = m.M * (u64)(u32)((u64)x - m.mbase);
+    const u64 t = ((u64)(u32)low * m.d) >> 32;
+    const u32 r = (u32)(((low >> 32) * m.d + t) >> 32);
+    const u32 k = m.cb + r;  // cb, r < d: a sum >= d, or one that wrapped 32 bits, loses one d
+    return k >= m.d || k < m.cb ? k - m.d : k;
 }
 #endif
 __device__ __forceinline__ long long gp_row(long long tt, int k) {
@@ -1015,15 +1028,7 @@ fq_jit_gpart(const TIn *__restrict__ col, long long n, const u64 *__restrict__ b
              u32 *__restrict__ hdr) {
     const u64 vbase = n > 0 ? gp_vbase(col) : 0ull;
 #if GP_MOD32
-    // key = x % d for a 4-byte row: x = mbase + a with a < 2^32 (mbase = the
-    // narrow rows' base, or 0 when that base would wrap: the values then lie
-    // below 2^32), so x % d = (mbase % d + a % d) mod d, a % d by Lemire's
-    // direct remainder (M = floor((2^64 - 1) / d) + 1, exact for 32-bit a and d)
-    const u64 c0 = n > 0 ? (u64)col[0] : 0ull;
-    const u64 mbase = c0 >= 0x80000000ull ? c0 - 0x80000000ull : 0ull;
-    const u32 md = (u32)c.k[0].c;
-    const u64 mM = 0xffffffffffffffffull / (u64)md + 1ull;
-    const u32 mcb = (u32)(mbase % (u64)md);
+    const GMod gm = gp_mod_init(n > 0 ? (u64)col[0] : 0ull, c);
 #endif
 #if !RANGE_BINS
     __shared__ TIn s_stage[GP_TILE];
@@ -1071,7 +1076,7 @@ fq_jit_gpart(const TIn *__restrict__ col, long long n, const u64 *__restrict__ b
                 fq_prep(x[k], row, c, bitmap, flags, r);
                 if (r.pass) {
 #if GP_MOD32
-                    bk = gp_key32(x[k], mbase, md, mM, mcb) >> (u32)(log2p >> 8);
+                    bk = gp_key32(x[k], gm) >> (u32)(log2p >> 8);
 #else
                     bk = gbin(r.k, log2p);
 #endif
@@ -1303,6 +1308,9 @@ extern "C" __global__ void __launch_bounds__(BT)
 fq_jit_groupby_bins(const PRow *__restrict__ vals, const u64 *__restrict__ order, const u32 *__restrict__ bstart,
                     int log2p, Consts c, Tab t, const TIn *__restrict__ col) {
     const u64 vbase = gp_vbase(col);  // the launch has rows, so col[0] exists
+#if GP_MOD32
+    const GMod gm = gp_mod_init((u64)col[0], c);
+#endif
     __shared__ u64 s_keys[S];
     __shared__ u64 s_st[NA][S];
     __shared__ int s_bypass[2];
@@ -1345,7 +1353,12 @@ fq_jit_groupby_bins(const PRow *__restrict__ vals, const u64 *__restrict__ order
                 }
                 Row r[GP_ROWS];
 #pragma unroll
-                for (int k = 0; k < GP_ROWS; ++k) fq_prep_all(x[k], (live >> k) & 1u, c, flags, r[k]);
+                for (int k = 0; k < GP_ROWS; ++k) {
+                    fq_prep_all(x[k], (live >> k) & 1u, c, flags, r[k]);
+#if GP_MOD32
+                    r[k].k = gp_key32(x[k], gm);  // (the 64-bit key fq_prep_all computed is dead)
+#endif
+                }
                 u32 cnt[GP_ROWS];
                 fq_runs(r, cnt);
 #if RANGE_BINS
@@ -1396,7 +1409,8 @@ bool gen_groupby_source(const GroupLaunch &G, int32_t tin, Gen &g, std::string &
         // from the row's 32-bit offset, and the rows' rank atomics issued
         // together.  Per 4.2e8-row chunk of g2 on one box: 1.137 ms with
         // neither, 1.132 with the batched ranks alone, 1.136 with the 32-bit
-        // key alone, 1.044 with both (profiles/r03_s4_gpart_ab.txt)
+        // key alone, 1.044 with both; the bins pass's key the same way: 0.566
+        // -> 0.483 ms (profiles/r03_s4_gpart_ab.txt)
         const KStep &ks = G.key.s[0];
         const bool mod32 = G.narrow && G.range_bins && tin == FQ_DT_UINT64 && G.key.n == 1 &&
                            (ks.code == K_MODM_U || ks.code == K_MODM32_U) && ks.operand == FQ_OPERAND_CONST &&
