@@ -130,29 +130,36 @@ def log(rank, *a):
 
 def latest_pmc_traffic(kernel_substr, query, rows_per_launch):
     """(HBM bytes per launch scaled to rows_per_launch, provenance) from the
-    newest committed rocprofv3 --pmc summary of this query (profiles/
-    *pmc_<query>[_.]*.json, tools/pmc_summary.py, gfx950 FETCH_SIZE x2
-    correction applied).  The summary must have been measured on the current
-    kernel sources (its kernel_sources_sha256): otherwise traffic is None and
-    the provenance says the file is stale.  The fingerprint covers the
-    query's own kernel sources (tools/srchash.py QUERY_SOURCES)."""
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_%s.json" % query)) +
-                   glob.glob(os.path.join(ROOT, "profiles", "*pmc_%s_*.json" % query)),
-                   key=os.path.basename)
-    subs = [kernel_substr] if isinstance(kernel_substr, str) else list(kernel_substr)
-    cur = kernel_sources_sha256(query)
-    stale = None
-    for f in reversed(files):  # the last by name measured on the current sources; else report the last one
+    most recently MEASURED committed rocprofv3 --pmc summary of this query
+    (profiles/*pmc_<query>[_.]*.json, tools/pmc_summary.py, gfx950 FETCH_SIZE
+    x2 correction applied).  Measurement order is the summary's
+    `measured_at_unix` stamp (tools/pmc_import.py: the import time, which
+    follows the gpurun call that measured it; summaries from before the stamp
+    carry their commit's time), not its file name; files without a stamp count
+    as oldest.  The summary must have been measured on the current kernel
+    sources (its query_sources_sha256): otherwise traffic is None and the
+    provenance says the file is stale.  The fingerprint covers the query's own
+    kernel sources (tools/srchash.py QUERY_SOURCES)."""
+    files = set(glob.glob(os.path.join(ROOT, "profiles", "*pmc_%s.json" % query)) +
+                glob.glob(os.path.join(ROOT, "profiles", "*pmc_%s_*.json" % query)))
+    summaries = []
+    for f in files:
         try:
             d = json.load(open(f))
         except Exception:
             continue
+        summaries.append((float(d.get("measured_at_unix") or 0.0), os.path.basename(f), d))
+    summaries.sort(key=lambda x: (x[0], x[1]))
+    subs = [kernel_substr] if isinstance(kernel_substr, str) else list(kernel_substr)
+    cur = kernel_sources_sha256(query)
+    stale = None
+    for when, name, d in reversed(summaries):  # the newest measured on the current sources; else report the newest
         ks = [k for k in d.get("kernels", []) if k.get("hbm_bytes_per_launch") and
               any(x in k.get("name", "") for x in subs)]
         if not ks:
             continue
-        src = {"file": "profiles/" + os.path.basename(f), "measured_at_commit": d.get("measured_at_commit"),
-               "query_sources_sha256": d.get("query_sources_sha256")}
+        src = {"file": "profiles/" + name, "measured_at_commit": d.get("measured_at_commit"),
+               "measured_at_unix": d.get("measured_at_unix"), "query_sources_sha256": d.get("query_sources_sha256")}
         if d.get("query_sources_sha256") != cur:
             if stale is None:
                 src["status"] = "stale: kernel sources changed since this PMC pass (current %s)" % cur[:12]
@@ -166,6 +173,26 @@ def latest_pmc_traffic(kernel_substr, query, rows_per_launch):
     if stale is not None:
         return None, stale
     return None, {"status": "no PMC summary for this query in profiles/"}
+
+
+def host_split(st, steps, ms_per_step, world):
+    """Rank 0's step, split by the engine's own host timers (fq_engine_stats),
+    per step.  One GPU: plan (SQL -> pipeline), exec (pipeline until the result
+    block), first_launch (query start -> first scan enqueued).  World > 1: the
+    distributed split -- partial (fq_engine_execute_partial: plan + this rank's
+    scans + local merge), exchange (the all-reduce rounds, including the wait for
+    the slowest rank), final (AggregateFinal over every rank's states) -- and
+    what those three account for of the step (the rest is the binding's
+    Python)."""
+    out = {"plan": st["plan_ms"] / steps, "first_launch": st["first_launch_ms"] / steps, "exec": st["exec_ms"] / steps}
+    if world > 1:
+        part, xch, fin = (st[k] / steps for k in ("partial_ms", "exchange_ms", "final_ms"))
+        out.update({"partial": part, "exchange": xch, "final": fin,
+                    "scans_event_ms": st["scan_ms"] / steps,
+                    "exchange_rounds": st["exchange_rounds"] / steps,
+                    "exchange_bytes": st["exchange_bytes"] / steps,
+                    "accounted_frac": (part + xch + fin) / ms_per_step if ms_per_step else None})
+    return out
 
 
 def cpu_baseline(sample_rows, threads, query="c3"):
@@ -474,6 +501,46 @@ def cpu_baseline_group(sample_rows, threads, query):
     }
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n, argv):
+    """`--gpus N` (N > 1) started without a launcher: run N fresh rank
+    processes through torch.distributed.run (127.0.0.1 rendezvous) and exit
+    with their status.  This process never touches the GPU (it has made no HIP
+    call when it gets here), and every rank is a new process, so no GPU state
+    crosses a fork or an exec.  Rank 0's JSON line reaches stdout directly."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + list(argv)
+    print("[bench] launching %d ranks: %s" % (n, " ".join(cmd)), file=sys.stderr, flush=True)
+    return subprocess.call(cmd)
+
+
+def dry_run(rank, world):
+    """--dry-run: the launch and the rendezvous without the GPU -- every rank
+    joins a gloo group and rank 0 prints which ranks arrived (the CPU test of
+    the launcher)."""
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    if world > 1:
+        dist.init_process_group("gloo")
+    mine = [rank, int(os.environ.get("LOCAL_RANK", "0")), os.getpid()]
+    seen = [None] * world
+    if world > 1:
+        dist.all_gather_object(seen, mine)
+    else:
+        seen = [mine]
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "ranks": seen}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -505,7 +572,27 @@ def main():
     ap.add_argument("--tune", action="append", default=[], metavar="KNOB=VALUE",
                     help="launch-shape knob through fq_tune_set (abi.TUNE names; sweeps only, the defaults "
                          "are the measured best)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launch and rendezvous only (gloo, no GPU): rank 0 prints the ranks that arrived")
     args = ap.parse_args()
+
+    # --gpus N is the world size.  Without a launcher (no WORLD_SIZE) and N > 1,
+    # start N ranks and relay their status; under a launcher the two must agree.
+    if args.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1:
+            if args.dist_backend == "nccl" and not args.dry_run and torch.cuda.device_count() < args.gpus:
+                # (device_count() makes no HIP context on this image)
+                raise SystemExit("bench.py: --gpus %d with RCCL needs %d GPUs, %d visible (--dist-backend gloo "
+                                 "rehearses N ranks on fewer)" % (args.gpus, args.gpus, torch.cuda.device_count()))
+            sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    elif int(os.environ["WORLD_SIZE"]) != args.gpus:
+        raise SystemExit("bench.py: --gpus %d but the launcher started WORLD_SIZE=%s ranks"
+                         % (args.gpus, os.environ["WORLD_SIZE"]))
+    if args.dry_run:
+        return dry_run(int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")))
+
     args.tuned = {}
     for kv in args.tune:
         k, v = kv.split("=", 1)
@@ -565,6 +652,11 @@ def main():
         if not int(flag.item()) and comm is not None:  # every rank takes the same transport
             comm.close()
             comm = None
+    # the world the exchange really spans: the RCCL communicator's own count
+    # (fq_comm_info), else the torch.distributed group's
+    ranks_seen = comm.info()[1] if comm is not None else (dist.get_world_size() if world > 1 else 1)
+    if ranks_seen != args.gpus:
+        raise SystemExit("bench.py: --gpus %d but the exchange spans %d ranks" % (args.gpus, ranks_seen))
 
     # One step on one GPU is what a host binding the C ABI does
     # (INTEGRATION.md): fq_engine_execute, then the one result row's values
@@ -664,6 +756,7 @@ def main():
             "value": value,
             "unit": "rows/s",
             "n_gpus": world,
+            "ranks_seen": ranks_seen,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": dt / args.steps * 1e3,
@@ -711,8 +804,7 @@ def main():
             "result": res if args.query not in GROUP_MOD else (
                 {"groups": ngroups, "first": [int(c[0]) for c in res], "last": [int(c[-1]) for c in res]}
                 if world == 1 else {"groups": ngroups, "first": list(res[0]), "last": list(res[-1])}),
-            "host_ms_per_step": {"plan": st["plan_ms"] / args.steps, "first_launch": st["first_launch_ms"] / args.steps,
-                                 "exec": st["exec_ms"] / args.steps},
+            "host_ms_per_step": host_split(st, args.steps, dt / args.steps * 1e3, world),
             "jit": {"specialised_launches": jitted, "kernels_compiled": jit1["kernels_compiled"],
                     "compile_ms": jit1["compile_ms"], "mode": jit1["mode"]},
         }

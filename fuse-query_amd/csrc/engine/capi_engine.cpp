@@ -65,6 +65,14 @@ struct fq_engine {
 // the Function-handle ABI (capi_function.cpp) runs its device calls here
 fq::Runtime *fq_engine_runtime(fq_engine *e) { return e->rt.get(); }
 
+// the exchange (fq_comm.cpp) accounts its wall time, rounds and bytes here
+void fq_engine_note_exchange(fq_engine *e, int64_t ns, uint64_t rounds, uint64_t bytes) {
+    e->rt->stats.exchange_ns += (uint64_t)ns;
+    e->rt->stats.exchanges++;
+    e->rt->stats.exchange_rounds += rounds;
+    e->rt->stats.exchange_bytes += bytes;
+}
+
 namespace {
 
 template <typename F>
@@ -95,6 +103,13 @@ bool grow_group_table(fq_engine *e, const fq::FQException &ex, int attempt) {
 struct GroupCapacityReset {
     fq_engine *e;
     ~GroupCapacityReset() { e->rt->group_capacity.store(4096); }
+};
+
+// host wall time of one call into a stats counter (failed calls count too)
+struct PhaseTimer {
+    std::atomic<uint64_t> &acc;
+    int64_t t0 = fq::now_ns();
+    ~PhaseTimer() { acc += (uint64_t)(fq::now_ns() - t0); }
 };
 
 fq::QueryContextRef make_ctx(fq_engine *e, int rank, int world) {
@@ -324,6 +339,7 @@ fq_status fq_engine_execute_partial(fq_engine *e, const char *sql, int32_t rank,
                                     size_t cap, size_t *len) {
     if (!e || !sql || !len) return fqc::fail(FQ_E_INVALID, "fq_engine_execute_partial: NULL argument");
     if (world < 1 || rank < 0 || rank >= world) return fqc::fail(FQ_E_INVALID, "bad rank/world");
+    PhaseTimer timer{e->rt->stats.partial_ns};
     return guard([&] {
         fq::ExecCtx ctx(e->rt.get());
         auto qctx = make_ctx(e, rank, world);
@@ -361,6 +377,23 @@ fq_status fq_engine_execute_partial(fq_engine *e, const char *sql, int32_t rank,
                                                     std::to_string(enc.size()) + " bytes)");
         memcpy(buf, enc.data(), enc.size());
         e->rt->stats.queries++;
+    });
+}
+
+fq_status fq_engine_partial_state_bytes(fq_engine *e, const char *sql, size_t *bytes) {
+    if (!e || !sql || !bytes) return fqc::fail(FQ_E_INVALID, "fq_engine_partial_state_bytes: NULL argument");
+    *bytes = 0;
+    return guard([&] {
+        auto qctx = make_ctx(e, 0, 1);
+        fq::QueryPlan plan = plan_for(e, sql, *qctx);
+        const fq::PlanNode *agg = aggregate_node(plan);
+        if (plan.explain || !agg) throw fq::FQException(FQ_E_UNSUPPORTED, "distributed execution covers aggregate queries only");
+        if (!agg->groups.empty()) return;  // one row per group: known only after the scan
+        // fresh functions have the state vectors' final shape (Null records are
+        // 16 bytes like Some ones), so this is exactly encode_states' length
+        std::vector<std::vector<fq::DataValue>> per_func;
+        for (const auto &x : agg->exprs) per_func.push_back(x.to_function(qctx->factory)->accumulate_result());
+        *bytes = fq::encode_states(per_func).size();
     });
 }
 
@@ -448,6 +481,7 @@ fq_status fq_engine_execute_final(fq_engine *e, const char *sql, const void *sta
                                   fq_result **out) {
     if (!e || !sql || !states || !out || world < 1) return fqc::fail(FQ_E_INVALID, "fq_engine_execute_final: bad argument");
     *out = nullptr;
+    PhaseTimer timer{e->rt->stats.final_ns};
     return guard([&] {
         fq::ExecCtx ctx(e->rt.get());
         auto qctx = make_ctx(e, 0, 1);
@@ -518,6 +552,14 @@ fq_status fq_engine_get_stats(fq_engine *e, fq_engine_stats *out) {
     out->plan_ms = (double)e->rt->stats.plan_ns.load() * 1e-6;
     out->exec_ms = (double)e->rt->stats.exec_ns.load() * 1e-6;
     out->first_launch_ms = (double)e->rt->stats.first_launch_ns.load() * 1e-6;
+    out->partial_ms = (double)e->rt->stats.partial_ns.load() * 1e-6;
+    out->exchange_ms = (double)e->rt->stats.exchange_ns.load() * 1e-6;
+    out->final_ms = (double)e->rt->stats.final_ns.load() * 1e-6;
+    out->exchanges = e->rt->stats.exchanges.load();
+    out->exchange_rounds = e->rt->stats.exchange_rounds.load();
+    out->exchange_bytes = e->rt->stats.exchange_bytes.load();
+    out->cached_block_bytes = fq::block_cache_bytes();
+    out->cached_workspace_bytes = fq::block_cache_workspace_bytes();
     return FQ_OK;
 }
 
@@ -531,6 +573,12 @@ fq_status fq_engine_reset_stats(fq_engine *e) {
     e->rt->stats.plan_ns = 0;
     e->rt->stats.exec_ns = 0;
     e->rt->stats.first_launch_ns = 0;
+    e->rt->stats.partial_ns = 0;
+    e->rt->stats.exchange_ns = 0;
+    e->rt->stats.final_ns = 0;
+    e->rt->stats.exchanges = 0;
+    e->rt->stats.exchange_rounds = 0;
+    e->rt->stats.exchange_bytes = 0;
     return FQ_OK;
 }
 

@@ -298,7 +298,10 @@ const DataField &DataSchema::field_with_name(const std::string &name) const { re
 // Sizes are rounded up to classes (4 per power of two, <= 25 % slack) so that
 // blocks of one class are interchangeable; blocks above kMaxBlock are never
 // cached (they are rare and would crowd out the frequent small ones), each
-// queue keeps at most kStreamBytes and the whole cache kCacheBytes.  Every
+// queue keeps at most kStreamBytes and the whole cache kCacheBytes.  The one
+// large workspace a queue may keep is counted apart (ws_cached_, capped at
+// kWorkspaceBytes over all queues), so a kept GROUP BY workspace never takes
+// the small blocks' room.  Every
 // allocation failure -- stream-ordered, hipMalloc or the workspace -- calls
 // reclaim_device_memory(): the cache is flushed and the default pool trimmed
 // to 0, then the allocation is retried once.
@@ -308,6 +311,7 @@ class BlockCache {
     static constexpr size_t kCacheBytes = 6ull << 30;
     static constexpr size_t kStreamBytes = 2ull << 30;
     static constexpr size_t kMaxBlock = 1ull << 30;
+    static constexpr size_t kWorkspaceBytes = 32ull << 30;  // kept workspaces, all queues
     static BlockCache &get() {
         static BlockCache *c = new BlockCache();  // never destroyed: buffers may outlive statics
         return *c;
@@ -351,7 +355,7 @@ class BlockCache {
         if (f == free_.end() || !f->second.ws || f->second.ws_bytes < min_bytes) return nullptr;
         void *p = f->second.ws;
         *bytes = f->second.ws_bytes;
-        cached_ -= f->second.ws_bytes;
+        ws_cached_ -= f->second.ws_bytes;
         f->second.ws = nullptr;
         f->second.ws_bytes = 0;
         return p;
@@ -359,10 +363,10 @@ class BlockCache {
     bool put_workspace(hipStream_t s, void *p, size_t bytes) {
         std::lock_guard<std::mutex> lk(mu_);
         auto f = free_.find(s);
-        if (f == free_.end() || f->second.ws) return false;
+        if (f == free_.end() || f->second.ws || ws_cached_ + bytes > kWorkspaceBytes) return false;
         f->second.ws = p;
         f->second.ws_bytes = bytes;
-        cached_ += bytes;
+        ws_cached_ += bytes;
         return true;
     }
     // s is idle and about to be destroyed: free its blocks, stop caching on it
@@ -376,7 +380,7 @@ class BlockCache {
         }
         if (f->second.ws) {
             (void)hipFree(f->second.ws);
-            cached_ -= f->second.ws_bytes;
+            ws_cached_ -= f->second.ws_bytes;
         }
         free_.erase(f);
     }
@@ -394,10 +398,15 @@ class BlockCache {
             (void)hipStreamSynchronize(f.first);
         }
         cached_ = 0;
+        ws_cached_ = 0;
     }
     size_t cached_bytes() {
         std::lock_guard<std::mutex> lk(mu_);
         return cached_;
+    }
+    size_t cached_workspace_bytes() {
+        std::lock_guard<std::mutex> lk(mu_);
+        return ws_cached_;
     }
 
    private:
@@ -409,7 +418,8 @@ class BlockCache {
     };
     std::mutex mu_;
     std::unordered_map<hipStream_t, Queue> free_;
-    size_t cached_ = 0;
+    size_t cached_ = 0;     // small blocks (kCacheBytes / kStreamBytes caps)
+    size_t ws_cached_ = 0;  // kept workspaces (kWorkspaceBytes cap)
 };
 
 // One reusable ordering event per (thread, device) for cross-queue drops.
@@ -457,6 +467,7 @@ void reclaim_device_memory() {
 }
 
 size_t block_cache_bytes() { return BlockCache::get().cached_bytes(); }
+size_t block_cache_workspace_bytes() { return BlockCache::get().cached_workspace_bytes(); }
 
 Runtime::Runtime(int device) : device_(device) {
     if (device == kHostOnly) return;  // planning / AggregateFinal merges only

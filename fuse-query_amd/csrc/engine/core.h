@@ -136,6 +136,9 @@ struct EngineStats {
     std::atomic<uint64_t> scan_launches{0}, scan_rows{0}, scan_bytes{0}, queries{0};
     std::atomic<uint64_t> scan_ns{0};
     std::atomic<uint64_t> plan_ns{0}, exec_ns{0}, first_launch_ns{0};
+    // the distributed split: partial, the exchange (fq_comm.cpp), final
+    std::atomic<uint64_t> partial_ns{0}, exchange_ns{0}, final_ns{0};
+    std::atomic<uint64_t> exchanges{0}, exchange_rounds{0}, exchange_bytes{0};
     // query start (steady_clock ns) while a query runs; the first scan launch
     // of the query adds (launch - start) to first_launch_ns and clears it
     std::atomic<int64_t> query_t0{0};
@@ -243,7 +246,8 @@ size_t size_class(size_t bytes);
 // every allocation failure calls it before its one retry; also before large
 // long-lived allocations and through fq_engine_trim_memory.
 void reclaim_device_memory();
-size_t block_cache_bytes();
+size_t block_cache_bytes();            // cached small blocks
+size_t block_cache_workspace_bytes();  // kept per-queue workspaces (counted apart)
 
 // Execution context of the thread running a pipe (tokio task in the
 // reference, processor_merge.rs:45-63): its device queue and workspaces.

@@ -4,6 +4,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <string>
 #include <vector>
 
@@ -21,7 +22,15 @@ struct fq_comm {
     int64_t cap_words = 0;
 };
 
+// engine/capi_engine.cpp
+void fq_engine_note_exchange(fq_engine *e, int64_t ns, uint64_t rounds, uint64_t bytes);
+
 namespace {
+
+int64_t now_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
 
 // first bytes of an exchanged row that carries a rank's error instead of its
 // partial states (those start with "FQS1", pipeline.cpp encode_states)
@@ -54,7 +63,12 @@ fq_status run_partial(fq_engine *e, const char *sql, int32_t rank, int32_t world
 }
 
 // One all-reduce of a [world x row_words] buffer in which this rank filled its row.
+// rounds and bytes of this thread's last exchange (fq_engine_note_exchange)
+thread_local uint64_t t_rounds = 0, t_bytes = 0;
+
 fq_status exchange_round(std::vector<uint64_t> &buf, fq_allreduce_fn allreduce, void *user) {
+    t_rounds++;
+    t_bytes += buf.size() * 8;
     fqc::fail(FQ_OK, "");  // a callback that fails without a message gets the generic one
     fq_status st = allreduce(buf.data(), (int64_t)buf.size(), user);
     if (st != FQ_OK && fq_last_error()[0] == '\0') return fqc::fail(st, "state exchange: all-reduce failed");
@@ -65,28 +79,30 @@ fq_status exchange_round(std::vector<uint64_t> &buf, fq_allreduce_fn allreduce, 
 
 extern "C" {
 
-fq_status fq_exchange_states(const void *local, size_t len, int32_t rank, int32_t world, fq_allreduce_fn allreduce,
-                             void *user, const void **rows, size_t *stride) {
+fq_status fq_exchange_states_sized(const void *local, size_t len, size_t cap, int32_t rank, int32_t world,
+                                   fq_allreduce_fn allreduce, void *user, const void **rows, size_t *stride) {
     if ((!local && len) || !allreduce || !rows || !stride) return fqc::fail(FQ_E_INVALID, "fq_exchange_states: NULL argument");
     if (world < 1 || rank < 0 || rank >= world) return fqc::fail(FQ_E_INVALID, "bad rank/world");
     thread_local std::vector<uint8_t> states;
+    t_rounds = 0;
+    t_bytes = 0;
     fq_status st;
 
-    // Round 1: [length, first CAP bytes] per rank.
-    constexpr int64_t kCapWords = FQ_EXCHANGE_CAP_BYTES / 8;
-    const int64_t row1 = 1 + kCapWords;
+    // Round 1: [length, first `cap` bytes] per rank.
+    const int64_t cap_words = (int64_t)((cap + 7) / 8);
+    const int64_t row1 = 1 + cap_words;
     std::vector<uint64_t> buf((size_t)(world * row1), 0);
     buf[(size_t)(rank * row1)] = len;
-    if (len) memcpy(&buf[(size_t)(rank * row1 + 1)], local, std::min<size_t>(len, FQ_EXCHANGE_CAP_BYTES));
+    if (len) memcpy(&buf[(size_t)(rank * row1 + 1)], local, std::min<size_t>(len, (size_t)cap_words * 8));
     if ((st = exchange_round(buf, allreduce, user)) != FQ_OK) return st;
 
     uint64_t max_len = 0;
     for (int32_t r = 0; r < world; ++r) max_len = std::max<uint64_t>(max_len, buf[(size_t)(r * row1)]);
-    if (max_len <= (uint64_t)FQ_EXCHANGE_CAP_BYTES) {
-        *stride = FQ_EXCHANGE_CAP_BYTES;
+    if (max_len <= (uint64_t)cap_words * 8) {
+        *stride = (size_t)cap_words * 8;
         states.resize((size_t)world * *stride);
         for (int32_t r = 0; r < world; ++r)
-            memcpy(&states[(size_t)r * *stride], &buf[(size_t)(r * row1 + 1)], *stride);
+            if (*stride) memcpy(&states[(size_t)r * *stride], &buf[(size_t)(r * row1 + 1)], *stride);
     } else {
         // Round 2: every rank saw the same lengths, so every rank takes it.
         const int64_t row2 = (int64_t)((max_len + 7) / 8);
@@ -99,6 +115,11 @@ fq_status fq_exchange_states(const void *local, size_t len, int32_t rank, int32_
     }
     *rows = states.data();
     return FQ_OK;
+}
+
+fq_status fq_exchange_states(const void *local, size_t len, int32_t rank, int32_t world, fq_allreduce_fn allreduce,
+                             void *user, const void **rows, size_t *stride) {
+    return fq_exchange_states_sized(local, len, FQ_EXCHANGE_CAP_BYTES, rank, world, allreduce, user, rows, stride);
 }
 
 fq_status fq_engine_execute_exchange(fq_engine *e, const char *sql, int32_t rank, int32_t world,
@@ -119,9 +140,18 @@ fq_status fq_engine_execute_exchange(fq_engine *e, const char *sql, int32_t rank
         local.insert(local.end(), (const uint8_t *)&code, (const uint8_t *)&code + 4);
         local.insert(local.end(), msg.begin(), msg.begin() + (long)std::min<size_t>(msg.size(), FQ_EXCHANGE_CAP_BYTES - 16));
     }
+    // Round 1 sized to the states: an ungrouped aggregate's are the same size on
+    // every rank (fq_engine_partial_state_bytes, a function of the SQL alone), so
+    // one all-reduce of world x (8 + that) bytes carries them; GROUP BY rows
+    // (data-dependent) send lengths first.  Planning is deterministic, so a
+    // statement that fails to plan falls back to the same cap on every rank.
+    size_t cap = 0;
+    if (fq_engine_partial_state_bytes(e, sql, &cap) != FQ_OK) cap = FQ_EXCHANGE_CAP_BYTES;
     const void *rows = nullptr;
     size_t stride = 0;
-    fq_status xs = fq_exchange_states(local.data(), local.size(), rank, world, allreduce, user, &rows, &stride);
+    const int64_t t0 = now_ns();
+    fq_status xs = fq_exchange_states_sized(local.data(), local.size(), cap, rank, world, allreduce, user, &rows, &stride);
+    fq_engine_note_exchange(e, now_ns() - t0, t_rounds, t_bytes);
     if (xs != FQ_OK) return xs;
     for (int32_t r = 0; r < world; ++r) {
         const uint8_t *row = (const uint8_t *)rows + (size_t)r * stride;

@@ -22,13 +22,13 @@ fq_status hip_fail(hipError_t e, const char *what);
 // time each (profiles/r01_readme_limit_trace.txt)
 uint64_t *host_staging();
 
-int device_cu_count();
+int device_cu_count();  // CUs of the current device (cached per device)
 
 // Launch-shape knob FQ_TUNE_* (fq_knobs.cpp): the compiled-in default unless a
 // tuning tool set it through fq_tune_set; read at every launch.
 int64_t knob(int k);
 // fq_tune_jit_dump_dir's directory ("" = off)
-std::string jit_dump_dir();  // CUs of the current device (cached per device)
+std::string jit_dump_dir();
 
 const char *dtype_name(int32_t dt);  // arrow DataType Debug name ("UInt64", ...)
 int dtype_size(int32_t dt);          // bytes per value; 0 for non-primitive

@@ -32,12 +32,14 @@ COMM_ID_BYTES = 128
 STATE_CAP = 4096  # FQ_EXCHANGE_CAP_BYTES
 
 COMM_SYMBOLS = [
-    "fq_exchange_states", "fq_engine_execute_exchange", "fq_comm_unique_id", "fq_comm_init", "fq_comm_info",
+    "fq_exchange_states", "fq_exchange_states_sized", "fq_engine_execute_exchange", "fq_comm_unique_id", "fq_comm_init", "fq_comm_info",
     "fq_comm_destroy", "fq_state_allreduce", "fq_comm_allreduce_u64", "fq_engine_execute_rccl",
 ]
 _protos = {
     "fq_exchange_states": (C.c_int32, [C.c_void_p, C.c_size_t, C.c_int32, C.c_int32, ALLREDUCE_FN, C.c_void_p,
                                        P(C.c_void_p), P(C.c_size_t)]),
+    "fq_exchange_states_sized": (C.c_int32, [C.c_void_p, C.c_size_t, C.c_size_t, C.c_int32, C.c_int32, ALLREDUCE_FN,
+                                             C.c_void_p, P(C.c_void_p), P(C.c_size_t)]),
     "fq_engine_execute_exchange": (C.c_int32, [C.c_void_p, C.c_char_p, C.c_int32, C.c_int32, ALLREDUCE_FN,
                                                C.c_void_p, P(C.c_void_p)]),
     "fq_comm_unique_id": (C.c_int32, [C.c_void_p]),
@@ -93,6 +95,12 @@ class RcclComm:
         check(lib.fq_comm_init(device, self.world, self.rank, uid, C.byref(h)))
         self.h = h
 
+    def info(self):
+        """(rank, world) as the communicator sees them (fq_comm_info)."""
+        r, w = C.c_int32(-1), C.c_int32(-1)
+        check(lib.fq_comm_info(self.h, C.byref(r), C.byref(w)))
+        return r.value, w.value
+
     def allreduce_(self, words):
         """In-place wrapping u64 sum of a numpy uint64 array over all ranks."""
         assert words.dtype == np.uint64 and words.flags.c_contiguous
@@ -111,14 +119,20 @@ class RcclComm:
             pass
 
 
-def allgather_states(states, group=None):
+def allgather_states(states, group=None, cap=None):
     """bytes of this rank -> [bytes of rank 0, ..., rank world-1] (zero padded
-    to a common stride) through the native exchange over `group`."""
+    to a common stride) through the native exchange over `group`; `cap`: the
+    first round's payload bytes per rank (fq_exchange_states_sized; the same
+    on every rank), default FQ_EXCHANGE_CAP_BYTES."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     fn = torch_allreduce_fn(group)
     rows, stride = C.c_void_p(), C.c_size_t()
-    check(lib.fq_exchange_states(states, len(states), rank, world, fn, None, C.byref(rows), C.byref(stride)))
+    if cap is None:
+        check(lib.fq_exchange_states(states, len(states), rank, world, fn, None, C.byref(rows), C.byref(stride)))
+    else:
+        check(lib.fq_exchange_states_sized(states, len(states), cap, rank, world, fn, None, C.byref(rows),
+                                           C.byref(stride)))
     blob = C.string_at(rows, stride.value * world)
     return [blob[r * stride.value:(r + 1) * stride.value] for r in range(world)]
 

@@ -26,14 +26,17 @@ ENGINE_SYMBOLS = [
     "fq_engine_release_numbers", "fq_engine_trim_memory", "fq_engine_execute", "fq_engine_explain", "fq_engine_execute_partial",
     "fq_engine_execute_final", "fq_engine_get_stats", "fq_engine_reset_stats", "fq_result_num_rows",
     "fq_result_num_columns", "fq_result_column_name", "fq_result_column_type", "fq_result_value",
-    "fq_result_text", "fq_result_free", "fq_result_mysql_type", "fq_result_values",
+    "fq_result_text", "fq_result_free", "fq_result_mysql_type", "fq_result_values", "fq_engine_partial_state_bytes",
 ]
 
 
 class fq_engine_stats(C.Structure):
     _fields_ = [("scan_launches", C.c_uint64), ("scan_rows", C.c_uint64), ("scan_bytes", C.c_uint64),
                 ("scan_ms", C.c_double), ("queries", C.c_uint64), ("plan_ms", C.c_double),
-                ("exec_ms", C.c_double), ("first_launch_ms", C.c_double)]
+                ("exec_ms", C.c_double), ("first_launch_ms", C.c_double), ("partial_ms", C.c_double),
+                ("exchange_ms", C.c_double), ("final_ms", C.c_double), ("exchanges", C.c_uint64),
+                ("exchange_rounds", C.c_uint64), ("exchange_bytes", C.c_uint64),
+                ("cached_block_bytes", C.c_uint64), ("cached_workspace_bytes", C.c_uint64)]
 
 
 _protos = {
@@ -49,6 +52,7 @@ _protos = {
                                               C.c_size_t, P(C.c_size_t)]),
     "fq_engine_execute_final": (C.c_int32, [C.c_void_p, C.c_char_p, C.c_void_p, C.c_size_t, C.c_int32,
                                             P(C.c_void_p)]),
+    "fq_engine_partial_state_bytes": (C.c_int32, [C.c_void_p, C.c_char_p, P(C.c_size_t)]),
     "fq_engine_get_stats": (C.c_int32, [C.c_void_p, P(fq_engine_stats)]),
     "fq_engine_reset_stats": (C.c_int32, [C.c_void_p]),
     "fq_result_num_rows": (C.c_int64, [C.c_void_p]),
@@ -255,6 +259,13 @@ class Engine:
                 continue
             check(st)
             return C.string_at(buf, n.value)
+
+    def partial_state_bytes(self, sql):
+        """fq_engine_partial_state_bytes: the partial states' size on every rank
+        (0 when it depends on the data, GROUP BY)."""
+        n = C.c_size_t(0)
+        check(lib.fq_engine_partial_state_bytes(self.h, sql.encode(), C.byref(n)))
+        return n.value
 
     def execute_final(self, sql, states, stride=None):
         """AggregateFinal over per-rank serialised states (list of bytes, rank order)."""

@@ -29,7 +29,9 @@ SCALAR_NULL, SCALAR_NONE, SCALAR_SOME = 0, 1, 2
 
 
 class fq_scalar(C.Structure):
-    _fields_ = [("kind", C.c_int32), ("dtype", C.c_int32), ("bits", C.c_uint64), ("str", C.c_char_p),
+    # str is a raw address: Utf8 payloads carry str_len and may hold NUL bytes
+    # (a c_char_p field would hand back a copy cut at the first NUL)
+    _fields_ = [("kind", C.c_int32), ("dtype", C.c_int32), ("bits", C.c_uint64), ("str", C.c_void_p),
                 ("str_len", C.c_uint64)]
 
 
@@ -105,7 +107,8 @@ class DataValue:
         s.kind = SCALAR_SOME
         if s.dtype == abi.DT_UTF8:
             raw = self.value.encode()
-            s.str = raw
+            s._buf = C.create_string_buffer(raw, max(1, len(raw)))  # the scalar keeps its bytes alive
+            s.str = C.addressof(s._buf)
             s.str_len = len(raw)
         else:
             s.bits = to_bits(self.value, s.dtype)
@@ -119,7 +122,7 @@ class DataValue:
         if s.kind == SCALAR_NONE:
             return DataValue(name, None)
         if s.dtype == abi.DT_UTF8:
-            return DataValue(name, C.string_at(s.str, s.str_len).decode())
+            return DataValue(name, C.string_at(s.str, s.str_len).decode() if s.str_len else "")
         return DataValue(name, from_bits(s.bits, s.dtype))
 
 

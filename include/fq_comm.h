@@ -12,10 +12,11 @@
  *   every rank writes its serialised states (fq_engine_execute_partial) into
  *   its own row of a zeroed [world x (1 + cap/8)] u64 buffer (word 0 = length)
  *   and a wrapping u64 SUM all-reduce turns that into an all-gather (each word
- *   has exactly one non-zero contributor -> bit-exact).  States longer than
- *   `cap` (GROUP BY states grow with the groups) are re-sent in a second
- *   all-reduce sized by the lengths every rank now knows, so all ranks take
- *   the same number of collectives.  AggregateFinal then merges in rank order
+ *   has exactly one non-zero contributor -> bit-exact).  cap is the states'
+ *   size when the SQL fixes it (ungrouped aggregates), else 0.  States longer
+ *   than `cap` (GROUP BY states grow with the groups, error records) are sent
+ *   in a second all-reduce sized by the lengths every rank now knows, so all
+ *   ranks take the same number of collectives.  AggregateFinal then merges in rank order
  *   on every rank (fq_engine_execute_final), so all ranks agree.
  *
  * Host-language neutral: the collective is a callback, so the same protocol
@@ -50,6 +51,14 @@ typedef fq_status (*fq_allreduce_fn)(uint64_t *buf, int64_t n_words, void *user)
  * valid until the next call on this thread.  Collective: every rank calls. */
 fq_status fq_exchange_states(const void *local, size_t len, int32_t rank, int32_t world, fq_allreduce_fn allreduce,
                              void *user, const void **rows, size_t *stride);
+/* The same with round 1 carrying `cap` payload bytes per rank (rounded up to
+ * 8; every rank must pass the same cap).  A string longer than cap on any
+ * rank sends every rank through round 2.  cap = 0: round 1 carries only the
+ * lengths.  fq_engine_execute_exchange passes fq_engine_partial_state_bytes,
+ * so an ungrouped aggregate takes ONE all-reduce of world x (8 + its states)
+ * bytes (C3 at world 8: 8 x 104 B) and GROUP BY rows send lengths first.    */
+fq_status fq_exchange_states_sized(const void *local, size_t len, size_t cap, int32_t rank, int32_t world,
+                                   fq_allreduce_fn allreduce, void *user, const void **rows, size_t *stride);
 
 /* Distributed aggregate query on rank `rank` of `world`: partial on this
  * rank's shard -> exchange through `allreduce` -> AggregateFinal in rank

@@ -60,6 +60,18 @@ typedef struct fq_engine_stats {
     double plan_ms;         /* host: SQL parse + plan + PipelineBuilder, summed   */
     double exec_ms;         /* host: pipeline execution until the result block    */
     double first_launch_ms; /* host: query start -> first scan enqueued, summed   */
+    /* the distributed split (fq_engine_execute_partial / _final and the
+     * exchange between them, fq_comm.h), host wall time summed over calls    */
+    double partial_ms;       /* fq_engine_execute_partial                      */
+    double exchange_ms;      /* the exchange's all-reduce rounds (incl. waiting
+                                for the slowest rank to arrive)                */
+    double final_ms;         /* fq_engine_execute_final                        */
+    uint64_t exchanges;      /* exchanges run                                  */
+    uint64_t exchange_rounds; /* all-reduce rounds those took (1 or 2 each)    */
+    uint64_t exchange_bytes; /* bytes all-reduced, summed over rounds          */
+    /* gauges (the process's device block cache now; not reset) */
+    uint64_t cached_block_bytes;     /* idle small blocks kept for reuse       */
+    uint64_t cached_workspace_bytes; /* idle per-queue GROUP BY workspaces     */
 } fq_engine_stats;
 
 /* device: HIP device ordinal.  Fails with FQ_E_HIP when no GPU is present.
@@ -97,6 +109,13 @@ fq_status fq_engine_explain(fq_engine *e, const char *sql, char *buf, size_t cap
  * size needed.                                                              */
 fq_status fq_engine_execute_partial(fq_engine *e, const char *sql, int32_t rank, int32_t world,
                                     void *buf, size_t cap, size_t *len);
+/* Size in bytes of the serialised partial states fq_engine_execute_partial
+ * produces for `sql` on ANY rank: an ungrouped aggregate's states have one
+ * fixed-size record per state value of each function (the shape of
+ * accumulate_result(), function.rs:28-131), so every rank can size the
+ * exchange without first exchanging lengths.  0 when the size depends on the
+ * data (GROUP BY: one row per group).                                       */
+fq_status fq_engine_partial_state_bytes(fq_engine *e, const char *sql, size_t *bytes);
 /* AggregateFinal over `world` serialised partial states laid out back to back
  * with a stride of `stride` bytes (rank order). */
 fq_status fq_engine_execute_final(fq_engine *e, const char *sql, const void *states, size_t stride,

@@ -1,10 +1,14 @@
 """CPU checks of bench.py's bookkeeping (no kernel runs): roofline.traffic
-comes from the last committed PMC summary measured on the current kernel
-sources, never from a stale one that merely sorts later by name, and a stale
-one is reported as such with its file and commit."""
+comes from the most recently measured committed PMC summary of the current
+kernel sources, never from a stale one or an older one that merely sorts later
+by name, and a stale one is reported as such with its file and commit; and
+`--gpus N` is the world size -- without a launcher bench.py starts N ranks
+itself, under one it refuses a different WORLD_SIZE."""
 import importlib.util
 import json
 import os
+import subprocess
+import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -16,8 +20,8 @@ def _bench():
     return m
 
 
-def _summary(path, sha, per_launch, rows=1000, commit="abc"):
-    json.dump({"measured_at_commit": commit, "query_sources_sha256": sha,
+def _summary(path, sha, per_launch, rows=1000, commit="abc", when=None):
+    json.dump({"measured_at_commit": commit, "query_sources_sha256": sha, "measured_at_unix": when,
                "kernels": [{"name": "agg_flat_kernel<...>", "hbm_bytes_per_launch": per_launch,
                             "rows_per_launch": rows}]}, open(path, "w"))
 
@@ -49,3 +53,63 @@ def test_traffic_reports_a_stale_file_when_none_is_current(tmp_path, monkeypatch
     t, src = b.latest_pmc_traffic("agg_flat", "c3", 2000)
     assert t is None and src["status"].startswith("no PMC summary")
 
+
+
+def test_traffic_takes_the_newest_measurement_not_the_last_name(tmp_path, monkeypatch):
+    # r03_s4_head_* sorts after r03_s4_final_* by name but was measured first
+    b = _bench()
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    cur = b.kernel_sources_sha256("c3")
+    _summary(prof / "r03_s4_final_pmc_c3.json", cur, 8000.0, commit="later", when=2000.0)
+    _summary(prof / "r03_s4_head_pmc_c3.json", cur, 8100.0, commit="earlier", when=1000.0)
+    _summary(prof / "r03_s4_zzz_pmc_c3.json", cur, 9000.0, commit="unstamped")  # no stamp: oldest
+    monkeypatch.setattr(b, "ROOT", str(tmp_path))
+    t, src = b.latest_pmc_traffic("agg_flat", "c3", 1000)
+    assert t == 8000.0 and src["file"] == "profiles/r03_s4_final_pmc_c3.json"
+    assert src["measured_at_commit"] == "later" and src["measured_at_unix"] == 2000.0
+
+
+def test_committed_summaries_carry_a_measurement_time():
+    # every committed summary bench.py may pick from has its measurement order
+    import glob
+    for f in glob.glob(os.path.join(ROOT, "profiles", "r0[3-9]*pmc_*.json")):
+        d = json.load(open(f))
+        if d.get("measured_at_commit"):
+            assert d.get("measured_at_unix"), f
+
+
+def _run_bench(args, env_extra=None, timeout=240):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra or {})
+    env["OMP_NUM_THREADS"] = "1"
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
+                          timeout=timeout, env=env, cwd=ROOT)
+
+
+def test_gpus_n_without_a_launcher_starts_n_ranks():
+    # no WORLD_SIZE: bench.py runs torch.distributed.run itself; every rank
+    # joins the (gloo) rendezvous and rank 0 reports who arrived
+    p = _run_bench(["--gpus", "3", "--dry-run"])
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    out = json.loads(lines[0])
+    assert out["dry_run"] and out["n_gpus"] == 3
+    assert sorted(r[0] for r in out["ranks"]) == [0, 1, 2]
+    assert len({r[2] for r in out["ranks"]}) == 3  # three processes
+    assert "launching 3 ranks" in p.stderr
+
+
+def test_gpus_and_launcher_world_mismatch_exits_nonzero():
+    p = _run_bench(["--gpus", "2", "--dry-run"], {"WORLD_SIZE": "3", "RANK": "0", "LOCAL_RANK": "0"}, timeout=120)
+    assert p.returncode != 0
+    assert "--gpus 2 but the launcher started WORLD_SIZE=3" in p.stderr
+    p = _run_bench(["--gpus", "1", "--dry-run"], {"WORLD_SIZE": "8", "RANK": "0", "LOCAL_RANK": "0"}, timeout=120)
+    assert p.returncode != 0 and "WORLD_SIZE=8" in p.stderr
+
+
+def test_gpus_n_with_rccl_needs_n_visible_gpus():
+    # no GPU here: asking for 2 RCCL ranks fails before anything starts
+    p = _run_bench(["--gpus", "2"], timeout=120)
+    assert p.returncode != 0 and "needs 2 GPUs, 0 visible" in p.stderr

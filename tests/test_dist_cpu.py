@@ -47,10 +47,12 @@ def worker(rank, world, port, n, out_q):
                  R.E_fn("min", num), R.E_fn("count", num)]
         mine = [(b, e) for _, b, e in shard(generate_parts(n), rank, world)]
         local = encode_states(R.aggregate_partial_states(n, exprs, mine))
-        everyone = fqd.allgather_states(local)
         with Engine(device=-1) as eng:
+            # round 1 sized to the states (what fq_engine_execute_exchange does)
+            cap = eng.partial_state_bytes(SQL % n)
+            everyone = fqd.allgather_states(local, cap=cap)
             rows = eng.execute_final(SQL % n, everyone).rows
-        out_q.put((rank, rows, [len(s) for s in everyone]))
+        out_q.put((rank, rows, [len(s) for s in everyone] + [len(local), cap]))
     finally:
         dist.destroy_process_group()
 
@@ -74,6 +76,9 @@ def test_sharded_exchange_and_final_merge(world, n):
         R.E_fn("count", num)]))]
     for rank, rows, lens in results:
         assert rows == exp, (rank, rows, exp)
+        # every rank's states are exactly the planned size: one round, stride = that size
+        *strides, local_len, cap = lens
+        assert local_len == cap and strides == [(cap + 7) // 8 * 8] * world, (rank, lens)
 
 
 GB_SQL = "SELECT number%%97, count(number), sum(number), min(number+3) FROM system.numbers_mt(%d) GROUP BY number%%97"
@@ -128,7 +133,7 @@ def test_group_by_exchange_and_final_merge():
         assert rows == exp, rank
 
 
-def ragged_worker(rank, world, port, lens, out_q):
+def ragged_worker(rank, world, port, lens, out_q, cap=None):
     for p in (os.path.join(ROOT, "fuse-query_amd"),):
         sys.path.insert(0, p)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -140,29 +145,32 @@ def ragged_worker(rank, world, port, lens, out_q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         mine = bytes((rank * 31 + i) % 251 + 1 for i in range(lens[rank]))
-        rows = fqd.allgather_states(mine)
+        rows = fqd.allgather_states(mine, cap=cap)
         out_q.put((rank, rows))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("lens", [(5000, 40), (0, 0, 7), (4096, 4097, 1), (10, 20)])
-def test_exchange_protocol_ragged_lengths(lens):
-    """fq_exchange_states: every rank takes the same number of all-reduces
-    even when only SOME ranks' states exceed the 4 KB first round (a per-rank
-    decision would leave the others waiting in a collective)."""
+@pytest.mark.parametrize("lens,cap", [((5000, 40), None), ((0, 0, 7), None), ((4096, 4097, 1), None), ((10, 20), None),
+                                      ((10, 20), 0), ((96, 96, 97), 96), ((96, 96, 96), 96), ((3, 0), 5)])
+def test_exchange_protocol_ragged_lengths(lens, cap):
+    """fq_exchange_states(_sized): every rank takes the same number of
+    all-reduces even when only SOME ranks' states exceed the first round's
+    cap (a per-rank decision would leave the others waiting in a collective);
+    cap None = FQ_EXCHANGE_CAP_BYTES, 0 = lengths only in round 1."""
     world = len(lens)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
-    procs = [ctx.Process(target=ragged_worker, args=(r, world, port, lens, q)) for r in range(world)]
+    procs = [ctx.Process(target=ragged_worker, args=(r, world, port, lens, q, cap)) for r in range(world)]
     for p in procs:
         p.start()
     results = [q.get(timeout=240) for _ in range(world)]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    stride = 4096 if max(lens) <= 4096 else (max(lens) + 7) // 8 * 8
+    c8 = ((4096 if cap is None else cap) + 7) // 8 * 8
+    stride = c8 if max(lens) <= c8 else (max(lens) + 7) // 8 * 8
     for rank, rows in results:
         assert len(rows) == world
         for r, row in enumerate(rows):
@@ -246,8 +254,11 @@ def c5_worker(rank, world, port, n, out_q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         mine = shard(generate_parts(n), rank, world)
-        everyone = fqd.allgather_states(encode_states(closed_form_states(mine)))
         with Engine(device=-1) as eng:
+            local = encode_states(closed_form_states(mine))
+            cap = eng.partial_state_bytes(SQL % n)
+            assert len(local) == cap  # a rank owning nothing ships Null states of the same size
+            everyone = fqd.allgather_states(local, cap=cap)
             rows = eng.execute_final(SQL % n, everyone).rows
         out_q.put((rank, [name for name, _, _ in mine], rows))
     finally:

@@ -170,30 +170,39 @@ def test_native_rccl_comm_single_rank():
 
 
 def test_world8_bench_rehearsal_on_one_gpu():
-    """bench.py's world > 1 path at the C5 shape: 8 ranks (torch.distributed.run,
-    gloo) share the box's one GPU, numbers_mt(1e10) split into one 10 GB
-    partition per rank (80 GB resident in total), the partial states exchanged
-    through the native protocol, every rank's final checked against the closed
-    form inside bench.py (it exits non-zero on a mismatch).  The driver's 8-GPU
-    run differs only in the transport (RCCL) and one GPU per rank."""
+    """bench.py's world > 1 path at the C5 shape, started the way the driver's
+    bench command is (`python3 bench.py --gpus 8 ...`, NO external launcher:
+    bench.py starts the 8 ranks itself): the ranks (gloo) share the box's one
+    GPU, numbers_mt(1e10) split into one 10 GB partition per rank (80 GB
+    resident in total), the partial states exchanged through the native
+    protocol in one all-reduce sized to them, every rank's final checked against
+    the closed form inside bench.py (it exits non-zero on a mismatch).  The
+    driver's 8-GPU run differs only in the transport (RCCL) and one GPU per rank."""
     import json
     import subprocess
     n = 10_000_000_000
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
-           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
-           os.path.join(ROOT, "bench.py"), "--gpus", "8", "--rows-total", str(n), "--dist-backend", "gloo",
-           "--steps", "2", "--warmup", "1", "--no-cpu-baseline"]
-    env = dict(os.environ, OMP_NUM_THREADS="2")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--rows-total", str(n),
+           "--dist-backend", "gloo", "--steps", "3", "--warmup", "1", "--no-cpu-baseline"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["OMP_NUM_THREADS"] = "2"
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=280, env=env, cwd=ROOT)
+    if os.path.isdir(os.path.join(ROOT, "gpurun_out")):  # evidence for profiles/
+        with open(os.path.join(ROOT, "gpurun_out", "world8_rehearsal.log"), "w") as fh:
+            fh.write("$ " + " ".join(cmd[1:]) + "\n" + p.stderr + p.stdout)
     assert p.returncode == 0, p.stderr[-3000:]
+    assert "launching 8 ranks" in p.stderr
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, p.stdout[-2000:]
     out = json.loads(lines[0])
-    if os.path.isdir(os.path.join(ROOT, "gpurun_out")):  # evidence for profiles/
+    if os.path.isdir(os.path.join(ROOT, "gpurun_out")):
         with open(os.path.join(ROOT, "gpurun_out", "world8_rehearsal.json"), "w") as fh:
             fh.write(lines[0] + "\n")
-    assert out["n_gpus"] == 8 and out["scaling"] == "strong"
+    assert out["n_gpus"] == 8 and out["ranks_seen"] == 8 and out["scaling"] == "strong"
     assert out["config"]["rows_total"] == n and out["config"]["partitions_per_gpu"] == 1
     s = n * (n - 1) // 2 % 2**64
     assert out["result"] == [s // n, n - 1, 0]
     assert "== closed form" in p.stderr
+    h = out["host_ms_per_step"]
+    # one all-reduce per step, of 8 ranks x (8 B length + 96 B of C3 states)
+    assert h["exchange_rounds"] == 1 and h["exchange_bytes"] == 8 * 104
+    assert h["exchange"] > 0 and h["partial"] > 0 and h["final"] > 0

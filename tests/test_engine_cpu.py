@@ -221,3 +221,33 @@ def test_group_by_plan_errors(eng):
 def test_explain_logic_predicate(eng):
     txt = eng.explain("SELECT sum(number) FROM system.numbers_mt(80000) WHERE number > 1 AND number < 5")
     assert "Filter: ((number > 1) AND (number < 5))" in txt
+
+
+@pytest.mark.parametrize("exprs,nvals", [
+    ("sum(number)/count(number), max(number), min(number)", [2, 1, 1]),  # C3
+    ("sum(number)", [1]),  # C2
+    ("max(number+1), count(number)", [1, 1]),
+    ("(sum(number)+1)*max(number)", [3]),  # the constant has a state value too (function_constant.rs)
+])
+def test_partial_state_bytes_is_the_states_size_on_every_rank(eng, exprs, nvals):
+    """fq_engine_partial_state_bytes: the serialised partial states' size is a
+    function of the SQL alone (one 16-byte record per accumulate_result value,
+    function.rs:28-131), so the exchange sizes its one all-reduce without first
+    exchanging lengths; the oracle's states (Null on a rank that owns nothing,
+    Some elsewhere) all encode to it."""
+    sql = "SELECT %s FROM system.numbers_mt(%%d)" % exprs
+    exp = 8 + sum(8 + 16 * k for k in nvals)
+    for n in (7, 1000000):
+        assert eng.partial_state_bytes(sql % n) == exp
+    if exprs.startswith("sum(number)/"):
+        num = R.E_field("number")
+        fs = [R.E_bin("/", R.E_fn("sum", num), R.E_fn("count", num)), R.E_fn("max", num), R.E_fn("min", num)]
+        for parts in ([], [(b, e) for _, b, e in generate_parts(1000000)][:3]):
+            assert len(encode_states(R.aggregate_partial_states(1000000, fs, parts))) == exp
+
+
+def test_partial_state_bytes_group_by_and_errors(eng):
+    # GROUP BY states grow with the groups: 0 = lengths go first
+    assert eng.partial_state_bytes("SELECT number%10, count(number) FROM system.numbers_mt(100) GROUP BY number%10") == 0
+    with pytest.raises(FQError, match="aggregate queries only"):
+        eng.partial_state_bytes("SELECT number FROM system.numbers_mt(100)")

@@ -156,3 +156,15 @@ def test_device_calls_need_a_gpu():
     with pytest.raises(FQError) as ei:
         sum_a().accumulate(e, b)
     assert ei.value.status == abi.FQ_E_HIP
+
+
+@pytest.mark.parametrize("text", ["a\x00bc", "\x00", "", "plain", "x" * 300 + "\x00" + "y"])
+def test_utf8_scalar_with_nul_bytes_round_trips(text):
+    # fq_scalar carries (str, str_len): a Utf8 DataValue may hold NUL bytes and
+    # must come back whole through the ABI (ConstantFunction state protocol)
+    c = ConstantFunction.try_create(V("Utf8", text))
+    assert c.merge_result() == V("Utf8", text)
+    assert c.accumulate_result() == [V("Utf8", text)]
+    c2 = c.clone()
+    c2.merge_state([V("Utf8", text + "\x00tail")])  # a constant keeps its own value (function_constant.rs)
+    assert c2.merge_result() == V("Utf8", text)

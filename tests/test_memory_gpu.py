@@ -72,3 +72,29 @@ def test_trim_memory_returns_held_memory(Engine):
         _stream(e)  # and the engine still runs afterwards
     finally:
         e.close()
+
+
+def test_kept_group_by_workspaces_leave_the_small_block_cache_room(Engine):
+    """A partitioned GROUP BY keeps one ~3.4 GB workspace per queue for the next
+    query (DeviceBuffer::alloc_workspace).  Those are counted apart from the
+    small-block cache's 6 GB cap: with two queues the kept workspaces alone pass
+    6 GB, and the small blocks of the next row pipeline must still be cached."""
+    import torch
+    torch.cuda.empty_cache()
+    e = Engine(streams=2)
+    try:
+        e.trim_memory()
+        n = 8_000_000_000  # 1e9-row partitions, generated in 4e8-row chunks
+        r = e.execute("SELECT number%%100000, count(number) FROM system.numbers_mt(%d) GROUP BY number%%100000" % n)
+        assert len(r.rows) == 100000 and r.rows[0] == (0, n // 100000) and r.rows[-1] == (99999, n // 100000)
+        ws = e.stats()["cached_workspace_bytes"]
+        assert ws > 6 * GB, ws  # one per queue, beyond the small-block cap together
+        _stream(e)
+        st = e.stats()
+        assert st["cached_block_bytes"] > 0, st
+        assert st["cached_workspace_bytes"] == ws
+        e.trim_memory()
+        st = e.stats()
+        assert st["cached_block_bytes"] == 0 and st["cached_workspace_bytes"] == 0
+    finally:
+        e.close()
