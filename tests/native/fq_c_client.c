@@ -12,11 +12,20 @@
  *  3. engine ABI: fq_engine_create -> materialise numbers_mt(N) -> the C3
  *     statement through fq_engine_execute -> fq_result values, checked
  *     against the closed forms.
- * Prints one "OK ..." line per check; exits non-zero on the first failure. */
+ * Prints one "OK ..." line per check; exits non-zero on the first failure.
+ *
+ * `fq_c_client --bench STEPS TOTAL [WARMUP]`: the timed drop-in stack (C, the
+ * /opt/rocm runtime, no torch): materialise numbers_mt(TOTAL) in HBM, then
+ * STEPS x the C3 statement through fq_engine_execute with the engine's
+ * per-scan HIP events on (FQ_OPT_PROFILE), every result checked against the
+ * closed form; prints one JSON line (rows/s, ms per step, the scan kernel's
+ * average event time and its fraction of the 8 TB/s HBM peak).           */
+#define _POSIX_C_SOURCE 199309L /* clock_gettime under -std=c11 */
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include <hip/hip_runtime_api.h>
 
@@ -102,7 +111,71 @@ static void engine_abi(uint64_t total) {
     fq_engine_destroy(e);
 }
 
+static double now_s(void) {
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return (double)t.tv_sec + (double)t.tv_nsec * 1e-9;
+}
+
+static void c3_row(fq_engine *e, const char *sql, uint64_t out[3]) {
+    fq_result *r = NULL;
+    CHECK(fq_engine_execute(e, sql, &r) == FQ_OK, "execute: %s", fq_last_error());
+    for (int c = 0; c < 3; ++c) out[c] = value_u64(r, c);
+    fq_result_free(r);
+}
+
+static int bench(int steps, uint64_t total, int warmup) {
+    fq_engine *e = NULL;
+    CHECK(fq_engine_create(0, &e) == FQ_OK, "engine: %s", fq_last_error());
+    CHECK(fq_engine_set_option(e, FQ_OPT_PROFILE, 1) == FQ_OK, "profile: %s", fq_last_error());
+    CHECK(fq_engine_materialize_numbers(e, total, 0, 1) == FQ_OK, "materialise: %s", fq_last_error());
+    char sql[256];
+    snprintf(sql, sizeof sql,
+             "SELECT sum(number)/count(number), max(number), min(number) FROM system.numbers_mt(%llu)",
+             (unsigned long long)total);
+    const uint64_t sum = (uint64_t)((unsigned __int128)total * (total - 1) / 2);
+    const uint64_t expect[3] = {sum / total, total - 1, 0};
+    uint64_t got[3];
+    for (int i = 0; i < (warmup > 0 ? warmup : 1); ++i) c3_row(e, sql, got);
+    CHECK(memcmp(got, expect, sizeof got) == 0, "C3 = %llu %llu %llu", (unsigned long long)got[0],
+          (unsigned long long)got[1], (unsigned long long)got[2]);
+    CHECK(fq_engine_reset_stats(e) == FQ_OK, "reset stats");
+    CHECK(hipDeviceSynchronize() == hipSuccess, "sync");
+    int bad = 0;
+    const double t0 = now_s();
+    for (int i = 0; i < steps; ++i) {
+        c3_row(e, sql, got);  /* the result row is on the host when execute returns */
+        bad |= memcmp(got, expect, sizeof got) != 0;
+    }
+    CHECK(hipDeviceSynchronize() == hipSuccess, "sync");
+    const double dt = now_s() - t0;
+    CHECK(!bad, "a timed step returned another result");
+    fq_engine_stats st;
+    CHECK(fq_engine_get_stats(e, &st) == FQ_OK, "stats");
+    const double launches = st.scan_launches ? (double)st.scan_launches : 1.0;
+    const double kms = st.scan_ms / launches, bytes = (double)st.scan_bytes / launches;
+    const double gbps = bytes / (kms * 1e-3) / 1e9;
+    printf("{\"path\": \"fq_c_client (C host, libfq_amd.so + /opt/rocm libamdhip64, no torch): fq_engine_execute "
+           "of the C3 statement\", \"workload\": \"%s\", \"steps\": %d, \"warmup\": %d, \"value\": %.6g, "
+           "\"unit\": \"rows/s\", \"ms_per_step\": %.6g, \"scan_launches_per_step\": %.6g, "
+           "\"kernel_ms_per_launch\": %.6g, \"bytes_per_launch\": %.6g, \"achieved_hbm_gbps\": %.6g, "
+           "\"frac\": %.6g, \"host_ms_per_step\": {\"plan\": %.6g, \"first_launch\": %.6g, \"exec\": %.6g}, "
+           "\"result\": [%llu, %llu, %llu]}\n",
+           sql, steps, warmup, (double)total * steps / dt, dt / steps * 1e3, (double)st.scan_launches / steps, kms,
+           bytes, gbps, gbps / 8000.0, st.plan_ms / steps, st.first_launch_ms / steps, st.exec_ms / steps,
+           (unsigned long long)got[0], (unsigned long long)got[1], (unsigned long long)got[2]);
+    fq_engine_destroy(e);
+    return 0;
+}
+
 int main(int argc, char **argv) {
+    if (argc > 1 && strcmp(argv[1], "--bench") == 0) {
+        const int steps = argc > 2 ? atoi(argv[2]) : 20;
+        const uint64_t total = argc > 3 ? strtoull(argv[3], NULL, 10) : 10000000000ull;
+        const int warmup = argc > 4 ? atoi(argv[4]) : 3;
+        CHECK(steps > 0 && total >= 8, "usage: fq_c_client --bench STEPS TOTAL [WARMUP]");
+        return bench(steps, total, warmup);
+    }
     const uint64_t n = argc > 1 ? strtoull(argv[1], NULL, 10) : 100000003ull;
     const uint64_t total = argc > 2 ? strtoull(argv[2], NULL, 10) : 1000000000ull;
     int32_t devices = 0;

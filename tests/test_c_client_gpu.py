@@ -37,3 +37,25 @@ def test_c_client_fails_loudly_without_gpu():
         pytest.skip("a GPU is visible")
     p = run()
     assert p.returncode == 1 and "FAIL" in p.stderr
+
+
+@pytest.mark.gpu
+def test_c_client_c3_full_size_timed():
+    """The drop-in stack a Rust host would run (C, libfq_amd.so on the /opt/rocm
+    HIP runtime, no torch in the process), timed: numbers_mt(1e10) resident,
+    10 x the C3 statement through fq_engine_execute with the engine's per-scan
+    HIP events, every result equal to the closed form."""
+    import json
+    n = 10_000_000_000
+    p = subprocess.run([BIN, "--bench", "10", str(n), "2"], capture_output=True, text=True, timeout=180)
+    assert p.returncode == 0, p.stderr
+    out = json.loads(p.stdout.strip().splitlines()[-1])
+    s = n * (n - 1) // 2 % 2**64
+    assert out["result"] == [s // n, n - 1, 0]
+    assert out["scan_launches_per_step"] == 8 and out["bytes_per_launch"] == 8 * n / 8
+    # the fused scan streams near the HBM roofline on this stack too (0.9 with torch's runtime)
+    assert out["frac"] > 0.8, out
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    if os.path.isdir(os.path.join(root, "gpurun_out")):
+        with open(os.path.join(root, "gpurun_out", "c_client_bench_c3.json"), "w") as fh:
+            fh.write(p.stdout)
