@@ -74,9 +74,9 @@ QUERIES = {
 GROUP_MOD = {"g1": 1000, "g2": 100000}
 # not a BASELINE config: FilterTransform -> ProjectionTransform (SURVEY 8f rank
 # 1), the README's expressions without its LIMIT.  Its result is 3.75e9 rows x 2
-# columns (60 GB): measured at the C ABI the engine's ProjectionTransform calls
-# per block (fq_filter_project over each resident numbers_mt partition, outputs
-# in HBM), checked by kept count and per-column wrapping sums (closed forms).
+# columns (60 GB), left in HBM: measured through the engine's block stream
+# (fq_engine_execute_blocks), checked by kept count and per-column wrapping
+# sums (closed forms).
 PROJECT_SQL = "SELECT number+1, number/2 FROM system.numbers_mt({N}) WHERE (number%8)<3"
 
 
@@ -289,15 +289,172 @@ def cpu_baseline_project(sample_rows, threads):
     }
 
 
+def _p1_expect(parts):
+    """(kept, sum(number+1), sum(number/2)) over numbers_mt partitions (closed forms)."""
+    kept = s1 = s2 = 0
+    for _, b, e in parts:
+        rows = stream_rows(b, e)
+        k, x, y = project_closed_form(b, b + rows - 1)
+        kept, s1, s2 = kept + k, (s1 + x) % U64, (s2 + y) % U64
+    return kept, s1, s2
+
+
+def _device_block_sums(b):
+    """(valid rows, wrapping sum of each column over its valid rows) of one
+    fq_device_block (block-stream layout or plain columns), on the GPU."""
+    out = [int(b.rows)]
+    n = b.columns[0].len if b.n_columns else 0
+    valid = None
+    if b.block_rows > 0 and n:
+        counts = ops.device_view(b.d_counts, 8 * b.n_blocks).view(torch.int64)
+        valid = (torch.arange(n, device="cuda") % b.block_rows) < \
+            counts.repeat_interleave(b.block_rows)[:n]
+    for j in range(b.n_columns):
+        c = b.columns[j]
+        if not c.len:
+            out.append(0)
+            continue
+        col = ops.device_view(c.data, 8 * c.len).view(torch.int64)
+        if valid is None:
+            col = col[:b.rows]
+        else:
+            col = torch.where(valid, col, torch.zeros_like(col))
+        out.append(int(col.sum().item()) % U64)
+    return out
+
+
+def run_project_engine(args, rank, world, local):
+    """--query p1, default path: FilterTransform -> ProjectionTransform through
+    the ENGINE (fq_engine_execute_blocks): SQL -> PipelineBuilder -> Source x P
+    -> Filter -> Projection -> Merge, the projection of each device block one
+    fq_filter_project_blocks launch (fq_jit_pblocks) on the shared queue, the
+    filtered and projected DataBlocks handed to the host in HBM in the
+    reference's per-10,000-row-block geometry (stream_expression.rs:38-50,
+    transform_projection.rs:45-56).  One step = the whole query, every block
+    pulled by the host; checked against the closed forms (every block's valid
+    rows summed on the GPU) before and after the timed steps."""
+    from fq_amd.engine import OPT_CHUNK_ROWS, Engine
+    if args.rows_total:
+        n_total = int(args.rows_total)
+    else:
+        n_total = int(args.rows_per_gpu) * world
+    sql = PROJECT_SQL.format(N=n_total)
+    mine = shard(generate_parts(n_total), rank, world)
+    total_rows = sum(stream_rows(b, e) for _, b, e in mine)
+    eng = Engine(device=local, profile=True)
+    if args.p1_chunk_rows:
+        eng.set_option(OPT_CHUNK_ROWS, int(args.p1_chunk_rows))
+    eng.materialize_numbers(n_total, rank, world)
+    torch.cuda.synchronize()
+    log(rank, "p1 (engine): %d partitions, %d rows (%.1f GB) resident on rank %d" % (
+        len(mine), total_rows, total_rows * 8 / 1e9, rank))
+    expect = _p1_expect(mine)
+
+    def step(check=False):
+        kept = s1 = s2 = 0
+        blocks = 0
+        with eng.execute_blocks(sql, rank, world) as st:
+            for b in st:
+                blocks += 1
+                if check:
+                    k, x, y = _device_block_sums(b)
+                    kept, s1, s2 = kept + k, (s1 + x) % U64, (s2 + y) % U64
+                else:
+                    kept += b.rows
+        return (kept, s1, s2) if check else kept, blocks
+
+    for _ in range(max(args.warmup, 1)):
+        got, blocks = step(check=True)
+        if got != expect:
+            raise SystemExit("PARITY FAILURE: got %r expected %r" % (got, expect))
+    log(rank, "result: kept rows and per-column wrapping sums == closed form (%d device blocks per query)" % blocks)
+    eng.reset_stats()
+    per_step = []
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    bad = 0
+    for _ in range(args.steps):
+        a = eng.stats()
+        k, _ = step()
+        b = eng.stats()
+        bad |= k != expect[0]
+        per_step.append(((b["project_ms"] - a["project_ms"]), (b["project_launches"] - a["project_launches"]),
+                         (b["project_bytes"] - a["project_bytes"])))
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda" if args.dist_backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    if bad:
+        raise SystemExit("PARITY FAILURE: a timed step kept another row count")
+    got, _ = step(check=True)
+    if got != expect:
+        raise SystemExit("PARITY FAILURE after the timed steps: got %r expected %r" % (got, expect))
+    st = eng.stats()
+    launches = max(st["project_launches"], 1)
+    avg_ms = st["project_ms"] / launches
+    bytes_per_launch = st["project_bytes"] / launches
+    rows_per_launch = st["project_rows"] / launches
+    achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
+    steps_frac = sorted((by / max(l, 1)) / ((ms / max(l, 1)) * 1e-3) / 1e9 / HBM_PEAK_GBPS for ms, l, by in per_step)
+    value = n_total * args.steps / dt
+    if rank == 0:
+        traffic, traffic_src = latest_pmc_traffic("fq_jit_pblocks", "p1", rows_per_launch)
+        out = {
+            "metric": METRIC, "value": value, "unit": "rows/s", "n_gpus": world, "ranks_seen": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3,
+            "higher_is_better": True, "scaling": "strong" if args.rows_total else "weak", "vs_baseline": None,
+            "vs_baseline_ref": "no published reference number for this query",
+            "dtype": "u64", "data": "synthetic: system.numbers_mt iota column (u64), resident in HBM before timing",
+            "config": {"workload": sql, "query": "p1", "rows_per_gpu": total_rows, "rows_total": n_total,
+                       "partitions_per_gpu": len(mine), "block_rows": BLOCK_SIZE,
+                       "device_blocks_per_step": blocks,
+                       "path": "fq_engine_execute_blocks: SQL -> PipelineBuilder -> Source x P -> FilterTransform -> "
+                               "ProjectionTransform (fq_filter_project_blocks per device block, fq_jit_pblocks) -> "
+                               "Merge; the host pulls every filtered + projected DataBlock, left in HBM in the "
+                               "reference's per-10,000-row-block geometry",
+                       "parallelism": "dp%d (numbers_mt partitions sharded, no exchange)" % world},
+            "achieved_hbm_gbps": achieved, "kernel_ms_per_launch": avg_ms,
+            "scan_launches_per_step": st["project_launches"] / args.steps,
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic, "traffic_source": traffic_src,
+                         "kernel": "fq_jit_pblocks (hipRTC-specialised) launched by the engine's ProjectionTransform, "
+                                   "one launch per device block; algorithmic bytes = 8 B per row read + 8 B per kept "
+                                   "row per projected column; event pair per launch on the engine's queue",
+                         "bytes_per_launch": bytes_per_launch,
+                         "frac_per_step": {"median": steps_frac[len(steps_frac) // 2], "min": steps_frac[0],
+                                           "max": steps_frac[-1], "steps": len(steps_frac)}},
+            "result": {"kept_rows_per_step": expect[0], "sum_number_plus_1": expect[1], "sum_number_div_2": expect[2]},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            try:
+                out["cpu_baseline"] = cpu_baseline_project(int(args.cpu_sample_rows or 1e10), args.cpu_threads)
+            except Exception as e:  # report, never hide
+                out["cpu_baseline"] = {"error": repr(e)}
+        if args.tuned:
+            out["tune"] = args.tuned
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def run_project(args, rank, world):
-    """--query p1: FilterTransform -> ProjectionTransform over this rank's
-    resident numbers_mt partitions, outputs in HBM; one step = every partition
-    once.  Default path: fq_filter_project_blocks over the partition's
-    10,000-row blocks (the reference filters and projects block by block,
-    transform_filter.rs:38-55 on each numbers_stream.rs block): block b's kept
-    rows at output rows [b * 10,000, + count[b]).  --project-path contiguous:
-    fq_filter_project (one contiguous output per partition, decoupled
-    look-back); the line reports that kernel's time beside the default's."""
+    """--query p1 --project-path blocks|contiguous: the kernel alone at the C
+    ABI over this rank's resident numbers_mt partitions, outputs in HBM; one
+    step = every partition once.  blocks: fq_filter_project_blocks over the
+    partition's 10,000-row blocks (block b's kept rows at output rows
+    [b * 10,000, + count[b])); contiguous: fq_filter_project (one contiguous
+    output per partition, decoupled look-back).  The launches cycle over
+    --p1-output-sets freshly allocated output pairs, and the line reports the
+    per-launch distribution (median / min / max) and each set's mean: which
+    pages an output pair lands on moves the kernel's time."""
     import ctypes as C
 
     from fq_amd._lib import check, lib
@@ -319,48 +476,49 @@ def run_project(args, rank, world):
     blocks = args.project_path == "blocks"
     maxr = max(c.len for c in cols)
     alloc = ops.contiguous_column if args.p1_outputs == "contiguous" else ops.empty_column
-    outs = [alloc(maxr, U), alloc(maxr, U)]
+    nsets = max(1, args.p1_output_sets)
+    sets = [[alloc(maxr, U), alloc(maxr, U)] for _ in range(nsets)]
     nb_max = -(-maxr // BLOCK_SIZE)
     counts = ops.Workspace(8 * nb_max)
     ws = ops.Workspace(max(lib.fq_filter_project_workspace_bytes(maxr), lib.fq_filter_project_blocks_workspace_bytes()))
     pred = predicate(U, [("%", 8)], "<", 3)
     exprs = (abi.fq_expr * 2)(chain(U, [("+", 1)])[0], chain(U, [("/", 2)])[0])
-    ptrs = (C.c_void_p * 2)(outs[0].ptr, outs[1].ptr)
+    ptr_sets = [(C.c_void_p * 2)(o[0].ptr, o[1].ptr) for o in sets]
     kept = C.c_int64(0)
     stream = torch.cuda.current_stream()
     sp = C.c_void_p(stream.cuda_stream)
     torch.cuda.synchronize()
     total_rows = sum(c.len for c in cols)
-    log(rank, "p1 (%s): %d partitions, %d rows (%.1f GB) resident on rank %d" % (
-        args.project_path, len(cols), total_rows, total_rows * 8 / 1e9, rank))
+    log(rank, "p1 (%s kernel): %d partitions, %d rows (%.1f GB) resident on rank %d, %d output sets" % (
+        args.project_path, len(cols), total_rows, total_rows * 8 / 1e9, rank, nsets))
 
-    def launch(col, use_blocks=blocks):
+    def launch(col, k, use_blocks=blocks):
         c = col.col()
         if use_blocks:
-            check(lib.fq_filter_project_blocks(C.byref(c), BLOCK_SIZE, C.byref(pred), exprs, 2, ptrs, counts.ptr,
+            check(lib.fq_filter_project_blocks(C.byref(c), BLOCK_SIZE, C.byref(pred), exprs, 2, ptr_sets[k], counts.ptr,
                                                C.byref(kept), ws.ptr, ws.nbytes, sp))
         else:
-            check(lib.fq_filter_project(C.byref(c), C.byref(pred), exprs, 2, ptrs, C.byref(kept), ws.ptr, ws.nbytes,
-                                        sp))
+            check(lib.fq_filter_project(C.byref(c), C.byref(pred), exprs, 2, ptr_sets[k], C.byref(kept), ws.ptr,
+                                        ws.nbytes, sp))
         return kept.value
 
-    def checked(col, use_blocks=blocks):
-        """(kept, wrapping sum of each output over its valid rows) of one launch:
-        outputs zeroed first, so rows past a block's count add nothing."""
-        for o in outs:
+    def checked(col, k, use_blocks=blocks):
+        """(kept, wrapping sum of each output over its valid rows) of one
+        launch: outputs zeroed first, so rows past a block's count add nothing."""
+        for o in sets[k]:
             o.buf.zero_()
-        k = launch(col, use_blocks)
-        n = col.len if use_blocks else k
-        sums = tuple(int(o.buf[:n * 8].view(torch.int64).sum().item()) % U64 for o in outs)
+        n_kept = launch(col, k, use_blocks)
+        n = col.len if use_blocks else n_kept
+        sums = tuple(int(o.buf[:n * 8].view(torch.int64).sum().item()) % U64 for o in sets[k])
         if use_blocks:
             nb = -(-col.len // BLOCK_SIZE)
-            if int(counts.buf[:8 * nb].view(torch.int64).sum().item()) != k:
+            if int(counts.buf[:8 * nb].view(torch.int64).sum().item()) != n_kept:
                 raise SystemExit("PARITY FAILURE: block counts do not add up to the kept rows")
-        return (k,) + sums
+        return (n_kept,) + sums
 
     for _ in range(max(args.warmup, 1)):
-        for col, exp in zip(cols, expect):
-            got = checked(col)
+        for i, (col, exp) in enumerate(zip(cols, expect)):
+            got = checked(col, i % nsets)
             if got != exp:
                 raise SystemExit("PARITY FAILURE: got %r expected %r" % (got, exp))
     log(rank, "result: kept rows and per-column wrapping sums == closed form on every partition")
@@ -370,13 +528,15 @@ def run_project(args, rank, world):
         dist.barrier()
     t0 = time.perf_counter()
     kept_total = 0
+    i = 0
     for _ in range(args.steps):
         for col in cols:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
-            kept_total += launch(col)
+            kept_total += launch(col, i % nsets)
             e1.record(stream)
-            evs.append((e0, e1, col.len))
+            evs.append((e0, e1, col.len, i % nsets))
+            i += 1
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -385,62 +545,51 @@ def run_project(args, rank, world):
         t = torch.tensor([dt], dtype=torch.float64, device="cuda" if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-    if checked(cols[-1]) != expect[-1]:
+    if checked(cols[-1], 0) != expect[-1]:
         raise SystemExit("PARITY FAILURE after the timed steps")
-    ms = [e0.elapsed_time(e1) for e0, e1, _ in evs]
+    ms = [e0.elapsed_time(e1) for e0, e1, _, _ in evs]
     avg_ms = sum(ms) / len(ms)
     kept_per_launch = kept_total / len(evs)
-    rows_per_launch = sum(r for _, _, r in evs) / len(evs)
+    rows_per_launch = sum(r for _, _, r, _ in evs) / len(evs)
     bytes_per_launch = 8 * rows_per_launch + 16 * kept_per_launch
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
+    fr = sorted(bytes_per_launch / (m * 1e-3) / 1e9 / HBM_PEAK_GBPS for m in ms)
+    set_ms = [sum(m for m, (_, _, _, k) in zip(ms, evs) if k == s) / max(1, sum(1 for e in evs if e[3] == s))
+              for s in range(nsets)]
     value = n_total * args.steps / dt
-    other = None
-    if rank == 0 and blocks and not args.no_contiguous_ref:
-        # the contiguous-output kernel on the same partition, for reference
-        if checked(cols[0], False) != expect[0]:
-            raise SystemExit("PARITY FAILURE (contiguous path)")
-        cms = []
-        for _ in range(3):
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
-            launch(cols[0], False)
-            e1.record(stream)
-            torch.cuda.synchronize()
-            cms.append(e0.elapsed_time(e1))
-        cb = 8 * cols[0].len + 16 * kept.value
-        other = {"path": "fq_filter_project (one contiguous output per partition, decoupled look-back, fq_jit_pselect)",
-                 "kernel_ms_per_launch": sum(cms) / len(cms),
-                 "frac": cb / (sum(cms) / len(cms) * 1e-3) / 1e9 / HBM_PEAK_GBPS}
     if rank == 0:
         kname = "fq_jit_pblocks" if blocks else "fq_jit_pselect"
         traffic, traffic_src = latest_pmc_traffic(kname, "p1", rows_per_launch)
-        path = ("fq_filter_project_blocks per resident partition: the partition's 10,000-row blocks filtered and "
-                "projected block by block as the reference does (transform_filter.rs:38-55 per numbers_stream.rs "
-                "block), block b's kept rows at output rows [b * 10,000, + count[b]), per-block counts in HBM"
+        path = ("fq_filter_project_blocks at the C ABI per resident partition (the kernel alone, not the engine): "
+                "the partition's 10,000-row blocks filtered and projected block by block, block b's kept rows at "
+                "output rows [b * 10,000, + count[b]), per-block counts in HBM"
                 if blocks else
-                "fq_filter_project per resident partition: predicate, decoupled look-back, both expressions, one "
-                "contiguous output per partition")
+                "fq_filter_project at the C ABI per resident partition: predicate, decoupled look-back, both "
+                "expressions, one contiguous output per partition")
         out = {
-            "metric": METRIC, "value": value, "unit": "rows/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,
-            "scaling": "strong" if args.rows_total else "weak", "vs_baseline": None,
+            "metric": METRIC, "value": value, "unit": "rows/s", "n_gpus": world, "ranks_seen": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3,
+            "higher_is_better": True, "scaling": "strong" if args.rows_total else "weak", "vs_baseline": None,
             "vs_baseline_ref": "no published reference number for this query",
             "dtype": "u64", "data": "synthetic: system.numbers_mt iota column (u64), resident in HBM before timing",
             "config": {"workload": sql, "query": "p1", "rows_per_gpu": total_rows, "rows_total": n_total,
                        "partitions_per_gpu": len(cols), "block_rows": BLOCK_SIZE, "path": path,
-                       "outputs": "physically contiguous HBM (hipDeviceMallocContiguous)" if args.p1_outputs ==
-                                  "contiguous" else "torch caching-allocator buffers",
+                       "outputs": ("%d pairs in physically contiguous HBM (hipDeviceMallocContiguous), cycled per "
+                                   "launch" if args.p1_outputs == "contiguous" else
+                                   "%d pairs of torch caching-allocator buffers, cycled per launch") % nsets,
                        "parallelism": "dp%d (numbers_mt partitions sharded)" % world},
             "achieved_hbm_gbps": achieved, "kernel_ms_per_launch": avg_ms, "scan_launches_per_step": len(cols),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic, "traffic_source": traffic_src,
+                         "frac": fr[len(fr) // 2], "frac_of_mean_ms": achieved / HBM_PEAK_GBPS,
+                         "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": "%s (hipRTC-specialised), one launch per partition; algorithmic bytes = 8 B per "
-                                   "row read + 16 B per kept row written" % kname,
-                         "bytes_per_launch": bytes_per_launch},
+                                   "row read + 16 B per kept row written; frac = the median launch" % kname,
+                         "bytes_per_launch": bytes_per_launch,
+                         "frac_per_launch": {"median": fr[len(fr) // 2], "min": fr[0], "max": fr[-1],
+                                             "launches": len(fr)},
+                         "ms_per_output_set": set_ms},
             "result": {"kept_rows_per_step": kept_total // args.steps},
         }
-        if other:
-            out["contiguous_output"] = other
         if world == 1 and not args.no_cpu_baseline:
             try:
                 out["cpu_baseline"] = cpu_baseline_project(int(args.cpu_sample_rows or 1e10), args.cpu_threads)
@@ -556,13 +705,16 @@ def main():
                          "box's 8 threads for c3, ~5 s for p1; 4e9 rows for GROUP BY, a hash insert per row, ~3-10 s)")
     ap.add_argument("--cpu-threads", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--project-path", default="blocks", choices=("blocks", "contiguous"),
-                    help="p1: block-stream output (fq_filter_project_blocks, default) or one contiguous output "
-                         "per partition (fq_filter_project)")
+    ap.add_argument("--project-path", default="engine", choices=("engine", "blocks", "contiguous"),
+                    help="p1: through the engine (fq_engine_execute_blocks, default), or the kernel alone at the "
+                         "C ABI: block-stream output (fq_filter_project_blocks) or one contiguous output per "
+                         "partition (fq_filter_project)")
     ap.add_argument("--p1-outputs", default="contiguous", choices=("contiguous", "torch"),
-                    help="p1: output columns in physically contiguous HBM (default) or torch buffers")
-    ap.add_argument("--no-contiguous-ref", action="store_true",
-                    help="p1: skip timing the contiguous-output kernel beside the block-stream one")
+                    help="p1 kernel paths: output columns in physically contiguous HBM (default) or torch buffers")
+    ap.add_argument("--p1-output-sets", type=int, default=4,
+                    help="p1 kernel paths: freshly allocated output pairs the launches cycle over")
+    ap.add_argument("--p1-chunk-rows", type=float, default=None,
+                    help="p1 engine path: rows per device block (FQ_OPT_CHUNK_ROWS; default 4e8)")
     ap.add_argument("--streams", type=int, default=1,
                     help="device queues the pipes share (FQ_OPT_STREAMS); 1 = the scans run back to back")
     ap.add_argument("--group-chunk-rows", type=int, default=None,
@@ -614,6 +766,8 @@ def main():
             dist.init_process_group("gloo")
 
     if args.query == "p1":
+        if args.project_path == "engine":
+            return run_project_engine(args, rank, world, local)
         return run_project(args, rank, world)
     if args.rows_total:
         n_total = int(args.rows_total)

@@ -50,6 +50,17 @@ struct fq_result {
     mutable std::vector<std::string> text;  // fq_result_text storage
 };
 
+struct fq_block_stream {
+    fq_engine *e = nullptr;
+    fq::QueryContextRef qctx;
+    fq::Pipeline pipeline;
+    fq::StreamRef s;
+    fq::DataBlock cur;  // the block the caller holds
+    std::vector<std::string> names;
+    std::vector<const char *> name_ptrs;
+    std::vector<fq_col> cols;
+};
+
 struct fq_engine {
     std::unique_ptr<fq::Runtime> rt;
     std::shared_ptr<fq::DataSource> ds;
@@ -143,7 +154,7 @@ fq::QueryPlan plan_for(fq_engine *e, const char *sql, const fq::QueryContext &qc
 // Host rows of the block are moved in when the block holds the only
 // reference to them (streams hand their blocks over), else copied.
 void append_block(fq_result *r, fq::DataBlock b0, fq::ExecCtx &ctx) {
-    fq::DataBlock b = b0.filter ? fq::materialize(b0, ctx) : std::move(b0);
+    fq::DataBlock b = fq::needs_materialize(b0) ? fq::materialize(b0, ctx) : std::move(b0);
     if (r->names.empty()) {
         for (const auto &f : b.schema->fields) {
             r->names.push_back(f.name);
@@ -380,6 +391,76 @@ fq_status fq_engine_execute_partial(fq_engine *e, const char *sql, int32_t rank,
     });
 }
 
+fq_status fq_engine_execute_blocks(fq_engine *e, const char *sql, int32_t rank, int32_t world, fq_block_stream **out) {
+    if (!e || !sql || !out) return fqc::fail(FQ_E_INVALID, "fq_engine_execute_blocks: NULL argument");
+    if (world < 1 || rank < 0 || rank >= world) return fqc::fail(FQ_E_INVALID, "bad rank/world");
+    *out = nullptr;
+    return guard([&] {
+        fq::ExecCtx ctx(e->rt.get());
+        auto bs = std::make_unique<fq_block_stream>();
+        bs->e = e;
+        bs->qctx = make_ctx(e, rank, world);
+        fq::QueryPlan plan = plan_for(e, sql, *bs->qctx);
+        if (plan.explain || aggregate_node(plan))
+            throw fq::FQException(FQ_E_UNSUPPORTED, "fq_engine_execute_blocks covers row pipelines (Filter / Projection "
+                                                    "/ Limit); aggregates return host rows through fq_engine_execute");
+        for (const auto &f : plan.nodes.back().schema->fields) bs->names.push_back(f.name);
+        for (const auto &n : bs->names) bs->name_ptrs.push_back(n.c_str());
+        bs->pipeline = fq::build_pipeline(plan, bs->qctx);
+        bs->s = bs->pipeline.execute();
+        e->rt->stats.queries++;
+        *out = bs.release();
+    });
+}
+
+fq_status fq_block_stream_next(fq_block_stream *bs, fq_device_block *out, int32_t *has_block) {
+    if (!bs || !out || !has_block) return fqc::fail(FQ_E_INVALID, "fq_block_stream_next: NULL argument");
+    *has_block = 0;
+    *out = fq_device_block{};
+    out->pipe = -1;
+    return guard([&] {
+        fq::ExecCtx ctx(bs->e->rt.get());
+        bs->cur = fq::DataBlock{};  // the caller is done with the previous block
+        bs->cols.clear();
+        if (!bs->s) return;
+        fq::DataBlock b;
+        if (!bs->s->next(b)) {
+            bs->s.reset();  // the pipes are joined: nothing runs after the end
+            return;
+        }
+        if (b.filter) b = fq::materialize(b, ctx);  // a Filter with no Projection above it
+        for (const auto &c : b.columns)
+            if (!c.on_device() && c.len > 0)
+                throw fq::FQException(FQ_E_UNSUPPORTED, "fq_block_stream_next: a host block in a row pipeline");
+        ctx.sync();  // the consumer-side transforms (a LIMIT's compaction) are done too
+        bs->cur = std::move(b);
+        for (const auto &c : bs->cur.columns) bs->cols.push_back(c.abi());
+        out->n_columns = (int32_t)bs->cols.size();
+        out->pipe = bs->cur.pipe < 0 ? 0 : bs->cur.pipe;  // no merge channel: the one source pipe
+        out->names = bs->name_ptrs.data();
+        out->columns = bs->cols.data();
+        out->rows = bs->cur.num_rows();
+        if (bs->cur.layout) {
+            out->block_rows = bs->cur.layout->block_rows;
+            out->n_blocks = bs->cur.layout->n_blocks;
+            out->d_counts = (const int64_t *)bs->cur.layout->counts->ptr;
+        }
+        *has_block = 1;
+    });
+}
+
+void fq_block_stream_free(fq_block_stream *bs) {
+    if (!bs) return;
+    try {
+        fq::ExecCtx ctx(bs->e->rt.get());
+        bs->cur = fq::DataBlock{};
+        bs->s.reset();  // closes the merge channel and joins the pipes
+        delete bs;
+    } catch (...) {
+        delete bs;
+    }
+}
+
 fq_status fq_engine_partial_state_bytes(fq_engine *e, const char *sql, size_t *bytes) {
     if (!e || !sql || !bytes) return fqc::fail(FQ_E_INVALID, "fq_engine_partial_state_bytes: NULL argument");
     *bytes = 0;
@@ -560,6 +641,11 @@ fq_status fq_engine_get_stats(fq_engine *e, fq_engine_stats *out) {
     out->exchange_bytes = e->rt->stats.exchange_bytes.load();
     out->cached_block_bytes = fq::block_cache_bytes();
     out->cached_workspace_bytes = fq::block_cache_workspace_bytes();
+    out->project_launches = e->rt->stats.project_launches.load();
+    out->project_rows = e->rt->stats.project_rows.load();
+    out->project_kept = e->rt->stats.project_kept.load();
+    out->project_bytes = e->rt->stats.project_bytes.load();
+    out->project_ms = (double)e->rt->stats.project_ns.load() * 1e-6;
     return FQ_OK;
 }
 
@@ -579,6 +665,11 @@ fq_status fq_engine_reset_stats(fq_engine *e) {
     e->rt->stats.exchanges = 0;
     e->rt->stats.exchange_rounds = 0;
     e->rt->stats.exchange_bytes = 0;
+    e->rt->stats.project_launches = 0;
+    e->rt->stats.project_rows = 0;
+    e->rt->stats.project_kept = 0;
+    e->rt->stats.project_bytes = 0;
+    e->rt->stats.project_ns = 0;
     return FQ_OK;
 }
 

@@ -545,11 +545,21 @@ Runtime::~Runtime() {
         if (w->ws) (void)hipFree(w->ws);
         for (auto ev : w->events) (void)hipEventDestroy(ev);
         for (auto *c : w->slot_chunks) (void)hipHostFree(c);
+        if (w->project_res) (void)hipHostFree(w->project_res);
     }
     for (auto &s : shared_) {
         BlockCache::get().drop_stream(s);
         (void)hipStreamDestroy(s);
     }
+}
+
+uint64_t *WorkerRes::project_result() {
+    if (!project_res) {
+        void *p = nullptr;
+        check_hip(hipHostMalloc(&p, 2 * sizeof(uint64_t), hipHostMallocDefault), "hipHostMalloc(projection result)");
+        project_res = (uint64_t *)p;
+    }
+    return project_res;
 }
 
 hipEvent_t WorkerRes::take_event() {
@@ -695,8 +705,20 @@ ExecCtx &ExecCtx::current() {
     return *g_current;
 }
 
+// Waits for the work enqueued on this context's queue so far.  An event, not
+// hipStreamSynchronize: on a queue shared by several pipes the wait must not
+// extend to launches other pipes enqueue meanwhile.
 void ExecCtx::sync() {
-    if (rt->has_device()) check_hip(hipStreamSynchronize(stream()), "hipStreamSynchronize");
+    if (!rt->has_device()) return;
+    hipEvent_t ev = res->take_event();
+    hipError_t e;
+    {
+        std::lock_guard<std::mutex> lk(*res->launch_mu);
+        e = hipEventRecord(ev, stream());
+    }
+    if (e == hipSuccess) e = hipEventSynchronize(ev);
+    res->give_event(ev);
+    check_hip(e, "hipEventSynchronize");
 }
 
 // ---------------------------------------------------------------------------
@@ -802,6 +824,7 @@ std::vector<DataValue> Column::to_host(hipStream_t st) const {
 
 int64_t DataBlock::num_rows() const {
     if (filter) throw_internal("num_rows() of a block with a pending filter");
+    if (layout) return layout->rows;
     return columns.empty() ? 0 : columns[0].len;
 }
 

@@ -139,6 +139,8 @@ struct EngineStats {
     // the distributed split: partial, the exchange (fq_comm.cpp), final
     std::atomic<uint64_t> partial_ns{0}, exchange_ns{0}, final_ns{0};
     std::atomic<uint64_t> exchanges{0}, exchange_rounds{0}, exchange_bytes{0};
+    // FilterTransform -> ProjectionTransform over block streams (fq_filter_project_blocks)
+    std::atomic<uint64_t> project_launches{0}, project_rows{0}, project_kept{0}, project_bytes{0}, project_ns{0};
     // query start (steady_clock ns) while a query runs; the first scan launch
     // of the query adds (launch - start) to first_launch_ns and clears it
     std::atomic<int64_t> query_t0{0};
@@ -156,6 +158,10 @@ struct WorkerRes {
     // the next partition's scan.  Chunks of kSlotChunk, reused across queries.
     static constexpr size_t kSlotChunk = 64;
     std::vector<fq_agg_state *> slot_chunks;
+    // pinned {kept rows, flag words} of this worker's block-stream projection
+    // launch (fq_filter_project_blocks_async; one in flight per worker)
+    uint64_t *project_res = nullptr;
+    uint64_t *project_result();
     hipEvent_t take_event();
     void give_event(hipEvent_t e) { events.push_back(e); }
 };
@@ -182,7 +188,10 @@ class Runtime {
     static constexpr int kHostOnly = -1;  // no GPU: planning and AggregateFinal merges only
     explicit Runtime(int device);
     bool has_device() const { return device_ != kHostOnly; }
-    static constexpr uint64_t kPoolKeepBytes = 8ull << 30;  // default mem pool release threshold
+    // default mem pool release threshold: a row pipeline without LIMIT keeps
+    // ~8-16 projected blocks of up to 5 GB in flight (8 pipes + the merge
+    // channel); below that working set every block would map fresh HBM
+    static constexpr uint64_t kPoolKeepBytes = 64ull << 30;
     ~Runtime();
     int device() const { return device_; }
     WorkerRes *acquire();
@@ -301,6 +310,18 @@ struct Column {
 
 class Function;
 
+// Block-stream geometry of a ProjectionTransform output over a numbers stream
+// (fq_filter_project_blocks): the columns span n_blocks reference blocks of
+// block_rows rows, and block b's rows are the first counts[b] of its range --
+// the reference's per-block filtered + projected DataBlocks
+// (stream_expression.rs:38-50, transform_projection.rs:45-56) kept where they
+// were produced.  materialize() compacts them for consumers that need one
+// array (host results, LIMIT); fq_engine_execute_blocks hands them over as is.
+struct BlockLayout {
+    int64_t block_rows = 0, n_blocks = 0;
+    int64_t rows = 0;                     // valid rows over all blocks
+    std::shared_ptr<DeviceBuffer> counts;  // int64 per block, HBM
+};
 
 struct DataBlock {
     SchemaRef schema;
@@ -313,6 +334,10 @@ struct DataBlock {
     // FilterTransform output not yet compacted: rows where this predicate is
     // true (the aggregate scan fuses it; other consumers call materialize()).
     std::shared_ptr<Function> filter;
+    // set: the columns hold a block stream (see BlockLayout), not one array
+    std::shared_ptr<const BlockLayout> layout;
+    // the MergeProcessor input (partition pipe) the block came from; -1 unknown
+    int32_t pipe = -1;
 
     int64_t num_rows() const;  // columns[0].len (data_block.rs:46-48); needs no pending filter
     int num_columns() const { return (int)columns.size(); }
@@ -320,8 +345,10 @@ struct DataBlock {
     uint64_t sub_blocks() const;  // reference blocks represented (>= 1 if rows > 0)
 };
 
-// Compact a block with a pending filter (fq_compare/eval + fq_filter_compact).
+// Compact a block with a pending filter (fq_compare/eval + fq_filter_compact)
+// or a block-stream layout (fq_blocks_compact) into plain columns.
 DataBlock materialize(const DataBlock &b, ExecCtx &ctx);
+inline bool needs_materialize(const DataBlock &b) { return b.filter || b.layout; }
 
 // DataColumnarValue
 struct ColumnarValue {

@@ -688,12 +688,94 @@ static DataBlock compact_block(const DataBlock &b, const Column &bitmap, ExecCtx
     return out;
 }
 
+// A block stream's valid rows into plain columns (fq_blocks_compact).
+static DataBlock compact_layout(const DataBlock &b, ExecCtx &ctx) {
+    const BlockLayout &L = *b.layout;
+    DataBlock nb = b;
+    nb.layout = nullptr;
+    std::vector<const void *> in;
+    std::vector<void *> out;
+    for (auto &c : nb.columns) {
+        if (dtype_size(c.dtype) != 8 || c.dtype == FQ_DT_BOOLEAN || !c.on_device())
+            throw_internal("block-stream layout over a column that is not 64-bit device data");
+        in.push_back(c.dptr());
+        Column o = Column::device(c.dtype, L.rows, ctx.stream());
+        out.push_back(o.dptr());
+        c = o;
+    }
+    const int64_t len = b.columns.empty() ? 0 : b.columns[0].len;
+    const size_t wsb = fq_blocks_compact_workspace_bytes(L.n_blocks);
+    auto ws = DeviceBuffer::alloc(wsb, ctx.stream());
+    check_fq(fq_blocks_compact((int32_t)in.size(), in.data(), len, L.block_rows, (const int64_t *)L.counts->ptr,
+                               out.data(), nullptr, ws->ptr, wsb, ctx.stream()));
+    return nb;
+}
+
 DataBlock materialize(const DataBlock &b, ExecCtx &ctx) {
+    if (b.layout) return compact_layout(b, ctx);
     if (!b.filter) return b;
     DataBlock nb = b;
     nb.filter = nullptr;
     Column bm = eval_predicate(*b.filter, nb, ctx);
     return compact_block(nb, bm, ctx);
+}
+
+// FilterTransform -> ProjectionTransform over a block that stands for a run of
+// reference blocks (sub_block_rows, numbers_stream.rs:29-48): the reference
+// filters and projects each 10,000-row block on its own
+// (stream_expression.rs:38-50), so the output keeps that geometry -- block b's
+// kept rows at rows [b * B, b * B + count[b]) -- and no block waits on another's
+// count (fq_filter_project_blocks).  The launch is enqueued with the queue's
+// other pipes (launch_mu: a timing event pair brackets exactly this launch) and
+// this pipe waits on its own event, not on the queue.
+static bool project_blocks(const DataBlock &b, const Column &c, const fq_pred *pred, std::vector<fq_expr> &exprs,
+                           std::vector<Column> &outs, std::vector<void *> &ptrs, const SchemaRef &schema, ExecCtx &ctx,
+                           DataBlock &out) {
+    const int64_t n = c.len, B = b.sub_block_rows;
+    const int64_t nb = n <= B ? 1 : (n + B - 1) / B;
+    auto layout = std::make_shared<BlockLayout>();
+    layout->block_rows = B;
+    layout->n_blocks = n == 0 ? 0 : nb;
+    layout->counts = DeviceBuffer::alloc((size_t)std::max<int64_t>(nb, 1) * 8, ctx.stream());
+    auto ws = DeviceBuffer::alloc(fq_filter_project_blocks_workspace_bytes(), ctx.stream());
+    uint64_t *res = ctx.res->project_result();
+    const bool prof = ctx.rt->profile.load();
+    hipEvent_t e0 = ctx.res->take_event(), e1 = ctx.res->take_event();
+    fq_col ic = c.abi();
+    fq_status st;
+    {
+        std::lock_guard<std::mutex> lk(*ctx.res->launch_mu);
+        if (prof) check_hip(hipEventRecord(e0, ctx.stream()), "hipEventRecord");
+        st = fq_filter_project_blocks_async(&ic, B, pred, exprs.data(), (int32_t)exprs.size(), ptrs.data(),
+                                            (int64_t *)layout->counts->ptr, res, ws->ptr, ws->bytes, ctx.stream());
+        if (st == FQ_OK) check_hip(hipEventRecord(e1, ctx.stream()), "hipEventRecord");
+    }
+    if (st == FQ_OK) {
+        hipError_t he = hipEventSynchronize(e1);
+        if (he == hipSuccess && prof) {
+            float ms = 0;
+            if (hipEventElapsedTime(&ms, e0, e1) == hipSuccess) ctx.rt->stats.project_ns += (uint64_t)((double)ms * 1e6);
+        }
+        check_hip(he, "hipEventSynchronize");
+    }
+    ctx.res->give_event(e0);
+    ctx.res->give_event(e1);
+    if (st == FQ_E_UNSUPPORTED) return false;  // the unfused path evaluates it (and raises what the reference does)
+    check_fq(st);
+    int64_t kept = 0;
+    check_fq(fq_filter_project_blocks_result(res, &kept));
+    layout->rows = kept;
+    auto &S = ctx.rt->stats;
+    S.project_launches++;
+    S.project_rows += (uint64_t)n;
+    S.project_kept += (uint64_t)kept;
+    S.project_bytes += (uint64_t)n * (uint64_t)dtype_size(c.dtype) + (uint64_t)kept * 8 * (uint64_t)outs.size();
+    out = DataBlock{};
+    out.schema = schema;
+    out.sub_block_rows = B;
+    out.layout = layout;
+    for (auto &o : outs) out.columns.push_back(o);
+    return true;
 }
 
 // ProjectionTransform over a block with a pending filter (or none): when every
@@ -741,6 +823,8 @@ bool project_fused(const DataBlock &b, const std::vector<FunctionRef> &funcs, co
         ptrs.push_back(outs.back().dptr());
         exprs.push_back(fc.expr);
     }
+    if (pred && b.sub_block_rows >= FQ_PROJECT_MIN_BLOCK_ROWS)
+        return project_blocks(b, c, pred, exprs, outs, ptrs, schema, ctx, out);
     const size_t wsb = fq_filter_project_workspace_bytes(n);
     auto ws = DeviceBuffer::alloc(wsb, ctx.stream());
     fq_col ic = c.abi();

@@ -95,8 +95,8 @@ bool NumbersTable::pinned(const std::string &part, Column &out) {
 // after the first few instead of after a whole partition).
 class NumbersStream : public BlockStream {
    public:
-    NumbersStream(NumbersTable *t, SchemaRef s, std::vector<Partition> parts, bool morsels)
-        : t_(t), schema_(std::move(s)), parts_(std::move(parts)), morsels_(morsels) {}
+    NumbersStream(NumbersTable *t, SchemaRef s, std::vector<Partition> parts, ReadMode mode)
+        : t_(t), schema_(std::move(s)), parts_(std::move(parts)), mode_(mode) {}
     bool next(DataBlock &out) override {
         if (off_ >= rows_) {  // next partition
             if (i_ >= parts_.size()) return false;
@@ -110,6 +110,11 @@ class NumbersStream : public BlockStream {
             off_ = 0;
             morsel_ = NumbersTable::kMorselFirst;
             has_pinned_ = t_->pinned(p.name, pinned_) && (uint64_t)pinned_.len == rows_;
+            // kChunks: equal pieces of whole 10,000-row blocks, at most chunk_rows() each
+            const uint64_t blocks = (rows_ + kBlockSize - 1) / kBlockSize;
+            const uint64_t per = std::max<uint64_t>(1, t_->chunk_rows() / kBlockSize);
+            const uint64_t pieces = (blocks + per - 1) / per;
+            piece_ = pieces ? (blocks + pieces - 1) / pieces * kBlockSize : rows_;
             if (rows_ == 0) {  // an empty partition still yields its (empty) block
                 emit(Column::device(FQ_DT_UINT64, 0, ExecCtx::current().stream()), out);
                 return true;
@@ -118,9 +123,10 @@ class NumbersStream : public BlockStream {
         // row pipelines: growing morsels; aggregates: the resident partition
         // whole, a generated one in chunk_rows() pieces (bounded HBM; whole
         // 10,000-row blocks, so the per-block state replay is unchanged)
-        const uint64_t n = morsels_      ? std::min(morsel_, rows_ - off_)
-                           : has_pinned_ ? rows_ - off_
-                                         : std::min(t_->chunk_rows(), rows_ - off_);
+        const uint64_t n = mode_ == ReadMode::kMorsels ? std::min(morsel_, rows_ - off_)
+                           : mode_ == ReadMode::kChunks ? std::min(piece_, rows_ - off_)
+                           : has_pinned_                ? rows_ - off_
+                                                        : std::min(t_->chunk_rows(), rows_ - off_);
         Column col;
         if (has_pinned_) {
             col = pinned_.slice((int64_t)off_, (int64_t)n);
@@ -146,15 +152,15 @@ class NumbersStream : public BlockStream {
     NumbersTable *t_;
     SchemaRef schema_;
     std::vector<Partition> parts_;
-    bool morsels_;
+    ReadMode mode_;
     size_t i_ = 0;
-    uint64_t begin_ = 0, rows_ = 0, off_ = 0, morsel_ = 0;
+    uint64_t begin_ = 0, rows_ = 0, off_ = 0, morsel_ = 0, piece_ = 0;
     bool has_pinned_ = false;
     Column pinned_;
 };
 
-StreamRef NumbersTable::read(const std::vector<Partition> &parts, bool morsels) {
-    return std::make_unique<NumbersStream>(this, schema_, parts, morsels);
+StreamRef NumbersTable::read(const std::vector<Partition> &parts, ReadMode mode) {
+    return std::make_unique<NumbersStream>(this, schema_, parts, mode);
 }
 
 DataSource::DataSource() : numbers_(std::make_shared<NumbersTable>()) {
@@ -304,6 +310,7 @@ StreamRef MergeProcessor::execute() {
                 while (!ch->is_closed() && s->next(b)) {
                     ctx.sync();  // device work of this block done before another thread reads it
                     Channel::Item it;
+                    b.pipe = (int32_t)pipe;
                     it.block = std::move(b);
                     if (!ch->send(std::move(it))) break;
                 }
@@ -328,7 +335,7 @@ StreamRef MergeProcessor::execute() {
 
 StreamRef SourceTransform::execute() {
     TableRef t = ctx_->get_table(db_, table_);  // transform_source.rs:49-52
-    return t->read(parts_, morsels_);
+    return t->read(parts_, mode_);
 }
 
 namespace {
@@ -360,7 +367,7 @@ struct FusionGuard {
 StreamRef FilterTransform::execute() {
     FunctionRef pred = func_->clone();
     return std::make_unique<MapStream>(input_->execute(), [pred](DataBlock b) {
-        if (b.filter) b = materialize(b, ExecCtx::current());
+        if (needs_materialize(b)) b = materialize(b, ExecCtx::current());
         b.filter = pred;
         return b;
     });
@@ -373,6 +380,7 @@ StreamRef ProjectionTransform::execute() {
     return std::make_unique<MapStream>(input_->execute(), [schema, funcs](DataBlock b) {
         ExecCtx &ctx = ExecCtx::current();
         DataBlock out;
+        if (b.layout) b = materialize(b, ctx);  // a block stream in: one array first
         if (project_fused(b, funcs, schema, ctx, out)) return out;  // filter + expressions in one pass
         b = materialize(b, ctx);
         const int64_t rows = b.num_rows();
@@ -392,6 +400,7 @@ StreamRef AggregatePartialTransform::execute() {
         FusionGuard guard(ctx, &fusion);
         DataBlock b;
         while (in->next(b)) {
+            if (b.layout) b = materialize(b, ctx);
             for (auto &f : funcs) f->accumulate(b, ctx);
             fusion.end_block();
         }

@@ -62,16 +62,22 @@ struct ReadDataSourcePlan {  // plan_read_datasource.rs
     std::vector<Partition> partitions;
 };
 
+// How a table yields a partition's rows (the same rows, in order, always):
+//   kWhole    aggregates: a resident partition as one block, a generated one in
+//             chunk_rows() pieces (bounded HBM)
+//   kChunks   row pipelines without LIMIT: pieces of at most chunk_rows() rows,
+//             resident or not, so the projected blocks in flight stay bounded
+//   kMorsels  row pipelines with LIMIT: growing morsels, so a satisfied LIMIT
+//             stops the scan early (stream_limit.rs:28-48)
+enum class ReadMode { kWhole, kChunks, kMorsels };
+
 class ITable {  // table.rs:13-22
    public:
     virtual ~ITable() = default;
     virtual std::string name() const = 0;
     virtual SchemaRef schema() const = 0;
     virtual ReadDataSourcePlan read_plan(const DataValue *table_arg) const = 0;
-    // morsels: the consumer is a row pipeline (Filter/Projection/Limit, no
-    // aggregate), so a partition may be yielded as several consecutive blocks
-    // and a satisfied LIMIT stops the scan early (stream_limit.rs:28-48)
-    virtual StreamRef read(const std::vector<Partition> &parts, bool morsels = false) = 0;
+    virtual StreamRef read(const std::vector<Partition> &parts, ReadMode mode = ReadMode::kWhole) = 0;
 };
 using TableRef = std::shared_ptr<ITable>;
 
@@ -83,7 +89,7 @@ class NumbersTable : public ITable {
     std::string name() const override { return "numbers_mt"; }
     SchemaRef schema() const override { return schema_; }
     ReadDataSourcePlan read_plan(const DataValue *table_arg) const override;
-    StreamRef read(const std::vector<Partition> &parts, bool morsels = false) override;
+    StreamRef read(const std::vector<Partition> &parts, ReadMode mode = ReadMode::kWhole) override;
     // morsel sizes: the first is kMorselFirst rows, each next one twice the
     // last up to kMorselMax (multiples of the 10,000-row block)
     static constexpr uint64_t kMorselFirst = 160000;
@@ -175,9 +181,8 @@ class MergeProcessor : public IProcessor {  // processor_merge.rs:16-94
 class SourceTransform : public IProcessor {  // transform_source.rs:14-53
    public:
     SourceTransform(QueryContextRef ctx, std::string db, std::string table, std::vector<Partition> parts,
-                    bool morsels = false)
-        : ctx_(std::move(ctx)), db_(std::move(db)), table_(std::move(table)), parts_(std::move(parts)),
-          morsels_(morsels) {}
+                    ReadMode mode = ReadMode::kWhole)
+        : ctx_(std::move(ctx)), db_(std::move(db)), table_(std::move(table)), parts_(std::move(parts)), mode_(mode) {}
     std::string name() const override { return "SourceTransform"; }
     void connect_to(ProcessorRef) override { throw_internal("Cannot call SourceTransform connect_to"); }
     StreamRef execute() override;
@@ -186,7 +191,7 @@ class SourceTransform : public IProcessor {  // transform_source.rs:14-53
     QueryContextRef ctx_;
     std::string db_, table_;
     std::vector<Partition> parts_;
-    bool morsels_;
+    ReadMode mode_;
 };
 
 class FilterTransform : public IProcessor {  // transform_filter.rs:17-77

@@ -605,11 +605,18 @@ std::string QueryPlan::display() const {
 // PipelineBuilder::build (pipeline_builder.rs:26-106)
 Pipeline build_pipeline(const QueryPlan &plan, const QueryContextRef &ctx, bool emit_states) {
     Pipeline p;
-    // no aggregate above the source: the source may stream morsels
-    bool row_pipeline = true;
-    for (const PlanNode &n : plan.nodes)
+    // No aggregate above the source: a row pipeline.  With a LIMIT its pipes
+    // read growing morsels on private queues (a satisfied LIMIT stops after
+    // the first few); without one they read bounded pieces and share the
+    // aggregates' queue, so their HBM-bound launches run back to back, each
+    // bracketed by its own timing events.
+    bool row_pipeline = true, has_limit = false;
+    for (const PlanNode &n : plan.nodes) {
         if (n.kind == PlanNode::kAggregate) row_pipeline = false;
-    p.set_own_queues(row_pipeline);
+        if (n.kind == PlanNode::kLimit) has_limit = true;
+    }
+    const ReadMode mode = !row_pipeline ? ReadMode::kWhole : has_limit ? ReadMode::kMorsels : ReadMode::kChunks;
+    p.set_own_queues(mode == ReadMode::kMorsels);
     for (const PlanNode &n : plan.nodes) {
         switch (n.kind) {
             case PlanNode::kLimit: {
@@ -689,7 +696,7 @@ Pipeline build_pipeline(const QueryPlan &plan, const QueryContextRef &ctx, bool 
                 workers = (workers == 0 || workers >= parts.size()) ? 1 : parts.size() / workers;
                 for (size_t i = 0; i < parts.size(); i += workers) {
                     std::vector<Partition> chunk(parts.begin() + i, parts.begin() + std::min(parts.size(), i + workers));
-                    p.add_source(std::make_shared<SourceTransform>(ctx, n.read.db, n.read.table, chunk, row_pipeline));
+                    p.add_source(std::make_shared<SourceTransform>(ctx, n.read.db, n.read.table, chunk, mode));
                 }
                 if (parts.empty()) p.add_source(std::make_shared<BlocksProcessor>(std::vector<DataBlock>{}));
                 break;

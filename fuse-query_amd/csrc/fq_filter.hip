@@ -375,6 +375,87 @@ __global__ void block_lengths_kernel(int64_t *__restrict__ counts, int64_t nb, i
         counts[b] = b * B + B <= n ? B : n - b * B;
 }
 
+// ---- fq_blocks_compact: a block stream's valid rows into one array ----
+// counts[b] -> exclusive offsets in three launches: per-chunk sums of
+// kCompactChunk counts, one workgroup scanning the chunk sums, then each chunk
+// scanning its counts from its base; a copy kernel moves block b's rows (one
+// workgroup per block, lane-consecutive 8-byte rows: coalesced both sides).
+constexpr int kCompactChunk = 1024;
+
+__global__ void __launch_bounds__(kCompactChunk)
+blocks_chunk_sums_kernel(const int64_t *__restrict__ counts, int64_t nb, int64_t *__restrict__ sums) {
+    __shared__ int64_t red[kCompactChunk / kWave];
+    const int64_t b = (int64_t)blockIdx.x * kCompactChunk + threadIdx.x;
+    int64_t v = b < nb ? counts[b] : 0;
+    for (int o = kWave / 2; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if ((threadIdx.x & (kWave - 1)) == 0) red[threadIdx.x / kWave] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int64_t t = 0;
+        for (int w = 0; w < kCompactChunk / kWave; ++w) t += red[w];
+        sums[blockIdx.x] = t;
+    }
+}
+
+// exclusive scan of `n` values in place by one workgroup; base[n] = the total
+__global__ void __launch_bounds__(kCompactChunk) blocks_scan_sums_kernel(int64_t *__restrict__ sums, int64_t n) {
+    __shared__ int64_t part[kCompactChunk];
+    const int64_t per = (n + kCompactChunk - 1) / kCompactChunk;
+    const int64_t lo = threadIdx.x * per, hi = lo + per < n ? lo + per : n;
+    int64_t t = 0;
+    for (int64_t i = lo; i < hi; ++i) t += sums[i];
+    part[threadIdx.x] = t;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int64_t run = 0;
+        for (int i = 0; i < kCompactChunk; ++i) {
+            const int64_t x = part[i];
+            part[i] = run;
+            run += x;
+        }
+        sums[n] = run;
+    }
+    __syncthreads();
+    int64_t run = part[threadIdx.x];
+    for (int64_t i = lo; i < hi; ++i) {
+        const int64_t x = sums[i];
+        sums[i] = run;
+        run += x;
+    }
+}
+
+__global__ void __launch_bounds__(kCompactChunk)
+blocks_offsets_kernel(const int64_t *__restrict__ counts, int64_t nb, const int64_t *__restrict__ sums,
+                      int64_t *__restrict__ offs) {
+    __shared__ int64_t part[kCompactChunk];
+    const int64_t b = (int64_t)blockIdx.x * kCompactChunk + threadIdx.x;
+    part[threadIdx.x] = b < nb ? counts[b] : 0;
+    __syncthreads();
+    for (int o = 1; o < kCompactChunk; o <<= 1) {  // Hillis-Steele inclusive scan
+        const int64_t add = threadIdx.x >= (unsigned)o ? part[threadIdx.x - o] : 0;
+        __syncthreads();
+        part[threadIdx.x] += add;
+        __syncthreads();
+    }
+    if (b < nb) offs[b] = sums[blockIdx.x] + part[threadIdx.x] - counts[b];
+    if (b == nb - 1) offs[nb] = sums[blockIdx.x] + part[threadIdx.x];
+}
+
+struct CompactCols {
+    const uint64_t *in[FQ_MAX_PROJECT];
+    uint64_t *out[FQ_MAX_PROJECT];
+};
+
+__global__ void __launch_bounds__(256)
+blocks_copy_kernel(CompactCols cols, int32_t n_cols, const int64_t *__restrict__ counts,
+                   const int64_t *__restrict__ offs, int64_t nb, int64_t block_rows) {
+    for (int64_t b = blockIdx.x; b < nb; b += gridDim.x) {
+        const int64_t c = counts[b], src = b * block_rows, dst = offs[b];
+        for (int j = 0; j < n_cols; ++j)
+            for (int64_t r = threadIdx.x; r < c; r += blockDim.x) cols.out[j][dst + r] = cols.in[j][src + r];
+    }
+}
+
 // Workspace of fq_filter_project: [total][flag words: predicate,
 // expressions][kMaxSelectXcds ticket counters, a 128 B line each][one
 // look-back status word per tile].
@@ -485,13 +566,13 @@ fq_status fq_filter_project(const fq_col *col, const fq_pred *pred, const fq_exp
 
 size_t fq_filter_project_blocks_workspace_bytes(void) { return 3 * sizeof(uint64_t); }  // total, flags, ticket
 
-fq_status fq_filter_project_blocks(const fq_col *col, int64_t block_rows, const fq_pred *pred, const fq_expr *values,
-                                   int32_t n_out, void *const *d_out, int64_t *d_counts, int64_t *out_len, void *d_ws,
-                                   size_t ws_bytes, void *stream) {
+fq_status fq_filter_project_blocks_async(const fq_col *col, int64_t block_rows, const fq_pred *pred,
+                                         const fq_expr *values, int32_t n_out, void *const *d_out, int64_t *d_counts,
+                                         uint64_t *h_result, void *d_ws, size_t ws_bytes, void *stream) {
     using namespace fqk;
     static_assert(FQ_PROJECT_MIN_BLOCK_ROWS == kProjectBlockTile, "the ABI's minimum block is the kernel's tile");
-    if (!out_len) return fqc::fail(FQ_E_INVALID, "fq_filter_project_blocks: NULL out_len");
-    *out_len = 0;
+    if (!h_result) return fqc::fail(FQ_E_INVALID, "fq_filter_project_blocks: NULL result words");
+    h_result[0] = h_result[1] = 0;
     if (block_rows < FQ_PROJECT_MIN_BLOCK_ROWS)
         return fqc::fail(FQ_E_INVALID, "fq_filter_project_blocks: block_rows below FQ_PROJECT_MIN_BLOCK_ROWS");
     ProjLaunch P;
@@ -509,10 +590,6 @@ fq_status fq_filter_project_blocks(const fq_col *col, int64_t block_rows, const 
     uint64_t *const total = (uint64_t *)d_ws;
     uint32_t *const flags = (uint32_t *)(total + 1);
     hipStream_t st = P.stream;
-    uint64_t local[2] = {0, 0};
-    uint64_t *const pinned = fqc::host_staging();
-    uint64_t *const host = pinned ? pinned : local;  // kept rows, flag words
-    host[0] = host[1] = 0;
     const int64_t nb = block_rows >= n ? 1 : (n + block_rows - 1) / block_rows;
     FQ_HIP_TRY(hipMemsetAsync(d_ws, 0, fq_filter_project_blocks_workspace_bytes(), st));
     if (P.pred.kind == FQ_PRED_NONE) {  // every row kept: outputs in place, counts = block lengths
@@ -520,19 +597,92 @@ fq_status fq_filter_project_blocks(const fq_col *col, int64_t block_rows, const 
         hipLaunchKernelGGL(block_lengths_kernel, dim3((unsigned)std::min<int64_t>((nb + 255) / 256, 4096)), dim3(256), 0,
                            st, d_counts, nb, std::min(block_rows, n), n);
         FQ_HIP_TRY(hipGetLastError());
-        FQ_HIP_TRY(hipMemcpyAsync(&host[1], flags, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-        host[0] = (uint64_t)n;
+        FQ_HIP_TRY(hipMemcpyAsync(&h_result[1], flags, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+        h_result[0] = (uint64_t)n;
     } else {
         if ((s = jit_project_blocks(col->dtype, P, block_rows, P.pred.kind == FQ_PRED_BITMAP ? P.pred.bitmap : nullptr,
                                     d_counts, flags, total, (uint32_t *)(total + 2))) != FQ_OK)
             return s;
-        FQ_HIP_TRY(hipMemcpyAsync(host, total, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+        FQ_HIP_TRY(hipMemcpyAsync(h_result, total, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     }
-    FQ_HIP_TRY(hipStreamSynchronize(st));
-    const uint32_t pred_flags = (uint32_t)(host[1] & 0xffffffffu), val_flags = (uint32_t)(host[1] >> 32);
+    return FQ_OK;
+}
+
+fq_status fq_filter_project_blocks_result(const uint64_t *h_result, int64_t *out_len) {
+    using namespace fqk;
+    if (!h_result || !out_len) return fqc::fail(FQ_E_INVALID, "fq_filter_project_blocks_result: NULL argument");
+    *out_len = 0;
+    const uint32_t pred_flags = (uint32_t)(h_result[1] & 0xffffffffu), val_flags = (uint32_t)(h_result[1] >> 32);
+    fq_status s;
     if ((s = flag_error(pred_flags)) != FQ_OK) return s;  // FilterTransform runs first
     if ((s = flag_error(val_flags)) != FQ_OK) return s;
-    *out_len = (int64_t)host[0];
+    *out_len = (int64_t)h_result[0];
+    return FQ_OK;
+}
+
+fq_status fq_filter_project_blocks(const fq_col *col, int64_t block_rows, const fq_pred *pred, const fq_expr *values,
+                                   int32_t n_out, void *const *d_out, int64_t *d_counts, int64_t *out_len, void *d_ws,
+                                   size_t ws_bytes, void *stream) {
+    if (!out_len) return fqc::fail(FQ_E_INVALID, "fq_filter_project_blocks: NULL out_len");
+    *out_len = 0;
+    uint64_t local[2] = {0, 0};
+    uint64_t *const pinned = fqc::host_staging();
+    uint64_t *const host = pinned ? pinned : local;  // kept rows, flag words
+    fq_status s = fq_filter_project_blocks_async(col, block_rows, pred, values, n_out, d_out, d_counts, host, d_ws,
+                                                 ws_bytes, stream);
+    if (s != FQ_OK) return s;
+    FQ_HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+    return fq_filter_project_blocks_result(host, out_len);
+}
+
+size_t fq_blocks_compact_workspace_bytes(int64_t n_blocks) {
+    const int64_t nb = n_blocks < 1 ? 1 : n_blocks;
+    const int64_t chunks = (nb + fqk::kCompactChunk - 1) / fqk::kCompactChunk;
+    return (size_t)(nb + 1 + chunks + 1) * sizeof(int64_t);
+}
+
+fq_status fq_blocks_compact(int32_t n_cols, const void *const *d_in, int64_t len, int64_t block_rows,
+                            const int64_t *d_counts, void *const *d_out, int64_t *out_len, void *d_ws, size_t ws_bytes,
+                            void *stream) {
+    using namespace fqk;
+    if (out_len) *out_len = 0;
+    if (n_cols < 0 || n_cols > FQ_MAX_PROJECT || (n_cols > 0 && (!d_in || !d_out)))
+        return fqc::fail(FQ_E_INVALID, "fq_blocks_compact: bad column list");
+    if (len < 0 || block_rows < 1) return fqc::fail(FQ_E_INVALID, "fq_blocks_compact: bad geometry");
+    if (len == 0) return FQ_OK;
+    const int64_t nb = (len + block_rows - 1) / block_rows;
+    if (!d_counts || !d_ws) return fqc::fail(FQ_E_INVALID, "fq_blocks_compact: NULL buffer");
+    if (ws_bytes < fq_blocks_compact_workspace_bytes(nb))
+        return fqc::fail(FQ_E_INVALID, "fq_blocks_compact: workspace too small");
+    CompactCols cols{};
+    for (int j = 0; j < n_cols; ++j) {
+        if (!d_in[j] || !d_out[j]) return fqc::fail(FQ_E_INVALID, "fq_blocks_compact: NULL column");
+        cols.in[j] = (const uint64_t *)d_in[j];
+        cols.out[j] = (uint64_t *)d_out[j];
+    }
+    hipStream_t st = (hipStream_t)stream;
+    int64_t *const offs = (int64_t *)d_ws;  // nb + 1
+    int64_t *const sums = offs + nb + 1;    // chunks + 1
+    const int64_t chunks = (nb + kCompactChunk - 1) / kCompactChunk;
+    hipLaunchKernelGGL(blocks_chunk_sums_kernel, dim3((unsigned)chunks), dim3(kCompactChunk), 0, st, d_counts, nb, sums);
+    FQ_HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(blocks_scan_sums_kernel, dim3(1), dim3(kCompactChunk), 0, st, sums, chunks);
+    FQ_HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(blocks_offsets_kernel, dim3((unsigned)chunks), dim3(kCompactChunk), 0, st, d_counts, nb, sums,
+                       offs);
+    FQ_HIP_TRY(hipGetLastError());
+    if (n_cols > 0) {
+        hipLaunchKernelGGL(blocks_copy_kernel, dim3((unsigned)std::min<int64_t>(nb, 1 << 20)), dim3(256), 0, st, cols,
+                           n_cols, d_counts, offs, nb, block_rows);
+        FQ_HIP_TRY(hipGetLastError());
+    }
+    if (!out_len) return FQ_OK;
+    uint64_t local = 0;
+    uint64_t *const pinned = fqc::host_staging();
+    uint64_t *const total = pinned ? pinned : &local;
+    FQ_HIP_TRY(hipMemcpyAsync(total, offs + nb, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    FQ_HIP_TRY(hipStreamSynchronize(st));
+    *out_len = (int64_t)*total;
     return FQ_OK;
 }
 

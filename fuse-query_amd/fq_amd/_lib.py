@@ -23,7 +23,8 @@ GPU_SYMBOLS = [
     "fq_predicate_bitmap", "fq_group_partition_workspace_bytes", "fq_group_aggregate_partitioned",
     "fq_group_dense_keys", "fq_group_table_merge", "fq_tune_set", "fq_tune_get", "fq_tune_reset",
     "fq_tune_select_counters", "fq_tune_jit_dump_dir", "fq_filter_project_blocks_workspace_bytes",
-    "fq_filter_project_blocks",
+    "fq_filter_project_blocks", "fq_filter_project_blocks_async", "fq_filter_project_blocks_result",
+    "fq_blocks_compact_workspace_bytes", "fq_blocks_compact",
 ]
 
 
@@ -83,6 +84,12 @@ _protos = {
     "fq_filter_project_blocks_workspace_bytes": (C.c_size_t, []),
     "fq_filter_project_blocks": (C.c_int32, [P(abi.fq_col), C.c_int64, P(abi.fq_pred), P(abi.fq_expr), C.c_int32,
                                              P(vp), vp, P(C.c_int64), vp, C.c_size_t, vp]),
+    "fq_filter_project_blocks_async": (C.c_int32, [P(abi.fq_col), C.c_int64, P(abi.fq_pred), P(abi.fq_expr),
+                                                   C.c_int32, P(vp), vp, P(C.c_uint64), vp, C.c_size_t, vp]),
+    "fq_filter_project_blocks_result": (C.c_int32, [P(C.c_uint64), P(C.c_int64)]),
+    "fq_blocks_compact_workspace_bytes": (C.c_size_t, [C.c_int64]),
+    "fq_blocks_compact": (C.c_int32, [C.c_int32, P(vp), C.c_int64, C.c_int64, vp, P(vp), P(C.c_int64), vp,
+                                      C.c_size_t, vp]),
     "fq_predicate_bitmap": (C.c_int32, [P(abi.fq_col), P(abi.fq_pred), vp, vp, vp]),
     "fq_group_table_bytes": (C.c_size_t, [C.c_int64, C.c_int32]),
     "fq_group_table_init": (C.c_int32, [P(abi.fq_group_table), vp]),

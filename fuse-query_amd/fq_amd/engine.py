@@ -27,6 +27,7 @@ ENGINE_SYMBOLS = [
     "fq_engine_execute_final", "fq_engine_get_stats", "fq_engine_reset_stats", "fq_result_num_rows",
     "fq_result_num_columns", "fq_result_column_name", "fq_result_column_type", "fq_result_value",
     "fq_result_text", "fq_result_free", "fq_result_mysql_type", "fq_result_values", "fq_engine_partial_state_bytes",
+    "fq_engine_execute_blocks", "fq_block_stream_next", "fq_block_stream_free",
 ]
 
 
@@ -36,7 +37,14 @@ class fq_engine_stats(C.Structure):
                 ("exec_ms", C.c_double), ("first_launch_ms", C.c_double), ("partial_ms", C.c_double),
                 ("exchange_ms", C.c_double), ("final_ms", C.c_double), ("exchanges", C.c_uint64),
                 ("exchange_rounds", C.c_uint64), ("exchange_bytes", C.c_uint64),
-                ("cached_block_bytes", C.c_uint64), ("cached_workspace_bytes", C.c_uint64)]
+                ("cached_block_bytes", C.c_uint64), ("cached_workspace_bytes", C.c_uint64),
+                ("project_launches", C.c_uint64), ("project_rows", C.c_uint64), ("project_kept", C.c_uint64),
+                ("project_bytes", C.c_uint64), ("project_ms", C.c_double)]
+
+
+class fq_device_block(C.Structure):
+    _fields_ = [("n_columns", C.c_int32), ("pipe", C.c_int32), ("names", P(C.c_char_p)), ("columns", P(abi.fq_col)),
+                ("rows", C.c_int64), ("block_rows", C.c_int64), ("n_blocks", C.c_int64), ("d_counts", C.c_void_p)]
 
 
 _protos = {
@@ -54,6 +62,9 @@ _protos = {
                                             P(C.c_void_p)]),
     "fq_engine_partial_state_bytes": (C.c_int32, [C.c_void_p, C.c_char_p, P(C.c_size_t)]),
     "fq_engine_get_stats": (C.c_int32, [C.c_void_p, P(fq_engine_stats)]),
+    "fq_engine_execute_blocks": (C.c_int32, [C.c_void_p, C.c_char_p, C.c_int32, C.c_int32, P(C.c_void_p)]),
+    "fq_block_stream_next": (C.c_int32, [C.c_void_p, P(fq_device_block), P(C.c_int32)]),
+    "fq_block_stream_free": (None, [C.c_void_p]),
     "fq_engine_reset_stats": (C.c_int32, [C.c_void_p]),
     "fq_result_num_rows": (C.c_int64, [C.c_void_p]),
     "fq_result_num_columns": (C.c_int32, [C.c_void_p]),
@@ -191,6 +202,48 @@ class Result:
         return "Result(names=%r, rows=%r)" % (self.names, self.rows[:10])
 
 
+class BlockStream:
+    """fq_engine_execute_blocks: a row pipeline's output as device DataBlocks
+    (include/fq_engine.h).  Iterating yields fq_device_block structs; each is
+    valid until the next one is pulled (or the stream is closed)."""
+
+    def __init__(self, engine, sql, rank=0, world=1):
+        h = C.c_void_p()
+        check(lib.fq_engine_execute_blocks(engine.h, sql.encode(), rank, world, C.byref(h)))
+        self.h = h
+        self.engine = engine  # the engine outlives its streams
+
+    def next(self):
+        """The next fq_device_block, or None at the end."""
+        b, has = fq_device_block(), C.c_int32(0)
+        check(lib.fq_block_stream_next(self.h, C.byref(b), C.byref(has)))
+        return b if has.value else None
+
+    def __iter__(self):
+        while True:
+            b = self.next()
+            if b is None:
+                return
+            yield b
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib.fq_block_stream_free(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class Engine:
     def __init__(self, device=0, worker_threads=8, modulo=True, profile=False, streams=1):
         h = C.c_void_p()
@@ -235,6 +288,11 @@ class Engine:
         out = C.c_void_p()
         check(lib.fq_engine_execute(self.h, sql.encode(), C.byref(out)))
         return Result(out)
+
+    def execute_blocks(self, sql, rank=0, world=1):
+        """The row pipeline's output blocks, left in HBM (BlockStream); rank of
+        world: this rank's numbers_mt partitions only."""
+        return BlockStream(self, sql, rank, world)
 
     def explain(self, sql):
         n = C.c_size_t(0)
@@ -284,4 +342,4 @@ class Engine:
         check(lib.fq_engine_reset_stats(self.h))
 
 
-__all__ = ["Engine", "Result", "FQError", "last_error", "ENGINE_SYMBOLS"]
+__all__ = ["Engine", "Result", "BlockStream", "FQError", "last_error", "ENGINE_SYMBOLS"]

@@ -106,6 +106,31 @@ def contiguous_column(n, dtype):
     return DeviceColumn(buf, n, dtype)
 
 
+def device_view(ptr, nbytes):
+    """A torch uint8 tensor over device memory the library owns (no copy, not
+    freed by torch): e.g. a block of fq_engine_execute_blocks."""
+    require_gpu()
+    return torch.as_tensor(_RawDevice(int(ptr), max(int(nbytes), 1)), device="cuda")
+
+
+def device_block_to_numpy(b):
+    """An fq_device_block's columns as numpy, one list of per-block arrays per
+    column (block-stream layout) or one array per column (plain)."""
+    cols = [b.columns[j] for j in range(b.n_columns)]
+    if b.block_rows > 0:
+        counts = device_view(b.d_counts, 8 * b.n_blocks).cpu().numpy().view(np.int64).copy() if b.n_blocks else \
+            np.zeros(0, np.int64)
+    out = []
+    for c in cols:
+        h = device_view(c.data, c.len * ELEM_SIZE[c.dtype]).cpu().numpy().view(NP_DTYPES[c.dtype]).copy() \
+            if c.len else np.zeros(0, NP_DTYPES[c.dtype])
+        if b.block_rows > 0:
+            out.append([h[k * b.block_rows: k * b.block_rows + int(n)] for k, n in enumerate(counts)])
+        else:
+            out.append(h[:b.rows])
+    return out
+
+
 def from_numpy(arr, dtype=None):
     require_gpu()
     arr = np.ascontiguousarray(arr)

@@ -72,6 +72,14 @@ typedef struct fq_engine_stats {
     /* gauges (the process's device block cache now; not reset) */
     uint64_t cached_block_bytes;     /* idle small blocks kept for reuse       */
     uint64_t cached_workspace_bytes; /* idle per-queue GROUP BY workspaces     */
+    /* FilterTransform -> ProjectionTransform over block streams (one
+     * fq_filter_project_blocks launch per device block of a partition)       */
+    uint64_t project_launches;
+    uint64_t project_rows;  /* rows those launches read                       */
+    uint64_t project_kept;  /* rows they kept                                 */
+    uint64_t project_bytes; /* algorithmic bytes: 8 per row read + 8 per kept
+                               row per projected column                       */
+    double project_ms;      /* summed event time of the launches (FQ_OPT_PROFILE) */
 } fq_engine_stats;
 
 /* device: HIP device ordinal.  Fails with FQ_E_HIP when no GPU is present.
@@ -120,6 +128,43 @@ fq_status fq_engine_partial_state_bytes(fq_engine *e, const char *sql, size_t *b
  * with a stride of `stride` bytes (rank order). */
 fq_status fq_engine_execute_final(fq_engine *e, const char *sql, const void *states, size_t stride,
                                   int32_t world, fq_result **out);
+
+/* ---- Row pipelines as a stream of device DataBlocks ----
+ * SelectExecutor::execute hands its caller the pipeline's SendableDataBlockStream
+ * (executor_select.rs:35-40, stream.rs:8-9); for Filter -> Projection over
+ * numbers_mt that stream is one filtered + projected DataBlock per 10,000-row
+ * source block (stream_expression.rs:38-50, transform_projection.rs:45-56).
+ * fq_engine_execute_blocks returns that stream with the blocks left in HBM:
+ * each fq_device_block is one device block of a partition pipe, which holds a
+ * run of the reference's blocks in its block-stream layout -- block b's rows
+ * are rows [b * block_rows, b * block_rows + d_counts[b]) of every column
+ * (fq_filter_project_blocks) -- or plain columns (block_rows = 0: every one of
+ * `rows` rows valid; e.g. after a LIMIT, or a projection without a filter).
+ * Blocks of one pipe arrive in row order; pipes interleave in arrival order
+ * like the reference's MergeProcessor channel (processor_merge.rs:45-63).
+ * The block's device memory and the pointers in *out stay valid until the next
+ * fq_block_stream_next or fq_block_stream_free on the stream; the device work
+ * that produced it is complete when next returns, and the caller's own work
+ * reading it must be complete before that next call.  Row pipelines only
+ * (aggregates: fq_engine_execute, FQ_E_UNSUPPORTED here).                   */
+typedef struct fq_block_stream fq_block_stream;
+typedef struct fq_device_block {
+    int32_t n_columns;
+    int32_t pipe;              /* partition pipe (partition order) it came from, -1 unknown */
+    const char *const *names;  /* the plan's output schema                 */
+    const fq_col *columns;     /* device columns (len = rows spanned)       */
+    int64_t rows;              /* valid rows                                */
+    int64_t block_rows;        /* > 0: block-stream layout of n_blocks blocks */
+    int64_t n_blocks;
+    const int64_t *d_counts;   /* device, n_blocks valid-row counts (NULL when block_rows = 0) */
+} fq_device_block;
+/* rank of world: the stream covers this rank's numbers_mt partitions
+ * [8r/G, 8(r+1)/G) (world 1: all of them), as fq_engine_execute_partial.  */
+fq_status fq_engine_execute_blocks(fq_engine *e, const char *sql, int32_t rank, int32_t world,
+                                   fq_block_stream **out);
+/* *has_block = 0 at the end of the stream (and *out is zeroed) */
+fq_status fq_block_stream_next(fq_block_stream *s, fq_device_block *out, int32_t *has_block);
+void fq_block_stream_free(fq_block_stream *s);
 
 fq_status fq_engine_get_stats(fq_engine *e, fq_engine_stats *out);
 fq_status fq_engine_reset_stats(fq_engine *e);

@@ -310,6 +310,28 @@ size_t fq_filter_project_blocks_workspace_bytes(void);
 fq_status fq_filter_project_blocks(const fq_col *col, int64_t block_rows, const fq_pred *pred,
                                    const fq_expr *values, int32_t n_out, void *const *d_out, int64_t *d_counts,
                                    int64_t *out_len, void *d_ws, size_t ws_bytes, void *stream);
+/* The same without waiting: the launch is enqueued on `stream` and, when the
+ * stream reaches it, the kept-row count and the flag words land in
+ * h_result[0..1] (pinned host memory the copy engine can write, e.g.
+ * hipHostMalloc).  After waiting (stream or event), fq_filter_project_blocks_
+ * result turns them into the call's status and *out_len.  For hosts that keep
+ * one queue busy with several pipes' launches (the engine's ProjectionTransform).
+ */
+fq_status fq_filter_project_blocks_async(const fq_col *col, int64_t block_rows, const fq_pred *pred,
+                                         const fq_expr *values, int32_t n_out, void *const *d_out, int64_t *d_counts,
+                                         uint64_t *h_result, void *d_ws, size_t ws_bytes, void *stream);
+fq_status fq_filter_project_blocks_result(const uint64_t *h_result, int64_t *out_len);
+/* A block stream's valid rows as one array: for each of n_cols 64-bit columns
+ * of the geometry above (len rows, ceil(len / block_rows) blocks, block b's
+ * valid rows the first d_counts[b] of its range), d_out[j] receives block 0's
+ * rows, then block 1's, ... (what arrow's concat of the reference's filtered
+ * blocks would hold).  *out_len (optional: the call then synchronises
+ * `stream`) = the rows written.  Workspace: fq_blocks_compact_workspace_bytes.
+ */
+size_t fq_blocks_compact_workspace_bytes(int64_t n_blocks);
+fq_status fq_blocks_compact(int32_t n_cols, const void *const *d_in, int64_t len, int64_t block_rows,
+                            const int64_t *d_counts, void *const *d_out, int64_t *out_len, void *d_ws, size_t ws_bytes,
+                            void *stream);
 /* FilterTransform's predicate alone as a Boolean column: LSB-first bitmap of
  * ceil(len/64) words, bits past len cleared (one kernel instead of one
  * fq_arith per expression node plus fq_compare).  d_flag: 4 bytes of device

@@ -832,6 +832,31 @@ def aggregate_query(total, exprs, where=None, modulo=True, parts=None):
     return out
 
 
+def projection_blocks(total, exprs, where=None, modulo=True):
+    """The non-aggregate stream as the reference yields it, per partition:
+    for every 10,000-row numbers block (numbers_stream.rs:27-83),
+    FilterTransform::expression_executor (transform_filter.rs:38-55) then each
+    projected expression (transform_projection.rs:45-56,
+    stream_expression.rs:38-50).  Returns [partition][block][column] -> list of
+    values (empty blocks kept)."""
+    out = []
+    for p in generate_parts(total):
+        funcs = [to_function(e, modulo=modulo) for e in exprs]
+        pred = to_function(where, modulo=modulo) if where is not None else None
+        blocks = []
+        for b in numbers_stream(total, [p]):
+            if pred is not None:
+                b = filter_block(pred, b)
+            cols = []
+            for f in funcs:
+                v = f.eval(b)
+                a = v if isinstance(v, Arr) else to_array(v, b.num_rows())
+                cols.append([a.get(i).value for i in range(b.num_rows())])
+            blocks.append(cols)
+        out.append(blocks)
+    return out
+
+
 def projection_query(total, exprs, where=None, limit=None, modulo=True):
     """Rows in partition order (the reference's merge order is arrival order)."""
     rows = []
