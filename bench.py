@@ -392,10 +392,10 @@ def run_project_engine(args, rank, world, local):
         dt = float(t.item())
     if bad:
         raise SystemExit("PARITY FAILURE: a timed step kept another row count")
+    st = eng.stats()
     got, _ = step(check=True)
     if got != expect:
         raise SystemExit("PARITY FAILURE after the timed steps: got %r expected %r" % (got, expect))
-    st = eng.stats()
     launches = max(st["project_launches"], 1)
     avg_ms = st["project_ms"] / launches
     bytes_per_launch = st["project_bytes"] / launches

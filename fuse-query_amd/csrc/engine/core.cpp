@@ -297,8 +297,12 @@ const DataField &DataSchema::field_with_name(const std::string &name) const { re
 //
 // Sizes are rounded up to classes (4 per power of two, <= 25 % slack) so that
 // blocks of one class are interchangeable; blocks above kMaxBlock are never
-// cached (they are rare and would crowd out the frequent small ones), each
-// queue keeps at most kStreamBytes and the whole cache kCacheBytes.  The one
+// cached among them (they would crowd out the frequent small ones), each
+// queue keeps at most kStreamBytes and the whole cache kCacheBytes.  Blocks
+// above kMaxBlock -- a row pipeline's projected columns, up to 2.5 GB each,
+// a few dozen per query -- are kept apart (large_cached_, kLargeBytes over all
+// queues): mapping them afresh from the pool cost ~150 ms per block on the
+// box (profiles/r04_c_prof_p1_timeline.txt).  The one
 // large workspace a queue may keep is counted apart (ws_cached_, capped at
 // kWorkspaceBytes over all queues), so a kept GROUP BY workspace never takes
 // the small blocks' room.  Every
@@ -312,6 +316,7 @@ class BlockCache {
     static constexpr size_t kStreamBytes = 2ull << 30;
     static constexpr size_t kMaxBlock = 1ull << 30;
     static constexpr size_t kWorkspaceBytes = 32ull << 30;  // kept workspaces, all queues
+    static constexpr size_t kLargeBytes = 96ull << 30;      // kept blocks above kMaxBlock, all queues
     static BlockCache &get() {
         static BlockCache *c = new BlockCache();  // never destroyed: buffers may outlive statics
         return *c;
@@ -329,17 +334,26 @@ class BlockCache {
         auto it = f->second.blocks.find(bytes);
         if (it == f->second.blocks.end()) return nullptr;
         void *p = it->second;
-        cached_ -= bytes;
-        f->second.bytes -= bytes;
+        if (bytes > kMaxBlock) {
+            large_cached_ -= bytes;
+        } else {
+            cached_ -= bytes;
+            f->second.bytes -= bytes;
+        }
         f->second.blocks.erase(it);
         return p;
     }
     // false: not cached (unregistered queue, oversized block or a cap
     // reached), the caller frees
     bool put(hipStream_t s, void *p, size_t bytes) {
-        if (bytes > kMaxBlock) return false;
         std::lock_guard<std::mutex> lk(mu_);
         auto f = free_.find(s);
+        if (bytes > kMaxBlock) {
+            if (f == free_.end() || large_cached_ + bytes > kLargeBytes) return false;
+            f->second.blocks.emplace(bytes, p);
+            large_cached_ += bytes;
+            return true;
+        }
         if (f == free_.end() || cached_ + bytes > kCacheBytes || f->second.bytes + bytes > kStreamBytes) return false;
         f->second.blocks.emplace(bytes, p);
         f->second.bytes += bytes;
@@ -376,7 +390,7 @@ class BlockCache {
         if (f == free_.end()) return;
         for (auto &b : f->second.blocks) {
             (void)hipFree(b.second);
-            cached_ -= b.first;
+            (b.first > kMaxBlock ? large_cached_ : cached_) -= b.first;
         }
         if (f->second.ws) {
             (void)hipFree(f->second.ws);
@@ -399,10 +413,11 @@ class BlockCache {
         }
         cached_ = 0;
         ws_cached_ = 0;
+        large_cached_ = 0;
     }
     size_t cached_bytes() {
         std::lock_guard<std::mutex> lk(mu_);
-        return cached_;
+        return cached_ + large_cached_;
     }
     size_t cached_workspace_bytes() {
         std::lock_guard<std::mutex> lk(mu_);
@@ -420,6 +435,7 @@ class BlockCache {
     std::unordered_map<hipStream_t, Queue> free_;
     size_t cached_ = 0;     // small blocks (kCacheBytes / kStreamBytes caps)
     size_t ws_cached_ = 0;  // kept workspaces (kWorkspaceBytes cap)
+    size_t large_cached_ = 0;  // blocks above kMaxBlock (kLargeBytes cap)
 };
 
 // One reusable ordering event per (thread, device) for cross-queue drops.

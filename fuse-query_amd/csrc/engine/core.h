@@ -188,10 +188,7 @@ class Runtime {
     static constexpr int kHostOnly = -1;  // no GPU: planning and AggregateFinal merges only
     explicit Runtime(int device);
     bool has_device() const { return device_ != kHostOnly; }
-    // default mem pool release threshold: a row pipeline without LIMIT keeps
-    // ~8-16 projected blocks of up to 5 GB in flight (8 pipes + the merge
-    // channel); below that working set every block would map fresh HBM
-    static constexpr uint64_t kPoolKeepBytes = 64ull << 30;
+    static constexpr uint64_t kPoolKeepBytes = 8ull << 30;  // default mem pool release threshold
     ~Runtime();
     int device() const { return device_; }
     WorkerRes *acquire();

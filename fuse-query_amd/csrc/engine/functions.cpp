@@ -743,15 +743,16 @@ static bool project_blocks(const DataBlock &b, const Column &c, const fq_pred *p
     hipEvent_t e0 = ctx.res->take_event(), e1 = ctx.res->take_event();
     fq_col ic = c.abi();
     fq_status st;
+    hipEvent_t done = ctx.res->take_event();
     {
         std::lock_guard<std::mutex> lk(*ctx.res->launch_mu);
-        if (prof) check_hip(hipEventRecord(e0, ctx.stream()), "hipEventRecord");
         st = fq_filter_project_blocks_async(&ic, B, pred, exprs.data(), (int32_t)exprs.size(), ptrs.data(),
-                                            (int64_t *)layout->counts->ptr, res, ws->ptr, ws->bytes, ctx.stream());
-        if (st == FQ_OK) check_hip(hipEventRecord(e1, ctx.stream()), "hipEventRecord");
+                                            (int64_t *)layout->counts->ptr, res, ws->ptr, ws->bytes,
+                                            prof ? e0 : nullptr, prof ? e1 : nullptr, ctx.stream());
+        if (st == FQ_OK) check_hip(hipEventRecord(done, ctx.stream()), "hipEventRecord");  // after the result copy
     }
     if (st == FQ_OK) {
-        hipError_t he = hipEventSynchronize(e1);
+        hipError_t he = hipEventSynchronize(done);
         if (he == hipSuccess && prof) {
             float ms = 0;
             if (hipEventElapsedTime(&ms, e0, e1) == hipSuccess) ctx.rt->stats.project_ns += (uint64_t)((double)ms * 1e6);
@@ -760,6 +761,7 @@ static bool project_blocks(const DataBlock &b, const Column &c, const fq_pred *p
     }
     ctx.res->give_event(e0);
     ctx.res->give_event(e1);
+    ctx.res->give_event(done);
     if (st == FQ_E_UNSUPPORTED) return false;  // the unfused path evaluates it (and raises what the reference does)
     check_fq(st);
     int64_t kept = 0;

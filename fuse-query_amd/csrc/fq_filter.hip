@@ -568,7 +568,8 @@ size_t fq_filter_project_blocks_workspace_bytes(void) { return 3 * sizeof(uint64
 
 fq_status fq_filter_project_blocks_async(const fq_col *col, int64_t block_rows, const fq_pred *pred,
                                          const fq_expr *values, int32_t n_out, void *const *d_out, int64_t *d_counts,
-                                         uint64_t *h_result, void *d_ws, size_t ws_bytes, void *stream) {
+                                         uint64_t *h_result, void *d_ws, size_t ws_bytes, void *ev_start,
+                                         void *ev_end, void *stream) {
     using namespace fqk;
     static_assert(FQ_PROJECT_MIN_BLOCK_ROWS == kProjectBlockTile, "the ABI's minimum block is the kernel's tile");
     if (!h_result) return fqc::fail(FQ_E_INVALID, "fq_filter_project_blocks: NULL result words");
@@ -592,17 +593,20 @@ fq_status fq_filter_project_blocks_async(const fq_col *col, int64_t block_rows, 
     hipStream_t st = P.stream;
     const int64_t nb = block_rows >= n ? 1 : (n + block_rows - 1) / block_rows;
     FQ_HIP_TRY(hipMemsetAsync(d_ws, 0, fq_filter_project_blocks_workspace_bytes(), st));
+    if (ev_start) FQ_HIP_TRY(hipEventRecord((hipEvent_t)ev_start, st));
     if (P.pred.kind == FQ_PRED_NONE) {  // every row kept: outputs in place, counts = block lengths
         if ((s = jit_project_map(col->dtype, P, flags + 1)) != FQ_OK) return s;
         hipLaunchKernelGGL(block_lengths_kernel, dim3((unsigned)std::min<int64_t>((nb + 255) / 256, 4096)), dim3(256), 0,
                            st, d_counts, nb, std::min(block_rows, n), n);
         FQ_HIP_TRY(hipGetLastError());
+        if (ev_end) FQ_HIP_TRY(hipEventRecord((hipEvent_t)ev_end, st));
         FQ_HIP_TRY(hipMemcpyAsync(&h_result[1], flags, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
         h_result[0] = (uint64_t)n;
     } else {
         if ((s = jit_project_blocks(col->dtype, P, block_rows, P.pred.kind == FQ_PRED_BITMAP ? P.pred.bitmap : nullptr,
                                     d_counts, flags, total, (uint32_t *)(total + 2))) != FQ_OK)
             return s;
+        if (ev_end) FQ_HIP_TRY(hipEventRecord((hipEvent_t)ev_end, st));
         FQ_HIP_TRY(hipMemcpyAsync(h_result, total, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     }
     return FQ_OK;
@@ -629,7 +633,7 @@ fq_status fq_filter_project_blocks(const fq_col *col, int64_t block_rows, const 
     uint64_t *const pinned = fqc::host_staging();
     uint64_t *const host = pinned ? pinned : local;  // kept rows, flag words
     fq_status s = fq_filter_project_blocks_async(col, block_rows, pred, values, n_out, d_out, d_counts, host, d_ws,
-                                                 ws_bytes, stream);
+                                                 ws_bytes, nullptr, nullptr, stream);
     if (s != FQ_OK) return s;
     FQ_HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
     return fq_filter_project_blocks_result(host, out_len);

@@ -85,7 +85,8 @@ _protos = {
     "fq_filter_project_blocks": (C.c_int32, [P(abi.fq_col), C.c_int64, P(abi.fq_pred), P(abi.fq_expr), C.c_int32,
                                              P(vp), vp, P(C.c_int64), vp, C.c_size_t, vp]),
     "fq_filter_project_blocks_async": (C.c_int32, [P(abi.fq_col), C.c_int64, P(abi.fq_pred), P(abi.fq_expr),
-                                                   C.c_int32, P(vp), vp, P(C.c_uint64), vp, C.c_size_t, vp]),
+                                                   C.c_int32, P(vp), vp, P(C.c_uint64), vp, C.c_size_t, vp, vp,
+                                                   vp]),
     "fq_filter_project_blocks_result": (C.c_int32, [P(C.c_uint64), P(C.c_int64)]),
     "fq_blocks_compact_workspace_bytes": (C.c_size_t, [C.c_int64]),
     "fq_blocks_compact": (C.c_int32, [C.c_int32, P(vp), C.c_int64, C.c_int64, vp, P(vp), P(C.c_int64), vp,

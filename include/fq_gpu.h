@@ -314,12 +314,15 @@ fq_status fq_filter_project_blocks(const fq_col *col, int64_t block_rows, const 
  * stream reaches it, the kept-row count and the flag words land in
  * h_result[0..1] (pinned host memory the copy engine can write, e.g.
  * hipHostMalloc).  After waiting (stream or event), fq_filter_project_blocks_
- * result turns them into the call's status and *out_len.  For hosts that keep
- * one queue busy with several pipes' launches (the engine's ProjectionTransform).
- */
+ * result turns them into the call's status and *out_len.  ev_start / ev_end
+ * (hipEvent_t, optional): recorded on `stream` right before and right after
+ * the kernel, so the pair times the kernel alone (not the workspace memset or
+ * the result copy).  For hosts that keep one queue busy with several pipes'
+ * launches (the engine's ProjectionTransform).                            */
 fq_status fq_filter_project_blocks_async(const fq_col *col, int64_t block_rows, const fq_pred *pred,
                                          const fq_expr *values, int32_t n_out, void *const *d_out, int64_t *d_counts,
-                                         uint64_t *h_result, void *d_ws, size_t ws_bytes, void *stream);
+                                         uint64_t *h_result, void *d_ws, size_t ws_bytes, void *ev_start,
+                                         void *ev_end, void *stream);
 fq_status fq_filter_project_blocks_result(const uint64_t *h_result, int64_t *out_len);
 /* A block stream's valid rows as one array: for each of n_cols 64-bit columns
  * of the geometry above (len rows, ceil(len / block_rows) blocks, block b's
