@@ -299,10 +299,12 @@ const DataField &DataSchema::field_with_name(const std::string &name) const { re
 // blocks of one class are interchangeable; blocks above kMaxBlock are never
 // cached among them (they would crowd out the frequent small ones), each
 // queue keeps at most kStreamBytes and the whole cache kCacheBytes.  Blocks
-// above kMaxBlock -- a row pipeline's projected columns, up to 2.5 GB each,
-// a few dozen per query -- are kept apart (large_cached_, kLargeBytes over all
-// queues): mapping them afresh from the pool cost ~150 ms per block on the
-// box (profiles/r04_c_prof_p1_timeline.txt).  The one
+// above kMaxBlock -- morsels past ~8M rows, a row pipeline's projected
+// columns (up to 2.5 GB each, a few dozen per query) -- are kept apart
+// (large_cached_, kLargeBytes over all queues): mapping them afresh from the
+// pool cost ~150 ms per 2.5 GB block on the box
+// (profiles/r04_c_prof_p1_timeline.txt), and 0.8 GB blocks that missed the
+// small class's 2 GB per-queue cap ran a p1 step at 900 ms instead of 28.  The one
 // large workspace a queue may keep is counted apart (ws_cached_, capped at
 // kWorkspaceBytes over all queues), so a kept GROUP BY workspace never takes
 // the small blocks' room.  Every
@@ -314,7 +316,7 @@ class BlockCache {
    public:
     static constexpr size_t kCacheBytes = 6ull << 30;
     static constexpr size_t kStreamBytes = 2ull << 30;
-    static constexpr size_t kMaxBlock = 1ull << 30;
+    static constexpr size_t kMaxBlock = 64ull << 20;  // above: the large-block class
     static constexpr size_t kWorkspaceBytes = 32ull << 30;  // kept workspaces, all queues
     static constexpr size_t kLargeBytes = 96ull << 30;      // kept blocks above kMaxBlock, all queues
     static BlockCache &get() {

@@ -943,6 +943,17 @@ __device__ __forceinline__ void gp_store(PRow *p, PRow v) { __builtin_nontempora
 __device__ __forceinline__ PRow gp_fetch(const PRow *p) { return __builtin_nontemporal_load(p); }
 #endif
 #define GP_TILE (BT * GP_ROWS)
+// Staging a tile's rows in LDS sorted by bin makes every store of a run
+// coalesced whatever the key order; range bins over 4-byte rows (numbers_mt
+// blocks: consecutive values, so a wave's rows share a bin and gp_rank hands
+// out consecutive places) store straight from the registers instead.  8-byte
+// rows are any column: random keys put a wave's 64 rows in ~64 bins, and the
+// direct stores ran gpart at 15.5 ms per 4.2e8 random rows (r04_d_g2_random)
+#if RANGE_BINS && GP_NARROW
+#define GP_STAGE 0
+#else
+#define GP_STAGE 1
+#endif
 #define GP_TBLK (GP_TILE / GP_BLK)
 // The kernels' log2p argument carries the bin shift of range bins in bits
 // 8..15: keys in [0, d), d <= P << shift, 2^shift <= S: bin b holds the keys
@@ -1030,8 +1041,9 @@ fq_jit_gpart(const TIn *__restrict__ col, long long n, const u64 *__restrict__ b
 #if GP_MOD32
     const GMod gm = gp_mod_init(n > 0 ? (u64)col[0] : 0ull, c);
 #endif
-#if !RANGE_BINS
-    __shared__ TIn s_stage[GP_TILE];
+#if GP_STAGE
+    // a tile's passing rows sorted by bin in LDS, written out run by run
+    __shared__ PRow s_stage[GP_TILE];
     __shared__ unsigned char s_bin[GP_TILE];
     __shared__ u32 s_start[256], s_tot;
 #endif
@@ -1129,10 +1141,8 @@ fq_jit_gpart(const TIn *__restrict__ col, long long n, const u64 *__restrict__ b
         }
 #endif
         __syncthreads();
-#if RANGE_BINS
-        const int t0 = 0;  // every thread takes blocks (no tile scan)
-#else
-        const int t0 = 64;
+#if GP_STAGE
+        const int t0 = 64;  // these 64 threads scan the bin counts meanwhile
         if (threadIdx.x < 64) {  // exclusive scan of the P <= 256 bin counts: 4 per lane
             const int l = threadIdx.x;
             u32 v[4], t = 0;
@@ -1157,6 +1167,8 @@ fq_jit_gpart(const TIn *__restrict__ col, long long n, const u64 *__restrict__ b
             }
             if (l == 63) s_tot = incl;
         }
+#else
+        const int t0 = 0;  // every thread takes blocks (no tile scan)
 #endif
         // the blocks this tile's run of bin b spills into, consecutive numbers
         // from the workgroup's region; bin b's chain is kept by thread t0 + b
@@ -1183,37 +1195,43 @@ fq_jit_gpart(const TIn *__restrict__ col, long long n, const u64 *__restrict__ b
             }
         }
         __syncthreads();
-#if RANGE_BINS
-        // straight from the registers: a wave's passing lanes mostly hold
-        // consecutive ranks of one bin (gp_rank), so the stores coalesce
-        // without the LDS staging the hash bins need (one barrier and 72 KB
-        // of LDS less)
+#if !GP_STAGE
+        {
+            // range bins over running keys: straight from the registers -- a
+            // wave's passing lanes mostly hold consecutive ranks of one bin
+            // (gp_rank), so the stores coalesce without the staging (one
+            // barrier and a per-row LDS round trip less)
 #pragma unroll
-        for (int k = 0; k < GP_ROWS; ++k) {
-            if (!((pass >> k) & 1u)) continue;
-            const u32 b = br[k] & 255u, o = s_fill[b] + (br[k] >> 8);
-            u32 blk = o < GP_BLK ? s_blk[b] : s_nb[b];
-            if (blk == 0xffffffffu) continue;  // (workspace overflow, reported)
-            if (o >= GP_BLK) blk += o / GP_BLK - 1u;
-            gp_store(out + (long long)blk * GP_BLK + (o & (GP_BLK - 1)), gp_pack(x[k], vbase, flags));
+            for (int k = 0; k < GP_ROWS; ++k) {
+                if (!((pass >> k) & 1u)) continue;
+                const u32 b = br[k] & 255u, o = s_fill[b] + (br[k] >> 8);
+                u32 blk = o < GP_BLK ? s_blk[b] : s_nb[b];
+                if (blk == 0xffffffffu) continue;  // (workspace overflow, reported)
+                if (o >= GP_BLK) blk += o / GP_BLK - 1u;
+                gp_store(out + (long long)blk * GP_BLK + (o & (GP_BLK - 1)), gp_pack(x[k], vbase, flags));
+            }
         }
 #else
+        {
+            // rows sorted by bin in LDS, then written run by run: consecutive
+            // threads store consecutive rows of one bin's chain
 #pragma unroll
-        for (int k = 0; k < GP_ROWS; ++k) {
-            if (!((pass >> k) & 1u)) continue;
-            const u32 pos = s_start[br[k] & 255u] + (br[k] >> 8);
-            s_stage[pos] = x[k];
-            s_bin[pos] = (unsigned char)(br[k] & 255u);
-        }
-        __syncthreads();
-        const u32 kept = s_tot;
-        for (u32 i = threadIdx.x; i < kept; i += BT) {
-            const u32 b = s_bin[i];
-            const u32 o = s_fill[b] + (i - s_start[b]);  // place in the chain from its current block
-            u32 blk = o < GP_BLK ? s_blk[b] : s_nb[b];
-            if (blk == 0xffffffffu) continue;  // (workspace overflow, reported)
-            if (o >= GP_BLK) blk += o / GP_BLK - 1u;
-            gp_store(out + (long long)blk * GP_BLK + (o & (GP_BLK - 1)), gp_pack(s_stage[i], vbase, flags));
+            for (int k = 0; k < GP_ROWS; ++k) {
+                if (!((pass >> k) & 1u)) continue;
+                const u32 pos = s_start[br[k] & 255u] + (br[k] >> 8);
+                s_stage[pos] = gp_pack(x[k], vbase, flags);
+                s_bin[pos] = (unsigned char)(br[k] & 255u);
+            }
+            __syncthreads();
+            const u32 kept = s_tot;
+            for (u32 i = threadIdx.x; i < kept; i += BT) {
+                const u32 b = s_bin[i];
+                const u32 o = s_fill[b] + (i - s_start[b]);  // place in the chain from its current block
+                u32 blk = o < GP_BLK ? s_blk[b] : s_nb[b];
+                if (blk == 0xffffffffu) continue;  // (workspace overflow, reported)
+                if (o >= GP_BLK) blk += o / GP_BLK - 1u;
+                gp_store(out + (long long)blk * GP_BLK + (o & (GP_BLK - 1)), s_stage[i]);
+            }
         }
 #endif
         __syncthreads();
@@ -1230,16 +1248,10 @@ fq_jit_gpart(const TIn *__restrict__ col, long long n, const u64 *__restrict__ b
         }
     }
     __syncthreads();
-#if RANGE_BINS
-    const int t0 = 0;
-#else
-    const int t0 = 64;
-#endif
-    if ((int)threadIdx.x >= t0)
-        for (int b = (int)threadIdx.x - t0; b < P; b += BT - t0) {
-            if (s_blk[b] != 0xffffffffu) blk_fill[s_blk[b]] = s_fill[b];
-            if (s_nblk[b]) atomicAdd(&bin_blocks[b], s_nblk[b]);
-        }
+    for (int b = (int)threadIdx.x; b < P; b += BT) {
+        if (s_blk[b] != 0xffffffffu) blk_fill[s_blk[b]] = s_fill[b];
+        if (s_nblk[b]) atomicAdd(&bin_blocks[b], s_nblk[b]);
+    }
     if (threadIdx.x == 0) used[blockIdx.x] = min(min(s_next, q), s_fail);
     flags = wave_or32(flags);
     if ((threadIdx.x & 63) == 0 && flags) atomicOr(&hdr[0], flags);
