@@ -829,7 +829,7 @@ void pack_group_consts(const GroupLaunch &G, HostGroupConsts &hc) {
 std::string group_shape_key(const GroupLaunch &G, int32_t tin, int dev) {
     std::string k = "G" + std::to_string(group_lds_local()) + std::to_string(group_key_plain()) +
                     std::to_string(group_chunked()) + std::to_string(group_wave_runs()) +
-                    std::to_string(group_cluster());
+                    std::to_string(group_cluster()) + "d" + std::to_string(fqc::knob(FQ_TUNE_GPART_DBUF));
     auto put = [&k](int32_t v) { k.append(reinterpret_cast<const char *>(&v), sizeof v); };
     auto prog = [&put](const KProg &p) {
         put(p.n);
@@ -1047,10 +1047,22 @@ fq_jit_gpart(const TIn *__restrict__ col, long long n, const u64 *__restrict__ b
     __shared__ unsigned char s_bin[GP_TILE];
     __shared__ u32 s_start[256], s_tot;
 #endif
-    __shared__ u32 s_cnt[256];
-    // per bin: the chain's current block and its rows, the first of the
-    // blocks taken for this tile, blocks taken in all
-    __shared__ u32 s_blk[256], s_fill[256], s_nb[256], s_nblk[256], s_next;
+    // per bin: this tile's rows, the chain's current block and its rows, the
+    // first of the blocks taken for this tile, blocks taken in all.  GP_DBUF:
+    // the counts and the chain state are double-buffered by tile parity --
+    // the claims of tile t write the state tile t + 1 starts from and zero its
+    // counts, so a tile takes two barriers instead of four (staged: three
+    // instead of five)
+#if GP_DBUF
+    __shared__ u32 s_cnt2[2][256], s_blk2[2][256], s_fill2[2][256];
+    int par = 0;
+#define s_cnt (s_cnt2[par])
+#define s_blk (s_blk2[par])
+#define s_fill (s_fill2[par])
+#else
+    __shared__ u32 s_cnt[256], s_blk[256], s_fill[256];
+#endif
+    __shared__ u32 s_nb[256], s_nblk[256], s_next;
     // first block of the first failed claim (workspace overflow): claims are
     // handed out in increasing order, so every block below it was written and
     // none above it was; used[] stops there.  (An LDS atomic on every claim
@@ -1061,6 +1073,9 @@ fq_jit_gpart(const TIn *__restrict__ col, long long n, const u64 *__restrict__ b
         s_blk[i] = 0xffffffffu;
         s_fill[i] = GP_BLK;  // full: the first row takes a block
         s_nblk[i] = 0;
+#if GP_DBUF
+        s_cnt2[0][i] = 0;
+#endif
     }
     if (threadIdx.x == 0) {
         s_next = 0;
@@ -1069,10 +1084,15 @@ fq_jit_gpart(const TIn *__restrict__ col, long long n, const u64 *__restrict__ b
     const u32 region = blockIdx.x * q;
     u32 flags = 0;
     const long long ntiles = (n + GP_TILE - 1) / GP_TILE;
+#if GP_DBUF
+    __syncthreads();
+#endif
     for (long long tt = blockIdx.x; tt < ntiles; tt += gridDim.x) {
+#if !GP_DBUF
         for (int i = threadIdx.x; i < P; i += BT) s_cnt[i] = 0;
-        TIn x[GP_ROWS];
         __syncthreads();
+#endif
+        TIn x[GP_ROWS];
         gp_load(col, n, tt, x);
         // per row: bin | rank << 8 (P <= 256 bins, rank < GP_TILE), one register instead of two
         u32 br[GP_ROWS], pass = 0;
@@ -1140,6 +1160,11 @@ fq_jit_gpart(const TIn *__restrict__ col, long long n, const u64 *__restrict__ b
             if (p) pass |= 1u << k;
         }
 #endif
+        // the rows as the blocks hold them (4 bytes for numbers_mt blocks): the
+        // 8-byte values are dead from here on
+        PRow px[GP_ROWS];
+#pragma unroll
+        for (int k = 0; k < GP_ROWS; ++k) px[k] = ((pass >> k) & 1u) ? gp_pack(x[k], vbase, flags) : (PRow)0;
         __syncthreads();
 #if GP_STAGE
         const int t0 = 64;  // these 64 threads scan the bin counts meanwhile
@@ -1176,7 +1201,16 @@ fq_jit_gpart(const TIn *__restrict__ col, long long n, const u64 *__restrict__ b
         if ((int)threadIdx.x >= t0) {
             for (int b = (int)threadIdx.x - t0; b < P; b += BT - t0) {
                 const u32 cnt = s_cnt[b], f = s_fill[b];
+#if GP_DBUF
+                s_cnt2[par ^ 1][b] = 0;
+                if (!cnt || f + cnt <= GP_BLK) {
+                    s_fill2[par ^ 1][b] = f + cnt;
+                    s_blk2[par ^ 1][b] = s_blk[b];
+                    continue;
+                }
+#else
                 if (!cnt || f + cnt <= GP_BLK) continue;
+#endif
                 const u32 need = (f + cnt - 1) / GP_BLK;
                 u32 base = atomicAdd(&s_next, need);
                 if (base + need > q) {  // cannot happen within the region bound; never write past it
@@ -1192,6 +1226,10 @@ fq_jit_gpart(const TIn *__restrict__ col, long long n, const u64 *__restrict__ b
                     s_nblk[b] += need;
                 }
                 s_nb[b] = base;
+#if GP_DBUF
+                s_blk2[par ^ 1][b] = base == 0xffffffffu ? 0xffffffffu : base + need - 1u;
+                s_fill2[par ^ 1][b] = f + cnt - need * GP_BLK;
+#endif
             }
         }
         __syncthreads();
@@ -1208,7 +1246,7 @@ fq_jit_gpart(const TIn *__restrict__ col, long long n, const u64 *__restrict__ b
                 u32 blk = o < GP_BLK ? s_blk[b] : s_nb[b];
                 if (blk == 0xffffffffu) continue;  // (workspace overflow, reported)
                 if (o >= GP_BLK) blk += o / GP_BLK - 1u;
-                gp_store(out + (long long)blk * GP_BLK + (o & (GP_BLK - 1)), gp_pack(x[k], vbase, flags));
+                gp_store(out + (long long)blk * GP_BLK + (o & (GP_BLK - 1)), px[k]);
             }
         }
 #else
@@ -1219,7 +1257,7 @@ fq_jit_gpart(const TIn *__restrict__ col, long long n, const u64 *__restrict__ b
             for (int k = 0; k < GP_ROWS; ++k) {
                 if (!((pass >> k) & 1u)) continue;
                 const u32 pos = s_start[br[k] & 255u] + (br[k] >> 8);
-                s_stage[pos] = gp_pack(x[k], vbase, flags);
+                s_stage[pos] = px[k];
                 s_bin[pos] = (unsigned char)(br[k] & 255u);
             }
             __syncthreads();
@@ -1234,6 +1272,9 @@ fq_jit_gpart(const TIn *__restrict__ col, long long n, const u64 *__restrict__ b
             }
         }
 #endif
+#if GP_DBUF
+        par ^= 1;  // the claims above wrote the next tile's state
+#else
         __syncthreads();
         for (int b = threadIdx.x; b < P; b += BT) {
             const u32 cnt = s_cnt[b], t = s_fill[b] + cnt;
@@ -1246,6 +1287,7 @@ fq_jit_gpart(const TIn *__restrict__ col, long long n, const u64 *__restrict__ b
                 s_fill[b] = t;
             }
         }
+#endif
     }
     __syncthreads();
     for (int b = (int)threadIdx.x; b < P; b += BT) {
@@ -1255,6 +1297,11 @@ fq_jit_gpart(const TIn *__restrict__ col, long long n, const u64 *__restrict__ b
     if (threadIdx.x == 0) used[blockIdx.x] = min(min(s_next, q), s_fail);
     flags = wave_or32(flags);
     if ((threadIdx.x & 63) == 0 && flags) atomicOr(&hdr[0], flags);
+#if GP_DBUF
+#undef s_cnt
+#undef s_blk
+#undef s_fill
+#endif
 }
 
 // rows of tile ti of a bin slice: row j of the tile is row j % GP_BLK of the
@@ -1429,6 +1476,8 @@ bool gen_groupby_source(const GroupLaunch &G, int32_t tin, Gen &g, std::string &
                            !ks.reversed && ks.c >= 1 && ks.c <= 0xffffffffull;
         src += "#define GP_MOD32 " + std::to_string(mod32 ? 1 : 0) + "\n#define GP_RANK_BATCH 1\n";
     }
+    // (4-byte rows only: the 8-byte rows' 64 KB staging leaves no LDS for the second buffers)
+    src += "#define GP_DBUF " + std::to_string(G.narrow && fqc::knob(FQ_TUNE_GPART_DBUF) ? 1 : 0) + "\n";
     // (range bins only: the hash bins' 72 KB staging leaves no LDS for it)
     // blocks are 2 KB either way: 256 8-byte rows, or 512 narrow ones (1 KB
     // blocks measured 1.11 -> 1.53 ms per 4.2e8-row partition pass)

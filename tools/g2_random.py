@@ -11,7 +11,7 @@ sum(x), max(x) ... GROUP BY x % 100000` over one 1.25e9-row partition: the same
 P (2^7 bins, ~1,024 groups per bin), three equal chunks of 4.17e8 rows, one
 table.  Checks a 2e7-row run against numpy first, then times --reps passes over
 the 10 GB partition with HIP events (median).  One JSON line on stdout.
-usage: g2_random.py [--reps 5] [--rows 1.25e9] [--narrow-iota]"""
+usage: g2_random.py [--reps 5] [--rows 1.25e9] [--narrow-iota] [--tune KNOB=V]"""
 import argparse
 import ctypes as C
 import json
@@ -76,8 +76,12 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--rows", type=float, default=1.25e9)
     ap.add_argument("--narrow-iota", action="store_true", help="a numbers_mt partition (4-byte rows) instead")
+    ap.add_argument("--tune", action="append", default=[], metavar="KNOB=VALUE", help="fq_tune_set (A/B sweeps)")
     a = ap.parse_args()
     ops.require_gpu()
+    for kv in a.tune:
+        k, v = kv.split("=", 1)
+        ops.tune_set(k.upper(), int(v))
     groups = check_small(a.narrow_iota)
     n = int(a.rows)
     chunk = ((n + 2) // 3 + 63) // 64 * 64
@@ -99,7 +103,7 @@ def main():
         "tool": "tools/g2_random.py", "column": "numbers_mt iota (4-byte partition rows)" if a.narrow_iota else
         "splitmix64(seed 0x5EED) random u64 (8-byte partition rows)",
         "query_shape": "GROUP BY x %% %d: count, sum, max; P = 2^%d bins, 3 chunks of %d rows" % (D, LOG2P, chunk),
-        "rows": n, "groups_checked_small": groups, "ms_per_partition": {"median": med, "min": ms[0], "max": ms[-1]},
+        "rows": n, "groups_checked_small": groups, "tune": a.tune, "ms_per_partition": {"median": med, "min": ms[0], "max": ms[-1]},
         "algorithmic_gbps": 8 * n / (med * 1e-3) / 1e9, "frac_of_8tbs": 8 * n / (med * 1e-3) / 1e9 / 8000.0,
     }), flush=True)
 
