@@ -316,3 +316,59 @@ def test_group_rows_with_a_wrapping_row_count_are_rejected():
     with Engine(device=-1) as eng:
         with pytest.raises(FQError, match="truncated"):
             eng.execute_final(sql, [bad])
+
+
+def error_worker(rank, world, port, sql, out_q):
+    sys.path.insert(0, os.path.join(ROOT, "fuse-query_amd"))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+
+    from fq_amd import FQError
+    from fq_amd import dist as fqd
+    from fq_amd.engine import Engine
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        with Engine(device=-1) as eng:
+            cap = eng.partial_state_bytes(sql)
+            try:
+                fqd.execute(eng, sql)
+                out_q.put((rank, None, cap, eng.stats()))
+            except FQError as e:
+                out_q.put((rank, (e.status, str(e)), cap, eng.stats()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("sql,rounds", [
+    ("SELECT sum(number) FROM system.numbers_mt(1000000)", 2),  # 32 B of states: the 103 B record takes round 2
+    (SQL % 1_000_000, 1),  # 120 B of states: the record fits round 1
+])
+def test_exchange_carries_error_records_past_the_sized_first_round(sql, rounds):
+    """fq_engine_execute_exchange over gloo with host-only engines: every
+    rank's partial fails (no device: the hot path has no CPU fallback), so every
+    rank ships an error record ("FQE1", status, message: 103 B here) instead of
+    its states.  Round 1 is sized to the SQL's states; a record longer than that
+    takes the second round, and every rank reports the same error -- none waits
+    in the collective.  The engine's exchange counters see the rounds."""
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=error_worker, args=(r, world, port, sql, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = sorted(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    from fq_amd import abi
+    errs = {err for _, err, _, _ in results}
+    assert len(errs) == 1
+    status, msg = errs.pop()
+    assert status == abi.FQ_E_HIP and "no device" in msg
+    for _, _, cap, st in results:
+        assert st["exchanges"] == 1 and st["exchange_rounds"] == rounds
+        round1 = world * (8 + (cap + 7) // 8 * 8)
+        assert st["exchange_bytes"] == round1 + (world * 104 if rounds == 2 else 0)
