@@ -208,3 +208,22 @@ def test_block_stream_c5_shape_closed_forms(eng):
         assert s1 % U64 == exp_s1 % U64 and s2 % U64 == exp_s2 % U64
     finally:
         eng.release_numbers()
+
+
+def test_block_stream_dropped_early_stops_the_pipes(eng):
+    """A host that stops pulling after the first block frees the stream: the
+    merge channel closes, the pipes stop after the block they are producing,
+    and the engine answers the next query normally (nothing left running)."""
+    import time
+    n = 4_000_000_000
+    sql = "SELECT number+1, number/2 FROM system.numbers_mt(%d) WHERE (number%%8)<3" % n
+    t0 = time.perf_counter()
+    s = eng.execute_blocks(sql)
+    b = s.next()
+    assert b is not None and b.rows > 0
+    s.close()
+    assert time.perf_counter() - t0 < 30
+    r = eng.execute("SELECT count(number), max(number) FROM system.numbers_mt(%d)" % 1_000_000)
+    assert r.rows == [(1_000_000, 999_999)]
+    per_pipe, _ = _pull(eng, "SELECT number+1, number/2 FROM system.numbers_mt(80000) WHERE (number%8)<3")
+    _check_against_oracle(per_pipe, R.projection_blocks(80_000, P1_EXPRS, P1_WHERE))
