@@ -49,7 +49,7 @@ constexpr KnobDef kDefs[FQ_TUNE_COUNT] = {
     {1, 0, 1, 1, false},         // SELECT_BLOCKS_DRAW
     {32, 8, 32, 1, true},        // SELECT_BLOCKS_ROWS
     {1, 0, 3, 1, false},         // SELECT_NT
-    {0, 0, 1, 1, false},         // GPART_DBUF
+    {1, 0, 1, 1, false},         // GPART_DBUF
 };
 
 std::atomic<int64_t> g_val[FQ_TUNE_COUNT] = {};
