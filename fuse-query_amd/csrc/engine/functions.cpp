@@ -786,7 +786,7 @@ static bool project_blocks(const DataBlock &b, const Column &c, const fq_pred *p
 // fused too when it is over that column, else its bitmap is evaluated
 // first).  false: not fusable, the caller materialises + evaluates.
 bool project_fused(const DataBlock &b, const std::vector<FunctionRef> &funcs, const SchemaRef &schema, ExecCtx &ctx,
-                   DataBlock &out) {
+                   DataBlock &out, bool block_stream) {
     if (funcs.empty() || funcs.size() > FQ_MAX_PROJECT || !b.schema || b.columns.empty()) return false;
     std::vector<FusedChain> chains(funcs.size());
     bool computes = false;
@@ -825,7 +825,7 @@ bool project_fused(const DataBlock &b, const std::vector<FunctionRef> &funcs, co
         ptrs.push_back(outs.back().dptr());
         exprs.push_back(fc.expr);
     }
-    if (pred && b.sub_block_rows >= FQ_PROJECT_MIN_BLOCK_ROWS)
+    if (block_stream && pred && b.sub_block_rows >= FQ_PROJECT_MIN_BLOCK_ROWS)
         return project_blocks(b, c, pred, exprs, outs, ptrs, schema, ctx, out);
     const size_t wsb = fq_filter_project_workspace_bytes(n);
     auto ws = DeviceBuffer::alloc(wsb, ctx.stream());

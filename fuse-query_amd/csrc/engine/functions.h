@@ -338,6 +338,7 @@ Column eval_predicate(Function &pred, const DataBlock &b, ExecCtx &ctx);
 // ProjectionTransform's expressions (and the block's pending filter) through
 // one fq_filter_project call; false when the shape is not fusable
 bool project_fused(const DataBlock &b, const std::vector<FunctionRef> &funcs, const SchemaRef &schema, ExecCtx &ctx,
-                   DataBlock &out);
+                   DataBlock &out,
+                   bool block_stream = true);
 
 }  // namespace fq

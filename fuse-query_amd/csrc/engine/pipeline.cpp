@@ -377,11 +377,12 @@ StreamRef ProjectionTransform::execute() {
     SchemaRef schema = schema_;
     std::vector<FunctionRef> funcs;
     for (auto &f : funcs_) funcs.push_back(f->clone());
-    return std::make_unique<MapStream>(input_->execute(), [schema, funcs](DataBlock b) {
+    const bool blocks = block_stream_;
+    return std::make_unique<MapStream>(input_->execute(), [schema, funcs, blocks](DataBlock b) {
         ExecCtx &ctx = ExecCtx::current();
         DataBlock out;
         if (b.layout) b = materialize(b, ctx);  // a block stream in: one array first
-        if (project_fused(b, funcs, schema, ctx, out)) return out;  // filter + expressions in one pass
+        if (project_fused(b, funcs, schema, ctx, out, blocks)) return out;  // filter + expressions in one pass
         b = materialize(b, ctx);
         const int64_t rows = b.num_rows();
         out.schema = schema;

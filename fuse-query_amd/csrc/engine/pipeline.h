@@ -208,8 +208,13 @@ class FilterTransform : public IProcessor {  // transform_filter.rs:17-77
 
 class ProjectionTransform : public IProcessor {  // transform_projection.rs:16-78
    public:
-    ProjectionTransform(SchemaRef schema, std::vector<FunctionRef> funcs)
-        : schema_(std::move(schema)), funcs_(std::move(funcs)), input_(std::make_shared<EmptyProcessor>()) {}
+    // block_stream: a filtered numbers stream is projected into the reference's
+    // per-block geometry (fq_filter_project_blocks); false -- a LIMIT above
+    // compacts every block anyway and wants latency -- one contiguous array
+    // per block (fq_filter_project)
+    ProjectionTransform(SchemaRef schema, std::vector<FunctionRef> funcs, bool block_stream = true)
+        : schema_(std::move(schema)), funcs_(std::move(funcs)), input_(std::make_shared<EmptyProcessor>()),
+          block_stream_(block_stream) {}
     std::string name() const override { return "ProjectionTransform"; }
     void connect_to(ProcessorRef input) override { input_ = std::move(input); }
     StreamRef execute() override;
@@ -218,6 +223,7 @@ class ProjectionTransform : public IProcessor {  // transform_projection.rs:16-7
     SchemaRef schema_;
     std::vector<FunctionRef> funcs_;
     ProcessorRef input_;
+    bool block_stream_;
 };
 
 class AggregatePartialTransform : public IProcessor {  // transform_aggregate_partial.rs:18-79

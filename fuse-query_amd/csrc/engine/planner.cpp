@@ -634,7 +634,7 @@ Pipeline build_pipeline(const QueryPlan &plan, const QueryContextRef &ctx, bool 
                         if (e.is_aggregate()) throw_internal("Unsupported aggregator function: " + e.debug());
                     std::vector<FunctionRef> fs;
                     for (const auto &e : n.exprs) fs.push_back(e.to_function(ctx->factory));
-                    return std::make_shared<ProjectionTransform>(n.schema, fs);
+                    return std::make_shared<ProjectionTransform>(n.schema, fs, mode != ReadMode::kMorsels);
                 });
                 break;
             }
