@@ -742,7 +742,14 @@ static bool project_blocks(const DataBlock &b, const Column &c, const fq_pred *p
     const bool prof = ctx.rt->profile.load();
     hipEvent_t e0 = ctx.res->take_event(), e1 = ctx.res->take_event();
     fq_col ic = c.abi();
-    fq_status st;
+    // the shape's kernel compiled (first use: hipRTC, ~0.2 s) before the
+    // queue's launch lock is taken: a zero-length call only prepares it
+    fq_col none = ic;
+    none.len = 0;
+    fq_status st = fq_filter_project_blocks_async(&none, B, pred, exprs.data(), (int32_t)exprs.size(), ptrs.data(),
+                                                  nullptr, res, nullptr, 0, nullptr, nullptr, ctx.stream());
+    if (st == FQ_E_UNSUPPORTED) return false;
+    check_fq(st);
     hipEvent_t done = ctx.res->take_event();
     {
         std::lock_guard<std::mutex> lk(*ctx.res->launch_mu);
