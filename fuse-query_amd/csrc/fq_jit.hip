@@ -829,7 +829,8 @@ void pack_group_consts(const GroupLaunch &G, HostGroupConsts &hc) {
 std::string group_shape_key(const GroupLaunch &G, int32_t tin, int dev) {
     std::string k = "G" + std::to_string(group_lds_local()) + std::to_string(group_key_plain()) +
                     std::to_string(group_chunked()) + std::to_string(group_wave_runs()) +
-                    std::to_string(group_cluster()) + "d" + std::to_string(fqc::knob(FQ_TUNE_GPART_DBUF));
+                    std::to_string(group_cluster()) + "d" + std::to_string(fqc::knob(FQ_TUNE_GPART_DBUF)) + "r" +
+                    std::to_string(fqc::knob(FQ_TUNE_GPART_ROWS8));
     auto put = [&k](int32_t v) { k.append(reinterpret_cast<const char *>(&v), sizeof v); };
     auto prog = [&put](const KProg &p) {
         put(p.n);
@@ -906,7 +907,9 @@ std::string state_update(int32_t kind, int32_t dt, const std::string &P, const s
 // 4-byte offsets from col[0] - 2^31: 8 + 4 + 4 = 16 B per passing row; a
 // value outside the range sets flag 1024 and the launch reports it.
 const char *kGroupPartitionKernels = R"GP(
+#ifndef GP_ROWS
 #define GP_ROWS 8
+#endif
 #if GP_NARROW
 typedef u32 PRow;  // a kept row in the blocks: its offset from col[0] - 2^31
 __device__ __forceinline__ u64 gp_vbase(const TIn *__restrict__ col) { return (u64)col[0] - 0x80000000ull; }
@@ -1476,8 +1479,11 @@ bool gen_groupby_source(const GroupLaunch &G, int32_t tin, Gen &g, std::string &
                            !ks.reversed && ks.c >= 1 && ks.c <= 0xffffffffull;
         src += "#define GP_MOD32 " + std::to_string(mod32 ? 1 : 0) + "\n#define GP_RANK_BATCH 1\n";
     }
-    // (4-byte rows only: the 8-byte rows' 64 KB staging leaves no LDS for the second buffers)
-    src += "#define GP_DBUF " + std::to_string(G.narrow && fqc::knob(FQ_TUNE_GPART_DBUF) ? 1 : 0) + "\n";
+    // 8-byte rows: GP_ROWS rows per thread per tile (FQ_TUNE_GPART_ROWS8); at 8 their 64 KB staging leaves
+    // no LDS for the double buffers
+    const int rows8 = G.narrow ? 8 : (int)fqc::knob(FQ_TUNE_GPART_ROWS8);
+    if (rows8 != 8) src += "#define GP_ROWS " + std::to_string(rows8) + "\n";
+    src += "#define GP_DBUF " + std::to_string((G.narrow || rows8 < 8) && fqc::knob(FQ_TUNE_GPART_DBUF) ? 1 : 0) + "\n";
     // (range bins only: the hash bins' 72 KB staging leaves no LDS for it)
     // blocks are 2 KB either way: 256 8-byte rows, or 512 narrow ones (1 KB
     // blocks measured 1.11 -> 1.53 ms per 4.2e8-row partition pass)
