@@ -10,6 +10,8 @@
 //   EXPLAIN <sql>                  -> OK <escaped text> | ERR <status> <message>
 //   FINAL <world> <hex>... <sql>   -> OK <row;row...>   | ERR <status> <message>
 //   EXCHANGE <len0> <len1> ...     -> OK | FAIL <why>
+//   XSIZED <cap> <len0> <len1> ... -> OK | FAIL <why>  (fq_exchange_states_sized)
+//   XERRORS <world> <sql>          -> OK | FAIL <why>  (error records through fq_engine_execute_exchange)
 //   FUZZ <seed> <count>            -> OK <n_ok> <n_err> (mutations of every EXPLAIN sql seen)
 //   MERGE                          -> OK | FAIL <why>
 #include <stdint.h>
@@ -113,7 +115,7 @@ struct LocalAllReduce {
     }
 };
 
-std::string exchange(const std::vector<size_t> &lens) {
+std::string run_exchange(const std::vector<size_t> &lens, long cap = -1) {
     const int world = (int)lens.size();
     LocalAllReduce ar;
     ar.world = world;
@@ -126,8 +128,11 @@ std::string exchange(const std::vector<size_t> &lens) {
             for (size_t i = 0; i < mine.size(); ++i) mine[i] = payload(r, i);
             const void *rows = nullptr;
             size_t stride = 0;
-            if (fq_exchange_states(mine.data(), mine.size(), r, world, LocalAllReduce::call, &ar, &rows, &stride) !=
-                FQ_OK) {
+            const fq_status st =
+                cap < 0 ? fq_exchange_states(mine.data(), mine.size(), r, world, LocalAllReduce::call, &ar, &rows, &stride)
+                        : fq_exchange_states_sized(mine.data(), mine.size(), (size_t)cap, r, world, LocalAllReduce::call,
+                                                   &ar, &rows, &stride);
+            if (st != FQ_OK) {
                 why[(size_t)r] = fq_last_error();
                 return;
             }
@@ -146,6 +151,35 @@ std::string exchange(const std::vector<size_t> &lens) {
     for (auto &w : why)
         if (!w.empty()) return "FAIL " + w;
     return "OK";
+}
+
+// fq_engine_execute_exchange with one host-only engine per rank thread: every
+// partial fails (no device), so every rank ships an error record through the
+// sized exchange and every rank must report the same error.
+std::string exchange_errors(int world, const std::string &sql) {
+    LocalAllReduce ar;
+    ar.world = world;
+    std::vector<std::string> msg((size_t)world);
+    std::vector<std::thread> ts;
+    for (int r = 0; r < world; ++r)
+        ts.emplace_back([&, r] {
+            fq_engine *e = nullptr;
+            if (fq_engine_create(-1, &e) != FQ_OK) {
+                msg[(size_t)r] = "create";
+                return;
+            }
+            fq_result *out = nullptr;
+            const fq_status st = fq_engine_execute_exchange(e, sql.c_str(), r, world, LocalAllReduce::call, &ar, &out);
+            msg[(size_t)r] = st == FQ_OK ? std::string("no error") : std::to_string(st) + " " + fq_last_error();
+            fq_engine_stats s;
+            if (fq_engine_get_stats(e, &s) != FQ_OK || s.exchanges != 1) msg[(size_t)r] += " (no exchange counted)";
+            fq_result_free(out);
+            fq_engine_destroy(e);
+        });
+    for (auto &t : ts) t.join();
+    for (auto &m : msg)
+        if (m != msg[0]) return "FAIL ranks disagree: " + msg[0] + " / " + m;
+    return msg[0].rfind(std::to_string(FQ_E_HIP) + " ", 0) == 0 ? "OK" : "FAIL " + msg[0];
 }
 
 std::string merge_check() {
@@ -226,7 +260,20 @@ int main() {
             std::vector<size_t> lens;
             size_t l;
             while (in >> l) lens.push_back(l);
-            out = exchange(lens);
+            out = run_exchange(lens);
+        } else if (cmd == "XSIZED") {  // XSIZED <cap> <len0> <len1> ...
+            long cap = 0;
+            in >> cap;
+            std::vector<size_t> lens;
+            size_t l;
+            while (in >> l) lens.push_back(l);
+            out = run_exchange(lens, cap);
+        } else if (cmd == "XERRORS") {  // XERRORS <world> <sql>
+            int world = 0;
+            in >> world;
+            std::string sql;
+            std::getline(in, sql);
+            out = exchange_errors(world, sql.substr(1));
         } else if (cmd == "FUZZ") {
             uint32_t seed = 0;
             int count = 0;

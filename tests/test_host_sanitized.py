@@ -114,6 +114,13 @@ def test_asan_ubsan_planner_final_exchange_fuzz(built):
     for lens in ((5000, 40), (0, 0, 7), (4096, 4097, 1), (10, 20, 30, 40, 50, 60, 70, 80)):
         cmds.append("EXCHANGE " + " ".join(map(str, lens)))
         expected.append("OK")
+    for cap, lens in ((0, (10, 20)), (96, (96, 97, 96)), (5, (3, 0)), (104, (104,) * 8)):
+        cmds.append("XSIZED %d %s" % (cap, " ".join(map(str, lens))))
+        expected.append("OK")
+    for sql in ("SELECT sum(number) FROM system.numbers_mt(1000)",
+                "SELECT sum(number)/count(number), max(number), min(number) FROM system.numbers_mt(1000)"):
+        cmds.append("XERRORS 3 " + sql)
+        expected.append("OK")
     cmds.append("MERGE")
     expected.append("OK")
     cmds.append("FUZZ 12345 20000")
@@ -126,6 +133,7 @@ def test_asan_ubsan_planner_final_exchange_fuzz(built):
 
 
 def test_tsan_exchange_threads(built):
-    cmds = ["EXCHANGE 5000 40 3", "EXCHANGE 4096 4097 1 9000", "EXCHANGE " + " ".join(["100"] * 8), "MERGE"]
+    cmds = ["EXCHANGE 5000 40 3", "EXCHANGE 4096 4097 1 9000", "EXCHANGE " + " ".join(["100"] * 8), "MERGE",
+            "XSIZED 96 96 97 96", "XERRORS 4 SELECT sum(number) FROM system.numbers_mt(1000)"]
     out = _run(built["tsan"], "\n".join(cmds) + "\n", {"TSAN_OPTIONS": "halt_on_error=1"})
     assert out == ["OK"] * len(cmds)
