@@ -830,7 +830,8 @@ std::string group_shape_key(const GroupLaunch &G, int32_t tin, int dev) {
     std::string k = "G" + std::to_string(group_lds_local()) + std::to_string(group_key_plain()) +
                     std::to_string(group_chunked()) + std::to_string(group_wave_runs()) +
                     std::to_string(group_cluster()) + "d" + std::to_string(fqc::knob(FQ_TUNE_GPART_DBUF)) + "r" +
-                    std::to_string(fqc::knob(FQ_TUNE_GPART_ROWS8));
+                    std::to_string(fqc::knob(FQ_TUNE_GPART_ROWS8)) + "n" +
+                    std::to_string(fqc::knob(FQ_TUNE_GPART_ROWS4));
     auto put = [&k](int32_t v) { k.append(reinterpret_cast<const char *>(&v), sizeof v); };
     auto prog = [&put](const KProg &p) {
         put(p.n);
@@ -958,6 +959,12 @@ __device__ __forceinline__ PRow gp_fetch(const PRow *p) { return __builtin_nonte
 #define GP_STAGE 1
 #endif
 #define GP_TBLK (GP_TILE / GP_BLK)
+// rows per thread of the partition pass's tiles (FQ_TUNE_GPART_ROWS4 for 4-byte rows)
+#ifndef GPR_ROWS
+#define GPR_ROWS GP_ROWS
+#endif
+#define GPR_TILE (BT * GPR_ROWS)
+#define GP_NOBIN 0xffffu
 // The kernels' log2p argument carries the bin shift of range bins in bits
 // 8..15: keys in [0, d), d <= P << shift, 2^shift <= S: bin b holds the keys
 // [b << shift, (b + 1) << shift), so its LDS table is indexed by the key's
@@ -1016,11 +1023,17 @@ __device__ __forceinline__ u32 gp_key32(TIn x, const GMod &m) {
 }
 #endif
 __device__ __forceinline__ long long gp_row(long long tt, int k) {
-    return tt * GP_TILE + (long long)k * BT + threadIdx.x;
+    return tt * GPR_TILE + (long long)k * BT + threadIdx.x;
 }
-__device__ __forceinline__ void gp_load(const TIn *__restrict__ col, long long n, long long tt, TIn (&x)[GP_ROWS]) {
+__device__ __forceinline__ void gp_load(const TIn *__restrict__ col, long long n, long long tt, TIn (&x)[GPR_ROWS]) {
+    if ((tt + 1) * GPR_TILE <= n) {  // a whole tile: no per-row bound
+        const TIn *p = col + gp_row(tt, 0);
 #pragma unroll
-    for (int k = 0; k < GP_ROWS; ++k) {
+        for (int k = 0; k < GPR_ROWS; ++k) x[k] = __builtin_nontemporal_load(p + k * BT);
+        return;
+    }
+#pragma unroll
+    for (int k = 0; k < GPR_ROWS; ++k) {
         const long long row = gp_row(tt, k);
         x[k] = row < n ? __builtin_nontemporal_load(col + row) : TIn(0);
     }
@@ -1035,7 +1048,10 @@ __device__ __forceinline__ void gp_load(const TIn *__restrict__ col, long long n
 // stored ran it 1.09 -> 1.81 ms per 4.2e8 narrow rows (64 VGPRs: spills);
 // loading them into LDS by LDS-DMA instead measured within 1 % of the plain
 // loads (round 3, profiles/r03_s3_g2_prefetch_ab.txt) and was removed.
-extern "C" __global__ void __launch_bounds__(BT) __attribute__((amdgpu_waves_per_eu(BT >= 1024 ? 8 : 1)))
+#ifndef GPR_WAVES
+#define GPR_WAVES (BT >= 1024 ? 8 : 1)
+#endif
+extern "C" __global__ void __launch_bounds__(BT) __attribute__((amdgpu_waves_per_eu(GPR_WAVES)))
 fq_jit_gpart(const TIn *__restrict__ col, long long n, const u64 *__restrict__ bitmap, Consts c,
              u32 *__restrict__ used, u32 *__restrict__ bin_blocks, u32 *__restrict__ blk_bin,
              u32 *__restrict__ blk_fill, unsigned q, PRow *__restrict__ out, int log2p,
@@ -1046,8 +1062,8 @@ fq_jit_gpart(const TIn *__restrict__ col, long long n, const u64 *__restrict__ b
 #endif
 #if GP_STAGE
     // a tile's passing rows sorted by bin in LDS, written out run by run
-    __shared__ PRow s_stage[GP_TILE];
-    __shared__ unsigned char s_bin[GP_TILE];
+    __shared__ PRow s_stage[GPR_TILE];
+    __shared__ unsigned char s_bin[GPR_TILE];
     __shared__ u32 s_start[256], s_tot;
 #endif
     // per bin: this tile's rows, the chain's current block and its rows, the
@@ -1086,7 +1102,7 @@ fq_jit_gpart(const TIn *__restrict__ col, long long n, const u64 *__restrict__ b
     }
     const u32 region = blockIdx.x * q;
     u32 flags = 0;
-    const long long ntiles = (n + GP_TILE - 1) / GP_TILE;
+    const long long ntiles = (n + GPR_TILE - 1) / GPR_TILE;
 #if GP_DBUF
     __syncthreads();
 #endif
@@ -1095,18 +1111,21 @@ fq_jit_gpart(const TIn *__restrict__ col, long long n, const u64 *__restrict__ b
         for (int i = threadIdx.x; i < P; i += BT) s_cnt[i] = 0;
         __syncthreads();
 #endif
-        TIn x[GP_ROWS];
+        TIn x[GPR_ROWS];
         gp_load(col, n, tt, x);
-        // per row: bin | rank << 8 (P <= 256 bins, rank < GP_TILE), one register instead of two
-        u32 br[GP_ROWS], pass = 0;
+        // per row: bin | rank << 8 (P <= 256 bins, rank < GPR_TILE), one register instead of two
+        u32 br[GPR_ROWS], pass = 0;
 #if RANGE_BINS && GP_RANK_BATCH
         // bins of all rows first, then every row's rank atomic issued before
         // any return is read (one LDS round trip per tile, not one per row)
+        // a row that does not pass holds bin GP_NOBIN, which no bin equals:
+        // the wave's tests below are then one compare each
+        const bool full = (tt + 1) * GPR_TILE <= n;  // no row past the end (the uniform common case)
 #pragma unroll
-        for (int k = 0; k < GP_ROWS; ++k) {
+        for (int k = 0; k < GPR_ROWS; ++k) {
             const long long row = gp_row(tt, k);
-            u32 bk = 0;
-            if (row < n) {
+            u32 bk = GP_NOBIN;
+            if (full || row < n) {
                 Row r;
                 fq_prep(x[k], row, c, bitmap, flags, r);
                 if (r.pass) {
@@ -1120,36 +1139,37 @@ fq_jit_gpart(const TIn *__restrict__ col, long long n, const u64 *__restrict__ b
             }
             br[k] = bk;
         }
-        u32 rv[GP_ROWS], uni = 0;
-        const int lane = (int)(threadIdx.x & 63);
+        // per row k: when the wave's passing lanes share one bin (act = their
+        // mask, b0 the bin), its first lane takes all their places with one
+        // LDS atomic; every atomic is issued before any return is read
+        u32 rv[GPR_ROWS], uni = 0;
 #pragma unroll
-        for (int k = 0; k < GP_ROWS; ++k) {
-            const bool p = (pass >> k) & 1u;
-            const u64 act = __ballot(p);
+        for (int k = 0; k < GPR_ROWS; ++k) {
+            const u64 act = __builtin_amdgcn_ballot_w64(br[k] != GP_NOBIN);
             rv[k] = 0u;
             if (!act) continue;
             const int l0 = __builtin_ctzll(act);
             const u32 b0 = (u32)__builtin_amdgcn_readlane((int)br[k], l0);
-            if (__ballot(p && br[k] == b0) == act) {
+            if (__builtin_amdgcn_ballot_w64(br[k] == b0) == act) {
                 uni |= 1u << k;
-                if (lane == l0) rv[k] = atomicAdd(&s_cnt[b0], (u32)__popcll(act));
-            } else if (p) {
+                if ((int)(threadIdx.x & 63) == l0) rv[k] = atomicAdd(&s_cnt[b0], (u32)__popcll(act));
+            } else if (br[k] != GP_NOBIN) {
                 rv[k] = atomicAdd(&s_cnt[br[k]], 1u);
             }
         }
 #pragma unroll
-        for (int k = 0; k < GP_ROWS; ++k) {
+        for (int k = 0; k < GPR_ROWS; ++k) {
             u32 r = rv[k];
             if ((uni >> k) & 1u) {
-                const u64 act = __ballot((pass >> k) & 1u);
+                const u64 act = __builtin_amdgcn_ballot_w64(br[k] != GP_NOBIN);
                 r = (u32)__builtin_amdgcn_readlane((int)r, __builtin_ctzll(act)) +
-                    (u32)__popcll(act & ((1ull << lane) - 1ull));
+                    __builtin_amdgcn_mbcnt_hi((u32)(act >> 32), __builtin_amdgcn_mbcnt_lo((u32)act, 0u));
             }
-            br[k] |= r << 8;
+            br[k] = (br[k] & 255u) | r << 8;
         }
 #else
 #pragma unroll
-        for (int k = 0; k < GP_ROWS; ++k) {
+        for (int k = 0; k < GPR_ROWS; ++k) {
             const long long row = gp_row(tt, k);
             bool p = false;
             u32 bk = 0;
@@ -1165,9 +1185,9 @@ fq_jit_gpart(const TIn *__restrict__ col, long long n, const u64 *__restrict__ b
 #endif
         // the rows as the blocks hold them (4 bytes for numbers_mt blocks): the
         // 8-byte values are dead from here on
-        PRow px[GP_ROWS];
+        PRow px[GPR_ROWS];
 #pragma unroll
-        for (int k = 0; k < GP_ROWS; ++k) px[k] = ((pass >> k) & 1u) ? gp_pack(x[k], vbase, flags) : (PRow)0;
+        for (int k = 0; k < GPR_ROWS; ++k) px[k] = ((pass >> k) & 1u) ? gp_pack(x[k], vbase, flags) : (PRow)0;
         __syncthreads();
 #if GP_STAGE
         const int t0 = 64;  // these 64 threads scan the bin counts meanwhile
@@ -1242,14 +1262,21 @@ fq_jit_gpart(const TIn *__restrict__ col, long long n, const u64 *__restrict__ b
             // wave's passing lanes mostly hold consecutive ranks of one bin
             // (gp_rank), so the stores coalesce without the staging (one
             // barrier and a per-row LDS round trip less)
+            // every row's two LDS reads are issued before any is waited on (a
+            // row that does not pass reads bin 255's entries, unused)
+            u32 o[GPR_ROWS], blk[GPR_ROWS];
 #pragma unroll
-            for (int k = 0; k < GP_ROWS; ++k) {
-                if (!((pass >> k) & 1u)) continue;
-                const u32 b = br[k] & 255u, o = s_fill[b] + (br[k] >> 8);
-                u32 blk = o < GP_BLK ? s_blk[b] : s_nb[b];
-                if (blk == 0xffffffffu) continue;  // (workspace overflow, reported)
-                if (o >= GP_BLK) blk += o / GP_BLK - 1u;
-                gp_store(out + (long long)blk * GP_BLK + (o & (GP_BLK - 1)), px[k]);
+            for (int k = 0; k < GPR_ROWS; ++k) o[k] = s_fill[br[k] & 255u] + (br[k] >> 8);
+#pragma unroll
+            for (int k = 0; k < GPR_ROWS; ++k) {
+                const u32 b = br[k] & 255u;
+                blk[k] = *(o[k] < GP_BLK ? &s_blk[b] : &s_nb[b]);
+            }
+#pragma unroll
+            for (int k = 0; k < GPR_ROWS; ++k) {
+                if (!((pass >> k) & 1u) || blk[k] == 0xffffffffu) continue;  // (0xffffffff: workspace overflow, reported)
+                const u32 bb = o[k] < GP_BLK ? blk[k] : blk[k] + o[k] / GP_BLK - 1u;
+                gp_store(out + (long long)bb * GP_BLK + (o[k] & (GP_BLK - 1)), px[k]);
             }
         }
 #else
@@ -1257,7 +1284,7 @@ fq_jit_gpart(const TIn *__restrict__ col, long long n, const u64 *__restrict__ b
             // rows sorted by bin in LDS, then written run by run: consecutive
             // threads store consecutive rows of one bin's chain
 #pragma unroll
-            for (int k = 0; k < GP_ROWS; ++k) {
+            for (int k = 0; k < GPR_ROWS; ++k) {
                 if (!((pass >> k) & 1u)) continue;
                 const u32 pos = s_start[br[k] & 255u] + (br[k] >> 8);
                 s_stage[pos] = px[k];
@@ -1483,6 +1510,9 @@ bool gen_groupby_source(const GroupLaunch &G, int32_t tin, Gen &g, std::string &
     // no LDS for the double buffers
     const int rows8 = G.narrow ? 8 : (int)fqc::knob(FQ_TUNE_GPART_ROWS8);
     if (rows8 != 8) src += "#define GP_ROWS " + std::to_string(rows8) + "\n";
+    if (G.narrow && fqc::knob(FQ_TUNE_GPART_ROWS4) != 8)
+        src += "#define GPR_ROWS " + std::to_string(fqc::knob(FQ_TUNE_GPART_ROWS4)) +
+               (G.threads >= 1024 ? "\n#define GPR_WAVES 12\n" : "\n");  // 42 VGPRs: three workgroups per CU
     src += "#define GP_DBUF " + std::to_string((G.narrow || rows8 < 8) && fqc::knob(FQ_TUNE_GPART_DBUF) ? 1 : 0) + "\n";
     // (range bins only: the hash bins' 72 KB staging leaves no LDS for it)
     // blocks are 2 KB either way: 256 8-byte rows, or 512 narrow ones (1 KB

@@ -51,6 +51,7 @@ constexpr KnobDef kDefs[FQ_TUNE_COUNT] = {
     {1, 0, 3, 1, false},         // SELECT_NT
     {1, 0, 1, 1, false},         // GPART_DBUF
     {8, 4, 8, 4, false},         // GPART_ROWS8
+    {8, 4, 8, 4, false},         // GPART_ROWS4
 };
 
 std::atomic<int64_t> g_val[FQ_TUNE_COUNT] = {};

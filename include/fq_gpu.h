@@ -420,7 +420,8 @@ fq_status fq_jit_prepare(const fq_col *col, int64_t block_rows, const fq_pred *p
 #define FQ_TUNE_SELECT_NT 29          /* nontemporal output stores: bit 0 block-stream, bit 1 contiguous kernel; 1 */
 #define FQ_TUNE_GPART_DBUF 30        /* GROUP BY partition pass (4-byte rows): tile state double-buffered, 2 barriers per tile: 1 (0/1) */
 #define FQ_TUNE_GPART_ROWS8 31       /* GROUP BY partition + bins passes, 8-byte rows: rows per thread per tile, 8 (4/8) */
-#define FQ_TUNE_COUNT 32
+#define FQ_TUNE_GPART_ROWS4 32      /* GROUP BY partition pass, 4-byte rows: rows per thread per tile, 8 (4/8) */
+#define FQ_TUNE_COUNT 33
 /* FQ_E_INVALID for an unknown knob or a value outside the knob's set */
 fq_status fq_tune_set(int32_t knob, int64_t value);
 /* the knob's current value; -1 for an unknown knob */
