@@ -537,6 +537,7 @@ fq_status fq_group_aggregate_partitioned(const fq_group_table *t, const fq_col *
     // hash, no probe, no claim).  The kernels get log2p | shift << 8.
     // profiles/r02_groupby_range_bins.txt
     int lp_arg = log2_parts;
+    bool fitted = false;
     const int64_t d = group_key_range(G.key, G.key_dtype);
     const int64_t S = group_lds_slots(G.n_aggs, G.lds_bytes);
     if (d > 0 && fqc::knob(FQ_TUNE_GROUP_RANGE_BINS)) {
@@ -545,6 +546,13 @@ fq_status fq_group_aggregate_partitioned(const fq_group_table *t, const fq_col *
         if (((int64_t)1 << sh) <= S) {
             G.range_bins = 1;
             lp_arg = log2_parts | (sh << 8);
+            // the bins pass's table then needs one bin's 2^sh slots only (FQ_TUNE_GBINS_FIT_LDS): a
+            // smaller S, so more than one workgroup per CU fits its LDS
+            const int64_t fit = ((int64_t)1 << sh) * 8 * (1 + G.n_aggs);
+            if (fqc::knob(FQ_TUNE_GBINS_FIT_LDS) && fit < G.lds_bytes) {
+                G.lds_bytes = (int)fit;
+                fitted = true;
+            }
         }
     }
     part_ws_bytes(G.n, X.log2p, &X, d_ws);
@@ -559,7 +567,11 @@ fq_status fq_group_aggregate_partitioned(const fq_group_table *t, const fq_col *
     X.q = part_region_blocks(G.n, tile, X.grid, 1 << log2_parts);
     if ((uint64_t)X.q * (uint64_t)X.grid > X.max_blocks)
         return fqc::fail(FQ_E_INTERNAL, "fq_group_aggregate_partitioned: partition regions exceed the workspace");
-    X.bins_grid = fqc::device_cu_count();
+    // more than one bins workgroup per CU only where both its table (fitted) and its registers (4-byte rows at
+    // FQ_TUNE_GBINS_ROWS = 4: 54 VGPRs) leave room for it: g2's kernel set 4.58 -> 4.46 ms per partition
+    // (profiles/r04_o_gbins_ab/)
+    const bool two = fitted && G.narrow && fqc::knob(FQ_TUNE_GBINS_ROWS) == 4;
+    X.bins_grid = fqc::device_cu_count() * (two ? (int)fqc::knob(FQ_TUNE_GBINS_WG_PER_CU) : 1);
     return jit_groupby_partitioned(col->dtype, G, X);
 }
 

@@ -831,7 +831,8 @@ std::string group_shape_key(const GroupLaunch &G, int32_t tin, int dev) {
                     std::to_string(group_chunked()) + std::to_string(group_wave_runs()) +
                     std::to_string(group_cluster()) + "d" + std::to_string(fqc::knob(FQ_TUNE_GPART_DBUF)) + "r" +
                     std::to_string(fqc::knob(FQ_TUNE_GPART_ROWS8)) + "n" +
-                    std::to_string(fqc::knob(FQ_TUNE_GPART_ROWS4));
+                    std::to_string(fqc::knob(FQ_TUNE_GPART_ROWS4)) + "b" +
+                    std::to_string(fqc::knob(FQ_TUNE_GBINS_ROWS));
     auto put = [&k](int32_t v) { k.append(reinterpret_cast<const char *>(&v), sizeof v); };
     auto prog = [&put](const KProg &p) {
         put(p.n);
@@ -1341,6 +1342,9 @@ fq_jit_gpart(const TIn *__restrict__ col, long long n, const u64 *__restrict__ b
 // LDS, not on a dependent HBM load
 #define GP_ORD 1024
 #define GP_ORD_TILES (GP_ORD / GP_TBLK)
+#ifndef GB_PREFETCH
+#define GB_PREFETCH 1
+#endif
 __device__ __forceinline__ u32 gb_load(const PRow *__restrict__ vals, u64 vbase, const u64 *s_ord, long long ti,
                                        TIn (&x)[GP_ROWS]) {
     u32 live = 0;
@@ -1425,10 +1429,13 @@ fq_jit_groupby_bins(const PRow *__restrict__ vals, const u64 *__restrict__ order
             // blocks [lo, e) as tiles of GP_TBLK blocks; the next tile's
             // loads are in flight while this one goes through the LDS table
             const long long nt = (e - lo + GP_TBLK - 1) / GP_TBLK;
+#if GB_PREFETCH
             TIn nxt[GP_ROWS];
             u32 nlive = gb_load(vals, vbase, s_ord, 0, nxt);
+#endif
             for (long long ti = 0; ti < nt; ++ti) {
                 TIn x[GP_ROWS];
+#if GB_PREFETCH
 #pragma unroll
                 for (int k = 0; k < GP_ROWS; ++k) x[k] = nxt[k];
                 const u32 live = nlive;
@@ -1440,6 +1447,15 @@ fq_jit_groupby_bins(const PRow *__restrict__ vals, const u64 *__restrict__ order
                     }
                     nlive = gb_load(vals, vbase, s_ord, ti + 1, nxt);
                 }
+#else
+                // (two workgroups per CU hide each other's loads)
+                if (ti > 0 && ti % GP_ORD_TILES == 0) {  // (uniform) the next GP_ORD entries
+                    __syncthreads();
+                    gb_stage(s_ord, order, lo, e, ti);
+                    __syncthreads();
+                }
+                const u32 live = gb_load(vals, vbase, s_ord, ti, x);
+#endif
                 Row r[GP_ROWS];
 #pragma unroll
                 for (int k = 0; k < GP_ROWS; ++k) {
@@ -1510,9 +1526,13 @@ bool gen_groupby_source(const GroupLaunch &G, int32_t tin, Gen &g, std::string &
     // no LDS for the double buffers
     const int rows8 = G.narrow ? 8 : (int)fqc::knob(FQ_TUNE_GPART_ROWS8);
     if (rows8 != 8) src += "#define GP_ROWS " + std::to_string(rows8) + "\n";
-    if (G.narrow && fqc::knob(FQ_TUNE_GPART_ROWS4) != 8)
+    // 4-byte rows: the bins pass's rows per thread (FQ_TUNE_GBINS_ROWS; at 4, without the next tile's loads in
+    // registers, 54 VGPRs: room for a second workgroup per CU) and the partition pass's (FQ_TUNE_GPART_ROWS4)
+    const int gbr = G.narrow ? (int)fqc::knob(FQ_TUNE_GBINS_ROWS) : 8;
+    if (gbr != 8) src += "#define GP_ROWS " + std::to_string(gbr) + "\n#define GB_PREFETCH 0\n";
+    if (G.narrow && (fqc::knob(FQ_TUNE_GPART_ROWS4) != 8 || gbr != 8))
         src += "#define GPR_ROWS " + std::to_string(fqc::knob(FQ_TUNE_GPART_ROWS4)) +
-               (G.threads >= 1024 ? "\n#define GPR_WAVES 12\n" : "\n");  // 42 VGPRs: three workgroups per CU
+               (G.threads >= 1024 && fqc::knob(FQ_TUNE_GPART_ROWS4) == 4 ? "\n#define GPR_WAVES 12\n" : "\n");  // 42 VGPRs: three workgroups per CU
     src += "#define GP_DBUF " + std::to_string((G.narrow || rows8 < 8) && fqc::knob(FQ_TUNE_GPART_DBUF) ? 1 : 0) + "\n";
     // (range bins only: the hash bins' 72 KB staging leaves no LDS for it)
     // blocks are 2 KB either way: 256 8-byte rows, or 512 narrow ones (1 KB

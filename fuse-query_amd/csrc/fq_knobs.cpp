@@ -52,6 +52,9 @@ constexpr KnobDef kDefs[FQ_TUNE_COUNT] = {
     {1, 0, 1, 1, false},         // GPART_DBUF
     {8, 4, 8, 4, false},         // GPART_ROWS8
     {8, 4, 8, 4, false},         // GPART_ROWS4
+    {4, 4, 8, 4, false},         // GBINS_ROWS
+    {2, 1, 4, 1, false},         // GBINS_WG_PER_CU
+    {1, 0, 1, 1, false},         // GBINS_FIT_LDS
 };
 
 std::atomic<int64_t> g_val[FQ_TUNE_COUNT] = {};

@@ -421,7 +421,10 @@ fq_status fq_jit_prepare(const fq_col *col, int64_t block_rows, const fq_pred *p
 #define FQ_TUNE_GPART_DBUF 30        /* GROUP BY partition pass (4-byte rows): tile state double-buffered, 2 barriers per tile: 1 (0/1) */
 #define FQ_TUNE_GPART_ROWS8 31       /* GROUP BY partition + bins passes, 8-byte rows: rows per thread per tile, 8 (4/8) */
 #define FQ_TUNE_GPART_ROWS4 32      /* GROUP BY partition pass, 4-byte rows: rows per thread per tile, 8 (4/8) */
-#define FQ_TUNE_COUNT 33
+#define FQ_TUNE_GBINS_ROWS 33       /* GROUP BY bins pass, 4-byte rows: rows per thread per tile, 4 (4/8)     */
+#define FQ_TUNE_GBINS_WG_PER_CU 34  /* GROUP BY bins pass, fitted table + 4 rows: workgroups per CU, 2 (1..4) */
+#define FQ_TUNE_GBINS_FIT_LDS 35    /* GROUP BY bins pass, range bins: LDS table of one bin's keys, 1 (0/1)  */
+#define FQ_TUNE_COUNT 36
 /* FQ_E_INVALID for an unknown knob or a value outside the knob's set */
 fq_status fq_tune_set(int32_t knob, int64_t value);
 /* the knob's current value; -1 for an unknown knob */
