@@ -826,13 +826,35 @@ void pack_group_consts(const GroupLaunch &G, HostGroupConsts &hc) {
     pack_tree_consts(G.pred, hc);
 }
 
+// Range bins over 4-byte rows store each row straight from its registers, which
+// coalesces when a wave's consecutive rows share a bin: keys that advance by at
+// most 16 per row (adds, subtractions and divisions by constants, small
+// multipliers, then the `% d` or `& m`).  Other key programs stage the tile in
+// LDS sorted by bin.  Resident numbers_mt(1e10) through the engine
+// (profiles/r04_o_group_key_shapes*.jsonl): `(number * 7919) % 100000` 84.7 ms
+// per query with direct stores, 62.8 staged; `(number / 3) % 100000` 58.4
+// direct, 62.8 staged.
+bool group_stage_narrow(const GroupLaunch &G) {
+    if (!G.narrow || !G.range_bins) return false;
+    for (int i = 0; i + 1 < G.key.n; ++i) {
+        const KStep &st = G.key.s[i];
+        if (st.operand != FQ_OPERAND_CONST || st.reversed) return true;
+        switch (st.code) {
+            case K_ADD_I: case K_SUB_I: case K_DIV_U: case K_SHR_U: case K_DIVM_U: case K_DIVM32_U: break;
+            case K_MUL_I: if (st.c > 16) return true; break;
+            default: return true;
+        }
+    }
+    return false;
+}
+
 std::string group_shape_key(const GroupLaunch &G, int32_t tin, int dev) {
     std::string k = "G" + std::to_string(group_lds_local()) + std::to_string(group_key_plain()) +
                     std::to_string(group_chunked()) + std::to_string(group_wave_runs()) +
                     std::to_string(group_cluster()) + "d" + std::to_string(fqc::knob(FQ_TUNE_GPART_DBUF)) + "r" +
                     std::to_string(fqc::knob(FQ_TUNE_GPART_ROWS8)) + "n" +
                     std::to_string(fqc::knob(FQ_TUNE_GPART_ROWS4)) + "b" +
-                    std::to_string(fqc::knob(FQ_TUNE_GBINS_ROWS));
+                    std::to_string(fqc::knob(FQ_TUNE_GBINS_ROWS)) + "s" + std::to_string(group_stage_narrow(G) ? 1 : 0);
     auto put = [&k](int32_t v) { k.append(reinterpret_cast<const char *>(&v), sizeof v); };
     auto prog = [&put](const KProg &p) {
         put(p.n);
@@ -954,10 +976,12 @@ __device__ __forceinline__ PRow gp_fetch(const PRow *p) { return __builtin_nonte
 // out consecutive places) store straight from the registers instead.  8-byte
 // rows are any column: random keys put a wave's 64 rows in ~64 bins, and the
 // direct stores ran gpart at 15.5 ms per 4.2e8 random rows (r04_d_g2_random)
+#ifndef GP_STAGE
 #if RANGE_BINS && GP_NARROW
 #define GP_STAGE 0
 #else
 #define GP_STAGE 1
+#endif
 #endif
 #define GP_TBLK (GP_TILE / GP_BLK)
 // rows per thread of the partition pass's tiles (FQ_TUNE_GPART_ROWS4 for 4-byte rows)
@@ -1521,6 +1545,7 @@ bool gen_groupby_source(const GroupLaunch &G, int32_t tin, Gen &g, std::string &
                            (ks.code == K_MODM_U || ks.code == K_MODM32_U) && ks.operand == FQ_OPERAND_CONST &&
                            !ks.reversed && ks.c >= 1 && ks.c <= 0xffffffffull;
         src += "#define GP_MOD32 " + std::to_string(mod32 ? 1 : 0) + "\n#define GP_RANK_BATCH 1\n";
+        if (group_stage_narrow(G)) src += "#define GP_STAGE 1\n";
     }
     // 8-byte rows: GP_ROWS rows per thread per tile (FQ_TUNE_GPART_ROWS8); at 8 their 64 KB staging leaves
     // no LDS for the double buffers
