@@ -30,16 +30,47 @@ for _p in (os.path.join(ROOT, "fuse-query_amd"), os.path.join(ROOT, "oracle")):
     if _p not in sys.path:
         sys.path.insert(0, _p)
 
-import torch  # noqa: E402
-import torch.distributed as dist  # noqa: E402
 
-from fq_amd import abi, ops  # noqa: E402
-from fq_amd import dist as fqd  # noqa: E402
-from fq_amd.engine import OPT_GROUP_CHUNK_ROWS, Engine  # noqa: E402
-from fq_amd.numbers import BLOCK_SIZE, generate_parts, shard, stream_rows  # noqa: E402
+def _numbers_module():
+    """fq_amd/numbers.py on its own: importing it through the package would run
+    fq_amd/__init__.py, which loads the HIP library."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("fq_numbers", os.path.join(ROOT, "fuse-query_amd", "fq_amd",
+                                                                             "numbers.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+_numbers = _numbers_module()
+BLOCK_SIZE, generate_parts, shard, stream_rows = (_numbers.BLOCK_SIZE, _numbers.generate_parts, _numbers.shard,
+                                                  _numbers.stream_rows)
 
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 from srchash import kernel_sources_sha256  # noqa: E402
+
+# torch and the HIP library are imported by _load_runtime(), after the
+# launcher decision: a `--gpus N` parent that starts the ranks never loads the
+# HIP runtime (it only spawns processes), and the C-host leg runs as a child
+# before this process touches the GPU.
+torch = dist = abi = ops = fqd = Engine = None
+OPT_GROUP_CHUNK_ROWS = PROFILE_SPAN = None
+HIP_MODULES = ("torch", "fq_amd._lib", "fq_amd.ops", "fq_amd.engine")
+
+
+def _load_runtime():
+    global torch, dist, abi, ops, fqd, Engine, OPT_GROUP_CHUNK_ROWS, PROFILE_SPAN
+    import torch as _torch
+    import torch.distributed as _dist
+
+    from fq_amd import abi as _abi
+    from fq_amd import dist as _fqd
+    from fq_amd import ops as _ops
+    from fq_amd.engine import OPT_GROUP_CHUNK_ROWS as _ogc
+    from fq_amd.engine import PROFILE_SPAN as _ps
+    from fq_amd.engine import Engine as _Engine
+    torch, dist, abi, ops, fqd, Engine, OPT_GROUP_CHUNK_ROWS, PROFILE_SPAN = (
+        _torch, _dist, _abi, _ops, _fqd, _Engine, _ogc, _ps)
 
 METRIC = "rows/s + achieved HBM GB/s on 10B-row numbers_mt agg, 1/2/4/8 GPUs"
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
@@ -52,24 +83,23 @@ README_REF = {q: "reference README.md:%d (%.2f s for 1e10 rows, 8 vCPU KVM)" % (
 U64 = 2**64
 
 QUERIES = {
-    "c2": ("SELECT sum(number) FROM system.numbers_mt({N})", abi.AGG_SUM),
-    "c3": ("SELECT sum(number)/count(number), max(number), min(number) FROM system.numbers_mt({N})",
-           abi.AGG_SUM | abi.AGG_COUNT | abi.AGG_MAX | abi.AGG_MIN),
-    "c4": ("SELECT max(number+1) FROM system.numbers_mt({N}) WHERE (number%8)<3", abi.AGG_MAX | abi.AGG_COUNT),
+    "c2": "SELECT sum(number) FROM system.numbers_mt({N})",
+    "c3": "SELECT sum(number)/count(number), max(number), min(number) FROM system.numbers_mt({N})",
+    "c4": "SELECT max(number+1) FROM system.numbers_mt({N}) WHERE (number%8)<3",
     # the README's other timed queries (README.md:58-61; count(number) aside:
     # it needs no column read)
-    "max": ("SELECT max(number) FROM system.numbers_mt({N})", abi.AGG_MAX),
-    "max1": ("SELECT max(number+1) FROM system.numbers_mt({N})", abi.AGG_MAX),
-    "avg": ("SELECT sum(number) / count(number) FROM system.numbers_mt({N})", abi.AGG_SUM | abi.AGG_COUNT),
+    "max": "SELECT max(number) FROM system.numbers_mt({N})",
+    "max1": "SELECT max(number+1) FROM system.numbers_mt({N})",
+    "avg": "SELECT sum(number) / count(number) FROM system.numbers_mt({N})",
     # not a BASELINE config: filtered SUM, which needs the per-block emptiness
     # of the reference's state machine (block-mode scan)
-    "c4s": ("SELECT sum(number+1) FROM system.numbers_mt({N}) WHERE (number%8)<3", abi.AGG_SUM),
+    "c4s": "SELECT sum(number+1) FROM system.numbers_mt({N}) WHERE (number%8)<3",
     # not a BASELINE config: GROUP BY (no reference transform)
-    "g1": ("SELECT number%1000, count(number), sum(number), max(number) FROM system.numbers_mt({N}) "
-           "GROUP BY number%1000", 0),
+    "g1": "SELECT number%1000, count(number), sum(number), max(number) FROM system.numbers_mt({N}) "
+          "GROUP BY number%1000",
     # high cardinality: more groups than an LDS table holds (radix-partitioned launches)
-    "g2": ("SELECT number%100000, count(number), sum(number), max(number) FROM system.numbers_mt({N}) "
-           "GROUP BY number%100000", 0),
+    "g2": "SELECT number%100000, count(number), sum(number), max(number) FROM system.numbers_mt({N}) "
+          "GROUP BY number%100000",
 }
 GROUP_MOD = {"g1": 1000, "g2": 100000}
 # not a BASELINE config: FilterTransform -> ProjectionTransform (SURVEY 8f rank
@@ -671,10 +701,105 @@ def launch_ranks(n, argv):
     return subprocess.call(cmd)
 
 
+def stdout_to_stderr(fn, *a):
+    """Run fn with file descriptor 1 pointed at stderr: RCCL prints its version
+    banner on stdout at communicator init, and stdout carries ONE JSON line."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        return fn(*a)
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
+def rccl_world1(eng, sql, expect, device, args):
+    return stdout_to_stderr(_rccl_world1, eng, sql, expect, device, args)
+
+
+def _rccl_world1(eng, sql, expect, device, args):
+    """The multi-GPU step's transport at world 1: fq_engine_execute_rccl (partial
+    -> the state exchange through the library's own RCCL communicator, host
+    staged: memcpy -> H2D -> ncclAllReduce -> D2H -> sync -> final), steps x
+    the same statement, every result checked.  The 8-GPU run uses the same
+    calls; one box has one GPU and RCCL takes one rank per device, so this is
+    the exchange's fixed cost, not its xGMI time."""
+    try:
+        comm = fqd.RcclComm.single(device)
+    except Exception as e:  # report, never hide
+        return {"error": repr(e)}
+    try:
+        for _ in range(max(args.warmup, 1)):
+            r = list(fqd.execute(eng, sql, comm).rows[0])
+        if r != expect:
+            return {"error": "result %r != closed form %r" % (r, expect)}
+        eng.reset_stats()
+        t0 = time.perf_counter()
+        bad = 0
+        for _ in range(args.steps):
+            bad |= list(fqd.execute(eng, sql, comm).rows[0]) != expect
+        dt = time.perf_counter() - t0
+        st = eng.stats()
+        k = args.steps
+        ms = dt / k * 1e3
+        out = {"transport": "fq_engine_execute_rccl over fq_comm_init(world 1): ncclAllReduce of the [length, "
+                            "states] row, staged through pinned host memory",
+               "ms_per_step": ms, "result_ok": not bad,
+               "partial_ms": st["partial_ms"] / k, "exchange_ms": st["exchange_ms"] / k,
+               "final_ms": st["final_ms"] / k, "exchange_rounds": st["exchange_rounds"] / k,
+               "exchange_bytes": st["exchange_bytes"] / k}
+        log(0, "rccl world 1: %.3f ms/step, exchange %.1f us, %d B in %d round(s)"
+            % (ms, out["exchange_ms"] * 1e3, out["exchange_bytes"], out["exchange_rounds"]))
+        return out
+    except Exception as e:
+        return {"error": repr(e)}
+    finally:
+        comm.close()
+
+
+def check_rank_device(args, rank, world, local):
+    """This rank's GPU, checked by the rank itself (the launcher parent never
+    touches HIP): RCCL needs one visible GPU per local rank; the gloo rehearsal
+    lets ranks share the visible GPUs.  Exits non-zero when the GPU is missing."""
+    ops.require_gpu()
+    visible = torch.cuda.device_count()
+    if args.dist_backend == "nccl" and world > 1 and local >= visible:
+        raise SystemExit("bench.py rank %d: --gpus %d with RCCL needs a GPU per rank (LOCAL_RANK %d, %d visible; "
+                         "--dist-backend gloo rehearses N ranks on fewer)" % (rank, args.gpus, local, visible))
+    return local % visible if args.dist_backend == "gloo" else local
+
+
+def run_c_host(args):
+    """fq_c_client --bench STEPS N WARMUP as a child process (the C host of the
+    C ABI: libfq_amd.so on /opt/rocm's HIP runtime, no Python or torch), over the
+    same C3 workload; its JSON line, or an error record.  Runs before this
+    process has touched the GPU, so the two never hold HBM at the same time."""
+    exe = os.path.join(ROOT, "fuse-query_amd", "lib", "fq_c_client")
+    n_total = int(args.rows_total or args.rows_per_gpu)
+    cmd = [exe, "--bench", str(args.steps), str(n_total), str(max(args.warmup, 1))]
+    try:
+        p = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    except Exception as e:  # report, never hide
+        return {"error": repr(e), "cmd": " ".join(cmd[1:])}
+    if p.returncode != 0:
+        return {"error": "exit %d: %s" % (p.returncode, p.stderr.strip()[-500:]), "cmd": " ".join(cmd[1:])}
+    try:
+        out = json.loads(p.stdout.strip().splitlines()[-1])
+    except Exception as e:
+        return {"error": "unparsable output %r: %r" % (p.stdout[-300:], e)}
+    out["cmd"] = "fuse-query_amd/lib/fq_c_client " + " ".join(cmd[1:])
+    log(0, "c_host: %.1f G rows/s, %.3f ms/step, scan frac %.3f (C host, no torch)"
+        % (out.get("value", 0) / 1e9, out.get("ms_per_step", 0), out.get("frac", 0)))
+    return out
+
+
 def dry_run(rank, world):
     """--dry-run: the launch and the rendezvous without the GPU -- every rank
     joins a gloo group and rank 0 prints which ranks arrived (the CPU test of
     the launcher)."""
+    import torch.distributed as dist
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     if world > 1:
         dist.init_process_group("gloo")
@@ -705,6 +830,10 @@ def main():
                          "box's 8 threads for c3, ~5 s for p1; 4e9 rows for GROUP BY, a hash insert per row, ~3-10 s)")
     ap.add_argument("--cpu-threads", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-c-host", action="store_true",
+                    help="skip the C-host leg (fq_c_client --bench in a child process, c3 at N=1)")
+    ap.add_argument("--no-rccl-world1", action="store_true",
+                    help="skip the world-1 RCCL exchange leg (fq_engine_execute_rccl, aggregates at N=1)")
     ap.add_argument("--project-path", default="engine", choices=("engine", "blocks", "contiguous"),
                     help="p1: through the engine (fq_engine_execute_blocks, default), or the kernel alone at the "
                          "C ABI: block-stream output (fq_filter_project_blocks) or one contiguous output per "
@@ -734,10 +863,12 @@ def main():
         raise SystemExit("bench.py: --gpus must be >= 1")
     if "WORLD_SIZE" not in os.environ:
         if args.gpus > 1:
-            if args.dist_backend == "nccl" and not args.dry_run and torch.cuda.device_count() < args.gpus:
-                # (device_count() makes no HIP context on this image)
-                raise SystemExit("bench.py: --gpus %d with RCCL needs %d GPUs, %d visible (--dist-backend gloo "
-                                 "rehearses N ranks on fewer)" % (args.gpus, args.gpus, torch.cuda.device_count()))
+            # The parent only spawns the ranks: it has loaded neither torch nor
+            # the HIP library (HIP_MODULES), so no HIP state exists to cross a
+            # fork; every rank checks its own device (check_rank_device).
+            loaded = [m for m in HIP_MODULES if m in sys.modules]
+            print("[bench] launcher parent: HIP-touching modules loaded before spawning: %s" % (loaded or "none"),
+                  file=sys.stderr, flush=True)
             sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     elif int(os.environ["WORLD_SIZE"]) != args.gpus:
         raise SystemExit("bench.py: --gpus %d but the launcher started WORLD_SIZE=%s ranks"
@@ -745,18 +876,23 @@ def main():
     if args.dry_run:
         return dry_run(int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")))
 
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # The drop-in stack a C/Rust host binds (tests/native/fq_c_client.c: no
+    # torch, /opt/rocm's HIP runtime), timed in a child process BEFORE this one
+    # touches the GPU, on the same workload: reported beside the line.
+    c_host = None
+    if world == 1 and args.query == "c3" and not args.no_c_host:
+        c_host = run_c_host(args)
+
+    _load_runtime()
     args.tuned = {}
     for kv in args.tune:
         k, v = kv.split("=", 1)
         ops.tune_set(k.upper(), int(v))
         args.tuned[k.upper()] = int(v)
-
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    ops.require_gpu()
-    if args.dist_backend == "gloo":
-        local = local % torch.cuda.device_count()  # rehearsal: ranks may share a GPU
+    local = check_rank_device(args, rank, world, local)
     torch.cuda.set_device(local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -775,12 +911,13 @@ def main():
     else:
         rows_per_gpu = int(args.rows_per_gpu)
         n_total = rows_per_gpu * world
-    sql, _mask = QUERIES[args.query]
-    sql = sql.format(N=n_total)
+    sql = QUERIES[args.query].format(N=n_total)
 
     # The engine: SQL -> Source x P -> [Filter] -> AggregatePartial x P -> Merge
     # -> AggregateFinal on this GPU (one host thread per pipe, fused scans).
-    eng = Engine(device=local, profile=True, streams=args.streams)
+    # FQ_OPT_PROFILE 2: one event span per query around its back-to-back scans
+    # (no event between two scans); with several queues an event pair per scan
+    eng = Engine(device=local, profile=PROFILE_SPAN if args.streams == 1 else True, streams=args.streams)
     if args.group_chunk_rows:
         eng.set_option(OPT_GROUP_CHUNK_ROWS, args.group_chunk_rows)
     mine = shard(generate_parts(n_total), rank, world)
@@ -797,7 +934,7 @@ def main():
     if world > 1 and args.dist_backend == "nccl":
         ok = 1
         try:
-            comm = fqd.RcclComm(local)
+            comm = stdout_to_stderr(fqd.RcclComm, local)
         except Exception as e:  # reported; the same protocol then runs over torch's RCCL group
             log(rank, "native RCCL communicator unavailable on rank %d: %r" % (rank, e))
             ok = 0
@@ -900,6 +1037,9 @@ def main():
     rows_per_launch = st["scan_rows"] / launches
     achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9  # algorithmic GB/s of the fused scan
     value = n_total * args.steps / dt
+    rccl_w1 = None
+    if world == 1 and args.dist_backend == "nccl" and args.query not in GROUP_MOD and not args.no_rccl_world1:
+        rccl_w1 = rccl_world1(eng, sql, expect, local, args)
     out = None
     if rank == 0:
         # the partitioned GROUP BY (g2): gpart + block scatter + bins per chunk
@@ -951,14 +1091,21 @@ def main():
                            "fq_group_aggregate_partitioned (fq_jit_gpart + block grouping + fq_jit_groupby_bins), "
                            "one set per partition; achieved = the column's 8 B/row over the set"
                            if args.query == "g2" else
-                           "fq_aggregate fused scan (%s + finalize), one launch per partition%s"
-                           % (kernel, " (hipRTC-specialised for this expression shape)" if jitted else "")),
+                           "fq_aggregate fused scan (%s, its workgroup partials folded by its last workgroup: "
+                           "FQ_AGG_ONE_LAUNCH), one launch per partition%s; %s"
+                           % (kernel, " (hipRTC-specialised for this expression shape)" if jitted else "",
+                              "timed by one HIP-event span per query on the engine's queue (first scan start to "
+                              "last scan end, launch gaps included) / launches" if args.streams == 1 else
+                              "timed by an event pair per launch")),
                 "bytes_per_launch": bytes_per_launch,
             },
             "result": res if args.query not in GROUP_MOD else (
                 {"groups": ngroups, "first": [int(c[0]) for c in res], "last": [int(c[-1]) for c in res]}
                 if world == 1 else {"groups": ngroups, "first": list(res[0]), "last": list(res[-1])}),
             "host_ms_per_step": host_split(st, args.steps, dt / args.steps * 1e3, world),
+            # the whole step against its scans: what the step spends beyond them
+            "step_over_scans": (dt / args.steps * 1e3) / (avg_launch_ms * st["scan_launches"] / args.steps)
+            if st["scan_launches"] else None,
             "jit": {"specialised_launches": jitted, "kernels_compiled": jit1["kernels_compiled"],
                     "compile_ms": jit1["compile_ms"], "mode": jit1["mode"]},
         }
@@ -971,6 +1118,10 @@ def main():
         except Exception as e:  # report, never hide
             out["cpu_baseline"] = {"error": repr(e)}
     if rank == 0:
+        if c_host is not None:
+            out["c_host"] = c_host
+        if rccl_w1 is not None:
+            out["rccl_world1"] = rccl_w1
         if args.tuned:
             out["tune"] = args.tuned
         print(json.dumps(out), flush=True)

@@ -7,6 +7,7 @@
 #include <mutex>
 #include <string>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "../fq_common.h"
@@ -71,7 +72,25 @@ struct fq_engine {
     // repeated statement skips the parser and PlanBuilder).
     std::mutex plan_mu;
     std::unordered_map<std::string, fq::QueryPlan> plans;
+    // Open block streams: their pipes run on this engine's pool, queues and
+    // workspaces, so fq_engine_destroy closes them first (see fq_engine.h).
+    std::mutex streams_mu;
+    std::unordered_set<fq_block_stream *> streams;
 };
+
+namespace {
+// Stop a block stream's pipes (the merge channel closes, every pipe is joined)
+// and drop its device blocks; the stream object stays for fq_block_stream_free.
+void close_stream(fq_block_stream *bs) {
+    if (!bs->e) return;
+    fq::ExecCtx ctx(bs->e->rt.get());
+    bs->cur = fq::DataBlock{};
+    bs->cols.clear();
+    bs->s.reset();
+    bs->pipeline = fq::Pipeline{};
+    bs->qctx.reset();
+}
+}  // namespace
 
 // the Function-handle ABI (capi_function.cpp) runs its device calls here
 fq::Runtime *fq_engine_runtime(fq_engine *e) { return e->rt.get(); }
@@ -212,6 +231,19 @@ fq_status fq_engine_create(int32_t device, fq_engine **out) {
 
 void fq_engine_destroy(fq_engine *e) {
     if (!e) return;
+    {
+        // streams still open: joined here, while the pool and queues they use
+        // exist; they become orphans that only fq_block_stream_free accepts
+        std::lock_guard<std::mutex> lk(e->streams_mu);
+        for (fq_block_stream *bs : e->streams) {
+            try {
+                close_stream(bs);
+            } catch (...) {
+            }
+            bs->e = nullptr;
+        }
+        e->streams.clear();
+    }
     if (e->ds) e->ds->numbers()->unpin_all();
     delete e;
 }
@@ -222,7 +254,10 @@ fq_status fq_engine_set_option(fq_engine *e, int32_t option, int64_t value) {
         switch (option) {
             case FQ_OPT_WORKER_THREADS: e->worker_threads = (size_t)(value < 0 ? 0 : value); break;
             case FQ_OPT_MODULO: e->modulo = value != 0; break;
-            case FQ_OPT_PROFILE: e->rt->profile = value != 0; break;
+            case FQ_OPT_PROFILE:
+                if (value < 0 || value > 2) throw fq::FQException(FQ_E_INVALID, "FQ_OPT_PROFILE is 0, 1 or 2");
+                e->rt->profile = (int)value;
+                break;
             case FQ_OPT_STREAMS: e->rt->set_streams((int)value); break;
             case FQ_OPT_CHUNK_ROWS:
                 if (value < 10000 || value % 10000)
@@ -409,6 +444,8 @@ fq_status fq_engine_execute_blocks(fq_engine *e, const char *sql, int32_t rank, 
         bs->pipeline = fq::build_pipeline(plan, bs->qctx);
         bs->s = bs->pipeline.execute();
         e->rt->stats.queries++;
+        std::lock_guard<std::mutex> lk(e->streams_mu);
+        e->streams.insert(bs.get());
         *out = bs.release();
     });
 }
@@ -418,6 +455,9 @@ fq_status fq_block_stream_next(fq_block_stream *bs, fq_device_block *out, int32_
     *has_block = 0;
     *out = fq_device_block{};
     out->pipe = -1;
+    if (!bs->e)
+        return fqc::fail(FQ_E_INVALID, "fq_block_stream_next: the stream's engine was destroyed (fq_engine_destroy "
+                                       "closes the streams still open)");
     return guard([&] {
         fq::ExecCtx ctx(bs->e->rt.get());
         bs->cur = fq::DataBlock{};  // the caller is done with the previous block
@@ -451,14 +491,17 @@ fq_status fq_block_stream_next(fq_block_stream *bs, fq_device_block *out, int32_
 
 void fq_block_stream_free(fq_block_stream *bs) {
     if (!bs) return;
-    try {
-        fq::ExecCtx ctx(bs->e->rt.get());
-        bs->cur = fq::DataBlock{};
-        bs->s.reset();  // closes the merge channel and joins the pipes
-        delete bs;
-    } catch (...) {
-        delete bs;
+    if (fq_engine *e = bs->e) {
+        {
+            std::lock_guard<std::mutex> lk(e->streams_mu);
+            e->streams.erase(bs);
+        }
+        try {
+            close_stream(bs);  // closes the merge channel and joins the pipes
+        } catch (...) {
+        }
     }
+    delete bs;
 }
 
 fq_status fq_engine_partial_state_bytes(fq_engine *e, const char *sql, size_t *bytes) {

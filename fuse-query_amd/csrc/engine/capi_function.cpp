@@ -88,9 +88,14 @@ fq::SchemaRef block_schema(const fq_block &b) {
 }
 
 // The caller's columns, borrowed: the buffers are never freed or cached here.
+// block_rows / filter become the DataBlock's reference-block geometry and its
+// pending filter, exactly what a numbers_mt pipe hands AggregatePartial.
 fq::DataBlock borrow_block(const fq_block &b) {
     fq::DataBlock blk;
     blk.schema = block_schema(b);
+    if (b.block_rows < 0) throw fq::FQException(FQ_E_INVALID, "fq_block: negative block_rows");
+    blk.sub_block_rows = b.block_rows;
+    if (b.filter) blk.filter = b.filter->f->clone();
     for (int32_t i = 0; i < b.n_columns; ++i) {
         const fq_col &c = b.columns[i];
         if (c.len < 0 || (c.len > 0 && !c.data)) throw fq::FQException(FQ_E_INVALID, "fq_block: bad column");
@@ -192,7 +197,10 @@ fq_status fq_function_eval(fq_engine *e, fq_function *f, const fq_block *b, void
         return fqc::fail(FQ_E_INVALID, "fq_function_eval: bad argument");
     return guard([&] {
         fq::ExecCtx ctx(device_runtime(e));
-        const fq::DataBlock blk = borrow_block(*b);
+        fq::DataBlock blk = borrow_block(*b);
+        // a filtered block evaluates its kept rows (per reference block, in
+        // order: their concatenation is the compacted column)
+        if (fq::needs_materialize(blk)) blk = fq::materialize(blk, ctx);
         const fq::ColumnarValue v = f->f->eval(blk, ctx);
         *out_bytes = 0;
         *out_len = 0;
@@ -229,6 +237,30 @@ fq_status fq_function_accumulate(fq_engine *e, fq_function *f, const fq_block *b
         const fq::DataBlock blk = borrow_block(*b);
         f->f->accumulate(blk, ctx);
         ctx.sync();
+    });
+}
+
+fq_status fq_functions_accumulate(fq_engine *e, fq_function *const *fs, int32_t n, const fq_block *b) {
+    if (!e || !b || n < 0 || (n > 0 && !fs)) return fqc::fail(FQ_E_INVALID, "fq_functions_accumulate: bad argument");
+    for (int32_t i = 0; i < n; ++i)
+        if (!fs[i]) return fqc::fail(FQ_E_INVALID, "fq_functions_accumulate: NULL function");
+    return guard([&] {
+        fq::ExecCtx ctx(device_runtime(e));
+        const fq::DataBlock blk = borrow_block(*b);
+        // AggregatePartialTransform::execute's loop for this one block: the
+        // aggregators defer to the fusion, which launches one scan per distinct
+        // (argument, filter) and replays the states in (function) order
+        fq::AggFusion fusion(ctx);
+        fq::AggFusion *prev = ctx.fusion;
+        ctx.fusion = &fusion;
+        try {
+            for (int32_t i = 0; i < n; ++i) fs[i]->f->accumulate(blk, ctx);
+        } catch (...) {
+            ctx.fusion = prev;
+            throw;
+        }
+        ctx.fusion = prev;
+        fusion.finish();
     });
 }
 

@@ -301,12 +301,12 @@ const DataField &DataSchema::field_with_name(const std::string &name) const { re
 // queue keeps at most kStreamBytes and the whole cache kCacheBytes.  Blocks
 // above kMaxBlock -- morsels past ~8M rows, a row pipeline's projected
 // columns (up to 2.5 GB each, a few dozen per query) -- are kept apart
-// (large_cached_, kLargeBytes over all queues): mapping them afresh from the
+// (large_cached_, large_cap_ over all queues): mapping them afresh from the
 // pool cost ~150 ms per 2.5 GB block on the box
 // (profiles/r04_c_prof_p1_timeline.txt), and 0.8 GB blocks that missed the
 // small class's 2 GB per-queue cap ran a p1 step at 900 ms instead of 28.  The one
 // large workspace a queue may keep is counted apart (ws_cached_, capped at
-// kWorkspaceBytes over all queues), so a kept GROUP BY workspace never takes
+// ws_cap_ over all queues), so a kept GROUP BY workspace never takes
 // the small blocks' room.  Every
 // allocation failure -- stream-ordered, hipMalloc or the workspace -- calls
 // reclaim_device_memory(): the cache is flushed and the default pool trimmed
@@ -317,15 +317,29 @@ class BlockCache {
     static constexpr size_t kCacheBytes = 6ull << 30;
     static constexpr size_t kStreamBytes = 2ull << 30;
     static constexpr size_t kMaxBlock = 64ull << 20;  // above: the large-block class
-    static constexpr size_t kWorkspaceBytes = 32ull << 30;  // kept workspaces, all queues
-    static constexpr size_t kLargeBytes = 96ull << 30;      // kept blocks above kMaxBlock, all queues
+    // The two big classes are sized to the device (add_stream reads its HBM):
+    // kept blocks above kMaxBlock at most 3/10 of it (96 GB on a 288 GB
+    // MI355X), the kept workspaces at most 1/10 (32 GB cap), and a large block
+    // is only kept while the device still has max(8 GB, 1/16) of its HBM free,
+    // so another allocator in the process (torch, RCCL) keeps room.
+    static constexpr size_t kLargeMaxBytes = 96ull << 30;
+    static constexpr size_t kWorkspaceMaxBytes = 32ull << 30;
     static BlockCache &get() {
         static BlockCache *c = new BlockCache();  // never destroyed: buffers may outlive statics
         return *c;
     }
     void add_stream(hipStream_t s) {
         if (!fqc::knob(FQ_TUNE_BLOCK_CACHE)) return;  // A/B switch: plain stream-ordered pool
+        size_t free_b = 0, total = 0;
+        const bool sized = hipMemGetInfo(&free_b, &total) == hipSuccess && total > 0;
+        (void)hipGetLastError();
         std::lock_guard<std::mutex> lk(mu_);
+        if (sized && !device_total_) {
+            device_total_ = total;
+            large_cap_ = std::min(kLargeMaxBytes, total / 10 * 3);
+            ws_cap_ = std::min(kWorkspaceMaxBytes, total / 10);
+            reserve_ = std::max<size_t>(8ull << 30, total / 16);
+        }
         free_.emplace(s, Queue());
     }
     // a cached block of s of exactly `bytes` (a size class), or nullptr
@@ -348,14 +362,20 @@ class BlockCache {
     // false: not cached (unregistered queue, oversized block or a cap
     // reached), the caller frees
     bool put(hipStream_t s, void *p, size_t bytes) {
-        std::lock_guard<std::mutex> lk(mu_);
-        auto f = free_.find(s);
         if (bytes > kMaxBlock) {
-            if (f == free_.end() || large_cached_ + bytes > kLargeBytes) return false;
+            // the device's free HBM, read before the lock (a driver call)
+            size_t free_b = 0, total = 0;
+            const bool known = hipMemGetInfo(&free_b, &total) == hipSuccess;
+            (void)hipGetLastError();
+            std::lock_guard<std::mutex> lk(mu_);
+            auto f = free_.find(s);
+            if (f == free_.end() || large_cached_ + bytes > large_cap_ || (known && free_b < reserve_)) return false;
             f->second.blocks.emplace(bytes, p);
             large_cached_ += bytes;
             return true;
         }
+        std::lock_guard<std::mutex> lk(mu_);
+        auto f = free_.find(s);
         if (f == free_.end() || cached_ + bytes > kCacheBytes || f->second.bytes + bytes > kStreamBytes) return false;
         f->second.blocks.emplace(bytes, p);
         f->second.bytes += bytes;
@@ -379,7 +399,7 @@ class BlockCache {
     bool put_workspace(hipStream_t s, void *p, size_t bytes) {
         std::lock_guard<std::mutex> lk(mu_);
         auto f = free_.find(s);
-        if (f == free_.end() || f->second.ws || ws_cached_ + bytes > kWorkspaceBytes) return false;
+        if (f == free_.end() || f->second.ws || ws_cached_ + bytes > ws_cap_) return false;
         f->second.ws = p;
         f->second.ws_bytes = bytes;
         ws_cached_ += bytes;
@@ -436,8 +456,10 @@ class BlockCache {
     std::mutex mu_;
     std::unordered_map<hipStream_t, Queue> free_;
     size_t cached_ = 0;     // small blocks (kCacheBytes / kStreamBytes caps)
-    size_t ws_cached_ = 0;  // kept workspaces (kWorkspaceBytes cap)
-    size_t large_cached_ = 0;  // blocks above kMaxBlock (kLargeBytes cap)
+    size_t ws_cached_ = 0;  // kept workspaces (ws_cap_)
+    size_t large_cached_ = 0;  // blocks above kMaxBlock (large_cap_)
+    size_t device_total_ = 0;  // HBM of the device the first queue belongs to
+    size_t large_cap_ = 24ull << 30, ws_cap_ = 8ull << 30, reserve_ = 8ull << 30;  // until add_stream sizes them
 };
 
 // One reusable ordering event per (thread, device) for cross-queue drops.
@@ -541,6 +563,9 @@ WorkerRes *Runtime::acquire() {
     w->launch_mu = shared_mu_[q].get();
     w->ws_bytes = fq_aggregate_workspace_bytes(0);
     check_hip(alloc_with_reclaim([&] { return hipMalloc(&w->ws, w->ws_bytes); }), "hipMalloc(workspace)");
+    // the in-launch finalize's completion counter starts at zero; every
+    // FQ_AGG_ONE_LAUNCH scan on this workspace leaves it zero
+    check_hip(hipMemset(w->ws, 0, w->ws_bytes), "hipMemset(workspace)");
     all_.push_back(std::move(w));
     return all_.back().get();
 }
@@ -548,6 +573,26 @@ WorkerRes *Runtime::acquire() {
 void Runtime::release(WorkerRes *w) {
     std::lock_guard<std::mutex> lk(mu_);
     free_.push_back(w);
+}
+
+hipEvent_t Runtime::take_event() {
+    {
+        std::lock_guard<std::mutex> lk(mu_);
+        if (!events_.empty()) {
+            hipEvent_t e = events_.back();
+            events_.pop_back();
+            return e;
+        }
+    }
+    hipEvent_t e;
+    check_hip(hipEventCreate(&e), "hipEventCreate");
+    return e;
+}
+
+void Runtime::give_event(hipEvent_t e) {
+    if (!e) return;
+    std::lock_guard<std::mutex> lk(mu_);
+    events_.push_back(e);
 }
 
 Runtime::~Runtime() {
@@ -565,6 +610,7 @@ Runtime::~Runtime() {
         for (auto *c : w->slot_chunks) (void)hipHostFree(c);
         if (w->project_res) (void)hipHostFree(w->project_res);
     }
+    for (auto ev : events_) (void)hipEventDestroy(ev);
     for (auto &s : shared_) {
         BlockCache::get().drop_stream(s);
         (void)hipStreamDestroy(s);
@@ -597,6 +643,7 @@ hipEvent_t WorkerRes::take_event() {
 void ThreadPool::submit(std::function<void()> task) {
     std::unique_lock<std::mutex> lk(mu_);
     queue_.push_back(std::move(task));
+    pending_.store(queue_.size(), std::memory_order_release);
     if (idle_ < queue_.size()) threads_.emplace_back([this] { run(); });  // never wait for a thread
     else cv_.notify_one();
 }
@@ -604,12 +651,23 @@ void ThreadPool::submit(std::function<void()> task) {
 void ThreadPool::run() {
     std::unique_lock<std::mutex> lk(mu_);
     for (;;) {
-        ++idle_;
+        ++idle_;  // polling counts as idle: submit() hands the task to this thread
+        const int64_t spin_ns = fqc::knob(FQ_TUNE_POOL_SPIN_US) * 1000;
+        if (queue_.empty() && !stop_ && spin_ns > 0) {
+            lk.unlock();
+            const int64_t until = now_ns() + spin_ns;
+            while (pending_.load(std::memory_order_acquire) == 0 && !stopping_.load(std::memory_order_relaxed) &&
+                   now_ns() < until) {
+                for (int i = 0; i < 32; ++i) __builtin_ia32_pause();
+            }
+            lk.lock();
+        }
         cv_.wait(lk, [&] { return stop_ || !queue_.empty(); });
         --idle_;
         if (queue_.empty()) return;  // stop_
         std::function<void()> t = std::move(queue_.front());
         queue_.pop_front();
+        pending_.store(queue_.size(), std::memory_order_release);
         lk.unlock();
         t();
         lk.lock();
@@ -620,6 +678,7 @@ ThreadPool::~ThreadPool() {
     {
         std::lock_guard<std::mutex> lk(mu_);
         stop_ = true;
+        stopping_ = true;
     }
     cv_.notify_all();
     for (auto &t : threads_)

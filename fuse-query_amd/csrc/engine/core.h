@@ -168,6 +168,9 @@ struct WorkerRes {
 
 // Persistent host threads for the pipes (the reference spawns tokio tasks per
 // query, processor_merge.rs:49); a submitted task never waits for a thread.
+// A thread that finished a task polls the queue for FQ_TUNE_POOL_SPIN_US
+// before it sleeps: the next query's pipes usually arrive within ~0.1 ms, and
+// waking a sleeping thread is tens of microseconds at the head of every query.
 class ThreadPool {
    public:
     ~ThreadPool();
@@ -178,7 +181,9 @@ class ThreadPool {
     std::condition_variable cv_;
     std::vector<std::thread> threads_;
     std::deque<std::function<void()>> queue_;
-    size_t idle_ = 0;
+    std::atomic<size_t> pending_{0};  // queue_.size(), readable without mu_
+    std::atomic<bool> stopping_{false};
+    size_t idle_ = 0;                 // threads sleeping or polling for a task
     bool stop_ = false;
     void run();
 };
@@ -194,8 +199,12 @@ class Runtime {
     WorkerRes *acquire();
     void release(WorkerRes *w);
     void set_streams(int n);
+    int active_streams() const { return active_streams_; }
+    // timing-capable events shared across pipe threads (ScanGroup)
+    hipEvent_t take_event();
+    void give_event(hipEvent_t e);
     EngineStats stats;
-    std::atomic<bool> profile{false};
+    std::atomic<int> profile{0};  // FQ_OPT_PROFILE: 1 event pairs per launch, 2 one span per query
     // GROUP BY table slots for the next query (grows x16 when a query fills
     // its table; the query is then re-run)
     std::atomic<int64_t> group_capacity{4096};
@@ -213,7 +222,8 @@ class Runtime {
     std::vector<hipStream_t> shared_;  // FQ_OPT_STREAMS queues shared by the pipes
     std::vector<std::unique_ptr<std::mutex>> shared_mu_;
     size_t next_shared_ = 0;
-    int active_streams_ = 1;
+    std::atomic<int> active_streams_{1};
+    std::vector<hipEvent_t> events_;  // take_event / give_event (under mu_)
 };
 
 // Device memory released with hipFreeAsync on the stream that owns it (or

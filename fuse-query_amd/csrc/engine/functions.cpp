@@ -419,8 +419,8 @@ static fq_agg_state run_scan(const Column &col, int64_t block_rows, const fq_pre
                              uint32_t mask, ExecCtx &ctx) {
     auto out = DeviceBuffer::alloc(sizeof(fq_agg_state), ctx.stream());
     fq_col c = col.abi();
-    check_fq(fq_aggregate(&c, block_rows, pred, value, mask, (fq_agg_state *)out->ptr, ctx.res->ws, ctx.res->ws_bytes,
-                          ctx.stream()));
+    check_fq(fq_aggregate(&c, block_rows, pred, value, mask | FQ_AGG_ONE_LAUNCH, (fq_agg_state *)out->ptr,
+                          ctx.res->ws, ctx.res->ws_bytes, ctx.stream()));
     fq_agg_state st{};
     check_hip(hipMemcpyAsync(&st, out->ptr, sizeof st, hipMemcpyDeviceToHost, ctx.stream()), "hipMemcpyAsync");
     ctx.sync();
@@ -853,9 +853,76 @@ bool project_fused(const DataBlock &b, const std::vector<FunctionRef> &funcs, co
 }
 
 // ---------------------------------------------------------------------------
+// ScanGroup
+// ---------------------------------------------------------------------------
+ScanGroup::~ScanGroup() {
+    for (auto &s : queues_) {
+        rt_->give_event(s.start);
+        rt_->give_event(s.end);
+    }
+}
+
+void ScanGroup::before_launch(ExecCtx &ctx) {
+    std::lock_guard<std::mutex> lk(mu_);
+    for (const QueueSpan &s : queues_)
+        if (s.q == ctx.stream()) return;
+    QueueSpan s;
+    s.q = ctx.stream();
+    s.launch_mu = ctx.res->launch_mu;
+    if (rt_->profile.load() == 2) {  // the span opens right before this queue's first scan
+        s.start = rt_->take_event();
+        check_hip(hipEventRecord(s.start, s.q), "hipEventRecord");
+    }
+    queues_.push_back(s);
+}
+
+void ScanGroup::arrive(bool wait) {
+    std::unique_lock<std::mutex> lk(mu_);
+    if (--left_ > 0) {
+        if (wait) cv_.wait(lk, [&] { return closed_; });
+        return;
+    }
+    // the last pipe: every pipe has enqueued its scans, so queues_ no longer
+    // changes; the end events are recorded without mu_ held (before_launch
+    // takes mu_ under a queue's launch lock)
+    std::vector<QueueSpan> qs = queues_;
+    lk.unlock();
+    for (QueueSpan &s : qs) {
+        std::lock_guard<std::mutex> ql(*s.launch_mu);
+        s.end = rt_->take_event();
+        check_hip(hipEventRecord(s.end, s.q), "hipEventRecord");
+    }
+    lk.lock();
+    queues_ = qs;
+    closed_ = true;
+    cv_.notify_all();
+}
+
+void ScanGroup::wait_end() {
+    std::vector<hipEvent_t> ends;
+    {
+        std::lock_guard<std::mutex> lk(mu_);
+        for (const QueueSpan &s : queues_) ends.push_back(s.end);
+    }
+    for (hipEvent_t e : ends)
+        if (e) check_hip(hipEventSynchronize(e), "hipEventSynchronize");
+}
+
+void ScanGroup::account() {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (accounted_) return;
+    accounted_ = true;
+    for (const QueueSpan &s : queues_) {
+        float ms = 0;
+        if (s.start && s.end && hipEventElapsedTime(&ms, s.start, s.end) == hipSuccess)
+            rt_->stats.scan_ns += (uint64_t)((double)ms * 1e6);
+    }
+}
+
+// ---------------------------------------------------------------------------
 // AggFusion
 // ---------------------------------------------------------------------------
-AggFusion::AggFusion(ExecCtx &ctx) : ctx_(ctx) {}
+AggFusion::AggFusion(ExecCtx &ctx, ScanTicket *ticket) : ctx_(ctx), ticket_(ticket) {}
 
 AggFusion::~AggFusion() {
     // an exception left scans in flight: they write into this worker's pinned
@@ -952,17 +1019,22 @@ void AggFusion::add(AggregatorFunction *agg, const DataBlock &b) {
 }
 
 void AggFusion::end_block() {
-    const bool prof = ctx_.rt->profile.load();
+    const int prof = ctx_.rt->profile.load();
+    // an event pair per scan; 2: one span per query when the query's pipes
+    // form a ScanGroup (a Function-handle call has none: pairs)
+    const bool pairs = prof == 1 || (prof == 2 && !(ticket_ && ticket_->group()));
     for (Group &g : cur_) {
         fq_col c = g.col.abi();
         void *dst = nullptr;
         check_hip(hipHostGetDevicePointer(&dst, slot_host(g.slot), 0), "hipHostGetDevicePointer");
         hipEvent_t e0 = nullptr, e1 = nullptr;
-        if (prof) {
+        if (pairs) {
             e0 = ctx_.res->take_event();
             e1 = ctx_.res->take_event();
+        }
+        if (prof) {
             // compile a specialised scan (first use of this expression shape)
-            // outside the timed event pair
+            // outside the timed region
             fq_jit_stats js;
             if (fq_jit_get_stats(&js) == FQ_OK &&
                 (js.mode == FQ_JIT_ALWAYS || (js.mode == FQ_JIT_AUTO && c.len >= js.min_rows)))
@@ -970,19 +1042,22 @@ void AggFusion::end_block() {
                                         g.value.expr.n_steps ? &g.value.expr : nullptr, g.mask, nullptr));
         }
         {
-            // events and the scan's two kernels enqueue back to back even when
-            // other pipes share this queue, so the event pair brackets this scan
+            // events and the scan enqueue back to back even when other pipes
+            // share this queue, so an event pair brackets this scan; the scan
+            // folds its partials in its last workgroup (FQ_AGG_ONE_LAUNCH: the
+            // worker's workspace counter was zeroed when it was allocated)
             std::lock_guard<std::mutex> lk(*ctx_.res->launch_mu);
-            if (prof) check_hip(hipEventRecord(e0, ctx_.stream()), "hipEventRecord");
+            if (ticket_ && ticket_->group()) ticket_->group()->before_launch(ctx_);
+            if (pairs) check_hip(hipEventRecord(e0, ctx_.stream()), "hipEventRecord");
             check_fq(fq_aggregate(&c, g.block_rows, g.has_pred ? g.pred.get() : nullptr,
-                                  g.value.expr.n_steps ? &g.value.expr : nullptr, g.mask, (fq_agg_state *)dst,
-                                  ctx_.res->ws, ctx_.res->ws_bytes, ctx_.stream()));
-            if (prof) check_hip(hipEventRecord(e1, ctx_.stream()), "hipEventRecord");
+                                  g.value.expr.n_steps ? &g.value.expr : nullptr, g.mask | FQ_AGG_ONE_LAUNCH,
+                                  (fq_agg_state *)dst, ctx_.res->ws, ctx_.res->ws_bytes, ctx_.stream()));
+            if (pairs) check_hip(hipEventRecord(e1, ctx_.stream()), "hipEventRecord");
         }
         launched_ = true;
         if (const int64_t q0 = ctx_.rt->stats.query_t0.exchange(0))
             ctx_.rt->stats.first_launch_ns += (uint64_t)(now_ns() - q0);
-        if (prof) events_.push_back({e0, e1});
+        if (pairs) events_.push_back({e0, e1});
         ctx_.rt->stats.scan_launches++;
         ctx_.rt->stats.scan_rows += (uint64_t)g.col.len;
         ctx_.rt->stats.scan_bytes += (uint64_t)g.col.len * (uint64_t)dtype_size(g.col.dtype);
@@ -997,9 +1072,12 @@ void AggFusion::end_block() {
 
 void AggFusion::finish() {
     end_block();
-    // only this pipe's scans, not the whole queue: with profiling the last
-    // scan's closing timing event already marks that point (no extra marker)
-    if (launched_) {
+    if (ticket_ && ticket_->group()) {
+        // the query's pipes wait together on one event behind the last scan
+        ticket_->arrive(launched_);
+    } else if (launched_) {
+        // only this pipe's scans, not the whole queue: with profiling the last
+        // scan's closing timing event already marks that point (no extra marker)
         if (!events_.empty()) check_hip(hipEventSynchronize(events_.back().second), "hipEventSynchronize");
         else wait_launched();
     }

@@ -286,13 +286,84 @@ struct FactoryOptions {
 };
 FunctionRef function_factory(const std::string &name, std::vector<FunctionRef> args, const FactoryOptions &o);
 
+// The AggregatePartial pipes of ONE query (pipeline_builder.rs:50-66 builds one
+// per source pipe) when they share one device queue.  Their scans run back to
+// back there; a completion event behind each pipe's scans would sit between
+// two scans (~9 us of idle queue each, profiles/r02_gap_probe_event_flags.txt).
+// Instead every pipe arrives here once it has enqueued its scans (or failed);
+// the pipe that arrives last records ONE event behind all of them, and every
+// pipe that launched waits on it -- the partial states are needed together by
+// AggregateFinal anyway (transform_aggregate_final.rs:50-66).
+// FQ_OPT_PROFILE = 2 (span): one timing event before the query's first scan,
+// so scan_ns gets (first scan start .. last scan end) once per query -- the
+// scans and the launch gaps between them, nothing else on a resident column.
+class ScanGroup {
+   public:
+    ScanGroup(Runtime *rt, int pipes) : rt_(rt), left_(pipes) {}
+    ~ScanGroup();
+    ScanGroup(const ScanGroup &) = delete;
+    ScanGroup &operator=(const ScanGroup &) = delete;
+    // a launch on ctx's queue follows (called under the queue's launch lock)
+    void before_launch(ExecCtx &ctx);
+    // a pipe has enqueued everything it will.  The last one to arrive records
+    // an end event on every queue the group launched on; with `wait` the
+    // others block until it has (a failing pipe leaves without waiting).
+    void arrive(bool wait);
+    // every queue the group launched on, done (after arrive)
+    void wait_end();
+    // after wait_end: the spans' time into scan_ns (once per query)
+    void account();
+
+   private:
+    struct QueueSpan {
+        hipStream_t q = nullptr;
+        std::mutex *launch_mu = nullptr;
+        hipEvent_t start = nullptr, end = nullptr;
+    };
+    Runtime *rt_;
+    std::mutex mu_;
+    std::condition_variable cv_;
+    int left_;
+    bool closed_ = false, accounted_ = false;
+    std::vector<QueueSpan> queues_;  // stable once every pipe has arrived
+};
+using ScanGroupRef = std::shared_ptr<ScanGroup>;
+
+// One pipe's place in a ScanGroup: arrives exactly once -- from
+// AggFusion::finish, or (a pipe that fails) when it goes out of scope, so the
+// other pipes never wait for a pipe that is gone.
+class ScanTicket {
+   public:
+    explicit ScanTicket(ScanGroup *g) : g_(g) {}
+    ~ScanTicket() {
+        if (g_ && !done_) g_->arrive(false);
+    }
+    ScanTicket(const ScanTicket &) = delete;
+    ScanTicket &operator=(const ScanTicket &) = delete;
+    ScanGroup *group() const { return g_; }
+    // this pipe has enqueued all its scans; launched: wait for the query's end
+    void arrive(bool launched) {
+        if (!g_ || done_) return;
+        done_ = true;
+        g_->arrive(launched);
+        if (launched) {
+            g_->wait_end();
+            g_->account();
+        }
+    }
+
+   private:
+    ScanGroup *g_;
+    bool done_ = false;
+};
+
 // Deferred, fused accumulate for AggregatePartialTransform: aggregators that
 // share an argument expression (and the block's pending predicate) are served
 // by ONE fq_aggregate scan per block; results are replayed into each
 // aggregator in the reference's (block, function) order at finish().
 class AggFusion {
    public:
-    explicit AggFusion(ExecCtx &ctx);
+    explicit AggFusion(ExecCtx &ctx, ScanTicket *ticket = nullptr);
     ~AggFusion();
     void add(AggregatorFunction *agg, const DataBlock &b);
     void add_error(const FQException &e);  // a non-aggregator failure at this point
@@ -320,6 +391,7 @@ class AggFusion {
         FQException err{0, ""};
     };
     ExecCtx &ctx_;
+    ScanTicket *ticket_ = nullptr;  // the query's pipes wait together (ScanGroup)
     std::vector<Group> cur_;
     std::vector<Entry> log_;
     std::vector<Column> keepalive_;

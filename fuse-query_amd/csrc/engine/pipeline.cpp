@@ -392,12 +392,14 @@ StreamRef ProjectionTransform::execute() {
 }
 
 StreamRef AggregatePartialTransform::execute() {
+    // this pipe's place in the query's ScanGroup: arrives once, also when it fails
+    ScanTicket ticket(group_.get());
     std::vector<FunctionRef> funcs;
     for (auto &f : funcs_) funcs.push_back(f->clone());
     ExecCtx &ctx = ExecCtx::current();
     StreamRef in = input_->execute();
     {
-        AggFusion fusion(ctx);
+        AggFusion fusion(ctx, &ticket);
         FusionGuard guard(ctx, &fusion);
         DataBlock b;
         while (in->next(b)) {

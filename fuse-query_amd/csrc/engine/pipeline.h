@@ -228,8 +228,10 @@ class ProjectionTransform : public IProcessor {  // transform_projection.rs:16-7
 
 class AggregatePartialTransform : public IProcessor {  // transform_aggregate_partial.rs:18-79
    public:
-    AggregatePartialTransform(SchemaRef schema, std::vector<FunctionRef> funcs)
-        : schema_(std::move(schema)), funcs_(std::move(funcs)), input_(std::make_shared<EmptyProcessor>()) {}
+    // group: the query's AggregatePartial pipes (they wait for their scans together)
+    AggregatePartialTransform(SchemaRef schema, std::vector<FunctionRef> funcs, ScanGroupRef group = nullptr)
+        : schema_(std::move(schema)), funcs_(std::move(funcs)), input_(std::make_shared<EmptyProcessor>()),
+          group_(std::move(group)) {}
     std::string name() const override { return "AggregatePartialTransform"; }
     void connect_to(ProcessorRef input) override { input_ = std::move(input); }
     StreamRef execute() override;
@@ -238,6 +240,7 @@ class AggregatePartialTransform : public IProcessor {  // transform_aggregate_pa
     SchemaRef schema_;
     std::vector<FunctionRef> funcs_;
     ProcessorRef input_;
+    ScanGroupRef group_;
 };
 
 class AggregateFinalTransform : public IProcessor {  // transform_aggregate_final.rs:18-79

@@ -670,7 +670,10 @@ Pipeline build_pipeline(const QueryPlan &plan, const QueryContextRef &ctx, bool 
                     for (const auto &e : n.exprs) fs.push_back(e.to_function(ctx->factory));
                     return fs;
                 };
-                p.add_simple_transform([&]() { return std::make_shared<AggregatePartialTransform>(n.schema, funcs()); });
+                // the query's partial pipes wait for their scans together (ScanGroup)
+                auto group = std::make_shared<ScanGroup>(ctx->rt, (int)std::max<size_t>(1, p.pipe_num()));
+                p.add_simple_transform(
+                    [&, group]() { return std::make_shared<AggregatePartialTransform>(n.schema, funcs(), group); });
                 p.merge_processor();
                 p.add_simple_transform(
                     [&]() { return std::make_shared<AggregateFinalTransform>(n.schema, funcs(), emit_states); });

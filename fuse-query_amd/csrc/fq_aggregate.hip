@@ -127,9 +127,12 @@ __device__ __forceinline__ uint32_t process(const TIn (&x)[M], const int64_t (&i
     return pass;
 }
 
-// wave butterfly + LDS combine; thread 0 of the workgroup returns the result
+// wave butterfly + LDS combine; thread 0 of the workgroup stores the result
+// (write_through: six 8-byte agent-scope stores, sc1 -- the in-launch
+// finalize's form 1, which then needs no release fence)
 template <typename V>
-__device__ __forceinline__ void reduce_and_store(Acc<V> &acc, Partial *out, int32_t dtype) {
+__device__ __forceinline__ void reduce_and_store(Acc<V> &acc, Partial *out, int32_t dtype,
+                                                 bool write_through = false) {
 #pragma unroll
     for (int off = kWave / 2; off > 0; off >>= 1) {
         acc.sum = acc.sum + shfl_xor64(acc.sum, off);
@@ -170,8 +173,84 @@ __device__ __forceinline__ void reduce_and_store(Acc<V> &acc, Partial *out, int3
         p.blocks = 0;
         p.flags = flags;
         p.dtype = dtype;
-        *out = p;
+        if (write_through) {
+            uint64_t w[6];
+            __builtin_memcpy(w, &p, sizeof p);
+            uint64_t *o = reinterpret_cast<uint64_t *>(out);
+#pragma unroll
+            for (int i = 0; i < 6; ++i) __hip_atomic_store(o + i, w[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            *out = p;
+        }
     }
+}
+
+// The launch's partials folded in a fixed order by ONE workgroup: thread t
+// folds partials t, t+256, ... then the wave butterfly and the LDS combine --
+// the same order in the separate finalize launch and in the last workgroup
+// of a FQ_AGG_ONE_LAUNCH scan, so both give the same bytes (float sums too).
+// `parts` is read with vector loads (no const/__restrict__: in the in-launch
+// fold they are other workgroups' stores, behind an agent-scope acquire).
+template <typename V>
+__device__ __forceinline__ void fold_partials(Partial *parts, int nparts, uint64_t blocks, uint64_t rows,
+                                              int32_t vdtype, int empty_if_zero, fq_agg_state *out) {
+    Acc<V> acc;
+    acc.init();
+    if (threadIdx.x == 0) acc.cnt = rows;  // count-only scans: no column read (nparts == 0)
+    for (int i = threadIdx.x; i < nparts; i += kThreads) {
+        const Partial p = parts[i];
+        acc.sum = acc.sum + from_bits<V>(p.sum);
+        acc.mx = vmax(acc.mx, from_bits<V>(p.max));
+        acc.mn = vmin(acc.mn, from_bits<V>(p.min));
+        acc.cnt += p.count;
+        acc.flags |= p.flags;
+    }
+    __shared__ Partial s_out;
+    reduce_and_store<V>(acc, &s_out, vdtype);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        fq_agg_state r;
+        r.sum = s_out.sum;
+        r.max = s_out.max;
+        r.min = s_out.min;
+        r.count = s_out.count;
+        r.blocks = blocks;
+        r.flags = s_out.flags;
+        if (empty_if_zero && r.count == 0) r.flags |= FQ_STATE_ANY_EMPTY;
+        r.dtype = vdtype;
+        *out = r;
+    }
+}
+
+// In-launch finalize (Fin, fq_scan.h): called by every workgroup right after
+// reduce_and_store wrote its Partial (thread 0's store).  The hand-off is the
+// agent-scope release / ticket / acquire of the CDNA guide's split-K recipe:
+// thread 0 drains its store, releases at agent scope (the XCD L2 written
+// back), waits again (the fence's own wait can be dropped), then draws a
+// ticket; the workgroup that draws grid - 1 acquires at agent scope and folds
+// every partial.  Correct wherever the workgroups ran, whatever XCD.
+template <typename V>
+__device__ __forceinline__ void finish_in_launch(Partial *parts, int32_t vdtype, const Fin &fin) {
+    __shared__ uint32_t s_last;
+    if (threadIdx.x == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (fin.form == 0) {  // plain store: write the XCD L2 back (form 1 stored write-through)
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        const uint32_t t = __hip_atomic_fetch_add(fin.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t last = t == gridDim.x - 1u ? 1u : 0u;
+        if (last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        s_last = last;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    fold_partials<V>(parts, (int)gridDim.x, fin.blocks, 0ull, vdtype, fin.empty_if_zero, fin.out);
+    // every workgroup has drawn its ticket: the counter is free for the next launch
+    if (threadIdx.x == 0) __hip_atomic_store(fin.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -181,7 +260,7 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 template <typename TIn, typename V, int PRED, bool CHAIN, int U>
 __global__ void __launch_bounds__(kThreads)
     agg_flat_kernel(const TIn *__restrict__ col, int64_t n, int64_t head, KPred pred, KProg val,
-                    uint32_t mask, int32_t vdtype, Partial *__restrict__ parts) {
+                    uint32_t mask, int32_t vdtype, Partial *parts, Fin fin) {
     constexpr int VE = 16 / sizeof(TIn);
     constexpr int E = VE * U;
     static_assert(E <= 32, "pass mask is 32 bits");
@@ -233,7 +312,8 @@ __global__ void __launch_bounds__(kThreads)
         int64_t idx[1] = {i};
         process<TIn, V, PRED, CHAIN, 1>(x, idx, 1u, pred, val, mask, acc);
     }
-    reduce_and_store<V>(acc, parts + blockIdx.x, vdtype);
+    reduce_and_store<V>(acc, parts + blockIdx.x, vdtype, fin.done && fin.form == 1);
+    if (fin.done) finish_in_launch<V>(parts, vdtype, fin);
 }
 
 // Block mode: one wave owns whole reference blocks of R rows; one ballot per
@@ -241,7 +321,7 @@ __global__ void __launch_bounds__(kThreads)
 template <typename TIn, typename V, int PRED, bool CHAIN, int U>
 __global__ void __launch_bounds__(kThreads)
     agg_block_kernel(const TIn *__restrict__ col, int64_t n, int64_t R, KPred pred, KProg val,
-                     uint32_t mask, int32_t vdtype, Partial *__restrict__ parts) {
+                     uint32_t mask, int32_t vdtype, Partial *parts, Fin fin) {
     Acc<V> acc;
     acc.init();
     const int lane = threadIdx.x & (kWave - 1);
@@ -270,41 +350,17 @@ __global__ void __launch_bounds__(kThreads)
         }
         if (__ballot(any != 0) == 0ull) acc.flags |= FQ_STATE_ANY_EMPTY;
     }
-    reduce_and_store<V>(acc, parts + blockIdx.x, vdtype);
+    reduce_and_store<V>(acc, parts + blockIdx.x, vdtype, fin.done && fin.form == 1);
+    if (fin.done) finish_in_launch<V>(parts, vdtype, fin);
 }
 
-// Single workgroup, fixed order: thread t folds partials t, t+256, ... then a
-// butterfly; the result is deterministic for a given grid.
+// Single workgroup, fixed order (fold_partials): the result is deterministic
+// for a given grid.
 template <typename V>
 __global__ void __launch_bounds__(kThreads)
-    agg_finalize_kernel(const Partial *__restrict__ parts, int nparts, uint64_t blocks, uint64_t rows,
-                        int32_t vdtype, int empty_if_zero, fq_agg_state *__restrict__ out) {
-    Acc<V> acc;
-    acc.init();
-    if (threadIdx.x == 0) acc.cnt = rows;  // count-only scans: no column read (nparts == 0)
-    for (int i = threadIdx.x; i < nparts; i += kThreads) {
-        const Partial p = parts[i];
-        acc.sum = acc.sum + from_bits<V>(p.sum);
-        acc.mx = vmax(acc.mx, from_bits<V>(p.max));
-        acc.mn = vmin(acc.mn, from_bits<V>(p.min));
-        acc.cnt += p.count;
-        acc.flags |= p.flags;
-    }
-    __shared__ Partial s_out;
-    reduce_and_store<V>(acc, &s_out, vdtype);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        fq_agg_state r;
-        r.sum = s_out.sum;
-        r.max = s_out.max;
-        r.min = s_out.min;
-        r.count = s_out.count;
-        r.blocks = blocks;
-        r.flags = s_out.flags;
-        if (empty_if_zero && r.count == 0) r.flags |= FQ_STATE_ANY_EMPTY;
-        r.dtype = vdtype;
-        *out = r;
-    }
+    agg_finalize_kernel(Partial *parts, int nparts, uint64_t blocks, uint64_t rows, int32_t vdtype,
+                        int empty_if_zero, fq_agg_state *out) {
+    fold_partials<V>(parts, nparts, blocks, rows, vdtype, empty_if_zero, out);
 }
 
 // ---------------------------------------------------------------------------
@@ -577,11 +633,11 @@ static fq_status launch_scan(const Launch &L) {
     if (PRED != FQ_PRED_NONE && L.block_mode) {
         hipLaunchKernelGGL((agg_block_kernel<TIn, V, PRED, CHAIN, 8>), dim3(L.grid), dim3(kThreads), 0,
                            L.stream, (const TIn *)L.col, L.n, L.block_rows, L.pred, L.val, L.mask,
-                           L.vdtype, L.parts);
+                           L.vdtype, L.parts, L.fin);
     } else {
         hipLaunchKernelGGL((agg_flat_kernel<TIn, V, PRED, CHAIN, U>), dim3(L.grid), dim3(kThreads), 0,
                            L.stream, (const TIn *)L.col, L.n, L.head, L.pred, L.val, L.mask, L.vdtype,
-                           L.parts);
+                           L.parts, L.fin);
     }
     FQ_HIP_TRY(hipGetLastError());
     return FQ_OK;
@@ -666,7 +722,15 @@ extern "C" {
 
 size_t fq_aggregate_workspace_bytes(int64_t len) {
     (void)len;
-    return (size_t)fqk::kMaxPartials * sizeof(fqk::Partial);
+    return fqk::kPartialsBytes + fqk::kCounterBytes;
+}
+
+fq_status fq_aggregate_workspace_init(void *d_ws, size_t ws_bytes, void *stream) {
+    if (!d_ws) return fqc::fail(FQ_E_INVALID, "fq_aggregate_workspace_init: NULL workspace");
+    if (ws_bytes < fq_aggregate_workspace_bytes(0))
+        return fqc::fail(FQ_E_INVALID, "fq_aggregate_workspace_init: workspace too small");
+    FQ_HIP_TRY(hipMemsetAsync((char *)d_ws + fqk::kPartialsBytes, 0, fqk::kCounterBytes, (hipStream_t)stream));
+    return FQ_OK;
 }
 
 }  // extern "C"
@@ -746,7 +810,12 @@ fq_status fq_aggregate(const fq_col *col, int64_t block_rows, const fq_pred *pre
                        uint32_t agg_mask, fq_agg_state *d_out, void *d_ws, size_t ws_bytes, void *stream) {
     using namespace fqk;
     if (!col || !d_out || !d_ws) return fqc::fail(FQ_E_INVALID, "fq_aggregate: NULL argument");
-    if (ws_bytes < fq_aggregate_workspace_bytes(col->len))
+    // FQ_TUNE_SCAN_FIN = 2: the separate finalize launch even when asked for one (A/B)
+    const bool one_launch = (agg_mask & FQ_AGG_ONE_LAUNCH) != 0 && fqc::knob(FQ_TUNE_SCAN_FIN) != 2;
+    agg_mask &= ~FQ_AGG_ONE_LAUNCH;
+    // one_launch needs the counter behind the partials; without it a
+    // pre-counter workspace (kPartialsBytes) still serves the two launches
+    if (ws_bytes < (one_launch ? fq_aggregate_workspace_bytes(col->len) : kPartialsBytes))
         return fqc::fail(FQ_E_INVALID, "fq_aggregate: workspace too small");
     Launch L;
     bool chain = false;
@@ -760,6 +829,13 @@ fq_status fq_aggregate(const fq_col *col, int64_t block_rows, const fq_pred *pre
         L.grid = 0;  // count(column): rows, not values (see launch_finalize)
         return dispatch_finalize(L, blocks, empty_if_zero, d_out);
     }
+    if (one_launch) {
+        L.fin.done = (uint32_t *)((char *)d_ws + kPartialsBytes);
+        L.fin.out = d_out;
+        L.fin.blocks = blocks;
+        L.fin.empty_if_zero = empty_if_zero;
+        L.fin.form = (int32_t)fqc::knob(FQ_TUNE_SCAN_FIN);
+    }
     bool jitted = false;
     const bool tree = (chain && prog_has_tree(L.val)) || pred_has_tree(L.pred);
     s = jit_scan(col->dtype, chain, L, &jitted, tree);
@@ -772,6 +848,7 @@ fq_status fq_aggregate(const fq_col *col, int64_t block_rows, const fq_pred *pre
         s = dispatch(col->dtype, L, chain);
         if (s != FQ_OK) return s;
     }
+    if (one_launch) return FQ_OK;  // the scan's last workgroup wrote *d_out
     return dispatch_finalize(L, blocks, empty_if_zero, d_out);
 }
 
@@ -779,6 +856,7 @@ fq_status fq_jit_prepare(const fq_col *col, int64_t block_rows, const fq_pred *p
                          uint32_t agg_mask, int32_t *specialised) {
     using namespace fqk;
     if (specialised) *specialised = 0;
+    agg_mask &= ~FQ_AGG_ONE_LAUNCH;  // the same kernel serves both finalize forms
     Launch L;
     bool chain = false;
     uint64_t blocks = 0;

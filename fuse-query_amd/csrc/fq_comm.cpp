@@ -146,7 +146,9 @@ fq_status fq_engine_execute_exchange(fq_engine *e, const char *sql, int32_t rank
     // (data-dependent) send lengths first.  Planning is deterministic, so a
     // statement that fails to plan falls back to the same cap on every rank.
     size_t cap = 0;
-    if (fq_engine_partial_state_bytes(e, sql, &cap) != FQ_OK) cap = FQ_EXCHANGE_CAP_BYTES;
+    // 0 = data-dependent (GROUP BY rows): the default cap, so a small result
+    // still takes ONE round and only a large one a second
+    if (fq_engine_partial_state_bytes(e, sql, &cap) != FQ_OK || cap == 0) cap = FQ_EXCHANGE_CAP_BYTES;
     const void *rows = nullptr;
     size_t stride = 0;
     const int64_t t0 = now_ns();

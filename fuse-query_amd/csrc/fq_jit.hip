@@ -588,9 +588,47 @@ bool gen_source(const Launch &L, int32_t tin, bool chain, Gen &g, std::string &s
     else if (L.vdtype == FQ_DT_INT64) lo = "(-9223372036854775807ll - 1)", hi = "9223372036854775807ll";
     else lo = "-__builtin_huge_val()", hi = "__builtin_huge_val()";
 
+    // reduce_and_store (fq_aggregate.hip): wave butterfly, LDS across the 4
+    // waves; thread 0 returns the workgroup's Partial
+    src += R"(
+__device__ __forceinline__ Partial wg_reduce(Acc acc) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        acc.sum = acc.sum + shfl64(acc.sum, off);
+        acc.mx = vmax(acc.mx, shfl64(acc.mx, off));
+        acc.mn = vmin(acc.mn, shfl64(acc.mn, off));
+        acc.cnt += shfl64(acc.cnt, off);
+        acc.flags |= (u32)__shfl_xor((int)acc.flags, off, 64);
+    }
+    __shared__ V s_sum[4], s_mx[4], s_mn[4];
+    __shared__ u64 s_cnt[4];
+    __shared__ u32 s_flags[4];
+    const int wave = threadIdx.x / 64;
+    if ((threadIdx.x & 63) == 0) {
+        s_sum[wave] = acc.sum; s_mx[wave] = acc.mx; s_mn[wave] = acc.mn;
+        s_cnt[wave] = acc.cnt; s_flags[wave] = acc.flags;
+    }
+    __syncthreads();
+    Partial p;
+    if (threadIdx.x == 0) {
+        V sum = s_sum[0], mx = s_mx[0], mn = s_mn[0];
+        u64 cnt = s_cnt[0];
+        u32 flags = s_flags[0];
+#pragma unroll
+        for (int w = 1; w < 4; ++w) {
+            sum = sum + s_sum[w]; mx = vmax(mx, s_mx[w]); mn = vmin(mn, s_mn[w]);
+            cnt += s_cnt[w]; flags |= s_flags[w];
+        }
+        p.sum = __builtin_bit_cast(u64, sum); p.max = __builtin_bit_cast(u64, mx); p.min = __builtin_bit_cast(u64, mn);
+        p.count = cnt; p.blocks = 0; p.flags = flags; p.dtype = )" + std::to_string(L.vdtype) + R"(;
+    }
+    return p;
+}
+)";
     src += "extern \"C\" __global__ void __launch_bounds__(256)\n"
            "fq_jit_scan(const TIn *__restrict__ col, long long n, long long head, long long R,\n"
-           "            const u64 *__restrict__ bitmap, Consts c, Partial *__restrict__ parts) {\n"
+           "            const u64 *__restrict__ bitmap, Consts c, Partial *parts, u32 *done, Partial *out,\n"
+           "            u64 blocks, int empty_if_zero, int form) {\n"
            "    Acc acc;\n    acc.sum = V(0); acc.mx = " + lo + "; acc.mn = " + hi + "; acc.cnt = 0; acc.flags = 0;\n";
     if (!L.block_mode) {
         // flat tile-contiguous streaming (agg_flat_kernel, U = 4 16-byte vectors per lane)
@@ -700,41 +738,62 @@ bool gen_source(const Launch &L, int32_t tin, bool chain, Gen &g, std::string &s
     }
 )";
     }
-    // reduce_and_store (fq_aggregate.hip)
-    src += R"(
+    // this workgroup's partial; with `done` (FQ_AGG_ONE_LAUNCH) the in-launch
+    // finalize of fq_aggregate.hip (finish_in_launch + fold_partials, same
+    // hand-off, same fold order)
+    src += R"JIT(
+    {
+        const Partial p = wg_reduce(acc);
+        if (threadIdx.x == 0) {
+            if (done && form == 1) {  // write-through (sc1): no release fence below
+                u64 w[6];
+                __builtin_memcpy(w, &p, sizeof p);
+                u64 *o = (u64 *)(parts + blockIdx.x);
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        acc.sum = acc.sum + shfl64(acc.sum, off);
-        acc.mx = vmax(acc.mx, shfl64(acc.mx, off));
-        acc.mn = vmin(acc.mn, shfl64(acc.mn, off));
-        acc.cnt += shfl64(acc.cnt, off);
-        acc.flags |= (u32)__shfl_xor((int)acc.flags, off, 64);
+                for (int i = 0; i < 6; ++i) __hip_atomic_store(o + i, w[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                parts[blockIdx.x] = p;
+            }
+        }
     }
-    __shared__ V s_sum[4], s_mx[4], s_mn[4];
-    __shared__ u64 s_cnt[4];
-    __shared__ u32 s_flags[4];
-    const int wave = threadIdx.x / 64;
-    if ((threadIdx.x & 63) == 0) {
-        s_sum[wave] = acc.sum; s_mx[wave] = acc.mx; s_mn[wave] = acc.mn;
-        s_cnt[wave] = acc.cnt; s_flags[wave] = acc.flags;
+    if (!done) return;
+    __shared__ u32 s_last;
+    if (threadIdx.x == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (form == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        const u32 t = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const u32 last = t == gridDim.x - 1u ? 1u : 0u;
+        if (last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        s_last = last;
     }
     __syncthreads();
+    if (!s_last) return;
+    Acc f;
+    f.sum = V(0); f.mx = )JIT" + lo + "; f.mn = " + hi + R"JIT(; f.cnt = 0; f.flags = 0;
+    for (int i = threadIdx.x; i < (int)gridDim.x; i += 256) {
+        const Partial q = parts[i];
+        f.sum = f.sum + __builtin_bit_cast(V, q.sum);
+        f.mx = vmax(f.mx, __builtin_bit_cast(V, q.max));
+        f.mn = vmin(f.mn, __builtin_bit_cast(V, q.min));
+        f.cnt += q.count;
+        f.flags |= q.flags;
+    }
+    __syncthreads();  // wg_reduce's LDS is reused
+    Partial r = wg_reduce(f);
     if (threadIdx.x == 0) {
-        V sum = s_sum[0], mx = s_mx[0], mn = s_mn[0];
-        u64 cnt = s_cnt[0];
-        u32 flags = s_flags[0];
-#pragma unroll
-        for (int w = 1; w < 4; ++w) {
-            sum = sum + s_sum[w]; mx = vmax(mx, s_mx[w]); mn = vmin(mn, s_mn[w]);
-            cnt += s_cnt[w]; flags |= s_flags[w];
-        }
-        Partial p;
-        p.sum = __builtin_bit_cast(u64, sum); p.max = __builtin_bit_cast(u64, mx); p.min = __builtin_bit_cast(u64, mn);
-        p.count = cnt; p.blocks = 0; p.flags = flags; p.dtype = )" + std::to_string(L.vdtype) + R"(;
-        parts[blockIdx.x] = p;
+        r.blocks = blocks;
+        if (empty_if_zero && r.count == 0) r.flags |= )JIT" + std::to_string(FQ_STATE_ANY_EMPTY) + R"JIT(u;
+        *out = r;
+        __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
-)";
+)JIT";
     return true;
 }
 
@@ -3014,7 +3073,12 @@ fq_status jit_scan(int32_t col_dtype, bool chain, const Launch &L, bool *used, b
     long long n = L.n, head = L.head, R = L.block_rows;
     const uint64_t *bitmap = L.pred.bitmap;
     Partial *parts = L.parts;
-    void *args[] = {&col, &n, &head, &R, &bitmap, &hc, &parts};
+    uint32_t *done = L.fin.done;
+    void *out = L.fin.out;
+    unsigned long long blocks = L.fin.blocks;
+    int empty_if_zero = L.fin.empty_if_zero;
+    int form = L.fin.form;
+    void *args[] = {&col, &n, &head, &R, &bitmap, &hc, &parts, &done, &out, &blocks, &empty_if_zero, &form};
     FQ_HIP_TRY(hipModuleLaunchKernel(fn, (unsigned)L.grid, 1, 1, kThreads, 1, 1, 0, L.stream, args, nullptr));
     g_jit_launches += 1;
     *used = true;

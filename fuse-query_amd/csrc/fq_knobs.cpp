@@ -55,6 +55,8 @@ constexpr KnobDef kDefs[FQ_TUNE_COUNT] = {
     {4, 4, 8, 4, false},         // GBINS_ROWS
     {2, 1, 4, 1, false},         // GBINS_WG_PER_CU
     {1, 0, 1, 1, false},         // GBINS_FIT_LDS
+    {1000, 0, 100000, 1, false}, // POOL_SPIN_US
+    {0, 0, 2, 1, false},         // SCAN_FIN
 };
 
 std::atomic<int64_t> g_val[FQ_TUNE_COUNT] = {};

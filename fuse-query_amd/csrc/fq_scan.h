@@ -12,6 +12,26 @@ namespace fqk {
 
 constexpr int kThreads = 256;       // 4 waves per workgroup
 constexpr int kMaxPartials = 4096;  // workgroups per launch upper bound
+// the workspace: kMaxPartials Partials, then the completion counter of the
+// in-launch finalize on a line of its own
+constexpr size_t kPartialsBytes = (size_t)kMaxPartials * sizeof(Partial);
+constexpr size_t kCounterBytes = 256;
+
+// In-launch finalize (FQ_AGG_ONE_LAUNCH): every workgroup publishes its
+// Partial and draws a ticket from `done`; the one that draws grid - 1 folds
+// all partials in agg_finalize_kernel's order into *out and resets `done` to
+// zero.  done == nullptr: the separate finalize launch does the fold.
+// form (FQ_TUNE_SCAN_FIN): 0 = the partial stored plain, then an agent-scope
+// release (buffer_wbl2: the XCD L2's dirty lines written back) before the
+// ticket; 1 = the partial stored write-through (sc1 stores: nothing to write
+// back), drained, then the ticket.  The last workgroup acquires either way.
+struct Fin {
+    uint32_t *done;
+    fq_agg_state *out;
+    uint64_t blocks;
+    int32_t empty_if_zero;
+    int32_t form;
+};
 
 struct Launch {
     const void *col;
@@ -26,6 +46,7 @@ struct Launch {
     Partial *parts;
     int grid;
     hipStream_t stream;
+    Fin fin;
 };
 
 // Host lowering (fq_aggregate.hip): fq_expr -> KProg (res_dtype = result

@@ -15,7 +15,7 @@ LIB_PATH = os.path.normpath(os.path.join(_HERE, "..", "lib", "libfq_amd.so"))
 # Exported symbols promised by include/fq_gpu.h (checked by the CPU tests)
 GPU_SYMBOLS = [
     "fq_abi_version", "fq_last_error", "fq_device_count", "fq_fill_numbers_u64", "fq_fill_value",
-    "fq_fill_splitmix64", "fq_aggregate_workspace_bytes", "fq_aggregate",
+    "fq_fill_splitmix64", "fq_aggregate_workspace_bytes", "fq_aggregate_workspace_init", "fq_aggregate",
     "fq_arith_result_type", "fq_arith", "fq_compare", "fq_filter_workspace_bytes",
     "fq_filter_compact", "fq_state_merge", "fq_jit_config", "fq_jit_get_stats", "fq_jit_prepare",
     "fq_group_table_bytes", "fq_group_table_init", "fq_group_aggregate", "fq_group_table_count",
@@ -63,6 +63,7 @@ _protos = {
     "fq_fill_numbers_u64": (C.c_int32, [vp, C.c_uint64, C.c_uint64, vp]),
     "fq_fill_splitmix64": (C.c_int32, [vp, C.c_uint64, C.c_uint64, C.c_uint64, vp]),
     "fq_aggregate_workspace_bytes": (C.c_size_t, [C.c_int64]),
+    "fq_aggregate_workspace_init": (C.c_int32, [vp, C.c_size_t, vp]),
     "fq_aggregate": (C.c_int32, [P(abi.fq_col), C.c_int64, P(abi.fq_pred), P(abi.fq_expr),
                                  C.c_uint32, vp, vp, C.c_size_t, vp]),
     "fq_arith_result_type": (C.c_int32, [C.c_int32, C.c_int32, C.c_int32, P(C.c_int32)]),

@@ -6,7 +6,7 @@ both speak the same struct layout.
 """
 import ctypes as C
 
-FQ_ABI_VERSION = 2
+FQ_ABI_VERSION = 3
 
 # status (src/error.rs:10-22)
 FQ_OK = 0
@@ -39,6 +39,7 @@ CMP_BY_SYM = {"=": CMP_EQ, "<": CMP_LT, "<=": CMP_LTEQ, ">": CMP_GT, ">=": CMP_G
 CMP_FLIP = {CMP_EQ: CMP_EQ, CMP_LT: CMP_GT, CMP_LTEQ: CMP_GTEQ, CMP_GT: CMP_LT, CMP_GTEQ: CMP_LTEQ}
 
 AGG_MIN, AGG_MAX, AGG_SUM, AGG_COUNT = 1, 2, 4, 8
+AGG_ONE_LAUNCH = 0x100  # fq_gpu.h FQ_AGG_ONE_LAUNCH: in-launch finalize (zeroed workspace counter)
 AGG_BY_NAME = {"min": AGG_MIN, "max": AGG_MAX, "sum": AGG_SUM, "count": AGG_COUNT}
 
 OPERAND_CONST, OPERAND_COLUMN, OPERAND_STACK = 0, 1, 2
@@ -128,5 +129,6 @@ TUNE = {
     "JIT_ISOLATED": 20, "GROUP_ROWMAP": 21, "GROUP_WG_PER_CU": 22, "GROUP_RANGE_BINS": 23, "GROUP_NARROW": 24,
     "SELECT_BLOCKS_WG_PER_CU": 25, "SELECT_BLOCKS_RUN": 26, "SELECT_BLOCKS_DRAW": 27, "SELECT_BLOCKS_ROWS": 28,
     "SELECT_NT": 29, "GPART_DBUF": 30, "GPART_ROWS8": 31, "GPART_ROWS4": 32, "GBINS_ROWS": 33, "GBINS_WG_PER_CU": 34, "GBINS_FIT_LDS": 35,
+    "POOL_SPIN_US": 36, "SCAN_FIN": 37,
 }
 TUNE_SELECT_COUNTERS = 13

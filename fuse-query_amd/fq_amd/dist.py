@@ -95,6 +95,19 @@ class RcclComm:
         check(lib.fq_comm_init(device, self.world, self.rank, uid, C.byref(h)))
         self.h = h
 
+    @classmethod
+    def single(cls, device):
+        """A one-rank communicator without torch.distributed (the unique id
+        never leaves this process): the RCCL exchange path at world 1."""
+        self = cls.__new__(cls)
+        self.rank, self.world = 0, 1
+        uid = C.create_string_buffer(COMM_ID_BYTES)
+        check(lib.fq_comm_unique_id(uid))
+        h = C.c_void_p()
+        check(lib.fq_comm_init(device, 1, 0, uid, C.byref(h)))
+        self.h = h
+        return self
+
     def info(self):
         """(rank, world) as the communicator sees them (fq_comm_info)."""
         r, w = C.c_int32(-1), C.c_int32(-1)

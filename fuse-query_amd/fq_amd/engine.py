@@ -20,6 +20,7 @@ from .expr import from_bits
 P = C.POINTER
 
 OPT_WORKER_THREADS, OPT_MODULO, OPT_PROFILE, OPT_STREAMS, OPT_CHUNK_ROWS, OPT_GROUP_CHUNK_ROWS = 1, 2, 3, 4, 5, 6
+PROFILE_PAIRS, PROFILE_SPAN = 1, 2  # FQ_OPT_PROFILE values
 
 ENGINE_SYMBOLS = [
     "fq_engine_create", "fq_engine_destroy", "fq_engine_set_option", "fq_engine_materialize_numbers",
@@ -211,7 +212,8 @@ class BlockStream:
         h = C.c_void_p()
         check(lib.fq_engine_execute_blocks(engine.h, sql.encode(), rank, world, C.byref(h)))
         self.h = h
-        self.engine = engine  # the engine outlives its streams
+        self.engine = engine
+        engine._streams.add(self)  # Engine.close() closes the streams still open
 
     def next(self):
         """The next fq_device_block, or None at the end."""
@@ -246,19 +248,25 @@ class BlockStream:
 
 class Engine:
     def __init__(self, device=0, worker_threads=8, modulo=True, profile=False, streams=1):
+        import weakref
+        self._streams = weakref.WeakSet()  # open BlockStreams
         h = C.c_void_p()
         check(lib.fq_engine_create(device, C.byref(h)))
         self.h = h
         self.set_option(OPT_WORKER_THREADS, worker_threads)
         self.set_option(OPT_MODULO, 1 if modulo else 0)
-        self.set_option(OPT_PROFILE, 1 if profile else 0)
+        # profile: False / True (= 1, an event pair per scan launch) / PROFILE_SPAN
+        # (= 2, one span from a query's first scan to its last, fq_engine.h)
+        self.set_option(OPT_PROFILE, int(profile))
         self.set_option(OPT_STREAMS, streams)
 
     def set_option(self, opt, value):
         check(lib.fq_engine_set_option(self.h, opt, int(value)))
 
     def close(self):
-        if self.h:
+        if getattr(self, "h", None):
+            for st in list(getattr(self, "_streams", ())):  # before the engine they run on
+                st.close()
             lib.fq_engine_destroy(self.h)
             self.h = None
 

@@ -36,7 +36,8 @@ class fq_scalar(C.Structure):
 
 
 class fq_block(C.Structure):
-    _fields_ = [("n_columns", C.c_int32), ("names", P(C.c_char_p)), ("columns", P(abi.fq_col))]
+    _fields_ = [("n_columns", C.c_int32), ("names", P(C.c_char_p)), ("columns", P(abi.fq_col)),
+                ("block_rows", C.c_int64), ("filter", OPT)]
 
 
 FUNCTION_SYMBOLS = [
@@ -44,6 +45,7 @@ FUNCTION_SYMBOLS = [
     "fq_function_display", "fq_function_set_depth", "fq_function_return_type", "fq_function_nullable",
     "fq_function_eval", "fq_function_accumulate", "fq_function_accumulate_result", "fq_function_merge_state",
     "fq_function_merge_result", "fq_data_value_arithmetic_op", "fq_data_value_aggregate_op",
+    "fq_functions_accumulate",
 ]
 
 _protos = {
@@ -59,6 +61,7 @@ _protos = {
     "fq_function_eval": (C.c_int32, [OPT, OPT, P(fq_block), C.c_void_p, C.c_size_t, P(C.c_size_t),
                                      P(C.c_int32), P(C.c_int64), P(C.c_int32), P(fq_scalar)]),
     "fq_function_accumulate": (C.c_int32, [OPT, OPT, P(fq_block)]),
+    "fq_functions_accumulate": (C.c_int32, [OPT, P(OPT), C.c_int32, P(fq_block)]),
     "fq_function_accumulate_result": (C.c_int32, [OPT, P(fq_scalar), C.c_size_t, P(C.c_size_t)]),
     "fq_function_merge_state": (C.c_int32, [OPT, P(fq_scalar), C.c_size_t]),
     "fq_function_merge_result": (C.c_int32, [OPT, P(fq_scalar)]),
@@ -147,12 +150,19 @@ def data_value_aggregate_op(op, left, right):
 
 class DataBlock:
     """data_block.rs:10-62 over device columns: names -> ops.DeviceColumn.
-    The columns stay owned by the caller (borrowed for each call)."""
+    The columns stay owned by the caller (borrowed for each call).
 
-    def __init__(self, names, columns):
+    block_rows > 0: the columns hold the reference's blocks of that many rows
+    (a numbers_mt partition of 10,000-row blocks) and accumulate replays the
+    per-block state machine; filter: a pending FilterTransform (a Boolean
+    Function) -- the block holds the rows where it is true, block by block."""
+
+    def __init__(self, names, columns, block_rows=0, filter=None):
         assert len(names) == len(columns)
         self.names = list(names)
         self.columns = list(columns)
+        self.block_rows = int(block_rows)
+        self.filter = filter
 
     def num_rows(self):
         return self.columns[0].len if self.columns else 0
@@ -162,8 +172,8 @@ class DataBlock:
         names = (C.c_char_p * max(n, 1))(*[s.encode() for s in self.names])
         cols = (abi.fq_col * max(n, 1))(*[c.col() if c.buf is not None else abi.fq_col(None, c.len, c.dtype, 0)
                                           for c in self.columns])
-        b = fq_block(n, names, cols)
-        b._keep = (names, cols)
+        b = fq_block(n, names, cols, self.block_rows, self.filter.h if self.filter is not None else None)
+        b._keep = (names, cols, self.filter)
         return b
 
 
@@ -236,6 +246,15 @@ class Function:
     def accumulate(self, engine, block):
         _sync_torch()
         check(lib.fq_function_accumulate(engine.h, self.h, C.byref(block._abi())))
+
+    @staticmethod
+    def accumulate_all(engine, funcs, block):
+        """transform_aggregate_partial.rs:53-58 for one block -- every function's
+        accumulate -- through fq_functions_accumulate: the aggregators sharing an
+        argument (and the block's filter) read the column once."""
+        _sync_torch()
+        arr = (OPT * max(1, len(funcs)))(*[f.h for f in funcs])
+        check(lib.fq_functions_accumulate(engine.h, arr, len(funcs), C.byref(block._abi())))
 
     def accumulate_result(self):
         n = C.c_size_t(0)

@@ -39,7 +39,13 @@ typedef struct fq_result fq_result;
 #define FQ_OPT_WORKER_THREADS 1 /* FuseQueryContext::worker_threads (context.rs:11); default 8 */
 #define FQ_OPT_MODULO 2         /* 1 (default): '%' extension on; 0: reference behaviour
                                    ("Unsupported Function: %", function_factory.rs:34-37) */
-#define FQ_OPT_PROFILE 3        /* 1: time every fused scan launch with HIP events */
+#define FQ_OPT_PROFILE 3        /* 1: time every fused scan launch with a HIP event pair;
+                                   2: one span per query -- a timing event right before
+                                   its first scan and the query's end event behind its
+                                   last (scan_ms then includes the launch gaps between
+                                   the scans, and on a generated partition its fills):
+                                   no event between two scans.  Row-pipeline and GROUP
+                                   BY launches are timed per launch with 1 or 2 */
 #define FQ_OPT_STREAMS 4        /* device queues the pipes share (default 1: the scans are
                                    HBM-bound, concurrency buys nothing and blurs timing) */
 #define FQ_OPT_CHUNK_ROWS 5     /* rows per device block of a numbers_mt partition that is NOT
@@ -55,7 +61,8 @@ typedef struct fq_engine_stats {
     uint64_t scan_launches; /* fused aggregate scans launched                    */
     uint64_t scan_rows;     /* rows those scans read                            */
     uint64_t scan_bytes;    /* algorithmic bytes those scans read               */
-    double scan_ms;         /* summed event time of those launches (FQ_OPT_PROFILE) */
+    double scan_ms;         /* summed event time of those launches (FQ_OPT_PROFILE 1),
+                               or of the queries' scan spans (FQ_OPT_PROFILE 2) */
     uint64_t queries;
     double plan_ms;         /* host: SQL parse + plan + PipelineBuilder, summed   */
     double exec_ms;         /* host: pipeline execution until the result block    */
@@ -150,7 +157,8 @@ fq_status fq_engine_execute_final(fq_engine *e, const char *sql, const void *sta
 typedef struct fq_block_stream fq_block_stream;
 typedef struct fq_device_block {
     int32_t n_columns;
-    int32_t pipe;              /* partition pipe (partition order) it came from, -1 unknown */
+    int32_t pipe;              /* partition pipe (partition order) it came from; a stream
+                                  with a single pipe reports 0; -1 only at the end */
     const char *const *names;  /* the plan's output schema                 */
     const fq_col *columns;     /* device columns (len = rows spanned)       */
     int64_t rows;              /* valid rows                                */
@@ -164,6 +172,11 @@ fq_status fq_engine_execute_blocks(fq_engine *e, const char *sql, int32_t rank, 
                                    fq_block_stream **out);
 /* *has_block = 0 at the end of the stream (and *out is zeroed) */
 fq_status fq_block_stream_next(fq_block_stream *s, fq_device_block *out, int32_t *has_block);
+/* Lifetime: a stream's pipes run on its engine's threads and device queues.
+ * fq_engine_destroy closes every stream still open (the pipes are stopped and
+ * joined, their blocks freed); such a stream's next call fails with
+ * FQ_E_INVALID and fq_block_stream_free still releases it.  Calls on one stream
+ * or engine must not run concurrently with fq_engine_destroy.               */
 void fq_block_stream_free(fq_block_stream *s);
 
 fq_status fq_engine_get_stats(fq_engine *e, fq_engine_stats *out);
@@ -219,6 +232,20 @@ typedef struct fq_block {
     int32_t n_columns;
     const char *const *names; /* DataSchema field names                       */
     const fq_col *columns;    /* device columns of equal len                  */
+    /* The reference's block geometry: > 0 -- the columns hold ceil(len /
+     * block_rows) of its blocks, block_rows rows each but the last
+     * (NumbersStream's 10,000, numbers_stream.rs:29), and accumulate replays
+     * the per-block state machine of function_aggregator.rs:57-100 over them
+     * (a Sum that meets an empty block after >= 2 blocks fails as the
+     * reference does); 0 -- the columns are ONE block.  One call can then
+     * stand for a whole partition instead of 125,000 calls.                 */
+    int64_t block_rows;
+    /* A pending FilterTransform (transform_filter.rs:38-55) or NULL: a Boolean
+     * Function handle (a comparison, or an and/or tree of them) over these
+     * columns; the block holds only the rows where it is true, each reference
+     * block filtered on its own (ExpressionStream, stream_expression.rs:38-50).
+     * accumulate fuses it into the scan; eval evaluates the kept rows.       */
+    const fq_function *filter;
 } fq_block;
 
 /* A DataValue of any type (data_value.rs:20-38), Utf8 included.
@@ -261,6 +288,16 @@ fq_status fq_function_eval(fq_engine *e, fq_function *f, const fq_block *b, void
                            size_t *out_bytes, int32_t *out_dtype, int64_t *out_len, int32_t *is_array,
                            fq_scalar *scalar);
 fq_status fq_function_accumulate(fq_engine *e, fq_function *f, const fq_block *b);
+/* AggregatePartialTransform's loop body for one block
+ * (transform_aggregate_partial.rs:53-58: `for func in funcs { func.accumulate(&block) }`)
+ * over n handles at once: the aggregator leaves of all n functions that share
+ * an argument expression (and the block's filter) are served by ONE fused scan
+ * of the column -- C3's sum/count, max and min by one read instead of four --
+ * and the states are replayed in the reference's (block, function) order, so
+ * every handle ends in the state n fq_function_accumulate calls leave.  The
+ * first failing function's error is returned (the reference's `?`); the
+ * functions before it have accumulated.  Complete when the call returns.   */
+fq_status fq_functions_accumulate(fq_engine *e, fq_function *const *fs, int32_t n, const fq_block *b);
 /* states: the function's partial state vector (aggregates in depth order);
  * *n = its length (FQ_E_INVALID when cap is short, *n = the size needed)   */
 fq_status fq_function_accumulate_result(const fq_function *f, fq_scalar *states, size_t cap, size_t *n);

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define FQ_ABI_VERSION 2
+#define FQ_ABI_VERSION 3
 
 /* ---- status (src/error.rs:10-22 FuseQueryError{SQLParse,Plan,Internal}) ---- */
 typedef int32_t fq_status;
@@ -232,8 +232,20 @@ fq_status fq_fill_value(void *d_out, int64_t n, int32_t dtype, uint64_t bits, vo
  * block_rows: reference block size of this device block (10000 for
  * numbers_mt, or col->len for a single DataBlock).  Workspace is device
  * memory of at least fq_aggregate_workspace_bytes(col->len) bytes.
- * value may be NULL (identity).  pred may be NULL (no WHERE).                */
+ * value may be NULL (identity).  pred may be NULL (no WHERE).
+ *
+ * The scan writes one partial per workgroup into the workspace; a second,
+ * one-workgroup launch folds them into *d_out.  With FQ_AGG_ONE_LAUNCH in
+ * agg_mask the scan's last workgroup folds them instead (same order, the
+ * same bytes), so a query's scans run back to back with no launch between
+ * them.  The caller then vouches that the workspace's completion counter is
+ * zero: fq_aggregate_workspace_init ran on the workspace (stream-ordered before
+ * the first such call) and only fq_aggregate calls used it since -- each call
+ * leaves the counter zero.  Calls sharing a workspace must be ordered (one
+ * stream), as for the partials.                                             */
+#define FQ_AGG_ONE_LAUNCH 0x100u
 size_t fq_aggregate_workspace_bytes(int64_t len);
+fq_status fq_aggregate_workspace_init(void *d_ws, size_t ws_bytes, void *stream);
 fq_status fq_aggregate(const fq_col *col, int64_t block_rows, const fq_pred *pred,
                        const fq_expr *value, uint32_t agg_mask, fq_agg_state *d_out,
                        void *d_ws, size_t ws_bytes, void *stream);
@@ -424,7 +436,10 @@ fq_status fq_jit_prepare(const fq_col *col, int64_t block_rows, const fq_pred *p
 #define FQ_TUNE_GBINS_ROWS 33       /* GROUP BY bins pass, 4-byte rows: rows per thread per tile, 4 (4/8)     */
 #define FQ_TUNE_GBINS_WG_PER_CU 34  /* GROUP BY bins pass, fitted table + 4 rows: workgroups per CU, 2 (1..4) */
 #define FQ_TUNE_GBINS_FIT_LDS 35    /* GROUP BY bins pass, range bins: LDS table of one bin's keys, 1 (0/1)  */
-#define FQ_TUNE_COUNT 36
+#define FQ_TUNE_POOL_SPIN_US 36     /* engine pipe threads poll for the next task before sleeping, 1000 us (0..100000) */
+#define FQ_TUNE_SCAN_FIN 37         /* FQ_AGG_ONE_LAUNCH partial hand-off: 0 plain store + agent release, 1 write-through
+                                       stores, 2 ignore the flag (separate finalize launch; A/B): 0 (0..2) */
+#define FQ_TUNE_COUNT 38
 /* FQ_E_INVALID for an unknown knob or a value outside the knob's set */
 fq_status fq_tune_set(int32_t knob, int64_t value);
 /* the knob's current value; -1 for an unknown knob */

@@ -16,10 +16,11 @@
  *
  * `fq_c_client --bench STEPS TOTAL [WARMUP]`: the timed drop-in stack (C, the
  * /opt/rocm runtime, no torch): materialise numbers_mt(TOTAL) in HBM, then
- * STEPS x the C3 statement through fq_engine_execute with the engine's
- * per-scan HIP events on (FQ_OPT_PROFILE), every result checked against the
+ * STEPS x the C3 statement through fq_engine_execute with the engine's scan
+ * timing on (FQ_OPT_PROFILE 2: one HIP-event span per query, first scan start
+ * to last scan end -- bench.py's setting), every result checked against the
  * closed form; prints one JSON line (rows/s, ms per step, the scan kernel's
- * average event time and its fraction of the 8 TB/s HBM peak).           */
+ * average time per launch and its fraction of the 8 TB/s HBM peak).      */
 #define _POSIX_C_SOURCE 199309L /* clock_gettime under -std=c11 */
 #include <stdint.h>
 #include <stdio.h>
@@ -127,7 +128,7 @@ static void c3_row(fq_engine *e, const char *sql, uint64_t out[3]) {
 static int bench(int steps, uint64_t total, int warmup) {
     fq_engine *e = NULL;
     CHECK(fq_engine_create(0, &e) == FQ_OK, "engine: %s", fq_last_error());
-    CHECK(fq_engine_set_option(e, FQ_OPT_PROFILE, 1) == FQ_OK, "profile: %s", fq_last_error());
+    CHECK(fq_engine_set_option(e, FQ_OPT_PROFILE, 2) == FQ_OK, "profile: %s", fq_last_error());
     CHECK(fq_engine_materialize_numbers(e, total, 0, 1) == FQ_OK, "materialise: %s", fq_last_error());
     char sql[256];
     snprintf(sql, sizeof sql,
@@ -159,16 +160,120 @@ static int bench(int steps, uint64_t total, int warmup) {
            "of the C3 statement\", \"workload\": \"%s\", \"steps\": %d, \"warmup\": %d, \"value\": %.6g, "
            "\"unit\": \"rows/s\", \"ms_per_step\": %.6g, \"scan_launches_per_step\": %.6g, "
            "\"kernel_ms_per_launch\": %.6g, \"bytes_per_launch\": %.6g, \"achieved_hbm_gbps\": %.6g, "
-           "\"frac\": %.6g, \"host_ms_per_step\": {\"plan\": %.6g, \"first_launch\": %.6g, \"exec\": %.6g}, "
-           "\"result\": [%llu, %llu, %llu]}\n",
+           "\"frac\": %.6g, \"step_over_scans\": %.6g, \"host_ms_per_step\": {\"plan\": %.6g, "
+           "\"first_launch\": %.6g, \"exec\": %.6g}, \"result\": [%llu, %llu, %llu]}\n",
            sql, steps, warmup, (double)total * steps / dt, dt / steps * 1e3, (double)st.scan_launches / steps, kms,
-           bytes, gbps, gbps / 8000.0, st.plan_ms / steps, st.first_launch_ms / steps, st.exec_ms / steps,
+           bytes, gbps, gbps / 8000.0, (dt * 1e3) / (st.scan_ms > 0 ? st.scan_ms : 1.0), st.plan_ms / steps,
+           st.first_launch_ms / steps, st.exec_ms / steps,
            (unsigned long long)got[0], (unsigned long long)got[1], (unsigned long long)got[2]);
     fq_engine_destroy(e);
     return 0;
 }
 
+/* ---- the Function-handle boundary, timed (`--handles STEPS TOTAL [WARMUP]`) ----
+ * What a Rust host that keeps the reference's own transforms does with the C3
+ * statement: its AggregatePartialTransform per partition pipe
+ * (transform_aggregate_partial.rs:50-78) over the 3 Functions of the plan --
+ * Sum/Count under an Arithmetic '/', Max, Min: 4 aggregator leaves -- with its
+ * own Arrow-layout column per partition in HBM, then AggregateFinal's
+ * merge_state / merge_result (transform_aggregate_final.rs:50-78).  One
+ * fq_functions_accumulate call per partition: the block spans the partition's
+ * 10,000-row reference blocks (block_rows) and the 4 leaves share one scan. */
+static fq_function *fn_create(const char *name, fq_function *a, fq_function *b) {
+    fq_function *args[2] = {a, b}, *out = NULL;
+    CHECK(fq_function_create(name, args, b ? 2 : 1, &out) == FQ_OK, "create %s: %s", name, fq_last_error());
+    return out;
+}
+
+static int handles(int steps, uint64_t total, int warmup) {
+    CHECK(total % 80000 == 0, "--handles needs numbers_mt(N) with whole 10,000-row blocks per partition");
+    fq_engine *e = NULL;
+    CHECK(fq_engine_create(0, &e) == FQ_OK, "engine: %s", fq_last_error());
+    CHECK(fq_engine_set_option(e, FQ_OPT_PROFILE, 1) == FQ_OK, "profile: %s", fq_last_error());
+    /* the host's own partitions: numbers_mt's 8 ranges (numbers_table.rs:29-55) */
+    enum { P = 8 };
+    const uint64_t chunk = total / P;
+    uint64_t *cols[P];
+    fq_col fc[P];
+    const char *names[1] = {"number"};
+    for (int p = 0; p < P; ++p) {
+        CHECK(hipMalloc((void **)&cols[p], chunk * 8) == hipSuccess, "hipMalloc partition %d", p);
+        CHECK(fq_fill_numbers_u64(cols[p], (uint64_t)p * chunk, chunk, NULL) == FQ_OK, "fill: %s", fq_last_error());
+        fc[p] = (fq_col){cols[p], (int64_t)chunk, FQ_DT_UINT64, 0};
+    }
+    CHECK(hipDeviceSynchronize() == hipSuccess, "sync");
+    /* the plan's functions (plan_expression.rs:40-75): sum(number)/count(number), max(number), min(number) */
+    fq_function *num = NULL;
+    CHECK(fq_function_field("number", &num) == FQ_OK, "field");
+    fq_function *tmpl[3];
+    tmpl[0] = fn_create("/", fn_create("sum", num, NULL), fn_create("count", num, NULL));
+    tmpl[1] = fn_create("max", num, NULL);
+    tmpl[2] = fn_create("min", num, NULL);
+    for (int i = 0; i < 3; ++i) CHECK(fq_function_set_depth(tmpl[i], 0) == FQ_OK, "depth");
+    const uint64_t sum = (uint64_t)((unsigned __int128)total * (total - 1) / 2);
+    const uint64_t expect[3] = {sum / total, total - 1, 0};
+    uint64_t got[3] = {0, 0, 0};
+    int bad = 0;
+    double t0 = 0;
+    for (int it = 0; it < (warmup > 0 ? warmup : 1) + steps; ++it) {
+        if (it == (warmup > 0 ? warmup : 1)) {
+            CHECK(fq_engine_reset_stats(e) == FQ_OK, "reset stats");
+            t0 = now_s();
+        }
+        fq_function *fin[3];
+        for (int i = 0; i < 3; ++i) CHECK(fq_function_clone(tmpl[i], &fin[i]) == FQ_OK, "clone");
+        for (int p = 0; p < P; ++p) {
+            fq_function *part[3];
+            for (int i = 0; i < 3; ++i) CHECK(fq_function_clone(tmpl[i], &part[i]) == FQ_OK, "clone");
+            const fq_block blk = {1, names, &fc[p], 10000, NULL};
+            CHECK(fq_functions_accumulate(e, part, 3, &blk) == FQ_OK, "accumulate: %s", fq_last_error());
+            for (int i = 0; i < 3; ++i) {  /* the partial's state row -> AggregateFinal */
+                fq_scalar st[4];
+                size_t n = 0;
+                CHECK(fq_function_accumulate_result(part[i], st, 4, &n) == FQ_OK, "accumulate_result");
+                CHECK(fq_function_merge_state(fin[i], st, n) == FQ_OK, "merge_state: %s", fq_last_error());
+                fq_function_free(part[i]);
+            }
+        }
+        for (int i = 0; i < 3; ++i) {
+            fq_scalar v;
+            CHECK(fq_function_merge_result(fin[i], &v) == FQ_OK && v.kind == FQ_SCALAR_SOME, "merge_result");
+            got[i] = v.bits;
+            fq_function_free(fin[i]);
+        }
+        bad |= memcmp(got, expect, sizeof got) != 0;
+    }
+    const double dt = now_s() - t0;
+    CHECK(!bad, "C3 through handles = %llu %llu %llu", (unsigned long long)got[0], (unsigned long long)got[1],
+          (unsigned long long)got[2]);
+    fq_engine_stats st;
+    CHECK(fq_engine_get_stats(e, &st) == FQ_OK, "stats");
+    const double launches = st.scan_launches ? (double)st.scan_launches : 1.0;
+    const double kms = st.scan_ms / launches, bytes = (double)st.scan_bytes / launches;
+    const double gbps = bytes / (kms * 1e-3) / 1e9;
+    printf("{\"path\": \"fq_c_client --handles: 8 partitions x fq_functions_accumulate over the plan's 3 Function "
+           "handles (4 aggregator leaves, one fused scan), block_rows 10000, then merge_state / merge_result\", "
+           "\"total\": %llu, \"steps\": %d, \"value\": %.6g, \"unit\": \"rows/s\", \"ms_per_step\": %.6g, "
+           "\"scan_launches_per_step\": %.6g, \"kernel_ms_per_launch\": %.6g, \"bytes_per_launch\": %.6g, "
+           "\"achieved_hbm_gbps\": %.6g, \"frac\": %.6g, \"result\": [%llu, %llu, %llu]}\n",
+           (unsigned long long)total, steps, (double)total * steps / dt, dt / steps * 1e3,
+           (double)st.scan_launches / steps, kms, bytes, gbps, gbps / 8000.0, (unsigned long long)got[0],
+           (unsigned long long)got[1], (unsigned long long)got[2]);
+    for (int i = 0; i < 3; ++i) fq_function_free(tmpl[i]);
+    fq_function_free(num);
+    for (int p = 0; p < P; ++p) (void)hipFree(cols[p]);
+    fq_engine_destroy(e);
+    return 0;
+}
+
 int main(int argc, char **argv) {
+    if (argc > 1 && strcmp(argv[1], "--handles") == 0) {
+        const int steps = argc > 2 ? atoi(argv[2]) : 10;
+        const uint64_t total = argc > 3 ? strtoull(argv[3], NULL, 10) : 10000000000ull;
+        const int warmup = argc > 4 ? atoi(argv[4]) : 2;
+        CHECK(steps > 0, "usage: fq_c_client --handles STEPS TOTAL [WARMUP]");
+        return handles(steps, total, warmup);
+    }
     if (argc > 1 && strcmp(argv[1], "--bench") == 0) {
         const int steps = argc > 2 ? atoi(argv[2]) : 20;
         const uint64_t total = argc > 3 ? strtoull(argv[3], NULL, 10) : 10000000000ull;

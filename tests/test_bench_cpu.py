@@ -110,6 +110,27 @@ def test_gpus_and_launcher_world_mismatch_exits_nonzero():
 
 
 def test_gpus_n_with_rccl_needs_n_visible_gpus():
-    # no GPU here: asking for 2 RCCL ranks fails before anything starts
-    p = _run_bench(["--gpus", "2"], timeout=120)
-    assert p.returncode != 0 and "needs 2 GPUs, 0 visible" in p.stderr
+    # no GPU here: the parent starts the ranks without touching HIP, and every
+    # rank checks its own device and exits non-zero
+    p = _run_bench(["--gpus", "2", "--no-cpu-baseline"], timeout=240)
+    assert p.returncode != 0
+    assert "launching 2 ranks" in p.stderr
+    assert "no GPU" in p.stderr or "needs a GPU per rank" in p.stderr, p.stderr[-3000:]
+
+
+def test_launcher_parent_loads_no_hip_module():
+    # `bench.py --gpus N` without a launcher only spawns processes: neither
+    # torch nor the HIP library is imported in the parent before it does
+    p = _run_bench(["--gpus", "2", "--dry-run"], timeout=240)
+    assert p.returncode == 0, p.stderr[-3000:]
+    assert "launcher parent: HIP-touching modules loaded before spawning: none" in p.stderr
+
+
+def test_bench_module_imports_without_the_hip_runtime():
+    # importing bench.py (what the tests above do) loads no HIP-touching module
+    code = ("import importlib.util, sys; spec = importlib.util.spec_from_file_location('b', %r); "
+            "m = importlib.util.module_from_spec(spec); spec.loader.exec_module(m); "
+            "print(sorted(x for x in m.HIP_MODULES if x in sys.modules))" % os.path.join(ROOT, "bench.py"))
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, cwd=ROOT)
+    assert p.returncode == 0, p.stderr
+    assert p.stdout.strip() == "[]"

@@ -55,13 +55,15 @@ def worker(rank, world, port, n, out_q, sqls=None):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         with Engine(device=0) as eng:
-            out = []
+            out, rounds = [], []
             for sql in (sqls or SQLS):
+                r0 = eng.stats()["exchange_rounds"]
                 try:
                     out.append(fqd.execute(eng, sql % n).rows)
                 except FQError as e:  # every rank must get the error, none may hang
                     out.append(("error", e.status, str(e)))
-        out_q.put((rank, out))
+                rounds.append(eng.stats()["exchange_rounds"] - r0)
+        out_q.put((rank, out, rounds))
     finally:
         dist.destroy_process_group()
 
@@ -81,7 +83,7 @@ def test_an_error_on_one_rank_reaches_every_rank():
         p.join(timeout=60)
         assert p.exitcode == 0
     from fq_amd import abi
-    for rank, out in results:
+    for rank, out, _ in results:
         for got in out:
             assert got == ("error", abi.FQ_E_DIVIDE_BY_ZERO, "Internal Error: Divide by zero error"), (rank, got)
 
@@ -109,10 +111,13 @@ def test_two_ranks_on_the_gpu_match_the_oracle():
     expg = R.group_by_query(n, R.E_bin("%", num, c(10)),
                             [R.E_fn("count", num), R.E_bin("/", R.E_fn("sum", num), R.E_fn("count", num)),
                              R.E_fn("max", R.E_bin("+", num, c(1)))], where=where)
-    for rank, out in results:
+    for rank, out, rounds in results:
         assert out[0] == exp3, rank
         assert out[1] == exp4, rank
         assert out[2] == expg, rank
+        # one all-reduce each: C3 / C4 sized to their states, the 10-group
+        # GROUP BY rows within the default cap (no lengths-only first round)
+        assert rounds == [1, 1, 1], rank
 
 
 def rccl_worker(port, n, out_q):

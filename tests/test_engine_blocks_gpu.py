@@ -227,3 +227,33 @@ def test_block_stream_dropped_early_stops_the_pipes(eng):
     assert r.rows == [(800_000, 799_999)]
     per_pipe, _ = _pull(eng, "SELECT number+1, number/2 FROM system.numbers_mt(80000) WHERE (number%8)<3")
     _check_against_oracle(per_pipe, R.projection_blocks(80_000, P1_EXPRS, P1_WHERE))
+
+
+def test_engine_destroyed_with_a_stream_open():
+    """fq_engine_destroy while a block stream is open (its pipes mid-partition,
+    blocked on the full merge channel): the engine closes and joins the stream
+    first -- no hang, no use of freed queues -- the orphaned stream's next call
+    fails with a message and fq_block_stream_free still releases it; the Python
+    Engine.close() closes its open BlockStreams itself."""
+    import ctypes as C
+
+    from fq_amd import abi
+    from fq_amd._lib import lib
+    from fq_amd.engine import Engine, fq_device_block
+    sql = b"SELECT number+1 FROM system.numbers_mt(4000000000) WHERE (number%8)<3"
+    e = Engine()
+    h = C.c_void_p()
+    assert lib.fq_engine_execute_blocks(e.h, sql, 0, 1, C.byref(h)) == 0
+    b, has = fq_device_block(), C.c_int32(0)
+    assert lib.fq_block_stream_next(h, C.byref(b), C.byref(has)) == 0 and has.value == 1
+    lib.fq_engine_destroy(e.h)  # the raw handle: the Python registry does not know this stream
+    e.h = None
+    assert lib.fq_block_stream_next(h, C.byref(b), C.byref(has)) == abi.FQ_E_INVALID
+    assert b"engine was destroyed" in lib.fq_last_error()
+    lib.fq_block_stream_free(h)
+    # the wrapper: close() closes the stream before the engine
+    e2 = Engine()
+    st = e2.execute_blocks(sql.decode())
+    assert st.next() is not None
+    e2.close()
+    assert st.h is None

@@ -134,3 +134,115 @@ def test_empty_block_sum_state_is_none():
     empty = F.DataBlock(["a"], [ops.from_numpy(np.zeros(0, dtype=np.int64), abi.DT_INT64)])
     f.accumulate(ENGINE, empty)
     assert f.accumulate_result() == [F.DataValue("Int64", None)]
+
+
+# ---- the Function-handle boundary with the reference's block geometry ----
+# A host that keeps the reference's transforms hands AggregatePartial a device
+# block that spans a partition's 10,000-row reference blocks (fq_block
+# block_rows) and carries FilterTransform's predicate (fq_block filter); the
+# per-block state machine of function_aggregator.rs:57-100 is replayed over it.
+
+def _num():
+    return F.FieldFunction.try_create("number")
+
+
+def _agg(name, arg=None):
+    return F.AggregatorFunction.try_create(name, [arg or _num()])
+
+
+def _lt(k):
+    return F.ComparisonFunction.try_create("<", [_num(), F.ConstantFunction.try_create(F.DataValue("UInt64", k))])
+
+
+def _oracle(n, exprs, where):
+    import fq_ref as R
+    num = R.E_field("number")
+    w = R.E_bin("<", num, R.E_const(where)) if where is not None else None
+    return R.aggregate_query(n, [R.E_fn(e, num) for e in exprs], where=w, parts=[(0, n - 1)])
+
+
+def test_handles_filtered_sum_over_empty_reference_block_fails_as_the_reference():
+    # numbers 0..99,999 as ONE device block of ten 10,000-row reference blocks;
+    # WHERE number < 25000 leaves blocks 3..9 empty: the reference's Sum meets
+    # a None block sum after two blocks and fails in to_array; Count/Max/Min
+    # skip the empty blocks
+    import fq_ref as R
+    n = 100_000
+    col = ops.numbers_column(0, n)
+    blk = F.DataBlock(["number"], [col], block_rows=10000, filter=_lt(25000))
+    with pytest.raises(R.RefError) as oracle_err:
+        _oracle(n, ["sum"], 25000)
+    f = _agg("sum")
+    with pytest.raises(F.FQError) as e:
+        f.accumulate(ENGINE, blk)
+    assert str(e.value) == "Internal Error: DataValue to array cannot be NONE NULL" == str(oracle_err.value)
+    # the same error through the fused multi-handle call (one scan, block mode)
+    with pytest.raises(F.FQError) as e2:
+        F.Function.accumulate_all(ENGINE, [_agg("count"), _agg("sum"), _agg("max")], blk)
+    assert str(e2.value) == str(e.value)
+    # the functions that do not need per-block sums: the oracle's values
+    want = [v.value for v in _oracle(n, ["count", "max", "min"], 25000)]
+    fs = [_agg("count"), _agg("max"), _agg("min")]
+    F.Function.accumulate_all(ENGINE, fs, blk)
+    assert [x.merge_result().value for x in fs] == want == [25000, 24999, 0]
+    # as ONE reference block (block_rows 0) the filtered Sum is fine
+    one = F.DataBlock(["number"], [col], block_rows=0, filter=_lt(25000))
+    f1 = _agg("sum")
+    f1.accumulate(ENGINE, one)
+    assert f1.merge_result() == F.DataValue("UInt64", 25000 * 24999 // 2)
+
+
+@pytest.mark.parametrize("k", [7, 25000, 10**6])
+def test_functions_accumulate_is_one_scan_and_equals_separate_calls(k):
+    # C3's aggregators plus a filter (numbers 0..999,999 in 10,000-row blocks,
+    # WHERE number < k): one fq_functions_accumulate = one fused scan, the same
+    # states as four fq_function_accumulate calls, and the oracle's merge
+    n = 1_000_000
+    col = ops.numbers_column(0, n)
+    blk = F.DataBlock(["number"], [col], block_rows=10000, filter=_lt(k))
+
+    def plan():  # sum(number)/count(number), max(number), min(number)
+        avg = F.ArithmeticFunction.try_create("/", [_agg("sum"), _agg("count")])
+        avg.set_depth(0)
+        return [avg, _agg("max"), _agg("min")]
+
+    fused, single = plan(), plan()
+    errs = []
+    s0 = ENGINE.stats()["scan_launches"]
+    try:
+        F.Function.accumulate_all(ENGINE, fused, blk)
+    except F.FQError as e:
+        errs.append(str(e))
+    s1 = ENGINE.stats()["scan_launches"]
+    assert s1 - s0 == 1
+    for f in single:
+        try:
+            f.accumulate(ENGINE, blk)
+        except F.FQError as e:
+            errs.append(str(e))
+            break
+    if k < n - 10000:  # a block is left empty: Sum fails, both ways alike
+        assert errs == ["Internal Error: DataValue to array cannot be NONE NULL"] * 2
+        return
+    assert not errs
+    assert [f.accumulate_result() for f in fused] == [f.accumulate_result() for f in single]
+    got = [f.merge_result().value for f in fused]
+    import fq_ref as R
+    num = R.E_field("number")
+    want = R.aggregate_query(n, [R.E_bin("/", R.E_fn("sum", num), R.E_fn("count", num)), R.E_fn("max", num),
+                                 R.E_fn("min", num)], where=R.E_bin("<", num, R.E_const(k)), parts=[(0, n - 1)])
+    assert got == [v.value for v in want]
+
+
+def test_eval_over_a_filtered_block_is_its_kept_rows():
+    x = np.random.default_rng(3).integers(0, 2**40, 50_000, dtype=np.uint64)
+    blk = F.DataBlock(["number"], [ops.from_numpy(x, abi.DT_UINT64)], block_rows=10000, filter=_lt(2**39))
+    f = F.ArithmeticFunction.try_create("+", [_num(), F.ConstantFunction.try_create(F.DataValue("UInt64", 1))])
+    got = f.eval(ENGINE, blk).to_numpy()
+    assert np.array_equal(got, x[x < 2**39] + np.uint64(1))
+
+
+def test_block_rows_is_validated():
+    blk = F.DataBlock(["number"], [ops.numbers_column(0, 10)], block_rows=-1)
+    with pytest.raises(F.FQError, match="negative block_rows"):
+        _agg("sum").accumulate(ENGINE, blk)

@@ -98,3 +98,28 @@ def test_kept_group_by_workspaces_leave_the_small_block_cache_room(Engine):
         assert st["cached_block_bytes"] == 0 and st["cached_workspace_bytes"] == 0
     finally:
         e.close()
+
+
+def test_large_block_cache_leaves_room_for_torch(Engine):
+    """The engine keeps a row pipeline's large projected blocks (2.5 GB each)
+    for the next query, but sized to the device -- at most 3/10 of its HBM --
+    and never past the point where less than max(8 GB, 1/16) of it would stay
+    free: after a 1e10-row p1 query (32 blocks of 2 x 2.5 GB) a torch
+    allocation of most of the free HBM still succeeds."""
+    import torch
+    torch.cuda.empty_cache()
+    e = Engine()
+    try:
+        total = torch.cuda.mem_get_info()[1]
+        with e.execute_blocks("SELECT number+1, number/2 FROM system.numbers_mt(10000000000) WHERE (number%8)<3") as st:
+            kept = sum(b.rows for b in st)
+        assert kept == 3_750_000_000
+        cached = e.stats()["cached_block_bytes"]
+        assert cached <= total * 3 // 10 + (64 << 20), (cached, total)
+        free = _free()
+        assert free >= max(8 * GB, total // 16) - 4 * GB, (free, total)
+        x = torch.empty(free - 2 * GB, dtype=torch.uint8, device="cuda")  # no OOM
+        del x
+        torch.cuda.empty_cache()
+    finally:
+        e.close()

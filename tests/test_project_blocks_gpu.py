@@ -246,3 +246,37 @@ def test_block_column_views(offset, block_rows):
     keep = h % np.uint64(5) < np.uint64(2)
     _check(h, keep, predicate(U64, [("%", 5)], "<", 2), [chain(U64, [("+", 1)])[0], None],
            [lambda k: k + np.uint64(1), lambda k: k], block_rows, col=col)
+
+
+@pytest.mark.parametrize("n_blocks,block_rows,n_cols", [(3000, 64, 1), (20011, 17, 2), (50000, 8, 3), (1025, 1000, 2)])
+def test_blocks_compact_multi_chunk_scan(n_blocks, block_rows, n_cols):
+    """fq_blocks_compact straight through the C ABI with more blocks than one
+    scan chunk holds (the engine's 4e8-row pieces have 40,000 blocks): random
+    per-block counts including zeros and full blocks, a short last block, 1-3
+    columns -- against numpy's concatenation of each block's valid rows."""
+    import ctypes as C
+
+    from fq_amd._lib import check, lib
+    rng = np.random.default_rng(n_blocks)
+    length = n_blocks * block_rows - block_rows // 2  # the last block is short
+    last = length - (n_blocks - 1) * block_rows
+    counts = rng.integers(0, block_rows + 1, n_blocks)
+    counts[rng.random(n_blocks) < 0.2] = 0
+    counts[rng.random(n_blocks) < 0.2] = block_rows
+    counts[-1] = min(counts[-1], last)
+    cols = [rng.integers(0, 2**63, length, dtype=np.uint64) for _ in range(n_cols)]
+    d_in = [ops.from_numpy(c, U64) for c in cols]
+    d_out = [ops.empty_column(max(int(counts.sum()), 1), U64) for _ in range(n_cols)]
+    d_counts = ops.from_numpy(counts.astype(np.int64), abi.DT_INT64)
+    ws = ops.Workspace(lib.fq_blocks_compact_workspace_bytes(n_blocks))
+    ins = (C.c_void_p * n_cols)(*[c.ptr for c in d_in])
+    outs = (C.c_void_p * n_cols)(*[o.ptr for o in d_out])
+    out_len = C.c_int64(-1)
+    torch.cuda.synchronize()
+    check(lib.fq_blocks_compact(n_cols, ins, length, block_rows, C.c_void_p(d_counts.ptr), outs, C.byref(out_len),
+                                ws.ptr, ws.nbytes, C.c_void_p(torch.cuda.current_stream().cuda_stream)))
+    assert out_len.value == int(counts.sum())
+    for c, o in zip(cols, d_out):
+        want = np.concatenate([c[b * block_rows: b * block_rows + int(k)] for b, k in enumerate(counts)])
+        got = o.to_numpy()[:out_len.value]
+        assert np.array_equal(got, want)

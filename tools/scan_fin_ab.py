@@ -1,0 +1,120 @@
+"""A/B in ONE process of what a C3 step costs beyond its scans (round 5):
+
+  kernel level -- 8 back-to-back fq_aggregate scans of resident 10 GB numbers_mt
+  partitions on one stream, one event pair around all 8 (none between), for
+  FQ_TUNE_SCAN_FIN = 2 (scan + separate finalize launch), 0 (in-launch
+  finalize, plain partial + agent release), 1 (in-launch, write-through
+  partial); modes alternate round by round;
+
+  engine level -- the C3 statement through fq_engine_execute (as bench.py's
+  step) for (SCAN_FIN, POOL_SPIN_US) in {(2, 0), (0, 0), (0, 1000), (1, 1000)},
+  alternating: step wall time and the engine's scan span (FQ_OPT_PROFILE 2).
+
+python tools/scan_fin_ab.py [rounds] > gpurun_out/scan_fin_ab.json"""
+import ctypes as C
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "fuse-query_amd"))
+import torch  # noqa: E402
+
+from fq_amd import abi, ops  # noqa: E402
+from fq_amd._lib import check, lib  # noqa: E402
+from fq_amd.engine import PROFILE_SPAN, Engine  # noqa: E402
+
+ROUNDS = int(sys.argv[1]) if len(sys.argv) > 1 else 6
+N = 10_000_000_000
+P = 1_250_000_000
+ALL = abi.AGG_SUM | abi.AGG_COUNT | abi.AGG_MAX | abi.AGG_MIN
+
+
+def kernel_level():
+    cols = [ops.numbers_column(i * P, P) for i in range(8)]
+    ws = ops.aggregate_workspace()
+    out = torch.empty(48 * 8, dtype=torch.uint8, device="cuda")
+    s = torch.cuda.current_stream()
+    sp = C.c_void_p(s.cuda_stream)
+    ccols = [c.col() for c in cols]
+
+    def run(mask):
+        for i, cc in enumerate(ccols):
+            check(lib.fq_aggregate(C.byref(cc), 10000, None, None, mask, C.c_void_p(out.data_ptr() + 48 * i),
+                                   ws.ptr, ws.nbytes, sp))
+
+    res = {m: [] for m in (2, 0, 1)}
+    sums = {}
+    for r in range(ROUNDS):
+        for m in ((2, 0, 1) if r % 2 == 0 else (1, 0, 2)):
+            ops.tune_set("SCAN_FIN", m)
+            mask = ALL | abi.AGG_ONE_LAUNCH
+            run(mask)
+            torch.cuda.synchronize()
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            for _ in range(5):
+                a.record(s)
+                run(mask)
+                b.record(s)
+                b.synchronize()
+                res[m].append(a.elapsed_time(b))
+            sums[m] = bytes(out.cpu().numpy())
+    ops.tune_set("SCAN_FIN", 0)
+    assert sums[0] == sums[1] == sums[2], "the three forms must give the same states"
+    return {str(m): {"median_ms_8_scans": statistics.median(v), "min": min(v), "max": max(v), "n": len(v),
+                     "per_scan_ms": statistics.median(v) / 8} for m, v in res.items()}
+
+
+def engine_level():
+    sql = ("SELECT sum(number)/count(number), max(number), min(number) FROM system.numbers_mt(%d)" % N).encode()
+    e = Engine(device=0, profile=PROFILE_SPAN)
+    e.materialize_numbers(N)
+    val = abi.fq_value()
+
+    def step():
+        r = C.c_void_p()
+        check(lib.fq_engine_execute(e.h, sql, C.byref(r)))
+        row = []
+        for c in range(3):
+            check(lib.fq_result_value(r, 0, c, C.byref(val)))
+            row.append(val.bits)
+        lib.fq_result_free(r)
+        return row
+
+    configs = [(2, 0), (0, 0), (0, 1000), (1, 1000)]
+    res = {c: {"step": [], "span": []} for c in configs}
+    s = N * (N - 1) // 2 % 2**64
+    for r in range(ROUNDS):
+        for c in (configs if r % 2 == 0 else configs[::-1]):
+            ops.tune_set("SCAN_FIN", c[0])
+            ops.tune_set("POOL_SPIN_US", c[1])
+            for _ in range(2):
+                assert step() == [s // N, N - 1, 0]
+            e.reset_stats()
+            t0 = time.perf_counter()
+            for _ in range(10):
+                step()
+            dt = (time.perf_counter() - t0) / 10 * 1e3
+            st = e.stats()
+            res[c]["step"].append(dt)
+            res[c]["span"].append(st["scan_ms"] / 10)
+    ops.tune_reset()
+    e.close()
+    out = {}
+    for c, v in res.items():
+        out["fin%d_spin%d" % c] = {"step_ms_median": statistics.median(v["step"]), "step_ms_all": v["step"],
+                                   "scan_span_ms_median": statistics.median(v["span"]),
+                                   "step_over_span": statistics.median(v["step"]) / statistics.median(v["span"])}
+    return out
+
+
+if __name__ == "__main__":
+    ops.require_gpu()
+    k = kernel_level()
+    torch.cuda.empty_cache()
+    out = {"kernel_8_scans": k, "engine_c3_step": engine_level(), "rounds": ROUNDS,
+           "note": "SCAN_FIN 2 = scan + finalize launch (round 4), 0 = in-launch finalize with an agent release, "
+                   "1 = in-launch with write-through partials; POOL_SPIN_US = pipe threads poll before sleeping"}
+    print(json.dumps(out, indent=1))

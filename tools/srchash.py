@@ -10,7 +10,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 # the sources each bench query's kernels are built from (csrc/ relative);
 # fq_knobs.cpp holds every launch-shape default
-_SCAN = ["fq_aggregate.hip", "fq_device.h", "fq_knobs.cpp"]
+_SCAN = ["fq_aggregate.hip", "fq_scan.h", "fq_device.h", "fq_knobs.cpp"]
 _JIT = ["fq_jit.hip", "fq_scan.h", "fq_device.h", "fq_knobs.cpp"]
 QUERY_SOURCES = {
     "c2": _SCAN, "c3": _SCAN, "max": _SCAN, "avg": _SCAN,
