@@ -774,8 +774,9 @@ def check_rank_device(args, rank, world, local):
 def run_c_host(args):
     """fq_c_client --bench STEPS N WARMUP as a child process (the C host of the
     C ABI: libfq_amd.so on /opt/rocm's HIP runtime, no Python or torch), over the
-    same C3 workload; its JSON line, or an error record.  Runs before this
-    process has touched the GPU, so the two never hold HBM at the same time."""
+    same C3 workload; its JSON line, or an error record.  It materialises its
+    own numbers_mt(N) (80 GB at 1e10 beside this process's 80 GB: 288 GB of
+    HBM hold both)."""
     exe = os.path.join(ROOT, "fuse-query_amd", "lib", "fq_c_client")
     n_total = int(args.rows_total or args.rows_per_gpu)
     cmd = [exe, "--bench", str(args.steps), str(n_total), str(max(args.warmup, 1))]
@@ -879,13 +880,6 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # The drop-in stack a C/Rust host binds (tests/native/fq_c_client.c: no
-    # torch, /opt/rocm's HIP runtime), timed in a child process BEFORE this one
-    # touches the GPU, on the same workload: reported beside the line.
-    c_host = None
-    if world == 1 and args.query == "c3" and not args.no_c_host:
-        c_host = run_c_host(args)
-
     _load_runtime()
     args.tuned = {}
     for kv in args.tune:
@@ -1040,6 +1034,16 @@ def main():
     rccl_w1 = None
     if world == 1 and args.dist_backend == "nccl" and args.query not in GROUP_MOD and not args.no_rccl_world1:
         rccl_w1 = rccl_world1(eng, sql, expect, local, args)
+    # The drop-in stack a C/Rust host binds (tests/native/fq_c_client.c: no
+    # torch, /opt/rocm's HIP runtime) on the same workload, in a child process
+    # AFTER this one's timed steps, while this one holds its memory and idles:
+    # a process that starts right after another freed ~80 GB of HBM runs its
+    # scans ~3-4 % slower while the driver reclaims that memory -- whichever
+    # host it is (profiles/r05_b_host_spread/), so neither leg may follow a free.
+    c_host = None
+    if world == 1 and args.query == "c3" and not args.no_c_host:
+        torch.cuda.synchronize()
+        c_host = run_c_host(args)
     out = None
     if rank == 0:
         # the partitioned GROUP BY (g2): gpart + block scatter + bins per chunk

@@ -415,11 +415,21 @@ void AggregatorFunction::accumulate_summary(const fq_agg_state &st) {
 
 static uint32_t scan_mask(uint32_t op) { return op | FQ_AGG_COUNT; }
 
+// The in-launch finalize (FQ_AGG_ONE_LAUNCH, the workers' workspaces are
+// zeroed at allocation) or the separate finalize launch: the latter measured
+// faster on MI355X -- 8 back-to-back scans 11.02 ms against 11.07 (write-
+// through partials) and 11.16 (agent release), profiles/r05_b_scan_fin_ab.json:
+// 512 workgroups each waiting on a device-scope ticket, then one workgroup's
+// serial fold, cost more than a 4.4 us kernel after a ~1.5 us boundary.
+static uint32_t engine_one_launch() {
+    return fqc::knob(FQ_TUNE_ENGINE_ONE_LAUNCH) ? FQ_AGG_ONE_LAUNCH : 0u;
+}
+
 static fq_agg_state run_scan(const Column &col, int64_t block_rows, const fq_pred *pred, const fq_expr *value,
                              uint32_t mask, ExecCtx &ctx) {
     auto out = DeviceBuffer::alloc(sizeof(fq_agg_state), ctx.stream());
     fq_col c = col.abi();
-    check_fq(fq_aggregate(&c, block_rows, pred, value, mask | FQ_AGG_ONE_LAUNCH, (fq_agg_state *)out->ptr,
+    check_fq(fq_aggregate(&c, block_rows, pred, value, mask | engine_one_launch(), (fq_agg_state *)out->ptr,
                           ctx.res->ws, ctx.res->ws_bytes, ctx.stream()));
     fq_agg_state st{};
     check_hip(hipMemcpyAsync(&st, out->ptr, sizeof st, hipMemcpyDeviceToHost, ctx.stream()), "hipMemcpyAsync");
@@ -898,14 +908,30 @@ void ScanGroup::arrive(bool wait) {
     cv_.notify_all();
 }
 
+// ONE pipe waits on the end events; the others sleep on the group's condition
+// and are woken together.  Eight threads in hipEventSynchronize on one event
+// were released one by one, ~15 us apart: ~100 us at the end of every C3
+// query (profiles/r05_c_c3_query_timeline.txt).
 void ScanGroup::wait_end() {
-    std::vector<hipEvent_t> ends;
-    {
-        std::lock_guard<std::mutex> lk(mu_);
-        for (const QueueSpan &s : queues_) ends.push_back(s.end);
+    std::unique_lock<std::mutex> lk(mu_);
+    if (waiter_) {
+        cv_.wait(lk, [&] { return ended_; });
+        if (end_error_ != hipSuccess) check_hip(end_error_, "hipEventSynchronize");
+        return;
     }
+    waiter_ = true;
+    std::vector<hipEvent_t> ends;
+    for (const QueueSpan &s : queues_) ends.push_back(s.end);
+    lk.unlock();
+    hipError_t err = hipSuccess;
     for (hipEvent_t e : ends)
-        if (e) check_hip(hipEventSynchronize(e), "hipEventSynchronize");
+        if (e && err == hipSuccess) err = hipEventSynchronize(e);
+    lk.lock();
+    ended_ = true;
+    end_error_ = err;
+    cv_.notify_all();
+    lk.unlock();
+    check_hip(err, "hipEventSynchronize");
 }
 
 void ScanGroup::account() {
@@ -1032,9 +1058,9 @@ void AggFusion::end_block() {
             e0 = ctx_.res->take_event();
             e1 = ctx_.res->take_event();
         }
-        if (prof) {
+        if (prof && (g.has_pred || g.value.expr.n_steps)) {
             // compile a specialised scan (first use of this expression shape)
-            // outside the timed region
+            // outside the timed region (identity scans are precompiled)
             fq_jit_stats js;
             if (fq_jit_get_stats(&js) == FQ_OK &&
                 (js.mode == FQ_JIT_ALWAYS || (js.mode == FQ_JIT_AUTO && c.len >= js.min_rows)))
@@ -1050,7 +1076,7 @@ void AggFusion::end_block() {
             if (ticket_ && ticket_->group()) ticket_->group()->before_launch(ctx_);
             if (pairs) check_hip(hipEventRecord(e0, ctx_.stream()), "hipEventRecord");
             check_fq(fq_aggregate(&c, g.block_rows, g.has_pred ? g.pred.get() : nullptr,
-                                  g.value.expr.n_steps ? &g.value.expr : nullptr, g.mask | FQ_AGG_ONE_LAUNCH,
+                                  g.value.expr.n_steps ? &g.value.expr : nullptr, g.mask | engine_one_launch(),
                                   (fq_agg_state *)dst, ctx_.res->ws, ctx_.res->ws_bytes, ctx_.stream()));
             if (pairs) check_hip(hipEventRecord(e1, ctx_.stream()), "hipEventRecord");
         }

@@ -325,6 +325,8 @@ class ScanGroup {
     std::condition_variable cv_;
     int left_;
     bool closed_ = false, accounted_ = false;
+    bool waiter_ = false, ended_ = false;  // wait_end: one pipe waits on the events
+    hipError_t end_error_ = hipSuccess;
     std::vector<QueueSpan> queues_;  // stable once every pipe has arrived
 };
 using ScanGroupRef = std::shared_ptr<ScanGroup>;

@@ -308,7 +308,11 @@ StreamRef MergeProcessor::execute() {
                 // the consumer gone (a satisfied LIMIT dropped the merged
                 // stream): stop pulling instead of scanning the rest
                 while (!ch->is_closed() && s->next(b)) {
-                    ctx.sync();  // device work of this block done before another thread reads it
+                    // device work of this block done before another thread reads
+                    // it; a host block (AggregatePartial's states) has none left
+                    bool device = (bool)b.layout || (bool)b.filter;
+                    for (const Column &c : b.columns) device |= c.on_device();
+                    if (device) ctx.sync();
                     Channel::Item it;
                     b.pipe = (int32_t)pipe;
                     it.block = std::move(b);

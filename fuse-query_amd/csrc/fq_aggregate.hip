@@ -810,8 +810,7 @@ fq_status fq_aggregate(const fq_col *col, int64_t block_rows, const fq_pred *pre
                        uint32_t agg_mask, fq_agg_state *d_out, void *d_ws, size_t ws_bytes, void *stream) {
     using namespace fqk;
     if (!col || !d_out || !d_ws) return fqc::fail(FQ_E_INVALID, "fq_aggregate: NULL argument");
-    // FQ_TUNE_SCAN_FIN = 2: the separate finalize launch even when asked for one (A/B)
-    const bool one_launch = (agg_mask & FQ_AGG_ONE_LAUNCH) != 0 && fqc::knob(FQ_TUNE_SCAN_FIN) != 2;
+    const bool one_launch = (agg_mask & FQ_AGG_ONE_LAUNCH) != 0;
     agg_mask &= ~FQ_AGG_ONE_LAUNCH;
     // one_launch needs the counter behind the partials; without it a
     // pre-counter workspace (kPartialsBytes) still serves the two launches

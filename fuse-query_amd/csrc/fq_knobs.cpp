@@ -56,7 +56,8 @@ constexpr KnobDef kDefs[FQ_TUNE_COUNT] = {
     {2, 1, 4, 1, false},         // GBINS_WG_PER_CU
     {1, 0, 1, 1, false},         // GBINS_FIT_LDS
     {1000, 0, 100000, 1, false}, // POOL_SPIN_US
-    {0, 0, 2, 1, false},         // SCAN_FIN
+    {1, 0, 1, 1, false},         // SCAN_FIN
+    {0, 0, 1, 1, false},         // ENGINE_ONE_LAUNCH
 };
 
 std::atomic<int64_t> g_val[FQ_TUNE_COUNT] = {};

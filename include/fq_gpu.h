@@ -438,8 +438,10 @@ fq_status fq_jit_prepare(const fq_col *col, int64_t block_rows, const fq_pred *p
 #define FQ_TUNE_GBINS_FIT_LDS 35    /* GROUP BY bins pass, range bins: LDS table of one bin's keys, 1 (0/1)  */
 #define FQ_TUNE_POOL_SPIN_US 36     /* engine pipe threads poll for the next task before sleeping, 1000 us (0..100000) */
 #define FQ_TUNE_SCAN_FIN 37         /* FQ_AGG_ONE_LAUNCH partial hand-off: 0 plain store + agent release, 1 write-through
-                                       stores, 2 ignore the flag (separate finalize launch; A/B): 0 (0..2) */
-#define FQ_TUNE_COUNT 38
+                                       stores: 1 (0/1) */
+#define FQ_TUNE_ENGINE_ONE_LAUNCH 38 /* the engine's scans pass FQ_AGG_ONE_LAUNCH: 0 (0/1; the separate finalize
+                                       launch measured faster, profiles/r05_b_scan_fin_ab.json) */
+#define FQ_TUNE_COUNT 39
 /* FQ_E_INVALID for an unknown knob or a value outside the knob's set */
 fq_status fq_tune_set(int32_t knob, int64_t value);
 /* the knob's current value; -1 for an unknown knob */

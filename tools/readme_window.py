@@ -18,7 +18,7 @@ SQLS = {
           "GROUP BY number%100000",
 }
 sql = SQLS[sys.argv[1] if len(sys.argv) > 1 else "readme"]
-e = Engine(device=0)
+e = Engine(device=0, profile=int(sys.argv[2]) if len(sys.argv) > 2 else 0)  # FQ_OPT_PROFILE (bench: 2)
 e.materialize_numbers(10**10)
 torch.cuda.synchronize()
 for _ in range(5):

@@ -1,13 +1,13 @@
 """A/B in ONE process of what a C3 step costs beyond its scans (round 5):
 
   kernel level -- 8 back-to-back fq_aggregate scans of resident 10 GB numbers_mt
-  partitions on one stream, one event pair around all 8 (none between), for
-  FQ_TUNE_SCAN_FIN = 2 (scan + separate finalize launch), 0 (in-launch
-  finalize, plain partial + agent release), 1 (in-launch, write-through
-  partial); modes alternate round by round;
+  partitions on one stream, one event pair around all 8 (none between):
+  "2" = scan + separate finalize launch, "0" = FQ_AGG_ONE_LAUNCH with
+  FQ_TUNE_SCAN_FIN 0 (plain partial + agent release), "1" = SCAN_FIN 1
+  (write-through partial); modes alternate round by round;
 
   engine level -- the C3 statement through fq_engine_execute (as bench.py's
-  step) for (SCAN_FIN, POOL_SPIN_US) in {(2, 0), (0, 0), (0, 1000), (1, 1000)},
+  step) for (form, POOL_SPIN_US), form 2 = FQ_TUNE_ENGINE_ONE_LAUNCH 0,
   alternating: step wall time and the engine's scan span (FQ_OPT_PROFILE 2).
 
 python tools/scan_fin_ab.py [rounds] > gpurun_out/scan_fin_ab.json"""
@@ -45,12 +45,14 @@ def kernel_level():
             check(lib.fq_aggregate(C.byref(cc), 10000, None, None, mask, C.c_void_p(out.data_ptr() + 48 * i),
                                    ws.ptr, ws.nbytes, sp))
 
+    # 2 = no FQ_AGG_ONE_LAUNCH (scan + finalize launch); 0 / 1 = in-launch, SCAN_FIN form 0 / 1
     res = {m: [] for m in (2, 0, 1)}
     sums = {}
     for r in range(ROUNDS):
         for m in ((2, 0, 1) if r % 2 == 0 else (1, 0, 2)):
-            ops.tune_set("SCAN_FIN", m)
-            mask = ALL | abi.AGG_ONE_LAUNCH
+            if m != 2:
+                ops.tune_set("SCAN_FIN", m)
+            mask = ALL | (abi.AGG_ONE_LAUNCH if m != 2 else 0)
             run(mask)
             torch.cuda.synchronize()
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -61,7 +63,7 @@ def kernel_level():
                 b.synchronize()
                 res[m].append(a.elapsed_time(b))
             sums[m] = bytes(out.cpu().numpy())
-    ops.tune_set("SCAN_FIN", 0)
+    ops.tune_reset()
     assert sums[0] == sums[1] == sums[2], "the three forms must give the same states"
     return {str(m): {"median_ms_8_scans": statistics.median(v), "min": min(v), "max": max(v), "n": len(v),
                      "per_scan_ms": statistics.median(v) / 8} for m, v in res.items()}
@@ -83,12 +85,15 @@ def engine_level():
         lib.fq_result_free(r)
         return row
 
-    configs = [(2, 0), (0, 0), (0, 1000), (1, 1000)]
+    # (form, POOL_SPIN_US): form 2 = the engine's scans without FQ_AGG_ONE_LAUNCH
+    configs = [(2, 0), (2, 1000), (0, 1000), (1, 1000)]
     res = {c: {"step": [], "span": []} for c in configs}
     s = N * (N - 1) // 2 % 2**64
     for r in range(ROUNDS):
         for c in (configs if r % 2 == 0 else configs[::-1]):
-            ops.tune_set("SCAN_FIN", c[0])
+            ops.tune_set("ENGINE_ONE_LAUNCH", 0 if c[0] == 2 else 1)
+            if c[0] != 2:
+                ops.tune_set("SCAN_FIN", c[0])
             ops.tune_set("POOL_SPIN_US", c[1])
             for _ in range(2):
                 assert step() == [s // N, N - 1, 0]
