@@ -208,13 +208,17 @@ def latest_pmc_traffic(kernel_substr, query, rows_per_launch):
 def host_split(st, steps, ms_per_step, world):
     """Rank 0's step, split by the engine's own host timers (fq_engine_stats),
     per step.  One GPU: plan (SQL -> pipeline), exec (pipeline until the result
-    block), first_launch (query start -> first scan enqueued).  World > 1: the
+    block), first_launch (query start -> first scan enqueued), tail (the scans'
+    end event seen -> the result block: merge + AggregateFinal), outside_exec
+    (the step minus plan and exec: result rows, frees, the binding's calls).  World > 1: the
     distributed split -- partial (fq_engine_execute_partial: plan + this rank's
     scans + local merge), exchange (the all-reduce rounds, including the wait for
     the slowest rank), final (AggregateFinal over every rank's states) -- and
     what those three account for of the step (the rest is the binding's
     Python)."""
     out = {"plan": st["plan_ms"] / steps, "first_launch": st["first_launch_ms"] / steps, "exec": st["exec_ms"] / steps}
+    if world == 1:
+        out.update({"tail": st["tail_ms"] / steps, "outside_exec": ms_per_step - (st["plan_ms"] + st["exec_ms"]) / steps})
     if world > 1:
         part, xch, fin = (st[k] / steps for k in ("partial_ms", "exchange_ms", "final_ms"))
         out.update({"partial": part, "exchange": xch, "final": fin,
@@ -1095,8 +1099,8 @@ def main():
                            "fq_group_aggregate_partitioned (fq_jit_gpart + block grouping + fq_jit_groupby_bins), "
                            "one set per partition; achieved = the column's 8 B/row over the set"
                            if args.query == "g2" else
-                           "fq_aggregate fused scan (%s, its workgroup partials folded by its last workgroup: "
-                           "FQ_AGG_ONE_LAUNCH), one launch per partition%s; %s"
+                           "fq_aggregate fused scan (%s, then agg_finalize_kernel folds its workgroup partials), "
+                           "one launch per partition%s; %s"
                            % (kernel, " (hipRTC-specialised for this expression shape)" if jitted else "",
                               "timed by one HIP-event span per query on the engine's queue (first scan start to "
                               "last scan end, launch gaps included) / launches" if args.streams == 1 else

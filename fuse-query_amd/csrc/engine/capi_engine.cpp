@@ -349,7 +349,10 @@ fq_status fq_engine_execute(fq_engine *e, const char *sql, fq_result **out) {
                     r = std::make_unique<fq_result>();
                     continue;
                 }
-                e->rt->stats.exec_ns += (uint64_t)(fq::now_ns() - t1);
+                const int64_t t2 = fq::now_ns();
+                e->rt->stats.exec_ns += (uint64_t)(t2 - t1);
+                const int64_t seen = e->rt->stats.scan_end_seen.exchange(0);
+                if (seen) e->rt->stats.tail_ns += (uint64_t)(t2 - seen);
                 break;
             }
             if (r->names.empty())
@@ -676,6 +679,7 @@ fq_status fq_engine_get_stats(fq_engine *e, fq_engine_stats *out) {
     out->plan_ms = (double)e->rt->stats.plan_ns.load() * 1e-6;
     out->exec_ms = (double)e->rt->stats.exec_ns.load() * 1e-6;
     out->first_launch_ms = (double)e->rt->stats.first_launch_ns.load() * 1e-6;
+    out->tail_ms = (double)e->rt->stats.tail_ns.load() * 1e-6;
     out->partial_ms = (double)e->rt->stats.partial_ns.load() * 1e-6;
     out->exchange_ms = (double)e->rt->stats.exchange_ns.load() * 1e-6;
     out->final_ms = (double)e->rt->stats.final_ns.load() * 1e-6;
@@ -702,6 +706,7 @@ fq_status fq_engine_reset_stats(fq_engine *e) {
     e->rt->stats.plan_ns = 0;
     e->rt->stats.exec_ns = 0;
     e->rt->stats.first_launch_ns = 0;
+    e->rt->stats.tail_ns = 0;
     e->rt->stats.partial_ns = 0;
     e->rt->stats.exchange_ns = 0;
     e->rt->stats.final_ns = 0;

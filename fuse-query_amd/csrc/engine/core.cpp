@@ -772,7 +772,21 @@ ExecCtx::ExecCtx(Runtime *r, bool own_queue) : rt(r), res(nullptr), prev_(g_curr
 
 ExecCtx::~ExecCtx() {
     g_current = prev_;
-    rt->release(res);
+    if (!leased_) rt->release(res);
+}
+
+std::shared_ptr<WorkerRes> ExecCtx::lease() {
+    if (leased_) throw_internal("ExecCtx::lease: already leased");
+    leased_ = true;
+    Runtime *r = rt;
+    return std::shared_ptr<WorkerRes>(res, [r](WorkerRes *w) { r->release(w); });
+}
+
+void complete_block(DataBlock &b) {
+    if (!b.complete) return;
+    std::function<void(DataBlock &)> f = std::move(b.complete);
+    b.complete = nullptr;
+    f(b);
 }
 
 ExecCtx *ExecCtx::current_or_null() { return g_current; }

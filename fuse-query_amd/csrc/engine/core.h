@@ -18,11 +18,11 @@
 #include <chrono>
 #include <condition_variable>
 #include <deque>
-#include <thread>
 #include <functional>
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "fq_gpu.h"
@@ -144,6 +144,10 @@ struct EngineStats {
     // query start (steady_clock ns) while a query runs; the first scan launch
     // of the query adds (launch - start) to first_launch_ns and clears it
     std::atomic<int64_t> query_t0{0};
+    // FQ_OPT_PROFILE 2: when the query's scan group saw its end event
+    // (ScanGroup::wait_end); fq_engine_execute adds (exec end - it) to tail_ns
+    std::atomic<int64_t> scan_end_seen{0};
+    std::atomic<uint64_t> tail_ns{0};
 };
 
 struct WorkerRes {
@@ -283,10 +287,15 @@ class ExecCtx {
     AggFusion *fusion = nullptr;  // set while an AggregatePartial drains its input
     hipStream_t stream() const { return stream_; }
     void sync();
+    // hands this context's WorkerRes (queue, workspace, pinned result slots)
+    // to a shared owner that releases it to the runtime: work this context
+    // enqueued may then be finished on another thread after it is gone
+    std::shared_ptr<WorkerRes> lease();
 
    private:
     ExecCtx *prev_;
     hipStream_t stream_ = nullptr;
+    bool leased_ = false;
 };
 
 // ---------------------------------------------------------------------------
@@ -345,6 +354,10 @@ struct DataBlock {
     std::shared_ptr<const BlockLayout> layout;
     // the MergeProcessor input (partition pipe) the block came from; -1 unknown
     int32_t pipe = -1;
+    // set: the block's columns are not final yet -- the consumer runs this
+    // (once, on its own thread) before reading them: AggregatePartial's states
+    // once the query's scans have ended (complete_block)
+    std::function<void(DataBlock &)> complete;
 
     int64_t num_rows() const;  // columns[0].len (data_block.rs:46-48); needs no pending filter
     int num_columns() const { return (int)columns.size(); }
@@ -355,6 +368,8 @@ struct DataBlock {
 // Compact a block with a pending filter (fq_compare/eval + fq_filter_compact)
 // or a block-stream layout (fq_blocks_compact) into plain columns.
 DataBlock materialize(const DataBlock &b, ExecCtx &ctx);
+// runs and clears b.complete, if set
+void complete_block(DataBlock &b);
 inline bool needs_materialize(const DataBlock &b) { return b.filter || b.layout; }
 
 // DataColumnarValue

@@ -914,6 +914,7 @@ void ScanGroup::arrive(bool wait) {
 // query (profiles/r05_c_c3_query_timeline.txt).
 void ScanGroup::wait_end() {
     std::unique_lock<std::mutex> lk(mu_);
+    cv_.wait(lk, [&] { return closed_; });  // every pipe has arrived: the end events exist
     if (waiter_) {
         cv_.wait(lk, [&] { return ended_; });
         if (end_error_ != hipSuccess) check_hip(end_error_, "hipEventSynchronize");
@@ -926,6 +927,7 @@ void ScanGroup::wait_end() {
     hipError_t err = hipSuccess;
     for (hipEvent_t e : ends)
         if (e && err == hipSuccess) err = hipEventSynchronize(e);
+    if (rt_->profile.load(std::memory_order_relaxed) == 2) rt_->stats.scan_end_seen = now_ns();
     lk.lock();
     ended_ = true;
     end_error_ = err;
@@ -948,7 +950,8 @@ void ScanGroup::account() {
 // ---------------------------------------------------------------------------
 // AggFusion
 // ---------------------------------------------------------------------------
-AggFusion::AggFusion(ExecCtx &ctx, ScanTicket *ticket) : ctx_(ctx), ticket_(ticket) {}
+AggFusion::AggFusion(ExecCtx &ctx, ScanTicket *ticket)
+    : ctx_(ctx), rt_(ctx.rt), res_(ctx.res), stream_(ctx.stream()), ticket_(ticket) {}
 
 AggFusion::~AggFusion() {
     // an exception left scans in flight: they write into this worker's pinned
@@ -960,13 +963,13 @@ AggFusion::~AggFusion() {
         }
     }
     for (auto &p : events_) {
-        ctx_.res->give_event(p.first);
-        ctx_.res->give_event(p.second);
+        res_->give_event(p.first);
+        res_->give_event(p.second);
     }
 }
 
 fq_agg_state *AggFusion::slot_host(size_t k) const {
-    return ctx_.res->slot_chunks[k / WorkerRes::kSlotChunk] + k % WorkerRes::kSlotChunk;
+    return res_->slot_chunks[k / WorkerRes::kSlotChunk] + k % WorkerRes::kSlotChunk;
 }
 
 size_t AggFusion::alloc_slot() {
@@ -983,13 +986,13 @@ size_t AggFusion::alloc_slot() {
 }
 
 void AggFusion::wait_launched() {
-    hipEvent_t done = ctx_.res->take_event();
+    hipEvent_t done = res_->take_event();
     {
-        std::lock_guard<std::mutex> lk(*ctx_.res->launch_mu);
-        check_hip(hipEventRecord(done, ctx_.stream()), "hipEventRecord");
+        std::lock_guard<std::mutex> lk(*res_->launch_mu);
+        check_hip(hipEventRecord(done, stream_), "hipEventRecord");
     }
     hipError_t e = hipEventSynchronize(done);
-    ctx_.res->give_event(done);
+    res_->give_event(done);
     check_hip(e, "hipEventSynchronize");
 }
 
@@ -1107,11 +1110,23 @@ void AggFusion::finish() {
         if (!events_.empty()) check_hip(hipEventSynchronize(events_.back().second), "hipEventSynchronize");
         else wait_launched();
     }
+    replay();
+}
+
+bool AggFusion::finish_deferred() {
+    end_block();
+    if (!launched_ || !ticket_ || !ticket_->group()) return false;
+    ticket_->arrive_only();
+    ticket_ = nullptr;  // the ticket lives on the pipe's stack
+    return true;
+}
+
+void AggFusion::replay() {
     finished_ = true;
     for (auto &p : events_) {
         float ms = 0;
         if (hipEventElapsedTime(&ms, p.first, p.second) == hipSuccess)
-            ctx_.rt->stats.scan_ns += (uint64_t)((double)ms * 1e6);
+            rt_->stats.scan_ns += (uint64_t)((double)ms * 1e6);
     }
     keepalive_.clear();
     for (Entry &en : log_) {

@@ -353,6 +353,13 @@ class ScanTicket {
             g_->account();
         }
     }
+    // the same without waiting: the pipe's states are read later, by whoever
+    // calls wait_end() (AggregatePartial's deferred block)
+    void arrive_only() {
+        if (!g_ || done_) return;
+        done_ = true;
+        g_->arrive(false);
+    }
 
    private:
     ScanGroup *g_;
@@ -371,6 +378,12 @@ class AggFusion {
     void add_error(const FQException &e);  // a non-aggregator failure at this point
     void end_block();                      // launch this block's scans
     void finish();                         // sync + replay; throws the first error
+    // In a scan group: launch the last block's scans and arrive at the group
+    // without waiting.  true: the caller keeps this object (and the context's
+    // WorkerRes, ExecCtx::lease) and calls replay() after the group's
+    // wait_end(), on any thread; false: nothing launched, call finish().
+    bool finish_deferred();
+    void replay();  // the scans have ended: states -> aggregators; throws the first error
 
    private:
     struct Group {
@@ -392,7 +405,12 @@ class AggFusion {
         bool has_error = false;
         FQException err{0, ""};
     };
-    ExecCtx &ctx_;
+    ExecCtx &ctx_;  // the pipe's context: add() / end_block() only
+    // what finish / replay / the destructor use, valid while the WorkerRes is
+    // held (the context, or its lease)
+    Runtime *rt_;
+    WorkerRes *res_;
+    hipStream_t stream_;
     ScanTicket *ticket_ = nullptr;  // the query's pipes wait together (ScanGroup)
     std::vector<Group> cur_;
     std::vector<Entry> log_;

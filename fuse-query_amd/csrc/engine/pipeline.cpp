@@ -270,6 +270,7 @@ class ChannelStream : public BlockStream {
     bool next(DataBlock &out) override {
         Channel::Item it;
         if (!ch->recv(it)) return false;
+        settle(it);
         if (it.is_err) {
             // Several pipes may fail; the reference surfaces whichever error
             // reaches its channel first (processor_merge.rs:45-63).  Report
@@ -277,12 +278,30 @@ class ChannelStream : public BlockStream {
             // what a sequential run of the partitions raises first.
             ch->close();
             Channel::Item e = std::move(it);
-            while (ch->recv(it))
+            while (ch->recv(it)) {
+                settle(it);
                 if (it.is_err && it.pipe < e.pipe) e = std::move(it);
+            }
             throw e.err;
         }
         out = std::move(it.block);
         return true;
+    }
+
+   private:
+    // a block whose states are finished here (DataBlock::complete): its
+    // failure is its pipe's error, ordered like one the pipe sent itself
+    static void settle(Channel::Item &it) {
+        if (it.is_err || !it.block.complete) return;
+        try {
+            complete_block(it.block);
+        } catch (const FQException &e) {
+            it.is_err = true;
+            it.err = e;
+        } catch (const std::exception &e) {
+            it.is_err = true;
+            it.err = FQException(FQ_E_INTERNAL, std::string("Internal Error: ") + e.what());
+        }
     }
 };
 
@@ -315,6 +334,7 @@ StreamRef MergeProcessor::execute() {
                     if (device) ctx.sync();
                     Channel::Item it;
                     b.pipe = (int32_t)pipe;
+                    it.pipe = pipe;
                     it.block = std::move(b);
                     if (!ch->send(std::move(it))) break;
                 }
@@ -395,6 +415,25 @@ StreamRef ProjectionTransform::execute() {
     });
 }
 
+namespace {
+// one partition's partial states still on the device: what the consumer needs
+// to finish them once the query's scans have ended (members in destruction
+// order: the fusion, which may still wait for its scans, before the lease)
+struct PendingPartial {
+    std::shared_ptr<WorkerRes> res;  // the pipe's result slots and queue
+    ScanGroupRef group;
+    std::vector<FunctionRef> funcs;
+    std::unique_ptr<AggFusion> fusion;
+};
+
+// the partial states block's one column (transform_aggregate_partial.rs:64-78)
+Column partial_states(const std::vector<FunctionRef> &funcs) {
+    std::vector<DataValue> rows;
+    for (auto &f : funcs) rows.push_back(DataValue::make_struct(f->accumulate_result()));
+    return Column::host_values(FQ_DT_NULL, std::move(rows));
+}
+}  // namespace
+
 StreamRef AggregatePartialTransform::execute() {
     // this pipe's place in the query's ScanGroup: arrives once, also when it fails
     ScanTicket ticket(group_.get());
@@ -402,22 +441,40 @@ StreamRef AggregatePartialTransform::execute() {
     for (auto &f : funcs_) funcs.push_back(f->clone());
     ExecCtx &ctx = ExecCtx::current();
     StreamRef in = input_->execute();
+    auto fusion = std::make_unique<AggFusion>(ctx, &ticket);
     {
-        AggFusion fusion(ctx, &ticket);
-        FusionGuard guard(ctx, &fusion);
+        FusionGuard guard(ctx, fusion.get());
         DataBlock b;
         while (in->next(b)) {
             if (b.layout) b = materialize(b, ctx);
             for (auto &f : funcs) f->accumulate(b, ctx);
-            fusion.end_block();
+            fusion->end_block();
         }
-        fusion.finish();
     }
-    std::vector<DataValue> rows;
-    for (auto &f : funcs) rows.push_back(DataValue::make_struct(f->accumulate_result()));
     DataBlock out;
     out.schema = schema_;
-    out.columns.push_back(Column::host_values(FQ_DT_NULL, std::move(rows)));
+    if (fusion->finish_deferred()) {
+        // The pipe does not wait: its block carries the states' completion,
+        // which the consumer runs (ChannelStream::next / AggregateFinal) once
+        // the query's scans have ended -- one thread waits on the group's end
+        // event and reads every partition's states, none is woken per pipe.
+        auto p = std::make_shared<PendingPartial>();
+        p->res = ctx.lease();
+        p->group = group_;
+        p->funcs = std::move(funcs);
+        p->fusion = std::move(fusion);
+        out.complete = [p](DataBlock &blk) {
+            p->group->wait_end();
+            p->group->account();
+            p->fusion->replay();
+            p->fusion.reset();
+            blk.columns.push_back(partial_states(p->funcs));
+        };
+    } else {
+        fusion->finish();
+        fusion.reset();
+        out.columns.push_back(partial_states(funcs));
+    }
     return std::make_unique<DataBlockStream>(std::vector<DataBlock>{out});
 }
 
@@ -432,6 +489,7 @@ StreamRef AggregateFinalTransform::execute() {
     std::vector<DataBlock> partials;
     DataBlock b;
     while (in->next(b)) partials.push_back(std::move(b));
+    for (DataBlock &pb : partials) complete_block(pb);  // one pipe: no channel ran it
     for (const DataBlock &pb : partials) {
         if (pb.columns.empty() || !pb.columns[0].host) continue;
         const std::vector<DataValue> &rows = *pb.columns[0].host;

@@ -2269,7 +2269,8 @@ std::string proj_shape_key(const ProjLaunch &P, int32_t tin, int dev) {
                     std::to_string(select_sleep()) + "v" + std::to_string(select_variant()) + "w" + std::to_string(select_lbw()) + "g" + std::to_string(select_debug()) + "n" +
                     std::to_string(select_xcds(dev)) + "r" + std::to_string(fqc::knob(FQ_TUNE_SELECT_BLOCKS_RUN)) + "d" +
                     std::to_string(fqc::knob(FQ_TUNE_SELECT_BLOCKS_DRAW)) + "b" + std::to_string(fqc::knob(FQ_TUNE_SELECT_BLOCKS_ROWS)) +
-                    "t" + std::to_string(fqc::knob(FQ_TUNE_SELECT_NT));
+                    "t" + std::to_string(fqc::knob(FQ_TUNE_SELECT_NT)) + "S" +
+                    std::to_string(fqc::knob(FQ_TUNE_SELECT_BLOCKS_STAGE));
     auto put = [&k](int32_t v) { k.append(reinterpret_cast<const char *>(&v), sizeof v); };
     put(dev);
     put(tin);
@@ -2311,14 +2312,23 @@ std::string proj_shape_key(const ProjLaunch &P, int32_t tin, int dev) {
 // re, the edge's rank, read from the tile's ballots and exclusive group
 // offsets in LDS (double-buffered by tile parity: two barriers per tile).
 // Outputs are written with nontemporal stores (PB_NT; 3.42 -> 3.12 ms per
-// 10 GB, no change for the look-back kernel).  16-byte row-pair loads (two
+// 10 GB, no change for the look-back kernel).  PB_STAGE (round 5): the tile's
+// kept rows go to LDS by in-tile rank first, then consecutive threads write
+// them out as 16-byte row pairs (pb_copy), so every store instruction covers
+// one contiguous span instead of the ~24 kept lanes of a 64-row ballot; the
+// stage holds a whole tile, so 16 rows per thread (32 KB, 4 workgroups per CU)
+// -- in one process, 4 rounds x 8 queries of p1 each
+// (profiles/r05_e_p1_stage_ab.json): 0.730 ms per 3.125e8-row block against
+// 0.760 for the round-4 kernel (32 rows, stores from registers); staged at 32
+// rows (2 workgroups per CU) 0.945, at 8 rows 0.766.  16-byte row-pair loads (two
 // ballots per 128 rows, each lane storing its two kept rows) measured 4.52
 // against 3.10 ms: a wave's stores then interleave and no longer combine.
 std::string gen_project_blocks_kernel(bool bitmap_pred) {
     std::string s = "#define PB_RUN " + std::to_string(fqc::knob(FQ_TUNE_SELECT_BLOCKS_RUN)) + "\n#define PB_DRAW " +
                     std::to_string(fqc::knob(FQ_TUNE_SELECT_BLOCKS_DRAW)) + "\n#define PB_ROWS " +
                     std::to_string(fqc::knob(FQ_TUNE_SELECT_BLOCKS_ROWS)) + "\n#define PB_NT " +
-                    std::to_string(fqc::knob(FQ_TUNE_SELECT_NT) & 1) + "\n";
+                    std::to_string(fqc::knob(FQ_TUNE_SELECT_NT) & 1) + "\n#define PB_STAGE " +
+                    std::to_string(fqc::knob(FQ_TUNE_SELECT_BLOCKS_STAGE)) + "\n";
     s += R"(
 #define PB_THREADS 256
 #define PB_WAVES (PB_THREADS / 64)
@@ -2356,6 +2366,25 @@ __device__ __forceinline__ void pb_scan(u32 *__restrict__ off, int ng, int lane)
     }
     if (lane == 63) off[PB_NE] = incl;
 }
+#if PB_STAGE
+// PB_STAGE: the tile's kept rows staged in LDS by in-tile rank, then written
+// out by consecutive threads: ranks [lo, hi) go to output rows d + rank.  al:
+// every output is 16-byte aligned -- row pairs as one 16-byte store each, the
+// odd row at either end alone; else one row per thread.
+__device__ __forceinline__ void pb_copy(const TIn *__restrict__ st, u32 lo, u32 hi, long long d, int al, int tid,
+                                        const Consts &c, u32 &vflags, const Outs &o) {
+    if (lo >= hi) return;
+    if (!al) {
+        for (u32 r = lo + tid; r < hi; r += PB_THREADS) PB_PUT(st[r], c, vflags, 1u, o, d + (long long)r);
+        return;
+    }
+    const long long p0 = d + lo, p1 = d + hi;
+    if ((p0 & 1) && tid == 0) PB_PUT(st[lo], c, vflags, 1u, o, p0);
+    if ((p1 & 1) && tid == 64) PB_PUT(st[hi - 1], c, vflags, 1u, o, p1 - 1);
+    for (long long q = ((p0 + 1) >> 1) + tid; q < (p1 >> 1); q += PB_THREADS)
+        fq_put2(st[2 * q - d], st[2 * q + 1 - d], c, vflags, o, q);
+}
+#endif
 )";
     const std::string pred8 = bitmap_pred ? "            const bool p = live && ((bm[row >> 6] >> (row & 63)) & 1ull);\n"
                                             "            (void)c;\n"
@@ -2363,8 +2392,13 @@ __device__ __forceinline__ void pb_scan(u32 *__restrict__ off, int ng, int lane)
     s += R"(extern "C" __global__ void __launch_bounds__(PB_THREADS)
 fq_jit_pblocks(const TIn *__restrict__ col, long long n, long long B, Consts c,
     const u64 *__restrict__ bm, Outs o, long long *__restrict__ counts, u32 *__restrict__ fl,
-    unsigned long long *__restrict__ total, u32 *__restrict__ ticket) {
+    unsigned long long *__restrict__ total, u32 *__restrict__ ticket, int al) {
     __shared__ PbShared sh;
+#if PB_STAGE
+    __shared__ TIn stage[PB_TILE];
+#else
+    (void)al;
+#endif
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const long long nb = (n + B - 1) / B;
     u64 kept = 0;  // the workgroup's kept rows
@@ -2436,6 +2470,16 @@ fq_jit_pblocks(const TIn *__restrict__ col, long long n, long long B, Consts c,
         // kept rows before the edge have in-tile ranks < re, the rest >= re
         const long long before = cur * B + (long long)carry;  // output row of in-tile rank 0
         const long long after = (cur + 1) * B - (long long)re;  // ... for ranks past the edge
+#if PB_STAGE
+#pragma unroll
+        for (int k = 0; k < PB_ROWS; ++k) {
+            const u64 b = bal[k * PB_WAVES + wave];
+            if ((b >> lane) & 1ull) stage[off[k * PB_WAVES + wave] + (u32)__popcll(b & lt)] = x[k];
+        }
+        __syncthreads();  // the next tile's stores to stage follow its two barriers
+        pb_copy(stage, 0, re, before, al, tid, c, vflags, o);
+        pb_copy(stage, re, tot, after, al, tid, c, vflags, o);
+#else
 #pragma unroll
         for (int k = 0; k < PB_ROWS; ++k) {
             const u64 b = bal[k * PB_WAVES + wave];
@@ -2444,6 +2488,7 @@ fq_jit_pblocks(const TIn *__restrict__ col, long long n, long long B, Consts c,
                 PB_PUT(x[k], c, vflags, 1u, o, (rank < re ? before : after) + (long long)rank);
             }
         }
+#endif
 )";
     s += R"(
         kept += tot;
@@ -3364,7 +3409,9 @@ fq_status jit_project_blocks(int32_t col_dtype, const ProjLaunch &P, int64_t blo
     // a block longer than the column is the whole column (one block; keeps n + B in range)
     long long n = P.n, B = std::min<int64_t>(block_rows, P.n);
     const int64_t nb = (P.n + B - 1) / B;
-    void *args[] = {&col, &n, &B, &hc, &d_bitmap, &outs, &d_counts, &d_flags, &d_total, &d_ticket};
+    int al = 1;  // PB_STAGE row pairs need 16-byte aligned outputs
+    for (int j = 0; j < P.n_out; ++j) al &= ((uintptr_t)P.out[j] & 15) == 0;
+    void *args[] = {&col, &n, &B, &hc, &d_bitmap, &outs, &d_counts, &d_flags, &d_total, &d_ticket, &al};
     hipFunction_t fn = k.blocks;
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);

@@ -304,11 +304,13 @@ def filter_project(col, pred, values, stream=None):
     return outs
 
 
-def filter_project_blocks(col, block_rows, pred, values, stream=None):
+def filter_project_blocks(col, block_rows, pred, values, stream=None, out_offset=0):
     """FilterTransform -> ProjectionTransform over a stream of DataBlocks of
     block_rows rows (fq_filter_project_blocks): -> ([DeviceColumn of col.len
     rows per output], per-block kept counts as an int64 numpy array).  Block
-    b's kept rows are rows [b * block_rows, + counts[b]) of each output."""
+    b's kept rows are rows [b * block_rows, + counts[b]) of each output.
+    out_offset: each output a view that many 8-byte rows into its buffer
+    (tests: outputs not 16-byte aligned)."""
     require_gpu()
     n_out = len(values)
     exprs = (abi.fq_expr * n_out)()
@@ -319,9 +321,13 @@ def filter_project_blocks(col, block_rows, pred, values, stream=None):
             v.n_steps = 0
             v.out_dtype = col.dtype
         exprs[j] = v
-        outs.append(empty_column(col.len, v.out_dtype))
+        if out_offset:
+            full = empty_column(col.len + out_offset, v.out_dtype)
+            outs.append(DeviceColumn(full.buf, col.len, v.out_dtype, offset=8 * out_offset))
+        else:
+            outs.append(empty_column(col.len, v.out_dtype))
     ptrs = (C.c_void_p * max(n_out, 1))(*[o.ptr for o in outs])
-    nb = (1 if block_rows >= col.len else -(-col.len // block_rows)) if block_rows > 0 and col.len > 0 else 0
+    nb =(1 if block_rows >= col.len else -(-col.len // block_rows)) if block_rows > 0 and col.len > 0 else 0
     counts = Workspace(max(8 * nb, 8))
     ws = Workspace(lib.fq_filter_project_blocks_workspace_bytes())
     n = C.c_int64(0)

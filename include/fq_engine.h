@@ -87,6 +87,8 @@ typedef struct fq_engine_stats {
     uint64_t project_bytes; /* algorithmic bytes: 8 per row read + 8 per kept
                                row per projected column                       */
     double project_ms;      /* summed event time of the launches (FQ_OPT_PROFILE) */
+    double tail_ms;         /* host, FQ_OPT_PROFILE 2: the scans' end event seen ->
+                               the result block (merge + AggregateFinal), summed */
 } fq_engine_stats;
 
 /* device: HIP device ordinal.  Fails with FQ_E_HIP when no GPU is present.

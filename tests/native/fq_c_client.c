@@ -161,11 +161,12 @@ static int bench(int steps, uint64_t total, int warmup) {
            "\"unit\": \"rows/s\", \"ms_per_step\": %.6g, \"scan_launches_per_step\": %.6g, "
            "\"kernel_ms_per_launch\": %.6g, \"bytes_per_launch\": %.6g, \"achieved_hbm_gbps\": %.6g, "
            "\"frac\": %.6g, \"step_over_scans\": %.6g, \"host_ms_per_step\": {\"plan\": %.6g, "
-           "\"first_launch\": %.6g, \"exec\": %.6g}, \"result\": [%llu, %llu, %llu]}\n",
+           "\"first_launch\": %.6g, \"exec\": %.6g, \"tail\": %.6g, \"outside_exec\": %.6g}, "
+           "\"result\": [%llu, %llu, %llu]}\n",
            sql, steps, warmup, (double)total * steps / dt, dt / steps * 1e3, (double)st.scan_launches / steps, kms,
            bytes, gbps, gbps / 8000.0, (dt * 1e3) / (st.scan_ms > 0 ? st.scan_ms : 1.0), st.plan_ms / steps,
-           st.first_launch_ms / steps, st.exec_ms / steps,
-           (unsigned long long)got[0], (unsigned long long)got[1], (unsigned long long)got[2]);
+           st.first_launch_ms / steps, st.exec_ms / steps, st.tail_ms / steps,
+           (dt * 1e3 - st.plan_ms - st.exec_ms) / steps, (unsigned long long)got[0], (unsigned long long)got[1], (unsigned long long)got[2]);
     fq_engine_destroy(e);
     return 0;
 }

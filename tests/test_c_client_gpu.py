@@ -69,20 +69,29 @@ def test_c_client_c3_through_function_handles():
     Function handles (4 aggregator leaves) on a device block of 125,000
     reference blocks (block_rows 10000), then merge_state / merge_result.
     One fused scan per partition (8 per query), the closed form every step, and
-    the scan's roofline fraction within 3 % of the engine's on the same box."""
+    the scan's roofline fraction within 3 % of the engine's on the same box.
+    The two alternate twice and each keeps its better run: a process that
+    starts right after another freed tens of GB of HBM scans 3-4 % slower
+    while the driver reclaims it (profiles/r05_b_host_spread/), and the tests
+    before this one free ~80 GB."""
     import json
     n = 10_000_000_000
-    p = subprocess.run([BIN, "--handles", "5", str(n), "1"], capture_output=True, text=True, timeout=240)
-    assert p.returncode == 0, p.stderr
-    h = json.loads(p.stdout.strip().splitlines()[-1])
     s = n * (n - 1) // 2 % 2**64
-    assert h["result"] == [s // n, n - 1, 0]
-    assert h["scan_launches_per_step"] == 8 and h["bytes_per_launch"] == 8 * n / 8
-    q = subprocess.run([BIN, "--bench", "5", str(n), "1"], capture_output=True, text=True, timeout=240)
-    assert q.returncode == 0, q.stderr
-    e = json.loads(q.stdout.strip().splitlines()[-1])
-    assert h["frac"] >= 0.97 * e["frac"], (h, e)
+    runs = {"--handles": [], "--bench": []}
+    out = ""
+    for _ in range(2):
+        for mode in runs:
+            p = subprocess.run([BIN, mode, "5", str(n), "1"], capture_output=True, text=True, timeout=240)
+            assert p.returncode == 0, p.stderr
+            r = json.loads(p.stdout.strip().splitlines()[-1])
+            assert r["result"] == [s // n, n - 1, 0]
+            assert r["scan_launches_per_step"] == 8 and r["bytes_per_launch"] == 8 * n / 8
+            runs[mode].append(r)
+            out += p.stdout
+    h = max(runs["--handles"], key=lambda r: r["frac"])
+    e = max(runs["--bench"], key=lambda r: r["frac"])
+    assert h["frac"] >= 0.97 * e["frac"], (runs["--handles"], runs["--bench"])
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     if os.path.isdir(os.path.join(root, "gpurun_out")):
         with open(os.path.join(root, "gpurun_out", "c_client_handles_c3.json"), "w") as fh:
-            fh.write(p.stdout + q.stdout)
+            fh.write(out)

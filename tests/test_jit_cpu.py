@@ -185,6 +185,20 @@ def test_project_shapes_compile(i):
     assert ops.jit_stats()["kernels_compiled"] == before + 1
 
 
+@pytest.mark.parametrize("rows", [8, 16, 32])
+@pytest.mark.parametrize("i", [1, 4, 6])
+def test_project_staged_blocks_variant_compiles(i, rows):
+    # FQ_TUNE_SELECT_BLOCKS_STAGE: fq_jit_pblocks stages the kept rows in LDS
+    dt, spec, values = PROJECT_SHAPES[i]
+    try:
+        ops.tune_set("SELECT_BLOCKS_STAGE", 1)
+        ops.tune_set("SELECT_BLOCKS_ROWS", rows)
+        st = ops.project_compile_check(dt, _project_pred(dt, spec), values)
+    finally:
+        ops.tune_reset()
+    assert st == abi.FQ_E_HIP, (st, ops.lib.fq_last_error())
+
+
 def test_project_rejects_bad_arguments():
     assert ops.project_compile_check(abi.DT_UINT32, None, [None]) == abi.FQ_E_UNSUPPORTED
     assert ops.project_compile_check(U64, None, [None] * 9) == abi.FQ_E_INVALID

@@ -40,6 +40,15 @@ def setup_module():
     ops = _ops
 
 
+@pytest.fixture(autouse=True, params=[0, 1], ids=["direct", "staged"])
+def stage(request):
+    """Every test twice: kept rows stored straight from registers, and staged
+    in LDS then written by consecutive threads (FQ_TUNE_SELECT_BLOCKS_STAGE)."""
+    ops.tune_set("SELECT_BLOCKS_STAGE", request.param)
+    yield request.param
+    ops.tune_set("SELECT_BLOCKS_STAGE", 0)
+
+
 def _blocks_of(outs, counts, block_rows):
     """Per output: the list of each block's valid rows (numpy)."""
     res = []
@@ -60,9 +69,9 @@ def _expect_blocks(host, keep, fns, block_rows):
     return exp
 
 
-def _check(host, keep, pred, values, fns, block_rows, col=None):
+def _check(host, keep, pred, values, fns, block_rows, col=None, out_offset=0):
     col = col if col is not None else ops.from_numpy(host)
-    outs, counts = ops.filter_project_blocks(col, block_rows, pred, values)
+    outs, counts = ops.filter_project_blocks(col, block_rows, pred, values, out_offset=out_offset)
     nb = -(-len(host) // block_rows)
     assert len(counts) == nb
     want = [int(keep[b0:b0 + block_rows].sum()) for b0 in range(0, len(host), block_rows)]
@@ -246,6 +255,17 @@ def test_block_column_views(offset, block_rows):
     keep = h % np.uint64(5) < np.uint64(2)
     _check(h, keep, predicate(U64, [("%", 5)], "<", 2), [chain(U64, [("+", 1)])[0], None],
            [lambda k: k + np.uint64(1), lambda k: k], block_rows, col=col)
+
+
+@pytest.mark.parametrize("block_rows", [TILE, 10_000, 10_001])
+def test_block_outputs_not_16_byte_aligned(block_rows):
+    """Outputs 8 bytes into their buffers: the staged writer stores one row per
+    thread instead of 16-byte row pairs; both give the same blocks."""
+    n = 10_000 * 31 + 5
+    host = np.arange(n, dtype=np.uint64) * np.uint64(3)
+    keep = host % np.uint64(8) < np.uint64(3)
+    _check(host, keep, predicate(U64, [("%", 8)], "<", 3), [chain(U64, [("+", 1)])[0], None],
+           [lambda k: k + np.uint64(1), lambda k: k], block_rows, out_offset=1)
 
 
 @pytest.mark.parametrize("n_blocks,block_rows,n_cols", [(3000, 64, 1), (20011, 17, 2), (50000, 8, 3), (1025, 1000, 2)])
