@@ -540,6 +540,13 @@ void Runtime::set_streams(int n) {
         BlockCache::get().add_stream(s);
         shared_.push_back(s);
         shared_mu_.push_back(std::make_unique<std::mutex>());
+        // the fold queue at the device's highest priority: a fold's one
+        // workgroup is dispatched ahead of the running scan's remaining ones
+        int lo = 0, hi = 0;
+        (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+        hipStream_t f;
+        check_hip(hipStreamCreateWithPriority(&f, hipStreamNonBlocking, hi), "hipStreamCreateWithPriority");
+        fold_.push_back(f);
     }
     // existing workers keep their queue; new ones pick round-robin among the first n
     next_shared_ = 0;
@@ -561,6 +568,9 @@ WorkerRes *Runtime::acquire() {
     const size_t q = next_shared_++ % (size_t)active_streams_;
     w->stream = shared_[q];
     w->launch_mu = shared_mu_[q].get();
+    w->fold = fold_[q];
+    check_hip(hipEventCreateWithFlags(&w->scan_done, hipEventDisableTiming), "hipEventCreateWithFlags");
+    check_hip(hipEventCreateWithFlags(&w->fold_done, hipEventDisableTiming), "hipEventCreateWithFlags");
     w->ws_bytes = fq_aggregate_workspace_bytes(0);
     check_hip(alloc_with_reclaim([&] { return hipMalloc(&w->ws, w->ws_bytes); }), "hipMalloc(workspace)");
     // the in-launch finalize's completion counter starts at zero; every
@@ -599,7 +609,10 @@ Runtime::~Runtime() {
     if (device_ == kHostOnly) return;
     (void)hipSetDevice(device_);
     for (auto &s : shared_) (void)hipStreamSynchronize(s);
+    for (auto &s : fold_) (void)hipStreamSynchronize(s);
     for (auto &w : all_) {
+        if (w->scan_done) (void)hipEventDestroy(w->scan_done);
+        if (w->fold_done) (void)hipEventDestroy(w->fold_done);
         if (w->own) {
             (void)hipStreamSynchronize(w->own);
             BlockCache::get().drop_stream(w->own);
@@ -615,6 +628,11 @@ Runtime::~Runtime() {
         BlockCache::get().drop_stream(s);
         (void)hipStreamDestroy(s);
     }
+    for (auto &s : fold_) (void)hipStreamDestroy(s);
+}
+
+void WorkerRes::ws_ready(hipStream_t s) {
+    if (fold_pending) check_hip(hipStreamWaitEvent(s, fold_done, 0), "hipStreamWaitEvent");
 }
 
 uint64_t *WorkerRes::project_result() {

@@ -156,6 +156,13 @@ struct WorkerRes {
     std::mutex *launch_mu = nullptr;  // serialises multi-call enqueues on a shared queue
     void *ws = nullptr;               // fq_aggregate workspace
     size_t ws_bytes = 0;
+    // the shared queue's fold queue (fq_aggregate_split): scans fold their
+    // partials there, beside the next scan.  fold_done marks this worker's
+    // last fold (fold_pending): the workspace's next scan waits for it.
+    hipStream_t fold = nullptr;
+    hipEvent_t scan_done = nullptr, fold_done = nullptr;
+    bool fold_pending = false;
+    void ws_ready(hipStream_t s);  // orders s after this workspace's pending fold
     std::vector<hipEvent_t> events;   // reusable events (timing pairs, completion)
     // Pinned, device-visible result slots: the scan's finalize kernel writes
     // its fq_agg_state straight to host memory, so no copy is queued behind
@@ -224,6 +231,7 @@ class Runtime {
     std::vector<std::unique_ptr<WorkerRes>> all_;
     std::vector<WorkerRes *> free_;
     std::vector<hipStream_t> shared_;  // FQ_OPT_STREAMS queues shared by the pipes
+    std::vector<hipStream_t> fold_;    // each one's fold queue (WorkerRes::fold)
     std::vector<std::unique_ptr<std::mutex>> shared_mu_;
     size_t next_shared_ = 0;
     std::atomic<int> active_streams_{1};

@@ -429,6 +429,7 @@ static fq_agg_state run_scan(const Column &col, int64_t block_rows, const fq_pre
                              uint32_t mask, ExecCtx &ctx) {
     auto out = DeviceBuffer::alloc(sizeof(fq_agg_state), ctx.stream());
     fq_col c = col.abi();
+    ctx.res->ws_ready(ctx.stream());
     check_fq(fq_aggregate(&c, block_rows, pred, value, mask | engine_one_launch(), (fq_agg_state *)out->ptr,
                           ctx.res->ws, ctx.res->ws_bytes, ctx.stream()));
     fq_agg_state st{};
@@ -869,6 +870,7 @@ ScanGroup::~ScanGroup() {
     for (auto &s : queues_) {
         rt_->give_event(s.start);
         rt_->give_event(s.end);
+        rt_->give_event(s.fold_end);
     }
 }
 
@@ -878,6 +880,7 @@ void ScanGroup::before_launch(ExecCtx &ctx) {
         if (s.q == ctx.stream()) return;
     QueueSpan s;
     s.q = ctx.stream();
+    s.fold = ctx.res->fold;
     s.launch_mu = ctx.res->launch_mu;
     if (rt_->profile.load() == 2) {  // the span opens right before this queue's first scan
         s.start = rt_->take_event();
@@ -899,6 +902,11 @@ void ScanGroup::arrive(bool wait) {
     lk.unlock();
     for (QueueSpan &s : qs) {
         std::lock_guard<std::mutex> ql(*s.launch_mu);
+        if (s.fold) {  // the last scan's fold ran beside it (fq_aggregate_split)
+            s.fold_end = rt_->take_event();
+            check_hip(hipEventRecord(s.fold_end, s.fold), "hipEventRecord");
+            check_hip(hipStreamWaitEvent(s.q, s.fold_end, 0), "hipStreamWaitEvent");
+        }
         s.end = rt_->take_event();
         check_hip(hipEventRecord(s.end, s.q), "hipEventRecord");
     }
@@ -989,6 +997,7 @@ void AggFusion::wait_launched() {
     hipEvent_t done = res_->take_event();
     {
         std::lock_guard<std::mutex> lk(*res_->launch_mu);
+        res_->ws_ready(stream_);  // a fold on the fold queue wrote a result too
         check_hip(hipEventRecord(done, stream_), "hipEventRecord");
     }
     hipError_t e = hipEventSynchronize(done);
@@ -1072,16 +1081,30 @@ void AggFusion::end_block() {
         }
         {
             // events and the scan enqueue back to back even when other pipes
-            // share this queue, so an event pair brackets this scan; the scan
-            // folds its partials in its last workgroup (FQ_AGG_ONE_LAUNCH: the
-            // worker's workspace counter was zeroed when it was allocated)
+            // share this queue, so an event pair brackets this scan
             std::lock_guard<std::mutex> lk(*ctx_.res->launch_mu);
+            const fq_pred *pred = g.has_pred ? g.pred.get() : nullptr;
+            const fq_expr *val = g.value.expr.n_steps ? &g.value.expr : nullptr;
+            const uint32_t mask = g.mask | engine_one_launch();
             if (ticket_ && ticket_->group()) ticket_->group()->before_launch(ctx_);
-            if (pairs) check_hip(hipEventRecord(e0, ctx_.stream()), "hipEventRecord");
-            check_fq(fq_aggregate(&c, g.block_rows, g.has_pred ? g.pred.get() : nullptr,
-                                  g.value.expr.n_steps ? &g.value.expr : nullptr, g.mask | engine_one_launch(),
-                                  (fq_agg_state *)dst, ctx_.res->ws, ctx_.res->ws_bytes, ctx_.stream()));
-            if (pairs) check_hip(hipEventRecord(e1, ctx_.stream()), "hipEventRecord");
+            res_->ws_ready(stream_);  // the workspace's last fold has read its partials
+            if (pairs) check_hip(hipEventRecord(e0, stream_), "hipEventRecord");
+            if (!pairs && ticket_ && ticket_->group() && !(mask & FQ_AGG_ONE_LAUNCH) && res_->fold &&
+                fqc::knob(FQ_TUNE_ENGINE_FOLD_STREAM)) {
+                // the fold on the queue's fold queue, beside the next scan; the
+                // group's end waits for the fold queue too (ScanGroup::arrive).
+                // Off by default: 8 scans 11.11 ms against 11.05 with the fold
+                // on the scan's queue, the C3 step 11.62 against 11.56
+                // (profiles/r05_h_scan_fin_ab.json)
+                check_fq(fq_aggregate_split(&c, g.block_rows, pred, val, mask, (fq_agg_state *)dst, res_->ws,
+                                            res_->ws_bytes, stream_, res_->fold, res_->scan_done));
+                check_hip(hipEventRecord(res_->fold_done, res_->fold), "hipEventRecord");
+                res_->fold_pending = true;
+            } else {
+                check_fq(fq_aggregate(&c, g.block_rows, pred, val, mask, (fq_agg_state *)dst, res_->ws,
+                                      res_->ws_bytes, stream_));
+            }
+            if (pairs) check_hip(hipEventRecord(e1, stream_), "hipEventRecord");
         }
         launched_ = true;
         if (const int64_t q0 = ctx_.rt->stats.query_t0.exchange(0))

@@ -317,8 +317,9 @@ class ScanGroup {
    private:
     struct QueueSpan {
         hipStream_t q = nullptr;
+        hipStream_t fold = nullptr;  // q's fold queue: the end waits for it too
         std::mutex *launch_mu = nullptr;
-        hipEvent_t start = nullptr, end = nullptr;
+        hipEvent_t start = nullptr, end = nullptr, fold_end = nullptr;
     };
     Runtime *rt_;
     std::mutex mu_;

@@ -802,15 +802,14 @@ static fq_status plan_scan(const fq_col *col, int64_t block_rows, const fq_pred 
     return FQ_OK;
 }
 
-}  // namespace fqk
-
-extern "C" {
-
-fq_status fq_aggregate(const fq_col *col, int64_t block_rows, const fq_pred *pred, const fq_expr *value,
-                       uint32_t agg_mask, fq_agg_state *d_out, void *d_ws, size_t ws_bytes, void *stream) {
-    using namespace fqk;
+// fq_aggregate / fq_aggregate_split: the scan on `stream`; the fold of its
+// partials on `stream` too, or (fold != nullptr) on `fold` behind `scan_done`
+static fq_status aggregate(const fq_col *col, int64_t block_rows, const fq_pred *pred, const fq_expr *value,
+                           uint32_t agg_mask, fq_agg_state *d_out, void *d_ws, size_t ws_bytes, hipStream_t stream,
+                           hipStream_t fold, hipEvent_t scan_done) {
     if (!col || !d_out || !d_ws) return fqc::fail(FQ_E_INVALID, "fq_aggregate: NULL argument");
     const bool one_launch = (agg_mask & FQ_AGG_ONE_LAUNCH) != 0;
+    if (one_launch && fold) return fqc::fail(FQ_E_INVALID, "fq_aggregate_split: FQ_AGG_ONE_LAUNCH has no fold");
     agg_mask &= ~FQ_AGG_ONE_LAUNCH;
     // one_launch needs the counter behind the partials; without it a
     // pre-counter workspace (kPartialsBytes) still serves the two launches
@@ -848,7 +847,31 @@ fq_status fq_aggregate(const fq_col *col, int64_t block_rows, const fq_pred *pre
         if (s != FQ_OK) return s;
     }
     if (one_launch) return FQ_OK;  // the scan's last workgroup wrote *d_out
+    if (fold) {
+        FQ_HIP_TRY(hipEventRecord(scan_done, stream));
+        FQ_HIP_TRY(hipStreamWaitEvent(fold, scan_done, 0));
+        L.stream = fold;
+    }
     return dispatch_finalize(L, blocks, empty_if_zero, d_out);
+}
+
+}  // namespace fqk
+
+extern "C" {
+
+fq_status fq_aggregate(const fq_col *col, int64_t block_rows, const fq_pred *pred, const fq_expr *value,
+                       uint32_t agg_mask, fq_agg_state *d_out, void *d_ws, size_t ws_bytes, void *stream) {
+    return fqk::aggregate(col, block_rows, pred, value, agg_mask, d_out, d_ws, ws_bytes, (hipStream_t)stream,
+                          nullptr, nullptr);
+}
+
+fq_status fq_aggregate_split(const fq_col *col, int64_t block_rows, const fq_pred *pred, const fq_expr *value,
+                             uint32_t agg_mask, fq_agg_state *d_out, void *d_ws, size_t ws_bytes, void *stream,
+                             void *fold_stream, void *scan_done) {
+    if (!fold_stream || !scan_done) return fqc::fail(FQ_E_INVALID, "fq_aggregate_split: NULL fold stream or event");
+    if (fold_stream == stream) return fqc::fail(FQ_E_INVALID, "fq_aggregate_split: the fold stream is the scan's");
+    return fqk::aggregate(col, block_rows, pred, value, agg_mask, d_out, d_ws, ws_bytes, (hipStream_t)stream,
+                          (hipStream_t)fold_stream, (hipEvent_t)scan_done);
 }
 
 fq_status fq_jit_prepare(const fq_col *col, int64_t block_rows, const fq_pred *pred, const fq_expr *value,

@@ -2315,12 +2315,14 @@ std::string proj_shape_key(const ProjLaunch &P, int32_t tin, int dev) {
 // 10 GB, no change for the look-back kernel).  PB_STAGE (round 5): the tile's
 // kept rows go to LDS by in-tile rank first, then consecutive threads write
 // them out as 16-byte row pairs (pb_copy), so every store instruction covers
-// one contiguous span instead of the ~24 kept lanes of a 64-row ballot; the
-// stage holds a whole tile, so 16 rows per thread (32 KB, 4 workgroups per CU)
-// -- in one process, 4 rounds x 8 queries of p1 each
-// (profiles/r05_e_p1_stage_ab.json): 0.730 ms per 3.125e8-row block against
-// 0.760 for the round-4 kernel (32 rows, stores from registers); staged at 32
-// rows (2 workgroups per CU) 0.945, at 8 rows 0.766.  16-byte row-pair loads (two
+// one contiguous span instead of the ~24 kept lanes of a 64-row ballot.  The
+// stage holds 1/PB_STAGE of a tile (a tile keeping more takes several passes).
+// In one process, 4 rounds x 8 queries of p1 each, ms per 3.125e8-row block
+// (profiles/r05_e_p1_stage_ab.json, r05_g_p1_stage_ab.json): 32 rows per
+// thread with a half-tile stage (32 KB, 4 workgroups per CU, p1's 3/8 kept in
+// one pass) 0.725; a whole-tile stage at 16 rows 0.730-0.734, at 32 rows (2
+// workgroups per CU) 0.945; a quarter-tile stage at 32 rows (two passes)
+// 0.733; the round-4 kernel (32 rows, stores from registers) 0.760-0.769.  16-byte row-pair loads (two
 // ballots per 128 rows, each lane storing its two kept rows) measured 4.52
 // against 3.10 ms: a wave's stores then interleave and no longer combine.
 std::string gen_project_blocks_kernel(bool bitmap_pred) {
@@ -2368,21 +2370,24 @@ __device__ __forceinline__ void pb_scan(u32 *__restrict__ off, int ng, int lane)
 }
 #if PB_STAGE
 // PB_STAGE: the tile's kept rows staged in LDS by in-tile rank, then written
-// out by consecutive threads: ranks [lo, hi) go to output rows d + rank.  al:
-// every output is 16-byte aligned -- row pairs as one 16-byte store each, the
-// odd row at either end alone; else one row per thread.
-__device__ __forceinline__ void pb_copy(const TIn *__restrict__ st, u32 lo, u32 hi, long long d, int al, int tid,
-                                        const Consts &c, u32 &vflags, const Outs &o) {
+// out by consecutive threads: ranks [lo, hi) go to output rows d + rank, rank
+// r in st[r - base].  al: every output is 16-byte aligned -- row pairs as one
+// 16-byte store each, the odd row at either end alone; else one row per thread.
+// The stage holds PB_CAP = PB_TILE / PB_STAGE rows: a tile keeping more takes
+// several passes.
+#define PB_CAP (PB_TILE / PB_STAGE)
+__device__ __forceinline__ void pb_copy(const TIn *__restrict__ st, u32 base, u32 lo, u32 hi, long long d, int al,
+                                        int tid, const Consts &c, u32 &vflags, const Outs &o) {
     if (lo >= hi) return;
     if (!al) {
-        for (u32 r = lo + tid; r < hi; r += PB_THREADS) PB_PUT(st[r], c, vflags, 1u, o, d + (long long)r);
+        for (u32 r = lo + tid; r < hi; r += PB_THREADS) PB_PUT(st[r - base], c, vflags, 1u, o, d + (long long)r);
         return;
     }
-    const long long p0 = d + lo, p1 = d + hi;
-    if ((p0 & 1) && tid == 0) PB_PUT(st[lo], c, vflags, 1u, o, p0);
-    if ((p1 & 1) && tid == 64) PB_PUT(st[hi - 1], c, vflags, 1u, o, p1 - 1);
+    const long long p0 = d + lo, p1 = d + hi, sb = d + base;
+    if ((p0 & 1) && tid == 0) PB_PUT(st[lo - base], c, vflags, 1u, o, p0);
+    if ((p1 & 1) && tid == 64) PB_PUT(st[hi - 1 - base], c, vflags, 1u, o, p1 - 1);
     for (long long q = ((p0 + 1) >> 1) + tid; q < (p1 >> 1); q += PB_THREADS)
-        fq_put2(st[2 * q - d], st[2 * q + 1 - d], c, vflags, o, q);
+        fq_put2(st[2 * q - sb], st[2 * q + 1 - sb], c, vflags, o, q);
 }
 #endif
 )";
@@ -2395,7 +2400,7 @@ fq_jit_pblocks(const TIn *__restrict__ col, long long n, long long B, Consts c,
     unsigned long long *__restrict__ total, u32 *__restrict__ ticket, int al) {
     __shared__ PbShared sh;
 #if PB_STAGE
-    __shared__ TIn stage[PB_TILE];
+    __shared__ TIn stage[PB_CAP];
 #else
     (void)al;
 #endif
@@ -2471,14 +2476,19 @@ fq_jit_pblocks(const TIn *__restrict__ col, long long n, long long B, Consts c,
         const long long before = cur * B + (long long)carry;  // output row of in-tile rank 0
         const long long after = (cur + 1) * B - (long long)re;  // ... for ranks past the edge
 #if PB_STAGE
+        for (u32 base = 0; base < tot; base += PB_CAP) {  // tot is the workgroup's: uniform
+            if (base) __syncthreads();  // the last pass's reads done (the next tile's follow its two barriers)
 #pragma unroll
-        for (int k = 0; k < PB_ROWS; ++k) {
-            const u64 b = bal[k * PB_WAVES + wave];
-            if ((b >> lane) & 1ull) stage[off[k * PB_WAVES + wave] + (u32)__popcll(b & lt)] = x[k];
+            for (int k = 0; k < PB_ROWS; ++k) {
+                const u64 b = bal[k * PB_WAVES + wave];
+                const u32 r = off[k * PB_WAVES + wave] + (u32)__popcll(b & lt) - base;
+                if (((b >> lane) & 1ull) && r < PB_CAP) stage[r] = x[k];
+            }
+            __syncthreads();
+            const u32 hi = tot - base < PB_CAP ? tot : base + PB_CAP;
+            pb_copy(stage, base, base, re < hi ? re : hi, before, al, tid, c, vflags, o);
+            pb_copy(stage, base, re > base ? re : base, hi, after, al, tid, c, vflags, o);
         }
-        __syncthreads();  // the next tile's stores to stage follow its two barriers
-        pb_copy(stage, 0, re, before, al, tid, c, vflags, o);
-        pb_copy(stage, re, tot, after, al, tid, c, vflags, o);
 #else
 #pragma unroll
         for (int k = 0; k < PB_ROWS; ++k) {

@@ -47,7 +47,7 @@ constexpr KnobDef kDefs[FQ_TUNE_COUNT] = {
     {8, 1, 16, 1, false},        // SELECT_BLOCKS_WG_PER_CU
     {1, 0, 4096, 1, false},      // SELECT_BLOCKS_RUN
     {1, 0, 1, 1, false},         // SELECT_BLOCKS_DRAW
-    {16, 8, 32, 1, true},        // SELECT_BLOCKS_ROWS
+    {32, 8, 32, 1, true},        // SELECT_BLOCKS_ROWS
     {1, 0, 3, 1, false},         // SELECT_NT
     {1, 0, 1, 1, false},         // GPART_DBUF
     {8, 4, 8, 4, false},         // GPART_ROWS8
@@ -58,7 +58,8 @@ constexpr KnobDef kDefs[FQ_TUNE_COUNT] = {
     {1000, 0, 100000, 1, false}, // POOL_SPIN_US
     {1, 0, 1, 1, false},         // SCAN_FIN
     {0, 0, 1, 1, false},         // ENGINE_ONE_LAUNCH
-    {1, 0, 1, 1, false},         // SELECT_BLOCKS_STAGE
+    {2, 0, 4, 1, true},          // SELECT_BLOCKS_STAGE
+    {0, 0, 1, 1, false},         // ENGINE_FOLD_STREAM
 };
 
 std::atomic<int64_t> g_val[FQ_TUNE_COUNT] = {};

@@ -16,6 +16,7 @@ LIB_PATH = os.path.normpath(os.path.join(_HERE, "..", "lib", "libfq_amd.so"))
 GPU_SYMBOLS = [
     "fq_abi_version", "fq_last_error", "fq_device_count", "fq_fill_numbers_u64", "fq_fill_value",
     "fq_fill_splitmix64", "fq_aggregate_workspace_bytes", "fq_aggregate_workspace_init", "fq_aggregate",
+    "fq_aggregate_split",
     "fq_arith_result_type", "fq_arith", "fq_compare", "fq_filter_workspace_bytes",
     "fq_filter_compact", "fq_state_merge", "fq_jit_config", "fq_jit_get_stats", "fq_jit_prepare",
     "fq_group_table_bytes", "fq_group_table_init", "fq_group_aggregate", "fq_group_table_count",
@@ -66,6 +67,8 @@ _protos = {
     "fq_aggregate_workspace_init": (C.c_int32, [vp, C.c_size_t, vp]),
     "fq_aggregate": (C.c_int32, [P(abi.fq_col), C.c_int64, P(abi.fq_pred), P(abi.fq_expr),
                                  C.c_uint32, vp, vp, C.c_size_t, vp]),
+    "fq_aggregate_split": (C.c_int32, [P(abi.fq_col), C.c_int64, P(abi.fq_pred), P(abi.fq_expr),
+                                       C.c_uint32, vp, vp, C.c_size_t, vp, vp, vp]),
     "fq_arith_result_type": (C.c_int32, [C.c_int32, C.c_int32, C.c_int32, P(C.c_int32)]),
     "fq_arith": (C.c_int32, [C.c_int32, P(abi.fq_col), P(abi.fq_value), P(abi.fq_col),
                              P(abi.fq_value), P(abi.fq_col), vp, vp]),

@@ -249,6 +249,17 @@ fq_status fq_aggregate_workspace_init(void *d_ws, size_t ws_bytes, void *stream)
 fq_status fq_aggregate(const fq_col *col, int64_t block_rows, const fq_pred *pred,
                        const fq_expr *value, uint32_t agg_mask, fq_agg_state *d_out,
                        void *d_ws, size_t ws_bytes, void *stream);
+/* fq_aggregate with the fold on another stream: the scan on `stream`, then
+ * `scan_done` (the caller's hipEvent_t) recorded behind it, `fold_stream` made
+ * to wait for it and the fold launched there -- the next launch on `stream`
+ * does not wait for the fold, which runs beside it.  The partials stay in the
+ * workspace until the fold has run: order the workspace's next use after
+ * fold_stream's work so far (e.g. an event recorded on fold_stream), and read
+ * *d_out after it.  FQ_AGG_ONE_LAUNCH (no fold) is refused.                 */
+fq_status fq_aggregate_split(const fq_col *col, int64_t block_rows, const fq_pred *pred,
+                             const fq_expr *value, uint32_t agg_mask, fq_agg_state *d_out,
+                             void *d_ws, size_t ws_bytes, void *stream, void *fold_stream,
+                             void *scan_done);
 
 /* ---- ArithmeticFunction::eval (data_array_arithmetic.rs:14-55) ----
  * Exactly one of {lhs, lhs_scalar} and one of {rhs, rhs_scalar} is non-NULL.
@@ -428,7 +439,7 @@ fq_status fq_jit_prepare(const fq_col *col, int64_t block_rows, const fq_pred *p
 #define FQ_TUNE_SELECT_BLOCKS_WG_PER_CU 25 /* block-stream filter+projection workgroups per CU, 8 (1..16) */
 #define FQ_TUNE_SELECT_BLOCKS_RUN 26  /* block-stream filter+projection: blocks per run, 1 (0 = one static run per workgroup) */
 #define FQ_TUNE_SELECT_BLOCKS_DRAW 27 /* block-stream runs drawn from a counter (1) or dealt round-robin (0), 1 */
-#define FQ_TUNE_SELECT_BLOCKS_ROWS 28 /* block-stream rows per thread per tile, 16 (8/16/32; tile = 256 x rows) */
+#define FQ_TUNE_SELECT_BLOCKS_ROWS 28 /* block-stream rows per thread per tile, 32 (8/16/32; tile = 256 x rows) */
 #define FQ_TUNE_SELECT_NT 29          /* nontemporal output stores: bit 0 block-stream, bit 1 contiguous kernel; 1 */
 #define FQ_TUNE_GPART_DBUF 30        /* GROUP BY partition pass (4-byte rows): tile state double-buffered, 2 barriers per tile: 1 (0/1) */
 #define FQ_TUNE_GPART_ROWS8 31       /* GROUP BY partition + bins passes, 8-byte rows: rows per thread per tile, 8 (4/8) */
@@ -442,8 +453,12 @@ fq_status fq_jit_prepare(const fq_col *col, int64_t block_rows, const fq_pred *p
 #define FQ_TUNE_ENGINE_ONE_LAUNCH 38 /* the engine's scans pass FQ_AGG_ONE_LAUNCH: 0 (0/1; the separate finalize
                                        launch measured faster, profiles/r05_b_scan_fin_ab.json) */
 #define FQ_TUNE_SELECT_BLOCKS_STAGE 39 /* block-stream filter+projection: kept rows staged in LDS, written by
-                                        consecutive threads (16-byte row pairs when aligned): 1 (0/1) */
-#define FQ_TUNE_COUNT 40
+                                        consecutive threads (16-byte row pairs when aligned), the stage
+                                        1/S of a tile (passes as needed): S = 2 (0 = off, 1/2/4) */
+#define FQ_TUNE_ENGINE_FOLD_STREAM 40 /* the engine's scans fold their partials on a second queue
+                                       (fq_aggregate_split) beside the next scan: 0 (0/1; measured
+                                       slower) */
+#define FQ_TUNE_COUNT 41
 /* FQ_E_INVALID for an unknown knob or a value outside the knob's set */
 fq_status fq_tune_set(int32_t knob, int64_t value);
 /* the knob's current value; -1 for an unknown knob */

@@ -185,13 +185,14 @@ def test_project_shapes_compile(i):
     assert ops.jit_stats()["kernels_compiled"] == before + 1
 
 
-@pytest.mark.parametrize("rows", [8, 16, 32])
+@pytest.mark.parametrize("rows,stage", [(8, 1), (16, 1), (16, 2), (32, 2), (32, 4), (16, 0)])
 @pytest.mark.parametrize("i", [1, 4, 6])
-def test_project_staged_blocks_variant_compiles(i, rows):
+def test_project_staged_blocks_variant_compiles(i, rows, stage):
     # FQ_TUNE_SELECT_BLOCKS_STAGE: fq_jit_pblocks stages the kept rows in LDS
+    # (a 1/stage-tile buffer, passes as needed; 0 = stores from registers)
     dt, spec, values = PROJECT_SHAPES[i]
     try:
-        ops.tune_set("SELECT_BLOCKS_STAGE", 1)
+        ops.tune_set("SELECT_BLOCKS_STAGE", stage)
         ops.tune_set("SELECT_BLOCKS_ROWS", rows)
         st = ops.project_compile_check(dt, _project_pred(dt, spec), values)
     finally:

@@ -40,13 +40,16 @@ def setup_module():
     ops = _ops
 
 
-@pytest.fixture(autouse=True, params=[0, 1], ids=["direct", "staged"])
+@pytest.fixture(autouse=True, params=[0, 1, 4], ids=["direct", "staged", "staged_quarter"])
 def stage(request):
-    """Every test twice: kept rows stored straight from registers, and staged
-    in LDS then written by consecutive threads (FQ_TUNE_SELECT_BLOCKS_STAGE)."""
+    """Every test three times: kept rows stored straight from registers, staged
+    in LDS (a whole tile) then written by consecutive threads, and staged
+    through a quarter-tile buffer -- a tile keeping more than a quarter of its
+    rows takes several passes (FQ_TUNE_SELECT_BLOCKS_STAGE)."""
+    before = ops.tune_get("SELECT_BLOCKS_STAGE")
     ops.tune_set("SELECT_BLOCKS_STAGE", request.param)
     yield request.param
-    ops.tune_set("SELECT_BLOCKS_STAGE", 0)
+    ops.tune_set("SELECT_BLOCKS_STAGE", before)
 
 
 def _blocks_of(outs, counts, block_rows):

@@ -2,14 +2,15 @@
 fq_jit_pblocks store variants (round 5): kept rows stored straight from the
 lanes' registers (FQ_TUNE_SELECT_BLOCKS_STAGE 0, the round-4 kernel) against
 staged in LDS by in-tile rank and written by consecutive threads as 16-byte row
-pairs (STAGE 1), at 8 / 16 / 32 rows per thread (the stage holds a whole tile:
-256 x rows x 8 B of LDS, which caps the workgroups per CU).  Configs alternate
+pairs (STAGE S: a stage of 1/S of the tile, 256 x rows x 8 / S bytes of LDS,
+which caps the workgroups per CU; a tile keeping more rows than the stage
+holds takes several passes), at 8 / 16 / 32 rows per thread.  Configs alternate
 round by round in one process (a fresh process after another freed its HBM runs
 slower, profiles/r05_b_host_spread/).  Every config's first query is checked
 against the closed forms (kept rows + both columns' wrapping sums), every timed
 one by its kept count.
 
-python tools/p1_stage_ab.py [rounds] [steps] > gpurun_out/p1_stage_ab.json"""
+python tools/p1_stage_ab.py [rounds] [steps] [S:R ...] > gpurun_out/p1_stage_ab.json"""
 import json
 import os
 import statistics
@@ -27,7 +28,9 @@ from fq_amd.engine import Engine  # noqa: E402
 ROUNDS = int(sys.argv[1]) if len(sys.argv) > 1 else 4
 STEPS = int(sys.argv[2]) if len(sys.argv) > 2 else 8
 N = 10_000_000_000
-CONFIGS = [(0, 32), (1, 32), (1, 16), (1, 8), (0, 16)]
+# (FQ_TUNE_SELECT_BLOCKS_STAGE, FQ_TUNE_SELECT_BLOCKS_ROWS); argv[3:] overrides as S:R pairs
+CONFIGS = ([tuple(int(x) for x in a.split(":")) for a in sys.argv[3:]] or
+           [(0, 32), (1, 16), (2, 16), (2, 32), (4, 32)])
 
 
 def main():
