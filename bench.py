@@ -158,6 +158,29 @@ def log(rank, *a):
         print("[bench]", *a, file=sys.stderr, flush=True)
 
 
+def settle(step, seconds, world, backend):
+    """Untimed steps for about `seconds` before the warmup.  For a few seconds
+    after a process frees HBM the driver clears it in the background, and a
+    scan that overlaps the clearing runs 3-4 % slower: in a fresh process, the
+    first second after another process freed 80 GB, the first three after 160 GB
+    (profiles/r05_j_reclaim_probe/; the GPU test suite before a bench frees more).
+    At world > 1 every step is a collective, so every rank runs the same count:
+    the most any rank needs for `seconds` at its first step's pace.  -> steps run."""
+    if seconds <= 0:
+        return 0
+    t0 = time.perf_counter()
+    step()
+    one = max(time.perf_counter() - t0, 1e-4)
+    n = max(int(seconds / one), 1)
+    if world > 1:
+        t = torch.tensor([n], dtype=torch.int64, device="cuda" if backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        n = int(t.item())
+    for _ in range(n - 1):
+        step()
+    return n
+
+
 def latest_pmc_traffic(kernel_substr, query, rows_per_launch):
     """(HBM bytes per launch scaled to rows_per_launch, provenance) from the
     most recently MEASURED committed rocprofv3 --pmc summary of this query
@@ -397,6 +420,7 @@ def run_project_engine(args, rank, world, local):
                     kept += b.rows
         return (kept, s1, s2) if check else kept, blocks
 
+    settled = settle(step, args.settle_s, world, args.dist_backend)
     for _ in range(max(args.warmup, 1)):
         got, blocks = step(check=True)
         if got != expect:
@@ -441,7 +465,8 @@ def run_project_engine(args, rank, world, local):
         traffic, traffic_src = latest_pmc_traffic("fq_jit_pblocks", "p1", rows_per_launch)
         out = {
             "metric": METRIC, "value": value, "unit": "rows/s", "n_gpus": world, "ranks_seen": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3,
+            "steps": args.steps, "warmup": args.warmup, "settle": {"s": args.settle_s, "steps": settled},
+            "ms_per_step": dt / args.steps * 1e3,
             "higher_is_better": True, "scaling": "strong" if args.rows_total else "weak", "vs_baseline": None,
             "vs_baseline_ref": "no published reference number for this query",
             "dtype": "u64", "data": "synthetic: system.numbers_mt iota column (u64), resident in HBM before timing",
@@ -825,6 +850,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--settle-s", type=float, default=3.0,
+                    help="untimed steps for about this long before the warmup: HBM that earlier processes freed is "
+                         "cleared by the driver in the background for a few seconds, and scans that overlap it run "
+                         "3-4 %% slower (0 = none)")
     ap.add_argument("--query", default="c3", choices=sorted(list(QUERIES) + ["p1"]))
     ap.add_argument("--rows-per-gpu", type=float, default=1e10)
     ap.add_argument("--rows-total", type=float, default=None,
@@ -999,6 +1028,7 @@ def main():
             return all(np.array_equal(g, exp[:, c]) for c, g in enumerate(got))
         return got == expect
 
+    settled = settle(step, args.settle_s, world, args.dist_backend)
     for _ in range(max(args.warmup, 1)):
         res = step()
     expect = closed_form(args.query, n_total)
@@ -1061,6 +1091,7 @@ def main():
             "ranks_seen": ranks_seen,
             "steps": args.steps,
             "warmup": args.warmup,
+            "settle": {"s": args.settle_s, "steps": settled},
             "ms_per_step": dt / args.steps * 1e3,
             "higher_is_better": True,
             "scaling": "strong" if args.rows_total else "weak",
