@@ -241,7 +241,8 @@ def host_split(st, steps, ms_per_step, world):
     Python)."""
     out = {"plan": st["plan_ms"] / steps, "first_launch": st["first_launch_ms"] / steps, "exec": st["exec_ms"] / steps}
     if world == 1:
-        out.update({"tail": st["tail_ms"] / steps, "outside_exec": ms_per_step - (st["plan_ms"] + st["exec_ms"]) / steps})
+        out.update({"tail": st["tail_ms"] / steps, "tail_states": st["complete_ms"] / steps,
+                    "outside_exec": ms_per_step - (st["plan_ms"] + st["exec_ms"]) / steps})
     if world > 1:
         part, xch, fin = (st[k] / steps for k in ("partial_ms", "exchange_ms", "final_ms"))
         out.update({"partial": part, "exchange": xch, "final": fin,

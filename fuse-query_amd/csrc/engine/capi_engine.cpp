@@ -680,6 +680,7 @@ fq_status fq_engine_get_stats(fq_engine *e, fq_engine_stats *out) {
     out->exec_ms = (double)e->rt->stats.exec_ns.load() * 1e-6;
     out->first_launch_ms = (double)e->rt->stats.first_launch_ns.load() * 1e-6;
     out->tail_ms = (double)e->rt->stats.tail_ns.load() * 1e-6;
+    out->complete_ms = (double)e->rt->stats.complete_ns.load() * 1e-6;
     out->partial_ms = (double)e->rt->stats.partial_ns.load() * 1e-6;
     out->exchange_ms = (double)e->rt->stats.exchange_ns.load() * 1e-6;
     out->final_ms = (double)e->rt->stats.final_ns.load() * 1e-6;
@@ -707,6 +708,7 @@ fq_status fq_engine_reset_stats(fq_engine *e) {
     e->rt->stats.exec_ns = 0;
     e->rt->stats.first_launch_ns = 0;
     e->rt->stats.tail_ns = 0;
+    e->rt->stats.complete_ns = 0;
     e->rt->stats.partial_ns = 0;
     e->rt->stats.exchange_ns = 0;
     e->rt->stats.final_ns = 0;

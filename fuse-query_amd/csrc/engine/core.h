@@ -148,6 +148,7 @@ struct EngineStats {
     // (ScanGroup::wait_end); fq_engine_execute adds (exec end - it) to tail_ns
     std::atomic<int64_t> scan_end_seen{0};
     std::atomic<uint64_t> tail_ns{0};
+    std::atomic<uint64_t> complete_ns{0};  // of tail_ns: the partitions' states read (DataBlock::complete)
 };
 
 struct WorkerRes {

@@ -1152,13 +1152,20 @@ void AggFusion::replay() {
             rt_->stats.scan_ns += (uint64_t)((double)ms * 1e6);
     }
     keepalive_.clear();
+    // each device slot (pinned host memory the scans' folds wrote) read once:
+    // the aggregators of one fused scan share it
+    std::vector<fq_agg_state> slots(nslots_);
+    std::vector<char> have(nslots_, 0);
     for (Entry &en : log_) {
         if (en.has_error) throw en.err;
         fq_agg_state st = en.st;
         if (en.slot != (size_t)-1) {
-            const uint64_t blocks = en.st.blocks;
-            memcpy(&st, slot_host(en.slot), sizeof st);
-            st.blocks = blocks;
+            if (!have[en.slot]) {
+                memcpy(&slots[en.slot], slot_host(en.slot), sizeof(fq_agg_state));
+                have[en.slot] = 1;
+            }
+            st = slots[en.slot];
+            st.blocks = en.st.blocks;
         }
         en.agg->accumulate_summary(st);
     }

@@ -315,11 +315,11 @@ StreamRef MergeProcessor::execute() {
     cs->ch = std::make_shared<Channel>();
     cs->ch->cap = list_.size();
     cs->ch->live = (int)list_.size();
-    for (size_t pipe = 0; pipe < list_.size(); ++pipe) {
+    auto task = [&](size_t pipe) {
         std::shared_ptr<Channel> ch = cs->ch;
         ProcessorRef in = list_[pipe];
         const bool own = own_queues_;
-        rt->pool.submit([in, ch, rt, pipe, own]() {
+        return [in, ch, rt, pipe, own]() {
             try {
                 ExecCtx ctx(rt, own);
                 StreamRef s = in->execute();
@@ -352,8 +352,16 @@ StreamRef MergeProcessor::execute() {
                 ch->send_error(std::move(it));
             }
             ch->done();
-        });
-    }
+        };
+    };
+    // Pipes whose output is one block (AggregatePartial: it enqueues its scans
+    // and hands over a deferred block without waiting) can run on this thread:
+    // pipe 0 then enqueues its first scan without waiting for a pool thread to
+    // wake, while the pool starts the others.  The channel holds every pipe's
+    // block, so nothing here waits for the consumer.
+    const size_t first = inline_first_ ? 1 : 0;
+    for (size_t pipe = first; pipe < list_.size(); ++pipe) rt->pool.submit(task(pipe));
+    if (inline_first_) task(0)();
     return cs;
 }
 
@@ -420,6 +428,7 @@ namespace {
 // to finish them once the query's scans have ended (members in destruction
 // order: the fusion, which may still wait for its scans, before the lease)
 struct PendingPartial {
+    Runtime *rt = nullptr;
     std::shared_ptr<WorkerRes> res;  // the pipe's result slots and queue
     ScanGroupRef group;
     std::vector<FunctionRef> funcs;
@@ -459,16 +468,20 @@ StreamRef AggregatePartialTransform::execute() {
         // the query's scans have ended -- one thread waits on the group's end
         // event and reads every partition's states, none is woken per pipe.
         auto p = std::make_shared<PendingPartial>();
+        p->rt = ctx.rt;
         p->res = ctx.lease();
         p->group = group_;
         p->funcs = std::move(funcs);
         p->fusion = std::move(fusion);
         out.complete = [p](DataBlock &blk) {
             p->group->wait_end();
+            const int64_t t0 = now_ns();
             p->group->account();
             p->fusion->replay();
             p->fusion.reset();
             blk.columns.push_back(partial_states(p->funcs));
+            if (p->rt->profile.load(std::memory_order_relaxed) == 2)
+                p->rt->stats.complete_ns += (uint64_t)(now_ns() - t0);
         };
     } else {
         fusion->finish();
@@ -1057,7 +1070,9 @@ void Pipeline::add_simple_transform(const std::function<ProcessorRef()> &f) {
 void Pipeline::merge_processor() {
     if (pipes_.empty()) throw_internal("Can't merge processor when the last pipe is empty");
     if (pipes_.back().size() > 1) {
-        auto p = std::make_shared<MergeProcessor>(own_queues_);
+        // AggregatePartial pipes emit one block each (pipeline_builder.rs:73-95)
+        const bool one_block = dynamic_cast<AggregatePartialTransform *>(pipes_.back()[0].get()) != nullptr;
+        auto p = std::make_shared<MergeProcessor>(own_queues_, one_block);
         for (auto &x : pipes_.back()) p->connect_to(x);
         pipes_.push_back({p});
     }

@@ -167,7 +167,8 @@ class EmptyProcessor : public IProcessor {  // processor_empty.rs:14-49
 
 class MergeProcessor : public IProcessor {  // processor_merge.rs:16-94
    public:
-    explicit MergeProcessor(bool own_queues = false) : own_queues_(own_queues) {}
+    explicit MergeProcessor(bool own_queues = false, bool inline_first = false)
+        : own_queues_(own_queues), inline_first_(inline_first) {}
     std::string name() const override { return "MergeProcessor"; }
     void connect_to(ProcessorRef input) override { list_.push_back(std::move(input)); }
     StreamRef execute() override;
@@ -175,7 +176,8 @@ class MergeProcessor : public IProcessor {  // processor_merge.rs:16-94
 
    private:
     std::vector<ProcessorRef> list_;
-    bool own_queues_;  // each input pipe on its worker's private device queue
+    bool own_queues_;     // each input pipe on its worker's private device queue
+    bool inline_first_;   // pipe 0 runs on the calling thread (one-block pipes)
 };
 
 class SourceTransform : public IProcessor {  // transform_source.rs:14-53

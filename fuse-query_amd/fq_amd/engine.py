@@ -40,7 +40,8 @@ class fq_engine_stats(C.Structure):
                 ("exchange_rounds", C.c_uint64), ("exchange_bytes", C.c_uint64),
                 ("cached_block_bytes", C.c_uint64), ("cached_workspace_bytes", C.c_uint64),
                 ("project_launches", C.c_uint64), ("project_rows", C.c_uint64), ("project_kept", C.c_uint64),
-                ("project_bytes", C.c_uint64), ("project_ms", C.c_double), ("tail_ms", C.c_double)]
+                ("project_bytes", C.c_uint64), ("project_ms", C.c_double), ("tail_ms", C.c_double),
+                ("complete_ms", C.c_double)]
 
 
 class fq_device_block(C.Structure):

@@ -89,6 +89,8 @@ typedef struct fq_engine_stats {
     double project_ms;      /* summed event time of the launches (FQ_OPT_PROFILE) */
     double tail_ms;         /* host, FQ_OPT_PROFILE 2: the scans' end event seen ->
                                the result block (merge + AggregateFinal), summed */
+    double complete_ms;     /* of tail_ms: reading the partitions' states into their
+                               aggregators (AggregatePartial's deferred blocks)  */
 } fq_engine_stats;
 
 /* device: HIP device ordinal.  Fails with FQ_E_HIP when no GPU is present.

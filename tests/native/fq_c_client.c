@@ -137,6 +137,11 @@ static int bench(int steps, uint64_t total, int warmup) {
     const uint64_t sum = (uint64_t)((unsigned __int128)total * (total - 1) / 2);
     const uint64_t expect[3] = {sum / total, total - 1, 0};
     uint64_t got[3];
+    /* untimed steps for ~2 s first: HBM another process freed is cleared by
+     * the driver in the background for a few seconds and slows the scans
+     * (bench.py settle, profiles/r05_j_reclaim_probe/) */
+    int settle = 0;
+    for (const double s0 = now_s(); now_s() - s0 < 2.0; ++settle) c3_row(e, sql, got);
     for (int i = 0; i < (warmup > 0 ? warmup : 1); ++i) c3_row(e, sql, got);
     CHECK(memcmp(got, expect, sizeof got) == 0, "C3 = %llu %llu %llu", (unsigned long long)got[0],
           (unsigned long long)got[1], (unsigned long long)got[2]);
@@ -158,14 +163,14 @@ static int bench(int steps, uint64_t total, int warmup) {
     const double gbps = bytes / (kms * 1e-3) / 1e9;
     printf("{\"path\": \"fq_c_client (C host, libfq_amd.so + /opt/rocm libamdhip64, no torch): fq_engine_execute "
            "of the C3 statement\", \"workload\": \"%s\", \"steps\": %d, \"warmup\": %d, \"value\": %.6g, "
-           "\"unit\": \"rows/s\", \"ms_per_step\": %.6g, \"scan_launches_per_step\": %.6g, "
+           "\"settle_steps\": %d, \"unit\": \"rows/s\", \"ms_per_step\": %.6g, \"scan_launches_per_step\": %.6g, "
            "\"kernel_ms_per_launch\": %.6g, \"bytes_per_launch\": %.6g, \"achieved_hbm_gbps\": %.6g, "
            "\"frac\": %.6g, \"step_over_scans\": %.6g, \"host_ms_per_step\": {\"plan\": %.6g, "
-           "\"first_launch\": %.6g, \"exec\": %.6g, \"tail\": %.6g, \"outside_exec\": %.6g}, "
+           "\"first_launch\": %.6g, \"exec\": %.6g, \"tail\": %.6g, \"tail_states\": %.6g, \"outside_exec\": %.6g}, "
            "\"result\": [%llu, %llu, %llu]}\n",
-           sql, steps, warmup, (double)total * steps / dt, dt / steps * 1e3, (double)st.scan_launches / steps, kms,
+           sql, steps, warmup, (double)total * steps / dt, settle, dt / steps * 1e3, (double)st.scan_launches / steps, kms,
            bytes, gbps, gbps / 8000.0, (dt * 1e3) / (st.scan_ms > 0 ? st.scan_ms : 1.0), st.plan_ms / steps,
-           st.first_launch_ms / steps, st.exec_ms / steps, st.tail_ms / steps,
+           st.first_launch_ms / steps, st.exec_ms / steps, st.tail_ms / steps, st.complete_ms / steps,
            (dt * 1e3 - st.plan_ms - st.exec_ms) / steps, (unsigned long long)got[0], (unsigned long long)got[1], (unsigned long long)got[2]);
     fq_engine_destroy(e);
     return 0;
@@ -216,8 +221,13 @@ static int handles(int steps, uint64_t total, int warmup) {
     uint64_t got[3] = {0, 0, 0};
     int bad = 0;
     double t0 = 0;
-    for (int it = 0; it < (warmup > 0 ? warmup : 1) + steps; ++it) {
-        if (it == (warmup > 0 ? warmup : 1)) {
+    /* untimed: the warmup steps, and steps for at least ~2 s (as --bench) */
+    const int w = warmup > 0 ? warmup : 1;
+    const double s0 = now_s();
+    int first = -1;
+    for (int it = 0; first < 0 || it < first + steps; ++it) {
+        if (first < 0 && it >= w && now_s() - s0 >= 2.0) {
+            first = it;
             CHECK(fq_engine_reset_stats(e) == FQ_OK, "reset stats");
             t0 = now_s();
         }

@@ -28,9 +28,18 @@ from fq_amd.engine import Engine  # noqa: E402
 ROUNDS = int(sys.argv[1]) if len(sys.argv) > 1 else 4
 STEPS = int(sys.argv[2]) if len(sys.argv) > 2 else 8
 N = 10_000_000_000
-# (FQ_TUNE_SELECT_BLOCKS_STAGE, FQ_TUNE_SELECT_BLOCKS_ROWS); argv[3:] overrides as S:R pairs
-CONFIGS = ([tuple(int(x) for x in a.split(":")) for a in sys.argv[3:]] or
-           [(0, 32), (1, 16), (2, 16), (2, 32), (4, 32)])
+# configs: S:R = (FQ_TUNE_SELECT_BLOCKS_STAGE, FQ_TUNE_SELECT_BLOCKS_ROWS), or any
+# knobs as KNOB=V[,KNOB=V...] (abi.TUNE names); argv[3:] overrides the default set
+
+
+def parse_config(a):
+    if "=" in a:
+        return tuple((k.upper(), int(v)) for k, v in (kv.split("=") for kv in a.split(",")))
+    st, rows = (int(x) for x in a.split(":"))
+    return (("SELECT_BLOCKS_STAGE", st), ("SELECT_BLOCKS_ROWS", rows))
+
+
+CONFIGS = [parse_config(a) for a in (sys.argv[3:] or ["0:32", "1:16", "2:16", "2:32", "4:32"])]
 
 
 def main():
@@ -56,8 +65,9 @@ def main():
     res = {c: {"step_ms": [], "kernel_ms": [], "frac": []} for c in CONFIGS}
     for r in range(ROUNDS):
         for c in (CONFIGS if r % 2 == 0 else CONFIGS[::-1]):
-            ops.tune_set("SELECT_BLOCKS_STAGE", c[0])
-            ops.tune_set("SELECT_BLOCKS_ROWS", c[1])
+            ops.tune_reset()
+            for k, v in c:
+                ops.tune_set(k, v)
             got = step(check=(r == 0))
             if r == 0 and got != expect:
                 raise SystemExit("PARITY FAILURE %r: got %r expected %r" % (c, got, expect))
@@ -79,8 +89,8 @@ def main():
     ops.tune_reset()
     eng.close()
     out = {"rounds": ROUNDS, "steps": STEPS, "workload": sql, "configs": {}}
-    for (s, rows), v in res.items():
-        out["configs"]["stage%d_rows%d" % (s, rows)] = {
+    for c, v in res.items():
+        out["configs"][",".join("%s=%d" % kv for kv in c)] = {
             "step_ms_median": statistics.median(v["step_ms"]), "kernel_ms_median": statistics.median(v["kernel_ms"]),
             "frac_median": statistics.median(v["frac"]), "kernel_ms_all": v["kernel_ms"], "step_ms_all": v["step_ms"]}
     print(json.dumps(out, indent=1))
