@@ -350,6 +350,12 @@ StreamRef MergeProcessor::execute() {
                 it.pipe = pipe;
                 it.err = FQException(FQ_E_INTERNAL, std::string("Internal Error: ") + e.what());
                 ch->send_error(std::move(it));
+            } catch (...) {  // every pipe reports done, or the consumer waits for it forever
+                Channel::Item it;
+                it.is_err = true;
+                it.pipe = pipe;
+                it.err = FQException(FQ_E_INTERNAL, "Internal Error: unknown exception in a pipe");
+                ch->send_error(std::move(it));
             }
             ch->done();
         };
