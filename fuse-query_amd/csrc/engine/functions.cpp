@@ -889,6 +889,12 @@ void ScanGroup::before_launch(ExecCtx &ctx) {
     queues_.push_back(s);
 }
 
+void ScanGroup::note_fold(hipStream_t q) {
+    std::lock_guard<std::mutex> lk(mu_);
+    for (QueueSpan &s : queues_)
+        if (s.q == q) s.folded = true;
+}
+
 void ScanGroup::arrive(bool wait) {
     std::unique_lock<std::mutex> lk(mu_);
     if (--left_ > 0) {
@@ -902,7 +908,7 @@ void ScanGroup::arrive(bool wait) {
     lk.unlock();
     for (QueueSpan &s : qs) {
         std::lock_guard<std::mutex> ql(*s.launch_mu);
-        if (s.fold) {  // the last scan's fold ran beside it (fq_aggregate_split)
+        if (s.fold && s.folded) {  // the last scan's fold ran beside it (fq_aggregate_split)
             s.fold_end = rt_->take_event();
             check_hip(hipEventRecord(s.fold_end, s.fold), "hipEventRecord");
             check_hip(hipStreamWaitEvent(s.q, s.fold_end, 0), "hipStreamWaitEvent");
@@ -1100,6 +1106,7 @@ void AggFusion::end_block() {
                                             res_->ws_bytes, stream_, res_->fold, res_->scan_done));
                 check_hip(hipEventRecord(res_->fold_done, res_->fold), "hipEventRecord");
                 res_->fold_pending = true;
+                ticket_->group()->note_fold(stream_);
             } else {
                 check_fq(fq_aggregate(&c, g.block_rows, pred, val, mask, (fq_agg_state *)dst, res_->ws,
                                       res_->ws_bytes, stream_));

@@ -305,6 +305,8 @@ class ScanGroup {
     ScanGroup &operator=(const ScanGroup &) = delete;
     // a launch on ctx's queue follows (called under the queue's launch lock)
     void before_launch(ExecCtx &ctx);
+    // that launch folded its partials on the queue's fold queue (same lock)
+    void note_fold(hipStream_t q);
     // a pipe has enqueued everything it will.  The last one to arrive records
     // an end event on every queue the group launched on; with `wait` the
     // others block until it has (a failing pipe leaves without waiting).
@@ -317,7 +319,8 @@ class ScanGroup {
    private:
     struct QueueSpan {
         hipStream_t q = nullptr;
-        hipStream_t fold = nullptr;  // q's fold queue: the end waits for it too
+        hipStream_t fold = nullptr;  // q's fold queue: the end waits for it when `folded`
+        bool folded = false;         // a scan on q folded there (fq_aggregate_split)
         std::mutex *launch_mu = nullptr;
         hipEvent_t start = nullptr, end = nullptr, fold_end = nullptr;
     };
