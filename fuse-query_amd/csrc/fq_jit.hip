@@ -2628,6 +2628,15 @@ fq_jit_pbits(const TIn *__restrict__ col, long long n, Consts c, u64 *__restrict
 // drawing and the class advances.  (Classes read from the hardware XCC_ID, as
 // in round 2, could leave a class with no resident workgroup: its tiles would
 // never be drawn and every look-back past them would hit the poll bound.)
+// That argument needs a resident workgroup in every class.  Beside other
+// kernels (the engine's LIMIT pipes run one of these per private queue) a
+// launch may get fewer resident workgroups than classes: their tiles wait on
+// undrawn tiles of absent classes until the other kernels free CUs, and two
+// such launches can hold each other's CUs until the poll bound (seen once in
+// round 5: "the offset look-back did not complete", tests/test_memory_gpu.py).
+// So PS_XCD is off by default (FQ_TUNE_SELECT_VARIANT 0): one counter, and the
+// lowest unfinished tile always has every predecessor drawn by a resident
+// workgroup.
 // Status words are 64-bit agent-scope atomics: flag in the top 2 bits, count
 // below.  The look-back is bounded: after ~2^20 polls the kernel flags an
 // error (fl[1] bit 31) and moves on, so a wave can never spin forever.

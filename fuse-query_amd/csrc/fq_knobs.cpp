@@ -31,7 +31,7 @@ constexpr KnobDef kDefs[FQ_TUNE_COUNT] = {
     {1, 0, 2, 1, false},         // GROUP_WAVE_RUNS
     {160, 0, 512, 1, false},     // GROUP_CLUSTER
     {1, 0, 1, 1, false},         // GROUP_CHUNKED
-    {1, 0, 1, 1, false},         // SELECT_VARIANT
+    {0, 0, 1, 1, false},         // SELECT_VARIANT
     {0, 0, 1, 1, false},         // SELECT_DEBUG
     {1, 1, 8, 1, true},          // SELECT_LBW
     {8, 1, 16, 1, false},        // SELECT_WG_PER_CU

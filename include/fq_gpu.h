@@ -423,7 +423,8 @@ fq_status fq_jit_prepare(const fq_col *col, int64_t block_rows, const fq_pred *p
 #define FQ_TUNE_GROUP_WAVE_RUNS 9    /* wave-uniform key runs merged across the wave: 1 (0..2)    */
 #define FQ_TUNE_GROUP_CLUSTER 10     /* clustered row layout threshold (key changes/wave): 160 (0..512) */
 #define FQ_TUNE_GROUP_CHUNKED 11     /* contiguous tile runs per workgroup: 1 (0/1)               */
-#define FQ_TUNE_SELECT_VARIANT 12    /* filter+projection: per-class ticket counters, 1 (0/1)    */
+#define FQ_TUNE_SELECT_VARIANT 12    /* filter+projection: per-class ticket counters, 0 (0/1; 1 is faster
+                                        alone on the GPU but can stall beside concurrent kernels, fq_jit.hip) */
 #define FQ_TUNE_SELECT_DEBUG 13      /* filter+projection: count phase cycles (fq_tune_select_counters), 0 (0/1) */
 #define FQ_TUNE_SELECT_LBW 14        /* look-back status words per lane per poll, 1 (1/2/4/8)     */
 #define FQ_TUNE_SELECT_WG_PER_CU 15  /* filter+projection workgroups per CU, 8 (1..16)            */

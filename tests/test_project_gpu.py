@@ -25,6 +25,16 @@ def setup_module():
     ops = _ops
 
 
+@pytest.fixture(autouse=True, params=[0, 1], ids=["one_ticket", "xcd_tickets"])
+def ticket_variant(request):
+    """Every test with the default single ticket counter and with the per-XCD
+    counters (FQ_TUNE_SELECT_VARIANT 1)."""
+    before = ops.tune_get("SELECT_VARIANT")
+    ops.tune_set("SELECT_VARIANT", request.param)
+    yield request.param
+    ops.tune_set("SELECT_VARIANT", before)
+
+
 def _u(x):
     return np.asarray(x, dtype=np.uint64)
 
