@@ -540,13 +540,7 @@ void Runtime::set_streams(int n) {
         BlockCache::get().add_stream(s);
         shared_.push_back(s);
         shared_mu_.push_back(std::make_unique<std::mutex>());
-        // the fold queue at the device's highest priority: a fold's one
-        // workgroup is dispatched ahead of the running scan's remaining ones
-        int lo = 0, hi = 0;
-        (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
-        hipStream_t f;
-        check_hip(hipStreamCreateWithPriority(&f, hipStreamNonBlocking, hi), "hipStreamCreateWithPriority");
-        fold_.push_back(f);
+        fold_.push_back(nullptr);  // created on first use (fold_queue)
     }
     // existing workers keep their queue; new ones pick round-robin among the first n
     next_shared_ = 0;
@@ -568,9 +562,7 @@ WorkerRes *Runtime::acquire() {
     const size_t q = next_shared_++ % (size_t)active_streams_;
     w->stream = shared_[q];
     w->launch_mu = shared_mu_[q].get();
-    w->fold = fold_[q];
-    check_hip(hipEventCreateWithFlags(&w->scan_done, hipEventDisableTiming), "hipEventCreateWithFlags");
-    check_hip(hipEventCreateWithFlags(&w->fold_done, hipEventDisableTiming), "hipEventCreateWithFlags");
+    w->queue_index = q;
     w->ws_bytes = fq_aggregate_workspace_bytes(0);
     check_hip(alloc_with_reclaim([&] { return hipMalloc(&w->ws, w->ws_bytes); }), "hipMalloc(workspace)");
     // the in-launch finalize's completion counter starts at zero; every
@@ -609,7 +601,8 @@ Runtime::~Runtime() {
     if (device_ == kHostOnly) return;
     (void)hipSetDevice(device_);
     for (auto &s : shared_) (void)hipStreamSynchronize(s);
-    for (auto &s : fold_) (void)hipStreamSynchronize(s);
+    for (auto &s : fold_)
+        if (s) (void)hipStreamSynchronize(s);
     for (auto &w : all_) {
         if (w->scan_done) (void)hipEventDestroy(w->scan_done);
         if (w->fold_done) (void)hipEventDestroy(w->fold_done);
@@ -628,7 +621,30 @@ Runtime::~Runtime() {
         BlockCache::get().drop_stream(s);
         (void)hipStreamDestroy(s);
     }
-    for (auto &s : fold_) (void)hipStreamDestroy(s);
+    for (auto &s : fold_)
+        if (s) (void)hipStreamDestroy(s);
+}
+
+// The fold queue of w's shared queue, at the device's highest priority (a
+// fold's one workgroup is dispatched ahead of the running scan's remaining
+// ones), and w's two events for it -- made only when the engine folds there
+// (FQ_TUNE_ENGINE_FOLD_STREAM): an idle stream per queue slowed the LIMIT
+// pipes' private queues (profiles/r05_t_limit_bisect.txt).
+hipStream_t Runtime::fold_queue(WorkerRes *w) {
+    if (w->fold) return w->fold;
+    {
+        std::lock_guard<std::mutex> lk(mu_);
+        hipStream_t &f = fold_[w->queue_index];
+        if (!f) {
+            int lo = 0, hi = 0;
+            (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+            check_hip(hipStreamCreateWithPriority(&f, hipStreamNonBlocking, hi), "hipStreamCreateWithPriority");
+        }
+        w->fold = f;
+    }
+    check_hip(hipEventCreateWithFlags(&w->scan_done, hipEventDisableTiming), "hipEventCreateWithFlags");
+    check_hip(hipEventCreateWithFlags(&w->fold_done, hipEventDisableTiming), "hipEventCreateWithFlags");
+    return w->fold;
 }
 
 void WorkerRes::ws_ready(hipStream_t s) {

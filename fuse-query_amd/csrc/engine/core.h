@@ -160,9 +160,10 @@ struct WorkerRes {
     // the shared queue's fold queue (fq_aggregate_split): scans fold their
     // partials there, beside the next scan.  fold_done marks this worker's
     // last fold (fold_pending): the workspace's next scan waits for it.
-    hipStream_t fold = nullptr;
+    hipStream_t fold = nullptr;       // Runtime::fold_queue, on first use
     hipEvent_t scan_done = nullptr, fold_done = nullptr;
     bool fold_pending = false;
+    size_t queue_index = 0;           // which shared queue (Runtime::shared_)
     void ws_ready(hipStream_t s);  // orders s after this workspace's pending fold
     std::vector<hipEvent_t> events;   // reusable events (timing pairs, completion)
     // Pinned, device-visible result slots: the scan's finalize kernel writes
@@ -212,6 +213,8 @@ class Runtime {
     void release(WorkerRes *w);
     void set_streams(int n);
     int active_streams() const { return active_streams_; }
+    // w's shared queue's fold queue (fq_aggregate_split), made on first use
+    hipStream_t fold_queue(WorkerRes *w);
     // timing-capable events shared across pipe threads (ScanGroup)
     hipEvent_t take_event();
     void give_event(hipEvent_t e);

@@ -880,7 +880,6 @@ void ScanGroup::before_launch(ExecCtx &ctx) {
         if (s.q == ctx.stream()) return;
     QueueSpan s;
     s.q = ctx.stream();
-    s.fold = ctx.res->fold;
     s.launch_mu = ctx.res->launch_mu;
     if (rt_->profile.load() == 2) {  // the span opens right before this queue's first scan
         s.start = rt_->take_event();
@@ -889,10 +888,13 @@ void ScanGroup::before_launch(ExecCtx &ctx) {
     queues_.push_back(s);
 }
 
-void ScanGroup::note_fold(hipStream_t q) {
+void ScanGroup::note_fold(hipStream_t q, hipStream_t fold) {
     std::lock_guard<std::mutex> lk(mu_);
     for (QueueSpan &s : queues_)
-        if (s.q == q) s.folded = true;
+        if (s.q == q) {
+            s.fold = fold;
+            s.folded = true;
+        }
 }
 
 void ScanGroup::arrive(bool wait) {
@@ -1095,8 +1097,9 @@ void AggFusion::end_block() {
             if (ticket_ && ticket_->group()) ticket_->group()->before_launch(ctx_);
             res_->ws_ready(stream_);  // the workspace's last fold has read its partials
             if (pairs) check_hip(hipEventRecord(e0, stream_), "hipEventRecord");
-            if (!pairs && ticket_ && ticket_->group() && !(mask & FQ_AGG_ONE_LAUNCH) && res_->fold &&
-                fqc::knob(FQ_TUNE_ENGINE_FOLD_STREAM)) {
+            if (!pairs && ticket_ && ticket_->group() && !(mask & FQ_AGG_ONE_LAUNCH) &&
+                fqc::knob(FQ_TUNE_ENGINE_FOLD_STREAM) && stream_ == res_->stream) {
+                rt_->fold_queue(res_);
                 // the fold on the queue's fold queue, beside the next scan; the
                 // group's end waits for the fold queue too (ScanGroup::arrive).
                 // Off by default: 8 scans 11.11 ms against 11.05 with the fold
@@ -1106,7 +1109,7 @@ void AggFusion::end_block() {
                                             res_->ws_bytes, stream_, res_->fold, res_->scan_done));
                 check_hip(hipEventRecord(res_->fold_done, res_->fold), "hipEventRecord");
                 res_->fold_pending = true;
-                ticket_->group()->note_fold(stream_);
+                ticket_->group()->note_fold(stream_, res_->fold);
             } else {
                 check_fq(fq_aggregate(&c, g.block_rows, pred, val, mask, (fq_agg_state *)dst, res_->ws,
                                       res_->ws_bytes, stream_));

@@ -306,7 +306,7 @@ class ScanGroup {
     // a launch on ctx's queue follows (called under the queue's launch lock)
     void before_launch(ExecCtx &ctx);
     // that launch folded its partials on the queue's fold queue (same lock)
-    void note_fold(hipStream_t q);
+    void note_fold(hipStream_t q, hipStream_t fold);
     // a pipe has enqueued everything it will.  The last one to arrive records
     // an end event on every queue the group launched on; with `wait` the
     // others block until it has (a failing pipe leaves without waiting).
