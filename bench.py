@@ -978,27 +978,21 @@ def main():
         raise SystemExit("bench.py: --gpus %d but the exchange spans %d ranks" % (args.gpus, ranks_seen))
 
     # One step on one GPU is what a host binding the C ABI does
-    # (INTEGRATION.md): fq_engine_execute, then the one result row's values
-    # through fq_result_value -- no Python Result object (its ~50 us of
-    # interpreter work per step is harness, not query).
+    # (INTEGRATION.md): fq_engine_execute_row -- execute, the one result row's
+    # values, the result freed, in one call; no Python Result object (its ~50 us
+    # of interpreter work per step is harness, not query).
     import ctypes as C
 
     from fq_amd._lib import check as _check
     from fq_amd._lib import lib as _lib
     sql_b = sql.encode()
-    val = abi.fq_value()
+    row_buf = (abi.fq_value * 8)()
+    ncols = C.c_int32(0)
 
     def c_row():
-        out = C.c_void_p()
-        _check(_lib.fq_engine_execute(eng.h, sql_b, C.byref(out)))
-        try:
-            row = []
-            for c in range(_lib.fq_result_num_columns(out)):
-                _check(_lib.fq_result_value(out, 0, c, C.byref(val)))
-                row.append(val.bits if val.is_some else None)
-            return row
-        finally:
-            _lib.fq_result_free(out)
+        # one call: execute, the row's values, the result freed (fq_engine_execute_row)
+        _check(_lib.fq_engine_execute_row(eng.h, sql_b, row_buf, 8, C.byref(ncols)))
+        return [v.bits if v.is_some else None for v in row_buf[:ncols.value]]
 
     def c_groups():
         # GROUP BY result columns as numpy arrays (fq_result_values), rows in key order

@@ -28,7 +28,7 @@ ENGINE_SYMBOLS = [
     "fq_engine_execute_final", "fq_engine_get_stats", "fq_engine_reset_stats", "fq_result_num_rows",
     "fq_result_num_columns", "fq_result_column_name", "fq_result_column_type", "fq_result_value",
     "fq_result_text", "fq_result_free", "fq_result_mysql_type", "fq_result_values", "fq_engine_partial_state_bytes",
-    "fq_engine_execute_blocks", "fq_block_stream_next", "fq_block_stream_free",
+    "fq_engine_execute_blocks", "fq_block_stream_next", "fq_block_stream_free", "fq_engine_execute_row",
 ]
 
 
@@ -57,6 +57,7 @@ _protos = {
     "fq_engine_release_numbers": (C.c_int32, [C.c_void_p]),
     "fq_engine_trim_memory": (C.c_int32, [C.c_void_p]),
     "fq_engine_execute": (C.c_int32, [C.c_void_p, C.c_char_p, P(C.c_void_p)]),
+    "fq_engine_execute_row": (C.c_int32, [C.c_void_p, C.c_char_p, P(abi.fq_value), C.c_int32, P(C.c_int32)]),
     "fq_engine_explain": (C.c_int32, [C.c_void_p, C.c_char_p, C.c_char_p, C.c_size_t, P(C.c_size_t)]),
     "fq_engine_execute_partial": (C.c_int32, [C.c_void_p, C.c_char_p, C.c_int32, C.c_int32, C.c_void_p,
                                               C.c_size_t, P(C.c_size_t)]),
@@ -297,6 +298,13 @@ class Engine:
         out = C.c_void_p()
         check(lib.fq_engine_execute(self.h, sql.encode(), C.byref(out)))
         return Result(out)
+
+    def execute_row(self, sql, cap=16):
+        """fq_engine_execute_row: a one-row statement's values (fq_value list)."""
+        row = (abi.fq_value * cap)()
+        n = C.c_int32(0)
+        check(lib.fq_engine_execute_row(self.h, sql.encode() if isinstance(sql, str) else sql, row, cap, C.byref(n)))
+        return [row[i] for i in range(min(n.value, cap))]
 
     def execute_blocks(self, sql, rank=0, world=1):
         """The row pipeline's output blocks, left in HBM (BlockStream); rank of

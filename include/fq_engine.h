@@ -186,6 +186,12 @@ void fq_block_stream_free(fq_block_stream *s);
 fq_status fq_engine_get_stats(fq_engine *e, fq_engine_stats *out);
 fq_status fq_engine_reset_stats(fq_engine *e);
 
+/* A statement whose result is one row (an ungrouped aggregate): its values in
+ * one call -- fq_engine_execute, the row's first min(cap, columns) values into
+ * row[], *ncols = its columns, the result freed.  Fails with FQ_E_INVALID when
+ * the statement returns another number of rows.                             */
+fq_status fq_engine_execute_row(fq_engine *e, const char *sql, fq_value *row, int32_t cap, int32_t *ncols);
+
 /* results */
 int64_t fq_result_num_rows(const fq_result *r);
 int32_t fq_result_num_columns(const fq_result *r);

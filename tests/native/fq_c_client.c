@@ -119,10 +119,13 @@ static double now_s(void) {
 }
 
 static void c3_row(fq_engine *e, const char *sql, uint64_t out[3]) {
-    fq_result *r = NULL;
-    CHECK(fq_engine_execute(e, sql, &r) == FQ_OK, "execute: %s", fq_last_error());
-    for (int c = 0; c < 3; ++c) out[c] = value_u64(r, c);
-    fq_result_free(r);
+    fq_value row[3];
+    int32_t n = 0;
+    CHECK(fq_engine_execute_row(e, sql, row, 3, &n) == FQ_OK && n == 3, "execute_row: %s", fq_last_error());
+    for (int c = 0; c < 3; ++c) {
+        CHECK(row[c].is_some && row[c].dtype == FQ_DT_UINT64, "column %d is not a UInt64 value", c);
+        out[c] = row[c].bits;
+    }
 }
 
 static int bench(int steps, uint64_t total, int warmup) {

@@ -102,6 +102,27 @@ def test_explain_aggregate_pipeline_shape():
 AGGS_C3 = [(abi.AGG_SUM, None), (abi.AGG_COUNT, None), (abi.AGG_MAX, None), (abi.AGG_MIN, None)]
 
 
+def test_execute_row_equals_the_result_api():
+    """fq_engine_execute_row: one call for a one-row statement -- the same
+    values and types as fq_engine_execute + fq_result_value; a statement with
+    another number of rows fails with FQ_E_INVALID and the row count."""
+    from fq_amd.engine import FQError
+    from fq_amd.expr import from_bits
+    for sql in ("SELECT sum(number)/count(number), max(number), min(number) FROM system.numbers_mt(1000003)",
+                "SELECT max(number), count(number) FROM system.numbers_mt(100000) WHERE number % 7 = 3",
+                "SELECT sum(number * 1.5), min(number - 5) FROM system.numbers_mt(777)"):
+        r = q(sql)
+        row = E.execute_row(sql)
+        assert len(r.rows) == 1 and len(row) == len(r.types)
+        for v, want, t in zip(row, r.rows[0], r.types):
+            assert v.is_some and v.dtype == t
+            assert from_bits(v.bits, t) == want
+    assert len(E.execute_row("SELECT count(number), sum(number), max(number) FROM system.numbers_mt(10)", cap=2)) == 2
+    with pytest.raises(FQError) as ei:
+        E.execute_row("SELECT number FROM system.numbers_mt(5)")
+    assert ei.value.status == abi.FQ_E_INVALID and "returned 5 rows" in str(ei.value)
+
+
 @pytest.mark.parametrize("n", [1, 7, 8, 9, 16, 10000, 79999, 80000, 100001, 1000000, 12345679])
 def test_c3_matches_oracle(n):
     r = q("SELECT sum(number)/count(number), max(number), min(number), count(number), sum(number) "
