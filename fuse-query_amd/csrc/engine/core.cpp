@@ -615,6 +615,8 @@ Runtime::~Runtime() {
         for (auto ev : w->events) (void)hipEventDestroy(ev);
         for (auto *c : w->slot_chunks) (void)hipHostFree(c);
         if (w->project_res) (void)hipHostFree(w->project_res);
+        if (w->project_ws) (void)hipFree(w->project_ws);
+        if (w->project_hres) (void)hipHostFree(w->project_hres);
     }
     for (auto ev : events_) (void)hipEventDestroy(ev);
     for (auto &s : shared_) {
@@ -649,6 +651,21 @@ hipStream_t Runtime::fold_queue(WorkerRes *w) {
 
 void WorkerRes::ws_ready(hipStream_t s) {
     if (fold_pending) check_hip(hipStreamWaitEvent(s, fold_done, 0), "hipStreamWaitEvent");
+}
+
+void WorkerRes::project_resident() {
+    if (project_ws) return;
+    const size_t bytes = fq_filter_project_blocks_workspace_bytes();
+    void *h = nullptr, *d = nullptr;
+    check_hip(hipHostMalloc(&h, 2 * sizeof(uint64_t), hipHostMallocMapped | hipHostMallocCoherent),
+              "hipHostMalloc(projection result)");
+    check_hip(hipHostGetDevicePointer(&d, h, 0), "hipHostGetDevicePointer");
+    void *ws = nullptr;
+    check_hip(alloc_with_reclaim([&] { return hipMalloc(&ws, bytes); }), "hipMalloc(projection workspace)");
+    check_hip(hipMemset(ws, 0, bytes), "hipMemset(projection workspace)");  // the kernel keeps it zeroed
+    project_hres = (uint64_t *)h;
+    project_dres = (uint64_t *)d;
+    project_ws = ws;
 }
 
 uint64_t *WorkerRes::project_result() {

@@ -175,6 +175,11 @@ struct WorkerRes {
     // launch (fq_filter_project_blocks_async; one in flight per worker)
     uint64_t *project_res = nullptr;
     uint64_t *project_result();
+    // fq_filter_project_blocks_launch: this worker's workspace, kept zeroed by
+    // the kernel, and the two result words it writes (host memory, mapped)
+    void *project_ws = nullptr;
+    uint64_t *project_hres = nullptr, *project_dres = nullptr;
+    void project_resident();  // makes the three on first use
     hipEvent_t take_event();
     void give_event(hipEvent_t e) { events.push_back(e); }
 };

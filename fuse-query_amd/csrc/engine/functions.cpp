@@ -748,8 +748,10 @@ static bool project_blocks(const DataBlock &b, const Column &c, const fq_pred *p
     layout->block_rows = B;
     layout->n_blocks = n == 0 ? 0 : nb;
     layout->counts = DeviceBuffer::alloc((size_t)std::max<int64_t>(nb, 1) * 8, ctx.stream());
-    auto ws = DeviceBuffer::alloc(fq_filter_project_blocks_workspace_bytes(), ctx.stream());
-    uint64_t *res = ctx.res->project_result();
+    // the worker's own workspace, kept zeroed by the kernel, and result words
+    // the kernel writes to host memory: nothing but the kernel on the queue
+    ctx.res->project_resident();
+    uint64_t *res = ctx.res->project_hres;
     const bool prof = ctx.rt->profile.load();
     hipEvent_t e0 = ctx.res->take_event(), e1 = ctx.res->take_event();
     fq_col ic = c.abi();
@@ -764,9 +766,10 @@ static bool project_blocks(const DataBlock &b, const Column &c, const fq_pred *p
     hipEvent_t done = ctx.res->take_event();
     {
         std::lock_guard<std::mutex> lk(*ctx.res->launch_mu);
-        st = fq_filter_project_blocks_async(&ic, B, pred, exprs.data(), (int32_t)exprs.size(), ptrs.data(),
-                                            (int64_t *)layout->counts->ptr, res, ws->ptr, ws->bytes,
-                                            prof ? e0 : nullptr, prof ? e1 : nullptr, ctx.stream());
+        st = fq_filter_project_blocks_launch(&ic, B, pred, exprs.data(), (int32_t)exprs.size(), ptrs.data(),
+                                             (int64_t *)layout->counts->ptr, res, ctx.res->project_dres,
+                                             ctx.res->project_ws, fq_filter_project_blocks_workspace_bytes(),
+                                             prof ? e0 : nullptr, prof ? e1 : nullptr, ctx.stream());
         if (st == FQ_OK) check_hip(hipEventRecord(done, ctx.stream()), "hipEventRecord");  // after the result copy
     }
     if (st == FQ_OK) {

@@ -566,10 +566,15 @@ fq_status fq_filter_project(const fq_col *col, const fq_pred *pred, const fq_exp
 
 size_t fq_filter_project_blocks_workspace_bytes(void) { return 3 * sizeof(uint64_t); }  // total, flags, ticket
 
-fq_status fq_filter_project_blocks_async(const fq_col *col, int64_t block_rows, const fq_pred *pred,
-                                         const fq_expr *values, int32_t n_out, void *const *d_out, int64_t *d_counts,
-                                         uint64_t *h_result, void *d_ws, size_t ws_bytes, void *ev_start,
-                                         void *ev_end, void *stream) {
+namespace {
+// fq_filter_project_blocks_async / _launch: d_result == nullptr -> the
+// workspace is zeroed before the kernel and the two result words copied after
+// it; else the workspace is zero already and the kernel's last workgroup
+// writes d_result and re-zeroes it.
+fq_status project_blocks_enqueue(const fq_col *col, int64_t block_rows, const fq_pred *pred, const fq_expr *values,
+                                 int32_t n_out, void *const *d_out, int64_t *d_counts, uint64_t *h_result,
+                                 uint64_t *d_result, void *d_ws, size_t ws_bytes, void *ev_start, void *ev_end,
+                                 void *stream) {
     using namespace fqk;
     static_assert(FQ_PROJECT_MIN_BLOCK_ROWS == kProjectBlockTile, "the ABI's minimum block is the kernel's tile");
     if (!h_result) return fqc::fail(FQ_E_INVALID, "fq_filter_project_blocks: NULL result words");
@@ -590,9 +595,11 @@ fq_status fq_filter_project_blocks_async(const fq_col *col, int64_t block_rows, 
         return fqc::fail(FQ_E_INVALID, "fq_filter_project_blocks: workspace too small");
     uint64_t *const total = (uint64_t *)d_ws;
     uint32_t *const flags = (uint32_t *)(total + 1);
+    uint32_t *const ticket = (uint32_t *)(total + 2), *const done = ticket + 1;
     hipStream_t st = P.stream;
     const int64_t nb = block_rows >= n ? 1 : (n + block_rows - 1) / block_rows;
-    FQ_HIP_TRY(hipMemsetAsync(d_ws, 0, fq_filter_project_blocks_workspace_bytes(), st));
+    const bool resident = d_result != nullptr && P.pred.kind != FQ_PRED_NONE;
+    if (!d_result || !resident) FQ_HIP_TRY(hipMemsetAsync(d_ws, 0, fq_filter_project_blocks_workspace_bytes(), st));
     if (ev_start) FQ_HIP_TRY(hipEventRecord((hipEvent_t)ev_start, st));
     if (P.pred.kind == FQ_PRED_NONE) {  // every row kept: outputs in place, counts = block lengths
         if ((s = jit_project_map(col->dtype, P, flags + 1)) != FQ_OK) return s;
@@ -602,14 +609,42 @@ fq_status fq_filter_project_blocks_async(const fq_col *col, int64_t block_rows, 
         if (ev_end) FQ_HIP_TRY(hipEventRecord((hipEvent_t)ev_end, st));
         FQ_HIP_TRY(hipMemcpyAsync(&h_result[1], flags, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
         h_result[0] = (uint64_t)n;
+        // the map path used the flag words: zero again for a resident workspace
+        if (d_result) FQ_HIP_TRY(hipMemsetAsync(d_ws, 0, fq_filter_project_blocks_workspace_bytes(), st));
     } else {
         if ((s = jit_project_blocks(col->dtype, P, block_rows, P.pred.kind == FQ_PRED_BITMAP ? P.pred.bitmap : nullptr,
-                                    d_counts, flags, total, (uint32_t *)(total + 2))) != FQ_OK)
+                                    d_counts, flags, total, ticket, resident ? done : nullptr,
+                                    resident ? d_result : nullptr)) != FQ_OK)
             return s;
         if (ev_end) FQ_HIP_TRY(hipEventRecord((hipEvent_t)ev_end, st));
-        FQ_HIP_TRY(hipMemcpyAsync(h_result, total, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+        if (!resident) FQ_HIP_TRY(hipMemcpyAsync(h_result, total, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     }
     return FQ_OK;
+}
+}  // namespace
+
+fq_status fq_filter_project_blocks_async(const fq_col *col, int64_t block_rows, const fq_pred *pred,
+                                         const fq_expr *values, int32_t n_out, void *const *d_out, int64_t *d_counts,
+                                         uint64_t *h_result, void *d_ws, size_t ws_bytes, void *ev_start,
+                                         void *ev_end, void *stream) {
+    return project_blocks_enqueue(col, block_rows, pred, values, n_out, d_out, d_counts, h_result, nullptr, d_ws,
+                                  ws_bytes, ev_start, ev_end, stream);
+}
+
+fq_status fq_filter_project_blocks_workspace_init(void *d_ws, size_t ws_bytes, void *stream) {
+    if (!d_ws || ws_bytes < fq_filter_project_blocks_workspace_bytes())
+        return fqc::fail(FQ_E_INVALID, "fq_filter_project_blocks_workspace_init: workspace too small");
+    FQ_HIP_TRY(hipMemsetAsync(d_ws, 0, fq_filter_project_blocks_workspace_bytes(), (hipStream_t)stream));
+    return FQ_OK;
+}
+
+fq_status fq_filter_project_blocks_launch(const fq_col *col, int64_t block_rows, const fq_pred *pred,
+                                          const fq_expr *values, int32_t n_out, void *const *d_out, int64_t *d_counts,
+                                          uint64_t *h_result, uint64_t *d_result, void *d_ws, size_t ws_bytes,
+                                          void *ev_start, void *ev_end, void *stream) {
+    if (!d_result) return fqc::fail(FQ_E_INVALID, "fq_filter_project_blocks_launch: NULL device result address");
+    return project_blocks_enqueue(col, block_rows, pred, values, n_out, d_out, d_counts, h_result, d_result, d_ws,
+                                  ws_bytes, ev_start, ev_end, stream);
 }
 
 fq_status fq_filter_project_blocks_result(const uint64_t *h_result, int64_t *out_len) {

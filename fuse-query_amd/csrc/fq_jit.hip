@@ -2397,7 +2397,8 @@ __device__ __forceinline__ void pb_copy(const TIn *__restrict__ st, u32 base, u3
     s += R"(extern "C" __global__ void __launch_bounds__(PB_THREADS)
 fq_jit_pblocks(const TIn *__restrict__ col, long long n, long long B, Consts c,
     const u64 *__restrict__ bm, Outs o, long long *__restrict__ counts, u32 *__restrict__ fl,
-    unsigned long long *__restrict__ total, u32 *__restrict__ ticket, int al) {
+    unsigned long long *__restrict__ total, u32 *__restrict__ ticket, int al, u32 *__restrict__ done,
+    unsigned long long *__restrict__ hres) {
     __shared__ PbShared sh;
 #if PB_STAGE
     __shared__ TIn stage[PB_CAP];
@@ -2500,7 +2501,7 @@ fq_jit_pblocks(const TIn *__restrict__ col, long long n, long long B, Consts c,
         }
 #endif
 )";
-    s += R"(
+    s += R"PB(
         kept += tot;
         if (e <= PB_TILE) {
             if (tid == 0) counts[cur] = (long long)(carry + re);
@@ -2516,8 +2517,35 @@ fq_jit_pblocks(const TIn *__restrict__ col, long long n, long long B, Consts c,
     if (lane == 0 && pflags) atomicOr(fl, pflags);
     if (lane == 0 && vflags) atomicOr(fl + 1, vflags);
     if (tid == 0 && kept) atomicAdd(total, (unsigned long long)kept);
+    if (hres) {
+        // fq_filter_project_blocks_launch: the last workgroup hands {kept rows,
+        // flag words} to host memory and re-zeroes the workspace for the next
+        // launch (no memset before, no copy after).  Every wave's atomics are
+        // done before its workgroup draws a ticket.
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const u32 t = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (t == gridDim.x - 1u) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                const unsigned long long k = __hip_atomic_load(total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const unsigned long long f0 = __hip_atomic_load(fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const unsigned long long f1 = __hip_atomic_load(fl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                hres[0] = k;
+                hres[1] = f0 | (f1 << 32);
+                __hip_atomic_store(total, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(fl, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(fl + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    }
 }
-)";
+)PB";
     return s;
 }
 
@@ -3413,7 +3441,8 @@ fq_status jit_project_select(int32_t col_dtype, const ProjLaunch &P, const uint6
 }
 
 fq_status jit_project_blocks(int32_t col_dtype, const ProjLaunch &P, int64_t block_rows, const uint64_t *d_bitmap,
-                             int64_t *d_counts, uint32_t *d_flags, uint64_t *d_total, uint32_t *d_ticket) {
+                             int64_t *d_counts, uint32_t *d_flags, uint64_t *d_total, uint32_t *d_ticket,
+                             uint32_t *d_done, uint64_t *d_hres) {
     ProjKernels k;
     fq_status s = get_proj_kernels(col_dtype, P, &k);
     if (s != FQ_OK || !k.blocks || P.n == 0) return s;
@@ -3430,7 +3459,8 @@ fq_status jit_project_blocks(int32_t col_dtype, const ProjLaunch &P, int64_t blo
     const int64_t nb = (P.n + B - 1) / B;
     int al = 1;  // PB_STAGE row pairs need 16-byte aligned outputs
     for (int j = 0; j < P.n_out; ++j) al &= ((uintptr_t)P.out[j] & 15) == 0;
-    void *args[] = {&col, &n, &B, &hc, &d_bitmap, &outs, &d_counts, &d_flags, &d_total, &d_ticket, &al};
+    void *args[] = {&col, &n, &B, &hc, &d_bitmap, &outs, &d_counts, &d_flags, &d_total, &d_ticket, &al, &d_done,
+                    &d_hres};
     hipFunction_t fn = k.blocks;
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);

@@ -195,8 +195,11 @@ fq_status jit_project_select(int32_t col_dtype, const ProjLaunch &P, const uint6
 // d_flags / *d_total / *d_ticket as jit_project_select (zeroed by the caller)
 constexpr int kProjectBlockThreads = 256;
 constexpr int64_t kProjectBlockTile = 256 * 32;
+// d_hres != nullptr: the last workgroup writes {kept, flag words} to d_hres
+// (host memory the device writes) and re-zeroes flags / total / ticket / done
 fq_status jit_project_blocks(int32_t col_dtype, const ProjLaunch &P, int64_t block_rows, const uint64_t *d_bitmap,
-                             int64_t *d_counts, uint32_t *d_flags, uint64_t *d_total, uint32_t *d_ticket);
+                             int64_t *d_counts, uint32_t *d_flags, uint64_t *d_total, uint32_t *d_ticket,
+                             uint32_t *d_done = nullptr, uint64_t *d_hres = nullptr);
 // no predicate: every row -> the n_out outputs
 fq_status jit_project_map(int32_t col_dtype, const ProjLaunch &P, uint32_t *d_flag);
 // hipRTC loadable and the policy not FQ_JIT_OFF

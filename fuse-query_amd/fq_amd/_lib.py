@@ -25,6 +25,7 @@ GPU_SYMBOLS = [
     "fq_group_dense_keys", "fq_group_table_merge", "fq_tune_set", "fq_tune_get", "fq_tune_reset",
     "fq_tune_select_counters", "fq_tune_jit_dump_dir", "fq_filter_project_blocks_workspace_bytes",
     "fq_filter_project_blocks", "fq_filter_project_blocks_async", "fq_filter_project_blocks_result",
+    "fq_filter_project_blocks_workspace_init", "fq_filter_project_blocks_launch",
     "fq_blocks_compact_workspace_bytes", "fq_blocks_compact",
 ]
 
@@ -92,6 +93,10 @@ _protos = {
                                                    C.c_int32, P(vp), vp, P(C.c_uint64), vp, C.c_size_t, vp, vp,
                                                    vp]),
     "fq_filter_project_blocks_result": (C.c_int32, [P(C.c_uint64), P(C.c_int64)]),
+    "fq_filter_project_blocks_workspace_init": (C.c_int32, [vp, C.c_size_t, vp]),
+    "fq_filter_project_blocks_launch": (C.c_int32, [P(abi.fq_col), C.c_int64, P(abi.fq_pred), P(abi.fq_expr),
+                                                    C.c_int32, P(vp), vp, P(C.c_uint64), vp, vp, C.c_size_t, vp,
+                                                    vp, vp]),
     "fq_blocks_compact_workspace_bytes": (C.c_size_t, [C.c_int64]),
     "fq_blocks_compact": (C.c_int32, [C.c_int32, P(vp), C.c_int64, C.c_int64, vp, P(vp), P(C.c_int64), vp,
                                       C.c_size_t, vp]),

@@ -347,6 +347,22 @@ fq_status fq_filter_project_blocks_async(const fq_col *col, int64_t block_rows, 
                                          uint64_t *h_result, void *d_ws, size_t ws_bytes, void *ev_start,
                                          void *ev_end, void *stream);
 fq_status fq_filter_project_blocks_result(const uint64_t *h_result, int64_t *out_len);
+/* The async launch with no memset before it and no copy after it: the
+ * kernel's last workgroup writes the kept-row count and the flag words to
+ * d_result (the device address of host memory the device writes, e.g.
+ * hipHostMalloc(hipHostMallocMapped) + hipHostGetDevicePointer; h_result the
+ * host address of the same two words) and leaves the workspace zeroed.  The
+ * caller vouches that the workspace is zero: fq_filter_project_blocks_
+ * workspace_init ran on it (stream-ordered before) and only these calls used
+ * it since; calls sharing a workspace are ordered (one stream).  Read the
+ * result with fq_filter_project_blocks_result after the stream's work.  A
+ * queue that runs several such launches back to back then runs nothing but
+ * the kernels (the engine's ProjectionTransform).                            */
+fq_status fq_filter_project_blocks_workspace_init(void *d_ws, size_t ws_bytes, void *stream);
+fq_status fq_filter_project_blocks_launch(const fq_col *col, int64_t block_rows, const fq_pred *pred,
+                                          const fq_expr *values, int32_t n_out, void *const *d_out, int64_t *d_counts,
+                                          uint64_t *h_result, uint64_t *d_result, void *d_ws, size_t ws_bytes,
+                                          void *ev_start, void *ev_end, void *stream);
 /* A block stream's valid rows as one array: for each of n_cols 64-bit columns
  * of the geometry above (len rows, ceil(len / block_rows) blocks, block b's
  * valid rows the first d_counts[b] of its range), d_out[j] receives block 0's
