@@ -613,6 +613,7 @@ Runtime::~Runtime() {
         }
         if (w->ws) (void)hipFree(w->ws);
         for (auto ev : w->events) (void)hipEventDestroy(ev);
+        for (auto ev : w->sync_events) (void)hipEventDestroy(ev);
         for (auto *c : w->slot_chunks) (void)hipHostFree(c);
         if (w->project_res) (void)hipHostFree(w->project_res);
         if (w->project_ws) (void)hipFree(w->project_ws);
@@ -675,6 +676,17 @@ uint64_t *WorkerRes::project_result() {
         project_res = (uint64_t *)p;
     }
     return project_res;
+}
+
+hipEvent_t WorkerRes::take_sync_event() {
+    if (!sync_events.empty()) {
+        hipEvent_t e = sync_events.back();
+        sync_events.pop_back();
+        return e;
+    }
+    hipEvent_t e;
+    check_hip(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreateWithFlags");
+    return e;
 }
 
 hipEvent_t WorkerRes::take_event() {
@@ -852,14 +864,14 @@ ExecCtx &ExecCtx::current() {
 // extend to launches other pipes enqueue meanwhile.
 void ExecCtx::sync() {
     if (!rt->has_device()) return;
-    hipEvent_t ev = res->take_event();
+    hipEvent_t ev = res->take_sync_event();
     hipError_t e;
     {
         std::lock_guard<std::mutex> lk(*res->launch_mu);
         e = hipEventRecord(ev, stream());
     }
     if (e == hipSuccess) e = hipEventSynchronize(ev);
-    res->give_event(ev);
+    res->give_sync_event(ev);
     check_hip(e, "hipEventSynchronize");
 }
 

@@ -182,6 +182,10 @@ struct WorkerRes {
     void project_resident();  // makes the three on first use
     hipEvent_t take_event();
     void give_event(hipEvent_t e) { events.push_back(e); }
+    // completion-only events (hipEventDisableTiming: no timestamp to write)
+    std::vector<hipEvent_t> sync_events;
+    hipEvent_t take_sync_event();
+    void give_sync_event(hipEvent_t e) { sync_events.push_back(e); }
 };
 
 // Persistent host threads for the pipes (the reference spawns tokio tasks per
@@ -371,6 +375,9 @@ struct DataBlock {
     std::shared_ptr<const BlockLayout> layout;
     // the MergeProcessor input (partition pipe) the block came from; -1 unknown
     int32_t pipe = -1;
+    // the device work that produced this block has completed (its producer
+    // waited for it): the merge need not wait again before handing it over
+    bool ready = false;
     // set: the block's columns are not final yet -- the consumer runs this
     // (once, on its own thread) before reading them: AggregatePartial's states
     // once the query's scans have ended (complete_block)

@@ -704,6 +704,7 @@ static DataBlock compact_layout(const DataBlock &b, ExecCtx &ctx) {
     const BlockLayout &L = *b.layout;
     DataBlock nb = b;
     nb.layout = nullptr;
+    nb.ready = false;  // the compaction below is new device work
     std::vector<const void *> in;
     std::vector<void *> out;
     for (auto &c : nb.columns) {
@@ -727,6 +728,7 @@ DataBlock materialize(const DataBlock &b, ExecCtx &ctx) {
     if (!b.filter) return b;
     DataBlock nb = b;
     nb.filter = nullptr;
+    nb.ready = false;
     Column bm = eval_predicate(*b.filter, nb, ctx);
     return compact_block(nb, bm, ctx);
 }
@@ -748,10 +750,19 @@ static bool project_blocks(const DataBlock &b, const Column &c, const fq_pred *p
     layout->block_rows = B;
     layout->n_blocks = n == 0 ? 0 : nb;
     layout->counts = DeviceBuffer::alloc((size_t)std::max<int64_t>(nb, 1) * 8, ctx.stream());
-    // the worker's own workspace, kept zeroed by the kernel, and result words
-    // the kernel writes to host memory: nothing but the kernel on the queue
-    ctx.res->project_resident();
-    uint64_t *res = ctx.res->project_hres;
+    // FQ_TUNE_ENGINE_PROJECT_LAUNCH: the worker's own workspace, kept zeroed
+    // by the kernel, and result words the kernel writes to host memory --
+    // nothing but the kernel on the queue; else a workspace per call, zeroed
+    // before it, and the result copied after it
+    std::shared_ptr<DeviceBuffer> ws;
+    uint64_t *res = nullptr;
+    if (fqc::knob(FQ_TUNE_ENGINE_PROJECT_LAUNCH)) {
+        ctx.res->project_resident();
+        res = ctx.res->project_hres;
+    } else {
+        ws = DeviceBuffer::alloc(fq_filter_project_blocks_workspace_bytes(), ctx.stream());
+        res = ctx.res->project_result();
+    }
     const bool prof = ctx.rt->profile.load();
     hipEvent_t e0 = ctx.res->take_event(), e1 = ctx.res->take_event();
     fq_col ic = c.abi();
@@ -763,13 +774,17 @@ static bool project_blocks(const DataBlock &b, const Column &c, const fq_pred *p
                                                   nullptr, res, nullptr, 0, nullptr, nullptr, ctx.stream());
     if (st == FQ_E_UNSUPPORTED) return false;
     check_fq(st);
-    hipEvent_t done = ctx.res->take_event();
+    hipEvent_t done = ctx.res->take_sync_event();
+    const bool launch = fqc::knob(FQ_TUNE_ENGINE_PROJECT_LAUNCH) != 0;
     {
         std::lock_guard<std::mutex> lk(*ctx.res->launch_mu);
-        st = fq_filter_project_blocks_launch(&ic, B, pred, exprs.data(), (int32_t)exprs.size(), ptrs.data(),
-                                             (int64_t *)layout->counts->ptr, res, ctx.res->project_dres,
-                                             ctx.res->project_ws, fq_filter_project_blocks_workspace_bytes(),
-                                             prof ? e0 : nullptr, prof ? e1 : nullptr, ctx.stream());
+        st = launch ? fq_filter_project_blocks_launch(&ic, B, pred, exprs.data(), (int32_t)exprs.size(), ptrs.data(),
+                                                      (int64_t *)layout->counts->ptr, res, ctx.res->project_dres,
+                                                      ctx.res->project_ws, fq_filter_project_blocks_workspace_bytes(),
+                                                      prof ? e0 : nullptr, prof ? e1 : nullptr, ctx.stream())
+                    : fq_filter_project_blocks_async(&ic, B, pred, exprs.data(), (int32_t)exprs.size(), ptrs.data(),
+                                                     (int64_t *)layout->counts->ptr, res, ws->ptr, ws->bytes,
+                                                     prof ? e0 : nullptr, prof ? e1 : nullptr, ctx.stream());
         if (st == FQ_OK) check_hip(hipEventRecord(done, ctx.stream()), "hipEventRecord");  // after the result copy
     }
     if (st == FQ_OK) {
@@ -782,7 +797,7 @@ static bool project_blocks(const DataBlock &b, const Column &c, const fq_pred *p
     }
     ctx.res->give_event(e0);
     ctx.res->give_event(e1);
-    ctx.res->give_event(done);
+    ctx.res->give_sync_event(done);
     if (st == FQ_E_UNSUPPORTED) return false;  // the unfused path evaluates it (and raises what the reference does)
     check_fq(st);
     int64_t kept = 0;
@@ -797,6 +812,7 @@ static bool project_blocks(const DataBlock &b, const Column &c, const fq_pred *p
     out.schema = schema;
     out.sub_block_rows = B;
     out.layout = layout;
+    out.ready = true;  // this pipe waited for the launch (done) above
     for (auto &o : outs) out.columns.push_back(o);
     return true;
 }
@@ -1005,14 +1021,14 @@ size_t AggFusion::alloc_slot() {
 }
 
 void AggFusion::wait_launched() {
-    hipEvent_t done = res_->take_event();
+    hipEvent_t done = res_->take_sync_event();
     {
         std::lock_guard<std::mutex> lk(*res_->launch_mu);
         res_->ws_ready(stream_);  // a fold on the fold queue wrote a result too
         check_hip(hipEventRecord(done, stream_), "hipEventRecord");
     }
     hipError_t e = hipEventSynchronize(done);
-    res_->give_event(done);
+    res_->give_sync_event(done);
     check_hip(e, "hipEventSynchronize");
 }
 

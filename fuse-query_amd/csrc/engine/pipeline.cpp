@@ -331,7 +331,7 @@ StreamRef MergeProcessor::execute() {
                     // it; a host block (AggregatePartial's states) has none left
                     bool device = (bool)b.layout || (bool)b.filter;
                     for (const Column &c : b.columns) device |= c.on_device();
-                    if (device) ctx.sync();
+                    if (device && !b.ready) ctx.sync();
                     Channel::Item it;
                     b.pipe = (int32_t)pipe;
                     it.pipe = pipe;
