@@ -752,8 +752,11 @@ static bool project_blocks(const DataBlock &b, const Column &c, const fq_pred *p
     layout->counts = DeviceBuffer::alloc((size_t)std::max<int64_t>(nb, 1) * 8, ctx.stream());
     // FQ_TUNE_ENGINE_PROJECT_LAUNCH: the worker's own workspace, kept zeroed
     // by the kernel, and result words the kernel writes to host memory --
-    // nothing but the kernel on the queue; else a workspace per call, zeroed
-    // before it, and the result copied after it
+    // nothing but the kernel on the queue; else (the default) a workspace per
+    // call, zeroed before it, and the result copied after it.  In one process
+    // the kernel's hand-off (a ticket per workgroup, the last one's host
+    // writes) cost more than the memset and copy it saves: 24.36 against
+    // 24.09 ms per p1 query (profiles/r05_y_p1_launch_ab.json)
     std::shared_ptr<DeviceBuffer> ws;
     uint64_t *res = nullptr;
     if (fqc::knob(FQ_TUNE_ENGINE_PROJECT_LAUNCH)) {

@@ -2521,16 +2521,16 @@ fq_jit_pblocks(const TIn *__restrict__ col, long long n, long long B, Consts c,
         // fq_filter_project_blocks_launch: the last workgroup hands {kept rows,
         // flag words} to host memory and re-zeroes the workspace for the next
         // launch (no memset before, no copy after).  Every wave's atomics are
-        // done before its workgroup draws a ticket.
+        // done (vmcnt) before its workgroup draws a ticket; the counters are
+        // device-scope atomics and read as such, so no L2 write-back is needed
+        // -- an agent-scope release per workgroup cost the kernel 4.6 %
+        // (profiles/r05_x_p1_launch_ab.json).  The outputs are read only after
+        // the kernel has completed (the caller waits on the stream).
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (tid == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             const u32 t = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (t == gridDim.x - 1u) {
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 const unsigned long long k = __hip_atomic_load(total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 const unsigned long long f0 = __hip_atomic_load(fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 const unsigned long long f1 = __hip_atomic_load(fl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -60,7 +60,7 @@ constexpr KnobDef kDefs[FQ_TUNE_COUNT] = {
     {0, 0, 1, 1, false},         // ENGINE_ONE_LAUNCH
     {2, 0, 4, 1, true},          // SELECT_BLOCKS_STAGE
     {0, 0, 1, 1, false},         // ENGINE_FOLD_STREAM
-    {1, 0, 1, 1, false},         // ENGINE_PROJECT_LAUNCH
+    {0, 0, 1, 1, false},         // ENGINE_PROJECT_LAUNCH
 };
 
 std::atomic<int64_t> g_val[FQ_TUNE_COUNT] = {};

@@ -476,7 +476,8 @@ fq_status fq_jit_prepare(const fq_col *col, int64_t block_rows, const fq_pred *p
                                        (fq_aggregate_split) beside the next scan: 0 (0/1; measured
                                        slower) */
 #define FQ_TUNE_ENGINE_PROJECT_LAUNCH 41 /* the engine's block projections: fq_filter_project_blocks_launch
-                                          (no memset / copy around the kernel) 1, or _async 0 (0/1) */
+                                          (no memset / copy around the kernel) 1, or _async 0: 0 (0/1;
+                                          the kernel's own hand-off measured slower) */
 #define FQ_TUNE_COUNT 42
 /* FQ_E_INVALID for an unknown knob or a value outside the knob's set */
 fq_status fq_tune_set(int32_t knob, int64_t value);
