@@ -375,6 +375,19 @@ __global__ void block_lengths_kernel(int64_t *__restrict__ counts, int64_t nb, i
         counts[b] = b * B + B <= n ? B : n - b * B;
 }
 
+// fq_filter_project_blocks_launch with FQ_TUNE_PROJECT_HANDOFF 0: after the
+// projection kernel, one thread moves {kept rows, flag words} to d_res and
+// zeroes the three workspace words -- one launch in place of the next call's
+// memset and this call's copy.
+__global__ void project_hand_off_kernel(uint64_t *__restrict__ ws, uint64_t *__restrict__ d_res) {
+    if (threadIdx.x != 0) return;
+    d_res[0] = ws[0];
+    d_res[1] = ws[1];
+    ws[0] = 0;
+    ws[1] = 0;
+    ws[2] = 0;
+}
+
 // ---- fq_blocks_compact: a block stream's valid rows into one array ----
 // counts[b] -> exclusive offsets in three launches: per-chunk sums of
 // kCompactChunk counts, one workgroup scanning the chunk sums, then each chunk
@@ -599,6 +612,7 @@ fq_status project_blocks_enqueue(const fq_col *col, int64_t block_rows, const fq
     hipStream_t st = P.stream;
     const int64_t nb = block_rows >= n ? 1 : (n + block_rows - 1) / block_rows;
     const bool resident = d_result != nullptr && P.pred.kind != FQ_PRED_NONE;
+    const bool in_kernel = fqc::knob(FQ_TUNE_PROJECT_HANDOFF) != 0;  // else the one-thread kernel after it
     if (!d_result || !resident) FQ_HIP_TRY(hipMemsetAsync(d_ws, 0, fq_filter_project_blocks_workspace_bytes(), st));
     if (ev_start) FQ_HIP_TRY(hipEventRecord((hipEvent_t)ev_start, st));
     if (P.pred.kind == FQ_PRED_NONE) {  // every row kept: outputs in place, counts = block lengths
@@ -613,11 +627,16 @@ fq_status project_blocks_enqueue(const fq_col *col, int64_t block_rows, const fq
         if (d_result) FQ_HIP_TRY(hipMemsetAsync(d_ws, 0, fq_filter_project_blocks_workspace_bytes(), st));
     } else {
         if ((s = jit_project_blocks(col->dtype, P, block_rows, P.pred.kind == FQ_PRED_BITMAP ? P.pred.bitmap : nullptr,
-                                    d_counts, flags, total, ticket, resident ? done : nullptr,
-                                    resident ? d_result : nullptr)) != FQ_OK)
+                                    d_counts, flags, total, ticket, resident && in_kernel ? done : nullptr,
+                                    resident && in_kernel ? d_result : nullptr)) != FQ_OK)
             return s;
         if (ev_end) FQ_HIP_TRY(hipEventRecord((hipEvent_t)ev_end, st));
-        if (!resident) FQ_HIP_TRY(hipMemcpyAsync(h_result, total, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+        if (!resident) {
+            FQ_HIP_TRY(hipMemcpyAsync(h_result, total, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+        } else if (!in_kernel) {
+            hipLaunchKernelGGL(project_hand_off_kernel, dim3(1), dim3(64), 0, st, total, d_result);
+            FQ_HIP_TRY(hipGetLastError());
+        }
     }
     return FQ_OK;
 }

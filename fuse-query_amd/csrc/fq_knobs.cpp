@@ -61,6 +61,7 @@ constexpr KnobDef kDefs[FQ_TUNE_COUNT] = {
     {2, 0, 4, 1, true},          // SELECT_BLOCKS_STAGE
     {0, 0, 1, 1, false},         // ENGINE_FOLD_STREAM
     {0, 0, 1, 1, false},         // ENGINE_PROJECT_LAUNCH
+    {0, 0, 1, 1, false},         // PROJECT_HANDOFF
 };
 
 std::atomic<int64_t> g_val[FQ_TUNE_COUNT] = {};

@@ -129,6 +129,6 @@ TUNE = {
     "JIT_ISOLATED": 20, "GROUP_ROWMAP": 21, "GROUP_WG_PER_CU": 22, "GROUP_RANGE_BINS": 23, "GROUP_NARROW": 24,
     "SELECT_BLOCKS_WG_PER_CU": 25, "SELECT_BLOCKS_RUN": 26, "SELECT_BLOCKS_DRAW": 27, "SELECT_BLOCKS_ROWS": 28,
     "SELECT_NT": 29, "GPART_DBUF": 30, "GPART_ROWS8": 31, "GPART_ROWS4": 32, "GBINS_ROWS": 33, "GBINS_WG_PER_CU": 34, "GBINS_FIT_LDS": 35,
-    "POOL_SPIN_US": 36, "SCAN_FIN": 37, "ENGINE_ONE_LAUNCH": 38, "SELECT_BLOCKS_STAGE": 39, "ENGINE_FOLD_STREAM": 40, "ENGINE_PROJECT_LAUNCH": 41,
+    "POOL_SPIN_US": 36, "SCAN_FIN": 37, "ENGINE_ONE_LAUNCH": 38, "SELECT_BLOCKS_STAGE": 39, "ENGINE_FOLD_STREAM": 40, "ENGINE_PROJECT_LAUNCH": 41, "PROJECT_HANDOFF": 42,
 }
 TUNE_SELECT_COUNTERS = 13

@@ -478,7 +478,9 @@ fq_status fq_jit_prepare(const fq_col *col, int64_t block_rows, const fq_pred *p
 #define FQ_TUNE_ENGINE_PROJECT_LAUNCH 41 /* the engine's block projections: fq_filter_project_blocks_launch
                                           (no memset / copy around the kernel) 1, or _async 0: 0 (0/1;
                                           the kernel's own hand-off measured slower) */
-#define FQ_TUNE_COUNT 42
+#define FQ_TUNE_PROJECT_HANDOFF 42 /* fq_filter_project_blocks_launch: the kernel's last workgroup hands the
+                                    result over (1) or a one-thread kernel after it (0): 0 (0/1) */
+#define FQ_TUNE_COUNT 43
 /* FQ_E_INVALID for an unknown knob or a value outside the knob's set */
 fq_status fq_tune_set(int32_t knob, int64_t value);
 /* the knob's current value; -1 for an unknown knob */

@@ -271,12 +271,15 @@ def test_block_outputs_not_16_byte_aligned(block_rows):
            [lambda k: k + np.uint64(1), lambda k: k], block_rows, out_offset=1)
 
 
+@pytest.mark.parametrize("handoff", [0, 1], ids=["after_kernel", "in_kernel"])
 @pytest.mark.parametrize("sel", ["mod8", "none_kept", "div_zero"])
-def test_launch_without_memset_or_copy_matches_async(sel):
-    """fq_filter_project_blocks_launch: the workspace zeroed once, the kernel's
-    last workgroup writes {kept, flags} to mapped host memory and re-zeroes
-    the workspace -- the same outputs, counts, kept rows and status as the
+def test_launch_without_memset_or_copy_matches_async(sel, handoff):
+    """fq_filter_project_blocks_launch: the workspace zeroed once; {kept,
+    flags} written to d_result and the workspace re-zeroed by a one-thread
+    kernel after the projection (FQ_TUNE_PROJECT_HANDOFF 0) or by its last
+    workgroup (1) -- the same outputs, counts, kept rows and status as the
     async path, launch after launch on one workspace (which ends zeroed)."""
+    ops.tune_set("PROJECT_HANDOFF", handoff)
     import ctypes as C
 
     from fq_amd._lib import lib
@@ -335,6 +338,7 @@ def test_launch_without_memset_or_copy_matches_async(sel):
                 for gb, eb in zip(o, e):
                     assert np.array_equal(gb, eb)
         assert not ws.buf[:wsb].cpu().numpy().any()  # left zeroed for the next launch
+    ops.tune_set("PROJECT_HANDOFF", 0)
 
 
 @pytest.mark.parametrize("n_blocks,block_rows,n_cols", [(3000, 64, 1), (20011, 17, 2), (50000, 8, 3), (1025, 1000, 2)])
