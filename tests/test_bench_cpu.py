@@ -134,3 +134,21 @@ def test_bench_module_imports_without_the_hip_runtime():
     p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, cwd=ROOT)
     assert p.returncode == 0, p.stderr
     assert p.stdout.strip() == "[]"
+
+
+def test_settle_runs_untimed_steps_for_about_the_requested_time():
+    # bench.settle: steps for ~`seconds` at the first step's pace (world 1: no
+    # collective); 0 s runs none, and a step slower than the budget runs once
+    import time
+    b = _bench()
+    calls = []
+
+    def step():
+        calls.append(time.perf_counter())
+        time.sleep(0.002)
+
+    assert b.settle(step, 0, 1, "gloo") == 0 and not calls
+    n = b.settle(step, 0.05, 1, "gloo")
+    assert n == len(calls) and 10 <= n <= 30, n
+    calls.clear()
+    assert b.settle(lambda: (calls.append(1), time.sleep(0.03)), 0.01, 1, "gloo") == 1 and len(calls) == 1
