@@ -269,6 +269,10 @@ fq_status fq_engine_set_option(fq_engine *e, int32_t option, int64_t value) {
                     throw fq::FQException(FQ_E_INVALID, "FQ_OPT_GROUP_CHUNK_ROWS must be a positive multiple of 64");
                 e->rt->group_chunk_rows.store(value);
                 break;
+            case FQ_OPT_FAULT_PIPE:
+                if (value < 0) throw fq::FQException(FQ_E_INVALID, "FQ_OPT_FAULT_PIPE is 0 or a pipe number");
+                e->rt->fault_pipe.store(value);
+                break;
             default: throw fq::FQException(FQ_E_INVALID, "fq_engine_set_option: unknown option");
         }
     });

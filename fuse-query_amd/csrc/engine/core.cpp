@@ -540,7 +540,6 @@ void Runtime::set_streams(int n) {
         BlockCache::get().add_stream(s);
         shared_.push_back(s);
         shared_mu_.push_back(std::make_unique<std::mutex>());
-        fold_.push_back(nullptr);  // created on first use (fold_queue)
     }
     // existing workers keep their queue; new ones pick round-robin among the first n
     next_shared_ = 0;
@@ -565,9 +564,6 @@ WorkerRes *Runtime::acquire() {
     w->queue_index = q;
     w->ws_bytes = fq_aggregate_workspace_bytes(0);
     check_hip(alloc_with_reclaim([&] { return hipMalloc(&w->ws, w->ws_bytes); }), "hipMalloc(workspace)");
-    // the in-launch finalize's completion counter starts at zero; every
-    // FQ_AGG_ONE_LAUNCH scan on this workspace leaves it zero
-    check_hip(hipMemset(w->ws, 0, w->ws_bytes), "hipMemset(workspace)");
     all_.push_back(std::move(w));
     return all_.back().get();
 }
@@ -601,11 +597,7 @@ Runtime::~Runtime() {
     if (device_ == kHostOnly) return;
     (void)hipSetDevice(device_);
     for (auto &s : shared_) (void)hipStreamSynchronize(s);
-    for (auto &s : fold_)
-        if (s) (void)hipStreamSynchronize(s);
     for (auto &w : all_) {
-        if (w->scan_done) (void)hipEventDestroy(w->scan_done);
-        if (w->fold_done) (void)hipEventDestroy(w->fold_done);
         if (w->own) {
             (void)hipStreamSynchronize(w->own);
             BlockCache::get().drop_stream(w->own);
@@ -617,65 +609,26 @@ Runtime::~Runtime() {
         for (auto *c : w->slot_chunks) (void)hipHostFree(c);
         if (w->project_res) (void)hipHostFree(w->project_res);
         if (w->project_ws) (void)hipFree(w->project_ws);
-        if (w->project_hres) (void)hipHostFree(w->project_hres);
     }
     for (auto ev : events_) (void)hipEventDestroy(ev);
     for (auto &s : shared_) {
         BlockCache::get().drop_stream(s);
         (void)hipStreamDestroy(s);
     }
-    for (auto &s : fold_)
-        if (s) (void)hipStreamDestroy(s);
-}
-
-// The fold queue of w's shared queue, at the device's highest priority (a
-// fold's one workgroup is dispatched ahead of the running scan's remaining
-// ones), and w's two events for it -- made only when the engine folds there
-// (FQ_TUNE_ENGINE_FOLD_STREAM): an idle stream per queue slowed the LIMIT
-// pipes' private queues (profiles/r05_t_limit_bisect.txt).
-hipStream_t Runtime::fold_queue(WorkerRes *w) {
-    if (w->fold) return w->fold;
-    {
-        std::lock_guard<std::mutex> lk(mu_);
-        hipStream_t &f = fold_[w->queue_index];
-        if (!f) {
-            int lo = 0, hi = 0;
-            (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
-            check_hip(hipStreamCreateWithPriority(&f, hipStreamNonBlocking, hi), "hipStreamCreateWithPriority");
-        }
-        w->fold = f;
-    }
-    check_hip(hipEventCreateWithFlags(&w->scan_done, hipEventDisableTiming), "hipEventCreateWithFlags");
-    check_hip(hipEventCreateWithFlags(&w->fold_done, hipEventDisableTiming), "hipEventCreateWithFlags");
-    return w->fold;
-}
-
-void WorkerRes::ws_ready(hipStream_t s) {
-    if (fold_pending) check_hip(hipStreamWaitEvent(s, fold_done, 0), "hipStreamWaitEvent");
 }
 
 void WorkerRes::project_resident() {
     if (project_ws) return;
-    const size_t bytes = fq_filter_project_blocks_workspace_bytes();
-    void *h = nullptr, *d = nullptr;
-    check_hip(hipHostMalloc(&h, 2 * sizeof(uint64_t), hipHostMallocMapped | hipHostMallocCoherent),
+    void *h = nullptr, *d = nullptr, *ws = nullptr;
+    check_hip(hipHostMalloc(&h, 4 * sizeof(uint64_t), hipHostMallocMapped | hipHostMallocCoherent),
               "hipHostMalloc(projection result)");
+    project_res = (uint64_t *)h;
     check_hip(hipHostGetDevicePointer(&d, h, 0), "hipHostGetDevicePointer");
-    void *ws = nullptr;
-    check_hip(alloc_with_reclaim([&] { return hipMalloc(&ws, bytes); }), "hipMalloc(projection workspace)");
-    check_hip(hipMemset(ws, 0, bytes), "hipMemset(projection workspace)");  // the kernel keeps it zeroed
-    project_hres = (uint64_t *)h;
     project_dres = (uint64_t *)d;
+    const size_t bytes = fq_filter_project_blocks_workspace_bytes();
+    check_hip(alloc_with_reclaim([&] { return hipMalloc(&ws, bytes); }), "hipMalloc(projection workspace)");
+    check_hip(hipMemset(ws, 0, bytes), "hipMemset(projection workspace)");  // the hand-off keeps it zeroed
     project_ws = ws;
-}
-
-uint64_t *WorkerRes::project_result() {
-    if (!project_res) {
-        void *p = nullptr;
-        check_hip(hipHostMalloc(&p, 2 * sizeof(uint64_t), hipHostMallocDefault), "hipHostMalloc(projection result)");
-        project_res = (uint64_t *)p;
-    }
-    return project_res;
 }
 
 hipEvent_t WorkerRes::take_sync_event() {

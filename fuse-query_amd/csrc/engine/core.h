@@ -157,28 +157,19 @@ struct WorkerRes {
     std::mutex *launch_mu = nullptr;  // serialises multi-call enqueues on a shared queue
     void *ws = nullptr;               // fq_aggregate workspace
     size_t ws_bytes = 0;
-    // the shared queue's fold queue (fq_aggregate_split): scans fold their
-    // partials there, beside the next scan.  fold_done marks this worker's
-    // last fold (fold_pending): the workspace's next scan waits for it.
-    hipStream_t fold = nullptr;       // Runtime::fold_queue, on first use
-    hipEvent_t scan_done = nullptr, fold_done = nullptr;
-    bool fold_pending = false;
     size_t queue_index = 0;           // which shared queue (Runtime::shared_)
-    void ws_ready(hipStream_t s);  // orders s after this workspace's pending fold
     std::vector<hipEvent_t> events;   // reusable events (timing pairs, completion)
     // Pinned, device-visible result slots: the scan's finalize kernel writes
     // its fq_agg_state straight to host memory, so no copy is queued behind
     // the next partition's scan.  Chunks of kSlotChunk, reused across queries.
     static constexpr size_t kSlotChunk = 64;
     std::vector<fq_agg_state *> slot_chunks;
-    // pinned {kept rows, flag words} of this worker's block-stream projection
-    // launch (fq_filter_project_blocks_async; one in flight per worker)
-    uint64_t *project_res = nullptr;
-    uint64_t *project_result();
-    // fq_filter_project_blocks_launch: this worker's workspace, kept zeroed by
-    // the kernel, and the two result words it writes (host memory, mapped)
+    // this worker's block-stream projection launch (fqk::filter_project_blocks_
+    // enqueue; one in flight per worker): {kept rows, flag words} in pinned,
+    // device-mapped host memory (project_res, its device address project_dres)
+    // and a workspace kept zeroed between launches (project_ws)
+    uint64_t *project_res = nullptr, *project_dres = nullptr;
     void *project_ws = nullptr;
-    uint64_t *project_hres = nullptr, *project_dres = nullptr;
     void project_resident();  // makes the three on first use
     hipEvent_t take_event();
     void give_event(hipEvent_t e) { events.push_back(e); }
@@ -222,8 +213,6 @@ class Runtime {
     void release(WorkerRes *w);
     void set_streams(int n);
     int active_streams() const { return active_streams_; }
-    // w's shared queue's fold queue (fq_aggregate_split), made on first use
-    hipStream_t fold_queue(WorkerRes *w);
     // timing-capable events shared across pipe threads (ScanGroup)
     hipEvent_t take_event();
     void give_event(hipEvent_t e);
@@ -236,6 +225,8 @@ class Runtime {
     std::atomic<int64_t> group_used_capacity{0};
     // rows per radix-partitioned GROUP BY launch (FQ_OPT_GROUP_CHUNK_ROWS)
     std::atomic<int64_t> group_chunk_rows{500000000};
+    // FQ_OPT_FAULT_PIPE (testing): merged pipe k (1-based) fails its context setup
+    std::atomic<int64_t> fault_pipe{0};
     ThreadPool pool;
 
    private:
@@ -244,7 +235,6 @@ class Runtime {
     std::vector<std::unique_ptr<WorkerRes>> all_;
     std::vector<WorkerRes *> free_;
     std::vector<hipStream_t> shared_;  // FQ_OPT_STREAMS queues shared by the pipes
-    std::vector<hipStream_t> fold_;    // each one's fold queue (WorkerRes::fold)
     std::vector<std::unique_ptr<std::mutex>> shared_mu_;
     size_t next_shared_ = 0;
     std::atomic<int> active_streams_{1};

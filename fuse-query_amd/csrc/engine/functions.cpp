@@ -415,23 +415,12 @@ void AggregatorFunction::accumulate_summary(const fq_agg_state &st) {
 
 static uint32_t scan_mask(uint32_t op) { return op | FQ_AGG_COUNT; }
 
-// The in-launch finalize (FQ_AGG_ONE_LAUNCH, the workers' workspaces are
-// zeroed at allocation) or the separate finalize launch: the latter measured
-// faster on MI355X -- 8 back-to-back scans 11.02 ms against 11.07 (write-
-// through partials) and 11.16 (agent release), profiles/r05_b_scan_fin_ab.json:
-// 512 workgroups each waiting on a device-scope ticket, then one workgroup's
-// serial fold, cost more than a 4.4 us kernel after a ~1.5 us boundary.
-static uint32_t engine_one_launch() {
-    return fqc::knob(FQ_TUNE_ENGINE_ONE_LAUNCH) ? FQ_AGG_ONE_LAUNCH : 0u;
-}
-
 static fq_agg_state run_scan(const Column &col, int64_t block_rows, const fq_pred *pred, const fq_expr *value,
                              uint32_t mask, ExecCtx &ctx) {
     auto out = DeviceBuffer::alloc(sizeof(fq_agg_state), ctx.stream());
     fq_col c = col.abi();
-    ctx.res->ws_ready(ctx.stream());
-    check_fq(fq_aggregate(&c, block_rows, pred, value, mask | engine_one_launch(), (fq_agg_state *)out->ptr,
-                          ctx.res->ws, ctx.res->ws_bytes, ctx.stream()));
+    check_fq(fq_aggregate(&c, block_rows, pred, value, mask, (fq_agg_state *)out->ptr, ctx.res->ws,
+                          ctx.res->ws_bytes, ctx.stream()));
     fq_agg_state st{};
     check_hip(hipMemcpyAsync(&st, out->ptr, sizeof st, hipMemcpyDeviceToHost, ctx.stream()), "hipMemcpyAsync");
     ctx.sync();
@@ -738,9 +727,19 @@ DataBlock materialize(const DataBlock &b, ExecCtx &ctx) {
 // filters and projects each 10,000-row block on its own
 // (stream_expression.rs:38-50), so the output keeps that geometry -- block b's
 // kept rows at rows [b * B, b * B + count[b]) -- and no block waits on another's
-// count (fq_filter_project_blocks).  The launch is enqueued with the queue's
-// other pipes (launch_mu: a timing event pair brackets exactly this launch) and
-// this pipe waits on its own event, not on the queue.
+// count (fqk::filter_project_blocks_enqueue).  The launch is enqueued with the
+// queue's other pipes (launch_mu) and this pipe waits for its own launch, not
+// for the queue.
+//
+// What sits on the queue around each projection kernel
+// (FQ_TUNE_ENGINE_PROJECT_LAUNCH): 0 -- a workspace memset before it, a copy of
+// the two result words after it and a completion event; 1 -- the worker's
+// resident workspace and a one-thread hand-off kernel after it (no memset, no
+// copy), then the completion event; 2 -- as 1 with no event: the pipe polls the
+// hand-off's words in mapped host memory (a sentinel until the kernel wrote
+// them).  With FQ_OPT_PROFILE an event pair brackets the kernel.
+static constexpr uint64_t kProjectPending = ~0ull;  // project_res[0] until the hand-off wrote it
+
 static bool project_blocks(const DataBlock &b, const Column &c, const fq_pred *pred, std::vector<fq_expr> &exprs,
                            std::vector<Column> &outs, std::vector<void *> &ptrs, const SchemaRef &schema, ExecCtx &ctx,
                            DataBlock &out) {
@@ -750,61 +749,75 @@ static bool project_blocks(const DataBlock &b, const Column &c, const fq_pred *p
     layout->block_rows = B;
     layout->n_blocks = n == 0 ? 0 : nb;
     layout->counts = DeviceBuffer::alloc((size_t)std::max<int64_t>(nb, 1) * 8, ctx.stream());
-    // FQ_TUNE_ENGINE_PROJECT_LAUNCH: the worker's own workspace, kept zeroed
-    // by the kernel, and result words the kernel writes to host memory --
-    // nothing but the kernel on the queue; else (the default) a workspace per
-    // call, zeroed before it, and the result copied after it.  In one process
-    // the kernel's hand-off (a ticket per workgroup, the last one's host
-    // writes) cost more than the memset and copy it saves: 24.36 against
-    // 24.09 ms per p1 query (profiles/r05_y_p1_launch_ab.json)
+    // (no predicate: the map kernel, whose words the host writes -- mode 0)
+    const int mode = pred && pred->kind != FQ_PRED_NONE ? (int)fqc::knob(FQ_TUNE_ENGINE_PROJECT_LAUNCH) : 0;
+    ctx.res->project_resident();
+    uint64_t *res = ctx.res->project_res;
     std::shared_ptr<DeviceBuffer> ws;
-    uint64_t *res = nullptr;
-    if (fqc::knob(FQ_TUNE_ENGINE_PROJECT_LAUNCH)) {
-        ctx.res->project_resident();
-        res = ctx.res->project_hres;
-    } else {
-        ws = DeviceBuffer::alloc(fq_filter_project_blocks_workspace_bytes(), ctx.stream());
-        res = ctx.res->project_result();
-    }
+    if (mode == 0) ws = DeviceBuffer::alloc(fq_filter_project_blocks_workspace_bytes(), ctx.stream());
     const bool prof = ctx.rt->profile.load();
-    hipEvent_t e0 = ctx.res->take_event(), e1 = ctx.res->take_event();
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (prof) {
+        e0 = ctx.res->take_event();
+        e1 = ctx.res->take_event();
+    }
     fq_col ic = c.abi();
     // the shape's kernel compiled (first use: hipRTC, ~0.2 s) before the
     // queue's launch lock is taken: a zero-length call only prepares it
     fq_col none = ic;
     none.len = 0;
-    fq_status st = fq_filter_project_blocks_async(&none, B, pred, exprs.data(), (int32_t)exprs.size(), ptrs.data(),
-                                                  nullptr, res, nullptr, 0, nullptr, nullptr, ctx.stream());
+    fq_status st = fqk::filter_project_blocks_enqueue(&none, B, pred, exprs.data(), (int32_t)exprs.size(), ptrs.data(),
+                                                      nullptr, res, nullptr, nullptr, 0, nullptr, nullptr, ctx.stream());
     if (st == FQ_E_UNSUPPORTED) return false;
     check_fq(st);
-    hipEvent_t done = ctx.res->take_sync_event();
-    const bool launch = fqc::knob(FQ_TUNE_ENGINE_PROJECT_LAUNCH) != 0;
+    hipEvent_t done = mode == 2 ? nullptr : ctx.res->take_sync_event();
     {
         std::lock_guard<std::mutex> lk(*ctx.res->launch_mu);
-        st = launch ? fq_filter_project_blocks_launch(&ic, B, pred, exprs.data(), (int32_t)exprs.size(), ptrs.data(),
-                                                      (int64_t *)layout->counts->ptr, res, ctx.res->project_dres,
-                                                      ctx.res->project_ws, fq_filter_project_blocks_workspace_bytes(),
-                                                      prof ? e0 : nullptr, prof ? e1 : nullptr, ctx.stream())
-                    : fq_filter_project_blocks_async(&ic, B, pred, exprs.data(), (int32_t)exprs.size(), ptrs.data(),
-                                                     (int64_t *)layout->counts->ptr, res, ws->ptr, ws->bytes,
-                                                     prof ? e0 : nullptr, prof ? e1 : nullptr, ctx.stream());
-        if (st == FQ_OK) check_hip(hipEventRecord(done, ctx.stream()), "hipEventRecord");  // after the result copy
+        if (mode != 0) {
+            res[0] = kProjectPending;
+            res[1] = 0;
+        }
+        st = fqk::filter_project_blocks_enqueue(&ic, B, pred, exprs.data(), (int32_t)exprs.size(), ptrs.data(),
+                                                (int64_t *)layout->counts->ptr, res,
+                                                mode == 0 ? nullptr : ctx.res->project_dres,
+                                                mode == 0 ? ws->ptr : ctx.res->project_ws,
+                                                fq_filter_project_blocks_workspace_bytes(), e0, e1, ctx.stream());
+        if (st == FQ_OK && done) check_hip(hipEventRecord(done, ctx.stream()), "hipEventRecord");  // after the result words
     }
     if (st == FQ_OK) {
-        hipError_t he = hipEventSynchronize(done);
+        hipError_t he = hipSuccess;
+        if (done) {
+            he = hipEventSynchronize(done);
+        } else {
+            // the hand-off kernel runs after the projection kernel on this
+            // queue and writes the count last: once it is there, so are the
+            // flags and the projected columns
+            volatile uint64_t *w = res;
+            for (int spin = 0; w[0] == kProjectPending; ++spin) {
+                if (spin < 2000) {
+                    __builtin_ia32_pause();
+                } else {
+                    he = hipStreamQuery(ctx.stream());  // a failed queue never writes the words
+                    if (he != hipSuccess && he != hipErrorNotReady) break;
+                    he = hipSuccess;
+                    std::this_thread::sleep_for(std::chrono::microseconds(2));
+                }
+            }
+            std::atomic_thread_fence(std::memory_order_acquire);
+        }
         if (he == hipSuccess && prof) {
             float ms = 0;
             if (hipEventElapsedTime(&ms, e0, e1) == hipSuccess) ctx.rt->stats.project_ns += (uint64_t)((double)ms * 1e6);
         }
-        check_hip(he, "hipEventSynchronize");
+        check_hip(he, done ? "hipEventSynchronize" : "hipStreamQuery");
     }
-    ctx.res->give_event(e0);
-    ctx.res->give_event(e1);
-    ctx.res->give_sync_event(done);
+    if (e0) ctx.res->give_event(e0);
+    if (e1) ctx.res->give_event(e1);
+    if (done) ctx.res->give_sync_event(done);
     if (st == FQ_E_UNSUPPORTED) return false;  // the unfused path evaluates it (and raises what the reference does)
     check_fq(st);
     int64_t kept = 0;
-    check_fq(fq_filter_project_blocks_result(res, &kept));
+    check_fq(fqk::filter_project_blocks_result(res, &kept));
     layout->rows = kept;
     auto &S = ctx.rt->stats;
     S.project_launches++;
@@ -815,7 +828,7 @@ static bool project_blocks(const DataBlock &b, const Column &c, const fq_pred *p
     out.schema = schema;
     out.sub_block_rows = B;
     out.layout = layout;
-    out.ready = true;  // this pipe waited for the launch (done) above
+    out.ready = true;  // this pipe waited for the launch above
     for (auto &o : outs) out.columns.push_back(o);
     return true;
 }
@@ -892,7 +905,6 @@ ScanGroup::~ScanGroup() {
     for (auto &s : queues_) {
         rt_->give_event(s.start);
         rt_->give_event(s.end);
-        rt_->give_event(s.fold_end);
     }
 }
 
@@ -910,16 +922,7 @@ void ScanGroup::before_launch(ExecCtx &ctx) {
     queues_.push_back(s);
 }
 
-void ScanGroup::note_fold(hipStream_t q, hipStream_t fold) {
-    std::lock_guard<std::mutex> lk(mu_);
-    for (QueueSpan &s : queues_)
-        if (s.q == q) {
-            s.fold = fold;
-            s.folded = true;
-        }
-}
-
-void ScanGroup::arrive(bool wait) {
+void ScanGroup::arrive(bool wait) noexcept {
     std::unique_lock<std::mutex> lk(mu_);
     if (--left_ > 0) {
         if (wait) cv_.wait(lk, [&] { return closed_; });
@@ -930,18 +933,25 @@ void ScanGroup::arrive(bool wait) {
     // takes mu_ under a queue's launch lock)
     std::vector<QueueSpan> qs = queues_;
     lk.unlock();
+    std::string err;
     for (QueueSpan &s : qs) {
-        std::lock_guard<std::mutex> ql(*s.launch_mu);
-        if (s.fold && s.folded) {  // the last scan's fold ran beside it (fq_aggregate_split)
-            s.fold_end = rt_->take_event();
-            check_hip(hipEventRecord(s.fold_end, s.fold), "hipEventRecord");
-            check_hip(hipStreamWaitEvent(s.q, s.fold_end, 0), "hipStreamWaitEvent");
+        try {
+            std::lock_guard<std::mutex> ql(*s.launch_mu);
+            s.end = rt_->take_event();
+            check_hip(hipEventRecord(s.end, s.q), "hipEventRecord");
+        } catch (const std::exception &e) {
+            // this queue's end is unknown: wait_end synchronises the queue itself
+            if (err.empty()) err = e.what();
+            if (s.end) rt_->give_event(s.end);
+            s.end = nullptr;
+        } catch (...) {
+            if (err.empty()) err = "Internal Error: unknown exception recording a scan group's end";
+            s.end = nullptr;
         }
-        s.end = rt_->take_event();
-        check_hip(hipEventRecord(s.end, s.q), "hipEventRecord");
     }
     lk.lock();
     queues_ = qs;
+    arrive_error_ = err;
     closed_ = true;
     cv_.notify_all();
 }
@@ -956,22 +966,24 @@ void ScanGroup::wait_end() {
     if (waiter_) {
         cv_.wait(lk, [&] { return ended_; });
         if (end_error_ != hipSuccess) check_hip(end_error_, "hipEventSynchronize");
+        if (!arrive_error_.empty()) throw FQException(FQ_E_HIP, arrive_error_);
         return;
     }
     waiter_ = true;
-    std::vector<hipEvent_t> ends;
-    for (const QueueSpan &s : queues_) ends.push_back(s.end);
+    std::vector<QueueSpan> qs = queues_;
     lk.unlock();
     hipError_t err = hipSuccess;
-    for (hipEvent_t e : ends)
-        if (e && err == hipSuccess) err = hipEventSynchronize(e);
+    for (const QueueSpan &s : qs)
+        if (err == hipSuccess) err = s.end ? hipEventSynchronize(s.end) : hipStreamSynchronize(s.q);
     if (rt_->profile.load(std::memory_order_relaxed) == 2) rt_->stats.scan_end_seen = now_ns();
     lk.lock();
     ended_ = true;
     end_error_ = err;
     cv_.notify_all();
+    const std::string arrive_error = arrive_error_;
     lk.unlock();
     check_hip(err, "hipEventSynchronize");
+    if (!arrive_error.empty()) throw FQException(FQ_E_HIP, arrive_error);
 }
 
 void ScanGroup::account() {
@@ -1027,7 +1039,6 @@ void AggFusion::wait_launched() {
     hipEvent_t done = res_->take_sync_event();
     {
         std::lock_guard<std::mutex> lk(*res_->launch_mu);
-        res_->ws_ready(stream_);  // a fold on the fold queue wrote a result too
         check_hip(hipEventRecord(done, stream_), "hipEventRecord");
     }
     hipError_t e = hipEventSynchronize(done);
@@ -1115,27 +1126,10 @@ void AggFusion::end_block() {
             std::lock_guard<std::mutex> lk(*ctx_.res->launch_mu);
             const fq_pred *pred = g.has_pred ? g.pred.get() : nullptr;
             const fq_expr *val = g.value.expr.n_steps ? &g.value.expr : nullptr;
-            const uint32_t mask = g.mask | engine_one_launch();
             if (ticket_ && ticket_->group()) ticket_->group()->before_launch(ctx_);
-            res_->ws_ready(stream_);  // the workspace's last fold has read its partials
             if (pairs) check_hip(hipEventRecord(e0, stream_), "hipEventRecord");
-            if (!pairs && ticket_ && ticket_->group() && !(mask & FQ_AGG_ONE_LAUNCH) &&
-                fqc::knob(FQ_TUNE_ENGINE_FOLD_STREAM) && stream_ == res_->stream) {
-                rt_->fold_queue(res_);
-                // the fold on the queue's fold queue, beside the next scan; the
-                // group's end waits for the fold queue too (ScanGroup::arrive).
-                // Off by default: 8 scans 11.11 ms against 11.05 with the fold
-                // on the scan's queue, the C3 step 11.62 against 11.56
-                // (profiles/r05_h_scan_fin_ab.json)
-                check_fq(fq_aggregate_split(&c, g.block_rows, pred, val, mask, (fq_agg_state *)dst, res_->ws,
-                                            res_->ws_bytes, stream_, res_->fold, res_->scan_done));
-                check_hip(hipEventRecord(res_->fold_done, res_->fold), "hipEventRecord");
-                res_->fold_pending = true;
-                ticket_->group()->note_fold(stream_, res_->fold);
-            } else {
-                check_fq(fq_aggregate(&c, g.block_rows, pred, val, mask, (fq_agg_state *)dst, res_->ws,
-                                      res_->ws_bytes, stream_));
-            }
+            check_fq(fq_aggregate(&c, g.block_rows, pred, val, g.mask, (fq_agg_state *)dst, res_->ws, res_->ws_bytes,
+                                  stream_));
             if (pairs) check_hip(hipEventRecord(e1, stream_), "hipEventRecord");
         }
         launched_ = true;

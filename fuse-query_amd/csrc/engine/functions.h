@@ -305,12 +305,13 @@ class ScanGroup {
     ScanGroup &operator=(const ScanGroup &) = delete;
     // a launch on ctx's queue follows (called under the queue's launch lock)
     void before_launch(ExecCtx &ctx);
-    // that launch folded its partials on the queue's fold queue (same lock)
-    void note_fold(hipStream_t q, hipStream_t fold);
-    // a pipe has enqueued everything it will.  The last one to arrive records
-    // an end event on every queue the group launched on; with `wait` the
-    // others block until it has (a failing pipe leaves without waiting).
-    void arrive(bool wait);
+    // a pipe has enqueued everything it will (or failed, or never started).
+    // The last one to arrive records an end event on every queue the group
+    // launched on; with `wait` the others block until it has (a failing pipe
+    // leaves without waiting).  Never throws: a failure to record an end event
+    // is kept and reported by wait_end, and the group closes either way, so no
+    // pipe waits for a group that cannot close (it runs from destructors).
+    void arrive(bool wait) noexcept;
     // every queue the group launched on, done (after arrive)
     void wait_end();
     // after wait_end: the spans' time into scan_ns (once per query)
@@ -319,10 +320,8 @@ class ScanGroup {
    private:
     struct QueueSpan {
         hipStream_t q = nullptr;
-        hipStream_t fold = nullptr;  // q's fold queue: the end waits for it when `folded`
-        bool folded = false;         // a scan on q folded there (fq_aggregate_split)
         std::mutex *launch_mu = nullptr;
-        hipEvent_t start = nullptr, end = nullptr, fold_end = nullptr;
+        hipEvent_t start = nullptr, end = nullptr;
     };
     Runtime *rt_;
     std::mutex mu_;
@@ -331,13 +330,16 @@ class ScanGroup {
     bool closed_ = false, accounted_ = false;
     bool waiter_ = false, ended_ = false;  // wait_end: one pipe waits on the events
     hipError_t end_error_ = hipSuccess;
+    std::string arrive_error_;       // the last arrival could not record an end event
     std::vector<QueueSpan> queues_;  // stable once every pipe has arrived
 };
 using ScanGroupRef = std::shared_ptr<ScanGroup>;
 
 // One pipe's place in a ScanGroup: arrives exactly once -- from
 // AggFusion::finish, or (a pipe that fails) when it goes out of scope, so the
-// other pipes never wait for a pipe that is gone.
+// other pipes never wait for a pipe that is gone.  A pipe that fails before
+// it makes its ticket (its ExecCtx could not be set up) arrives through
+// AggregatePartialTransform::abandon instead.
 class ScanTicket {
    public:
     explicit ScanTicket(ScanGroup *g) : g_(g) {}

@@ -305,6 +305,18 @@ class ChannelStream : public BlockStream {
     }
 };
 
+// A pipe's task failed: its error goes to the channel the way the reference's
+// task sends its Err (processor_merge.rs:50-54), and the pipe's processor
+// releases what the other pipes wait on.
+static void pipe_failed(const ProcessorRef &in, const std::shared_ptr<Channel> &ch, size_t pipe, const FQException &e) {
+    in->abandon();
+    Channel::Item it;
+    it.is_err = true;
+    it.pipe = pipe;
+    it.err = e;
+    ch->send_error(std::move(it));
+}
+
 // MergeProcessor::execute (processor_merge.rs:37-66): one host thread per
 // input pipe (the tokio::spawn), each with its own device context.
 StreamRef MergeProcessor::execute() {
@@ -321,6 +333,8 @@ StreamRef MergeProcessor::execute() {
         const bool own = own_queues_;
         return [in, ch, rt, pipe, own]() {
             try {
+                if (rt->fault_pipe.load(std::memory_order_relaxed) == (int64_t)pipe + 1)
+                    throw FQException(FQ_E_HIP, "hipMalloc(workspace): out of memory (FQ_OPT_FAULT_PIPE)");
                 ExecCtx ctx(rt, own);
                 StreamRef s = in->execute();
                 DataBlock b;
@@ -339,23 +353,11 @@ StreamRef MergeProcessor::execute() {
                     if (!ch->send(std::move(it))) break;
                 }
             } catch (const FQException &e) {
-                Channel::Item it;
-                it.is_err = true;
-                it.pipe = pipe;
-                it.err = e;
-                ch->send_error(std::move(it));
+                pipe_failed(in, ch, pipe, e);
             } catch (const std::exception &e) {
-                Channel::Item it;
-                it.is_err = true;
-                it.pipe = pipe;
-                it.err = FQException(FQ_E_INTERNAL, std::string("Internal Error: ") + e.what());
-                ch->send_error(std::move(it));
+                pipe_failed(in, ch, pipe, FQException(FQ_E_INTERNAL, std::string("Internal Error: ") + e.what()));
             } catch (...) {  // every pipe reports done, or the consumer waits for it forever
-                Channel::Item it;
-                it.is_err = true;
-                it.pipe = pipe;
-                it.err = FQException(FQ_E_INTERNAL, "Internal Error: unknown exception in a pipe");
-                ch->send_error(std::move(it));
+                pipe_failed(in, ch, pipe, FQException(FQ_E_INTERNAL, "Internal Error: unknown exception in a pipe"));
             }
             ch->done();
         };
@@ -367,7 +369,20 @@ StreamRef MergeProcessor::execute() {
     // behind that ~1.4 ms scan anyway.  The channel holds every pipe's block,
     // so nothing here waits for the consumer.
     if (inline_first_) task(0)();
-    for (size_t pipe = inline_first_ ? 1 : 0; pipe < list_.size(); ++pipe) rt->pool.submit(task(pipe));
+    for (size_t pipe = inline_first_ ? 1 : 0; pipe < list_.size(); ++pipe) {
+        try {
+            rt->pool.submit(task(pipe));
+        } catch (const std::exception &e) {
+            // this pipe and the ones after it never run: each reports its
+            // failure and is done, so the consumer and the scan group do not
+            // wait for them
+            for (size_t p = pipe; p < list_.size(); ++p) {
+                pipe_failed(list_[p], cs->ch, p, FQException(FQ_E_INTERNAL, std::string("Internal Error: ") + e.what()));
+                cs->ch->done();
+            }
+            break;
+        }
+    }
     return cs;
 }
 
@@ -449,9 +464,13 @@ Column partial_states(const std::vector<FunctionRef> &funcs) {
 }
 }  // namespace
 
+void AggregatePartialTransform::abandon() {
+    if (!entered_.exchange(true) && group_) group_->arrive(false);
+}
+
 StreamRef AggregatePartialTransform::execute() {
     // this pipe's place in the query's ScanGroup: arrives once, also when it fails
-    ScanTicket ticket(group_.get());
+    ScanTicket ticket(entered_.exchange(true) ? nullptr : group_.get());
     std::vector<FunctionRef> funcs;
     for (auto &f : funcs_) funcs.push_back(f->clone());
     ExecCtx &ctx = ExecCtx::current();

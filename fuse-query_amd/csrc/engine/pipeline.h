@@ -154,6 +154,10 @@ class IProcessor {
     virtual void connect_to(std::shared_ptr<IProcessor> input) = 0;
     virtual StreamRef execute() = 0;
     virtual std::string format(FormatterSettings &s) const;
+    // the pipe this processor ends failed before (or without) running
+    // execute(): release whatever other pipes wait on (MergeProcessor calls it
+    // from the failing pipe's task)
+    virtual void abandon() {}
 };
 using ProcessorRef = std::shared_ptr<IProcessor>;
 
@@ -237,12 +241,17 @@ class AggregatePartialTransform : public IProcessor {  // transform_aggregate_pa
     std::string name() const override { return "AggregatePartialTransform"; }
     void connect_to(ProcessorRef input) override { input_ = std::move(input); }
     StreamRef execute() override;
+    // a pipe whose ExecCtx could not be set up never reaches execute(): its
+    // place in the scan group arrives here, so the other pipes' deferred
+    // states (ScanGroup::wait_end) do not wait for it
+    void abandon() override;
 
    private:
     SchemaRef schema_;
     std::vector<FunctionRef> funcs_;
     ProcessorRef input_;
     ScanGroupRef group_;
+    std::atomic<bool> entered_{false};  // execute() took this pipe's ScanTicket
 };
 
 class AggregateFinalTransform : public IProcessor {  // transform_aggregate_final.rs:18-79

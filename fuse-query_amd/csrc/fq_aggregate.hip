@@ -128,11 +128,8 @@ __device__ __forceinline__ uint32_t process(const TIn (&x)[M], const int64_t (&i
 }
 
 // wave butterfly + LDS combine; thread 0 of the workgroup stores the result
-// (write_through: six 8-byte agent-scope stores, sc1 -- the in-launch
-// finalize's form 1, which then needs no release fence)
 template <typename V>
-__device__ __forceinline__ void reduce_and_store(Acc<V> &acc, Partial *out, int32_t dtype,
-                                                 bool write_through = false) {
+__device__ __forceinline__ void reduce_and_store(Acc<V> &acc, Partial *out, int32_t dtype) {
 #pragma unroll
     for (int off = kWave / 2; off > 0; off >>= 1) {
         acc.sum = acc.sum + shfl_xor64(acc.sum, off);
@@ -173,24 +170,16 @@ __device__ __forceinline__ void reduce_and_store(Acc<V> &acc, Partial *out, int3
         p.blocks = 0;
         p.flags = flags;
         p.dtype = dtype;
-        if (write_through) {
-            uint64_t w[6];
-            __builtin_memcpy(w, &p, sizeof p);
-            uint64_t *o = reinterpret_cast<uint64_t *>(out);
-#pragma unroll
-            for (int i = 0; i < 6; ++i) __hip_atomic_store(o + i, w[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            *out = p;
-        }
+        *out = p;
     }
 }
 
 // The launch's partials folded in a fixed order by ONE workgroup: thread t
-// folds partials t, t+256, ... then the wave butterfly and the LDS combine --
-// the same order in the separate finalize launch and in the last workgroup
-// of a FQ_AGG_ONE_LAUNCH scan, so both give the same bytes (float sums too).
-// `parts` is read with vector loads (no const/__restrict__: in the in-launch
-// fold they are other workgroups' stores, behind an agent-scope acquire).
+// folds partials t, t+256, ... then the wave butterfly and the LDS combine,
+// so a grid gives the same bytes run to run (float sums too).  An in-launch
+// fold by the scan's last workgroup (agent-scope release / ticket / acquire)
+// measured slower than this separate 4.4 us launch: 8 scans 11.07 against
+// 11.02 ms (profiles/r05_b_scan_fin_ab.json), and was removed in round 6.
 template <typename V>
 __device__ __forceinline__ void fold_partials(Partial *parts, int nparts, uint64_t blocks, uint64_t rows,
                                               int32_t vdtype, int empty_if_zero, fq_agg_state *out) {
@@ -222,37 +211,6 @@ __device__ __forceinline__ void fold_partials(Partial *parts, int nparts, uint64
     }
 }
 
-// In-launch finalize (Fin, fq_scan.h): called by every workgroup right after
-// reduce_and_store wrote its Partial (thread 0's store).  The hand-off is the
-// agent-scope release / ticket / acquire of the CDNA guide's split-K recipe:
-// thread 0 drains its store, releases at agent scope (the XCD L2 written
-// back), waits again (the fence's own wait can be dropped), then draws a
-// ticket; the workgroup that draws grid - 1 acquires at agent scope and folds
-// every partial.  Correct wherever the workgroups ran, whatever XCD.
-template <typename V>
-__device__ __forceinline__ void finish_in_launch(Partial *parts, int32_t vdtype, const Fin &fin) {
-    __shared__ uint32_t s_last;
-    if (threadIdx.x == 0) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (fin.form == 0) {  // plain store: write the XCD L2 back (form 1 stored write-through)
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        const uint32_t t = __hip_atomic_fetch_add(fin.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint32_t last = t == gridDim.x - 1u ? 1u : 0u;
-        if (last) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        s_last = last;
-    }
-    __syncthreads();
-    if (!s_last) return;
-    fold_partials<V>(parts, (int)gridDim.x, fin.blocks, 0ull, vdtype, fin.empty_if_zero, fin.out);
-    // every workgroup has drawn its ticket: the counter is free for the next launch
-    if (threadIdx.x == 0) __hip_atomic_store(fin.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 // Flat streaming mode: grid-stride over 16-byte vectors, U vectors in flight
@@ -260,7 +218,7 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 template <typename TIn, typename V, int PRED, bool CHAIN, int U>
 __global__ void __launch_bounds__(kThreads)
     agg_flat_kernel(const TIn *__restrict__ col, int64_t n, int64_t head, KPred pred, KProg val,
-                    uint32_t mask, int32_t vdtype, Partial *parts, Fin fin) {
+                    uint32_t mask, int32_t vdtype, Partial *parts) {
     constexpr int VE = 16 / sizeof(TIn);
     constexpr int E = VE * U;
     static_assert(E <= 32, "pass mask is 32 bits");
@@ -312,8 +270,7 @@ __global__ void __launch_bounds__(kThreads)
         int64_t idx[1] = {i};
         process<TIn, V, PRED, CHAIN, 1>(x, idx, 1u, pred, val, mask, acc);
     }
-    reduce_and_store<V>(acc, parts + blockIdx.x, vdtype, fin.done && fin.form == 1);
-    if (fin.done) finish_in_launch<V>(parts, vdtype, fin);
+    reduce_and_store<V>(acc, parts + blockIdx.x, vdtype);
 }
 
 // Block mode: one wave owns whole reference blocks of R rows; one ballot per
@@ -321,7 +278,7 @@ __global__ void __launch_bounds__(kThreads)
 template <typename TIn, typename V, int PRED, bool CHAIN, int U>
 __global__ void __launch_bounds__(kThreads)
     agg_block_kernel(const TIn *__restrict__ col, int64_t n, int64_t R, KPred pred, KProg val,
-                     uint32_t mask, int32_t vdtype, Partial *parts, Fin fin) {
+                     uint32_t mask, int32_t vdtype, Partial *parts) {
     Acc<V> acc;
     acc.init();
     const int lane = threadIdx.x & (kWave - 1);
@@ -350,8 +307,7 @@ __global__ void __launch_bounds__(kThreads)
         }
         if (__ballot(any != 0) == 0ull) acc.flags |= FQ_STATE_ANY_EMPTY;
     }
-    reduce_and_store<V>(acc, parts + blockIdx.x, vdtype, fin.done && fin.form == 1);
-    if (fin.done) finish_in_launch<V>(parts, vdtype, fin);
+    reduce_and_store<V>(acc, parts + blockIdx.x, vdtype);
 }
 
 // Single workgroup, fixed order (fold_partials): the result is deterministic
@@ -633,11 +589,11 @@ static fq_status launch_scan(const Launch &L) {
     if (PRED != FQ_PRED_NONE && L.block_mode) {
         hipLaunchKernelGGL((agg_block_kernel<TIn, V, PRED, CHAIN, 8>), dim3(L.grid), dim3(kThreads), 0,
                            L.stream, (const TIn *)L.col, L.n, L.block_rows, L.pred, L.val, L.mask,
-                           L.vdtype, L.parts, L.fin);
+                           L.vdtype, L.parts);
     } else {
         hipLaunchKernelGGL((agg_flat_kernel<TIn, V, PRED, CHAIN, U>), dim3(L.grid), dim3(kThreads), 0,
                            L.stream, (const TIn *)L.col, L.n, L.head, L.pred, L.val, L.mask, L.vdtype,
-                           L.parts, L.fin);
+                           L.parts);
     }
     FQ_HIP_TRY(hipGetLastError());
     return FQ_OK;
@@ -722,15 +678,7 @@ extern "C" {
 
 size_t fq_aggregate_workspace_bytes(int64_t len) {
     (void)len;
-    return fqk::kPartialsBytes + fqk::kCounterBytes;
-}
-
-fq_status fq_aggregate_workspace_init(void *d_ws, size_t ws_bytes, void *stream) {
-    if (!d_ws) return fqc::fail(FQ_E_INVALID, "fq_aggregate_workspace_init: NULL workspace");
-    if (ws_bytes < fq_aggregate_workspace_bytes(0))
-        return fqc::fail(FQ_E_INVALID, "fq_aggregate_workspace_init: workspace too small");
-    FQ_HIP_TRY(hipMemsetAsync((char *)d_ws + fqk::kPartialsBytes, 0, fqk::kCounterBytes, (hipStream_t)stream));
-    return FQ_OK;
+    return fqk::kPartialsBytes;
 }
 
 }  // extern "C"
@@ -802,19 +750,13 @@ static fq_status plan_scan(const fq_col *col, int64_t block_rows, const fq_pred 
     return FQ_OK;
 }
 
-// fq_aggregate / fq_aggregate_split: the scan on `stream`; the fold of its
-// partials on `stream` too, or (fold != nullptr) on `fold` behind `scan_done`
+// fq_aggregate: the scan, then the fold of its partials, both on `stream`
 static fq_status aggregate(const fq_col *col, int64_t block_rows, const fq_pred *pred, const fq_expr *value,
-                           uint32_t agg_mask, fq_agg_state *d_out, void *d_ws, size_t ws_bytes, hipStream_t stream,
-                           hipStream_t fold, hipEvent_t scan_done) {
+                           uint32_t agg_mask, fq_agg_state *d_out, void *d_ws, size_t ws_bytes, hipStream_t stream) {
     if (!col || !d_out || !d_ws) return fqc::fail(FQ_E_INVALID, "fq_aggregate: NULL argument");
-    const bool one_launch = (agg_mask & FQ_AGG_ONE_LAUNCH) != 0;
-    if (one_launch && fold) return fqc::fail(FQ_E_INVALID, "fq_aggregate_split: FQ_AGG_ONE_LAUNCH has no fold");
-    agg_mask &= ~FQ_AGG_ONE_LAUNCH;
-    // one_launch needs the counter behind the partials; without it a
-    // pre-counter workspace (kPartialsBytes) still serves the two launches
-    if (ws_bytes < (one_launch ? fq_aggregate_workspace_bytes(col->len) : kPartialsBytes))
-        return fqc::fail(FQ_E_INVALID, "fq_aggregate: workspace too small");
+    if (ws_bytes < kPartialsBytes) return fqc::fail(FQ_E_INVALID, "fq_aggregate: workspace too small");
+    if (agg_mask & ~(uint32_t)(FQ_AGG_MIN | FQ_AGG_MAX | FQ_AGG_SUM | FQ_AGG_COUNT))
+        return fqc::fail(FQ_E_INVALID, "fq_aggregate: unknown bits in agg_mask");
     Launch L;
     bool chain = false;
     uint64_t blocks = 0;
@@ -826,13 +768,6 @@ static fq_status aggregate(const fq_col *col, int64_t block_rows, const fq_pred 
     if (agg_mask == FQ_AGG_COUNT && !chain && L.pred.kind == FQ_PRED_NONE) {
         L.grid = 0;  // count(column): rows, not values (see launch_finalize)
         return dispatch_finalize(L, blocks, empty_if_zero, d_out);
-    }
-    if (one_launch) {
-        L.fin.done = (uint32_t *)((char *)d_ws + kPartialsBytes);
-        L.fin.out = d_out;
-        L.fin.blocks = blocks;
-        L.fin.empty_if_zero = empty_if_zero;
-        L.fin.form = (int32_t)fqc::knob(FQ_TUNE_SCAN_FIN);
     }
     bool jitted = false;
     const bool tree = (chain && prog_has_tree(L.val)) || pred_has_tree(L.pred);
@@ -846,12 +781,6 @@ static fq_status aggregate(const fq_col *col, int64_t block_rows, const fq_pred 
         s = dispatch(col->dtype, L, chain);
         if (s != FQ_OK) return s;
     }
-    if (one_launch) return FQ_OK;  // the scan's last workgroup wrote *d_out
-    if (fold) {
-        FQ_HIP_TRY(hipEventRecord(scan_done, stream));
-        FQ_HIP_TRY(hipStreamWaitEvent(fold, scan_done, 0));
-        L.stream = fold;
-    }
     return dispatch_finalize(L, blocks, empty_if_zero, d_out);
 }
 
@@ -861,24 +790,13 @@ extern "C" {
 
 fq_status fq_aggregate(const fq_col *col, int64_t block_rows, const fq_pred *pred, const fq_expr *value,
                        uint32_t agg_mask, fq_agg_state *d_out, void *d_ws, size_t ws_bytes, void *stream) {
-    return fqk::aggregate(col, block_rows, pred, value, agg_mask, d_out, d_ws, ws_bytes, (hipStream_t)stream,
-                          nullptr, nullptr);
-}
-
-fq_status fq_aggregate_split(const fq_col *col, int64_t block_rows, const fq_pred *pred, const fq_expr *value,
-                             uint32_t agg_mask, fq_agg_state *d_out, void *d_ws, size_t ws_bytes, void *stream,
-                             void *fold_stream, void *scan_done) {
-    if (!fold_stream || !scan_done) return fqc::fail(FQ_E_INVALID, "fq_aggregate_split: NULL fold stream or event");
-    if (fold_stream == stream) return fqc::fail(FQ_E_INVALID, "fq_aggregate_split: the fold stream is the scan's");
-    return fqk::aggregate(col, block_rows, pred, value, agg_mask, d_out, d_ws, ws_bytes, (hipStream_t)stream,
-                          (hipStream_t)fold_stream, (hipEvent_t)scan_done);
+    return fqk::aggregate(col, block_rows, pred, value, agg_mask, d_out, d_ws, ws_bytes, (hipStream_t)stream);
 }
 
 fq_status fq_jit_prepare(const fq_col *col, int64_t block_rows, const fq_pred *pred, const fq_expr *value,
                          uint32_t agg_mask, int32_t *specialised) {
     using namespace fqk;
     if (specialised) *specialised = 0;
-    agg_mask &= ~FQ_AGG_ONE_LAUNCH;  // the same kernel serves both finalize forms
     Launch L;
     bool chain = false;
     uint64_t blocks = 0;

@@ -54,3 +54,22 @@ bool cast_scalar(uint64_t bits, int32_t from, int32_t to, uint64_t *out);
         hipError_t fq_e_ = (expr);                                \
         if (fq_e_ != hipSuccess) return fqc::hip_fail(fq_e_, #expr); \
     } while (0)
+
+// Internal entry points the engine calls beside the C ABI (fq_filter.hip).
+namespace fqk {
+// fq_filter_project_blocks without waiting (the engine's ProjectionTransform,
+// which keeps one queue busy with several pipes' launches): enqueued on
+// `stream`; when the stream reaches it, {kept rows, flag words} land in
+// h_result[0..1] (pinned host memory), to be turned into the call's status
+// and row count by filter_project_blocks_result after waiting.  ev_start /
+// ev_end (optional) bracket the kernel alone.  d_result == nullptr: the
+// workspace is zeroed before the kernel and the words copied after it; else
+// d_result is the device address of h_result (mapped host memory), the
+// workspace is zero already (zeroed once by the caller) and a one-thread
+// kernel after the projection hands the words over and re-zeroes it.
+fq_status filter_project_blocks_enqueue(const fq_col *col, int64_t block_rows, const fq_pred *pred,
+                                        const fq_expr *values, int32_t n_out, void *const *d_out, int64_t *d_counts,
+                                        uint64_t *h_result, uint64_t *d_result, void *d_ws, size_t ws_bytes,
+                                        void *ev_start, void *ev_end, void *stream);
+fq_status filter_project_blocks_result(const uint64_t *h_result, int64_t *out_len);
+}  // namespace fqk

@@ -236,17 +236,6 @@ __global__ void __launch_bounds__(256)
     flush_flags(flags, flag);
 }
 
-// interleave two 32-bit ballots into one 64-row bitmap word (x -> even bits)
-__device__ __forceinline__ uint64_t spread32(uint32_t v) {
-    uint64_t x = v;
-    x = (x | (x << 16)) & 0x0000FFFF0000FFFFull;
-    x = (x | (x << 8)) & 0x00FF00FF00FF00FFull;
-    x = (x | (x << 4)) & 0x0F0F0F0F0F0F0F0Full;
-    x = (x | (x << 2)) & 0x3333333333333333ull;
-    x = (x | (x << 1)) & 0x5555555555555555ull;
-    return x;
-}
-
 // A wave compares 8 x 128 rows per iteration (lane l holds rows 2l and 2l+1
 // of each 128-row segment in one 16-byte load; 8 loads in flight) and lanes
 // 0..15 store the segments' 16 bitmap words (128 contiguous bytes).
@@ -255,8 +244,8 @@ __device__ __forceinline__ uint64_t spread32(uint32_t v) {
 // lane l the two results of lane l >> 1 (word 0) and of lane 32 + (l >> 1)
 // (word 1), so each word is a single ballot; interleaving two 32-bit ballots
 // on the scalar unit instead (spread32, 4 per segment) cost 1.68 vs 1.55 ms
-// per 10 GB (tools/bench_kernels.py; FQ_TUNE_CMP_SPREAD=1 keeps it for A/B).
-template <typename TC, int CMP, bool LSC, bool RSC, bool SPREAD>
+// per 10 GB (tools/bench_kernels.py, round 1; removed in round 6).
+template <typename TC, int CMP, bool LSC, bool RSC>
 __global__ void __launch_bounds__(256)
     compare_vec_kernel(const TC *__restrict__ l, uint64_t lc, const TC *__restrict__ r, uint64_t rc,
                        uint64_t *__restrict__ bitmap, int64_t ngroups) {
@@ -284,19 +273,11 @@ __global__ void __launch_bounds__(256)
             else x[0] = x[1] = lconst;
             if constexpr (!RSC) __builtin_memcpy(y, &b[k], 16);
             else y[0] = y[1] = rconst;
-            uint64_t w0, w1;
-            if constexpr (SPREAD) {
-                const uint64_t b0 = __ballot(compare<TC>(CMP, x[0], y[0]));
-                const uint64_t b1 = __ballot(compare<TC>(CMP, x[1], y[1]));
-                w0 = spread32((uint32_t)b0) | (spread32((uint32_t)b1) << 1);
-                w1 = spread32((uint32_t)(b0 >> 32)) | (spread32((uint32_t)(b1 >> 32)) << 1);
-            } else {
-                const int two = (compare<TC>(CMP, x[0], y[0]) ? 1 : 0) | (compare<TC>(CMP, x[1], y[1]) ? 2 : 0);
-                const int lo = __builtin_amdgcn_ds_bpermute((lane >> 1) << 2, two);
-                const int hi = __builtin_amdgcn_ds_bpermute((32 + (lane >> 1)) << 2, two);
-                w0 = __ballot((lo >> (lane & 1)) & 1);
-                w1 = __ballot((hi >> (lane & 1)) & 1);
-            }
+            const int two = (compare<TC>(CMP, x[0], y[0]) ? 1 : 0) | (compare<TC>(CMP, x[1], y[1]) ? 2 : 0);
+            const int lo = __builtin_amdgcn_ds_bpermute((lane >> 1) << 2, two);
+            const int hi = __builtin_amdgcn_ds_bpermute((32 + (lane >> 1)) << 2, two);
+            const uint64_t w0 = __ballot((lo >> (lane & 1)) & 1);
+            const uint64_t w1 = __ballot((hi >> (lane & 1)) & 1);
             mine = lane == 2 * k ? w0 : mine;
             mine = lane == 2 * k + 1 ? w1 : mine;
         }
@@ -310,16 +291,9 @@ static void launch_vec_op(bool lsc, bool rsc, const void *l, uint64_t lc, const 
     const TC *L = (const TC *)l, *R = (const TC *)r;
     if constexpr (CMPK) {
         uint64_t *bm = (uint64_t *)out;
-        const bool spread = fqc::knob(FQ_TUNE_CMP_SPREAD) != 0;  // A/B: the scalar-unit interleave
-        if (spread) {
-            if (lsc) hipLaunchKernelGGL((compare_vec_kernel<TC, OP, true, false, true>), dim3(grid), dim3(256), 0, st, L, lc, R, rc, bm, units);
-            else if (rsc) hipLaunchKernelGGL((compare_vec_kernel<TC, OP, false, true, true>), dim3(grid), dim3(256), 0, st, L, lc, R, rc, bm, units);
-            else hipLaunchKernelGGL((compare_vec_kernel<TC, OP, false, false, true>), dim3(grid), dim3(256), 0, st, L, lc, R, rc, bm, units);
-        } else {
-            if (lsc) hipLaunchKernelGGL((compare_vec_kernel<TC, OP, true, false, false>), dim3(grid), dim3(256), 0, st, L, lc, R, rc, bm, units);
-            else if (rsc) hipLaunchKernelGGL((compare_vec_kernel<TC, OP, false, true, false>), dim3(grid), dim3(256), 0, st, L, lc, R, rc, bm, units);
-            else hipLaunchKernelGGL((compare_vec_kernel<TC, OP, false, false, false>), dim3(grid), dim3(256), 0, st, L, lc, R, rc, bm, units);
-        }
+        if (lsc) hipLaunchKernelGGL((compare_vec_kernel<TC, OP, true, false>), dim3(grid), dim3(256), 0, st, L, lc, R, rc, bm, units);
+        else if (rsc) hipLaunchKernelGGL((compare_vec_kernel<TC, OP, false, true>), dim3(grid), dim3(256), 0, st, L, lc, R, rc, bm, units);
+        else hipLaunchKernelGGL((compare_vec_kernel<TC, OP, false, false>), dim3(grid), dim3(256), 0, st, L, lc, R, rc, bm, units);
         (void)flag;
     } else {
         TC *O = (TC *)out;

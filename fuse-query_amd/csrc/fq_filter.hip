@@ -375,10 +375,10 @@ __global__ void block_lengths_kernel(int64_t *__restrict__ counts, int64_t nb, i
         counts[b] = b * B + B <= n ? B : n - b * B;
 }
 
-// fq_filter_project_blocks_launch with FQ_TUNE_PROJECT_HANDOFF 0: after the
-// projection kernel, one thread moves {kept rows, flag words} to d_res and
-// zeroes the three workspace words -- one launch in place of the next call's
-// memset and this call's copy.
+// filter_project_blocks_enqueue with a resident workspace: after the
+// projection kernel, one thread moves {kept rows, flag words} to d_res (host
+// memory the device writes) and zeroes the three workspace words -- one launch
+// in place of the next call's memset and this call's copy.
 __global__ void project_hand_off_kernel(uint64_t *__restrict__ ws, uint64_t *__restrict__ d_res) {
     if (threadIdx.x != 0) return;
     d_res[0] = ws[0];
@@ -470,8 +470,8 @@ blocks_copy_kernel(CompactCols cols, int32_t n_cols, const int64_t *__restrict__
 }
 
 // Workspace of fq_filter_project: [total][flag words: predicate,
-// expressions][kMaxSelectXcds ticket counters, a 128 B line each][one
-// look-back status word per tile].
+// expressions][the ticket counter, a 128 B line][one look-back status word
+// per tile].
 struct ProjWs {
     uint64_t *total;
     uint32_t *flags, *ticket;
@@ -485,7 +485,7 @@ ProjWs proj_ws(void *d_ws, int64_t n) {
     w.total = (uint64_t *)d_ws;
     w.flags = (uint32_t *)(w.total + 1);
     w.ticket = (uint32_t *)(w.total + 2);
-    w.status = w.total + 2 + 16 * kMaxSelectXcds;
+    w.status = w.total + 2 + 16;
     return w;
 }
 
@@ -532,7 +532,7 @@ extern "C" {
 
 size_t fq_filter_project_workspace_bytes(int64_t len) {
     const fqk::ProjWs w = fqk::proj_ws(nullptr, len < 0 ? 0 : len);
-    return (size_t)(2 + 16 * fqk::kMaxSelectXcds + w.ntiles) * sizeof(uint64_t);
+    return (size_t)(2 + 16 + w.ntiles) * sizeof(uint64_t);
 }
 
 fq_status fq_filter_project(const fq_col *col, const fq_pred *pred, const fq_expr *values, int32_t n_out,
@@ -579,16 +579,14 @@ fq_status fq_filter_project(const fq_col *col, const fq_pred *pred, const fq_exp
 
 size_t fq_filter_project_blocks_workspace_bytes(void) { return 3 * sizeof(uint64_t); }  // total, flags, ticket
 
-namespace {
-// fq_filter_project_blocks_async / _launch: d_result == nullptr -> the
-// workspace is zeroed before the kernel and the two result words copied after
-// it; else the workspace is zero already and the kernel's last workgroup
-// writes d_result and re-zeroes it.
-fq_status project_blocks_enqueue(const fq_col *col, int64_t block_rows, const fq_pred *pred, const fq_expr *values,
-                                 int32_t n_out, void *const *d_out, int64_t *d_counts, uint64_t *h_result,
-                                 uint64_t *d_result, void *d_ws, size_t ws_bytes, void *ev_start, void *ev_end,
-                                 void *stream) {
-    using namespace fqk;
+}  // extern "C"
+
+namespace fqk {
+
+fq_status filter_project_blocks_enqueue(const fq_col *col, int64_t block_rows, const fq_pred *pred,
+                                        const fq_expr *values, int32_t n_out, void *const *d_out, int64_t *d_counts,
+                                        uint64_t *h_result, uint64_t *d_result, void *d_ws, size_t ws_bytes,
+                                        void *ev_start, void *ev_end, void *stream) {
     static_assert(FQ_PROJECT_MIN_BLOCK_ROWS == kProjectBlockTile, "the ABI's minimum block is the kernel's tile");
     if (!h_result) return fqc::fail(FQ_E_INVALID, "fq_filter_project_blocks: NULL result words");
     h_result[0] = h_result[1] = 0;
@@ -608,12 +606,11 @@ fq_status project_blocks_enqueue(const fq_col *col, int64_t block_rows, const fq
         return fqc::fail(FQ_E_INVALID, "fq_filter_project_blocks: workspace too small");
     uint64_t *const total = (uint64_t *)d_ws;
     uint32_t *const flags = (uint32_t *)(total + 1);
-    uint32_t *const ticket = (uint32_t *)(total + 2), *const done = ticket + 1;
+    uint32_t *const ticket = (uint32_t *)(total + 2);
     hipStream_t st = P.stream;
     const int64_t nb = block_rows >= n ? 1 : (n + block_rows - 1) / block_rows;
-    const bool resident = d_result != nullptr && P.pred.kind != FQ_PRED_NONE;
-    const bool in_kernel = fqc::knob(FQ_TUNE_PROJECT_HANDOFF) != 0;  // else the one-thread kernel after it
-    if (!d_result || !resident) FQ_HIP_TRY(hipMemsetAsync(d_ws, 0, fq_filter_project_blocks_workspace_bytes(), st));
+    const bool resident = d_result != nullptr;
+    if (!resident) FQ_HIP_TRY(hipMemsetAsync(d_ws, 0, fq_filter_project_blocks_workspace_bytes(), st));
     if (ev_start) FQ_HIP_TRY(hipEventRecord((hipEvent_t)ev_start, st));
     if (P.pred.kind == FQ_PRED_NONE) {  // every row kept: outputs in place, counts = block lengths
         if ((s = jit_project_map(col->dtype, P, flags + 1)) != FQ_OK) return s;
@@ -623,52 +620,25 @@ fq_status project_blocks_enqueue(const fq_col *col, int64_t block_rows, const fq
         if (ev_end) FQ_HIP_TRY(hipEventRecord((hipEvent_t)ev_end, st));
         FQ_HIP_TRY(hipMemcpyAsync(&h_result[1], flags, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
         h_result[0] = (uint64_t)n;
-        // the map path used the flag words: zero again for a resident workspace
-        if (d_result) FQ_HIP_TRY(hipMemsetAsync(d_ws, 0, fq_filter_project_blocks_workspace_bytes(), st));
+        // the map kernel used the flag words: zero again for a resident workspace
+        if (resident) FQ_HIP_TRY(hipMemsetAsync(d_ws, 0, fq_filter_project_blocks_workspace_bytes(), st));
+        return FQ_OK;
+    }
+    if ((s = jit_project_blocks(col->dtype, P, block_rows, P.pred.kind == FQ_PRED_BITMAP ? P.pred.bitmap : nullptr,
+                                d_counts, flags, total, ticket)) != FQ_OK)
+        return s;
+    if (ev_end) FQ_HIP_TRY(hipEventRecord((hipEvent_t)ev_end, st));
+    if (resident) {
+        hipLaunchKernelGGL(project_hand_off_kernel, dim3(1), dim3(64), 0, st, total, d_result);
+        FQ_HIP_TRY(hipGetLastError());
     } else {
-        if ((s = jit_project_blocks(col->dtype, P, block_rows, P.pred.kind == FQ_PRED_BITMAP ? P.pred.bitmap : nullptr,
-                                    d_counts, flags, total, ticket, resident && in_kernel ? done : nullptr,
-                                    resident && in_kernel ? d_result : nullptr)) != FQ_OK)
-            return s;
-        if (ev_end) FQ_HIP_TRY(hipEventRecord((hipEvent_t)ev_end, st));
-        if (!resident) {
-            FQ_HIP_TRY(hipMemcpyAsync(h_result, total, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-        } else if (!in_kernel) {
-            hipLaunchKernelGGL(project_hand_off_kernel, dim3(1), dim3(64), 0, st, total, d_result);
-            FQ_HIP_TRY(hipGetLastError());
-        }
+        FQ_HIP_TRY(hipMemcpyAsync(h_result, total, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     }
     return FQ_OK;
 }
-}  // namespace
 
-fq_status fq_filter_project_blocks_async(const fq_col *col, int64_t block_rows, const fq_pred *pred,
-                                         const fq_expr *values, int32_t n_out, void *const *d_out, int64_t *d_counts,
-                                         uint64_t *h_result, void *d_ws, size_t ws_bytes, void *ev_start,
-                                         void *ev_end, void *stream) {
-    return project_blocks_enqueue(col, block_rows, pred, values, n_out, d_out, d_counts, h_result, nullptr, d_ws,
-                                  ws_bytes, ev_start, ev_end, stream);
-}
-
-fq_status fq_filter_project_blocks_workspace_init(void *d_ws, size_t ws_bytes, void *stream) {
-    if (!d_ws || ws_bytes < fq_filter_project_blocks_workspace_bytes())
-        return fqc::fail(FQ_E_INVALID, "fq_filter_project_blocks_workspace_init: workspace too small");
-    FQ_HIP_TRY(hipMemsetAsync(d_ws, 0, fq_filter_project_blocks_workspace_bytes(), (hipStream_t)stream));
-    return FQ_OK;
-}
-
-fq_status fq_filter_project_blocks_launch(const fq_col *col, int64_t block_rows, const fq_pred *pred,
-                                          const fq_expr *values, int32_t n_out, void *const *d_out, int64_t *d_counts,
-                                          uint64_t *h_result, uint64_t *d_result, void *d_ws, size_t ws_bytes,
-                                          void *ev_start, void *ev_end, void *stream) {
-    if (!d_result) return fqc::fail(FQ_E_INVALID, "fq_filter_project_blocks_launch: NULL device result address");
-    return project_blocks_enqueue(col, block_rows, pred, values, n_out, d_out, d_counts, h_result, d_result, d_ws,
-                                  ws_bytes, ev_start, ev_end, stream);
-}
-
-fq_status fq_filter_project_blocks_result(const uint64_t *h_result, int64_t *out_len) {
-    using namespace fqk;
-    if (!h_result || !out_len) return fqc::fail(FQ_E_INVALID, "fq_filter_project_blocks_result: NULL argument");
+fq_status filter_project_blocks_result(const uint64_t *h_result, int64_t *out_len) {
+    if (!h_result || !out_len) return fqc::fail(FQ_E_INVALID, "fq_filter_project_blocks: NULL result");
     *out_len = 0;
     const uint32_t pred_flags = (uint32_t)(h_result[1] & 0xffffffffu), val_flags = (uint32_t)(h_result[1] >> 32);
     fq_status s;
@@ -678,6 +648,10 @@ fq_status fq_filter_project_blocks_result(const uint64_t *h_result, int64_t *out
     return FQ_OK;
 }
 
+}  // namespace fqk
+
+extern "C" {
+
 fq_status fq_filter_project_blocks(const fq_col *col, int64_t block_rows, const fq_pred *pred, const fq_expr *values,
                                    int32_t n_out, void *const *d_out, int64_t *d_counts, int64_t *out_len, void *d_ws,
                                    size_t ws_bytes, void *stream) {
@@ -686,11 +660,11 @@ fq_status fq_filter_project_blocks(const fq_col *col, int64_t block_rows, const 
     uint64_t local[2] = {0, 0};
     uint64_t *const pinned = fqc::host_staging();
     uint64_t *const host = pinned ? pinned : local;  // kept rows, flag words
-    fq_status s = fq_filter_project_blocks_async(col, block_rows, pred, values, n_out, d_out, d_counts, host, d_ws,
-                                                 ws_bytes, nullptr, nullptr, stream);
+    fq_status s = fqk::filter_project_blocks_enqueue(col, block_rows, pred, values, n_out, d_out, d_counts, host,
+                                                     nullptr, d_ws, ws_bytes, nullptr, nullptr, stream);
     if (s != FQ_OK) return s;
     FQ_HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
-    return fq_filter_project_blocks_result(host, out_len);
+    return fqk::filter_project_blocks_result(host, out_len);
 }
 
 size_t fq_blocks_compact_workspace_bytes(int64_t n_blocks) {

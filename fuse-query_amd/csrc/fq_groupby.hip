@@ -450,7 +450,7 @@ static fq_status prepare_group(const fq_group_table *t, const fq_col *col, const
     // against 2.25 ms here, and the table holds twice the groups)
     G.lds_bytes = group_lds_bytes();
     G.threads = group_threads();
-    G.rowmap = (int)fqc::knob(FQ_TUNE_GROUP_ROWMAP);
+    G.rowmap = 1;  // lane-consecutive rows (row pairs per lane measured 1.6x slower)
     const int64_t nvec = (G.n - G.head) / 2;
     int64_t grid = (nvec + 4 * G.threads - 1) / (4 * G.threads);
     if (grid < 1) grid = 1;
@@ -546,10 +546,10 @@ fq_status fq_group_aggregate_partitioned(const fq_group_table *t, const fq_col *
         if (((int64_t)1 << sh) <= S) {
             G.range_bins = 1;
             lp_arg = log2_parts | (sh << 8);
-            // the bins pass's table then needs one bin's 2^sh slots only (FQ_TUNE_GBINS_FIT_LDS): a
+            // the bins pass's table then needs one bin's 2^sh slots only: a
             // smaller S, so more than one workgroup per CU fits its LDS
             const int64_t fit = ((int64_t)1 << sh) * 8 * (1 + G.n_aggs);
-            if (fqc::knob(FQ_TUNE_GBINS_FIT_LDS) && fit < G.lds_bytes) {
+            if (fit < G.lds_bytes) {
                 G.lds_bytes = (int)fit;
                 fitted = true;
             }
@@ -567,10 +567,10 @@ fq_status fq_group_aggregate_partitioned(const fq_group_table *t, const fq_col *
     X.q = part_region_blocks(G.n, tile, X.grid, 1 << log2_parts);
     if ((uint64_t)X.q * (uint64_t)X.grid > X.max_blocks)
         return fqc::fail(FQ_E_INTERNAL, "fq_group_aggregate_partitioned: partition regions exceed the workspace");
-    // more than one bins workgroup per CU only where both its table (fitted) and its registers (4-byte rows at
-    // FQ_TUNE_GBINS_ROWS = 4: 54 VGPRs) leave room for it: g2's kernel set 4.58 -> 4.46 ms per partition
+    // more than one bins workgroup per CU only where both its table (fitted) and its registers (4-byte rows, 4
+    // per thread: 54 VGPRs) leave room for it: g2's kernel set 4.58 -> 4.46 ms per partition
     // (profiles/r04_o_gbins_ab/)
-    const bool two = fitted && G.narrow && fqc::knob(FQ_TUNE_GBINS_ROWS) == 4;
+    const bool two = fitted && G.narrow;  // 4 rows per thread in the narrow bins pass (fq_jit.hip)
     X.bins_grid = fqc::device_cu_count() * (two ? (int)fqc::knob(FQ_TUNE_GBINS_WG_PER_CU) : 1);
     return jit_groupby_partitioned(col->dtype, G, X);
 }

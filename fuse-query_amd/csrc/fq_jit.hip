@@ -129,7 +129,7 @@ const Rtc &rtc() {
         Rtc x;
         RtcThread::get().run([&x] {
             void *h = nullptr;
-            if (fqc::knob(FQ_TUNE_JIT_ISOLATED)) {
+            {  // its own link namespace: hipRTC's LLVM never meets another copy in the process
                 const char *root = getenv("ROCM_PATH");
                 const std::string path = std::string(root && *root ? root : "/opt/rocm") + "/lib/libhiprtc.so.7";
                 h = dlmopen(LM_ID_NEWLM, path.c_str(), RTLD_NOW | RTLD_LOCAL);
@@ -627,8 +627,7 @@ __device__ __forceinline__ Partial wg_reduce(Acc acc) {
 )";
     src += "extern \"C\" __global__ void __launch_bounds__(256)\n"
            "fq_jit_scan(const TIn *__restrict__ col, long long n, long long head, long long R,\n"
-           "            const u64 *__restrict__ bitmap, Consts c, Partial *parts, u32 *done, Partial *out,\n"
-           "            u64 blocks, int empty_if_zero, int form) {\n"
+           "            const u64 *__restrict__ bitmap, Consts c, Partial *parts) {\n"
            "    Acc acc;\n    acc.sum = V(0); acc.mx = " + lo + "; acc.mn = " + hi + "; acc.cnt = 0; acc.flags = 0;\n";
     if (!L.block_mode) {
         // flat tile-contiguous streaming (agg_flat_kernel, U = 4 16-byte vectors per lane)
@@ -738,60 +737,10 @@ __device__ __forceinline__ Partial wg_reduce(Acc acc) {
     }
 )";
     }
-    // this workgroup's partial; with `done` (FQ_AGG_ONE_LAUNCH) the in-launch
-    // finalize of fq_aggregate.hip (finish_in_launch + fold_partials, same
-    // hand-off, same fold order)
+    // this workgroup's partial (agg_finalize_kernel folds them, fq_aggregate.hip)
     src += R"JIT(
-    {
-        const Partial p = wg_reduce(acc);
-        if (threadIdx.x == 0) {
-            if (done && form == 1) {  // write-through (sc1): no release fence below
-                u64 w[6];
-                __builtin_memcpy(w, &p, sizeof p);
-                u64 *o = (u64 *)(parts + blockIdx.x);
-#pragma unroll
-                for (int i = 0; i < 6; ++i) __hip_atomic_store(o + i, w[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            } else {
-                parts[blockIdx.x] = p;
-            }
-        }
-    }
-    if (!done) return;
-    __shared__ u32 s_last;
-    if (threadIdx.x == 0) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (form == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        const u32 t = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const u32 last = t == gridDim.x - 1u ? 1u : 0u;
-        if (last) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        s_last = last;
-    }
-    __syncthreads();
-    if (!s_last) return;
-    Acc f;
-    f.sum = V(0); f.mx = )JIT" + lo + "; f.mn = " + hi + R"JIT(; f.cnt = 0; f.flags = 0;
-    for (int i = threadIdx.x; i < (int)gridDim.x; i += 256) {
-        const Partial q = parts[i];
-        f.sum = f.sum + __builtin_bit_cast(V, q.sum);
-        f.mx = vmax(f.mx, __builtin_bit_cast(V, q.max));
-        f.mn = vmin(f.mn, __builtin_bit_cast(V, q.min));
-        f.cnt += q.count;
-        f.flags |= q.flags;
-    }
-    __syncthreads();  // wg_reduce's LDS is reused
-    Partial r = wg_reduce(f);
-    if (threadIdx.x == 0) {
-        r.blocks = blocks;
-        if (empty_if_zero && r.count == 0) r.flags |= )JIT" + std::to_string(FQ_STATE_ANY_EMPTY) + R"JIT(u;
-        *out = r;
-        __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    const Partial p = wg_reduce(acc);
+    if (threadIdx.x == 0) parts[blockIdx.x] = p;
 }
 )JIT";
     return true;
@@ -809,17 +758,14 @@ __device__ __forceinline__ Partial wg_reduce(Acc acc) {
 // enough to find or claim a slot across XCDs.
 // ---------------------------------------------------------------------------
 
-// LDS slot hash of the GROUP BY kernel: 1 (default) keeps consecutive keys in
-// consecutive slots, 0 = Fibonacci hash of the whole key (FQ_TUNE_GROUP_LDS_LOCAL)
-int group_lds_local() { return (int)fqc::knob(FQ_TUNE_GROUP_LDS_LOCAL); }
-
-// HBM key probe of the GROUP BY kernel: 1 = plain cached read first
-// (FQ_TUNE_GROUP_KEY_PLAIN), 0 = agent-scope atomic read
-int group_key_plain() { return (int)fqc::knob(FQ_TUNE_GROUP_KEY_PLAIN); }
-
-// wave-uniform key runs merged across the wave (fq_wave_runs): 1 (default),
-// 0 = off (FQ_TUNE_GROUP_WAVE_RUNS; tools/group_shapes_probe.py)
-int group_wave_runs() { return (int)fqc::knob(FQ_TUNE_GROUP_WAVE_RUNS); }
+// Fixed by round-1/2 sweeps (their knobs were removed in round 6):
+// LDS slot hash keeps consecutive keys in consecutive slots (1; 0 = Fibonacci
+// hash of the whole key, profiles/r01_groupby_sweep_hash.txt); the HBM key
+// probe reads plain before any CAS (1; r01_groupby_sweep_keyprobe.txt);
+// wave-uniform key runs merged across the wave (1; r02_group_shapes.txt)
+constexpr int group_lds_local() { return 1; }
+constexpr int group_key_plain() { return 1; }
+constexpr int group_wave_runs() { return 1; }
 
 // clustered-key row layout of the GROUP BY kernel (mode 1 in fq_jit_groupby):
 // chosen per workgroup from its first tile when a wave's 512 rows change key
@@ -910,10 +856,7 @@ bool group_stage_narrow(const GroupLaunch &G) {
 std::string group_shape_key(const GroupLaunch &G, int32_t tin, int dev) {
     std::string k = "G" + std::to_string(group_lds_local()) + std::to_string(group_key_plain()) +
                     std::to_string(group_chunked()) + std::to_string(group_wave_runs()) +
-                    std::to_string(group_cluster()) + "d" + std::to_string(fqc::knob(FQ_TUNE_GPART_DBUF)) + "r" +
-                    std::to_string(fqc::knob(FQ_TUNE_GPART_ROWS8)) + "n" +
-                    std::to_string(fqc::knob(FQ_TUNE_GPART_ROWS4)) + "b" +
-                    std::to_string(fqc::knob(FQ_TUNE_GBINS_ROWS)) + "s" + std::to_string(group_stage_narrow(G) ? 1 : 0);
+                    std::to_string(group_cluster()) + "s" + std::to_string(group_stage_narrow(G) ? 1 : 0);
     auto put = [&k](int32_t v) { k.append(reinterpret_cast<const char *>(&v), sizeof v); };
     auto prog = [&put](const KProg &p) {
         put(p.n);
@@ -1043,7 +986,7 @@ __device__ __forceinline__ PRow gp_fetch(const PRow *p) { return __builtin_nonte
 #endif
 #endif
 #define GP_TBLK (GP_TILE / GP_BLK)
-// rows per thread of the partition pass's tiles (FQ_TUNE_GPART_ROWS4 for 4-byte rows)
+// rows per thread of the partition pass's tiles
 #ifndef GPR_ROWS
 #define GPR_ROWS GP_ROWS
 #endif
@@ -1606,18 +1549,12 @@ bool gen_groupby_source(const GroupLaunch &G, int32_t tin, Gen &g, std::string &
         src += "#define GP_MOD32 " + std::to_string(mod32 ? 1 : 0) + "\n#define GP_RANK_BATCH 1\n";
         if (group_stage_narrow(G)) src += "#define GP_STAGE 1\n";
     }
-    // 8-byte rows: GP_ROWS rows per thread per tile (FQ_TUNE_GPART_ROWS8); at 8 their 64 KB staging leaves
-    // no LDS for the double buffers
-    const int rows8 = G.narrow ? 8 : (int)fqc::knob(FQ_TUNE_GPART_ROWS8);
-    if (rows8 != 8) src += "#define GP_ROWS " + std::to_string(rows8) + "\n";
-    // 4-byte rows: the bins pass's rows per thread (FQ_TUNE_GBINS_ROWS; at 4, without the next tile's loads in
-    // registers, 54 VGPRs: room for a second workgroup per CU) and the partition pass's (FQ_TUNE_GPART_ROWS4)
-    const int gbr = G.narrow ? (int)fqc::knob(FQ_TUNE_GBINS_ROWS) : 8;
-    if (gbr != 8) src += "#define GP_ROWS " + std::to_string(gbr) + "\n#define GB_PREFETCH 0\n";
-    if (G.narrow && (fqc::knob(FQ_TUNE_GPART_ROWS4) != 8 || gbr != 8))
-        src += "#define GPR_ROWS " + std::to_string(fqc::knob(FQ_TUNE_GPART_ROWS4)) +
-               (G.threads >= 1024 && fqc::knob(FQ_TUNE_GPART_ROWS4) == 4 ? "\n#define GPR_WAVES 12\n" : "\n");  // 42 VGPRs: three workgroups per CU
-    src += "#define GP_DBUF " + std::to_string((G.narrow || rows8 < 8) && fqc::knob(FQ_TUNE_GPART_DBUF) ? 1 : 0) + "\n";
+    // Rows per thread per tile (round-4 sweeps, profiles/r04_m_gpart_rows4_ab/, r04_o_gbins_ab/): 8-byte rows
+    // 8 in both passes (their 64 KB staging leaves no LDS for the double buffers); 4-byte rows 8 in the
+    // partition pass (double-buffered tile state, two barriers per tile) and 4 in the bins pass, without the
+    // next tile's loads in registers (54 VGPRs: room for a second workgroup per CU)
+    if (G.narrow) src += "#define GP_ROWS 4\n#define GB_PREFETCH 0\n#define GPR_ROWS 8\n";
+    src += std::string("#define GP_DBUF ") + (G.narrow ? "1" : "0") + "\n";
     // (range bins only: the hash bins' 72 KB staging leaves no LDS for it)
     // blocks are 2 KB either way: 256 8-byte rows, or 512 narrow ones (1 KB
     // blocks measured 1.11 -> 1.53 ms per 4.2e8-row partition pass)
@@ -2240,36 +2177,9 @@ void pack_proj_consts(const ProjLaunch &P, HostProjConsts &hc) {
     pack_tree_consts(P.pred, hc);
 }
 
-// FQ_TUNE_SELECT_VARIANT (tuning, tools/select_sweep.sh): bit 0 per-XCD ticket
-// counters (default on).
-int select_variant() { return (int)fqc::knob(FQ_TUNE_SELECT_VARIANT); }
-// FQ_TUNE_SELECT_DEBUG=1 (tuning only): the select kernel counts tiles, polls and
-// cycles per phase into a module global that is printed after each launch
-int select_debug() { return (int)fqc::knob(FQ_TUNE_SELECT_DEBUG); }
-// the last debug launch's counters (fq_tune_select_counters)
-std::mutex g_select_counters_mu;
-uint64_t g_select_counters[FQ_TUNE_SELECT_COUNTERS] = {};
-// FQ_TUNE_SELECT_LBW: status words per lane per look-back round trip (1/2/4/8;
-// wider windows measured slower: the polls' extra agent-scope loads cost more
-// than the round trips they save, tools/select_sweep.sh)
-int select_lbw() { return (int)fqc::knob(FQ_TUNE_SELECT_LBW); }
-// XCDs of the device (MI355X: 32 CUs each; 8 in SPX mode, fewer in the
-// partitioned modes), at most kMaxSelectXcds ticket counters
-int select_xcds(int dev) {
-    int cus = 256;
-    if (dev >= 0 && hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
-        (void)hipGetLastError();
-        cus = 256;
-    }
-    return std::max(1, std::min(kMaxSelectXcds, cus / 32));
-}
-
 std::string proj_shape_key(const ProjLaunch &P, int32_t tin, int dev) {
-    std::string k = "PROJ" + std::to_string(select_threads()) + "x" + std::to_string(select_rows_per_thread()) + "s" +
-                    std::to_string(select_sleep()) + "v" + std::to_string(select_variant()) + "w" + std::to_string(select_lbw()) + "g" + std::to_string(select_debug()) + "n" +
-                    std::to_string(select_xcds(dev)) + "r" + std::to_string(fqc::knob(FQ_TUNE_SELECT_BLOCKS_RUN)) + "d" +
-                    std::to_string(fqc::knob(FQ_TUNE_SELECT_BLOCKS_DRAW)) + "b" + std::to_string(fqc::knob(FQ_TUNE_SELECT_BLOCKS_ROWS)) +
-                    "t" + std::to_string(fqc::knob(FQ_TUNE_SELECT_NT)) + "S" +
+    // the tunable part of the shape: the block kernel's rows per thread and stage
+    std::string k = "PROJb" + std::to_string(fqc::knob(FQ_TUNE_SELECT_BLOCKS_ROWS)) + "S" +
                     std::to_string(fqc::knob(FQ_TUNE_SELECT_BLOCKS_STAGE));
     auto put = [&k](int32_t v) { k.append(reinterpret_cast<const char *>(&v), sizeof v); };
     put(dev);
@@ -2302,17 +2212,17 @@ std::string proj_shape_key(const ProjLaunch &P, int32_t tin, int dev) {
 // rows [b * B, b * B + count[b]) -- an output block starts where its input
 // block does, so no block's offsets depend on another block's count and no
 // workgroup waits on another (no look-back: fq_jit_pselect's contiguous output
-// needs one).  Workgroups draw runs of PB_RUN whole blocks from a counter, so
-// the runs in flight are adjacent (one static range per workgroup, or runs
-// dealt round-robin, measured 7-10 % slower: profiles/r03_s3_blocks_sweeps.txt),
-// and walk a run in tiles of PB_THREADS x PB_ROWS rows that ignore block
+// needs one).  Workgroups draw whole blocks from a counter, so the blocks in
+// flight are adjacent (one static range per workgroup, or blocks dealt
+// round-robin, measured 7-10 % slower: profiles/r03_s3_blocks_sweeps.txt),
+// and walk a block in tiles of PB_THREADS x PB_ROWS rows that ignore block
 // edges; B >= the tile, so a tile holds at most one block edge: rows before it
 // go to the open block at its running count (carry), rows after it start the
 // next block.  Kept rows before the edge are exactly those of in-tile rank <
 // re, the edge's rank, read from the tile's ballots and exclusive group
 // offsets in LDS (double-buffered by tile parity: two barriers per tile).
-// Outputs are written with nontemporal stores (PB_NT; 3.42 -> 3.12 ms per
-// 10 GB, no change for the look-back kernel).  PB_STAGE (round 5): the tile's
+// Outputs are written with nontemporal stores (3.42 -> 3.12 ms per 10 GB, no
+// change for the look-back kernel).  PB_STAGE (round 5): the tile's
 // kept rows go to LDS by in-tile rank first, then consecutive threads write
 // them out as 16-byte row pairs (pb_copy), so every store instruction covers
 // one contiguous span instead of the ~24 kept lanes of a 64-row ballot.  The
@@ -2326,21 +2236,14 @@ std::string proj_shape_key(const ProjLaunch &P, int32_t tin, int dev) {
 // ballots per 128 rows, each lane storing its two kept rows) measured 4.52
 // against 3.10 ms: a wave's stores then interleave and no longer combine.
 std::string gen_project_blocks_kernel(bool bitmap_pred) {
-    std::string s = "#define PB_RUN " + std::to_string(fqc::knob(FQ_TUNE_SELECT_BLOCKS_RUN)) + "\n#define PB_DRAW " +
-                    std::to_string(fqc::knob(FQ_TUNE_SELECT_BLOCKS_DRAW)) + "\n#define PB_ROWS " +
-                    std::to_string(fqc::knob(FQ_TUNE_SELECT_BLOCKS_ROWS)) + "\n#define PB_NT " +
-                    std::to_string(fqc::knob(FQ_TUNE_SELECT_NT) & 1) + "\n#define PB_STAGE " +
+    std::string s = "#define PB_ROWS " + std::to_string(fqc::knob(FQ_TUNE_SELECT_BLOCKS_ROWS)) + "\n#define PB_STAGE " +
                     std::to_string(fqc::knob(FQ_TUNE_SELECT_BLOCKS_STAGE)) + "\n";
     s += R"(
 #define PB_THREADS 256
 #define PB_WAVES (PB_THREADS / 64)
 #define PB_TILE (PB_THREADS * PB_ROWS)
 #define PB_NE (PB_ROWS * PB_WAVES)  // 64-row ballots per tile
-#if PB_NT
 #define PB_PUT fq_put_nt
-#else
-#define PB_PUT fq_put
-#endif
 struct PbShared {
     u64 bal[2][PB_NE];      // ballot of 64-row group i = k * PB_WAVES + wave (tile rows [64 i, 64 i + 64))
     u32 off[2][PB_NE + 1];  // exclusive in-tile offset of each group; [PB_NE]: the tile's kept rows
@@ -2397,8 +2300,7 @@ __device__ __forceinline__ void pb_copy(const TIn *__restrict__ st, u32 base, u3
     s += R"(extern "C" __global__ void __launch_bounds__(PB_THREADS)
 fq_jit_pblocks(const TIn *__restrict__ col, long long n, long long B, Consts c,
     const u64 *__restrict__ bm, Outs o, long long *__restrict__ counts, u32 *__restrict__ fl,
-    unsigned long long *__restrict__ total, u32 *__restrict__ ticket, int al, u32 *__restrict__ done,
-    unsigned long long *__restrict__ hres) {
+    unsigned long long *__restrict__ total, u32 *__restrict__ ticket, int al) {
     __shared__ PbShared sh;
 #if PB_STAGE
     __shared__ TIn stage[PB_CAP];
@@ -2411,25 +2313,14 @@ fq_jit_pblocks(const TIn *__restrict__ col, long long n, long long B, Consts c,
     u32 pflags = 0, vflags = 0;
     const u64 lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     int par = 0;
-#if PB_RUN && PB_DRAW
+    // one block per draw from the counter: the blocks in flight stay adjacent
     __shared__ long long s_run;
-    const long long nruns = (nb + PB_RUN - 1) / PB_RUN;
     for (;;) {
         if (tid == 0) s_run = (long long)atomicAdd(ticket, 1u);
         __syncthreads();
         const long long run = s_run;
-        if (run >= nruns) break;
-        const long long b_lo = run * PB_RUN, b_hi = b_lo + PB_RUN < nb ? b_lo + PB_RUN : nb;
-#elif PB_RUN
-    (void)ticket;
-    const long long nruns = (nb + PB_RUN - 1) / PB_RUN;
-    for (long long run = blockIdx.x; run < nruns; run += gridDim.x) {
-        const long long b_lo = run * PB_RUN, b_hi = b_lo + PB_RUN < nb ? b_lo + PB_RUN : nb;
-#else
-    (void)ticket;
-    {
-        const long long b_lo = nb * (long long)blockIdx.x / gridDim.x, b_hi = nb * ((long long)blockIdx.x + 1) / gridDim.x;
-#endif
+        if (run >= nb) break;
+        const long long b_lo = run, b_hi = run + 1;
     const long long end = b_hi * B < n ? b_hi * B : n;
     long long cur = b_lo;  // the open block
     u64 carry = 0;         // its kept rows so far
@@ -2517,33 +2408,6 @@ fq_jit_pblocks(const TIn *__restrict__ col, long long n, long long B, Consts c,
     if (lane == 0 && pflags) atomicOr(fl, pflags);
     if (lane == 0 && vflags) atomicOr(fl + 1, vflags);
     if (tid == 0 && kept) atomicAdd(total, (unsigned long long)kept);
-    if (hres) {
-        // fq_filter_project_blocks_launch: the last workgroup hands {kept rows,
-        // flag words} to host memory and re-zeroes the workspace for the next
-        // launch (no memset before, no copy after).  Every wave's atomics are
-        // done (vmcnt) before its workgroup draws a ticket; the counters are
-        // device-scope atomics and read as such, so no L2 write-back is needed
-        // -- an agent-scope release per workgroup cost the kernel 4.6 %
-        // (profiles/r05_x_p1_launch_ab.json).  The outputs are read only after
-        // the kernel has completed (the caller waits on the stream).
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (tid == 0) {
-            const u32 t = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (t == gridDim.x - 1u) {
-                const unsigned long long k = __hip_atomic_load(total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const unsigned long long f0 = __hip_atomic_load(fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const unsigned long long f1 = __hip_atomic_load(fl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                hres[0] = k;
-                hres[1] = f0 | (f1 << 32);
-                __hip_atomic_store(total, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(fl, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(fl + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-    }
 }
 )PB";
     return s;
@@ -2565,8 +2429,7 @@ bool gen_project_source(const ProjLaunch &P, int32_t tin, int dev, Gen &g, std::
     src += "struct Outs { void *p[" + std::to_string(FQ_MAX_PROJECT) + "]; };\n";
     src += "#define PS_ROWS " + std::to_string(select_rows_per_thread()) + "\n#define PS_THREADS " +
            std::to_string(select_threads()) + "\n#define PS_SLEEP " + std::to_string(select_sleep()) +
-           "\n#define PS_XCD " + std::to_string(select_variant() & 1) + "\n#define PS_LBW " + std::to_string(select_lbw()) + "\n#define PS_DEBUG " + std::to_string(select_debug()) + "\n#define PS_NXCD " + std::to_string(select_xcds(dev)) + "\n#define PS_NT " +
-           std::to_string((fqc::knob(FQ_TUNE_SELECT_NT) >> 1) & 1) + "\n";
+           "\n";
     src += "typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));\n";
     src += "__device__ __forceinline__ bool fq_pred(TIn x, const Consts &c, u32 &flags, u32 live) {\n";
     src += expr_pred ? pred_body : "    (void)x; (void)c; (void)flags; (void)live;\n    return true;\n";
@@ -2643,28 +2506,15 @@ fq_jit_pbits(const TIn *__restrict__ col, long long n, Consts c, u64 *__restrict
 // held two tiles and published the second's A while the first waited
 // measured no faster -- tools/select_sweep.sh, profiles/r02_select_*).
 //
-// Tickets: one device-scope counter serves ~90 atomics per us (round-1
-// measurement), >= 1.7 ms for the 152,588 tiles of a 10 GB column.  With
-// PS_XCD the workgroups fall into X.ncls classes by blockIdx (blocks are dealt
-// round-robin over the XCDs, so a class is in practice one XCD's workgroups;
-// ncls <= the grid, and the host sizes the grid to the resident capacity):
-// counter x hands out tiles x, x + ncls, ...  A workgroup whose counter is
-// exhausted draws from the next class's, and leaves only when every counter
-// is exhausted.  Progress: the lowest drawn-but-unfinished tile m needs every
-// tile below it drawn; a class whose counter is below m has resident
-// workgroups, none holding a tile below m (else m is not lowest), so they are
-// drawing and the class advances.  (Classes read from the hardware XCC_ID, as
-// in round 2, could leave a class with no resident workgroup: its tiles would
-// never be drawn and every look-back past them would hit the poll bound.)
-// That argument needs a resident workgroup in every class.  Beside other
-// kernels (the engine's LIMIT pipes run one of these per private queue) a
-// launch may get fewer resident workgroups than classes: their tiles wait on
-// undrawn tiles of absent classes until the other kernels free CUs, and two
-// such launches can hold each other's CUs until the poll bound (seen once in
-// round 5: "the offset look-back did not complete", tests/test_memory_gpu.py).
-// So PS_XCD is off by default (FQ_TUNE_SELECT_VARIANT 0): one counter, and the
+// Tickets: ONE device-scope counter, so tiles are drawn in order and the
 // lowest unfinished tile always has every predecessor drawn by a resident
-// workgroup.
+// workgroup -- the look-back progresses whatever else runs on the GPU.  (Round
+// 2's per-XCD ticket classes were faster alone on the GPU, but their progress
+// argument needed a resident workgroup in every class: beside the engine's
+// other LIMIT pipes on private queues a launch could hold fewer, and two such
+// launches once waited on each other's CUs until the poll bound -- round 5,
+// tests/test_memory_gpu.py.  Removed in round 6; tests/test_project_gpu.py
+// runs two look-back launches side by side.)
 // Status words are 64-bit agent-scope atomics: flag in the top 2 bits, count
 // below.  The look-back is bounded: after ~2^20 polls the kernel flags an
 // error (fl[1] bit 31) and moves on, so a wave can never spin forever.
@@ -2678,31 +2528,8 @@ fq_jit_pbits(const TIn *__restrict__ col, long long n, Consts c, u64 *__restrict
 #ifndef PS_SLEEP
 #define PS_SLEEP 2
 #endif
-#ifndef PS_XCD
-#define PS_XCD 1
-#endif
-#ifndef PS_NXCD
-#define PS_NXCD 8
-#endif
 #ifndef PS_LBW
 #define PS_LBW 1
-#endif
-#ifndef PS_DEBUG
-#define PS_DEBUG 0
-#endif
-#if PS_DEBUG
-// [0] tiles [1] failed polls [2] look-back cycles [3] ticket cycles
-// [4] load+predicate cycles [5] store cycles [6] workgroup cycles [7] windows
-// [8] earliest workgroup start [9] latest start [10] earliest end [11] latest end
-// [12] sum of workgroup wall ticks (100 MHz)
-__device__ unsigned long long ps_dbg[13];
-// per workgroup: start, end (wall clock), XCC_ID, tiles
-__device__ unsigned long long ps_wg[8192][4];
-#define PS_T(v) const long long v = clock64()
-#define PS_ADD(i, x) (X.dbg[i] += (unsigned long long)(x))
-#else
-#define PS_T(v)
-#define PS_ADD(i, x)
 #endif
 #define PS_WAVES (PS_THREADS / 64)
 #define PS_TILE (PS_THREADS * PS_ROWS)
@@ -2725,30 +2552,14 @@ struct PsShared {
     long long tk;  // ticket drawn (broadcast)
 };
 struct PsCtx {
-#if PS_DEBUG
-    unsigned long long dbg[8];  // thread 0's per-phase sums, flushed once per workgroup
-#endif
     const TIn *__restrict__ col;
     long long n, ntiles;
     const u64 *__restrict__ bm;
     u64 *__restrict__ status;
     u32 *__restrict__ ticket;
-    u32 cls, ncls;
 };
-// the next tile for this workgroup (thread 0 only); >= ntiles when none is
-// left.  An exhausted class moves on to the other classes' counters.
-__device__ __forceinline__ long long ps_ticket(const PsCtx &X) {
-#if PS_XCD
-    for (u32 i = 0; i < X.ncls; ++i) {
-        const u32 cl = (X.cls + i) % X.ncls;
-        const long long t = (long long)atomicAdd(X.ticket + 32 * cl, 1u) * X.ncls + cl;
-        if (t < X.ntiles) return t;
-    }
-    return X.ntiles;
-#else
-    return atomicAdd(X.ticket, 1u);
-#endif
-}
+// the next tile for this workgroup (thread 0 only); >= ntiles when none is left
+__device__ __forceinline__ long long ps_ticket(const PsCtx &X) { return atomicAdd(X.ticket, 1u); }
 __device__ __forceinline__ void ps_load(const PsCtx &X, long long t, TIn (&x)[PS_ROWS]) {
     const long long r0 = t * PS_TILE + threadIdx.x;
     if (t * PS_TILE + PS_TILE <= X.n) {
@@ -2862,15 +2673,12 @@ template <int S>
 __device__ __forceinline__ bool ps_single(PsCtx &X, const Consts &c, const Outs &o, u64 *__restrict__ total,
                                           PsShared &sh, TIn (&x)[PS_ROWS], u32 &pflags, u32 &vflags) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    PS_T(c0);
     if (tid == 0) sh.tk = ps_ticket(X);
     __syncthreads();
-    PS_T(c1);
     const long long t = sh.tk;
     if (t >= X.ntiles) return false;
     ps_load(X, t, x);
     ps_pred<S>(X, c, sh, t, x, pflags);
-    PS_T(c2);
     if (wave == 0) {
         u64 excl = 0;
         if (t != 0) {
@@ -2881,12 +2689,6 @@ __device__ __forceinline__ bool ps_single(PsCtx &X, const Consts &c, const Outs 
                 __builtin_amdgcn_s_sleep(PS_SLEEP);
 #endif
             }
-#if PS_DEBUG
-            if (lane == 0) {
-                PS_ADD(1, polls);
-                PS_ADD(7, (u64)((t - 1 - j) / 64 + 1));
-            }
-#endif
         }
         if (lane == 0) {
             sh.base[S] = excl;
@@ -2894,30 +2696,15 @@ __device__ __forceinline__ bool ps_single(PsCtx &X, const Consts &c, const Outs 
         }
     }
     __syncthreads();
-    PS_T(c3);
     const u64 base = sh.base[S];
     const u64 lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
 #pragma unroll
     for (int k = 0; k < PS_ROWS; ++k) {
         const u64 b = sh.bal[S][k][wave];
         if ((b >> lane) & 1ull)
-#if PS_NT
-            fq_put_nt(x[k], c, vflags, 1u, o, (long long)(base + sh.off[S][k * PS_WAVES + wave] + (u32)__popcll(b & lt)));
-#else
             fq_put(x[k], c, vflags, 1u, o, (long long)(base + sh.off[S][k * PS_WAVES + wave] + (u32)__popcll(b & lt)));
-#endif
     }
     if (t == X.ntiles - 1 && tid == 0) *total = base + sh.agg[S];
-#if PS_DEBUG
-    PS_T(c4);
-    if (tid == 0) {
-        PS_ADD(0, 1);
-        PS_ADD(3, c1 - c0);
-        PS_ADD(4, c2 - c1);
-        PS_ADD(2, c3 - c2);
-        PS_ADD(5, c4 - c3);
-    }
-#endif
     return true;
 }
 extern "C" __global__ void __launch_bounds__(PS_THREADS)
@@ -2931,40 +2718,12 @@ fq_jit_pselect(const TIn *__restrict__ col, long long n, Consts c, const u64 *__
     X.bm = bm;
     X.status = status;
     X.ticket = ticket;
-    X.ncls = gridDim.x < (unsigned)PS_NXCD ? gridDim.x : (unsigned)PS_NXCD;
-    X.cls = blockIdx.x % X.ncls;
-#if PS_DEBUG
-    for (int i = 0; i < 8; ++i) X.dbg[i] = 0;
-#endif
     u32 pflags = 0, vflags = 0;
-    PS_T(k0);
-#if PS_DEBUG
-    const unsigned long long w0 = wall_clock64();
-#endif
     {
         TIn x[PS_ROWS];
         while (ps_single<0>(X, c, o, total, sh, x, pflags, vflags) && ps_single<1>(X, c, o, total, sh, x, pflags, vflags)) {
         }
     }
-#if PS_DEBUG
-    PS_T(k1);
-    const unsigned long long w1 = wall_clock64();
-    if (threadIdx.x == 0) {
-        PS_ADD(6, k1 - k0);
-        for (int i = 0; i < 8; ++i) atomicAdd(&ps_dbg[i], X.dbg[i]);
-        atomicAdd(&ps_dbg[12], w1 - w0);
-        if (blockIdx.x < 8192) {
-            ps_wg[blockIdx.x][0] = w0;
-            ps_wg[blockIdx.x][1] = w1;
-            ps_wg[blockIdx.x][2] = (u32)__builtin_amdgcn_s_getreg((3 << 11) | 20);
-            ps_wg[blockIdx.x][3] = X.dbg[0];
-        }
-        atomicMin(&ps_dbg[8], w0);
-        atomicMax(&ps_dbg[9], w0);
-        atomicMin(&ps_dbg[10], w1);
-        atomicMax(&ps_dbg[11], w1);
-    }
-#endif
     pflags = wave_or(pflags);
     vflags = wave_or(vflags);
     if ((threadIdx.x & 63) == 0 && pflags) atomicOr(fl, pflags);
@@ -3165,12 +2924,7 @@ fq_status jit_scan(int32_t col_dtype, bool chain, const Launch &L, bool *used, b
     long long n = L.n, head = L.head, R = L.block_rows;
     const uint64_t *bitmap = L.pred.bitmap;
     Partial *parts = L.parts;
-    uint32_t *done = L.fin.done;
-    void *out = L.fin.out;
-    unsigned long long blocks = L.fin.blocks;
-    int empty_if_zero = L.fin.empty_if_zero;
-    int form = L.fin.form;
-    void *args[] = {&col, &n, &head, &R, &bitmap, &hc, &parts, &done, &out, &blocks, &empty_if_zero, &form};
+    void *args[] = {&col, &n, &head, &R, &bitmap, &hc, &parts};
     FQ_HIP_TRY(hipModuleLaunchKernel(fn, (unsigned)L.grid, 1, 1, kThreads, 1, 1, 0, L.stream, args, nullptr));
     g_jit_launches += 1;
     *used = true;
@@ -3398,8 +3152,8 @@ fq_status jit_project_select(int32_t col_dtype, const ProjLaunch &P, const uint6
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     (void)hipGetLastError();
-    // every workgroup resident (the ticket classes' progress argument needs it):
-    // at most the occupancy the compiled kernel allows per CU
+    // one resident wave of workgroups: at most the occupancy the compiled kernel
+    // allows per CU (more would only queue behind them)
     hipFunction_t fn = k.scatter;
     const int threads = select_threads();
     static std::mutex occ_mu;
@@ -3421,28 +3175,11 @@ fq_status jit_project_select(int32_t col_dtype, const ProjLaunch &P, const uint6
     FQ_HIP_TRY(hipModuleLaunchKernel(fn, (unsigned)grid, 1, 1, (unsigned)threads, 1, 1, 0, P.stream,
                                      args, nullptr));
     g_jit_launches += 1;
-    if (select_debug() && k.mod) {  // tuning only: keep and clear the kernel's phase counters
-        hipDeviceptr_t d = nullptr;
-        size_t bytes = 0;
-        unsigned long long h[FQ_TUNE_SELECT_COUNTERS] = {0};
-        if (hipModuleGetGlobal(&d, &bytes, k.mod, "ps_dbg") == hipSuccess && bytes == sizeof h) {
-            (void)hipStreamSynchronize(P.stream);
-            if (hipMemcpyDtoH(h, d, sizeof h) == hipSuccess) {
-                std::lock_guard<std::mutex> lk(g_select_counters_mu);
-                for (int i = 0; i < FQ_TUNE_SELECT_COUNTERS; ++i) g_select_counters[i] = h[i];
-            }
-            unsigned long long z[FQ_TUNE_SELECT_COUNTERS] = {0};
-            z[8] = z[10] = ~0ull;
-            (void)hipMemcpyHtoD(d, z, sizeof z);
-        }
-        (void)hipGetLastError();
-    }
     return FQ_OK;
 }
 
 fq_status jit_project_blocks(int32_t col_dtype, const ProjLaunch &P, int64_t block_rows, const uint64_t *d_bitmap,
-                             int64_t *d_counts, uint32_t *d_flags, uint64_t *d_total, uint32_t *d_ticket,
-                             uint32_t *d_done, uint64_t *d_hres) {
+                             int64_t *d_counts, uint32_t *d_flags, uint64_t *d_total, uint32_t *d_ticket) {
     ProjKernels k;
     fq_status s = get_proj_kernels(col_dtype, P, &k);
     if (s != FQ_OK || !k.blocks || P.n == 0) return s;
@@ -3459,8 +3196,7 @@ fq_status jit_project_blocks(int32_t col_dtype, const ProjLaunch &P, int64_t blo
     const int64_t nb = (P.n + B - 1) / B;
     int al = 1;  // PB_STAGE row pairs need 16-byte aligned outputs
     for (int j = 0; j < P.n_out; ++j) al &= ((uintptr_t)P.out[j] & 15) == 0;
-    void *args[] = {&col, &n, &B, &hc, &d_bitmap, &outs, &d_counts, &d_flags, &d_total, &d_ticket, &al, &d_done,
-                    &d_hres};
+    void *args[] = {&col, &n, &B, &hc, &d_bitmap, &outs, &d_counts, &d_flags, &d_total, &d_ticket, &al};
     hipFunction_t fn = k.blocks;
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -3484,9 +3220,7 @@ fq_status jit_project_blocks(int32_t col_dtype, const ProjLaunch &P, int64_t blo
         }
     }
     const int wg_per_cu = (int)fqc::knob(FQ_TUNE_SELECT_BLOCKS_WG_PER_CU);
-    const int64_t run = fqc::knob(FQ_TUNE_SELECT_BLOCKS_RUN);
-    const int64_t units = run > 0 ? (nb + run - 1) / run : nb;
-    const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(units, (int64_t)cus * std::min(wg_per_cu, occ)));
+    const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(nb, (int64_t)cus * std::min(wg_per_cu, occ)));
     FQ_HIP_TRY(hipModuleLaunchKernel(fn, (unsigned)grid, 1, 1, kProjectBlockThreads, 1, 1, 0, P.stream, args,
                                      nullptr));
     g_jit_launches += 1;
@@ -3525,13 +3259,6 @@ fq_status fq_jit_config(int32_t mode, int64_t min_rows) {
     if (min_rows < 0) return fqc::fail(FQ_E_INVALID, "fq_jit_config: negative min_rows");
     fqk::g_mode.store(mode);
     fqk::g_min_rows.store(min_rows);
-    return FQ_OK;
-}
-
-fq_status fq_tune_select_counters(uint64_t *out, int32_t n) {
-    if (!out || n < 0 || n > FQ_TUNE_SELECT_COUNTERS) return fqc::fail(FQ_E_INVALID, "fq_tune_select_counters: bad argument");
-    std::lock_guard<std::mutex> lk(fqk::g_select_counters_mu);
-    for (int32_t i = 0; i < n; ++i) out[i] = fqk::g_select_counters[i];
     return FQ_OK;
 }
 

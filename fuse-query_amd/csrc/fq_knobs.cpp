@@ -19,49 +19,25 @@ struct KnobDef {
 
 // index = FQ_TUNE_*; the sweeps behind the defaults are in DESIGN.md
 constexpr KnobDef kDefs[FQ_TUNE_COUNT] = {
-    {2, 1, 16, 1, false},        // SCAN_WG_PER_CU
-    {0, 0, 16, 1, false},        // EW_WG_PER_CU
-    {0, 0, 1, 1, false},         // CMP_SPREAD
-    {2, 1, 4, 1, false},         // GPART_WG_PER_CU
+    {2, 1, 16, 1, false},           // SCAN_WG_PER_CU
+    {0, 0, 16, 1, false},           // EW_WG_PER_CU
+    {8, 4, 16, 1, true},            // BLOCK_U
+    {8, 1, 16, 1, false},           // SELECT_WG_PER_CU
+    {8, 1, 16, 1, false},           // SELECT_BLOCKS_WG_PER_CU
+    {32, 8, 32, 1, true},           // SELECT_BLOCKS_ROWS
+    {2, 0, 4, 1, true},             // SELECT_BLOCKS_STAGE
+    {1, 0, 1, 1, false},            // BLOCK_CACHE
+    {0, 0, 100000, 1, false},       // POOL_SPIN_US
     {1024, 256, 1024, 256, false},  // GROUP_THREADS
-    {128, 8, 160, 1, false},     // GROUP_LDS_KB
-    {8, 4, 16, 1, true},         // BLOCK_U
-    {1, 0, 1, 1, false},         // GROUP_LDS_LOCAL
-    {1, 0, 1, 1, false},         // GROUP_KEY_PLAIN
-    {1, 0, 2, 1, false},         // GROUP_WAVE_RUNS
-    {160, 0, 512, 1, false},     // GROUP_CLUSTER
-    {1, 0, 1, 1, false},         // GROUP_CHUNKED
-    {0, 0, 1, 1, false},         // SELECT_VARIANT
-    {0, 0, 1, 1, false},         // SELECT_DEBUG
-    {1, 1, 8, 1, true},          // SELECT_LBW
-    {8, 1, 16, 1, false},        // SELECT_WG_PER_CU
-    {256, 256, 1024, 1, true},   // SELECT_THREADS
-    {32, 8, 32, 1, true},        // SELECT_ROWS
-    {2, 0, 127, 1, false},       // SELECT_SLEEP
-    {1, 0, 1, 1, false},         // BLOCK_CACHE
-    {1, 0, 1, 1, false},         // JIT_ISOLATED
-    {1, 0, 1, 1, false},         // GROUP_ROWMAP
-    {1, 1, 8, 1, false},         // GROUP_WG_PER_CU
-    {1, 0, 1, 1, false},         // GROUP_RANGE_BINS
-    {1, 0, 1, 1, false},         // GROUP_NARROW
-    {8, 1, 16, 1, false},        // SELECT_BLOCKS_WG_PER_CU
-    {1, 0, 4096, 1, false},      // SELECT_BLOCKS_RUN
-    {1, 0, 1, 1, false},         // SELECT_BLOCKS_DRAW
-    {32, 8, 32, 1, true},        // SELECT_BLOCKS_ROWS
-    {1, 0, 3, 1, false},         // SELECT_NT
-    {1, 0, 1, 1, false},         // GPART_DBUF
-    {8, 4, 8, 4, false},         // GPART_ROWS8
-    {8, 4, 8, 4, false},         // GPART_ROWS4
-    {4, 4, 8, 4, false},         // GBINS_ROWS
-    {2, 1, 4, 1, false},         // GBINS_WG_PER_CU
-    {1, 0, 1, 1, false},         // GBINS_FIT_LDS
-    {1000, 0, 100000, 1, false}, // POOL_SPIN_US
-    {1, 0, 1, 1, false},         // SCAN_FIN
-    {0, 0, 1, 1, false},         // ENGINE_ONE_LAUNCH
-    {2, 0, 4, 1, true},          // SELECT_BLOCKS_STAGE
-    {0, 0, 1, 1, false},         // ENGINE_FOLD_STREAM
-    {0, 0, 1, 1, false},         // ENGINE_PROJECT_LAUNCH
-    {0, 0, 1, 1, false},         // PROJECT_HANDOFF
+    {128, 8, 160, 1, false},        // GROUP_LDS_KB
+    {1, 1, 8, 1, false},            // GROUP_WG_PER_CU
+    {160, 0, 512, 1, false},        // GROUP_CLUSTER
+    {1, 0, 1, 1, false},            // GROUP_CHUNKED
+    {1, 0, 1, 1, false},            // GROUP_RANGE_BINS
+    {1, 0, 1, 1, false},            // GROUP_NARROW
+    {2, 1, 4, 1, false},            // GPART_WG_PER_CU
+    {2, 1, 4, 1, false},            // GBINS_WG_PER_CU
+    {0, 0, 2, 1, false},            // ENGINE_PROJECT_LAUNCH
 };
 
 std::atomic<int64_t> g_val[FQ_TUNE_COUNT] = {};

@@ -12,26 +12,8 @@ namespace fqk {
 
 constexpr int kThreads = 256;       // 4 waves per workgroup
 constexpr int kMaxPartials = 4096;  // workgroups per launch upper bound
-// the workspace: kMaxPartials Partials, then the completion counter of the
-// in-launch finalize on a line of its own
+// the workspace: kMaxPartials Partials, folded by agg_finalize_kernel
 constexpr size_t kPartialsBytes = (size_t)kMaxPartials * sizeof(Partial);
-constexpr size_t kCounterBytes = 256;
-
-// In-launch finalize (FQ_AGG_ONE_LAUNCH): every workgroup publishes its
-// Partial and draws a ticket from `done`; the one that draws grid - 1 folds
-// all partials in agg_finalize_kernel's order into *out and resets `done` to
-// zero.  done == nullptr: the separate finalize launch does the fold.
-// form (FQ_TUNE_SCAN_FIN): 0 = the partial stored plain, then an agent-scope
-// release (buffer_wbl2: the XCD L2's dirty lines written back) before the
-// ticket; 1 = the partial stored write-through (sc1 stores: nothing to write
-// back), drained, then the ticket.  The last workgroup acquires either way.
-struct Fin {
-    uint32_t *done;
-    fq_agg_state *out;
-    uint64_t blocks;
-    int32_t empty_if_zero;
-    int32_t form;
-};
 
 struct Launch {
     const void *col;
@@ -46,7 +28,6 @@ struct Launch {
     Partial *parts;
     int grid;
     hipStream_t stream;
-    Fin fin;
 };
 
 // Host lowering (fq_aggregate.hip): fq_expr -> KProg (res_dtype = result
@@ -177,16 +158,14 @@ fq_status jit_project_bits(int32_t col_dtype, const ProjLaunch &P, uint64_t *d_b
 // rows.  status: one zeroed word per tile; ticket: one zeroed word;
 // d_flags[0] predicate errors, d_flags[1] expression errors (bit 31: the
 // look-back gave up); *d_total = rows kept.
-// tile = select_threads() x select_rows_per_thread() rows (FQ_TUNE_SELECT_THREADS
-// 256/512/1024, FQ_TUNE_SELECT_ROWS 8/16/32: tuning; tools/select_sweep.sh)
-inline int select_threads() { return (int)fqc::knob(FQ_TUNE_SELECT_THREADS); }
-inline int select_rows_per_thread() { return (int)fqc::knob(FQ_TUNE_SELECT_ROWS); }
-// s_sleep between look-back polls of a predecessor that has not published
-// (FQ_TUNE_SELECT_SLEEP 0..127, tuning; default 2)
-inline int select_sleep() { return (int)fqc::knob(FQ_TUNE_SELECT_SLEEP); }
-// ticket counters of fq_jit_pselect (one per XCD, each on its own 128-B line)
-constexpr int kMaxSelectXcds = 16;
-inline int64_t select_tile_rows() { return (int64_t)select_threads() * select_rows_per_thread(); }
+// tile = select_threads() x select_rows_per_thread() rows, s_sleep
+// select_sleep() between look-back polls of a predecessor that has not
+// published (round-2 sweeps, tools/select_sweep.sh; their knobs were removed
+// in round 6)
+constexpr int select_threads() { return 256; }
+constexpr int select_rows_per_thread() { return 32; }
+constexpr int select_sleep() { return 2; }
+constexpr int64_t select_tile_rows() { return (int64_t)select_threads() * select_rows_per_thread(); }
 fq_status jit_project_select(int32_t col_dtype, const ProjLaunch &P, const uint64_t *d_bitmap, uint64_t *status,
                              uint32_t *ticket, uint32_t *d_flags, uint64_t *d_total);
 // stream of DataBlocks of block_rows rows (fq_filter_project_blocks): block b's
@@ -195,11 +174,9 @@ fq_status jit_project_select(int32_t col_dtype, const ProjLaunch &P, const uint6
 // d_flags / *d_total / *d_ticket as jit_project_select (zeroed by the caller)
 constexpr int kProjectBlockThreads = 256;
 constexpr int64_t kProjectBlockTile = 256 * 32;
-// d_hres != nullptr: the last workgroup writes {kept, flag words} to d_hres
-// (host memory the device writes) and re-zeroes flags / total / ticket / done
 fq_status jit_project_blocks(int32_t col_dtype, const ProjLaunch &P, int64_t block_rows, const uint64_t *d_bitmap,
-                             int64_t *d_counts, uint32_t *d_flags, uint64_t *d_total, uint32_t *d_ticket,
-                             uint32_t *d_done = nullptr, uint64_t *d_hres = nullptr);
+                             int64_t *d_counts, uint32_t *d_flags, uint64_t *d_total, uint32_t *d_ticket);
+// filter_project_blocks_enqueue / _result: fq_common.h (the engine calls them)
 // no predicate: every row -> the n_out outputs
 fq_status jit_project_map(int32_t col_dtype, const ProjLaunch &P, uint32_t *d_flag);
 // hipRTC loadable and the policy not FQ_JIT_OFF

@@ -15,17 +15,14 @@ LIB_PATH = os.path.normpath(os.path.join(_HERE, "..", "lib", "libfq_amd.so"))
 # Exported symbols promised by include/fq_gpu.h (checked by the CPU tests)
 GPU_SYMBOLS = [
     "fq_abi_version", "fq_last_error", "fq_device_count", "fq_fill_numbers_u64", "fq_fill_value",
-    "fq_fill_splitmix64", "fq_aggregate_workspace_bytes", "fq_aggregate_workspace_init", "fq_aggregate",
-    "fq_aggregate_split",
+    "fq_fill_splitmix64", "fq_aggregate_workspace_bytes", "fq_aggregate",
     "fq_arith_result_type", "fq_arith", "fq_compare", "fq_filter_workspace_bytes",
     "fq_filter_compact", "fq_state_merge", "fq_jit_config", "fq_jit_get_stats", "fq_jit_prepare",
     "fq_group_table_bytes", "fq_group_table_init", "fq_group_aggregate", "fq_group_table_count",
     "fq_group_table_extract", "fq_logic", "fq_filter_project_workspace_bytes", "fq_filter_project",
     "fq_predicate_bitmap", "fq_group_partition_workspace_bytes", "fq_group_aggregate_partitioned",
     "fq_group_dense_keys", "fq_group_table_merge", "fq_tune_set", "fq_tune_get", "fq_tune_reset",
-    "fq_tune_select_counters", "fq_tune_jit_dump_dir", "fq_filter_project_blocks_workspace_bytes",
-    "fq_filter_project_blocks", "fq_filter_project_blocks_async", "fq_filter_project_blocks_result",
-    "fq_filter_project_blocks_workspace_init", "fq_filter_project_blocks_launch",
+    "fq_tune_jit_dump_dir", "fq_filter_project_blocks_workspace_bytes", "fq_filter_project_blocks",
     "fq_blocks_compact_workspace_bytes", "fq_blocks_compact",
 ]
 
@@ -65,11 +62,8 @@ _protos = {
     "fq_fill_numbers_u64": (C.c_int32, [vp, C.c_uint64, C.c_uint64, vp]),
     "fq_fill_splitmix64": (C.c_int32, [vp, C.c_uint64, C.c_uint64, C.c_uint64, vp]),
     "fq_aggregate_workspace_bytes": (C.c_size_t, [C.c_int64]),
-    "fq_aggregate_workspace_init": (C.c_int32, [vp, C.c_size_t, vp]),
     "fq_aggregate": (C.c_int32, [P(abi.fq_col), C.c_int64, P(abi.fq_pred), P(abi.fq_expr),
                                  C.c_uint32, vp, vp, C.c_size_t, vp]),
-    "fq_aggregate_split": (C.c_int32, [P(abi.fq_col), C.c_int64, P(abi.fq_pred), P(abi.fq_expr),
-                                       C.c_uint32, vp, vp, C.c_size_t, vp, vp, vp]),
     "fq_arith_result_type": (C.c_int32, [C.c_int32, C.c_int32, C.c_int32, P(C.c_int32)]),
     "fq_arith": (C.c_int32, [C.c_int32, P(abi.fq_col), P(abi.fq_value), P(abi.fq_col),
                              P(abi.fq_value), P(abi.fq_col), vp, vp]),
@@ -89,14 +83,6 @@ _protos = {
     "fq_filter_project_blocks_workspace_bytes": (C.c_size_t, []),
     "fq_filter_project_blocks": (C.c_int32, [P(abi.fq_col), C.c_int64, P(abi.fq_pred), P(abi.fq_expr), C.c_int32,
                                              P(vp), vp, P(C.c_int64), vp, C.c_size_t, vp]),
-    "fq_filter_project_blocks_async": (C.c_int32, [P(abi.fq_col), C.c_int64, P(abi.fq_pred), P(abi.fq_expr),
-                                                   C.c_int32, P(vp), vp, P(C.c_uint64), vp, C.c_size_t, vp, vp,
-                                                   vp]),
-    "fq_filter_project_blocks_result": (C.c_int32, [P(C.c_uint64), P(C.c_int64)]),
-    "fq_filter_project_blocks_workspace_init": (C.c_int32, [vp, C.c_size_t, vp]),
-    "fq_filter_project_blocks_launch": (C.c_int32, [P(abi.fq_col), C.c_int64, P(abi.fq_pred), P(abi.fq_expr),
-                                                    C.c_int32, P(vp), vp, P(C.c_uint64), vp, vp, C.c_size_t, vp,
-                                                    vp, vp]),
     "fq_blocks_compact_workspace_bytes": (C.c_size_t, [C.c_int64]),
     "fq_blocks_compact": (C.c_int32, [C.c_int32, P(vp), C.c_int64, C.c_int64, vp, P(vp), P(C.c_int64), vp,
                                       C.c_size_t, vp]),
@@ -116,7 +102,6 @@ _protos = {
     "fq_tune_set": (C.c_int32, [C.c_int32, C.c_int64]),
     "fq_tune_get": (C.c_int64, [C.c_int32]),
     "fq_tune_reset": (C.c_int32, []),
-    "fq_tune_select_counters": (C.c_int32, [P(C.c_uint64), C.c_int32]),
     "fq_tune_jit_dump_dir": (C.c_int32, [C.c_char_p]),
 }
 for _name, (_res, _args) in _protos.items():

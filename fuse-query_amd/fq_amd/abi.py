@@ -39,7 +39,6 @@ CMP_BY_SYM = {"=": CMP_EQ, "<": CMP_LT, "<=": CMP_LTEQ, ">": CMP_GT, ">=": CMP_G
 CMP_FLIP = {CMP_EQ: CMP_EQ, CMP_LT: CMP_GT, CMP_LTEQ: CMP_GTEQ, CMP_GT: CMP_LT, CMP_GTEQ: CMP_LTEQ}
 
 AGG_MIN, AGG_MAX, AGG_SUM, AGG_COUNT = 1, 2, 4, 8
-AGG_ONE_LAUNCH = 0x100  # fq_gpu.h FQ_AGG_ONE_LAUNCH: in-launch finalize (zeroed workspace counter)
 AGG_BY_NAME = {"min": AGG_MIN, "max": AGG_MAX, "sum": AGG_SUM, "count": AGG_COUNT}
 
 OPERAND_CONST, OPERAND_COLUMN, OPERAND_STACK = 0, 1, 2
@@ -122,13 +121,8 @@ assert C.sizeof(fq_step) == 24
 
 # launch-shape knobs (fq_tune_set; tuning tools only)
 TUNE = {
-    "SCAN_WG_PER_CU": 0, "EW_WG_PER_CU": 1, "CMP_SPREAD": 2, "GPART_WG_PER_CU": 3, "GROUP_THREADS": 4,
-    "GROUP_LDS_KB": 5, "BLOCK_U": 6, "GROUP_LDS_LOCAL": 7, "GROUP_KEY_PLAIN": 8, "GROUP_WAVE_RUNS": 9,
-    "GROUP_CLUSTER": 10, "GROUP_CHUNKED": 11, "SELECT_VARIANT": 12, "SELECT_DEBUG": 13, "SELECT_LBW": 14,
-    "SELECT_WG_PER_CU": 15, "SELECT_THREADS": 16, "SELECT_ROWS": 17, "SELECT_SLEEP": 18, "BLOCK_CACHE": 19,
-    "JIT_ISOLATED": 20, "GROUP_ROWMAP": 21, "GROUP_WG_PER_CU": 22, "GROUP_RANGE_BINS": 23, "GROUP_NARROW": 24,
-    "SELECT_BLOCKS_WG_PER_CU": 25, "SELECT_BLOCKS_RUN": 26, "SELECT_BLOCKS_DRAW": 27, "SELECT_BLOCKS_ROWS": 28,
-    "SELECT_NT": 29, "GPART_DBUF": 30, "GPART_ROWS8": 31, "GPART_ROWS4": 32, "GBINS_ROWS": 33, "GBINS_WG_PER_CU": 34, "GBINS_FIT_LDS": 35,
-    "POOL_SPIN_US": 36, "SCAN_FIN": 37, "ENGINE_ONE_LAUNCH": 38, "SELECT_BLOCKS_STAGE": 39, "ENGINE_FOLD_STREAM": 40, "ENGINE_PROJECT_LAUNCH": 41, "PROJECT_HANDOFF": 42,
+    "SCAN_WG_PER_CU": 0, "EW_WG_PER_CU": 1, "BLOCK_U": 2, "SELECT_WG_PER_CU": 3, "SELECT_BLOCKS_WG_PER_CU": 4,
+    "SELECT_BLOCKS_ROWS": 5, "SELECT_BLOCKS_STAGE": 6, "BLOCK_CACHE": 7, "POOL_SPIN_US": 8, "GROUP_THREADS": 9,
+    "GROUP_LDS_KB": 10, "GROUP_WG_PER_CU": 11, "GROUP_CLUSTER": 12, "GROUP_CHUNKED": 13, "GROUP_RANGE_BINS": 14,
+    "GROUP_NARROW": 15, "GPART_WG_PER_CU": 16, "GBINS_WG_PER_CU": 17, "ENGINE_PROJECT_LAUNCH": 18,
 }
-TUNE_SELECT_COUNTERS = 13

@@ -20,6 +20,7 @@ from .expr import from_bits
 P = C.POINTER
 
 OPT_WORKER_THREADS, OPT_MODULO, OPT_PROFILE, OPT_STREAMS, OPT_CHUNK_ROWS, OPT_GROUP_CHUNK_ROWS = 1, 2, 3, 4, 5, 6
+OPT_FAULT_PIPE = 7  # testing: merged pipe k (1-based) fails its device-context setup
 PROFILE_PAIRS, PROFILE_SPAN = 1, 2  # FQ_OPT_PROFILE values
 
 ENGINE_SYMBOLS = [

@@ -164,14 +164,6 @@ class Workspace:
         return C.c_void_p(self.buf.data_ptr())
 
 
-def aggregate_workspace(stream=None):
-    """A workspace for fq_aggregate with its completion counter zeroed
-    (fq_aggregate_workspace_init): FQ_AGG_ONE_LAUNCH scans may use it."""
-    ws = Workspace(lib.fq_aggregate_workspace_bytes(0))
-    check(lib.fq_aggregate_workspace_init(ws.ptr, ws.nbytes, _stream(stream)))
-    return ws
-
-
 def aggregate_async(col, block_rows=0, pred=None, value=None, mask=0xF, ws=None, out=None,
                     stream=None):
     """Launch fq_aggregate; returns the device tensor holding the fq_agg_state."""
@@ -507,7 +499,3 @@ def tune_reset():
     check(lib.fq_tune_reset())
 
 
-def tune_select_counters():
-    out = (C.c_uint64 * abi.TUNE_SELECT_COUNTERS)()
-    check(lib.fq_tune_select_counters(out, abi.TUNE_SELECT_COUNTERS))
-    return list(out)

@@ -56,6 +56,10 @@ typedef struct fq_result fq_result;
                                    multiple of 64; default 500,000,000: at most a ~4.3 GB
                                    partition workspace, which the device block cache keeps per
                                    queue; a block is split into equal chunks of at most this) */
+#define FQ_OPT_FAULT_PIPE 7     /* testing: pipe k (1-based; 0 = off, the default) of the next
+                                   merged queries fails while it sets up its device context, as a
+                                   failed workspace allocation would -- the query must return
+                                   that error, never wait for the pipe (processor_merge.rs:50-54) */
 
 typedef struct fq_engine_stats {
     uint64_t scan_launches; /* fused aggregate scans launched                    */

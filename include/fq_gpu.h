@@ -235,31 +235,13 @@ fq_status fq_fill_value(void *d_out, int64_t n, int32_t dtype, uint64_t bits, vo
  * value may be NULL (identity).  pred may be NULL (no WHERE).
  *
  * The scan writes one partial per workgroup into the workspace; a second,
- * one-workgroup launch folds them into *d_out.  With FQ_AGG_ONE_LAUNCH in
- * agg_mask the scan's last workgroup folds them instead (same order, the
- * same bytes), so a query's scans run back to back with no launch between
- * them.  The caller then vouches that the workspace's completion counter is
- * zero: fq_aggregate_workspace_init ran on the workspace (stream-ordered before
- * the first such call) and only fq_aggregate calls used it since -- each call
- * leaves the counter zero.  Calls sharing a workspace must be ordered (one
- * stream), as for the partials.                                             */
-#define FQ_AGG_ONE_LAUNCH 0x100u
+ * one-workgroup launch folds them into *d_out in a fixed order (the same
+ * bytes run to run, float sums too).  Calls sharing a workspace must be
+ * ordered (one stream).                                                     */
 size_t fq_aggregate_workspace_bytes(int64_t len);
-fq_status fq_aggregate_workspace_init(void *d_ws, size_t ws_bytes, void *stream);
 fq_status fq_aggregate(const fq_col *col, int64_t block_rows, const fq_pred *pred,
                        const fq_expr *value, uint32_t agg_mask, fq_agg_state *d_out,
                        void *d_ws, size_t ws_bytes, void *stream);
-/* fq_aggregate with the fold on another stream: the scan on `stream`, then
- * `scan_done` (the caller's hipEvent_t) recorded behind it, `fold_stream` made
- * to wait for it and the fold launched there -- the next launch on `stream`
- * does not wait for the fold, which runs beside it.  The partials stay in the
- * workspace until the fold has run: order the workspace's next use after
- * fold_stream's work so far (e.g. an event recorded on fold_stream), and read
- * *d_out after it.  FQ_AGG_ONE_LAUNCH (no fold) is refused.                 */
-fq_status fq_aggregate_split(const fq_col *col, int64_t block_rows, const fq_pred *pred,
-                             const fq_expr *value, uint32_t agg_mask, fq_agg_state *d_out,
-                             void *d_ws, size_t ws_bytes, void *stream, void *fold_stream,
-                             void *scan_done);
 
 /* ---- ArithmeticFunction::eval (data_array_arithmetic.rs:14-55) ----
  * Exactly one of {lhs, lhs_scalar} and one of {rhs, rhs_scalar} is non-NULL.
@@ -333,36 +315,6 @@ size_t fq_filter_project_blocks_workspace_bytes(void);
 fq_status fq_filter_project_blocks(const fq_col *col, int64_t block_rows, const fq_pred *pred,
                                    const fq_expr *values, int32_t n_out, void *const *d_out, int64_t *d_counts,
                                    int64_t *out_len, void *d_ws, size_t ws_bytes, void *stream);
-/* The same without waiting: the launch is enqueued on `stream` and, when the
- * stream reaches it, the kept-row count and the flag words land in
- * h_result[0..1] (pinned host memory the copy engine can write, e.g.
- * hipHostMalloc).  After waiting (stream or event), fq_filter_project_blocks_
- * result turns them into the call's status and *out_len.  ev_start / ev_end
- * (hipEvent_t, optional): recorded on `stream` right before and right after
- * the kernel, so the pair times the kernel alone (not the workspace memset or
- * the result copy).  For hosts that keep one queue busy with several pipes'
- * launches (the engine's ProjectionTransform).                            */
-fq_status fq_filter_project_blocks_async(const fq_col *col, int64_t block_rows, const fq_pred *pred,
-                                         const fq_expr *values, int32_t n_out, void *const *d_out, int64_t *d_counts,
-                                         uint64_t *h_result, void *d_ws, size_t ws_bytes, void *ev_start,
-                                         void *ev_end, void *stream);
-fq_status fq_filter_project_blocks_result(const uint64_t *h_result, int64_t *out_len);
-/* The async launch with no memset before it and no copy after it: the
- * kernel's last workgroup writes the kept-row count and the flag words to
- * d_result (the device address of host memory the device writes, e.g.
- * hipHostMalloc(hipHostMallocMapped) + hipHostGetDevicePointer; h_result the
- * host address of the same two words) and leaves the workspace zeroed.  The
- * caller vouches that the workspace is zero: fq_filter_project_blocks_
- * workspace_init ran on it (stream-ordered before) and only these calls used
- * it since; calls sharing a workspace are ordered (one stream).  Read the
- * result with fq_filter_project_blocks_result after the stream's work.  A
- * queue that runs several such launches back to back then runs nothing but
- * the kernels (the engine's ProjectionTransform).                            */
-fq_status fq_filter_project_blocks_workspace_init(void *d_ws, size_t ws_bytes, void *stream);
-fq_status fq_filter_project_blocks_launch(const fq_col *col, int64_t block_rows, const fq_pred *pred,
-                                          const fq_expr *values, int32_t n_out, void *const *d_out, int64_t *d_counts,
-                                          uint64_t *h_result, uint64_t *d_result, void *d_ws, size_t ws_bytes,
-                                          void *ev_start, void *ev_end, void *stream);
 /* A block stream's valid rows as one array: for each of n_cols 64-bit columns
  * of the geometry above (len rows, ceil(len / block_rows) blocks, block b's
  * valid rows the first d_counts[b] of its range), d_out[j] receives block 0's
@@ -427,72 +379,34 @@ fq_status fq_jit_prepare(const fq_col *col, int64_t block_rows, const fq_pred *p
  * library reads no environment variable for them and never prints: the sweep
  * tools (bench.py --tune, tools/) set them here.  Knobs read by a hipRTC
  * kernel are part of its shape key, so a change applies from the next launch. */
-#define FQ_TUNE_SCAN_WG_PER_CU 0     /* fused aggregate scan: workgroups per CU, 2 (1..16)      */
-#define FQ_TUNE_EW_WG_PER_CU 1       /* arith/compare kernels: 0 = per-op defaults (8/2), 1..16 */
-#define FQ_TUNE_CMP_SPREAD 2         /* compare kernel scalar-unit interleave: 0 (0/1)           */
-#define FQ_TUNE_GPART_WG_PER_CU 3    /* GROUP BY partition kernel: workgroups per CU, 2 (1..4)   */
-#define FQ_TUNE_GROUP_THREADS 4      /* GROUP BY kernels: threads per workgroup, 1024 (256..1024 step 256) */
-#define FQ_TUNE_GROUP_LDS_KB 5       /* GROUP BY LDS table budget, 128 (8..160)                  */
-#define FQ_TUNE_BLOCK_U 6            /* block-mode scan: 16-B vectors per lane in flight, 8 (4/8/16) */
-#define FQ_TUNE_GROUP_LDS_LOCAL 7    /* LDS slot hash keeps consecutive keys adjacent: 1 (0/1)   */
-#define FQ_TUNE_GROUP_KEY_PLAIN 8    /* HBM key probe reads plain before atomic: 1 (0/1)          */
-#define FQ_TUNE_GROUP_WAVE_RUNS 9    /* wave-uniform key runs merged across the wave: 1 (0..2)    */
-#define FQ_TUNE_GROUP_CLUSTER 10     /* clustered row layout threshold (key changes/wave): 160 (0..512) */
-#define FQ_TUNE_GROUP_CHUNKED 11     /* contiguous tile runs per workgroup: 1 (0/1)               */
-#define FQ_TUNE_SELECT_VARIANT 12    /* filter+projection: per-class ticket counters, 0 (0/1; 1 is faster
-                                        alone on the GPU but can stall beside concurrent kernels, fq_jit.hip) */
-#define FQ_TUNE_SELECT_DEBUG 13      /* filter+projection: count phase cycles (fq_tune_select_counters), 0 (0/1) */
-#define FQ_TUNE_SELECT_LBW 14        /* look-back status words per lane per poll, 1 (1/2/4/8)     */
-#define FQ_TUNE_SELECT_WG_PER_CU 15  /* filter+projection workgroups per CU, 8 (1..16)            */
-#define FQ_TUNE_SELECT_THREADS 16    /* filter+projection threads per workgroup, 256 (256/512/1024) */
-#define FQ_TUNE_SELECT_ROWS 17       /* filter+projection rows per thread per tile, 32 (8/16/32)  */
-#define FQ_TUNE_SELECT_SLEEP 18      /* s_sleep between look-back polls, 2 (0..127)              */
-#define FQ_TUNE_BLOCK_CACHE 19       /* engine's stream-ordered device block cache, 1 (0/1)       */
-#define FQ_TUNE_JIT_ISOLATED 20      /* hipRTC loaded in its own link namespace, 1 (0/1; before the first compile) */
-#define FQ_TUNE_GROUP_ROWMAP 21      /* GROUP BY LDS kernel row map: 1 (0/1)                     */
-#define FQ_TUNE_GROUP_WG_PER_CU 22   /* GROUP BY LDS kernel workgroups per CU: 1 (1..8)           */
-#define FQ_TUNE_GROUP_RANGE_BINS 23  /* partitioned GROUP BY: range bins for `% d` keys, 1 (0/1) */
-#define FQ_TUNE_GROUP_NARROW 24      /* partitioned GROUP BY: honour FQ_GROUP_NARROW_ROWS, 1 (0/1) */
-#define FQ_TUNE_SELECT_BLOCKS_WG_PER_CU 25 /* block-stream filter+projection workgroups per CU, 8 (1..16) */
-#define FQ_TUNE_SELECT_BLOCKS_RUN 26  /* block-stream filter+projection: blocks per run, 1 (0 = one static run per workgroup) */
-#define FQ_TUNE_SELECT_BLOCKS_DRAW 27 /* block-stream runs drawn from a counter (1) or dealt round-robin (0), 1 */
-#define FQ_TUNE_SELECT_BLOCKS_ROWS 28 /* block-stream rows per thread per tile, 32 (8/16/32; tile = 256 x rows) */
-#define FQ_TUNE_SELECT_NT 29          /* nontemporal output stores: bit 0 block-stream, bit 1 contiguous kernel; 1 */
-#define FQ_TUNE_GPART_DBUF 30        /* GROUP BY partition pass (4-byte rows): tile state double-buffered, 2 barriers per tile: 1 (0/1) */
-#define FQ_TUNE_GPART_ROWS8 31       /* GROUP BY partition + bins passes, 8-byte rows: rows per thread per tile, 8 (4/8) */
-#define FQ_TUNE_GPART_ROWS4 32      /* GROUP BY partition pass, 4-byte rows: rows per thread per tile, 8 (4/8) */
-#define FQ_TUNE_GBINS_ROWS 33       /* GROUP BY bins pass, 4-byte rows: rows per thread per tile, 4 (4/8)     */
-#define FQ_TUNE_GBINS_WG_PER_CU 34  /* GROUP BY bins pass, fitted table + 4 rows: workgroups per CU, 2 (1..4) */
-#define FQ_TUNE_GBINS_FIT_LDS 35    /* GROUP BY bins pass, range bins: LDS table of one bin's keys, 1 (0/1)  */
-#define FQ_TUNE_POOL_SPIN_US 36     /* engine pipe threads poll for the next task before sleeping, 1000 us (0..100000) */
-#define FQ_TUNE_SCAN_FIN 37         /* FQ_AGG_ONE_LAUNCH partial hand-off: 0 plain store + agent release, 1 write-through
-                                       stores: 1 (0/1) */
-#define FQ_TUNE_ENGINE_ONE_LAUNCH 38 /* the engine's scans pass FQ_AGG_ONE_LAUNCH: 0 (0/1; the separate finalize
-                                       launch measured faster, profiles/r05_b_scan_fin_ab.json) */
-#define FQ_TUNE_SELECT_BLOCKS_STAGE 39 /* block-stream filter+projection: kept rows staged in LDS, written by
-                                        consecutive threads (16-byte row pairs when aligned), the stage
-                                        1/S of a tile (passes as needed): S = 2 (0 = off, 1/2/4) */
-#define FQ_TUNE_ENGINE_FOLD_STREAM 40 /* the engine's scans fold their partials on a second queue
-                                       (fq_aggregate_split) beside the next scan: 0 (0/1; measured
-                                       slower) */
-#define FQ_TUNE_ENGINE_PROJECT_LAUNCH 41 /* the engine's block projections: fq_filter_project_blocks_launch
-                                          (no memset / copy around the kernel) 1, or _async 0: 0 (0/1;
-                                          the kernel's own hand-off measured slower) */
-#define FQ_TUNE_PROJECT_HANDOFF 42 /* fq_filter_project_blocks_launch: the kernel's last workgroup hands the
-                                    result over (1) or a one-thread kernel after it (0): 0 (0/1) */
-#define FQ_TUNE_COUNT 43
+#define FQ_TUNE_SCAN_WG_PER_CU 0      /* fused aggregate scan: workgroups per CU, 2 (1..16)           */
+#define FQ_TUNE_EW_WG_PER_CU 1        /* arith/compare kernels: 0 = per-op defaults (8/2), 1..16      */
+#define FQ_TUNE_BLOCK_U 2             /* block-mode scan: 16-B vectors per lane in flight, 8 (4/8/16) */
+#define FQ_TUNE_SELECT_WG_PER_CU 3    /* filter+projection (look-back kernel): workgroups per CU, 8 (1..16) */
+#define FQ_TUNE_SELECT_BLOCKS_WG_PER_CU 4 /* block-stream filter+projection: workgroups per CU, 8 (1..16) */
+#define FQ_TUNE_SELECT_BLOCKS_ROWS 5  /* block-stream filter+projection: rows per thread per tile, 32 (8/16/32) */
+#define FQ_TUNE_SELECT_BLOCKS_STAGE 6 /* block-stream filter+projection: kept rows staged in LDS and written by
+                                         consecutive threads, the stage 1/S of a tile: S = 2 (0 = off, 1/2/4) */
+#define FQ_TUNE_BLOCK_CACHE 7         /* engine's stream-ordered device block cache, 1 (0/1)          */
+#define FQ_TUNE_POOL_SPIN_US 8        /* engine pipe threads poll for the next task before sleeping, 0 us (0..100000) */
+#define FQ_TUNE_GROUP_THREADS 9       /* GROUP BY kernels: threads per workgroup, 1024 (256..1024 step 256) */
+#define FQ_TUNE_GROUP_LDS_KB 10       /* GROUP BY LDS table budget, 128 (8..160)                      */
+#define FQ_TUNE_GROUP_WG_PER_CU 11    /* GROUP BY LDS kernel workgroups per CU: 1 (1..8)              */
+#define FQ_TUNE_GROUP_CLUSTER 12      /* clustered row layout threshold (key changes/wave): 160 (0..512) */
+#define FQ_TUNE_GROUP_CHUNKED 13      /* contiguous tile runs per workgroup: 1 (0/1)                  */
+#define FQ_TUNE_GROUP_RANGE_BINS 14   /* partitioned GROUP BY: range bins for `% d` keys, 1 (0/1)     */
+#define FQ_TUNE_GROUP_NARROW 15       /* partitioned GROUP BY: honour FQ_GROUP_NARROW_ROWS, 1 (0/1)   */
+#define FQ_TUNE_GPART_WG_PER_CU 16    /* GROUP BY partition kernel: workgroups per CU, 2 (1..4)       */
+#define FQ_TUNE_GBINS_WG_PER_CU 17    /* GROUP BY bins pass, fitted table: workgroups per CU, 2 (1..4) */
+#define FQ_TUNE_ENGINE_PROJECT_LAUNCH 18 /* the engine's block projections: what sits on the queue around each
+                                            kernel (engine/functions.cpp project_blocks), 0 (0..2) */
+#define FQ_TUNE_COUNT 19
 /* FQ_E_INVALID for an unknown knob or a value outside the knob's set */
 fq_status fq_tune_set(int32_t knob, int64_t value);
 /* the knob's current value; -1 for an unknown knob */
 int64_t fq_tune_get(int32_t knob);
 /* every knob back to its default */
 fq_status fq_tune_reset(void);
-/* Counters of the last fq_jit_pselect launch made with FQ_TUNE_SELECT_DEBUG
- * = 1 (FQ_TUNE_SELECT_COUNTERS words: tiles, polls, look-back, ticket,
- * load+predicate, store cycles, workgroup cycles, look-back windows, first/last
- * workgroup start, first/last end, summed workgroup life); n <= that.       */
-#define FQ_TUNE_SELECT_COUNTERS 13
-fq_status fq_tune_select_counters(uint64_t *out, int32_t n);
 /* dir != NULL: every hipRTC source compiled from now on is written to dir
  * (with its code object) for ISA inspection; NULL turns it off.            */
 fq_status fq_tune_jit_dump_dir(const char *dir);

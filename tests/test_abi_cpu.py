@@ -153,16 +153,28 @@ def test_engine_and_function_symbol_lists_match_header():
 
 def test_tuning_knobs_defaults_set_reset():
     from fq_amd import ops
-    assert ops.tune_get("SCAN_WG_PER_CU") == 2 and ops.tune_get("SELECT_LBW") == 1
-    assert ops.tune_get("SELECT_THREADS") == 256 and ops.tune_get("GROUP_LDS_KB") == 128
-    ops.tune_set("SELECT_LBW", 4)
-    assert ops.tune_get("SELECT_LBW") == 4
-    for name, bad in [("SELECT_LBW", 3), ("SELECT_THREADS", 768), ("GROUP_THREADS", 300), ("SCAN_WG_PER_CU", 0)]:
+    assert ops.tune_get("SCAN_WG_PER_CU") == 2 and ops.tune_get("SELECT_BLOCKS_STAGE") == 2
+    assert ops.tune_get("POOL_SPIN_US") == 0 and ops.tune_get("GROUP_LDS_KB") == 128
+    ops.tune_set("SELECT_BLOCKS_STAGE", 4)
+    assert ops.tune_get("SELECT_BLOCKS_STAGE") == 4
+    for name, bad in [("SELECT_BLOCKS_STAGE", 3), ("SELECT_BLOCKS_ROWS", 12), ("GROUP_THREADS", 300),
+                      ("SCAN_WG_PER_CU", 0)]:
         with pytest.raises(Exception, match="outside knob"):
             ops.tune_set(name, bad)
     ops.tune_reset()
-    assert ops.tune_get("SELECT_LBW") == 1
+    assert ops.tune_get("SELECT_BLOCKS_STAGE") == 2
     assert lib.fq_tune_get(99) == -1
+
+
+def test_knob_table_is_small_and_mirrored():
+    """The launch-shape knobs are the ones a sweep can still move (VERDICT round
+    5: at most ~20); abi.TUNE mirrors include/fq_gpu.h name for name."""
+    from fq_amd import abi
+    hdr = open(os.path.join(ROOT, "include", "fq_gpu.h")).read()
+    declared = dict((m.group(1), int(m.group(2))) for m in re.finditer(r"#define FQ_TUNE_(\w+) (\d+)", hdr))
+    count = declared.pop("COUNT")
+    assert count <= 20 and sorted(declared.values()) == list(range(count))
+    assert declared == abi.TUNE
 
 
 def test_product_reads_no_tuning_environment_and_never_prints():

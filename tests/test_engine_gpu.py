@@ -276,6 +276,30 @@ def test_error_aggregate_in_where():
         "Internal Error: Aggregate function (sum([number]) > 1) is found in WHERE in query"
 
 
+@pytest.mark.parametrize("pipe", [1, 4, 8])
+@pytest.mark.parametrize("sql", [
+    "SELECT sum(number)/count(number), max(number), min(number) FROM system.numbers_mt(8000000)",
+    "SELECT max(number+1) FROM system.numbers_mt(8000000) WHERE (number%8)<3",
+    # a LIMIT no partition can satisfy: every pipe is read to its end
+    "SELECT number+1, number/2 FROM system.numbers_mt(8000000) WHERE number%999999937 = 0 LIMIT 3",
+])
+def test_pipe_that_cannot_set_up_its_context_fails_the_query(sql, pipe):
+    """A pipe whose device context cannot be set up (a failed workspace
+    allocation, forced by FQ_OPT_FAULT_PIPE) sends its error the way the
+    reference's task sends Err (processor_merge.rs:50-54) and releases its place
+    in the query's scan group: the query returns the error -- the other pipes'
+    deferred states never wait for it -- and the engine runs on."""
+    from fq_amd import FQError
+    from fq_amd.engine import OPT_FAULT_PIPE
+    with Engine(profile=True) as e2:
+        want = e2.execute(sql).rows
+        e2.set_option(OPT_FAULT_PIPE, pipe)
+        with pytest.raises(FQError, match="out of memory"):
+            e2.execute(sql)
+        e2.set_option(OPT_FAULT_PIPE, 0)
+        assert e2.execute(sql).rows == want
+
+
 # ---- distributed split on one device ---------------------------------------
 
 def test_partial_final_split_matches_single_pipeline():

@@ -262,136 +262,12 @@ def test_specialised_scan_bit_identical_to_interpreter(shape, jit_mode):
     assert got == exp
 
 
-ONE_LAUNCH_SHAPES = ["identity", "i32", "chain_f64", "c4", "block_sum", "bitmap", "one_wg", "none_pass", "empty"]
-
-
-@pytest.mark.parametrize("shape", ONE_LAUNCH_SHAPES)
-def test_one_launch_finalize_bit_identical(shape, jit_mode):
-    """FQ_AGG_ONE_LAUNCH: the scan's last workgroup folds the partials (agent-scope
-    release / ticket / acquire, fq_aggregate.hip finish_in_launch and the hipRTC
-    twin) instead of the finalize launch -- the same fold order, so the same
-    fq_agg_state bytes, every launch, on one workspace whose counter each launch
-    leaves at zero."""
-    import torch
-    n, br, pred, value, mask = 3_000_017, 0, None, None, ALL
-    col = ops.splitmix_column(0x1A, 0, n)
-    if shape == "i32":
-        x = np.random.default_rng(5).integers(-2**31, 2**31, 1_000_003, dtype=np.int64).astype(np.int32)
-        col = ops.from_numpy(x, abi.DT_INT32)
-    elif shape == "chain_f64":
-        value, _ = chain(abi.DT_UINT64, [("%", 1000), ("*", 0.5), ("+", COL)])
-    elif shape == "c4":
-        value, _ = chain(abi.DT_UINT64, [("+", 1)])
-        pred = predicate(abi.DT_UINT64, [("%", 8)], "<", 3)
-        mask = abi.AGG_MAX | abi.AGG_COUNT
-    elif shape == "block_sum":  # block mode: the per-block emptiness flag travels through the fold
-        col = ops.numbers_column(0, 200_000)
-        pred = predicate(abi.DT_UINT64, [("/", 10000)], "<", 3)  # blocks 3.. are empty
-        br = 10000
-    elif shape == "bitmap":
-        bm = ops.compare("<", col, 2**63)
-        pred = abi.fq_pred()
-        pred.kind = abi.PRED_BITMAP
-        pred.bitmap = bm.ptr
-    elif shape == "one_wg":  # a grid of one workgroup: it is its own last
-        col = ops.numbers_column(5, 1000)
-    elif shape == "none_pass":  # one block, nothing passes: empty_if_zero through the fold
-        col = ops.numbers_column(0, 5000)
-        pred = predicate(abi.DT_UINT64, [], ">", 10**9)
-        mask = abi.AGG_SUM | abi.AGG_COUNT
-    elif shape == "empty":
-        col = ops.numbers_column(0, 0)
-    exp = bytes(ops.aggregate(col, br, pred, value, mask))
-    ws = ops.aggregate_workspace()
-    for _ in range(3):
-        got = bytes(ops.aggregate(col, br, pred, value, mask | abi.AGG_ONE_LAUNCH, ws=ws))
-        assert got == exp, shape
-    torch.cuda.synchronize()
-    counter = ws.buf[4096 * 48:4096 * 48 + 4].cpu().numpy().view(np.uint32)[0]
-    assert counter == 0
-
-
-@pytest.mark.parametrize("shape", ONE_LAUNCH_SHAPES + ["count_column"])
-def test_split_fold_bit_identical(shape, jit_mode):
-    """fq_aggregate_split: the scan on one stream, its fold on another behind an
-    event -- the same fq_agg_state bytes as fq_aggregate.  Three scans on one
-    stream into three outputs, each fold waiting only for its scan; the next
-    scan reuses the workspace only after the previous fold (an event on the fold
-    stream), as the engine orders it."""
-    import ctypes as C
-
-    import torch
-
-    from fq_amd._lib import check, lib
-    n, br, pred, value, mask = 2_000_003, 0, None, None, ALL
-    col = ops.splitmix_column(0x5B, 0, n)
-    if shape == "i32":
-        x = np.random.default_rng(6).integers(-2**31, 2**31, 700_001, dtype=np.int64).astype(np.int32)
-        col = ops.from_numpy(x, abi.DT_INT32)
-    elif shape == "chain_f64":
-        value, _ = chain(abi.DT_UINT64, [("%", 1000), ("*", 0.5), ("+", COL)])
-    elif shape == "c4":
-        value, _ = chain(abi.DT_UINT64, [("+", 1)])
-        pred = predicate(abi.DT_UINT64, [("%", 8)], "<", 3)
-        mask = abi.AGG_MAX | abi.AGG_COUNT
-    elif shape == "block_sum":
-        col = ops.numbers_column(0, 200_000)
-        pred = predicate(abi.DT_UINT64, [("/", 10000)], "<", 3)
-        br = 10000
-    elif shape == "bitmap":
-        bm = ops.compare("<", col, 2**63)
-        pred = abi.fq_pred()
-        pred.kind = abi.PRED_BITMAP
-        pred.bitmap = bm.ptr
-    elif shape == "one_wg":
-        col = ops.numbers_column(5, 1000)
-    elif shape == "none_pass":
-        col = ops.numbers_column(0, 5000)
-        pred = predicate(abi.DT_UINT64, [], ">", 10**9)
-        mask = abi.AGG_SUM | abi.AGG_COUNT
-    elif shape == "empty":
-        col = ops.numbers_column(0, 0)
-    elif shape == "count_column":  # count(column): no scan, the fold alone
-        mask = abi.AGG_COUNT
-    exp = bytes(ops.aggregate(col, br, pred, value, mask))
-    ws = ops.aggregate_workspace()
-    scan_s, fold_s = torch.cuda.Stream(), torch.cuda.Stream()
-    ev = torch.cuda.Event()
-    ev.record(scan_s)  # torch creates the HIP event on its first record
-    fold_done = torch.cuda.Event()
-    outs = [torch.zeros(48, dtype=torch.uint8, device="cuda") for _ in range(3)]
-    c = col.col()
-    torch.cuda.synchronize()
-    for i, out in enumerate(outs):
-        if i:
-            scan_s.wait_event(fold_done)
-        check(lib.fq_aggregate_split(C.byref(c), br, C.byref(pred) if pred is not None else None,
-                                     C.byref(value) if value is not None else None, mask,
-                                     C.c_void_p(out.data_ptr()), ws.ptr, ws.nbytes,
-                                     C.c_void_p(scan_s.cuda_stream), C.c_void_p(fold_s.cuda_stream),
-                                     C.c_void_p(ev.cuda_event)))
-        fold_done.record(fold_s)
-    torch.cuda.synchronize()
-    for out in outs:
-        assert bytes(out.cpu().numpy()) == exp, shape
-    # refused: no fold stream, the scan's own stream, an in-launch fold
-    args = (C.byref(c), br, C.byref(pred) if pred is not None else None,
-            C.byref(value) if value is not None else None)
-    tail = (C.c_void_p(outs[0].data_ptr()), ws.ptr, ws.nbytes, C.c_void_p(scan_s.cuda_stream))
-    assert lib.fq_aggregate_split(*args, mask, *tail, None, C.c_void_p(ev.cuda_event)) == abi.FQ_E_INVALID
-    assert lib.fq_aggregate_split(*args, mask, *tail, C.c_void_p(scan_s.cuda_stream),
-                                  C.c_void_p(ev.cuda_event)) == abi.FQ_E_INVALID
-    assert lib.fq_aggregate_split(*args, mask | abi.AGG_ONE_LAUNCH, *tail, C.c_void_p(fold_s.cuda_stream),
-                                  C.c_void_p(ev.cuda_event)) == abi.FQ_E_INVALID
-    torch.cuda.synchronize()
-
-
-def test_one_launch_needs_the_counter_in_the_workspace():
+def test_unknown_aggregate_mask_bits_are_refused():
+    """agg_mask carries FQ_AGG_* bits only (round 5's in-launch finalize flag
+    0x100 is gone with its variant)."""
     col = ops.numbers_column(0, 100_000)
-    small = ops.Workspace(4096 * 48)  # the partials only (the pre-counter size)
-    ops.aggregate(col, 0, None, None, ALL, ws=small)  # two launches: fine
-    with pytest.raises(Exception, match="workspace too small"):
-        ops.aggregate(col, 0, None, None, ALL | abi.AGG_ONE_LAUNCH, ws=small)
+    with pytest.raises(Exception, match="unknown bits"):
+        ops.aggregate(col, 0, None, None, ALL | 0x100)
 
 
 def _trunc_divmod(a, b):

@@ -271,76 +271,6 @@ def test_block_outputs_not_16_byte_aligned(block_rows):
            [lambda k: k + np.uint64(1), lambda k: k], block_rows, out_offset=1)
 
 
-@pytest.mark.parametrize("handoff", [0, 1], ids=["after_kernel", "in_kernel"])
-@pytest.mark.parametrize("sel", ["mod8", "none_kept", "div_zero"])
-def test_launch_without_memset_or_copy_matches_async(sel, handoff):
-    """fq_filter_project_blocks_launch: the workspace zeroed once; {kept,
-    flags} written to d_result and the workspace re-zeroed by a one-thread
-    kernel after the projection (FQ_TUNE_PROJECT_HANDOFF 0) or by its last
-    workgroup (1) -- the same outputs, counts, kept rows and status as the
-    async path, launch after launch on one workspace (which ends zeroed)."""
-    ops.tune_set("PROJECT_HANDOFF", handoff)
-    import ctypes as C
-
-    from fq_amd._lib import lib
-    n, br = 1_000_003, 10_000
-    host = np.arange(n, dtype=np.uint64) * np.uint64(3)
-    col = ops.from_numpy(host)
-    if sel == "mod8":
-        pred, vals = predicate(U64, [("%", 8)], "<", 3), [chain(U64, [("+", 1)])[0], None]
-    elif sel == "none_kept":
-        pred, vals = predicate(U64, [], ">", 2**62), [None]
-    else:  # 7 / (number - 300): the zero divisor only on a kept row
-        pred, vals = predicate(U64, [], ">", 200), [chain(U64, [("-", 300), ("/", 7, True)])[0]]
-    exp_outs, exp_counts = None, None
-    try:
-        exp_outs, exp_counts = ops.filter_project_blocks(col, br, pred, vals)
-        exp_err = None
-    except ops.FQError as e:
-        exp_err = e
-    nb = -(-n // br)
-    exprs = (abi.fq_expr * len(vals))()
-    for j, v in enumerate(vals):
-        if v is None:
-            v = abi.fq_expr()
-            v.n_steps = 0
-            v.out_dtype = U64
-        exprs[j] = v
-    wsb = lib.fq_filter_project_blocks_workspace_bytes()
-    ws = ops.Workspace(wsb)
-    assert lib.fq_filter_project_blocks_workspace_init(ws.ptr, ws.nbytes, None) == abi.FQ_OK
-    # the kernel writes the two words to any device-writable address: here a
-    # device buffer, copied back (the engine passes mapped host memory)
-    dres = torch.zeros(2, dtype=torch.int64, device="cuda")
-    hres = (C.c_uint64 * 2)()
-    c = col.col()
-    for _ in range(3):
-        outs = [ops.empty_column(n, exprs[j].out_dtype) for j in range(len(vals))]
-        ptrs = (C.c_void_p * len(outs))(*[o.ptr for o in outs])
-        counts = ops.Workspace(8 * nb)
-        dres.fill_(-1)
-        st = lib.fq_filter_project_blocks_launch(C.byref(c), br, C.byref(pred), exprs, len(vals), ptrs, counts.ptr,
-                                                 hres, C.c_void_p(dres.data_ptr()), ws.ptr, ws.nbytes, None, None,
-                                                 None)
-        assert st == abi.FQ_OK, ops.lib.fq_last_error()
-        torch.cuda.synchronize()
-        words = dres.cpu().numpy().view(np.uint64)
-        hres[0], hres[1] = int(words[0]), int(words[1])
-        kept = C.c_int64(-1)
-        st = lib.fq_filter_project_blocks_result(hres, C.byref(kept))
-        if exp_err is not None:
-            assert st == exp_err.status
-        else:
-            assert st == abi.FQ_OK and kept.value == int(exp_counts.sum())
-            got = counts.buf[:8 * nb].view(torch.int64).cpu().numpy()
-            assert np.array_equal(got, exp_counts)
-            for o, e in zip(_blocks_of(outs, got, br), _blocks_of(exp_outs, exp_counts, br)):
-                for gb, eb in zip(o, e):
-                    assert np.array_equal(gb, eb)
-        assert not ws.buf[:wsb].cpu().numpy().any()  # left zeroed for the next launch
-    ops.tune_set("PROJECT_HANDOFF", 0)
-
-
 @pytest.mark.parametrize("n_blocks,block_rows,n_cols", [(3000, 64, 1), (20011, 17, 2), (50000, 8, 3), (1025, 1000, 2)])
 def test_blocks_compact_multi_chunk_scan(n_blocks, block_rows, n_cols):
     """fq_blocks_compact straight through the C ABI with more blocks than one

@@ -25,14 +25,49 @@ def setup_module():
     ops = _ops
 
 
-@pytest.fixture(autouse=True, params=[0, 1], ids=["one_ticket", "xcd_tickets"])
-def ticket_variant(request):
-    """Every test with the default single ticket counter and with the per-XCD
-    counters (FQ_TUNE_SELECT_VARIANT 1)."""
-    before = ops.tune_get("SELECT_VARIANT")
-    ops.tune_set("SELECT_VARIANT", request.param)
-    yield request.param
-    ops.tune_set("SELECT_VARIANT", before)
+def test_two_lookback_launches_side_by_side():
+    """The configuration that stalled once in round 5 ("the offset look-back did
+    not complete"): look-back launches running together on separate queues, each
+    with more workgroups than stay resident beside the other.  Two host threads,
+    each on its own HIP stream, run fq_filter_project over its own 4e7-row
+    column four times (4,883 tiles, a grid of up to 2,048 workgroups per launch)
+    -- every launch completes with numpy's rows.  The single ticket counter
+    draws tiles in order, so the lowest unfinished tile's predecessors are all
+    held by resident workgroups whatever else shares the GPU (fq_jit.hip)."""
+    import threading
+
+    import torch
+    n = 40_000_000
+    cases = []
+    for seed, (mod, lt) in ((0x11, (8, 3)), (0x22, (1000, 500))):
+        col = ops.splitmix_column(seed, 0, n)
+        host = col.to_numpy()
+        keep = host % np.uint64(mod) < np.uint64(lt)
+        cases.append((col, predicate(U64, [("%", mod)], "<", lt), host[keep]))
+    torch.cuda.synchronize()
+    start = threading.Barrier(2)
+    errors = []
+
+    def run(col, pred, kept):
+        try:
+            stream = torch.cuda.Stream()
+            with torch.cuda.stream(stream):
+                start.wait()
+                for _ in range(4):
+                    outs = ops.filter_project(col, pred, [chain(U64, [("+", 1)])[0]], stream=stream)
+                    got = outs[0].to_numpy()
+                    if outs[0].len != len(kept) or not np.array_equal(got, kept + np.uint64(1)):
+                        errors.append("rows differ")
+        except Exception as e:  # the poll bound reports "did not complete"
+            errors.append(repr(e))
+
+    threads = [threading.Thread(target=run, args=c) for c in cases]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=100)
+    assert not any(t.is_alive() for t in threads), "a look-back launch did not finish"
+    assert errors == []
 
 
 def _u(x):

@@ -47,7 +47,8 @@ def main():
     sql = bench.PROJECT_SQL.format(N=N)
     mine = bench.shard(bench.generate_parts(N), 0, 1)
     expect = bench._p1_expect(mine)
-    eng = Engine(device=0, profile=True)
+    # P1_PROFILE=0: no timing events at all (kernel_ms then comes from rocprof)
+    eng = Engine(device=0, profile=os.environ.get("P1_PROFILE", "1") != "0")
     eng.materialize_numbers(N, 0, 1)
     torch.cuda.synchronize()
 
@@ -85,14 +86,15 @@ def main():
             kms = st["project_ms"] / launches
             res[c]["step_ms"].append(dt)
             res[c]["kernel_ms"].append(kms)
-            res[c]["frac"].append(st["project_bytes"] / launches / (kms * 1e-3) / 1e9 / bench.HBM_PEAK_GBPS)
+            res[c]["frac"].append(st["project_bytes"] / launches / (kms * 1e-3) / 1e9 / bench.HBM_PEAK_GBPS
+                                  if kms > 0 else None)
     ops.tune_reset()
     eng.close()
     out = {"rounds": ROUNDS, "steps": STEPS, "workload": sql, "configs": {}}
     for c, v in res.items():
         out["configs"][",".join("%s=%d" % kv for kv in c)] = {
             "step_ms_median": statistics.median(v["step_ms"]), "kernel_ms_median": statistics.median(v["kernel_ms"]),
-            "frac_median": statistics.median(v["frac"]), "kernel_ms_all": v["kernel_ms"], "step_ms_all": v["step_ms"]}
+            "frac_median": statistics.median(v["frac"]) if None not in v["frac"] else None, "kernel_ms_all": v["kernel_ms"], "step_ms_all": v["step_ms"]}
     print(json.dumps(out, indent=1))
 
 
