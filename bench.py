@@ -992,11 +992,29 @@ def main():
     execute_row = _lib.fq_engine_execute_row
     eng_h = eng.h
 
-    def c_row_call():
-        # one call: execute, the row's values into row_buf, the result freed (fq_engine_execute_row)
-        st = execute_row(eng_h, sql_b, row_buf, 8, ncols_ref)
-        if st:
-            _check(st)
+    if world == 1:
+        def c_row_call():
+            # one call: execute, the row's values into row_buf, the result freed (fq_engine_execute_row)
+            st = execute_row(eng_h, sql_b, row_buf, 8, ncols_ref)
+            if st:
+                _check(st)
+    elif comm is not None:
+        # one call at world > 1 too: partial -> RCCL exchange -> final -> the row
+        # (fq_engine_execute_rccl_row), the exchange bounded by the communicator's deadline
+        rccl_row, comm_h = _lib.fq_engine_execute_rccl_row, comm.h
+
+        def c_row_call():
+            st = rccl_row(eng_h, sql_b, comm_h, row_buf, 8, ncols_ref)
+            if st:
+                _check(st)
+    else:
+        # the gloo rehearsal: the same protocol through the torch callback
+        ex_row, fn = _lib.fq_engine_execute_exchange_row, fqd.torch_allreduce_fn(None, args.comm_timeout_ms / 1e3)
+
+        def c_row_call():
+            st = ex_row(eng_h, sql_b, rank, world, fn, None, row_buf, 8, ncols_ref)
+            if st:
+                _check(st)
 
     def row_values():
         return [v.bits if v.is_some else None for v in row_buf[:ncols.value]]
@@ -1022,10 +1040,11 @@ def main():
             _lib.fq_result_free(out)
 
     def step():
+        if args.query not in GROUP_MOD:
+            return c_row()
         if world == 1:
-            return c_groups() if args.query in GROUP_MOD else c_row()
-        r = fqd.execute(eng, sql, comm)
-        return r.rows if args.query in GROUP_MOD else list(r.rows[0])
+            return c_groups()
+        return fqd.execute(eng, sql, comm).rows
 
     def same_result(got, expect):
         if args.query in GROUP_MOD and world == 1:
@@ -1049,9 +1068,10 @@ def main():
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
-    # an ungrouped query on one GPU: the timed steps leave each step's row in
-    # row_buf and the Python list is built once, from the last step's row
-    one_row = world == 1 and args.query not in GROUP_MOD
+    # an ungrouped query: each timed step is ONE library call (world 1:
+    # fq_engine_execute_row; world > 1: fq_engine_execute_rccl_row) that leaves
+    # its row in row_buf; the Python list is built once, from the last step's row
+    one_row = args.query not in GROUP_MOD
     timed = c_row_call if one_row else step
     for _ in range(args.steps):
         res = timed()
@@ -1077,6 +1097,20 @@ def main():
     rows_per_launch = st["scan_rows"] / launches
     achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9  # algorithmic GB/s of the fused scan
     value = n_total * args.steps / dt
+    # every rank's own scan fraction and exchange time: the line reports the
+    # spread (the slowest rank sets the step)
+    per_rank = None
+    if world > 1:
+        mine_stats = torch.tensor([achieved / HBM_PEAK_GBPS, st.get("exchange_ms", 0.0) / args.steps,
+                                   st.get("partial_ms", 0.0) / args.steps],
+                                  dtype=torch.float64, device="cuda" if args.dist_backend == "nccl" else "cpu")
+        gathered = [torch.zeros_like(mine_stats) for _ in range(world)]
+        dist.all_gather(gathered, mine_stats)
+        g = [t.cpu().tolist() for t in gathered]
+        per_rank = {"scan_frac": {"min": min(x[0] for x in g), "max": max(x[0] for x in g)},
+                    "exchange_ms_per_step": {"min": min(x[1] for x in g), "max": max(x[1] for x in g)},
+                    "partial_ms_per_step": {"min": min(x[2] for x in g), "max": max(x[2] for x in g)},
+                    "ranks": world}
     rccl_w1 = None
     if world == 1 and args.dist_backend == "nccl" and args.query not in GROUP_MOD and not args.no_rccl_world1:
         rccl_w1 = rccl_world1(eng, sql, expect, local, args)
@@ -1120,8 +1154,9 @@ def main():
                 "block_rows": BLOCK_SIZE,
                 "path": "fq_engine_execute: SQL -> PipelineBuilder -> Source x P -> AggregatePartial x P "
                         "(fused gfx950 scan) -> Merge -> AggregateFinal"
-                        + ("" if world == 1 else " ; cross-GPU: fq_engine_execute_rccl, one ncclAllReduce of partial states"
-                            if comm is not None else " ; cross-GPU: fq_engine_execute_exchange over torch.distributed (%s)"
+                        + ("" if world == 1 else " ; cross-GPU: fq_engine_execute_rccl_row (one call per step), one "
+                            "ncclAllReduce of partial states" if comm is not None else
+                            " ; cross-GPU: fq_engine_execute_exchange_row over torch.distributed (%s)"
                             % args.dist_backend),
                 "parallelism": "dp%d (numbers_mt partitions sharded, %s all-reduce of states)"
                                % (world, "RCCL" if args.dist_backend == "nccl" else "gloo rehearsal"),
@@ -1160,6 +1195,9 @@ def main():
             "jit": {"specialised_launches": jitted, "kernels_compiled": jit1["kernels_compiled"],
                     "compile_ms": jit1["compile_ms"], "mode": jit1["mode"]},
         }
+        if per_rank is not None:
+            out["per_rank"] = per_rank
+            out["roofline"]["frac_min_over_ranks"] = per_rank["scan_frac"]["min"]
     if world > 1:
         dist.barrier()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -789,20 +789,26 @@ const char *fq_result_text(const fq_result *r, int64_t row, int32_t col) {
 }
 void fq_result_free(fq_result *r) { delete r; }
 
+// a one-row result's values into row[] (the first min(cap, columns)), the
+// result freed: fq_engine_execute_row and the exchange _row calls (fq_comm.cpp)
+fq_status fq_result_take_row(fq_result *r, fq_value *row, int32_t cap, int32_t *ncols, const char *what) {
+    std::unique_ptr<fq_result> hold(r);
+    const int64_t rows = fq_result_num_rows(r);
+    if (rows != 1)
+        return fqc::fail(FQ_E_INVALID,
+                         std::string(what) + ": the statement returned " + std::to_string(rows) + " rows, not one");
+    *ncols = (int32_t)r->cols.size();
+    for (int32_t c = 0; c < *ncols && c < cap; ++c) row[c] = r->cols[(size_t)c].abi(0);
+    return FQ_OK;
+}
+
 fq_status fq_engine_execute_row(fq_engine *e, const char *sql, fq_value *row, int32_t cap, int32_t *ncols) {
     if (!e || !sql || !ncols || cap < 0 || (cap > 0 && !row))
         return fqc::fail(FQ_E_INVALID, "fq_engine_execute_row: NULL argument");
     fq_result *r = nullptr;
     const fq_status s = fq_engine_execute(e, sql, &r);
     if (s != FQ_OK) return s;
-    std::unique_ptr<fq_result> hold(r);
-    const int64_t rows = fq_result_num_rows(r);
-    if (rows != 1)
-        return fqc::fail(FQ_E_INVALID,
-                         "fq_engine_execute_row: the statement returned " + std::to_string(rows) + " rows, not one");
-    *ncols = (int32_t)r->cols.size();
-    for (int32_t c = 0; c < *ncols && c < cap; ++c) row[c] = r->cols[(size_t)c].abi(0);
-    return FQ_OK;
+    return fq_result_take_row(r, row, cap, ncols, "fq_engine_execute_row");
 }
 
 }  // extern "C"

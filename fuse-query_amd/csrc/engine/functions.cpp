@@ -750,7 +750,8 @@ static bool project_blocks(const DataBlock &b, const Column &c, const fq_pred *p
     layout->n_blocks = n == 0 ? 0 : nb;
     layout->counts = DeviceBuffer::alloc((size_t)std::max<int64_t>(nb, 1) * 8, ctx.stream());
     // (no predicate: the map kernel, whose words the host writes -- mode 0)
-    const int mode = pred && pred->kind != FQ_PRED_NONE ? (int)fqc::knob(FQ_TUNE_ENGINE_PROJECT_LAUNCH) : 0;
+    // (an empty block launches nothing -- no hand-off to wait for: mode 0)
+    const int mode = pred && pred->kind != FQ_PRED_NONE && n > 0 ? (int)fqc::knob(FQ_TUNE_ENGINE_PROJECT_LAUNCH) : 0;
     ctx.res->project_resident();
     uint64_t *res = ctx.res->project_res;
     std::shared_ptr<DeviceBuffer> ws;

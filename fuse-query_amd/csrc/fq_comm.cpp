@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <chrono>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include <rccl/rccl.h>
@@ -20,16 +21,32 @@ struct fq_comm {
     uint64_t *d_buf = nullptr;  // device staging for fq_comm_allreduce_u64
     uint64_t *h_buf = nullptr;  // pinned host staging
     int64_t cap_words = 0;
+    int64_t timeout_ms = FQ_COMM_TIMEOUT_MS;  // fq_comm_set_timeout
+    bool aborted = false;                    // ncclCommAbort ran: every later call fails
+    std::string abort_reason;
 };
 
 // engine/capi_engine.cpp
 void fq_engine_note_exchange(fq_engine *e, int64_t ns, uint64_t rounds, uint64_t bytes);
+extern "C" fq_status fq_result_take_row(fq_result *r, fq_value *row, int32_t cap, int32_t *ncols, const char *what);
 
 namespace {
 
 int64_t now_ns() {
     return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
         .count();
+}
+
+// ncclCommAbort, once: the communicator is unusable afterwards (its collective
+// kernels stopped, its staging buffers possibly half written)
+fq_status fq_comm_abort_reason(fq_comm *c, const std::string &why) {
+    if (!c->aborted) {
+        c->aborted = true;
+        c->abort_reason = "rank " + std::to_string(c->rank) + " of " + std::to_string(c->world) + ": " + why;
+        (void)ncclCommAbort(c->nccl);
+        c->nccl = nullptr;
+    }
+    return fqc::fail(FQ_E_RCCL, c->abort_reason);
 }
 
 // first bytes of an exchanged row that carries a rank's error instead of its
@@ -45,6 +62,39 @@ fq_status nccl_fail(ncclResult_t r, const char *what) {
         ncclResult_t fq_r_ = (expr);                             \
         if (fq_r_ != ncclSuccess) return nccl_fail(fq_r_, #expr); \
     } while (0)
+
+// The communicator is non-blocking (ncclCommInitRankConfig, blocking = 0):
+// every RCCL step returns at once and this loop waits for it -- `done` true --
+// while watching the communicator's asynchronous error and a deadline.  A
+// peer that crashed, or never reaches the collective, would otherwise leave
+// this rank spinning in it for ever (the reference's merge sees a failed
+// task's Err on its channel instead, processor_merge.rs:50-54): past the
+// deadline, or on an RCCL error, the communicator is aborted (ncclCommAbort
+// also stops this rank's collective kernel) and the call fails with the rank
+// and the step named.
+template <class Done>
+fq_status comm_wait(fq_comm *c, const char *what, Done done) {
+    const int64_t t0 = now_ns();
+    const int64_t limit = c->timeout_ms * 1000000;
+    for (int spin = 0;; ++spin) {
+        const int d = done();  // 1 done, 0 not yet, -1 failed (message set)
+        if (d > 0) return FQ_OK;
+        if (d < 0) return fq_comm_abort_reason(c, fq_last_error());
+        ncclResult_t ae = ncclSuccess;
+        const ncclResult_t qr = ncclCommGetAsyncError(c->nccl, &ae);
+        if (qr != ncclSuccess || (ae != ncclSuccess && ae != ncclInProgress))
+            return fq_comm_abort_reason(c, std::string("RCCL error: ") + what + ": " +
+                                               ncclGetErrorString(qr != ncclSuccess ? qr : ae));
+        if (now_ns() - t0 > limit)
+            return fq_comm_abort_reason(c, std::string(what) + " did not complete within " + std::to_string(c->timeout_ms) +
+                                               " ms: a peer rank failed or never reached it");
+        if (spin < 4096) {
+            __builtin_ia32_pause();
+        } else {
+            std::this_thread::sleep_for(std::chrono::microseconds(spin < 65536 ? 5 : 200));
+        }
+    }
+}
 
 // fq_engine_execute_partial into a growing buffer.
 fq_status run_partial(fq_engine *e, const char *sql, int32_t rank, int32_t world, std::vector<uint8_t> &out) {
@@ -78,6 +128,11 @@ fq_status exchange_round(std::vector<uint64_t> &buf, fq_allreduce_fn allreduce, 
 }  // namespace
 
 extern "C" {
+
+fq_status fq_exchange_fail(fq_status st, const char *msg) {
+    if (st == FQ_OK) return FQ_OK;
+    return fqc::fail(st, msg ? msg : "state exchange: all-reduce failed");
+}
 
 fq_status fq_exchange_states_sized(const void *local, size_t len, size_t cap, int32_t rank, int32_t world,
                                    fq_allreduce_fn allreduce, void *user, const void **rows, size_t *stride) {
@@ -177,14 +232,21 @@ fq_status fq_comm_unique_id(void *id_out) {
 }
 
 fq_status fq_comm_init(int32_t device, int32_t world, int32_t rank, const void *id, fq_comm **out) {
+    return fq_comm_init_timeout(device, world, rank, id, FQ_COMM_TIMEOUT_MS, out);
+}
+
+fq_status fq_comm_init_timeout(int32_t device, int32_t world, int32_t rank, const void *id, int64_t timeout_ms,
+                               fq_comm **out) {
     if (!id || !out) return fqc::fail(FQ_E_INVALID, "fq_comm_init: NULL argument");
     if (world < 1 || rank < 0 || rank >= world) return fqc::fail(FQ_E_INVALID, "bad rank/world");
+    if (timeout_ms <= 0) return fqc::fail(FQ_E_INVALID, "fq_comm_init: the timeout must be positive");
     *out = nullptr;
     FQ_HIP_TRY(hipSetDevice(device));
     auto *c = new fq_comm();
     c->device = device;
     c->rank = rank;
     c->world = world;
+    c->timeout_ms = timeout_ms;
     hipError_t he = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (he != hipSuccess) {
         delete c;
@@ -192,13 +254,37 @@ fq_status fq_comm_init(int32_t device, int32_t world, int32_t rank, const void *
     }
     ncclUniqueId uid;
     memcpy(&uid, id, sizeof(uid));
-    ncclResult_t r = ncclCommInitRank(&c->nccl, world, uid, rank);
-    if (r != ncclSuccess) {
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;  // every call returns at once; comm_wait bounds the wait
+    ncclResult_t r = ncclCommInitRankConfig(&c->nccl, world, uid, rank, &cfg);
+    fq_status st = FQ_OK;
+    if (r != ncclSuccess && r != ncclInProgress) {
+        st = nccl_fail(r, "ncclCommInitRankConfig");
+        if (c->nccl) (void)ncclCommAbort(c->nccl);
+        c->nccl = nullptr;
+    } else {
+        // every rank must arrive: a peer that never does fails this one at the deadline
+        st = comm_wait(c, "ncclCommInitRankConfig", [&] {
+            ncclResult_t ae = ncclInProgress;
+            (void)ncclCommGetAsyncError(c->nccl, &ae);
+            return ae == ncclSuccess ? 1 : 0;
+        });
+    }
+    if (st != FQ_OK) {
+        const std::string msg = fq_last_error();
+        if (c->nccl) (void)ncclCommAbort(c->nccl);
         (void)hipStreamDestroy(c->stream);
         delete c;
-        return nccl_fail(r, "ncclCommInitRank");
+        return fqc::fail(st, msg);
     }
     *out = c;
+    return FQ_OK;
+}
+
+fq_status fq_comm_set_timeout(fq_comm *c, int64_t timeout_ms) {
+    if (!c) return fqc::fail(FQ_E_INVALID, "fq_comm_set_timeout: NULL comm");
+    if (timeout_ms <= 0) return fqc::fail(FQ_E_INVALID, "fq_comm_set_timeout: the timeout must be positive");
+    c->timeout_ms = timeout_ms;
     return FQ_OK;
 }
 
@@ -212,7 +298,22 @@ fq_status fq_comm_info(const fq_comm *c, int32_t *rank, int32_t *world) {
 void fq_comm_destroy(fq_comm *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    if (c->nccl) (void)ncclCommDestroy(c->nccl);
+    if (c->nccl) {
+        // a non-blocking communicator finalizes asynchronously: wait (bounded),
+        // else abort -- a peer that is gone must not hold this rank's exit
+        ncclResult_t fr = ncclCommFinalize(c->nccl);
+        bool ok = fr == ncclSuccess || fr == ncclInProgress;
+        const int64_t t0 = now_ns();
+        while (ok) {
+            ncclResult_t ae = ncclInProgress;
+            if (ncclCommGetAsyncError(c->nccl, &ae) != ncclSuccess) ok = false;
+            else if (ae == ncclSuccess) break;
+            else if (ae != ncclInProgress || now_ns() - t0 > c->timeout_ms * 1000000) ok = false;
+            else std::this_thread::sleep_for(std::chrono::microseconds(50));
+        }
+        if (ok) (void)ncclCommDestroy(c->nccl);
+        else (void)ncclCommAbort(c->nccl);
+    }
     if (c->d_buf) (void)hipFree(c->d_buf);
     if (c->h_buf) (void)hipHostFree(c->h_buf);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -221,14 +322,23 @@ void fq_comm_destroy(fq_comm *c) {
 
 fq_status fq_state_allreduce(fq_comm *c, uint64_t *d_buf, int64_t n_words, void *stream) {
     if (!c || (!d_buf && n_words > 0) || n_words < 0) return fqc::fail(FQ_E_INVALID, "fq_state_allreduce: bad argument");
+    if (c->aborted) return fqc::fail(FQ_E_RCCL, c->abort_reason);
     if (n_words == 0) return FQ_OK;
-    FQ_NCCL_TRY(ncclAllReduce(d_buf, d_buf, (size_t)n_words, ncclUint64, ncclSum, c->nccl, (hipStream_t)stream));
-    return FQ_OK;
+    const ncclResult_t r = ncclAllReduce(d_buf, d_buf, (size_t)n_words, ncclUint64, ncclSum, c->nccl, (hipStream_t)stream);
+    if (r == ncclSuccess) return FQ_OK;
+    if (r != ncclInProgress) return fq_comm_abort_reason(c, std::string("RCCL error: ncclAllReduce: ") + ncclGetErrorString(r));
+    // non-blocking communicator: the enqueue itself completes asynchronously
+    return comm_wait(c, "ncclAllReduce (enqueue)", [&] {
+        ncclResult_t ae = ncclInProgress;
+        (void)ncclCommGetAsyncError(c->nccl, &ae);
+        return ae == ncclSuccess ? 1 : 0;
+    });
 }
 
 fq_status fq_comm_allreduce_u64(uint64_t *buf, int64_t n_words, void *comm) {
     auto *c = (fq_comm *)comm;
     if (!c || (!buf && n_words > 0) || n_words < 0) return fqc::fail(FQ_E_INVALID, "fq_comm_allreduce_u64: bad argument");
+    if (c->aborted) return fqc::fail(FQ_E_RCCL, c->abort_reason);
     if (n_words == 0) return FQ_OK;
     FQ_HIP_TRY(hipSetDevice(c->device));
     if (n_words > c->cap_words) {
@@ -247,7 +357,15 @@ fq_status fq_comm_allreduce_u64(uint64_t *buf, int64_t n_words, void *comm) {
     fq_status st = fq_state_allreduce(c, c->d_buf, n_words, c->stream);
     if (st != FQ_OK) return st;
     FQ_HIP_TRY(hipMemcpyAsync(c->h_buf, c->d_buf, bytes, hipMemcpyDeviceToHost, c->stream));
-    FQ_HIP_TRY(hipStreamSynchronize(c->stream));
+    // the collective waits for every peer: bounded by the deadline
+    st = comm_wait(c, "the state all-reduce", [&] {
+        const hipError_t q = hipStreamQuery(c->stream);
+        if (q == hipSuccess) return 1;
+        if (q == hipErrorNotReady) return 0;
+        (void)fqc::hip_fail(q, "hipStreamQuery(exchange)");
+        return -1;
+    });
+    if (st != FQ_OK) return st;
     memcpy(buf, c->h_buf, bytes);
     return FQ_OK;
 }
@@ -255,6 +373,23 @@ fq_status fq_comm_allreduce_u64(uint64_t *buf, int64_t n_words, void *comm) {
 fq_status fq_engine_execute_rccl(fq_engine *e, const char *sql, fq_comm *c, fq_result **out) {
     if (!c) return fqc::fail(FQ_E_INVALID, "fq_engine_execute_rccl: NULL comm");
     return fq_engine_execute_exchange(e, sql, c->rank, c->world, fq_comm_allreduce_u64, c, out);
+}
+
+fq_status fq_engine_execute_exchange_row(fq_engine *e, const char *sql, int32_t rank, int32_t world,
+                                         fq_allreduce_fn allreduce, void *user, fq_value *row, int32_t cap,
+                                         int32_t *ncols) {
+    if (!ncols || cap < 0 || (cap > 0 && !row))
+        return fqc::fail(FQ_E_INVALID, "fq_engine_execute_exchange_row: NULL argument");
+    fq_result *r = nullptr;
+    const fq_status s = fq_engine_execute_exchange(e, sql, rank, world, allreduce, user, &r);
+    if (s != FQ_OK) return s;
+    return fq_result_take_row(r, row, cap, ncols, "fq_engine_execute_exchange_row");
+}
+
+fq_status fq_engine_execute_rccl_row(fq_engine *e, const char *sql, fq_comm *c, fq_value *row, int32_t cap,
+                                     int32_t *ncols) {
+    if (!c) return fqc::fail(FQ_E_INVALID, "fq_engine_execute_rccl_row: NULL comm");
+    return fq_engine_execute_exchange_row(e, sql, c->rank, c->world, fq_comm_allreduce_u64, c, row, cap, ncols);
 }
 
 }  // extern "C"

@@ -589,7 +589,9 @@ fq_status filter_project_blocks_enqueue(const fq_col *col, int64_t block_rows, c
                                         void *ev_start, void *ev_end, void *stream) {
     static_assert(FQ_PROJECT_MIN_BLOCK_ROWS == kProjectBlockTile, "the ABI's minimum block is the kernel's tile");
     if (!h_result) return fqc::fail(FQ_E_INVALID, "fq_filter_project_blocks: NULL result words");
-    h_result[0] = h_result[1] = 0;
+    // a resident call's words are the caller's until the hand-off writes them
+    // (the engine keeps a sentinel there to poll for)
+    if (!d_result) h_result[0] = h_result[1] = 0;
     if (block_rows < FQ_PROJECT_MIN_BLOCK_ROWS)
         return fqc::fail(FQ_E_INVALID, "fq_filter_project_blocks: block_rows below FQ_PROJECT_MIN_BLOCK_ROWS");
     ProjLaunch P;

@@ -32,16 +32,27 @@ COMM_ID_BYTES = 128
 STATE_CAP = 4096  # FQ_EXCHANGE_CAP_BYTES
 
 COMM_SYMBOLS = [
-    "fq_exchange_states", "fq_exchange_states_sized", "fq_engine_execute_exchange", "fq_comm_unique_id", "fq_comm_init", "fq_comm_info",
+    "fq_exchange_fail", "fq_exchange_states", "fq_exchange_states_sized", "fq_engine_execute_exchange",
+    "fq_engine_execute_exchange_row",
+    "fq_comm_unique_id", "fq_comm_init", "fq_comm_init_timeout", "fq_comm_set_timeout", "fq_comm_info",
     "fq_comm_destroy", "fq_state_allreduce", "fq_comm_allreduce_u64", "fq_engine_execute_rccl",
+    "fq_engine_execute_rccl_row",
 ]
+COMM_TIMEOUT_MS = 60000  # FQ_COMM_TIMEOUT_MS
 _protos = {
+    "fq_exchange_fail": (C.c_int32, [C.c_int32, C.c_char_p]),
     "fq_exchange_states": (C.c_int32, [C.c_void_p, C.c_size_t, C.c_int32, C.c_int32, ALLREDUCE_FN, C.c_void_p,
                                        P(C.c_void_p), P(C.c_size_t)]),
     "fq_exchange_states_sized": (C.c_int32, [C.c_void_p, C.c_size_t, C.c_size_t, C.c_int32, C.c_int32, ALLREDUCE_FN,
                                              C.c_void_p, P(C.c_void_p), P(C.c_size_t)]),
     "fq_engine_execute_exchange": (C.c_int32, [C.c_void_p, C.c_char_p, C.c_int32, C.c_int32, ALLREDUCE_FN,
                                                C.c_void_p, P(C.c_void_p)]),
+    "fq_engine_execute_exchange_row": (C.c_int32, [C.c_void_p, C.c_char_p, C.c_int32, C.c_int32, ALLREDUCE_FN,
+                                                   C.c_void_p, P(abi.fq_value), C.c_int32, P(C.c_int32)]),
+    "fq_comm_init_timeout": (C.c_int32, [C.c_int32, C.c_int32, C.c_int32, C.c_void_p, C.c_int64, P(C.c_void_p)]),
+    "fq_comm_set_timeout": (C.c_int32, [C.c_void_p, C.c_int64]),
+    "fq_engine_execute_rccl_row": (C.c_int32, [C.c_void_p, C.c_char_p, C.c_void_p, P(abi.fq_value), C.c_int32,
+                                               P(C.c_int32)]),
     "fq_comm_unique_id": (C.c_int32, [C.c_void_p]),
     "fq_comm_init": (C.c_int32, [C.c_int32, C.c_int32, C.c_int32, C.c_void_p, P(C.c_void_p)]),
     "fq_comm_info": (C.c_int32, [C.c_void_p, P(C.c_int32), P(C.c_int32)]),
@@ -56,24 +67,38 @@ for _n, (_r, _a) in _protos.items():
     _f.argtypes = _a
 
 
-def torch_allreduce_fn(group=None):
+def torch_allreduce_fn(group=None, timeout_s=None):
     """An fq_allreduce_fn over a torch.distributed group (keep the returned
-    object alive while the library may call it)."""
+    object alive while the library may call it).  timeout_s: the deadline of
+    each all-reduce, as fq_comm's for RCCL -- a peer that never arrives makes
+    the exchange fail with FQ_E_RCCL and this rank named, instead of a wait
+    without end (the group's own timeout is the fallback)."""
+    import datetime
     on_gpu = dist.get_backend(group) == "nccl"
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
 
     def cb(ptr, n, _user):
+        import time
+        t0 = time.monotonic()
         try:
             words = np.ctypeslib.as_array(ptr, shape=(n,)).view(np.int64)
             t = torch.from_numpy(words)
+            d = t.cuda() if on_gpu else t  # gloo: in place on the library's words
+            work = dist.all_reduce(d, op=dist.ReduceOp.SUM, group=group, async_op=True)
+            if timeout_s is None:
+                work.wait()
+            elif not work.wait(timeout=datetime.timedelta(seconds=timeout_s)):
+                raise TimeoutError
             if on_gpu:
-                d = t.cuda()
-                dist.all_reduce(d, op=dist.ReduceOp.SUM, group=group)
                 t.copy_(d.cpu())
-            else:
-                dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)  # in place on the library's words
             return abi.FQ_OK
-        except Exception:  # the library reports a generic exchange failure
-            return abi.FQ_E_RCCL
+        except Exception as e:
+            timed_out = timeout_s is not None and (isinstance(e, TimeoutError) or
+                                                   time.monotonic() - t0 >= 0.9 * timeout_s)
+            why = ("did not complete within %g s: a peer rank failed or never reached it" % timeout_s if timed_out
+                   else "failed: %s" % (str(e).splitlines()[0][:200] if str(e) else type(e).__name__))
+            return lib.fq_exchange_fail(abi.FQ_E_RCCL,
+                                        ("rank %d of %d: the state all-reduce %s" % (rank, world, why)).encode())
 
     return ALLREDUCE_FN(cb)
 
@@ -82,7 +107,7 @@ class RcclComm:
     """The library's RCCL communicator over all ranks of the default
     torch.distributed group (which only carries the unique id)."""
 
-    def __init__(self, device, group=None):
+    def __init__(self, device, group=None, timeout_ms=COMM_TIMEOUT_MS):
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
         uid = C.create_string_buffer(COMM_ID_BYTES)
@@ -92,7 +117,7 @@ class RcclComm:
         dist.broadcast_object_list(box, src=0, group=group)
         uid = C.create_string_buffer(box[0], COMM_ID_BYTES)
         h = C.c_void_p()
-        check(lib.fq_comm_init(device, self.world, self.rank, uid, C.byref(h)))
+        check(lib.fq_comm_init_timeout(device, self.world, self.rank, uid, int(timeout_ms), C.byref(h)))
         self.h = h
 
     @classmethod
@@ -132,14 +157,15 @@ class RcclComm:
             pass
 
 
-def allgather_states(states, group=None, cap=None):
+def allgather_states(states, group=None, cap=None, timeout_s=None):
     """bytes of this rank -> [bytes of rank 0, ..., rank world-1] (zero padded
     to a common stride) through the native exchange over `group`; `cap`: the
     first round's payload bytes per rank (fq_exchange_states_sized; the same
-    on every rank), default FQ_EXCHANGE_CAP_BYTES."""
+    on every rank), default FQ_EXCHANGE_CAP_BYTES; timeout_s: each
+    all-reduce's deadline (torch_allreduce_fn)."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
-    fn = torch_allreduce_fn(group)
+    fn = torch_allreduce_fn(group, timeout_s)
     rows, stride = C.c_void_p(), C.c_size_t()
     if cap is None:
         check(lib.fq_exchange_states(states, len(states), rank, world, fn, None, C.byref(rows), C.byref(stride)))
@@ -162,3 +188,20 @@ def execute(engine, sql, comm=None, group=None):
         check(lib.fq_engine_execute_exchange(engine.h, sql.encode(), dist.get_rank(group),
                                              dist.get_world_size(group), fn, None, C.byref(out)))
     return Result(out)
+
+
+def execute_row(engine, sql, comm=None, group=None, row=None, timeout_s=None):
+    """execute() for a one-row statement in ONE library call
+    (fq_engine_execute_rccl_row / fq_engine_execute_exchange_row): the row's
+    values (None for a None value).  `row`: an (abi.fq_value * k) buffer to
+    reuse (timed loops); the values are then row[:ncols]."""
+    buf = row if row is not None else (abi.fq_value * 8)()
+    ncols = C.c_int32(0)
+    if comm is not None:
+        check(lib.fq_engine_execute_rccl_row(engine.h, sql.encode(), comm.h, buf, len(buf), C.byref(ncols)))
+    else:
+        fn = torch_allreduce_fn(group, timeout_s)
+        check(lib.fq_engine_execute_exchange_row(engine.h, sql.encode(), dist.get_rank(group),
+                                                 dist.get_world_size(group), fn, None, buf, len(buf),
+                                                 C.byref(ncols)))
+    return [v.bits if v.is_some else None for v in buf[:ncols.value]]

@@ -40,6 +40,11 @@ extern "C" {
  * Returns FQ_OK or an fq_status (message via fq_last_error()).             */
 typedef fq_status (*fq_allreduce_fn)(uint64_t *buf, int64_t n_words, void *user);
 
+/* For an fq_allreduce_fn that fails: sets this thread's fq_last_error() text
+ * (the exchange runs the callback on the calling thread) and returns st, so
+ * the caller of the exchange sees why, e.g. which rank timed out.          */
+fq_status fq_exchange_fail(fq_status st, const char *msg);
+
 /* Payload words per rank carried by the first all-reduce (4 KB: an ungrouped
  * query's states are 8 + 16 per value + 8 per function bytes).             */
 #define FQ_EXCHANGE_CAP_BYTES 4096
@@ -70,15 +75,38 @@ fq_status fq_exchange_states_sized(const void *local, size_t len, size_t cap, in
 fq_status fq_engine_execute_exchange(fq_engine *e, const char *sql, int32_t rank, int32_t world,
                                      fq_allreduce_fn allreduce, void *user, fq_result **out);
 
-/* ---- RCCL communicator (one process per GPU, ncclCommInitRank) ---- */
+/* One-call forms for a statement whose result is one row (an ungrouped
+ * aggregate; fq_engine_execute_row's contract): the exchange, then the row's
+ * first min(cap, columns) values into row[], *ncols = its columns, the result
+ * freed.  Collective like fq_engine_execute_exchange.                      */
+fq_status fq_engine_execute_exchange_row(fq_engine *e, const char *sql, int32_t rank, int32_t world,
+                                         fq_allreduce_fn allreduce, void *user, fq_value *row, int32_t cap,
+                                         int32_t *ncols);
+
+/* ---- RCCL communicator (one process per GPU, non-blocking) ---- */
 typedef struct fq_comm fq_comm;
 #define FQ_COMM_ID_BYTES 128 /* NCCL_UNIQUE_ID_BYTES */
+/* Every RCCL step of a communicator -- its init, each all-reduce -- is
+ * bounded: the communicator is non-blocking (ncclCommInitRankConfig,
+ * blocking = 0) and the library polls ncclCommGetAsyncError against this
+ * deadline.  A peer that crashed or never reaches the collective fails the
+ * call with FQ_E_RCCL ("rank r of G: <step> did not complete within T ms: a
+ * peer rank failed or never reached it") after ncclCommAbort, instead of a
+ * wait without end; every later call on the communicator fails the same way
+ * (the reference's merge gets a failed task's Err, processor_merge.rs:50-54). */
+#define FQ_COMM_TIMEOUT_MS 60000
 
 /* rank 0 creates the id and ships it to the other ranks (any host channel) */
 fq_status fq_comm_unique_id(void *id_out /* FQ_COMM_ID_BYTES */);
-/* collective over all `world` ranks; `device` is this rank's HIP ordinal  */
+/* collective over all `world` ranks; `device` is this rank's HIP ordinal;
+ * every rank must arrive within FQ_COMM_TIMEOUT_MS (or timeout_ms)        */
 fq_status fq_comm_init(int32_t device, int32_t world, int32_t rank, const void *id, fq_comm **out);
+fq_status fq_comm_init_timeout(int32_t device, int32_t world, int32_t rank, const void *id, int64_t timeout_ms,
+                               fq_comm **out);
+/* the deadline of the communicator's later steps (> 0 ms) */
+fq_status fq_comm_set_timeout(fq_comm *c, int64_t timeout_ms);
 fq_status fq_comm_info(const fq_comm *c, int32_t *rank, int32_t *world);
+/* finalizes (bounded by the deadline, else aborts) and frees */
 void fq_comm_destroy(fq_comm *c);
 
 /* SURVEY 8b `fq_state_allreduce`: in-place wrapping u64 SUM all-reduce of a
@@ -88,11 +116,15 @@ fq_status fq_state_allreduce(fq_comm *c, uint64_t *d_buf, int64_t n_words, void 
 
 /* An fq_allreduce_fn over `comm` (pass the fq_comm* as `user`): stages the
  * host words through pinned + device buffers the comm owns, one
- * ncclAllReduce on the comm's stream, and waits for it.                    */
+ * ncclAllReduce on the comm's stream, and waits for it (bounded by the
+ * communicator's deadline).                                                */
 fq_status fq_comm_allreduce_u64(uint64_t *buf, int64_t n_words, void *comm);
 
 /* fq_engine_execute_exchange over RCCL: rank/world from the comm. */
 fq_status fq_engine_execute_rccl(fq_engine *e, const char *sql, fq_comm *c, fq_result **out);
+/* the same in one call for a one-row statement (fq_engine_execute_exchange_row) */
+fq_status fq_engine_execute_rccl_row(fq_engine *e, const char *sql, fq_comm *c, fq_value *row, int32_t cap,
+                                     int32_t *ncols);
 
 #ifdef __cplusplus
 }

@@ -372,3 +372,63 @@ def test_exchange_carries_error_records_past_the_sized_first_round(sql, rounds):
         assert st["exchanges"] == 1 and st["exchange_rounds"] == rounds
         round1 = world * (8 + (cap + 7) // 8 * 8)
         assert st["exchange_bytes"] == round1 + (world * 104 if rounds == 2 else 0)
+
+
+def dead_peer_worker(rank, world, port, mode, deadline_s, out_q):
+    """rank 0 exchanges; rank 1 never reaches the exchange ("absent": it
+    idles past the deadline) or dies before it ("dead")."""
+    import time
+    for p in (os.path.join(ROOT, "fuse-query_amd"), os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")):
+        sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+
+    from fq_amd import FQError
+    from fq_amd import dist as fqd
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.barrier()
+    if rank == 1:
+        if mode == "absent":
+            time.sleep(deadline_s * 4)
+        os._exit(0)
+    t0 = time.monotonic()
+    try:
+        fqd.allgather_states(b"FQS1" + bytes(60), cap=64, timeout_s=deadline_s)
+        out_q.put(("returned", time.monotonic() - t0, ""))
+        code = 0
+    except FQError as e:
+        out_q.put(("failed", time.monotonic() - t0, "%d %s" % (e.status, e)))
+        code = 3  # what a bench rank does: exit non-zero, the launcher tears the job down
+    out_q.close()
+    out_q.join_thread()
+    os._exit(code)  # no group teardown with a peer gone
+
+
+@pytest.mark.parametrize("mode", ["absent", "dead"])
+def test_exchange_with_a_peer_that_never_arrives_fails_within_the_deadline(mode):
+    """The exchange protocol's deadline: rank 0 runs the
+    native fq_exchange_states protocol through the fq_allreduce_fn callback
+    with a 3 s deadline while rank 1 never reaches the collective, or is gone.
+    Rank 0 must not wait without end: the call fails with FQ_E_RCCL naming the
+    rank within the deadline (+ slack), and the process exits non-zero.  The
+    RCCL transport bounds the same wait natively (fq_comm.cpp comm_wait:
+    ncclCommGetAsyncError polled against FQ_COMM_TIMEOUT_MS, then
+    ncclCommAbort)."""
+    from fq_amd import abi
+    deadline = 3.0
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=dead_peer_worker, args=(r, 2, port, mode, deadline, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    what, elapsed, msg = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+    assert what == "failed", (what, msg)
+    assert msg.startswith("%d rank 0 of 2: the state all-reduce" % abi.FQ_E_RCCL), msg
+    assert elapsed < deadline + 10, elapsed
+    if mode == "absent":
+        assert "did not complete within 3 s" in msg and elapsed >= deadline * 0.9, (msg, elapsed)
+    assert procs[0].exitcode == 3
