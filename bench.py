@@ -883,6 +883,9 @@ def main():
                     help="device queues the pipes share (FQ_OPT_STREAMS); 1 = the scans run back to back")
     ap.add_argument("--group-chunk-rows", type=int, default=None,
                     help="rows per radix-partitioned GROUP BY launch (FQ_OPT_GROUP_CHUNK_ROWS; tuning)")
+    ap.add_argument("--comm-timeout-ms", type=int, default=60000,
+                    help="deadline of every cross-GPU exchange step (FQ_COMM_TIMEOUT_MS): a rank that dies or never "
+                         "arrives fails the others with FQ_E_RCCL instead of a wait without end")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="nccl = RCCL over xGMI (default); gloo rehearses N ranks on fewer GPUs")
     ap.add_argument("--tune", action="append", default=[], metavar="KNOB=VALUE",
@@ -962,7 +965,7 @@ def main():
     if world > 1 and args.dist_backend == "nccl":
         ok = 1
         try:
-            comm = stdout_to_stderr(fqd.RcclComm, local)
+            comm = stdout_to_stderr(fqd.RcclComm, local, None, args.comm_timeout_ms)
         except Exception as e:  # reported; the same protocol then runs over torch's RCCL group
             log(rank, "native RCCL communicator unavailable on rank %d: %r" % (rank, e))
             ok = 0
