@@ -537,6 +537,90 @@ int32_t fqo_numbers_partial(uint64_t total, int32_t src, uint64_t seed, int32_t 
     return rc;
 }
 
+/* The same work cut finer than the reference can (BASELINE.md 2's all-cores
+ * leg): generate_parts always makes 8 partitions (numbers_table.rs:29-55), so
+ * the reference never runs more than 8 tasks.  Here every partition's block
+ * list is cut into `slices` runs of whole blocks, each its own task with its
+ * own partial states (out_states: [8 * slices][n_aggs], partition-major), run
+ * in waves of n_threads; AggregateFinal's merge of the rows gives the
+ * reference's result (sums add, min/max and counts commute). */
+typedef struct {
+    block_fn fn;
+    void *ctx;
+    uint64_t idx, lo, hi;
+} window_t;
+
+static int window_fn(void *c, uint64_t b, uint64_t e) {
+    window_t *w = (window_t *)c;
+    int rc = 0;
+    if (w->idx >= w->lo && w->idx < w->hi) rc = w->fn(w->ctx, b, e);
+    w->idx++;
+    return rc;
+}
+
+typedef struct {
+    task_t task;
+    uint64_t total;
+    int32_t part, slice, slices;
+} slice_job_t;
+
+static int count_blocks_fn(void *ctx, uint64_t b, uint64_t e) {
+    (void)b;
+    (void)e;
+    ++*(uint64_t *)ctx;
+    return 0;
+}
+
+static void *slice_thread(void *arg) {
+    slice_job_t *j = (slice_job_t *)arg;
+    uint64_t b, e, nb = 0;
+    fqo_partition_range(j->total, j->part, &b, &e);
+    numbers_blocks(b, e, count_blocks_fn, &nb);
+    window_t w = {numbers_block_fn, &j->task, 0, nb * (uint64_t)j->slice / (uint64_t)j->slices,
+                  nb * (uint64_t)(j->slice + 1) / (uint64_t)j->slices};
+    numbers_blocks(b, e, window_fn, &w);
+    return NULL;
+}
+
+int32_t fqo_numbers_partial_split(uint64_t total, const fq_pred *pred, int32_t n_aggs, const int32_t *agg_ops,
+                                  const fq_expr *agg_args, int32_t n_threads, int32_t slices,
+                                  fqo_state *out_states, char *errbuf, int32_t errlen) {
+    const int32_t np = fqo_num_partitions(total);
+    if (np <= 0 || slices < 1) return 0;
+    const int32_t nj = np * slices;
+    slice_job_t *jobs = (slice_job_t *)calloc((size_t)nj, sizeof(slice_job_t));
+    for (int32_t i = 0; i < nj; ++i) {
+        jobs[i].total = total;
+        jobs[i].part = i / slices;
+        jobs[i].slice = i % slices;
+        jobs[i].slices = slices;
+        jobs[i].task.src = FQO_SRC_NUMBERS;
+        jobs[i].task.col_dtype = FQ_DT_UINT64;
+        jobs[i].task.pred = pred;
+        jobs[i].task.n_aggs = n_aggs;
+        jobs[i].task.agg_ops = agg_ops;
+        jobs[i].task.agg_args = agg_args;
+        jobs[i].task.states = out_states + (size_t)i * n_aggs;
+        init_states(jobs[i].task.states, n_aggs);
+    }
+    if (n_threads <= 0 || n_threads > nj) n_threads = nj;
+    pthread_t *th = (pthread_t *)calloc((size_t)n_threads, sizeof(pthread_t));
+    for (int32_t w = 0; w < nj; w += n_threads) {
+        const int32_t k = (nj - w) < n_threads ? (nj - w) : n_threads;
+        for (int32_t i = 0; i < k; ++i) pthread_create(&th[i], NULL, slice_thread, &jobs[w + i]);
+        for (int32_t i = 0; i < k; ++i) pthread_join(th[i], NULL);
+    }
+    free(th);
+    int32_t rc = 0;
+    for (int32_t i = 0; i < nj && !rc; ++i)
+        if (jobs[i].task.err.status) {
+            rc = jobs[i].task.err.status;
+            if (errbuf && errlen > 0) snprintf(errbuf, (size_t)errlen, "%s", jobs[i].task.err.msg);
+        }
+    free(jobs);
+    return rc;
+}
+
 int32_t fqo_column_partial(const void *col, int32_t col_dtype, int64_t len, int64_t block_rows,
                            const fq_pred *pred, int32_t n_aggs, const int32_t *agg_ops,
                            const fq_expr *agg_args, fqo_state *out_states, char *errbuf,

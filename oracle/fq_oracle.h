@@ -73,6 +73,14 @@ int32_t fqo_numbers_partial(uint64_t total, int32_t src, uint64_t seed, int32_t 
                             const fq_expr *agg_args, int32_t n_threads, fqo_state *out_states,
                             int32_t *part_status, char *errbuf, int32_t errlen);
 
+/* The same work in 8 * slices tasks (each partition's blocks cut into
+ * `slices` runs of whole blocks), n_threads at a time: more parallelism than
+ * the reference's 8 fixed partitions allow (the all-cores baseline leg).
+ * out_states: [8 * slices][n_aggs]; merging all rows gives the same result. */
+int32_t fqo_numbers_partial_split(uint64_t total, const fq_pred *pred, int32_t n_aggs, const int32_t *agg_ops,
+                                  const fq_expr *agg_args, int32_t n_threads, int32_t slices,
+                                  fqo_state *out_states, char *errbuf, int32_t errlen);
+
 /* Same over an explicit host column cut into blocks of block_rows rows. */
 int32_t fqo_column_partial(const void *col, int32_t col_dtype, int64_t len, int64_t block_rows,
                            const fq_pred *pred, int32_t n_aggs, const int32_t *agg_ops,

@@ -54,6 +54,10 @@ def load(native=False):
     lib.fqo_numbers_partial.argtypes = [
         C.c_uint64, C.c_int32, C.c_uint64, C.c_int32, C.c_int32, P(abi.fq_pred), C.c_int32,
         P(C.c_int32), P(abi.fq_expr), C.c_int32, P(fqo_state), P(C.c_int32), C.c_char_p, C.c_int32]
+    lib.fqo_numbers_partial_split.restype = C.c_int32
+    lib.fqo_numbers_partial_split.argtypes = [
+        C.c_uint64, P(abi.fq_pred), C.c_int32, P(C.c_int32), P(abi.fq_expr), C.c_int32, C.c_int32, P(fqo_state),
+        C.c_char_p, C.c_int32]
     lib.fqo_column_partial.restype = C.c_int32
     lib.fqo_column_partial.argtypes = [
         C.c_void_p, C.c_int32, C.c_int64, C.c_int64, P(abi.fq_pred), C.c_int32, P(C.c_int32),
@@ -120,6 +124,21 @@ def numbers_partial(total, aggs, pred=None, src=SRC_NUMBERS, seed=0, p0=0, p1=No
                           ops, args, threads, states, st, err, 512)
     rows = [[states[i * n + a] for a in range(n)] for i in range(np_)]
     return rows, list(st), err.value.decode()
+
+
+def numbers_partial_split(total, aggs, pred=None, threads=0, slices=1, native=False):
+    """numbers_partial with every partition's blocks cut into `slices` tasks
+    (fqo_numbers_partial_split): (states[task][agg], err)."""
+    L = lib(native)
+    n = len(aggs)
+    ops = (C.c_int32 * n)(*[a for a, _ in aggs])
+    args = (abi.fq_expr * n)(*[(e if e is not None else _identity(abi.DT_UINT64)) for _, e in aggs])
+    nt = L.fqo_num_partitions(total) * slices
+    states = (fqo_state * (nt * n))()
+    err = C.create_string_buffer(512)
+    rc = L.fqo_numbers_partial_split(total, C.byref(pred) if pred is not None else None, n, ops, args, threads,
+                                     slices, states, err, 512)
+    return [[states[i * n + a] for a in range(n)] for i in range(nt)], rc, err.value.decode()
 
 
 def column_partial(arr, dtype, block_rows, aggs, pred=None):
