@@ -742,7 +742,7 @@ static constexpr uint64_t kProjectPending = ~0ull;  // project_res[0] until the 
 
 static bool project_blocks(const DataBlock &b, const Column &c, const fq_pred *pred, std::vector<fq_expr> &exprs,
                            std::vector<Column> &outs, std::vector<void *> &ptrs, const SchemaRef &schema, ExecCtx &ctx,
-                           DataBlock &out) {
+                           DataBlock &out, LaunchSpan *span) {
     const int64_t n = c.len, B = b.sub_block_rows;
     const int64_t nb = n <= B ? 1 : (n + B - 1) / B;
     auto layout = std::make_shared<BlockLayout>();
@@ -756,7 +756,10 @@ static bool project_blocks(const DataBlock &b, const Column &c, const fq_pred *p
     uint64_t *res = ctx.res->project_res;
     std::shared_ptr<DeviceBuffer> ws;
     if (mode == 0) ws = DeviceBuffer::alloc(fq_filter_project_blocks_workspace_bytes(), ctx.stream());
-    const bool prof = ctx.rt->profile.load();
+    // FQ_OPT_PROFILE 1: an event pair around each kernel; 2 with a span: none
+    // here (LaunchSpan times the query's launches together)
+    const int profile = ctx.rt->profile.load();
+    const bool prof = profile == 1 || (profile == 2 && !span);
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (prof) {
         e0 = ctx.res->take_event();
@@ -774,6 +777,7 @@ static bool project_blocks(const DataBlock &b, const Column &c, const fq_pred *p
     hipEvent_t done = mode == 2 ? nullptr : ctx.res->take_sync_event();
     {
         std::lock_guard<std::mutex> lk(*ctx.res->launch_mu);
+        if (span) span->before_launch(ctx);
         if (mode != 0) {
             res[0] = kProjectPending;
             res[1] = 0;
@@ -793,15 +797,21 @@ static bool project_blocks(const DataBlock &b, const Column &c, const fq_pred *p
             // the hand-off kernel runs after the projection kernel on this
             // queue and writes the count last: once it is there, so are the
             // flags and the projected columns
+            // flagging the words is all the wait does: no HIP call per check
+            // (eight pipes polling the runtime slowed the launches), one
+            // hipStreamQuery per ~1 ms for a queue that failed and will never
+            // write them
             volatile uint64_t *w = res;
             for (int spin = 0; w[0] == kProjectPending; ++spin) {
-                if (spin < 2000) {
+                if (spin < 256) {
                     __builtin_ia32_pause();
-                } else {
-                    he = hipStreamQuery(ctx.stream());  // a failed queue never writes the words
+                    continue;
+                }
+                std::this_thread::sleep_for(std::chrono::microseconds(20));
+                if (spin % 64 == 0) {
+                    he = hipStreamQuery(ctx.stream());
                     if (he != hipSuccess && he != hipErrorNotReady) break;
                     he = hipSuccess;
-                    std::this_thread::sleep_for(std::chrono::microseconds(2));
                 }
             }
             std::atomic_thread_fence(std::memory_order_acquire);
@@ -840,7 +850,7 @@ static bool project_blocks(const DataBlock &b, const Column &c, const fq_pred *p
 // fused too when it is over that column, else its bitmap is evaluated
 // first).  false: not fusable, the caller materialises + evaluates.
 bool project_fused(const DataBlock &b, const std::vector<FunctionRef> &funcs, const SchemaRef &schema, ExecCtx &ctx,
-                   DataBlock &out, bool block_stream) {
+                   DataBlock &out, bool block_stream, LaunchSpan *span) {
     if (funcs.empty() || funcs.size() > FQ_MAX_PROJECT || !b.schema || b.columns.empty()) return false;
     std::vector<FusedChain> chains(funcs.size());
     bool computes = false;
@@ -880,7 +890,7 @@ bool project_fused(const DataBlock &b, const std::vector<FunctionRef> &funcs, co
         exprs.push_back(fc.expr);
     }
     if (block_stream && pred && b.sub_block_rows >= FQ_PROJECT_MIN_BLOCK_ROWS)
-        return project_blocks(b, c, pred, exprs, outs, ptrs, schema, ctx, out);
+        return project_blocks(b, c, pred, exprs, outs, ptrs, schema, ctx, out, span);
     const size_t wsb = fq_filter_project_workspace_bytes(n);
     auto ws = DeviceBuffer::alloc(wsb, ctx.stream());
     fq_col ic = c.abi();
@@ -897,6 +907,52 @@ bool project_fused(const DataBlock &b, const std::vector<FunctionRef> &funcs, co
         out.columns.push_back(o);
     }
     return true;
+}
+
+// ---------------------------------------------------------------------------
+// LaunchSpan
+// ---------------------------------------------------------------------------
+LaunchSpan::~LaunchSpan() {
+    for (auto &s : queues_) rt_->give_event(s.start);
+}
+
+void LaunchSpan::before_launch(ExecCtx &ctx) {
+    if (rt_->profile.load(std::memory_order_relaxed) != 2) return;
+    std::lock_guard<std::mutex> lk(mu_);
+    for (const QueueSpan &s : queues_)
+        if (s.q == ctx.stream()) return;
+    QueueSpan s;
+    s.q = ctx.stream();
+    s.launch_mu = ctx.res->launch_mu;
+    s.start = rt_->take_event();
+    check_hip(hipEventRecord(s.start, s.q), "hipEventRecord");
+    queues_.push_back(s);
+}
+
+void LaunchSpan::arrive() noexcept {
+    std::vector<QueueSpan> qs;
+    {
+        std::lock_guard<std::mutex> lk(mu_);
+        if (--left_ != 0) return;
+        qs = queues_;
+    }
+    // the last pipe: every launch of the query has completed (each pipe waited
+    // for its own); one end event per queue closes its span
+    for (QueueSpan &s : qs) {
+        hipEvent_t end = nullptr;
+        try {
+            end = rt_->take_event();
+            {
+                std::lock_guard<std::mutex> ql(*s.launch_mu);
+                if (hipEventRecord(end, s.q) != hipSuccess) continue;
+            }
+            float ms = 0;
+            if (hipEventSynchronize(end) == hipSuccess && hipEventElapsedTime(&ms, s.start, end) == hipSuccess)
+                rt_->stats.project_ns += (uint64_t)((double)ms * 1e6);
+        } catch (...) {  // timing only: never fail the query for it
+        }
+        if (end) rt_->give_event(end);
+    }
 }
 
 // ---------------------------------------------------------------------------

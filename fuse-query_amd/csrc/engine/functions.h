@@ -335,6 +335,38 @@ class ScanGroup {
 };
 using ScanGroupRef = std::shared_ptr<ScanGroup>;
 
+// The block-stream projections of ONE query (a row pipeline's
+// ProjectionTransform pipes, fq_filter_project_blocks) timed as one span per
+// queue, like ScanGroup's scans: FQ_OPT_PROFILE 2 records a start event right
+// before the queue's first launch of the query and, when the last pipe's
+// stream has ended, an end event -- project_ns gets the span (the launches
+// and every gap between them); no event sits between two launches.  (The end
+// is recorded once that pipe has seen its last launch complete, so the span
+// also holds that pipe's wake-up: it over-states, never under-states.)
+class LaunchSpan {
+   public:
+    LaunchSpan(Runtime *rt, int pipes) : rt_(rt), left_(pipes) {}
+    ~LaunchSpan();
+    LaunchSpan(const LaunchSpan &) = delete;
+    LaunchSpan &operator=(const LaunchSpan &) = delete;
+    // a launch on ctx's queue follows (under the queue's launch lock)
+    void before_launch(ExecCtx &ctx);
+    // a pipe's stream has ended (or the pipe is gone); never throws
+    void arrive() noexcept;
+
+   private:
+    struct QueueSpan {
+        hipStream_t q = nullptr;
+        std::mutex *launch_mu = nullptr;
+        hipEvent_t start = nullptr;
+    };
+    Runtime *rt_;
+    std::mutex mu_;
+    int left_;
+    std::vector<QueueSpan> queues_;
+};
+using LaunchSpanRef = std::shared_ptr<LaunchSpan>;
+
 // One pipe's place in a ScanGroup: arrives exactly once -- from
 // AggFusion::finish, or (a pipe that fails) when it goes out of scope, so the
 // other pipes never wait for a pipe that is gone.  A pipe that fails before
@@ -437,6 +469,7 @@ Column eval_predicate(Function &pred, const DataBlock &b, ExecCtx &ctx);
 // one fq_filter_project call; false when the shape is not fusable
 bool project_fused(const DataBlock &b, const std::vector<FunctionRef> &funcs, const SchemaRef &schema, ExecCtx &ctx,
                    DataBlock &out,
-                   bool block_stream = true);
+                   bool block_stream = true,
+                   LaunchSpan *span = nullptr);
 
 }  // namespace fq

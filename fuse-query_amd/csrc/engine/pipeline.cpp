@@ -426,22 +426,62 @@ StreamRef FilterTransform::execute() {
     });
 }
 
+namespace {
+// a pipe's stream that reports its end (or its destruction, a pipe that
+// failed or was stopped) to the query's LaunchSpan, once
+class SpanStream : public BlockStream {
+   public:
+    SpanStream(StreamRef in, LaunchSpanRef span) : in_(std::move(in)), span_(std::move(span)) {}
+    ~SpanStream() override { end(); }
+    bool next(DataBlock &out) override {
+        if (in_->next(out)) return true;
+        end();
+        return false;
+    }
+
+   private:
+    void end() {
+        if (span_) span_->arrive();
+        span_.reset();
+    }
+    StreamRef in_;
+    LaunchSpanRef span_;
+};
+}  // namespace
+
+void ProjectionTransform::abandon() {
+    if (!entered_.exchange(true) && span_) span_->arrive();
+}
+
 StreamRef ProjectionTransform::execute() {
     SchemaRef schema = schema_;
     std::vector<FunctionRef> funcs;
     for (auto &f : funcs_) funcs.push_back(f->clone());
     const bool blocks = block_stream_;
-    return std::make_unique<MapStream>(input_->execute(), [schema, funcs, blocks](DataBlock b) {
+    LaunchSpanRef span = entered_.exchange(true) ? nullptr : span_;
+    // the span's arrival is owned by the SpanStream from here on
+    struct Arrive {
+        LaunchSpanRef s;
+        ~Arrive() {
+            if (s) s->arrive();
+        }
+    } arrive_on_throw{span};
+    StreamRef in = input_->execute();
+    LaunchSpan *sp = span.get();
+    StreamRef mapped = std::make_unique<MapStream>(std::move(in), [schema, funcs, blocks, sp](DataBlock b) {
         ExecCtx &ctx = ExecCtx::current();
         DataBlock out;
         if (b.layout) b = materialize(b, ctx);  // a block stream in: one array first
-        if (project_fused(b, funcs, schema, ctx, out, blocks)) return out;  // filter + expressions in one pass
+        if (project_fused(b, funcs, schema, ctx, out, blocks, sp)) return out;  // filter + expressions in one pass
         b = materialize(b, ctx);
         const int64_t rows = b.num_rows();
         out.schema = schema;
         for (auto &f : funcs) out.columns.push_back(f->eval(b, ctx).to_array(rows, ctx));
         return out;
     });
+    arrive_on_throw.s.reset();
+    if (!span) return mapped;
+    return std::make_unique<SpanStream>(std::move(mapped), std::move(span));
 }
 
 namespace {

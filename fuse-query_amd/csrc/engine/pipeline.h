@@ -218,18 +218,23 @@ class ProjectionTransform : public IProcessor {  // transform_projection.rs:16-7
     // per-block geometry (fq_filter_project_blocks); false -- a LIMIT above
     // compacts every block anyway and wants latency -- one contiguous array
     // per block (fq_filter_project)
-    ProjectionTransform(SchemaRef schema, std::vector<FunctionRef> funcs, bool block_stream = true)
+    // span: the query's block-stream projections timed together (LaunchSpan)
+    ProjectionTransform(SchemaRef schema, std::vector<FunctionRef> funcs, bool block_stream = true,
+                        LaunchSpanRef span = nullptr)
         : schema_(std::move(schema)), funcs_(std::move(funcs)), input_(std::make_shared<EmptyProcessor>()),
-          block_stream_(block_stream) {}
+          block_stream_(block_stream), span_(std::move(span)) {}
     std::string name() const override { return "ProjectionTransform"; }
     void connect_to(ProcessorRef input) override { input_ = std::move(input); }
     StreamRef execute() override;
+    void abandon() override;  // a pipe that never ran still counts in the span
 
    private:
     SchemaRef schema_;
     std::vector<FunctionRef> funcs_;
     ProcessorRef input_;
     bool block_stream_;
+    LaunchSpanRef span_;
+    std::atomic<bool> entered_{false};
 };
 
 class AggregatePartialTransform : public IProcessor {  // transform_aggregate_partial.rs:18-79

@@ -629,12 +629,16 @@ Pipeline build_pipeline(const QueryPlan &plan, const QueryContextRef &ctx, bool 
                 break;
             }
             case PlanNode::kProjection: {
-                p.add_simple_transform([&]() {
+                // the block-stream projections of the query's pipes are timed as one span (LaunchSpan)
+                const bool blocks = mode != ReadMode::kMorsels;
+                auto span = blocks ? std::make_shared<LaunchSpan>(ctx->rt, (int)std::max<size_t>(1, p.pipe_num()))
+                                   : nullptr;
+                p.add_simple_transform([&, span, blocks]() {
                     for (const auto &e : n.exprs)  // transform_projection.rs:24-31
                         if (e.is_aggregate()) throw_internal("Unsupported aggregator function: " + e.debug());
                     std::vector<FunctionRef> fs;
                     for (const auto &e : n.exprs) fs.push_back(e.to_function(ctx->factory));
-                    return std::make_shared<ProjectionTransform>(n.schema, fs, mode != ReadMode::kMorsels);
+                    return std::make_shared<ProjectionTransform>(n.schema, fs, blocks, span);
                 });
                 break;
             }

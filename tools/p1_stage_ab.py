@@ -47,8 +47,8 @@ def main():
     sql = bench.PROJECT_SQL.format(N=N)
     mine = bench.shard(bench.generate_parts(N), 0, 1)
     expect = bench._p1_expect(mine)
-    # P1_PROFILE=0: no timing events at all (kernel_ms then comes from rocprof)
-    eng = Engine(device=0, profile=os.environ.get("P1_PROFILE", "1") != "0")
+    # P1_PROFILE: 2 (default) one span per query, 1 an event pair per launch, 0 none (kernel_ms then from rocprof)
+    eng = Engine(device=0, profile=int(os.environ.get("P1_PROFILE", "2")))
     eng.materialize_numbers(N, 0, 1)
     torch.cuda.synchronize()
 
