@@ -731,15 +731,14 @@ DataBlock materialize(const DataBlock &b, ExecCtx &ctx) {
 // queue's other pipes (launch_mu) and this pipe waits for its own launch, not
 // for the queue.
 //
-// What sits on the queue around each projection kernel
-// (FQ_TUNE_ENGINE_PROJECT_LAUNCH): 0 -- a workspace memset before it, a copy of
-// the two result words after it and a completion event; 1 -- the worker's
-// resident workspace and a one-thread hand-off kernel after it (no memset, no
-// copy), then the completion event; 2 -- as 1 with no event: the pipe polls the
-// hand-off's words in mapped host memory (a sentinel until the kernel wrote
-// them).  With FQ_OPT_PROFILE an event pair brackets the kernel.
-static constexpr uint64_t kProjectPending = ~0ull;  // project_res[0] until the hand-off wrote it
-
+// Around each projection kernel the queue carries only a one-thread hand-off
+// kernel: it moves {kept rows, flag words} into the worker's pinned, mapped
+// result words and re-zeroes the worker's resident workspace (no memset before,
+// no copy after), then the pipe's completion event.  In one process, 4 rounds x
+// 8 queries of p1 (profiles/r06_a_p1_queue_ab.json, r06_d_p1_queue_ab_span.json):
+// memset + copy 24.36 / 23.52 ms per query, this 23.94 / 23.33, the hand-off
+// alone with the pipe polling the words 24.03 / 23.52 -- the first pair with an
+// event pair around every launch, the second with one span per query.
 static bool project_blocks(const DataBlock &b, const Column &c, const fq_pred *pred, std::vector<fq_expr> &exprs,
                            std::vector<Column> &outs, std::vector<void *> &ptrs, const SchemaRef &schema, ExecCtx &ctx,
                            DataBlock &out, LaunchSpan *span) {
@@ -749,13 +748,13 @@ static bool project_blocks(const DataBlock &b, const Column &c, const fq_pred *p
     layout->block_rows = B;
     layout->n_blocks = n == 0 ? 0 : nb;
     layout->counts = DeviceBuffer::alloc((size_t)std::max<int64_t>(nb, 1) * 8, ctx.stream());
-    // (no predicate: the map kernel, whose words the host writes -- mode 0)
-    // (an empty block launches nothing -- no hand-off to wait for: mode 0)
-    const int mode = pred && pred->kind != FQ_PRED_NONE && n > 0 ? (int)fqc::knob(FQ_TUNE_ENGINE_PROJECT_LAUNCH) : 0;
+    // the map kernel (no predicate) has its words written by the host and no
+    // hand-off: a workspace of its own, zeroed before it, the flags copied after
+    const bool resident = pred && pred->kind != FQ_PRED_NONE;
     ctx.res->project_resident();
     uint64_t *res = ctx.res->project_res;
     std::shared_ptr<DeviceBuffer> ws;
-    if (mode == 0) ws = DeviceBuffer::alloc(fq_filter_project_blocks_workspace_bytes(), ctx.stream());
+    if (!resident) ws = DeviceBuffer::alloc(fq_filter_project_blocks_workspace_bytes(), ctx.stream());
     // FQ_OPT_PROFILE 1: an event pair around each kernel; 2 with a span: none
     // here (LaunchSpan times the query's launches together)
     const int profile = ctx.rt->profile.load();
@@ -774,57 +773,31 @@ static bool project_blocks(const DataBlock &b, const Column &c, const fq_pred *p
                                                       nullptr, res, nullptr, nullptr, 0, nullptr, nullptr, ctx.stream());
     if (st == FQ_E_UNSUPPORTED) return false;
     check_fq(st);
-    hipEvent_t done = mode == 2 ? nullptr : ctx.res->take_sync_event();
+    hipEvent_t done = ctx.res->take_sync_event();
     {
         std::lock_guard<std::mutex> lk(*ctx.res->launch_mu);
         if (span) span->before_launch(ctx);
-        if (mode != 0) {
-            res[0] = kProjectPending;
-            res[1] = 0;
-        }
+        // this worker's last hand-off has landed (the pipe waited for it); an
+        // empty block launches nothing, so its words must read 0 kept rows
+        res[0] = res[1] = 0;
         st = fqk::filter_project_blocks_enqueue(&ic, B, pred, exprs.data(), (int32_t)exprs.size(), ptrs.data(),
                                                 (int64_t *)layout->counts->ptr, res,
-                                                mode == 0 ? nullptr : ctx.res->project_dres,
-                                                mode == 0 ? ws->ptr : ctx.res->project_ws,
+                                                resident ? ctx.res->project_dres : nullptr,
+                                                resident ? ctx.res->project_ws : ws->ptr,
                                                 fq_filter_project_blocks_workspace_bytes(), e0, e1, ctx.stream());
-        if (st == FQ_OK && done) check_hip(hipEventRecord(done, ctx.stream()), "hipEventRecord");  // after the result words
+        if (st == FQ_OK) check_hip(hipEventRecord(done, ctx.stream()), "hipEventRecord");  // after the result words
     }
     if (st == FQ_OK) {
-        hipError_t he = hipSuccess;
-        if (done) {
-            he = hipEventSynchronize(done);
-        } else {
-            // the hand-off kernel runs after the projection kernel on this
-            // queue and writes the count last: once it is there, so are the
-            // flags and the projected columns
-            // flagging the words is all the wait does: no HIP call per check
-            // (eight pipes polling the runtime slowed the launches), one
-            // hipStreamQuery per ~1 ms for a queue that failed and will never
-            // write them
-            volatile uint64_t *w = res;
-            for (int spin = 0; w[0] == kProjectPending; ++spin) {
-                if (spin < 256) {
-                    __builtin_ia32_pause();
-                    continue;
-                }
-                std::this_thread::sleep_for(std::chrono::microseconds(20));
-                if (spin % 64 == 0) {
-                    he = hipStreamQuery(ctx.stream());
-                    if (he != hipSuccess && he != hipErrorNotReady) break;
-                    he = hipSuccess;
-                }
-            }
-            std::atomic_thread_fence(std::memory_order_acquire);
-        }
+        const hipError_t he = hipEventSynchronize(done);
         if (he == hipSuccess && prof) {
             float ms = 0;
             if (hipEventElapsedTime(&ms, e0, e1) == hipSuccess) ctx.rt->stats.project_ns += (uint64_t)((double)ms * 1e6);
         }
-        check_hip(he, done ? "hipEventSynchronize" : "hipStreamQuery");
+        check_hip(he, "hipEventSynchronize");
     }
     if (e0) ctx.res->give_event(e0);
     if (e1) ctx.res->give_event(e1);
-    if (done) ctx.res->give_sync_event(done);
+    ctx.res->give_sync_event(done);
     if (st == FQ_E_UNSUPPORTED) return false;  // the unfused path evaluates it (and raises what the reference does)
     check_fq(st);
     int64_t kept = 0;

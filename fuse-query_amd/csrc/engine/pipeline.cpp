@@ -451,6 +451,7 @@ class SpanStream : public BlockStream {
 
 void ProjectionTransform::abandon() {
     if (!entered_.exchange(true) && span_) span_->arrive();
+    input_->abandon();
 }
 
 StreamRef ProjectionTransform::execute() {
@@ -506,6 +507,7 @@ Column partial_states(const std::vector<FunctionRef> &funcs) {
 
 void AggregatePartialTransform::abandon() {
     if (!entered_.exchange(true) && group_) group_->arrive(false);
+    input_->abandon();
 }
 
 StreamRef AggregatePartialTransform::execute() {

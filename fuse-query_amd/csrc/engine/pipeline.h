@@ -156,7 +156,7 @@ class IProcessor {
     virtual std::string format(FormatterSettings &s) const;
     // the pipe this processor ends failed before (or without) running
     // execute(): release whatever other pipes wait on (MergeProcessor calls it
-    // from the failing pipe's task)
+    // from the failing pipe's task; transforms pass it to their input)
     virtual void abandon() {}
 };
 using ProcessorRef = std::shared_ptr<IProcessor>;
@@ -206,6 +206,7 @@ class FilterTransform : public IProcessor {  // transform_filter.rs:17-77
     std::string name() const override { return "FilterTransform"; }
     void connect_to(ProcessorRef input) override { input_ = std::move(input); }
     StreamRef execute() override;
+    void abandon() override { input_->abandon(); }
 
    private:
     FunctionRef func_;
@@ -342,6 +343,7 @@ class LimitTransform : public IProcessor {  // transform_limit.rs:12-43
     std::string name() const override { return "LimitTransform"; }
     void connect_to(ProcessorRef input) override { input_ = std::move(input); }
     StreamRef execute() override;
+    void abandon() override { input_->abandon(); }
 
    private:
     size_t limit_;

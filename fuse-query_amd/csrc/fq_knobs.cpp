@@ -37,7 +37,6 @@ constexpr KnobDef kDefs[FQ_TUNE_COUNT] = {
     {1, 0, 1, 1, false},            // GROUP_NARROW
     {2, 1, 4, 1, false},            // GPART_WG_PER_CU
     {2, 1, 4, 1, false},            // GBINS_WG_PER_CU
-    {0, 0, 2, 1, false},            // ENGINE_PROJECT_LAUNCH
 };
 
 std::atomic<int64_t> g_val[FQ_TUNE_COUNT] = {};

@@ -124,5 +124,5 @@ TUNE = {
     "SCAN_WG_PER_CU": 0, "EW_WG_PER_CU": 1, "BLOCK_U": 2, "SELECT_WG_PER_CU": 3, "SELECT_BLOCKS_WG_PER_CU": 4,
     "SELECT_BLOCKS_ROWS": 5, "SELECT_BLOCKS_STAGE": 6, "BLOCK_CACHE": 7, "POOL_SPIN_US": 8, "GROUP_THREADS": 9,
     "GROUP_LDS_KB": 10, "GROUP_WG_PER_CU": 11, "GROUP_CLUSTER": 12, "GROUP_CHUNKED": 13, "GROUP_RANGE_BINS": 14,
-    "GROUP_NARROW": 15, "GPART_WG_PER_CU": 16, "GBINS_WG_PER_CU": 17, "ENGINE_PROJECT_LAUNCH": 18,
+    "GROUP_NARROW": 15, "GPART_WG_PER_CU": 16, "GBINS_WG_PER_CU": 17,
 }

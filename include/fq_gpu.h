@@ -398,9 +398,7 @@ fq_status fq_jit_prepare(const fq_col *col, int64_t block_rows, const fq_pred *p
 #define FQ_TUNE_GROUP_NARROW 15       /* partitioned GROUP BY: honour FQ_GROUP_NARROW_ROWS, 1 (0/1)   */
 #define FQ_TUNE_GPART_WG_PER_CU 16    /* GROUP BY partition kernel: workgroups per CU, 2 (1..4)       */
 #define FQ_TUNE_GBINS_WG_PER_CU 17    /* GROUP BY bins pass, fitted table: workgroups per CU, 2 (1..4) */
-#define FQ_TUNE_ENGINE_PROJECT_LAUNCH 18 /* the engine's block projections: what sits on the queue around each
-                                            kernel (engine/functions.cpp project_blocks), 0 (0..2) */
-#define FQ_TUNE_COUNT 19
+#define FQ_TUNE_COUNT 18
 /* FQ_E_INVALID for an unknown knob or a value outside the knob's set */
 fq_status fq_tune_set(int32_t knob, int64_t value);
 /* the knob's current value; -1 for an unknown knob */

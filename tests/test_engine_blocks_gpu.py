@@ -259,21 +259,18 @@ def test_engine_destroyed_with_a_stream_open():
     assert st.h is None
 
 
-@pytest.mark.parametrize("mode", [0, 1, 2], ids=["memset_copy", "hand_off_kernel", "hand_off_polled"])
-def test_block_stream_under_each_queue_form(eng, mode):
-    """What the engine puts on the queue around each projection kernel
-    (FQ_TUNE_ENGINE_PROJECT_LAUNCH, engine/functions.cpp project_blocks): a
-    memset + result copy + completion event; a resident workspace and a
-    one-thread hand-off kernel + event; the hand-off kernel alone, the pipe
-    polling its words in mapped host memory.  Every form yields the
-    reference's blocks, several launches per pipe, and the divide-by-zero
-    error of a kept row."""
-    from fq_amd import FQError, ops
+def test_block_stream_launch_after_launch_and_after_an_error(eng):
+    """The engine's projection launches (engine/functions.cpp project_blocks):
+    the worker's resident workspace and result words, a one-thread hand-off
+    kernel after each projection kernel, one span per query -- several launches
+    per pipe yield the reference's blocks, twice, then the divide-by-zero error
+    of a kept row, then the right blocks again (the workspace re-zeroed, the
+    words of the failed launch not carried over)."""
+    from fq_amd import FQError
     from fq_amd.engine import OPT_CHUNK_ROWS
     n = 800_000 * 3 + 80_017
     sql = "SELECT number+1, number/2 FROM system.numbers_mt(%d) WHERE (number%%8)<3" % n
     expect = R.projection_blocks(n, P1_EXPRS, P1_WHERE)
-    ops.tune_set("ENGINE_PROJECT_LAUNCH", mode)
     try:
         eng.set_option(OPT_CHUNK_ROWS, 100_000)
         for _ in range(2):
@@ -282,8 +279,7 @@ def test_block_stream_under_each_queue_form(eng, mode):
             assert len(layouts) == 32
         with pytest.raises(FQError, match="Divide by zero"):
             _pull(eng, "SELECT 7/(number-300000) FROM system.numbers_mt(%d) WHERE number > 200000" % n)
-        per_pipe, _ = _pull(eng, sql)  # the engine runs on after the error
+        per_pipe, _ = _pull(eng, sql)
         _check_against_oracle(per_pipe, expect)
     finally:
-        ops.tune_set("ENGINE_PROJECT_LAUNCH", 0)
         eng.set_option(OPT_CHUNK_ROWS, 400_000_000)

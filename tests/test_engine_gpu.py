@@ -282,6 +282,8 @@ def test_error_aggregate_in_where():
     "SELECT max(number+1) FROM system.numbers_mt(8000000) WHERE (number%8)<3",
     # a LIMIT no partition can satisfy: every pipe is read to its end
     "SELECT number+1, number/2 FROM system.numbers_mt(8000000) WHERE number%999999937 = 0 LIMIT 3",
+    # a block-stream row pipeline (its projections timed by one LaunchSpan)
+    "SELECT number+1, number/2 FROM system.numbers_mt(800000) WHERE (number%8)<3",
 ])
 def test_pipe_that_cannot_set_up_its_context_fails_the_query(sql, pipe):
     """A pipe whose device context cannot be set up (a failed workspace
