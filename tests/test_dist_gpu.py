@@ -211,3 +211,38 @@ def test_world8_bench_rehearsal_on_one_gpu():
     # one all-reduce per step, of 8 ranks x (8 B length + 96 B of C3 states)
     assert h["exchange_rounds"] == 1 and h["exchange_bytes"] == 8 * 104
     assert h["exchange"] > 0 and h["partial"] > 0 and h["final"] > 0
+
+
+_ABSENT_PEER_CHILD = r"""
+import ctypes as C, json, sys, time
+sys.path.insert(0, %r)
+import torch
+from fq_amd import abi
+from fq_amd._lib import lib
+from fq_amd import dist as fqd
+uid = C.create_string_buffer(fqd.COMM_ID_BYTES)
+assert lib.fq_comm_unique_id(uid) == abi.FQ_OK
+h = C.c_void_p()
+t0 = time.monotonic()
+st = lib.fq_comm_init_timeout(0, 2, 0, uid, 3000, C.byref(h))
+print(json.dumps({"status": st, "msg": lib.fq_last_error().decode(), "elapsed": time.monotonic() - t0}), flush=True)
+"""
+
+
+def test_rccl_init_with_a_rank_that_never_arrives_fails_within_the_deadline():
+    """RCCL's own path to the deadline (fq_comm.cpp comm_wait): rank 0 of a
+    world-2 communicator whose rank 1 never arrives.  The non-blocking init
+    polls ncclCommGetAsyncError; after the 3 s deadline the communicator is
+    aborted and the call fails with FQ_E_RCCL naming the rank and the step --
+    no wait without end.  (Run in a child process with its own time limit: a
+    regression here must fail the test, not hang the suite.)"""
+    import json
+    import subprocess
+    code = _ABSENT_PEER_CHILD % os.path.join(ROOT, "fuse-query_amd")
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=90, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-2000:]
+    out = json.loads(p.stdout.strip().splitlines()[-1])
+    from fq_amd import abi
+    assert out["status"] == abi.FQ_E_RCCL, out
+    assert out["msg"].startswith("rank 0 of 2: ") and "did not complete within 3000 ms" in out["msg"], out
+    assert 2.5 <= out["elapsed"] < 30, out
