@@ -541,9 +541,34 @@ void Runtime::set_streams(int n) {
         shared_.push_back(s);
         shared_mu_.push_back(std::make_unique<std::mutex>());
     }
-    // existing workers keep their queue; new ones pick round-robin among the first n
+    // new workers pick round-robin among the first n; idle ones are dealt
+    // again once every queue has drained (a worker's resident projection
+    // workspace is re-zeroed by work on its old queue), so the next query's
+    // pipes spread over exactly n queues -- workers in use keep theirs
+    (void)hipDeviceSynchronize();
+    (void)hipGetLastError();
+    // blocks cached on the queues the pipes leave would hold the large
+    // class's cap while the new queues map every block afresh
+    if (n != active_streams_.load()) reclaim_device_memory();
     next_shared_ = 0;
     active_streams_ = n;
+    for (WorkerRes *w : free_) {
+        const size_t q = next_shared_++ % (size_t)n;
+        w->stream = shared_[q];
+        w->launch_mu = shared_mu_[q].get();
+        w->queue_index = q;
+    }
+}
+
+hipStream_t Runtime::row_queue(size_t lane, std::mutex **mu) {
+    const size_t q = lane % kRowQueues;
+    std::lock_guard<std::mutex> lk(mu_);
+    if (!row_[q]) {
+        check_hip(hipStreamCreateWithFlags(&row_[q], hipStreamNonBlocking), "hipStreamCreateWithFlags");
+        BlockCache::get().add_stream(row_[q]);
+    }
+    *mu = &row_mu_[q];
+    return row_[q];
 }
 
 WorkerRes *Runtime::acquire() {
@@ -597,6 +622,8 @@ Runtime::~Runtime() {
     if (device_ == kHostOnly) return;
     (void)hipSetDevice(device_);
     for (auto &s : shared_) (void)hipStreamSynchronize(s);
+    for (auto &s : row_)
+        if (s) (void)hipStreamSynchronize(s);
     for (auto &w : all_) {
         if (w->own) {
             (void)hipStreamSynchronize(w->own);
@@ -615,6 +642,11 @@ Runtime::~Runtime() {
         BlockCache::get().drop_stream(s);
         (void)hipStreamDestroy(s);
     }
+    for (auto &s : row_)
+        if (s) {
+            BlockCache::get().drop_stream(s);
+            (void)hipStreamDestroy(s);
+        }
 }
 
 void WorkerRes::project_resident() {
@@ -772,16 +804,19 @@ std::shared_ptr<DeviceBuffer> DeviceBuffer::alloc_sync(size_t bytes) {
     return b;
 }
 
-ExecCtx::ExecCtx(Runtime *r, bool own_queue) : rt(r), res(nullptr), prev_(g_current) {
+ExecCtx::ExecCtx(Runtime *r, QueueKind kind, size_t lane) : rt(r), res(nullptr), prev_(g_current) {
     if (rt->has_device()) check_hip(hipSetDevice(rt->device()), "hipSetDevice");
     res = rt->acquire();
     stream_ = res->stream;
-    if (own_queue && rt->has_device()) {
+    launch_mu_ = res->launch_mu;
+    if (kind == QueueKind::kOwn && rt->has_device()) {
         if (!res->own) {
             check_hip(hipStreamCreateWithFlags(&res->own, hipStreamNonBlocking), "hipStreamCreateWithFlags");
             BlockCache::get().add_stream(res->own);
         }
         stream_ = res->own;
+    } else if (kind == QueueKind::kRow && rt->has_device()) {
+        stream_ = rt->row_queue(lane, &launch_mu_);
     }
     g_current = this;
 }
@@ -820,7 +855,7 @@ void ExecCtx::sync() {
     hipEvent_t ev = res->take_sync_event();
     hipError_t e;
     {
-        std::lock_guard<std::mutex> lk(*res->launch_mu);
+        std::lock_guard<std::mutex> lk(*launch_mu_);
         e = hipEventRecord(ev, stream());
     }
     if (e == hipSuccess) e = hipEventSynchronize(ev);

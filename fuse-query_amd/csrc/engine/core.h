@@ -213,6 +213,13 @@ class Runtime {
     void release(WorkerRes *w);
     void set_streams(int n);
     int active_streams() const { return active_streams_; }
+    // block-stream row pipelines' queues (QueueKind::kRow): two, measured
+    // against one in one process, ms per p1 query (profiles/r06_f_p1_streams_ab.json):
+    // 1 queue 23.80, 2 queues 23.07, 4 queues unstable (their cached blocks
+    // outgrow the large class); aggregates stay on one (2: C3 11.10 -> 11.71,
+    // profiles/r06_g_c3_streams_ab.json)
+    static constexpr size_t kRowQueues = 2;
+    hipStream_t row_queue(size_t lane, std::mutex **mu);
     // timing-capable events shared across pipe threads (ScanGroup)
     hipEvent_t take_event();
     void give_event(hipEvent_t e);
@@ -236,6 +243,8 @@ class Runtime {
     std::vector<WorkerRes *> free_;
     std::vector<hipStream_t> shared_;  // FQ_OPT_STREAMS queues shared by the pipes
     std::vector<std::unique_ptr<std::mutex>> shared_mu_;
+    hipStream_t row_[kRowQueues] = {};
+    std::mutex row_mu_[kRowQueues];
     size_t next_shared_ = 0;
     std::atomic<int> active_streams_{1};
     std::vector<hipEvent_t> events_;  // take_event / give_event (under mu_)
@@ -282,12 +291,19 @@ size_t block_cache_workspace_bytes();  // kept per-queue workspaces (counted apa
 
 // Execution context of the thread running a pipe (tokio task in the
 // reference, processor_merge.rs:45-63): its device queue and workspaces.
+// Which device queue a context's work goes to:
+//   kShared  the worker's shared queue (FQ_OPT_STREAMS of them; aggregates:
+//            their HBM-bound scans run back to back)
+//   kOwn     the worker's private queue (LIMIT row pipelines synchronise per
+//            morsel; a shared queue would make every pipe wait for the others)
+//   kRow     row queue `lane % Runtime::kRowQueues` (block-stream row
+//            pipelines: one projection launch's tail overlaps the next one's
+//            ramp on the other queue)
+enum class QueueKind { kShared, kOwn, kRow };
+
 class ExecCtx {
    public:
-    // own_queue: this context's device work goes to its worker's private
-    // queue instead of the shared one (row pipelines synchronise per morsel,
-    // and a shared queue would make every pipe wait for all the others)
-    explicit ExecCtx(Runtime *rt, bool own_queue = false);
+    explicit ExecCtx(Runtime *rt, QueueKind kind = QueueKind::kShared, size_t lane = 0);
     ~ExecCtx();
     ExecCtx(const ExecCtx &) = delete;
     ExecCtx &operator=(const ExecCtx &) = delete;
@@ -297,6 +313,8 @@ class ExecCtx {
     WorkerRes *res;
     AggFusion *fusion = nullptr;  // set while an AggregatePartial drains its input
     hipStream_t stream() const { return stream_; }
+    // serialises multi-call enqueues on this context's queue
+    std::mutex *launch_mu() const { return launch_mu_; }
     void sync();
     // hands this context's WorkerRes (queue, workspace, pinned result slots)
     // to a shared owner that releases it to the runtime: work this context
@@ -306,6 +324,7 @@ class ExecCtx {
    private:
     ExecCtx *prev_;
     hipStream_t stream_ = nullptr;
+    std::mutex *launch_mu_ = nullptr;
     bool leased_ = false;
 };
 

@@ -775,7 +775,7 @@ static bool project_blocks(const DataBlock &b, const Column &c, const fq_pred *p
     check_fq(st);
     hipEvent_t done = ctx.res->take_sync_event();
     {
-        std::lock_guard<std::mutex> lk(*ctx.res->launch_mu);
+        std::lock_guard<std::mutex> lk(*ctx.launch_mu());
         if (span) span->before_launch(ctx);
         // this worker's last hand-off has landed (the pipe waited for it); an
         // empty block launches nothing, so its words must read 0 kept rows
@@ -896,7 +896,7 @@ void LaunchSpan::before_launch(ExecCtx &ctx) {
         if (s.q == ctx.stream()) return;
     QueueSpan s;
     s.q = ctx.stream();
-    s.launch_mu = ctx.res->launch_mu;
+    s.launch_mu = ctx.launch_mu();
     s.start = rt_->take_event();
     check_hip(hipEventRecord(s.start, s.q), "hipEventRecord");
     queues_.push_back(s);
@@ -910,22 +910,33 @@ void LaunchSpan::arrive() noexcept {
         qs = queues_;
     }
     // the last pipe: every launch of the query has completed (each pipe waited
-    // for its own); one end event per queue closes its span
+    // for its own); one end event per queue closes its span.  The query's
+    // span is the union over its queues (the row queues' launches overlap):
+    // earliest start to latest end, both measured from the first queue's start.
+    if (qs.empty()) return;
+    float lo = 0, hi = 0;
+    bool ok = true;
     for (QueueSpan &s : qs) {
         hipEvent_t end = nullptr;
         try {
             end = rt_->take_event();
             {
                 std::lock_guard<std::mutex> ql(*s.launch_mu);
-                if (hipEventRecord(end, s.q) != hipSuccess) continue;
+                ok = ok && hipEventRecord(end, s.q) == hipSuccess;
             }
-            float ms = 0;
-            if (hipEventSynchronize(end) == hipSuccess && hipEventElapsedTime(&ms, s.start, end) == hipSuccess)
-                rt_->stats.project_ns += (uint64_t)((double)ms * 1e6);
+            float a = 0, b = 0;
+            ok = ok && hipEventSynchronize(end) == hipSuccess &&
+                 hipEventElapsedTime(&a, qs[0].start, s.start) == hipSuccess &&
+                 hipEventElapsedTime(&b, qs[0].start, end) == hipSuccess;
+            lo = std::min(lo, a);
+            hi = std::max(hi, b);
         } catch (...) {  // timing only: never fail the query for it
+            ok = false;
         }
         if (end) rt_->give_event(end);
     }
+    (void)hipGetLastError();
+    if (ok) rt_->stats.project_ns += (uint64_t)((double)(hi - lo) * 1e6);
 }
 
 // ---------------------------------------------------------------------------
@@ -944,7 +955,7 @@ void ScanGroup::before_launch(ExecCtx &ctx) {
         if (s.q == ctx.stream()) return;
     QueueSpan s;
     s.q = ctx.stream();
-    s.launch_mu = ctx.res->launch_mu;
+    s.launch_mu = ctx.launch_mu();
     if (rt_->profile.load() == 2) {  // the span opens right before this queue's first scan
         s.start = rt_->take_event();
         check_hip(hipEventRecord(s.start, s.q), "hipEventRecord");
@@ -1031,7 +1042,7 @@ void ScanGroup::account() {
 // AggFusion
 // ---------------------------------------------------------------------------
 AggFusion::AggFusion(ExecCtx &ctx, ScanTicket *ticket)
-    : ctx_(ctx), rt_(ctx.rt), res_(ctx.res), stream_(ctx.stream()), ticket_(ticket) {}
+    : ctx_(ctx), rt_(ctx.rt), res_(ctx.res), stream_(ctx.stream()), launch_mu_(ctx.launch_mu()), ticket_(ticket) {}
 
 AggFusion::~AggFusion() {
     // an exception left scans in flight: they write into this worker's pinned
@@ -1068,7 +1079,7 @@ size_t AggFusion::alloc_slot() {
 void AggFusion::wait_launched() {
     hipEvent_t done = res_->take_sync_event();
     {
-        std::lock_guard<std::mutex> lk(*res_->launch_mu);
+        std::lock_guard<std::mutex> lk(*launch_mu_);
         check_hip(hipEventRecord(done, stream_), "hipEventRecord");
     }
     hipError_t e = hipEventSynchronize(done);
@@ -1153,7 +1164,7 @@ void AggFusion::end_block() {
         {
             // events and the scan enqueue back to back even when other pipes
             // share this queue, so an event pair brackets this scan
-            std::lock_guard<std::mutex> lk(*ctx_.res->launch_mu);
+            std::lock_guard<std::mutex> lk(*ctx_.launch_mu());
             const fq_pred *pred = g.has_pred ? g.pred.get() : nullptr;
             const fq_expr *val = g.value.expr.n_steps ? &g.value.expr : nullptr;
             if (ticket_ && ticket_->group()) ticket_->group()->before_launch(ctx_);

@@ -336,11 +336,12 @@ class ScanGroup {
 using ScanGroupRef = std::shared_ptr<ScanGroup>;
 
 // The block-stream projections of ONE query (a row pipeline's
-// ProjectionTransform pipes, fq_filter_project_blocks) timed as one span per
-// queue, like ScanGroup's scans: FQ_OPT_PROFILE 2 records a start event right
-// before the queue's first launch of the query and, when the last pipe's
-// stream has ended, an end event -- project_ns gets the span (the launches
-// and every gap between them); no event sits between two launches.  (The end
+// ProjectionTransform pipes, fq_filter_project_blocks) timed as one span,
+// like ScanGroup's scans: FQ_OPT_PROFILE 2 records a start event right before
+// each queue's first launch of the query and, when the last pipe's stream has
+// ended, an end event per queue -- project_ns gets the union of the queues'
+// spans, earliest start to latest end (the launches, overlapped across the
+// row queues, and every gap); no event sits between two launches.  (The end
 // is recorded once that pipe has seen its last launch complete, so the span
 // also holds that pipe's wake-up: it over-states, never under-states.)
 class LaunchSpan {
@@ -449,6 +450,7 @@ class AggFusion {
     Runtime *rt_;
     WorkerRes *res_;
     hipStream_t stream_;
+    std::mutex *launch_mu_;
     ScanTicket *ticket_ = nullptr;  // the query's pipes wait together (ScanGroup)
     std::vector<Group> cur_;
     std::vector<Entry> log_;

@@ -330,12 +330,12 @@ StreamRef MergeProcessor::execute() {
     auto task = [&](size_t pipe) {
         std::shared_ptr<Channel> ch = cs->ch;
         ProcessorRef in = list_[pipe];
-        const bool own = own_queues_;
-        return [in, ch, rt, pipe, own]() {
+        const QueueKind queues = queues_;
+        return [in, ch, rt, pipe, queues]() {
             try {
                 if (rt->fault_pipe.load(std::memory_order_relaxed) == (int64_t)pipe + 1)
                     throw FQException(FQ_E_HIP, "hipMalloc(workspace): out of memory (FQ_OPT_FAULT_PIPE)");
-                ExecCtx ctx(rt, own);
+                ExecCtx ctx(rt, queues, pipe);
                 StreamRef s = in->execute();
                 DataBlock b;
                 // the consumer gone (a satisfied LIMIT dropped the merged
@@ -732,7 +732,7 @@ GroupPlan plan_group_by(const fq_group_table &d, const fq_col &c, const fq_pred 
     fq_col sample = c;
     sample.len = rows;
     {
-        std::lock_guard<std::mutex> lk(*ctx.res->launch_mu);
+        std::lock_guard<std::mutex> lk(*ctx.launch_mu());
         check_fq(fq_group_table_init(&t, ctx.stream()));
         check_fq(fq_group_aggregate(&t, &sample, pred, key, nullptr, ctx.stream()));
     }
@@ -830,7 +830,7 @@ StreamRef GroupByPartialTransform::execute() {
                 shared_->mem = DeviceBuffer::alloc(fq_group_table_bytes(d.capacity, d.n_aggs), ctx.stream());
                 d.d_mem = shared_->mem->ptr;
                 {
-                    std::lock_guard<std::mutex> lk2(*ctx.res->launch_mu);
+                    std::lock_guard<std::mutex> lk2(*ctx.launch_mu());
                     check_fq(fq_group_table_init(&d, ctx.stream()));
                 }
                 ctx.sync();  // other pipes may use other queues
@@ -878,7 +878,7 @@ StreamRef GroupByPartialTransform::execute() {
             ws = slot;
         }
         {
-            std::lock_guard<std::mutex> lk(*ctx.res->launch_mu);
+            std::lock_guard<std::mutex> lk(*ctx.launch_mu());
             if (prof) check_hip(hipEventRecord(e0, ctx.stream()), "hipEventRecord");
             if (lp > 0) {
                 fq_pred pc{};
@@ -1139,7 +1139,7 @@ void Pipeline::merge_processor() {
     if (pipes_.back().size() > 1) {
         // AggregatePartial pipes emit one block each (pipeline_builder.rs:73-95)
         const bool one_block = dynamic_cast<AggregatePartialTransform *>(pipes_.back()[0].get()) != nullptr;
-        auto p = std::make_shared<MergeProcessor>(own_queues_, one_block);
+        auto p = std::make_shared<MergeProcessor>(queues_, one_block);
         for (auto &x : pipes_.back()) p->connect_to(x);
         pipes_.push_back({p});
     }

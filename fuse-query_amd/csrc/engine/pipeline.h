@@ -171,8 +171,8 @@ class EmptyProcessor : public IProcessor {  // processor_empty.rs:14-49
 
 class MergeProcessor : public IProcessor {  // processor_merge.rs:16-94
    public:
-    explicit MergeProcessor(bool own_queues = false, bool inline_first = false)
-        : own_queues_(own_queues), inline_first_(inline_first) {}
+    explicit MergeProcessor(QueueKind queues = QueueKind::kShared, bool inline_first = false)
+        : queues_(queues), inline_first_(inline_first) {}
     std::string name() const override { return "MergeProcessor"; }
     void connect_to(ProcessorRef input) override { list_.push_back(std::move(input)); }
     StreamRef execute() override;
@@ -180,7 +180,7 @@ class MergeProcessor : public IProcessor {  // processor_merge.rs:16-94
 
    private:
     std::vector<ProcessorRef> list_;
-    bool own_queues_;     // each input pipe on its worker's private device queue
+    QueueKind queues_;    // the input pipes' device queues (kRow: pipe p on row queue p)
     bool inline_first_;   // pipe 0 runs on the calling thread (one-block pipes)
 };
 
@@ -374,11 +374,11 @@ class Pipeline {
     StreamRef execute();
     std::string display() const;
     // row pipelines (no aggregate): merged pipes run on private device queues
-    void set_own_queues(bool v) { own_queues_ = v; }
+    void set_queues(QueueKind k) { queues_ = k; }
 
    private:
     std::vector<std::vector<ProcessorRef>> pipes_;
-    bool own_queues_ = false;
+    QueueKind queues_ = QueueKind::kShared;
 };
 
 // serialised partial states (one 16-byte record per DataValue)

@@ -607,16 +607,18 @@ Pipeline build_pipeline(const QueryPlan &plan, const QueryContextRef &ctx, bool 
     Pipeline p;
     // No aggregate above the source: a row pipeline.  With a LIMIT its pipes
     // read growing morsels on private queues (a satisfied LIMIT stops after
-    // the first few); without one they read bounded pieces and share the
-    // aggregates' queue, so their HBM-bound launches run back to back, each
-    // bracketed by its own timing events.
+    // the first few); without one they read bounded pieces on the two row
+    // queues (pipe p on queue p % 2: a projection launch's tail overlaps the
+    // next one's start, Runtime::kRowQueues).  Aggregates share one queue.
     bool row_pipeline = true, has_limit = false;
     for (const PlanNode &n : plan.nodes) {
         if (n.kind == PlanNode::kAggregate) row_pipeline = false;
         if (n.kind == PlanNode::kLimit) has_limit = true;
     }
     const ReadMode mode = !row_pipeline ? ReadMode::kWhole : has_limit ? ReadMode::kMorsels : ReadMode::kChunks;
-    p.set_own_queues(mode == ReadMode::kMorsels);
+    p.set_queues(mode == ReadMode::kMorsels ? QueueKind::kOwn
+                 : mode == ReadMode::kChunks ? QueueKind::kRow
+                                             : QueueKind::kShared);
     for (const PlanNode &n : plan.nodes) {
         switch (n.kind) {
             case PlanNode::kLimit: {

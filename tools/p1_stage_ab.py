@@ -23,13 +23,14 @@ import bench  # noqa: E402
 
 bench._load_runtime()
 torch, ops = bench.torch, bench.ops
-from fq_amd.engine import Engine  # noqa: E402
+from fq_amd.engine import OPT_STREAMS, Engine  # noqa: E402
 
 ROUNDS = int(sys.argv[1]) if len(sys.argv) > 1 else 4
 STEPS = int(sys.argv[2]) if len(sys.argv) > 2 else 8
 N = 10_000_000_000
 # configs: S:R = (FQ_TUNE_SELECT_BLOCKS_STAGE, FQ_TUNE_SELECT_BLOCKS_ROWS), or any
-# knobs as KNOB=V[,KNOB=V...] (abi.TUNE names); argv[3:] overrides the default set
+# knobs as KNOB=V[,KNOB=V...] (abi.TUNE names; STREAMS=n is the engine's
+# FQ_OPT_STREAMS, 1 when a config does not name it); argv[3:] overrides the default set
 
 
 def parse_config(a):
@@ -67,8 +68,10 @@ def main():
     for r in range(ROUNDS):
         for c in (CONFIGS if r % 2 == 0 else CONFIGS[::-1]):
             ops.tune_reset()
+            eng.set_option(OPT_STREAMS, dict(c).get("STREAMS", 1))
             for k, v in c:
-                ops.tune_set(k, v)
+                if k != "STREAMS":
+                    ops.tune_set(k, v)
             got = step(check=(r == 0))
             if r == 0 and got != expect:
                 raise SystemExit("PARITY FAILURE %r: got %r expected %r" % (c, got, expect))
