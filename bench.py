@@ -166,20 +166,25 @@ def settle(step, seconds, world, backend):
     first second after another process freed 80 GB, the first three after 160 GB
     (profiles/r05_j_reclaim_probe/; the GPU test suite before a bench frees more).
     At world > 1 every step is a collective, so every rank runs the same count:
-    the most any rank needs for `seconds` at its first step's pace.  -> steps run."""
+    the most any rank needs for the rest of `seconds` at its SECOND step's pace
+    (the first compiles hipRTC kernels and maps buffers: at its pace a c4
+    settle ran ~0.1 s instead of 3).  -> steps run."""
     if seconds <= 0:
         return 0
     t0 = time.perf_counter()
     step()
-    one = max(time.perf_counter() - t0, 1e-4)
-    n = max(int(seconds / one), 1)
+    t1 = time.perf_counter()
+    step()
+    t2 = time.perf_counter()
+    one = max(t2 - t1, 1e-4)
+    n = max(int((seconds - (t2 - t0)) / one), 0)
     if world > 1:
         t = torch.tensor([n], dtype=torch.int64, device="cuda" if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         n = int(t.item())
-    for _ in range(n - 1):
+    for _ in range(n):
         step()
-    return n
+    return n + 2
 
 
 def latest_pmc_traffic(kernel_substr, query, rows_per_launch):

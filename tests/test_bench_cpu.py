@@ -137,8 +137,9 @@ def test_bench_module_imports_without_the_hip_runtime():
 
 
 def test_settle_runs_untimed_steps_for_about_the_requested_time():
-    # bench.settle: steps for ~`seconds` at the first step's pace (world 1: no
-    # collective); 0 s runs none, and a step slower than the budget runs once
+    # bench.settle: steps for ~`seconds` at the SECOND step's pace (world 1: no
+    # collective); 0 s runs none, a step slower than the budget runs twice, and
+    # a slow first step (hipRTC compile, first mapping) does not cut the settle
     import time
     b = _bench()
     calls = []
@@ -151,4 +152,13 @@ def test_settle_runs_untimed_steps_for_about_the_requested_time():
     n = b.settle(step, 0.05, 1, "gloo")
     assert n == len(calls) and 10 <= n <= 30, n
     calls.clear()
-    assert b.settle(lambda: (calls.append(1), time.sleep(0.03)), 0.01, 1, "gloo") == 1 and len(calls) == 1
+    assert b.settle(lambda: (calls.append(1), time.sleep(0.03)), 0.01, 1, "gloo") == 2 and len(calls) == 2
+    calls.clear()
+
+    def slow_first():
+        time.sleep(0.05 if not calls else 0.002)
+        calls.append(time.perf_counter())
+
+    t0 = time.perf_counter()
+    n = b.settle(slow_first, 0.2, 1, "gloo")
+    assert n == len(calls) and time.perf_counter() - t0 >= 0.15, (n, time.perf_counter() - t0)
