@@ -46,8 +46,10 @@ typedef struct fq_result fq_result;
                                    the scans, and on a generated partition its fills):
                                    no event between two scans.  Row-pipeline and GROUP
                                    BY launches are timed per launch with 1 or 2 */
-#define FQ_OPT_STREAMS 4        /* device queues the pipes share (default 1: the scans are
-                                   HBM-bound, concurrency buys nothing and blurs timing) */
+#define FQ_OPT_STREAMS 4        /* device queues the aggregate pipes share (default 1: the scans
+                                   are HBM-bound; two cost 5.5 %).  Row pipelines without a LIMIT
+                                   use two row queues of their own, with a LIMIT one private
+                                   queue per pipe */
 #define FQ_OPT_CHUNK_ROWS 5     /* rows per device block of a numbers_mt partition that is NOT
                                    resident (a multiple of 10,000; default 400,000,000 = 3.2 GB):
                                    aggregates over numbers_mt(1e12) stream through bounded HBM
