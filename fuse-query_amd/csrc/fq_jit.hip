@@ -2232,9 +2232,15 @@ std::string proj_shape_key(const ProjLaunch &P, int32_t tin, int dev) {
 // thread with a half-tile stage (32 KB, 4 workgroups per CU, p1's 3/8 kept in
 // one pass) 0.725; a whole-tile stage at 16 rows 0.730-0.734, at 32 rows (2
 // workgroups per CU) 0.945; a quarter-tile stage at 32 rows (two passes)
-// 0.733; the round-4 kernel (32 rows, stores from registers) 0.760-0.769.  16-byte row-pair loads (two
-// ballots per 128 rows, each lane storing its two kept rows) measured 4.52
-// against 3.10 ms: a wave's stores then interleave and no longer combine.
+// 0.733; the round-4 kernel (32 rows, stores from registers) 0.760-0.769.
+// Row pairs (round 6): each lane loads two adjacent rows with one 16-byte
+// non-temporal load and a 128-row group takes two ballots (first and second
+// rows); in-tile ranks count both.  Round 4 measured pairs slower (4.52 vs
+// 3.10 ms) while lanes stored their own kept rows -- a wave's stores then
+// interleave; behind the LDS stage the stores no longer depend on the lane
+// mapping and pairs win: 0.7045 -> 0.6768 ms per 3.125e8-row block, 22.66 ->
+// 21.75 ms per p1 query, one process, 4 rounds (profiles/r06_i_p1_pairs_ab.json).
+// A tile that is ragged or not 16-byte aligned loads its pairs 8 bytes at a time.
 std::string gen_project_blocks_kernel(bool bitmap_pred) {
     std::string s = "#define PB_ROWS " + std::to_string(fqc::knob(FQ_TUNE_SELECT_BLOCKS_ROWS)) + "\n#define PB_STAGE " +
                     std::to_string(fqc::knob(FQ_TUNE_SELECT_BLOCKS_STAGE)) + "\n";
@@ -2242,10 +2248,13 @@ std::string gen_project_blocks_kernel(bool bitmap_pred) {
 #define PB_THREADS 256
 #define PB_WAVES (PB_THREADS / 64)
 #define PB_TILE (PB_THREADS * PB_ROWS)
-#define PB_NE (PB_ROWS * PB_WAVES)  // 64-row ballots per tile
+#define PB_NP (PB_ROWS / 2)        // 16-byte row pairs per thread per tile
+#define PB_NE (PB_NP * PB_WAVES)   // 128-row groups per tile
 #define PB_PUT fq_put_nt
+// group i = k * PB_WAVES + wave holds tile rows [128 i, 128 i + 128): lane l's
+// pair is rows 128 i + 2 l (its b0 bit) and 128 i + 2 l + 1 (its b1 bit)
 struct PbShared {
-    u64 bal[2][PB_NE];      // ballot of 64-row group i = k * PB_WAVES + wave (tile rows [64 i, 64 i + 64))
+    u64 b0[2][PB_NE], b1[2][PB_NE];
     u32 off[2][PB_NE + 1];  // exclusive in-tile offset of each group; [PB_NE]: the tile's kept rows
 };
 // exclusive scan of the ng group counts in off[] by wave 0; off[PB_NE] = total
@@ -2269,7 +2278,7 @@ __device__ __forceinline__ void pb_scan(u32 *__restrict__ off, int ng, int lane)
         if (lane * PER + q < ng) off[lane * PER + q] = run;
         run += cv[q];
     }
-    if (lane == 63) off[PB_NE] = incl;
+    if (lane == 63) off[ng] = incl;
 }
 #if PB_STAGE
 // PB_STAGE: the tile's kept rows staged in LDS by in-tile rank, then written
@@ -2294,9 +2303,6 @@ __device__ __forceinline__ void pb_copy(const TIn *__restrict__ st, u32 base, u3
 }
 #endif
 )";
-    const std::string pred8 = bitmap_pred ? "            const bool p = live && ((bm[row >> 6] >> (row & 63)) & 1ull);\n"
-                                            "            (void)c;\n"
-                                          : "            const bool p = fq_pred(x[k], c, pflags, live) && live;\n";
     s += R"(extern "C" __global__ void __launch_bounds__(PB_THREADS)
 fq_jit_pblocks(const TIn *__restrict__ col, long long n, long long B, Consts c,
     const u64 *__restrict__ bm, Outs o, long long *__restrict__ counts, u32 *__restrict__ fl,
@@ -2325,56 +2331,73 @@ fq_jit_pblocks(const TIn *__restrict__ col, long long n, long long B, Consts c,
     long long cur = b_lo;  // the open block
     u64 carry = 0;         // its kept rows so far
     for (long long r0 = b_lo * B; r0 < end; r0 += PB_TILE, par ^= 1) {
-        u64 *__restrict__ bal = sh.bal[par];
-        u32 *__restrict__ off = sh.off[par];
 )";
+    const std::string predp =
+        bitmap_pred ? "            const bool p0 = live0 && ((bm[row >> 6] >> (row & 63)) & 1ull);\n"
+                      "            const bool p1 = live1 && ((bm[(row + 1) >> 6] >> ((row + 1) & 63)) & 1ull);\n"
+                      "            (void)c;\n"
+                    : "            const bool p0 = fq_pred(x0[k], c, pflags, live0) && live0;\n"
+                      "            const bool p1 = fq_pred(x1[k], c, pflags, live1) && live1;\n";
     s += R"(
-        TIn x[PB_ROWS];
-        const long long rt = r0 + tid;
-        if (r0 + PB_TILE <= end) {
+        u64 *__restrict__ b0s = sh.b0[par];
+        u64 *__restrict__ b1s = sh.b1[par];
+        u32 *__restrict__ off = sh.off[par];
+        // 16-byte row-pair loads when the tile is whole and 16-byte aligned
+        TIn x0[PB_NP], x1[PB_NP];
+        if (r0 + PB_TILE <= end && ((((unsigned long long)(col + r0)) & 15ull) == 0ull)) {
+            const u32x4 *__restrict__ vp = (const u32x4 *)(col + r0);
 #pragma unroll
-            for (int k = 0; k < PB_ROWS; ++k) x[k] = __builtin_nontemporal_load(col + rt + k * PB_THREADS);
+            for (int k = 0; k < PB_NP; ++k) {
+                const u32x4 raw = __builtin_nontemporal_load(vp + tid + k * PB_THREADS);
+                __builtin_memcpy(&x0[k], &raw, 8);
+                __builtin_memcpy(&x1[k], ((const char *)&raw) + 8, 8);
+            }
         } else {
 #pragma unroll
-            for (int k = 0; k < PB_ROWS; ++k) {
-                const long long row = rt + k * PB_THREADS;
-                x[k] = row < end ? __builtin_nontemporal_load(col + row) : TIn(0);
+            for (int k = 0; k < PB_NP; ++k) {
+                const long long row = r0 + 2 * (long long)(tid + k * PB_THREADS);
+                x0[k] = row < end ? __builtin_nontemporal_load(col + row) : TIn(0);
+                x1[k] = row + 1 < end ? __builtin_nontemporal_load(col + row + 1) : TIn(0);
             }
         }
 #pragma unroll
-        for (int k = 0; k < PB_ROWS; ++k) {
-            const long long row = rt + k * PB_THREADS;
-            const u32 live = row < end ? 1u : 0u;
-)" + pred8 + R"(
-            const u64 b = __ballot(p);
+        for (int k = 0; k < PB_NP; ++k) {
+            const long long row = r0 + 2 * (long long)(tid + k * PB_THREADS);
+            const u32 live0 = row < end ? 1u : 0u, live1 = row + 1 < end ? 1u : 0u;
+)" + predp + R"(
+            const u64 c0 = __ballot(p0), c1 = __ballot(p1);
             if (lane == 0) {
-                bal[k * PB_WAVES + wave] = b;
-                off[k * PB_WAVES + wave] = (u32)__popcll(b);
+                b0s[k * PB_WAVES + wave] = c0;
+                b1s[k * PB_WAVES + wave] = c1;
+                off[k * PB_WAVES + wave] = (u32)(__popcll(c0) + __popcll(c1));
             }
         }
         __syncthreads();
         if (wave == 0) pb_scan(off, PB_NE, lane);
         __syncthreads();
         const u32 tot = off[PB_NE];
-        // the open block's edge: inside the tile (or at its end) when e <= PB_TILE
         const long long bnd = (cur + 1) * B < n ? (cur + 1) * B : n;
         const long long e = bnd - r0;
-        u32 re = tot;  // kept rows of the tile before the edge
+        u32 re = tot;  // kept rows of the tile before the open block's edge
         if (e < PB_TILE) {
-            const int g = (int)(e >> 6), bit = (int)(e & 63);
-            re = off[g] + (u32)__popcll(bal[g] & ((1ull << bit) - 1ull));
+            const int g = (int)(e >> 7), pos = (int)(e & 127), h = pos >> 1;
+            const u64 m = (1ull << h) - 1ull;
+            re = off[g] + (u32)__popcll(b0s[g] & m) + (u32)__popcll(b1s[g] & m) +
+                 ((pos & 1) ? (u32)((b0s[g] >> h) & 1ull) : 0u);
         }
-        // kept rows before the edge have in-tile ranks < re, the rest >= re
-        const long long before = cur * B + (long long)carry;  // output row of in-tile rank 0
-        const long long after = (cur + 1) * B - (long long)re;  // ... for ranks past the edge
+        const long long before = cur * B + (long long)carry;
+        const long long after = (cur + 1) * B - (long long)re;
 #if PB_STAGE
-        for (u32 base = 0; base < tot; base += PB_CAP) {  // tot is the workgroup's: uniform
-            if (base) __syncthreads();  // the last pass's reads done (the next tile's follow its two barriers)
+        for (u32 base = 0; base < tot; base += PB_CAP) {
+            if (base) __syncthreads();
 #pragma unroll
-            for (int k = 0; k < PB_ROWS; ++k) {
-                const u64 b = bal[k * PB_WAVES + wave];
-                const u32 r = off[k * PB_WAVES + wave] + (u32)__popcll(b & lt) - base;
-                if (((b >> lane) & 1ull) && r < PB_CAP) stage[r] = x[k];
+            for (int k = 0; k < PB_NP; ++k) {
+                const u64 c0 = b0s[k * PB_WAVES + wave], c1 = b1s[k * PB_WAVES + wave];
+                const u32 k0 = (u32)((c0 >> lane) & 1ull), k1 = (u32)((c1 >> lane) & 1ull);
+                // rank - base, wrapping for ranks below base (then >= PB_CAP)
+                const u32 r = off[k * PB_WAVES + wave] + (u32)__popcll(c0 & lt) + (u32)__popcll(c1 & lt) - base;
+                if (k0 && r < PB_CAP) stage[r] = x0[k];
+                if (k1 && r + k0 < PB_CAP) stage[r + k0] = x1[k];
             }
             __syncthreads();
             const u32 hi = tot - base < PB_CAP ? tot : base + PB_CAP;
@@ -2383,12 +2406,12 @@ fq_jit_pblocks(const TIn *__restrict__ col, long long n, long long B, Consts c,
         }
 #else
 #pragma unroll
-        for (int k = 0; k < PB_ROWS; ++k) {
-            const u64 b = bal[k * PB_WAVES + wave];
-            if ((b >> lane) & 1ull) {
-                const u32 rank = off[k * PB_WAVES + wave] + (u32)__popcll(b & lt);
-                PB_PUT(x[k], c, vflags, 1u, o, (rank < re ? before : after) + (long long)rank);
-            }
+        for (int k = 0; k < PB_NP; ++k) {
+            const u64 c0 = b0s[k * PB_WAVES + wave], c1 = b1s[k * PB_WAVES + wave];
+            const u32 k0 = (u32)((c0 >> lane) & 1ull), k1 = (u32)((c1 >> lane) & 1ull);
+            const u32 rank = off[k * PB_WAVES + wave] + (u32)__popcll(c0 & lt) + (u32)__popcll(c1 & lt);
+            if (k0) PB_PUT(x0[k], c, vflags, 1u, o, (rank < re ? before : after) + (long long)rank);
+            if (k1) PB_PUT(x1[k], c, vflags, 1u, o, (rank + k0 < re ? before : after) + (long long)(rank + k0));
         }
 #endif
 )";
