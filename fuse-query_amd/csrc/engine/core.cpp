@@ -649,7 +649,7 @@ Runtime::~Runtime() {
         }
 }
 
-void WorkerRes::project_resident() {
+void WorkerRes::project_resident(hipStream_t st) {
     if (project_ws) return;
     void *h = nullptr, *d = nullptr, *ws = nullptr;
     check_hip(hipHostMalloc(&h, 4 * sizeof(uint64_t), hipHostMallocMapped | hipHostMallocCoherent),
@@ -659,7 +659,9 @@ void WorkerRes::project_resident() {
     project_dres = (uint64_t *)d;
     const size_t bytes = fq_filter_project_blocks_workspace_bytes();
     check_hip(alloc_with_reclaim([&] { return hipMalloc(&ws, bytes); }), "hipMalloc(projection workspace)");
-    check_hip(hipMemset(ws, 0, bytes), "hipMemset(projection workspace)");  // the hand-off keeps it zeroed
+    // ordered before this worker's first projection launch on st; the hand-off
+    // kernel after every launch keeps it zeroed from then on
+    check_hip(hipMemsetAsync(ws, 0, bytes, st), "hipMemsetAsync(projection workspace)");
     project_ws = ws;
 }
 

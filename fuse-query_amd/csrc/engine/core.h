@@ -170,7 +170,10 @@ struct WorkerRes {
     // and a workspace kept zeroed between launches (project_ws)
     uint64_t *project_res = nullptr, *project_dres = nullptr;
     void *project_ws = nullptr;
-    void project_resident();  // makes the three on first use
+    // makes the three on first use; the workspace is zeroed on `st`, the
+    // queue of the launch that follows (a non-blocking queue does not wait
+    // for a memset on the null stream)
+    void project_resident(hipStream_t st);
     hipEvent_t take_event();
     void give_event(hipEvent_t e) { events.push_back(e); }
     // completion-only events (hipEventDisableTiming: no timestamp to write)

@@ -751,7 +751,7 @@ static bool project_blocks(const DataBlock &b, const Column &c, const fq_pred *p
     // the map kernel (no predicate) has its words written by the host and no
     // hand-off: a workspace of its own, zeroed before it, the flags copied after
     const bool resident = pred && pred->kind != FQ_PRED_NONE;
-    ctx.res->project_resident();
+    ctx.res->project_resident(ctx.stream());
     uint64_t *res = ctx.res->project_res;
     std::shared_ptr<DeviceBuffer> ws;
     if (!resident) ws = DeviceBuffer::alloc(fq_filter_project_blocks_workspace_bytes(), ctx.stream());
