@@ -162,3 +162,31 @@ def test_settle_runs_untimed_steps_for_about_the_requested_time():
     t0 = time.perf_counter()
     n = b.settle(slow_first, 0.2, 1, "gloo")
     assert n == len(calls) and time.perf_counter() - t0 >= 0.15, (n, time.perf_counter() - t0)
+
+
+def test_kernel_gaps_busy_time_is_the_union_of_launch_intervals(tmp_path):
+    # tools/kernel_gaps.py --window: the rocprof figure held beside bench.py's
+    # span when launches on the two row queues overlap -- the time at least one
+    # launch ran (never their sum), over the COUNT launches ending SKIP_LAST
+    # before the last
+    import csv
+    import json
+    import subprocess
+    import sys
+    path = tmp_path / "trace.csv"
+    rows = [(0, 100, "fq_jit_pblocks"), (50, 150, "fq_jit_pblocks"),  # overlap: busy 150
+            (150, 160, "other"), (200, 300, "fq_jit_pblocks"),          # gap 50, busy +100
+            (1000, 1100, "fq_jit_pblocks")]                            # the checked step, skipped
+    with open(path, "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["Kernel_Name", "Start_Timestamp", "End_Timestamp"])
+        for s, e, n in rows:
+            w.writerow([n, s, e])
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, os.path.join(root, "tools", "kernel_gaps.py"), str(path), "pblocks",
+                          "--window", "3", "1"], capture_output=True, text=True, check=True).stdout
+    d = json.loads(out)
+    assert d["launches"] == 3
+    assert abs(d["busy_union_ms"] - 250e-6) < 1e-12, d   # ns -> ms: 250 ns
+    assert abs(d["span_ms"] - 300e-6) < 1e-12, d
+    assert abs(d["kernel_ms_mean"] - 100e-6) < 1e-12, d
