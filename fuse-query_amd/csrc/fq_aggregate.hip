@@ -215,7 +215,7 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 // Flat streaming mode: grid-stride over 16-byte vectors, U vectors in flight
 // per lane.  `head` scalar elements precede the first 16-byte boundary.
-template <typename TIn, typename V, int PRED, bool CHAIN, int U>
+template <typename TIn, typename V, int PRED, bool CHAIN, int U, bool PF = false>
 __global__ void __launch_bounds__(kThreads)
     agg_flat_kernel(const TIn *__restrict__ col, int64_t n, int64_t head, KPred pred, KProg val,
                     uint32_t mask, int32_t vdtype, Partial *parts) {
@@ -237,11 +237,30 @@ __global__ void __launch_bounds__(kThreads)
     // profiles/r01_tune_*.json); few workgroups per CU (see launch) helps too.
     constexpr int64_t TV = (int64_t)U * kThreads;
     const int64_t ntiles = nvec / TV;
+    u32x4 nxt[U];  // PF: the next tile's vectors in flight while this tile is reduced (launch_scan)
+    if constexpr (PF) {
+        if ((int64_t)blockIdx.x < ntiles) {
+#pragma unroll
+            for (int k = 0; k < U; ++k)
+                nxt[k] = __builtin_nontemporal_load(vp + (int64_t)blockIdx.x * TV + threadIdx.x + (int64_t)k * kThreads);
+        }
+    }
     for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const int64_t base = t * TV + threadIdx.x;
         u32x4 raw[U];
+        if constexpr (PF) {
 #pragma unroll
-        for (int k = 0; k < U; ++k) raw[k] = __builtin_nontemporal_load(vp + base + (int64_t)k * kThreads);
+            for (int k = 0; k < U; ++k) raw[k] = nxt[k];
+            const int64_t tn = t + gridDim.x;
+            if (tn < ntiles) {
+#pragma unroll
+                for (int k = 0; k < U; ++k)
+                    nxt[k] = __builtin_nontemporal_load(vp + tn * TV + threadIdx.x + (int64_t)k * kThreads);
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < U; ++k) raw[k] = __builtin_nontemporal_load(vp + base + (int64_t)k * kThreads);
+        }
         TIn x[E];
         int64_t idx[E];
 #pragma unroll
@@ -591,9 +610,20 @@ static fq_status launch_scan(const Launch &L) {
                            L.stream, (const TIn *)L.col, L.n, L.block_rows, L.pred, L.val, L.mask,
                            L.vdtype, L.parts);
     } else {
-        hipLaunchKernelGGL((agg_flat_kernel<TIn, V, PRED, CHAIN, U>), dim3(L.grid), dim3(kThreads), 0,
-                           L.stream, (const TIn *)L.col, L.n, L.head, L.pred, L.val, L.mask, L.vdtype,
-                           L.parts);
+        // the next tile's loads in flight while this one is reduced, for scans
+        // without max/min: sum(number) 1.4132 -> 1.3991 ms per 10 GB, sum+count
+        // 1.4094 -> 1.3939; with max or min it costs instead (C3 1.3800 ->
+        // 1.3889, max 1.3904 -> 1.3959).  One process each, 6 rounds
+        // alternating (profiles/r06_o_*_pf_ab.json); the arithmetic order is
+        // the same either way.
+        if (PRED == FQ_PRED_NONE && !CHAIN && !(L.mask & (FQ_AGG_MAX | FQ_AGG_MIN)))
+            hipLaunchKernelGGL((agg_flat_kernel<TIn, V, PRED, CHAIN, U, true>), dim3(L.grid), dim3(kThreads), 0,
+                               L.stream, (const TIn *)L.col, L.n, L.head, L.pred, L.val, L.mask, L.vdtype,
+                               L.parts);
+        else
+            hipLaunchKernelGGL((agg_flat_kernel<TIn, V, PRED, CHAIN, U>), dim3(L.grid), dim3(kThreads), 0,
+                               L.stream, (const TIn *)L.col, L.n, L.head, L.pred, L.val, L.mask, L.vdtype,
+                               L.parts);
     }
     FQ_HIP_TRY(hipGetLastError());
     return FQ_OK;
