@@ -92,7 +92,9 @@ typedef struct fq_engine_stats {
     uint64_t project_kept;  /* rows they kept                                 */
     uint64_t project_bytes; /* algorithmic bytes: 8 per row read + 8 per kept
                                row per projected column                       */
-    double project_ms;      /* summed event time of the launches (FQ_OPT_PROFILE) */
+    double project_ms;      /* FQ_OPT_PROFILE 1: the launches' event pairs, summed;
+                               2: per query, earliest first-launch start to latest
+                               end over the row queues (overlap counted once) */
     double tail_ms;         /* host, FQ_OPT_PROFILE 2: the scans' end event seen ->
                                the result block (merge + AggregateFinal), summed */
     double complete_ms;     /* of tail_ms: reading the partitions' states into their
