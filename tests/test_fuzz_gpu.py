@@ -7,6 +7,7 @@ of the reference's Function machinery).  Results must be identical (f64
 sums within a relative 1e-12: the reduction order differs); when the
 reference raises, the engine must raise the same text."""
 import math
+import os
 import random
 
 import pytest
@@ -111,6 +112,8 @@ def run_engine(sql):
 
 
 N_CHOICES = [1000, 80000, 100001, 1_000_003]
+# FQ_FUZZ_SCALE=k runs k times the seeds (a deeper one-off run; the suite runs 1)
+SCALE = max(1, int(os.environ.get("FQ_FUZZ_SCALE", "1")))
 
 
 @pytest.fixture(params=["auto", "always"])
@@ -123,7 +126,7 @@ def jit(request):
     ops.jit_config(abi.JIT_AUTO, 1 << 22)
 
 
-@pytest.mark.parametrize("seed", range(64))
+@pytest.mark.parametrize("seed", range(64 * SCALE))
 def test_random_aggregate_query(seed, jit):
     rng = random.Random(1000 + seed + (100000 if jit == "always" else 0))
     n = rng.choice(N_CHOICES)
@@ -145,7 +148,7 @@ def test_random_aggregate_query(seed, jit):
     assert len(got) == 1 and all(same(g, x) for g, x in zip(got[0], exp)), (sql, got, exp)
 
 
-@pytest.mark.parametrize("seed", range(48))
+@pytest.mark.parametrize("seed", range(48 * SCALE))
 def test_random_projection_query(seed):
     rng = random.Random(5000 + seed)
     n = rng.choice([1000, 100001])
@@ -173,7 +176,7 @@ def gen_int_expr(rng, depth):
     return "number", R.E_field("number")
 
 
-@pytest.mark.parametrize("seed", range(20))
+@pytest.mark.parametrize("seed", range(20 * SCALE))
 def test_random_group_by_query(seed):
     # GROUP BY has no reference transform: fq_ref.group_by_query states the
     # device path's semantics with the reference's Function machinery
