@@ -49,7 +49,8 @@ typedef struct fq_result fq_result;
 #define FQ_OPT_STREAMS 4        /* device queues the aggregate pipes share (default 1: the scans
                                    are HBM-bound; two cost 5.5 %).  Row pipelines without a LIMIT
                                    use two row queues of their own, with a LIMIT one private
-                                   queue per pipe */
+                                   queue per pipe.  Set it between queries: the call waits for
+                                   the device, and a new count flushes the block cache */
 #define FQ_OPT_CHUNK_ROWS 5     /* rows per device block of a numbers_mt partition that is NOT
                                    resident (a multiple of 10,000; default 400,000,000 = 3.2 GB):
                                    aggregates over numbers_mt(1e12) stream through bounded HBM
